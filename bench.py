@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X network core against BASELINE.json's metric:
+
+  "APSP routing build (s) @10k nodes; packets routed/sec per sim round"
+
+Primary line (`value`): one routing-table build of the C3 workload (10k-node
+ring + chords, mean degree 8, every node used) -- seconds per
+build, rows sharded across ranks, RCCL all-gather of the row blocks when N > 1.
+`delivery` sub-object: one C4 delivery round (100k hosts, 1M packets) per step,
+packets/s.  Inputs are resident in HBM when the timed region starts.
+
+Single GPU:  python bench.py [--steps K --warmup W]
+N GPUs:      python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "APSP routing build (s) @10k nodes; packets routed/sec per sim round"
+# Peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level table)
+HBM_PEAK_GBS = 8000.0
+# 157.3 TFLOP/s FP32 vector = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz x 2 (FMA) -> 78.6 T 32-bit VALU ops/s
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+T0 = 946684800 * 10**9  # EmulatedTime SIMULATION_START
+
+
+def parse_args():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--nodes", type=int, default=10000)
+    p.add_argument("--degree", type=float, default=8.0)
+    p.add_argument("--hosts", type=int, default=100000)
+    p.add_argument("--packets", type=int, default=1000000)
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    p.add_argument("--no-delivery", action="store_true")
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
+                   help="PMC summary (HBM bytes per launch) written by tools/pmc_summary.py")
+    return p.parse_args()
+
+
+class Dist:
+    def __init__(self, n_gpus):
+        import torch
+
+        self.torch = torch
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != n_gpus:
+            raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={self.world}")
+        torch.cuda.set_device(self.local)
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.dist:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if not self.dist:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        self.dist.all_reduce(t)
+        return float(t.item())
+
+
+def timed(D, fn, steps, warmup):
+    torch = D.torch
+    for _ in range(warmup):
+        fn()
+    D.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    D.barrier()
+    return D.max(time.perf_counter() - t0) / steps
+
+
+def load_pmc(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+def main():
+    a = parse_args()
+    D = Dist(a.gpus)
+    torch = D.torch
+    from shadow_amd import Context, NetworkGraph, synth
+    from shadow_amd.worker import DeviceTable, HostTable, PacketBatch, Deliveries, deliver_round
+
+    ctx = Context(D.local, stream=torch.cuda.current_stream().cuda_stream)
+    pmc = load_pmc(a.pmc_json)
+
+    # ---------------- routing-table build (C3) ----------------
+    g = synth.ring_chords_graph(a.nodes, a.degree, seed=1)
+    net = NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
+    used = np.arange(a.nodes, dtype=np.uint32)
+    nu = len(used)
+    rows = (nu + D.world - 1) // D.world
+    r0, r1 = min(D.rank * rows, nu), min((D.rank + 1) * rows, nu)
+    full_lat = torch.empty(D.world * rows * nu, dtype=torch.int64, device="cuda")
+    full_loss = torch.empty(D.world * rows * nu, dtype=torch.float32, device="cuda")
+    my_lat = full_lat[D.rank * rows * nu:(D.rank + 1) * rows * nu]
+    my_loss = full_loss[D.rank * rows * nu:(D.rank + 1) * rows * nu]
+
+    def build():
+        net.build_rows_device(used, r0, r1, my_lat.data_ptr(), my_loss.data_ptr(), True)
+        if D.dist:
+            D.dist.all_gather_into_tensor(full_lat, my_lat)
+            D.dist.all_gather_into_tensor(full_loss, my_loss)
+
+    t_build = timed(D, build, a.steps, a.warmup)
+    # instrumented pass: per-kernel device time of the dominant kernel on its stream
+    ctx.enable_timers(True)
+    build()
+    relax_ms, relax_launches, relax_work = ctx.read_timer("relax_packed")
+    out_ms, _, _ = ctx.read_timer("out_packed")
+    ctx.enable_timers(False)
+    n_arcs = int(net.edge_src.size * 2 - 2 * np.count_nonzero(net.edge_src == net.edge_dst))
+    avg_launch_s = relax_ms / 1e3 / max(relax_launches, 1)
+    ops_per_launch = 2.0 * relax_work / max(relax_launches, 1)  # add + min per relaxation
+    achieved = ops_per_launch / avg_launch_s / 1e12 if relax_launches else 0.0
+    pm = pmc.get("relax_packed", {})
+    roofline = {"kernel": "k_relax_packed", "bound": "valu", "achieved": round(achieved, 3),
+                "peak": round(VALU_PEAK_TOPS, 1), "unit": "Tops/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
+                "traffic": pm.get("hbm_bytes_per_launch"),
+                "avg_launch_ms": round(avg_launch_s * 1e3, 4), "launches_per_build": relax_launches,
+                "relaxations_per_launch": relax_work / max(relax_launches, 1),
+                "ops_per_relaxation": 2}
+
+    cpu = None
+    if D.rank == 0 and D.world == 1 and not a.no_cpu:
+        from oracle import oracle as O  # the checker, timed as the CPU baseline
+
+        threads = min(16, os.cpu_count() or 1)
+        t0 = time.perf_counter()
+        rc, _, _, _ = O.shortest_paths(g["n"], g["src"], g["dst"], g["lat"], g["loss"], False, used, threads=threads)
+        t_cpu = time.perf_counter() - t0
+        assert rc == 0
+        cpu = {"value": round(t_cpu, 4), "unit": "s", "cores": threads, "kind": "port",
+               "sample": f"all {nu} sources (binary-heap Dijkstra, dense output, no HashMap materialisation) "
+                         f"on the same graph, {threads} threads"}
+
+    result = {
+        "metric": METRIC, "value": round(t_build, 6), "unit": "s", "n_gpus": D.world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(t_build * 1e3, 4), "higher_is_better": False,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u64+f32",
+        "data": "synthetic (seeded ring+chords graph, SURVEY §8d C3)",
+        "config": {"workload": "C3 APSP routing build: 10k-node undirected ring+chords graph, mean degree 8, "
+                               "latency U[1,100] ms (integer us), loss 0 w.p. 0.8 else U(0,0.02); all nodes used; "
+                               "source rows sharded across ranks" + (", RCCL all-gather" if D.world > 1 else ""),
+                   "nodes": a.nodes, "arcs": n_arcs, "parallelism": f"rows{D.world}"},
+        "roofline": roofline, "cpu_baseline": cpu,
+        "apsp_detail": {"out_kernel_ms": round(out_ms, 4),
+                        "fw_equivalent_Tops": round(2.0 * nu * a.nodes ** 2 / t_build / 1e12, 2)},
+    }
+    if cpu:
+        result["apsp_detail"]["speedup_vs_cpu"] = round(cpu["value"] / t_build, 1)
+
+    # ---------------- delivery round (C4) ----------------
+    if not a.no_delivery:
+        hosts = synth.make_hosts(a.hosts, a.nodes, general_seed=1, exact_seeds=True)
+        # weak scaling: each rank sends a.packets from the hosts whose node rows it owns
+        mine = np.nonzero((hosts["route"] >= r0) & (hosts["route"] < r1))[0]
+        sub = dict(n=len(mine), ip=hosts["ip"][mine], route=hosts["route"][mine], seed=hosts["seed"][mine])
+        pk = synth.make_packets(a.packets, sub, T0 + 10**9, T0 + 10**9 + 10**6, seed=100 + D.rank)
+        src_global = mine[pk["src"]].astype(np.uint32)
+        ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+        table = DeviceTable(my_lat, my_loss, nu, r0)
+        batch = PacketBatch.from_numpy(src_global, pk["dst_ip"], pk["payload"], pk["send_time"])
+        out = Deliveries.allocate(a.packets, a.hosts)
+        round_end, sim_end = T0 + 10**9 + 10**6, 2**63
+
+        def rnd():
+            deliver_round(ht, table, batch, round_end, sim_end, 0, out=out, ctx=ctx)
+
+        t_round = timed(D, rnd, a.steps, a.warmup)
+        ctx.enable_timers(True)
+        rnd()
+        kt = {k: ctx.read_timer(k) for k in ("seg_bounds", "walk", "scan", "scatter", "sort_small", "sort_big")}
+        ctx.enable_timers(False)
+        walk_ms, walk_n, walk_bytes = kt["walk"]
+        walk_s = walk_ms / 1e3 / max(walk_n, 1)
+        ach = walk_bytes / max(walk_n, 1) / walk_s / 1e9 if walk_n else 0.0
+        total_pkts = D.sum(float(a.packets))
+        round_bytes = 45.0 * a.packets + 84.0 * a.hosts  # SURVEY §8d algorithmic bytes per round
+        pmw = pmc.get("walk", {})
+        delivery = {
+            "metric": "packets routed/sec per sim round", "value": round(total_pkts / t_round, 1),
+            "unit": "packets/s", "higher_is_better": True, "ms_per_round": round(t_round * 1e3, 4),
+            "scaling": "weak", "dtype": "u64+f32+f64",
+            "config": {"workload": "C4 delivery round: 100k hosts on the C3 graph (node h mod 10k), 1M packets per "
+                                   "rank, src-major, dst uniform != src, 20% zero-payload, send_time U[1 ms round)",
+                       "hosts": a.hosts, "packets_per_rank": a.packets},
+            "roofline": {"kernel": "k_walk", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmw.get("hbm_bytes_per_launch"),
+                         "avg_launch_ms": round(walk_s * 1e3, 4)},
+            "round_hbm_GBs": round(round_bytes / t_round / 1e9, 1),
+            "kernel_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in kt.items()},
+        }
+        if D.rank == 0 and D.world == 1 and not a.no_cpu:
+            from oracle import oracle as O
+
+            lat_h = my_lat.cpu().numpy().view(np.uint64).reshape(-1, nu)[: r1 - r0]
+            loss_h = my_loss.cpu().numpy().reshape(-1, nu)[: r1 - r0]
+            rng0 = np.stack([O.xoshiro_seed(int(s)) for s in hosts["seed"]]).astype(np.uint64)
+            ctr0 = np.zeros(a.hosts, np.uint64)
+            t0 = time.perf_counter()
+            O.deliver_round(round_end, sim_end, 0, src_global, pk["dst_ip"], pk["payload"], pk["send_time"],
+                            hosts["ip"], hosts["route"], lat_h, loss_h, rng0, ctr0)
+            tc = time.perf_counter() - t0
+            delivery["cpu_baseline"] = {"value": round(a.packets / tc, 1), "unit": "packets/s", "cores": 1,
+                                        "kind": "port", "sample": f"one full round of {a.packets} packets, "
+                                        "send_packet semantics + per-destination EventQueue order, 1 thread"}
+            delivery["speedup_vs_cpu"] = round(delivery["value"] / delivery["cpu_baseline"]["value"], 1)
+        result["delivery"] = delivery
+
+    if D.rank == 0:
+        print(json.dumps(result), flush=True)
+    if D.dist:
+        D.dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

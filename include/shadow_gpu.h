@@ -1,0 +1,211 @@
+/*
+ * shadow_gpu.h -- C ABI of the MI355X network core for Shadow (gfx950 / HIP).
+ *
+ * This is the drop-in boundary for two stages of Shadow 3.2.0's network core:
+ *
+ *   1. Routing-table build.  Replaces
+ *        NetworkGraph::compute_shortest_paths   src/main/network/graph/mod.rs:183-228
+ *        NetworkGraph::get_direct_paths         src/main/network/graph/mod.rs:230-252
+ *      and the id remap of generate_routing_info (src/main/core/sim_config.rs:411-448).
+ *      The result is a dense table instead of HashMap<(u32,u32),PathProperties>
+ *      (RoutingInfo, graph/mod.rs:434-481): row i / column j = nodes[i] / nodes[j].
+ *
+ *   2. Inter-host packet delivery for one scheduling round.  Replaces the
+ *      per-packet body of Worker::send_packet (src/main/core/worker.rs:322-397)
+ *      and WorkerShared::push_packet_to_host (worker.rs:597-607): destination
+ *      resolution (Dns::addr_to_host_id, network/dns.rs:174-176), path lookup
+ *      (WorkerShared::latency/reliability, worker.rs:517-531), the per-host
+ *      Xoshiro256++ loss draw (host/host.rs:221,645-647), arrival time, event
+ *      ids (host.rs:649-653) and the destination EventQueue order
+ *      (core/work/event.rs:84-155).
+ *
+ * Conventions: plain C, int32_t status codes (sg_status), never unwinds.
+ * Pointers documented "device" are HIP device pointers on the context's
+ * device; everything else is host memory.  The reference's panics
+ * (unreachable pair, graph/mod.rs:219; unit overflow, graph/mod.rs:336) become
+ * status codes.  Calls on one context are not thread-safe (the reference makes
+ * these calls from one thread: sim_config.rs:137 and the manager's round loop).
+ */
+#ifndef SHADOW_GPU_H
+#define SHADOW_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG_ABI_VERSION 1
+
+typedef enum sg_status {
+  SG_OK = 0,
+  SG_ERR_NO_EDGE = 1,       /* graph/mod.rs:266-268  "No edge connecting node {} to {}" */
+  SG_ERR_MULTI_EDGE = 2,    /* graph/mod.rs:269-275  "More than one edge connecting node {} to {}" */
+  SG_ERR_UNREACHABLE = 3,   /* graph/mod.rs:219      assert_eq!(paths.len(), n^2) (panic) */
+  SG_ERR_OOM = 4,
+  SG_ERR_INVALID_ARG = 5,
+  SG_ERR_DEVICE = 6,        /* HIP runtime error */
+  SG_ERR_PARSE = 7,         /* NetworkGraph::parse / ShadowEdge::try_from (graph/mod.rs:72-181) */
+  SG_ERR_UNSORTED = 8,      /* sg_deliver_round: packets not grouped by ascending source host */
+  SG_ERR_DUPLICATE_IP = 9   /* two hosts with one address (IpAssignment::assign_ip, graph/mod.rs:383-394) */
+} sg_status;
+
+typedef struct sg_ctx sg_ctx;     /* one HIP device + stream + workspace */
+typedef struct sg_net sg_net;     /* device-resident network graph */
+typedef struct sg_hosts sg_hosts; /* device-resident host table: addresses, routes, RNG, event ids */
+typedef struct sg_gml sg_gml;     /* host-side parsed GML graph */
+
+int32_t sg_abi_version(void);
+
+/* ---- context ------------------------------------------------------------ */
+int32_t sg_ctx_create(int32_t device, sg_ctx** out);
+void sg_ctx_destroy(sg_ctx* ctx);
+/* Use an existing hipStream_t (e.g. torch's current stream); NULL = the context's own stream. */
+int32_t sg_ctx_set_stream(sg_ctx* ctx, void* hip_stream);
+void* sg_ctx_stream(const sg_ctx* ctx);
+int32_t sg_ctx_synchronize(sg_ctx* ctx);
+/* Message and (row, col) of the last failing call on this context. */
+const char* sg_ctx_last_error(const sg_ctx* ctx);
+void sg_ctx_last_error_pair(const sg_ctx* ctx, uint32_t* row, uint32_t* col);
+/* Measurement hooks (bench.py): when enabled, every launch of an instrumented
+ * kernel is bracketed by HIP events on the context stream.  read_timer returns
+ * the summed device time, the launch count and the algorithmic work declared
+ * by the launch sites ("relax": relaxations; "deliver_*": bytes).  Enabling or
+ * disabling resets all timers. */
+int32_t sg_ctx_enable_timers(sg_ctx* ctx, int32_t enable);
+int32_t sg_ctx_read_timer(sg_ctx* ctx, const char* kernel, double* total_ms, uint64_t* launches,
+                          double* work);
+
+/* ---- GML ingest (NetworkGraph::parse, graph/mod.rs:134-181) -------------- */
+/* Edge list in GML edge order; node indices are petgraph NodeIndex values
+ * (GML node order).  Latency in integer ns (units.rs:377-438), loss f32. */
+typedef struct sg_graph {
+  uint32_t n_nodes;
+  uint32_t n_edges;
+  const uint32_t* edge_src;
+  const uint32_t* edge_dst;
+  const uint64_t* edge_latency_ns;
+  const float* edge_packet_loss;
+  const uint32_t* node_gml_id; /* optional (may be NULL): GML ids, for messages */
+  uint8_t directed;
+} sg_graph;
+
+/* Parse GML text.  On failure returns SG_ERR_PARSE and writes a message into
+ * err (if err_len > 0).  Latency unit overflow is reported here. */
+int32_t sg_gml_parse(const char* text, size_t len, sg_gml** out, char* err, size_t err_len);
+/* Borrow the parsed edge list (valid until sg_gml_destroy). */
+int32_t sg_gml_graph(const sg_gml* g, sg_graph* out);
+/* NetworkGraph::node_id_to_index (graph/mod.rs:126-128); SG_ERR_INVALID_ARG if absent. */
+int32_t sg_gml_node_index(const sg_gml* g, uint32_t gml_id, uint32_t* out_index);
+void sg_gml_destroy(sg_gml* g);
+
+/* ---- routing-table build ------------------------------------------------- */
+/* Upload a graph to the device and build its in-arc (CSC) form. */
+int32_t sg_net_create(sg_ctx* ctx, const sg_graph* g, sg_net** out);
+void sg_net_destroy(sg_net* net);
+
+#define SG_ROUTE_SHORTEST_PATH 0x1u /* network.use_shortest_path (configuration.rs:315-326) */
+#define SG_ROUTE_OUT_DEVICE 0x2u    /* out_* are device pointers (else host) */
+
+/*
+ * Rows [row_begin, row_end) of the routing table over `nodes` (petgraph
+ * indices of the used nodes, n_used of them; the caller's order defines the
+ * table's row/column order):
+ *   out_latency_ns [(i-row_begin)*n_used + j] = path(nodes[i] -> nodes[j]).latency_ns
+ *   out_packet_loss[(i-row_begin)*n_used + j] = path(nodes[i] -> nodes[j]).packet_loss
+ * With SG_ROUTE_SHORTEST_PATH: the lexicographic (latency, loss) optimum of
+ * the left fold PathProperties::default() + e1 + ... + ek over every path,
+ * bit-exact (petgraph::algo::dijkstra semantics), diagonal = the node's single
+ * self-loop.  Without: the single direct edge of every pair.
+ * Errors as the reference: missing/duplicate self-loop (first node in order),
+ * missing/duplicate direct edge (first pair in row-major order), unreachable
+ * pair (first pair in row-major order); sg_ctx_last_error_pair gives (i, j).
+ * Rows may be sharded across devices by calling with disjoint row ranges.
+ */
+int32_t sg_routing_build(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32_t n_used,
+                         uint32_t row_begin, uint32_t row_end, uint32_t flags,
+                         uint64_t* out_latency_ns, float* out_packet_loss);
+
+/* RoutingInfo::get_smallest_latency_ns (graph/mod.rs:478-480) over `count`
+ * device latencies; UINT64_MAX when count == 0. */
+int32_t sg_routing_min_latency(sg_ctx* ctx, const uint64_t* d_latency_ns, size_t count,
+                               uint64_t* out_min);
+
+/* ---- packet delivery ------------------------------------------------------ */
+/*
+ * Host table.  host_ipv4[h] = the host's address (host byte order, as
+ * u32::from(Ipv4Addr)); host_route_idx[h] = index of the host's graph node in
+ * the routing table's node list; host_seed[h] = HostInfo.seed (node_seed):
+ * the RNG is Xoshiro256PlusPlus::seed_from_u64(seed) (host.rs:221).  HostId =
+ * h (hosts sorted by name, configuration.rs:107).  Addresses must be unique.
+ */
+int32_t sg_hosts_create(sg_ctx* ctx, uint32_t n_hosts, const uint32_t* host_ipv4,
+                        const uint32_t* host_route_idx, const uint64_t* host_seed,
+                        sg_hosts** out);
+/* Copy RNG state (4 u64 per host, Xoshiro s[0..3]) and event-id counters
+ * (Host::event_id_counter) out of / into the device (host memory). */
+int32_t sg_hosts_get_state(sg_hosts* hosts, uint64_t* rng_state, uint64_t* event_ctr);
+int32_t sg_hosts_set_state(sg_hosts* hosts, const uint64_t* rng_state, const uint64_t* event_ctr);
+void sg_hosts_destroy(sg_hosts* hosts);
+
+/* Routing-table shard resident on the device (rows [row_begin, row_begin+n_rows)). */
+typedef struct sg_table {
+  const uint64_t* latency_ns; /* device, n_rows x n_cols */
+  const float* packet_loss;   /* device, n_rows x n_cols */
+  uint32_t n_cols;
+  uint32_t row_begin;
+  uint32_t n_rows;
+} sg_table;
+
+/* Round clock (EmulatedTime ns).  round_end = the worker's barrier
+ * (worker.rs:262-268); sim_end / bootstrap_end from WorkerShared. */
+typedef struct sg_round {
+  uint64_t round_end_ns;
+  uint64_t sim_end_ns;
+  uint64_t bootstrap_end_ns;
+} sg_round;
+
+/* One round's sent packets, device SoA, grouped by ascending source host and
+ * in each host's send order (the order Worker::send_packet saw them). */
+typedef struct sg_packets {
+  uint32_t n_packets;
+  const uint32_t* src_host;     /* HostId of the sending host */
+  const uint32_t* dst_ipv4;     /* destination address (host byte order) */
+  const uint32_t* payload_len;  /* PacketRc::payload_len (packet.rs:394-396) */
+  const uint64_t* send_time_ns; /* Worker::current_time() at the send */
+} sg_packets;
+
+enum {
+  SG_PKT_DELIVERED = 0,  /* PacketStatus::InetSent; pushed to the destination queue */
+  SG_PKT_DROP_LOSS = 1,  /* InetDropped by the reliability draw (worker.rs:365-368) */
+  SG_PKT_DROP_NO_DST = 2,/* InetDropped: unknown destination, no draw (worker.rs:341-351) */
+  SG_PKT_SIM_END = 3     /* now >= sim_end: ignored, no draw (worker.rs:332-335) */
+};
+
+/* Device outputs. */
+typedef struct sg_deliveries {
+  uint8_t* status;           /* n_packets, SG_PKT_* */
+  uint64_t* deliver_time_ns; /* n_packets (0 unless delivered) */
+  uint64_t* event_id;        /* n_packets, src_host_event_id (UINT64_MAX unless delivered) */
+  uint32_t* dst_order;       /* n_packets capacity: delivered packet indices bucketed by
+                                destination, each bucket in EventQueue pop order */
+  uint32_t* dst_offsets;     /* n_hosts + 1 */
+} sg_deliveries;
+
+typedef struct sg_round_stats {
+  uint64_t n_delivered;
+  uint64_t min_deliver_time_ns; /* Worker::update_next_event_time input min (worker.rs:388) */
+  uint64_t min_used_latency_ns; /* Worker::update_lowest_used_latency input min (worker.rs:372) */
+} sg_round_stats;
+
+/* Run one round.  Updates the hosts' RNG streams and event counters on the
+ * device.  `stats` (host) may be NULL for a fully asynchronous call. */
+int32_t sg_deliver_round(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table,
+                         const sg_round* round, const sg_packets* packets, sg_deliveries* out,
+                         sg_round_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHADOW_GPU_H */

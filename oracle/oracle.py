@@ -1,0 +1,180 @@
+"""ctypes front end for the CPU oracle (oracle/sg_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+`cpu_baseline` leg of bench.py, never by the product package `shadow_amd`.
+Every function cites the reference code it restates (see sg_oracle.c).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libsg_oracle.so")
+
+OK, ERR_NO_EDGE, ERR_MULTI_EDGE, ERR_UNREACHABLE, ERR_OOM, ERR_ARG = range(6)
+ST_DELIVERED, ST_DROP_LOSS, ST_DROP_NO_DST, ST_SIM_END = range(4)
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
+            os.path.join(_HERE, "sg_oracle.c")
+        ):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        u32p, u64p, f32p, u8p = (C.POINTER(t) for t in (C.c_uint32, C.c_uint64, C.c_float, C.c_uint8))
+        L.sgo_shortest_paths.restype = C.c_int
+        L.sgo_shortest_paths.argtypes = [C.c_uint32, C.c_uint32, u32p, u32p, u64p, f32p, C.c_int, u32p,
+                                         C.c_uint32, C.c_uint32, C.c_uint32, u64p, f32p, C.c_int, u32p, u32p]
+        L.sgo_direct_paths.restype = C.c_int
+        L.sgo_direct_paths.argtypes = [C.c_uint32, C.c_uint32, u32p, u32p, u64p, f32p, C.c_int, u32p,
+                                       C.c_uint32, u64p, f32p, u32p, u32p]
+        L.sgo_path_add.restype = None
+        L.sgo_path_add.argtypes = [C.c_uint64, C.c_float, C.c_uint64, C.c_float, u64p, f32p]
+        L.sgo_splitmix64_next.restype = C.c_uint64
+        L.sgo_splitmix64_next.argtypes = [u64p]
+        L.sgo_xoshiro_seed_from_u64.restype = None
+        L.sgo_xoshiro_seed_from_u64.argtypes = [C.c_uint64, u64p]
+        L.sgo_xoshiro_next_u64.restype = C.c_uint64
+        L.sgo_xoshiro_next_u64.argtypes = [u64p]
+        L.sgo_xoshiro_next_f64.restype = C.c_double
+        L.sgo_xoshiro_next_f64.argtypes = [u64p]
+        L.sgo_siphash13.restype = C.c_uint64
+        L.sgo_siphash13.argtypes = [C.c_char_p, C.c_size_t]
+        L.sgo_host_seed.restype = C.c_uint64
+        L.sgo_host_seed.argtypes = [C.c_uint64, C.c_char_p, C.c_size_t]
+        L.sgo_smallest_latency.restype = C.c_uint64
+        L.sgo_smallest_latency.argtypes = [u64p, C.c_size_t]
+        L.sgo_deliver_round.restype = C.c_int64
+        L.sgo_deliver_round.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u32p, u32p, u32p, u64p,
+                                        C.c_uint32, u32p, u32p, C.c_uint32, u64p, f32p, u64p, u64p, u8p, u64p,
+                                        u64p, u32p, u32p, u64p, u64p]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def _arr(x, dtype):
+    return np.ascontiguousarray(np.asarray(x, dtype=dtype))
+
+
+def path_add(a_lat, a_loss, b_lat, b_loss):
+    """PathProperties + PathProperties (graph/mod.rs:322-331)."""
+    ol, of = C.c_uint64(), C.c_float()
+    lib().sgo_path_add(a_lat, a_loss, b_lat, b_loss, C.byref(ol), C.byref(of))
+    return ol.value, np.float32(of.value)
+
+
+def shortest_paths(n_nodes, src, dst, lat, loss, directed, used, rows=None, threads=1):
+    """NetworkGraph::compute_shortest_paths (graph/mod.rs:183-228), dense output.
+
+    Returns (rc, lat[rows x n_used] u64, loss[rows x n_used] f32, (err_row, err_col)).
+    """
+    src, dst = _arr(src, np.uint32), _arr(dst, np.uint32)
+    lat, loss = _arr(lat, np.uint64), _arr(loss, np.float32)
+    used = _arr(used, np.uint32)
+    nu = len(used)
+    r0, r1 = (0, nu) if rows is None else rows
+    out_lat = np.zeros((r1 - r0, nu), np.uint64)
+    out_loss = np.zeros((r1 - r0, nu), np.float32)
+    ea, eb = C.c_uint32(0), C.c_uint32(0)
+    rc = lib().sgo_shortest_paths(n_nodes, len(src), _p(src, C.c_uint32), _p(dst, C.c_uint32),
+                                  _p(lat, C.c_uint64), _p(loss, C.c_float), int(bool(directed)),
+                                  _p(used, C.c_uint32), nu, r0, r1, _p(out_lat, C.c_uint64),
+                                  _p(out_loss, C.c_float), threads, C.byref(ea), C.byref(eb))
+    return rc, out_lat, out_loss, (ea.value, eb.value)
+
+
+def direct_paths(n_nodes, src, dst, lat, loss, directed, used):
+    """NetworkGraph::get_direct_paths (graph/mod.rs:230-252), dense output."""
+    src, dst = _arr(src, np.uint32), _arr(dst, np.uint32)
+    lat, loss = _arr(lat, np.uint64), _arr(loss, np.float32)
+    used = _arr(used, np.uint32)
+    nu = len(used)
+    out_lat = np.zeros((nu, nu), np.uint64)
+    out_loss = np.zeros((nu, nu), np.float32)
+    ea, eb = C.c_uint32(0), C.c_uint32(0)
+    rc = lib().sgo_direct_paths(n_nodes, len(src), _p(src, C.c_uint32), _p(dst, C.c_uint32),
+                                _p(lat, C.c_uint64), _p(loss, C.c_float), int(bool(directed)),
+                                _p(used, C.c_uint32), nu, _p(out_lat, C.c_uint64), _p(out_loss, C.c_float),
+                                C.byref(ea), C.byref(eb))
+    return rc, out_lat, out_loss, (ea.value, eb.value)
+
+
+def xoshiro_seed(seed: int) -> np.ndarray:
+    """Xoshiro256PlusPlus::seed_from_u64 (SplitMix64; sim_config.rs:48-51, host.rs:221)."""
+    s = np.zeros(4, np.uint64)
+    lib().sgo_xoshiro_seed_from_u64(seed, _p(s, C.c_uint64))
+    return s
+
+
+def xoshiro_next_u64(state: np.ndarray) -> int:
+    return lib().sgo_xoshiro_next_u64(_p(state, C.c_uint64))
+
+
+def xoshiro_next_f64(state: np.ndarray) -> float:
+    """rand 0.9 `random::<f64>()` on the host stream (worker.rs:360)."""
+    return lib().sgo_xoshiro_next_f64(_p(state, C.c_uint64))
+
+
+def siphash13(data: bytes) -> int:
+    return lib().sgo_siphash13(data, len(data))
+
+
+def host_seed(general_seed: int, hostname: str) -> int:
+    """HostInfo.seed (sim_config.rs:50-54,221-225,242). Parity unpinned (std SipHash)."""
+    b = hostname.encode()
+    return lib().sgo_host_seed(general_seed, b, len(b))
+
+
+def smallest_latency(lat: np.ndarray) -> int:
+    lat = _arr(lat, np.uint64).ravel()
+    return lib().sgo_smallest_latency(_p(lat, C.c_uint64), lat.size)
+
+
+def deliver_round(round_end, sim_end, bootstrap_end, src_host, dst_ip, payload_len, send_time,
+                  host_ip, host_row, tab_lat, tab_loss, rng, event_ctr):
+    """Worker::send_packet over a round's batch (worker.rs:322-397) + event order (event.rs:84-155).
+
+    rng (H x 4 u64) and event_ctr (H u64) are updated in place.
+    Returns dict(status, deliver_time, event_id, dst_order, dst_offsets, min_deliver, min_lat, delivered).
+    """
+    src_host, dst_ip = _arr(src_host, np.uint32), _arr(dst_ip, np.uint32)
+    payload_len, send_time = _arr(payload_len, np.uint32), _arr(send_time, np.uint64)
+    host_ip, host_row = _arr(host_ip, np.uint32), _arr(host_row, np.uint32)
+    tab_lat, tab_loss = _arr(tab_lat, np.uint64), _arr(tab_loss, np.float32)
+    assert rng.dtype == np.uint64 and rng.flags.c_contiguous and event_ctr.dtype == np.uint64
+    n, H = len(src_host), len(host_ip)
+    ncols = tab_lat.shape[-1]
+    status = np.zeros(n, np.uint8)
+    deliver = np.zeros(n, np.uint64)
+    eid = np.zeros(n, np.uint64)
+    order = np.zeros(max(n, 1), np.uint32)
+    offs = np.zeros(H + 1, np.uint32)
+    mind, minl = C.c_uint64(), C.c_uint64()
+    nd = lib().sgo_deliver_round(round_end, sim_end, bootstrap_end, n, _p(src_host, C.c_uint32),
+                                 _p(dst_ip, C.c_uint32), _p(payload_len, C.c_uint32), _p(send_time, C.c_uint64),
+                                 H, _p(host_ip, C.c_uint32), _p(host_row, C.c_uint32), ncols,
+                                 _p(tab_lat, C.c_uint64), _p(tab_loss, C.c_float), _p(rng, C.c_uint64),
+                                 _p(event_ctr, C.c_uint64), _p(status, C.c_uint8), _p(deliver, C.c_uint64),
+                                 _p(eid, C.c_uint64), _p(order, C.c_uint32), _p(offs, C.c_uint32),
+                                 C.byref(mind), C.byref(minl))
+    if nd < 0:
+        raise ValueError("sgo_deliver_round: bad argument")
+    return dict(status=status, deliver_time=deliver, event_id=eid, dst_order=order[:nd],
+                dst_offsets=offs, min_deliver=mind.value, min_lat=minl.value, delivered=int(nd))

@@ -1,0 +1,629 @@
+/*
+ * sg_oracle.c -- CPU restatement of Shadow's network-core hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP
+ * implementation in shadow_amd/csrc.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's `cpu_baseline` leg may load it.  The product path never
+ * links or calls it (and fails loudly when the HIP library is missing).
+ *
+ * Parity pinning: the reference (Rust, Shadow 3.2.0) cannot be built here
+ * (no cargo/rustc; petgraph / rand / rand_xoshiro not vendored -- SURVEY §8c).
+ * This restatement is pinned by
+ *   - graph/mod.rs:564-651 test_shortest_path (9 exact latencies x {directed,
+ *     undirected}) and graph/mod.rs:519-533 test_path_add,
+ *   - configuration.rs:1366-1380 ONE_GBIT_SWITCH_GRAPH -> {(0,0): (1 ms, 0.0)},
+ *   - the upstream rand_xoshiro 0.7.0 known-answer vector for xoshiro256++
+ *     (state [1,2,3,4]) [external, restated from the published algorithm],
+ *   - networkx/scipy shortest-path latencies on random graphs (tests/).
+ * The f32 loss bits, the f64 draw and the event order follow the cited code;
+ * the reference's own tests do not pin them ("parity unpinned" for those
+ * bits beyond the restatement -- see DESIGN.md §Oracle).
+ *
+ * Build: make -C oracle   (gcc -O2 -ffp-contract=off: one rounding per f32 op,
+ * no FMA, matching Rust's f32 arithmetic in graph/mod.rs:328).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+
+#define SGO_OK 0
+#define SGO_ERR_NO_EDGE 1     /* graph/mod.rs:266-268 "No edge connecting node" */
+#define SGO_ERR_MULTI_EDGE 2  /* graph/mod.rs:269-275 "More than one edge connecting" */
+#define SGO_ERR_UNREACHABLE 3 /* graph/mod.rs:219 assert_eq!(paths.len(), n^2) panics */
+#define SGO_ERR_OOM 4
+#define SGO_ERR_ARG 5
+
+/* ------------------------------------------------------------------------- */
+/* PathProperties semiring (graph/mod.rs:297-340)                            */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  uint64_t lat;
+  float loss;
+} sgo_pp;
+
+/* graph/mod.rs:322-331: (lat + lat, 1f32 - (1f32 - a) * (1f32 - b)).  Each
+ * f32 op rounds once; -ffp-contract=off keeps the product from fusing. */
+static inline sgo_pp pp_add(sgo_pp a, uint64_t e_lat, float e_loss) {
+  sgo_pp r;
+  r.lat = a.lat + e_lat; /* release-build Rust wraps; latencies never get near 2^64 */
+  float oma = 1.0f - a.loss;
+  float ome = 1.0f - e_loss;
+  float prod = oma * ome;
+  r.loss = 1.0f - prod;
+  return r;
+}
+
+/* graph/mod.rs:305-313: latency first, then packet loss (f32 partial_cmp). */
+static inline int pp_lt(sgo_pp a, sgo_pp b) {
+  return a.lat < b.lat || (a.lat == b.lat && a.loss < b.loss);
+}
+
+void sgo_path_add(uint64_t a_lat, float a_loss, uint64_t b_lat, float b_loss, uint64_t* out_lat,
+                  float* out_loss) {
+  sgo_pp a = {a_lat, a_loss};
+  sgo_pp r = pp_add(a, b_lat, b_loss);
+  *out_lat = r.lat;
+  *out_loss = r.loss;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Adjacency as petgraph sees it (graph/mod.rs:134-181).                      */
+/* Directed: one arc per GML edge.  Undirected: both directions, a self-loop  */
+/* is iterated once (petgraph Edges::next skips the second copy).             */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  uint32_t n;
+  uint32_t* off; /* n+1 */
+  uint32_t* dst; /* arcs */
+  uint32_t* edge; /* GML edge index of each arc */
+} sgo_adj;
+
+static void adj_free(sgo_adj* a) {
+  free(a->off);
+  free(a->dst);
+  free(a->edge);
+}
+
+static int adj_build(sgo_adj* a, uint32_t n, uint32_t m, const uint32_t* esrc, const uint32_t* edst,
+                     int directed) {
+  a->n = n;
+  a->off = (uint32_t*)calloc((size_t)n + 1, sizeof(uint32_t));
+  size_t cap = directed ? m : 2 * (size_t)m;
+  a->dst = (uint32_t*)malloc((cap ? cap : 1) * sizeof(uint32_t));
+  a->edge = (uint32_t*)malloc((cap ? cap : 1) * sizeof(uint32_t));
+  if (!a->off || !a->dst || !a->edge) return SGO_ERR_OOM;
+  for (uint32_t i = 0; i < m; i++) {
+    if (esrc[i] >= n || edst[i] >= n) return SGO_ERR_ARG;
+    a->off[esrc[i] + 1]++;
+    if (!directed && esrc[i] != edst[i]) a->off[edst[i] + 1]++;
+  }
+  for (uint32_t v = 0; v < n; v++) a->off[v + 1] += a->off[v];
+  uint32_t* cur = (uint32_t*)malloc(((size_t)n + 1) * sizeof(uint32_t));
+  if (!cur) return SGO_ERR_OOM;
+  memcpy(cur, a->off, ((size_t)n + 1) * sizeof(uint32_t));
+  for (uint32_t i = 0; i < m; i++) {
+    uint32_t s = esrc[i], d = edst[i];
+    a->dst[cur[s]] = d;
+    a->edge[cur[s]++] = i;
+    if (!directed && s != d) {
+      a->dst[cur[d]] = s;
+      a->edge[cur[d]++] = i;
+    }
+  }
+  free(cur);
+  return SGO_OK;
+}
+
+/* ------------------------------------------------------------------------- */
+/* petgraph 0.8.1 algo::dijkstra restated (call sites graph/mod.rs:195,198): */
+/* binary heap, lazy insertion, skip visited targets, update on strict '<',  */
+/* start score = PathProperties::default().                                  */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  sgo_pp key;
+  uint32_t node;
+} heap_item;
+
+typedef struct {
+  heap_item* a;
+  size_t n, cap;
+} heap_t;
+
+static inline int heap_less(const heap_item* x, const heap_item* y) { return pp_lt(x->key, y->key); }
+
+static int heap_push(heap_t* h, sgo_pp key, uint32_t node) {
+  if (h->n == h->cap) {
+    size_t nc = h->cap ? 2 * h->cap : 1024;
+    heap_item* na = (heap_item*)realloc(h->a, nc * sizeof(heap_item));
+    if (!na) return SGO_ERR_OOM;
+    h->a = na;
+    h->cap = nc;
+  }
+  size_t i = h->n++;
+  heap_item it = {key, node};
+  while (i > 0) {
+    size_t p = (i - 1) / 2;
+    if (!heap_less(&it, &h->a[p])) break;
+    h->a[i] = h->a[p];
+    i = p;
+  }
+  h->a[i] = it;
+  return SGO_OK;
+}
+
+static heap_item heap_pop(heap_t* h) {
+  heap_item top = h->a[0];
+  heap_item last = h->a[--h->n];
+  size_t i = 0;
+  for (;;) {
+    size_t l = 2 * i + 1, r = l + 1, m = i;
+    const heap_item* best = &last;
+    if (l < h->n && heap_less(&h->a[l], best)) { m = l; best = &h->a[l]; }
+    if (r < h->n && heap_less(&h->a[r], best)) { m = r; best = &h->a[r]; }
+    if (m == i) break;
+    h->a[i] = h->a[m];
+    i = m;
+  }
+  if (h->n) h->a[i] = last;
+  return top;
+}
+
+typedef struct {
+  const sgo_adj* adj;
+  const uint64_t* elat;
+  const float* eloss;
+  const uint32_t* used;
+  uint32_t n_used;
+  uint64_t* out_lat;
+  float* out_loss;
+  uint32_t row_begin, row_end;
+  int64_t next_row; /* shared work counter */
+  pthread_mutex_t mu;
+  int err;
+  uint32_t err_row, err_col;
+} sssp_job;
+
+static int dijkstra_row(sssp_job* J, uint32_t row, sgo_pp* score, uint8_t* has, uint8_t* visited,
+                        heap_t* h) {
+  const sgo_adj* A = J->adj;
+  uint32_t n = A->n, src = J->used[row];
+  memset(has, 0, n);
+  memset(visited, 0, n);
+  h->n = 0;
+  sgo_pp zero = {0, 0.0f};
+  score[src] = zero;
+  has[src] = 1;
+  if (heap_push(h, zero, src)) return SGO_ERR_OOM;
+  while (h->n) {
+    heap_item it = heap_pop(h);
+    uint32_t u = it.node;
+    if (visited[u]) continue;
+    for (uint32_t k = A->off[u]; k < A->off[u + 1]; k++) {
+      uint32_t v = A->dst[k];
+      if (visited[v]) continue;
+      uint32_t e = A->edge[k];
+      sgo_pp cand = pp_add(it.key, J->elat[e], J->eloss[e]);
+      if (!has[v] || pp_lt(cand, score[v])) {
+        score[v] = cand;
+        has[v] = 1;
+        if (heap_push(h, cand, v)) return SGO_ERR_OOM;
+      }
+    }
+    visited[u] = 1;
+  }
+  size_t base = (size_t)(row - J->row_begin) * J->n_used;
+  for (uint32_t j = 0; j < J->n_used; j++) {
+    uint32_t d = J->used[j];
+    if (!has[d]) {
+      pthread_mutex_lock(&J->mu);
+      if (J->err == 0 || row < J->err_row || (row == J->err_row && j < J->err_col)) {
+        J->err = SGO_ERR_UNREACHABLE;
+        J->err_row = row;
+        J->err_col = j;
+      }
+      pthread_mutex_unlock(&J->mu);
+      J->out_lat[base + j] = UINT64_MAX;
+      J->out_loss[base + j] = 0.0f;
+      continue;
+    }
+    J->out_lat[base + j] = score[d].lat;
+    J->out_loss[base + j] = score[d].loss;
+  }
+  return SGO_OK;
+}
+
+static void* sssp_worker(void* arg) {
+  sssp_job* J = (sssp_job*)arg;
+  uint32_t n = J->adj->n;
+  sgo_pp* score = (sgo_pp*)malloc((size_t)n * sizeof(sgo_pp) + 1);
+  uint8_t* has = (uint8_t*)malloc((size_t)n + 1);
+  uint8_t* visited = (uint8_t*)malloc((size_t)n + 1);
+  heap_t h = {0, 0, 0};
+  int rc = (!score || !has || !visited) ? SGO_ERR_OOM : SGO_OK;
+  while (rc == SGO_OK) {
+    int64_t row = __atomic_fetch_add(&J->next_row, 1, __ATOMIC_RELAXED);
+    if (row >= (int64_t)J->row_end) break;
+    rc = dijkstra_row(J, (uint32_t)row, score, has, visited, &h);
+  }
+  if (rc == SGO_ERR_OOM) {
+    pthread_mutex_lock(&J->mu);
+    J->err = SGO_ERR_OOM;
+    pthread_mutex_unlock(&J->mu);
+  }
+  free(score);
+  free(has);
+  free(visited);
+  free(h.a);
+  return NULL;
+}
+
+/* Number of GML edges connecting u->v as petgraph edges_connecting counts them
+ * (graph/mod.rs:256-293); *first receives the first such edge in adjacency order. */
+static uint32_t count_connecting(const sgo_adj* A, uint32_t u, uint32_t v, uint32_t* first) {
+  uint32_t c = 0;
+  for (uint32_t k = A->off[u]; k < A->off[u + 1]; k++)
+    if (A->dst[k] == v) {
+      if (c == 0) *first = A->edge[k];
+      c++;
+    }
+  return c;
+}
+
+/*
+ * NetworkGraph::compute_shortest_paths (graph/mod.rs:183-228), dense output:
+ *   out[(i - row_begin) * n_used + j] = path(used[i] -> used[j]) for rows
+ *   i in [row_begin, row_end).  Diagonal = the raw self-loop edge (:210-217).
+ * Error precedence follows the reference: self-loop errors (first used node
+ * in order, :211-217) before the unreachable assert (:219).
+ * n_threads <= 0 -> 1.  err_a/err_b receive the failing (row, col) indices.
+ */
+int sgo_shortest_paths(uint32_t n, uint32_t m, const uint32_t* esrc, const uint32_t* edst,
+                       const uint64_t* elat, const float* eloss, int directed, const uint32_t* used,
+                       uint32_t n_used, uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
+                       float* out_loss, int n_threads, uint32_t* err_a, uint32_t* err_b) {
+  if (row_end > n_used || row_begin > row_end) return SGO_ERR_ARG;
+  for (uint32_t j = 0; j < n_used; j++)
+    if (used[j] >= n) return SGO_ERR_ARG;
+  sgo_adj A;
+  memset(&A, 0, sizeof(A));
+  int rc = adj_build(&A, n, m, esrc, edst, directed);
+  if (rc) {
+    adj_free(&A);
+    return rc;
+  }
+  sssp_job J;
+  memset(&J, 0, sizeof(J));
+  J.adj = &A;
+  J.elat = elat;
+  J.eloss = eloss;
+  J.used = used;
+  J.n_used = n_used;
+  J.out_lat = out_lat;
+  J.out_loss = out_loss;
+  J.row_begin = row_begin;
+  J.row_end = row_end;
+  J.next_row = row_begin;
+  pthread_mutex_init(&J.mu, NULL);
+  if (n_threads <= 1) {
+    sssp_worker(&J);
+  } else {
+    pthread_t* th = (pthread_t*)malloc((size_t)n_threads * sizeof(pthread_t));
+    for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, sssp_worker, &J);
+    for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+    free(th);
+  }
+  pthread_mutex_destroy(&J.mu);
+  if (J.err == SGO_ERR_OOM) {
+    adj_free(&A);
+    return SGO_ERR_OOM;
+  }
+  /* self-pair override with the single self-loop (graph/mod.rs:210-217); all
+   * used nodes are checked, in order, not just this row block. */
+  for (uint32_t j = 0; j < n_used; j++) {
+    uint32_t u = used[j], e = 0;
+    uint32_t c = count_connecting(&A, u, u, &e);
+    if (c != 1) {
+      if (err_a) *err_a = j;
+      if (err_b) *err_b = j;
+      adj_free(&A);
+      return c == 0 ? SGO_ERR_NO_EDGE : SGO_ERR_MULTI_EDGE;
+    }
+    if (j >= row_begin && j < row_end) {
+      size_t idx = (size_t)(j - row_begin) * n_used + j;
+      out_lat[idx] = elat[e];
+      out_loss[idx] = eloss[e];
+    }
+  }
+  adj_free(&A);
+  if (J.err == SGO_ERR_UNREACHABLE) {
+    if (err_a) *err_a = J.err_row;
+    if (err_b) *err_b = J.err_col;
+    return SGO_ERR_UNREACHABLE;
+  }
+  return SGO_OK;
+}
+
+/*
+ * NetworkGraph::get_direct_paths (graph/mod.rs:230-252): the raw edge for every
+ * used pair; exactly one edge required; first failing pair in row-major order.
+ */
+int sgo_direct_paths(uint32_t n, uint32_t m, const uint32_t* esrc, const uint32_t* edst,
+                     const uint64_t* elat, const float* eloss, int directed, const uint32_t* used,
+                     uint32_t n_used, uint64_t* out_lat, float* out_loss, uint32_t* err_a,
+                     uint32_t* err_b) {
+  for (uint32_t j = 0; j < n_used; j++)
+    if (used[j] >= n) return SGO_ERR_ARG;
+  sgo_adj A;
+  memset(&A, 0, sizeof(A));
+  int rc = adj_build(&A, n, m, esrc, edst, directed);
+  if (rc) {
+    adj_free(&A);
+    return rc;
+  }
+  uint32_t* cnt = (uint32_t*)calloc((size_t)n + 1, sizeof(uint32_t));
+  uint32_t* first = (uint32_t*)malloc(((size_t)n + 1) * sizeof(uint32_t));
+  if (!cnt || !first) {
+    free(cnt);
+    free(first);
+    adj_free(&A);
+    return SGO_ERR_OOM;
+  }
+  rc = SGO_OK;
+  for (uint32_t i = 0; i < n_used && rc == SGO_OK; i++) {
+    uint32_t u = used[i];
+    for (uint32_t k = A.off[u]; k < A.off[u + 1]; k++) {
+      uint32_t v = A.dst[k];
+      if (cnt[v]++ == 0) first[v] = A.edge[k];
+    }
+    for (uint32_t j = 0; j < n_used; j++) {
+      uint32_t v = used[j];
+      if (cnt[v] != 1) {
+        rc = cnt[v] == 0 ? SGO_ERR_NO_EDGE : SGO_ERR_MULTI_EDGE;
+        if (err_a) *err_a = i;
+        if (err_b) *err_b = j;
+        break;
+      }
+      out_lat[(size_t)i * n_used + j] = elat[first[v]];
+      out_loss[(size_t)i * n_used + j] = eloss[first[v]];
+    }
+    for (uint32_t k = A.off[u]; k < A.off[u + 1]; k++) cnt[A.dst[k]] = 0;
+  }
+  free(cnt);
+  free(first);
+  adj_free(&A);
+  return rc;
+}
+
+/* RoutingInfo::get_smallest_latency_ns (graph/mod.rs:478-480): min over all
+ * entries, self pairs included. */
+uint64_t sgo_smallest_latency(const uint64_t* lat, size_t count) {
+  uint64_t m = UINT64_MAX;
+  for (size_t i = 0; i < count; i++)
+    if (lat[i] < m) m = lat[i];
+  return m;
+}
+
+/* ------------------------------------------------------------------------- */
+/* RNG: rand_xoshiro 0.7.0 Xoshiro256PlusPlus (host/host.rs:221), seeded by   */
+/* SeedableRng::seed_from_u64 = SplitMix64 (sim_config.rs:48-51), and         */
+/* rand 0.9.1 StandardUniform f64 = (next_u64 >> 11) * 2^-53 (worker.rs:360). */
+/* [external: restated from the published upstream algorithms]               */
+/* ------------------------------------------------------------------------- */
+static inline uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+uint64_t sgo_splitmix64_next(uint64_t* state) {
+  *state += 0x9E3779B97F4A7C15ull;
+  uint64_t z = *state;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+void sgo_xoshiro_seed_from_u64(uint64_t seed, uint64_t s[4]) {
+  uint64_t st = seed;
+  for (int i = 0; i < 4; i++) s[i] = sgo_splitmix64_next(&st);
+  if (!s[0] && !s[1] && !s[2] && !s[3]) sgo_xoshiro_seed_from_u64(0, s); /* from_seed all-zero guard */
+}
+
+uint64_t sgo_xoshiro_next_u64(uint64_t s[4]) {
+  uint64_t r = rotl64(s[0] + s[3], 23) + s[0];
+  uint64_t t = s[1] << 17;
+  s[2] ^= s[0];
+  s[3] ^= s[1];
+  s[1] ^= s[2];
+  s[0] ^= s[3];
+  s[2] ^= t;
+  s[3] = rotl64(s[3], 45);
+  return r;
+}
+
+double sgo_xoshiro_next_f64(uint64_t s[4]) {
+  return (double)(sgo_xoshiro_next_u64(s) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+/* std DefaultHasher = SipHash-1-3 with k0 = k1 = 0 (sim_config.rs:221-225). */
+#define SIPROUND                   \
+  do {                             \
+    v0 += v1;                      \
+    v1 = rotl64(v1, 13);           \
+    v1 ^= v0;                      \
+    v0 = rotl64(v0, 32);           \
+    v2 += v3;                      \
+    v3 = rotl64(v3, 16);           \
+    v3 ^= v2;                      \
+    v0 += v3;                      \
+    v3 = rotl64(v3, 21);           \
+    v3 ^= v0;                      \
+    v2 += v1;                      \
+    v1 = rotl64(v1, 17);           \
+    v1 ^= v2;                      \
+    v2 = rotl64(v2, 32);           \
+  } while (0)
+
+uint64_t sgo_siphash13(const uint8_t* data, size_t len) {
+  uint64_t v0 = 0x736f6d6570736575ull, v1 = 0x646f72616e646f6dull;
+  uint64_t v2 = 0x6c7967656e657261ull, v3 = 0x7465646279746573ull;
+  size_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint64_t m = 0;
+    for (int b = 0; b < 8; b++) m |= (uint64_t)data[i + b] << (8 * b);
+    v3 ^= m;
+    SIPROUND;
+    v0 ^= m;
+  }
+  uint64_t b = (uint64_t)len << 56;
+  for (size_t k = 0; i + k < len; k++) b |= (uint64_t)data[i + k] << (8 * k);
+  v3 ^= b;
+  SIPROUND;
+  v0 ^= b;
+  v2 ^= 0xff;
+  SIPROUND;
+  SIPROUND;
+  SIPROUND;
+  return v0 ^ v1 ^ v2 ^ v3;
+}
+
+/* HostInfo.seed (sim_config.rs:50-54,221-225,242): first u64 of the
+ * general-seed stream XOR SipHash13(hostname bytes || 0xFF). */
+uint64_t sgo_host_seed(uint64_t general_seed, const char* hostname, size_t len) {
+  uint64_t s[4];
+  sgo_xoshiro_seed_from_u64(general_seed, s);
+  uint64_t r = sgo_xoshiro_next_u64(s);
+  uint8_t* buf = (uint8_t*)malloc(len + 1);
+  memcpy(buf, hostname, len);
+  buf[len] = 0xff;
+  uint64_t h = sgo_siphash13(buf, len + 1);
+  free(buf);
+  return r ^ h;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Worker::send_packet over one round's batch (worker.rs:322-397) + event     */
+/* order (event.rs:84-155) + push_packet_to_host (worker.rs:597-607).          */
+/* ------------------------------------------------------------------------- */
+#define SGO_ST_DELIVERED 0  /* PacketStatus::InetSent, pushed to dst queue */
+#define SGO_ST_DROP_LOSS 1  /* InetDropped after the reliability draw (:365-368) */
+#define SGO_ST_DROP_NO_DST 2 /* InetDropped, unknown destination, no draw (:341-351) */
+#define SGO_ST_SIM_END 3    /* now >= sim_end: returns before anything (:332-335) */
+
+typedef struct {
+  uint32_t ip, host;
+} ip_host;
+
+static int cmp_ip(const void* a, const void* b) {
+  uint32_t x = ((const ip_host*)a)->ip, y = ((const ip_host*)b)->ip;
+  return x < y ? -1 : x > y;
+}
+
+typedef struct {
+  uint64_t t;
+  uint32_t src;
+  uint64_t eid;
+  uint32_t idx;
+} ord_item;
+
+/* Event ordering (event.rs:84-155): time, then Packet data by (src_host_id,
+ * src_host_event_id).  The key is unique per delivered packet. */
+static int cmp_ord(const void* a, const void* b) {
+  const ord_item* x = (const ord_item*)a;
+  const ord_item* y = (const ord_item*)b;
+  if (x->t != y->t) return x->t < y->t ? -1 : 1;
+  if (x->src != y->src) return x->src < y->src ? -1 : 1;
+  return x->eid < y->eid ? -1 : (x->eid > y->eid);
+}
+
+/*
+ * Packets appear in each source host's send order (the order send_packet is
+ * called for that host); hosts may interleave.  host_row[h] = routing-table row/column of host h's node; the
+ * table is n_cols x n_cols (row = source).  rng (4*n_hosts) and event_ctr
+ * (n_hosts) are the per-host Xoshiro state and event-id counter, in/out.
+ * Outputs: status, deliver_time, event_id per packet; dst_order = delivered
+ * packet indices grouped by destination host and ordered as the destination's
+ * EventQueue pops them: (time, src_host_id, src_host_event_id); dst_offsets
+ * (n_hosts+1); min_deliver = min next-event time (worker.rs:388), min_lat =
+ * min used latency (worker.rs:372); UINT64_MAX when nothing was delivered.
+ * Returns the number of delivered packets, or -1 on a bad argument.
+ */
+int64_t sgo_deliver_round(uint64_t round_end, uint64_t sim_end, uint64_t bootstrap_end,
+                          uint32_t n_pkts, const uint32_t* src_host, const uint32_t* dst_ip,
+                          const uint32_t* payload_len, const uint64_t* send_time, uint32_t n_hosts,
+                          const uint32_t* host_ip, const uint32_t* host_row, uint32_t n_cols,
+                          const uint64_t* tab_lat, const float* tab_loss, uint64_t* rng,
+                          uint64_t* event_ctr, uint8_t* status, uint64_t* deliver_time,
+                          uint64_t* event_id, uint32_t* dst_order, uint32_t* dst_offsets,
+                          uint64_t* min_deliver, uint64_t* min_lat) {
+  ip_host* map = (ip_host*)malloc(((size_t)n_hosts + 1) * sizeof(ip_host));
+  uint32_t* dst_host = (uint32_t*)malloc(((size_t)n_pkts + 1) * sizeof(uint32_t));
+  if (!map || !dst_host) return -1;
+  for (uint32_t h = 0; h < n_hosts; h++) {
+    map[h].ip = host_ip[h];
+    map[h].host = h;
+    if (host_row[h] >= n_cols) return -1;
+  }
+  qsort(map, n_hosts, sizeof(ip_host), cmp_ip);
+  uint64_t mind = UINT64_MAX, minl = UINT64_MAX;
+  int64_t delivered = 0;
+  for (uint32_t i = 0; i < n_pkts; i++) {
+    uint32_t s = src_host[i];
+    if (s >= n_hosts) return -1;
+    uint64_t now = send_time[i];
+    deliver_time[i] = 0;
+    event_id[i] = UINT64_MAX;
+    dst_host[i] = UINT32_MAX;
+    if (now >= sim_end) {
+      status[i] = SGO_ST_SIM_END;
+      continue;
+    }
+    ip_host key = {dst_ip[i], 0};
+    ip_host* f = (ip_host*)bsearch(&key, map, n_hosts, sizeof(ip_host), cmp_ip);
+    if (!f) {
+      status[i] = SGO_ST_DROP_NO_DST;
+      continue;
+    }
+    uint32_t d = f->host;
+    size_t cell = (size_t)host_row[s] * n_cols + host_row[d];
+    double reliability = (double)(1.0f - tab_loss[cell]); /* worker.rs:357-359,526-531 */
+    double chance = sgo_xoshiro_next_f64(&rng[4 * (size_t)s]);
+    int bootstrapping = now < bootstrap_end;
+    if (!bootstrapping && chance >= reliability && payload_len[i] > 0) {
+      status[i] = SGO_ST_DROP_LOSS;
+      continue;
+    }
+    uint64_t delay = tab_lat[cell];
+    if (delay < minl) minl = delay;
+    uint64_t t = now + delay;
+    if (t < round_end) t = round_end;
+    if (t < mind) mind = t;
+    status[i] = SGO_ST_DELIVERED;
+    deliver_time[i] = t;
+    event_id[i] = event_ctr[s]++;
+    dst_host[i] = d;
+    delivered++;
+  }
+  /* bucket by destination, then each bucket in EventQueue pop order. */
+  memset(dst_offsets, 0, ((size_t)n_hosts + 1) * sizeof(uint32_t));
+  for (uint32_t i = 0; i < n_pkts; i++)
+    if (dst_host[i] != UINT32_MAX) dst_offsets[dst_host[i] + 1]++;
+  for (uint32_t h = 0; h < n_hosts; h++) dst_offsets[h + 1] += dst_offsets[h];
+  ord_item* tmp = (ord_item*)malloc(((size_t)delivered + 1) * sizeof(ord_item));
+  uint32_t* cur = (uint32_t*)malloc(((size_t)n_hosts + 1) * sizeof(uint32_t));
+  memcpy(cur, dst_offsets, ((size_t)n_hosts + 1) * sizeof(uint32_t));
+  for (uint32_t i = 0; i < n_pkts; i++)
+    if (dst_host[i] != UINT32_MAX) {
+      ord_item it = {deliver_time[i], src_host[i], event_id[i], i};
+      tmp[cur[dst_host[i]]++] = it;
+    }
+  for (uint32_t h = 0; h < n_hosts; h++) {
+    uint32_t b = dst_offsets[h], e = dst_offsets[h + 1];
+    qsort(tmp + b, e - b, sizeof(ord_item), cmp_ord);
+  }
+  for (int64_t k = 0; k < delivered; k++) dst_order[k] = tmp[k].idx;
+  free(tmp);
+  free(cur);
+  free(map);
+  free(dst_host);
+  *min_deliver = mind;
+  *min_lat = minl;
+  return delivered;
+}

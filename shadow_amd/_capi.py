@@ -1,0 +1,149 @@
+"""ctypes binding of include/shadow_gpu.h (libshadow_gpu.so, built in-tree).
+
+The product path has no CPU fallback: if the HIP library is missing or fails
+to load, importing a compute entry point raises `ShadowGpuUnavailable`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libshadow_gpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "shadow_gpu.h")
+
+# sg_status (include/shadow_gpu.h)
+SG_OK = 0
+SG_ERR_NO_EDGE = 1
+SG_ERR_MULTI_EDGE = 2
+SG_ERR_UNREACHABLE = 3
+SG_ERR_OOM = 4
+SG_ERR_INVALID_ARG = 5
+SG_ERR_DEVICE = 6
+SG_ERR_PARSE = 7
+SG_ERR_UNSORTED = 8
+SG_ERR_DUPLICATE_IP = 9
+
+SG_ROUTE_SHORTEST_PATH = 0x1
+SG_ROUTE_OUT_DEVICE = 0x2
+
+SG_PKT_DELIVERED, SG_PKT_DROP_LOSS, SG_PKT_DROP_NO_DST, SG_PKT_SIM_END = range(4)
+
+EXPORTED = [
+    "sg_abi_version", "sg_ctx_create", "sg_ctx_destroy", "sg_ctx_set_stream", "sg_ctx_stream",
+    "sg_ctx_synchronize", "sg_ctx_last_error", "sg_ctx_last_error_pair", "sg_ctx_enable_timers",
+    "sg_ctx_read_timer", "sg_gml_parse", "sg_gml_graph",
+    "sg_gml_node_index", "sg_gml_destroy", "sg_net_create", "sg_net_destroy", "sg_routing_build",
+    "sg_routing_min_latency", "sg_hosts_create", "sg_hosts_get_state", "sg_hosts_set_state",
+    "sg_hosts_destroy", "sg_deliver_round",
+]
+
+
+class ShadowGpuUnavailable(RuntimeError):
+    pass
+
+
+class ShadowGpuError(RuntimeError):
+    """A non-OK sg_status.  `pair` = (row, col) of the failing entry where relevant."""
+
+    def __init__(self, code: int, message: str, pair=(0, 0)):
+        super().__init__(message)
+        self.code = code
+        self.pair = pair
+
+
+class sg_graph(C.Structure):
+    _fields_ = [("n_nodes", C.c_uint32), ("n_edges", C.c_uint32),
+                ("edge_src", C.POINTER(C.c_uint32)), ("edge_dst", C.POINTER(C.c_uint32)),
+                ("edge_latency_ns", C.POINTER(C.c_uint64)), ("edge_packet_loss", C.POINTER(C.c_float)),
+                ("node_gml_id", C.POINTER(C.c_uint32)), ("directed", C.c_uint8)]
+
+
+class sg_table(C.Structure):
+    _fields_ = [("latency_ns", C.c_void_p), ("packet_loss", C.c_void_p), ("n_cols", C.c_uint32),
+                ("row_begin", C.c_uint32), ("n_rows", C.c_uint32)]
+
+
+class sg_round(C.Structure):
+    _fields_ = [("round_end_ns", C.c_uint64), ("sim_end_ns", C.c_uint64), ("bootstrap_end_ns", C.c_uint64)]
+
+
+class sg_packets(C.Structure):
+    _fields_ = [("n_packets", C.c_uint32), ("src_host", C.c_void_p), ("dst_ipv4", C.c_void_p),
+                ("payload_len", C.c_void_p), ("send_time_ns", C.c_void_p)]
+
+
+class sg_deliveries(C.Structure):
+    _fields_ = [("status", C.c_void_p), ("deliver_time_ns", C.c_void_p), ("event_id", C.c_void_p),
+                ("dst_order", C.c_void_p), ("dst_offsets", C.c_void_p)]
+
+
+class sg_round_stats(C.Structure):
+    _fields_ = [("n_delivered", C.c_uint64), ("min_deliver_time_ns", C.c_uint64),
+                ("min_used_latency_ns", C.c_uint64)]
+
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load libshadow_gpu.so; raises ShadowGpuUnavailable (never falls back)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or os.environ.get("SHADOW_GPU_LIB", LIB_PATH)
+    if not os.path.exists(path):
+        raise ShadowGpuUnavailable(
+            f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    try:
+        L = C.CDLL(path)
+    except OSError as e:
+        raise ShadowGpuUnavailable(f"cannot load {path}: {e}") from e
+    vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
+    u32p, u64p = C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
+    sig = {
+        "sg_abi_version": (i32, []),
+        "sg_ctx_create": (i32, [i32, C.POINTER(vp)]),
+        "sg_ctx_destroy": (None, [vp]),
+        "sg_ctx_set_stream": (i32, [vp, vp]),
+        "sg_ctx_stream": (vp, [vp]),
+        "sg_ctx_synchronize": (i32, [vp]),
+        "sg_ctx_last_error": (C.c_char_p, [vp]),
+        "sg_ctx_last_error_pair": (None, [vp, u32p, u32p]),
+        "sg_ctx_enable_timers": (i32, [vp, i32]),
+        "sg_ctx_read_timer": (i32, [vp, C.c_char_p, C.POINTER(C.c_double), u64p, C.POINTER(C.c_double)]),
+        "sg_gml_parse": (i32, [C.c_char_p, C.c_size_t, C.POINTER(vp), C.c_char_p, C.c_size_t]),
+        "sg_gml_graph": (i32, [vp, C.POINTER(sg_graph)]),
+        "sg_gml_node_index": (i32, [vp, u32, u32p]),
+        "sg_gml_destroy": (None, [vp]),
+        "sg_net_create": (i32, [vp, C.POINTER(sg_graph), C.POINTER(vp)]),
+        "sg_net_destroy": (None, [vp]),
+        "sg_routing_build": (i32, [vp, vp, vp, u32, u32, u32, u32, vp, vp]),
+        "sg_routing_min_latency": (i32, [vp, vp, C.c_size_t, u64p]),
+        "sg_hosts_create": (i32, [vp, u32, vp, vp, vp, C.POINTER(vp)]),
+        "sg_hosts_get_state": (i32, [vp, vp, vp]),
+        "sg_hosts_set_state": (i32, [vp, vp, vp]),
+        "sg_hosts_destroy": (None, [vp]),
+        "sg_deliver_round": (i32, [vp, vp, C.POINTER(sg_table), C.POINTER(sg_round), C.POINTER(sg_packets),
+                                   C.POINTER(sg_deliveries), C.POINTER(sg_round_stats)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    if L.sg_abi_version() != 1:
+        raise ShadowGpuUnavailable("ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(ctx_handle, rc: int) -> None:
+    if rc == SG_OK:
+        return
+    L = load()
+    msg = L.sg_ctx_last_error(ctx_handle).decode(errors="replace") if ctx_handle else f"status {rc}"
+    r, c = C.c_uint32(), C.c_uint32()
+    if ctx_handle:
+        L.sg_ctx_last_error_pair(ctx_handle, C.byref(r), C.byref(c))
+    raise ShadowGpuError(rc, msg, (r.value, c.value))

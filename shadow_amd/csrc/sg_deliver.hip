@@ -1,0 +1,592 @@
+// sg_deliver.hip -- one scheduling round of inter-host packet delivery.
+//
+// Replaces the per-packet body of Worker::send_packet (worker.rs:322-397) and
+// WorkerShared::push_packet_to_host (worker.rs:597-607), batched at the round
+// boundary.  Batching is exact: every packet sent in [start, end) is delivered
+// at max(now + latency, end) (worker.rs:380-384) and Host::execute(end) only
+// pops events < end (host.rs:749-758), so no destination can observe a packet
+// of this round before the round ends.
+//
+// Pipeline (all on the context stream):
+//   k_seg_bounds   per packet: per-source-host segment [begin, end), order check
+//   k_walk         per source host: the host's packets in send order --
+//                  resolve dst (Dns::addr_to_host_id), path (latency, loss),
+//                  Xoshiro256++ f64 draw, drop test, arrival time, event id
+//   scan           per-destination counts -> dst_offsets
+//   k_scatter      delivered packets -> destination buckets (unordered)
+//   k_sort_small   thread per destination: order bucket by the EventQueue key
+//   k_sort_big     block per large bucket: LDS bitonic chunks + merge passes
+// Event order (event.rs:84-155): (time, Packet < Local, src_host_id,
+// src_host_event_id).  Inside a bucket every element is a packet; since the
+// input is grouped by ascending source host in send order and event ids grow
+// in send order, (src_host_id, src_host_event_id) order == packet-index order,
+// so the bucket key is (deliver_time, packet index).
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "sg_device.h"
+#include "sg_internal.h"
+
+struct sg_hosts {
+  sg_ctx* ctx = nullptr;
+  uint32_t n = 0;
+  uint32_t* route = nullptr;  // host -> routing-table index
+  uint64_t* rng = nullptr;    // SoA [4][n]
+  uint64_t* ctr = nullptr;    // n
+  // address -> host: dense window or sorted table
+  uint32_t ip_base = 0, dense_span = 0;
+  uint32_t* dense = nullptr;
+  uint32_t* sorted_ip = nullptr;
+  uint32_t* sorted_host = nullptr;
+  ~sg_hosts() {
+    void* ps[] = {route, rng, ctr, dense, sorted_ip, sorted_host};
+    for (void* p : ps)
+      if (p) (void)hipFree(p);
+  }
+};
+
+namespace sg {
+
+constexpr uint32_t NONE = ~0u;
+constexpr int SMALL_BUCKET = 32;
+constexpr int SORT_BLOCK = 256;
+constexpr int SORT_CHUNK = 2048;  // elements sorted in LDS per chunk
+
+enum : uint32_t { ERR_UNSORTED = 1, ERR_SRC_RANGE = 2, ERR_ROUTE_RANGE = 4 };
+
+struct HostMap {
+  uint32_t ip_base, dense_span, n_sorted;
+  const uint32_t* dense;
+  const uint32_t* sorted_ip;
+  const uint32_t* sorted_host;
+  // Dns::addr_to_host_id (dns.rs:174-176)
+  __device__ __forceinline__ uint32_t resolve(uint32_t ip) const {
+    if (dense) {
+      uint32_t off = ip - ip_base;
+      return off < dense_span ? dense[off] : NONE;
+    }
+    uint32_t lo = 0, hi = n_sorted;
+    while (lo < hi) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (sorted_ip[mid] < ip)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    return (lo < n_sorted && sorted_ip[lo] == ip) ? sorted_host[lo] : NONE;
+  }
+};
+
+__global__ void k_seed_hosts(const uint64_t* __restrict__ seed, uint32_t n, uint64_t* __restrict__ rng) {
+  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < n; h += gridDim.x * blockDim.x) {
+    Xoshiro x = xoshiro_seed_from_u64(seed[h]);
+    rng[h] = x.s0;
+    rng[(size_t)n + h] = x.s1;
+    rng[2 * (size_t)n + h] = x.s2;
+    rng[3 * (size_t)n + h] = x.s3;
+  }
+}
+
+__global__ void k_seg_bounds(const uint32_t* __restrict__ src, uint32_t P, uint32_t H,
+                             uint32_t* __restrict__ seg_begin, uint32_t* __restrict__ seg_end,
+                             uint32_t* __restrict__ err) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < P; i += gridDim.x * blockDim.x) {
+    uint32_t h = src[i];
+    if (h >= H) {
+      atomicOr(err, ERR_SRC_RANGE);
+      continue;
+    }
+    uint32_t prev = i ? src[i - 1] : NONE;
+    uint32_t next = i + 1 < P ? src[i + 1] : NONE;
+    if (i && prev > h) atomicOr(err, ERR_UNSORTED);
+    if (prev != h) seg_begin[h] = i;
+    if (next != h) seg_end[h] = i + 1;
+  }
+}
+
+struct WalkArgs {
+  const uint32_t* src;
+  const uint32_t* dst_ip;
+  const uint32_t* payload;
+  const uint64_t* send;
+  uint32_t P, H;
+  const uint32_t* seg_begin;
+  const uint32_t* seg_end;
+  const uint32_t* route;
+  uint64_t* rng;
+  uint64_t* ctr;
+  HostMap map;
+  const uint64_t* tab_lat;
+  const float* tab_loss;
+  uint32_t n_cols, row_begin, n_rows;
+  uint64_t round_end, sim_end, bootstrap_end;
+  uint8_t* status;
+  uint64_t* deliver;
+  uint64_t* eid;
+  uint32_t* dst_host;
+  uint32_t* dst_cnt;
+  unsigned long long* stats;  // [n_delivered, min_deliver, min_lat]
+  uint32_t* err;
+};
+
+// One thread per source host: the host's RNG stream is sequential
+// (Host::random_mut, host.rs:645-647), so its packets are walked in send order.
+__global__ void __launch_bounds__(256) k_walk(WalkArgs a) {
+  const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long nd = 0, mind = ~0ull, minl = ~0ull;
+  if (h < a.H) {
+    const uint32_t b = a.seg_begin[h], e = a.seg_end[h];
+    if (b < e) {
+      const uint32_t r = a.route[h];
+      if (r < a.row_begin || r - a.row_begin >= a.n_rows) {
+        atomicOr(a.err, ERR_ROUTE_RANGE);
+      } else {
+        const size_t row = (size_t)(r - a.row_begin) * a.n_cols;
+        Xoshiro x{a.rng[h], a.rng[(size_t)a.H + h], a.rng[2 * (size_t)a.H + h],
+                  a.rng[3 * (size_t)a.H + h]};
+        uint64_t c = a.ctr[h];
+        for (uint32_t i = b; i < e; i++) {
+          const uint64_t now = a.send[i];
+          uint8_t st;
+          uint64_t t = 0, id = ~0ull;
+          uint32_t d = NONE;
+          if (now >= a.sim_end) {  // worker.rs:332-335
+            st = SG_PKT_SIM_END;
+          } else {
+            d = a.map.resolve(a.dst_ip[i]);  // worker.rs:341
+            if (d == NONE) {
+              st = SG_PKT_DROP_NO_DST;
+            } else {
+              const size_t cell = row + a.route[d];
+              // reliability = f64::from(1.0f32 - loss) (worker.rs:357-359, 526-531)
+              const double rel = (double)__fsub_rn(1.0f, a.tab_loss[cell]);
+              const double chance = x.next_f64();  // worker.rs:360
+              const bool boot = now < a.bootstrap_end;
+              if (!boot && chance >= rel && a.payload[i] > 0) {  // worker.rs:365-368
+                st = SG_PKT_DROP_LOSS;
+                d = NONE;
+              } else {
+                const uint64_t lat = a.tab_lat[cell];  // worker.rs:370
+                t = now + lat;
+                if (t < a.round_end) t = a.round_end;  // worker.rs:381-384
+                id = c++;                              // host.rs:649-653
+                st = SG_PKT_DELIVERED;
+                nd++;
+                mind = min(mind, (unsigned long long)t);
+                minl = min(minl, (unsigned long long)lat);
+                atomicAdd(&a.dst_cnt[d], 1u);
+              }
+            }
+          }
+          a.status[i] = st;
+          a.deliver[i] = t;
+          a.eid[i] = id;
+          a.dst_host[i] = d;
+        }
+        a.rng[h] = x.s0;
+        a.rng[(size_t)a.H + h] = x.s1;
+        a.rng[2 * (size_t)a.H + h] = x.s2;
+        a.rng[3 * (size_t)a.H + h] = x.s3;
+        a.ctr[h] = c;
+      }
+    }
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    nd += __shfl_xor(nd, d, 64);
+    mind = min(mind, (unsigned long long)__shfl_xor(mind, d, 64));
+    minl = min(minl, (unsigned long long)__shfl_xor(minl, d, 64));
+  }
+  if ((threadIdx.x & 63) == 0 && nd) {
+    atomicAdd(&a.stats[0], nd);
+    atomicMin(&a.stats[1], mind);
+    atomicMin(&a.stats[2], minl);
+  }
+}
+
+__global__ void k_scatter(const uint32_t* __restrict__ dst_host, const uint64_t* __restrict__ deliver,
+                          uint32_t P, const uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
+                          uint64_t* __restrict__ kt, uint32_t* __restrict__ ki) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < P; i += gridDim.x * blockDim.x) {
+    uint32_t d = dst_host[i];
+    if (d == NONE) continue;
+    uint32_t p = off[d] + atomicAdd(&cur[d], 1u);
+    kt[p] = deliver[i];
+    ki[p] = i;
+  }
+}
+
+__device__ __forceinline__ bool key_less(uint64_t ta, uint32_t ia, uint64_t tb, uint32_t ib) {
+  return ta < tb || (ta == tb && ia < ib);
+}
+
+// Thread per destination: insertion sort of a small bucket; big buckets are
+// queued for k_sort_big.
+__global__ void k_sort_small(const uint32_t* __restrict__ off, uint32_t H, uint64_t* __restrict__ kt,
+                             uint32_t* __restrict__ ki, uint32_t* __restrict__ order,
+                             uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
+  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < H; h += gridDim.x * blockDim.x) {
+    const uint32_t b = off[h], e = off[h + 1];
+    if (e - b > SMALL_BUCKET) {
+      big_list[atomicAdd(big_count, 1u)] = h;
+      continue;
+    }
+    for (uint32_t i = b + 1; i < e; i++) {
+      uint64_t t = kt[i];
+      uint32_t x = ki[i];
+      uint32_t j = i;
+      while (j > b && key_less(t, x, kt[j - 1], ki[j - 1])) {
+        kt[j] = kt[j - 1];
+        ki[j] = ki[j - 1];
+        j--;
+      }
+      kt[j] = t;
+      ki[j] = x;
+    }
+    for (uint32_t i = b; i < e; i++) order[i] = ki[i];
+  }
+}
+
+// Block per large bucket.  Chunks of SORT_CHUNK are bitonic-sorted in LDS,
+// then merged pairwise (merge path) between two global buffers.
+__global__ void __launch_bounds__(SORT_BLOCK)
+    k_sort_big(const uint32_t* __restrict__ off, const uint32_t* __restrict__ big_list,
+               const uint32_t* __restrict__ big_count, uint64_t* __restrict__ kt,
+               uint32_t* __restrict__ ki, uint64_t* __restrict__ kt2, uint32_t* __restrict__ ki2,
+               uint32_t* __restrict__ order) {
+  __shared__ uint64_t st[SORT_CHUNK];
+  __shared__ uint32_t si[SORT_CHUNK];
+  const uint32_t nbig = *big_count;
+  for (uint32_t q = blockIdx.x; q < nbig; q += gridDim.x) {
+    const uint32_t h = big_list[q];
+    const uint32_t b = off[h], e = off[h + 1], n = e - b;
+    // 1. sort chunks in LDS
+    for (uint32_t c0 = 0; c0 < n; c0 += SORT_CHUNK) {
+      const uint32_t cn = min((uint32_t)SORT_CHUNK, n - c0);
+      uint32_t pow2 = 1;
+      while (pow2 < cn) pow2 <<= 1;
+      for (uint32_t i = threadIdx.x; i < pow2; i += SORT_BLOCK) {
+        if (i < cn) {
+          st[i] = kt[b + c0 + i];
+          si[i] = ki[b + c0 + i];
+        } else {
+          st[i] = ~0ull;
+          si[i] = ~0u;
+        }
+      }
+      __syncthreads();
+      for (uint32_t k = 2; k <= pow2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+          for (uint32_t i = threadIdx.x; i < pow2; i += SORT_BLOCK) {
+            uint32_t l = i ^ j;
+            if (l > i) {
+              bool up = (i & k) == 0;
+              bool sw = up ? key_less(st[l], si[l], st[i], si[i]) : key_less(st[i], si[i], st[l], si[l]);
+              if (sw) {
+                uint64_t tt = st[i];
+                st[i] = st[l];
+                st[l] = tt;
+                uint32_t ii = si[i];
+                si[i] = si[l];
+                si[l] = ii;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      for (uint32_t i = threadIdx.x; i < cn; i += SORT_BLOCK) {
+        kt[b + c0 + i] = st[i];
+        ki[b + c0 + i] = si[i];
+      }
+      __syncthreads();
+    }
+    // 2. merge runs of width w into the other buffer until one run remains
+    uint64_t* at = kt + b;
+    uint32_t* ai = ki + b;
+    uint64_t* bt = kt2 + b;
+    uint32_t* bi = ki2 + b;
+    for (uint32_t w = SORT_CHUNK; w < n; w <<= 1) {
+      for (uint32_t p = threadIdx.x; p < n; p += SORT_BLOCK) {
+        // output position p belongs to the pair of runs starting at s
+        const uint32_t s = (p / (2 * w)) * (2 * w);
+        const uint32_t m = min(s + w, n), t = min(s + 2 * w, n);
+        const uint32_t k = p - s;  // rank within the merged pair
+        // merge path: find i in run A (s..m) and j = k - i in run B (m..t)
+        uint32_t lo = k > (t - m) ? k - (t - m) : 0, hi = min(k, m - s);
+        while (lo < hi) {
+          uint32_t i = (lo + hi) >> 1;  // take i from A, k-i from B
+          uint32_t j = k - i;
+          // A[i] < B[j-1] ?  (stable: A wins ties; keys are unique anyway)
+          if (key_less(bt == kt2 + b ? at[s + i] : at[s + i], ai[s + i], at[m + j - 1], ai[m + j - 1]))
+            lo = i + 1;
+          else
+            hi = i;
+        }
+        const uint32_t i = lo, j = k - lo;
+        bool takeA;
+        if (s + i >= m)
+          takeA = false;
+        else if (m + j >= t)
+          takeA = true;
+        else
+          takeA = !key_less(at[m + j], ai[m + j], at[s + i], ai[s + i]);
+        if (takeA) {
+          bt[p] = at[s + i];
+          bi[p] = ai[s + i];
+        } else {
+          bt[p] = at[m + j];
+          bi[p] = ai[m + j];
+        }
+      }
+      __syncthreads();
+      uint64_t* tt = at;
+      at = bt;
+      bt = tt;
+      uint32_t* ti = ai;
+      ai = bi;
+      bi = ti;
+    }
+    for (uint32_t p = threadIdx.x; p < n; p += SORT_BLOCK) order[b + p] = ai[p];
+    __syncthreads();
+  }
+}
+
+static void fail_flags(uint32_t err) {
+  if (err & ERR_SRC_RANGE) throw Error(SG_ERR_INVALID_ARG, "packet source host out of range");
+  if (err & ERR_UNSORTED)
+    throw Error(SG_ERR_UNSORTED, "packets must be grouped by ascending source host (send order within a host)");
+  if (err & ERR_ROUTE_RANGE)
+    throw Error(SG_ERR_INVALID_ARG, "a sending host's route row is outside the table shard");
+}
+
+static void deliver_round(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const sg_round* rd,
+                          const sg_packets* pk, sg_deliveries* out, sg_round_stats* stats) {
+  hipStream_t st = ctx->stream;
+  const uint32_t P = pk->n_packets, H = hs->n;
+  // workspace: [seg_begin H][seg_end H][dst_cnt H][cur H][big_count 1][err 1] + stats
+  uint32_t* ws = ctx->d_seg.get<uint32_t>(4 * (size_t)H + 8);
+  uint32_t* seg_begin = ws;
+  uint32_t* seg_end = ws + H;
+  uint32_t* dst_cnt = ws + 2 * (size_t)H;
+  uint32_t* cur = ws + 3 * (size_t)H;
+  uint32_t* big_count = ws + 4 * (size_t)H;
+  uint32_t* err = big_count + 1;
+  unsigned long long* dstats = ctx->d_misc.get<unsigned long long>(4);
+  SG_HIP(hipMemsetAsync(ws, 0, (4 * (size_t)H + 8) * 4, st));
+  SG_HIP(hipMemsetAsync(dstats, 0, 8, st));
+  SG_HIP(hipMemsetAsync(dstats + 1, 0xff, 16, st));
+  uint32_t* dst_host = ctx->d_dst.get<uint32_t>(P);
+  uint64_t* kt = ctx->d_keys.get<uint64_t>(P);
+  uint32_t* ki = ctx->d_vals.get<uint32_t>(P);
+  uint32_t* big_list = ctx->d_lists.get<uint32_t>(H);
+  if (P) {
+    {
+      TimedLaunch tl(ctx, "seg_bounds", 4.0 * P + 8.0 * H);
+      hipLaunchKernelGGL(k_seg_bounds, dim3(grid_for(P, 256, 16384)), dim3(256), 0, st, pk->src_host, P,
+                         H, seg_begin, seg_end, err);
+    }
+    WalkArgs a;
+    a.src = pk->src_host;
+    a.dst_ip = pk->dst_ipv4;
+    a.payload = pk->payload_len;
+    a.send = pk->send_time_ns;
+    a.P = P;
+    a.H = H;
+    a.seg_begin = seg_begin;
+    a.seg_end = seg_end;
+    a.route = hs->route;
+    a.rng = hs->rng;
+    a.ctr = hs->ctr;
+    a.map = HostMap{hs->ip_base, hs->dense_span, hs->n, hs->dense, hs->sorted_ip, hs->sorted_host};
+    a.tab_lat = tab->latency_ns;
+    a.tab_loss = tab->packet_loss;
+    a.n_cols = tab->n_cols;
+    a.row_begin = tab->row_begin;
+    a.n_rows = tab->n_rows;
+    a.round_end = rd->round_end_ns;
+    a.sim_end = rd->sim_end_ns;
+    a.bootstrap_end = rd->bootstrap_end_ns;
+    a.status = out->status;
+    a.deliver = out->deliver_time_ns;
+    a.eid = out->event_id;
+    a.dst_host = dst_host;
+    a.dst_cnt = dst_cnt;
+    a.stats = dstats;
+    a.err = err;
+    {
+      // per packet: 20 B in, 12 B path gather, 4 B dst map, 21 B out (status, time, id), 4 B dst scratch;
+      // per host: 8 B segment, 4 B route, 32+32 B RNG, 8+8 B event counter
+      TimedLaunch tl(ctx, "walk", 61.0 * P + 92.0 * H);
+      hipLaunchKernelGGL(k_walk, dim3(grid_for(H, 256)), dim3(256), 0, st, a);
+    }
+    SG_CHECK_LAUNCH();
+  }
+  {
+    TimedLaunch tl(ctx, "scan", 8.0 * H);
+    exclusive_scan_u32(ctx, dst_cnt, out->dst_offsets, H);
+  }
+  if (P) {
+    {
+      TimedLaunch tl(ctx, "scatter", 24.0 * P);
+      hipLaunchKernelGGL(k_scatter, dim3(grid_for(P, 256, 16384)), dim3(256), 0, st, dst_host,
+                         out->deliver_time_ns, P, out->dst_offsets, cur, kt, ki);
+    }
+    {
+      TimedLaunch tl(ctx, "sort_small", 16.0 * P + 8.0 * H);
+      hipLaunchKernelGGL(k_sort_small, dim3(grid_for(H, 256)), dim3(256), 0, st, out->dst_offsets, H, kt,
+                         ki, out->dst_order, big_list, big_count);
+    }
+    uint64_t* kt2 = ctx->d_keys2.get<uint64_t>(P);
+    uint32_t* ki2 = ctx->d_vals2.get<uint32_t>(P);
+    {
+      TimedLaunch tl(ctx, "sort_big", 0.0);
+      hipLaunchKernelGGL(k_sort_big, dim3(std::min<uint32_t>(H, 2048)), dim3(SORT_BLOCK), 0, st,
+                         out->dst_offsets, big_list, big_count, kt, ki, kt2, ki2, out->dst_order);
+    }
+    SG_CHECK_LAUNCH();
+  }
+  struct {
+    unsigned long long s[3];
+    uint32_t err;
+  } h;
+  SG_HIP(hipMemcpyAsync(h.s, dstats, 24, hipMemcpyDeviceToHost, st));
+  SG_HIP(hipMemcpyAsync(&h.err, err, 4, hipMemcpyDeviceToHost, st));
+  SG_HIP(hipStreamSynchronize(st));
+  fail_flags(h.err);
+  if (stats) {
+    stats->n_delivered = h.s[0];
+    stats->min_deliver_time_ns = h.s[1];
+    stats->min_used_latency_ns = h.s[2];
+  }
+}
+
+}  // namespace sg
+
+extern "C" {
+
+int32_t sg_hosts_create(sg_ctx* ctx, uint32_t n_hosts, const uint32_t* host_ipv4,
+                        const uint32_t* host_route_idx, const uint64_t* host_seed,
+                        sg_hosts** out) {
+  if (!out) return SG_ERR_INVALID_ARG;
+  *out = nullptr;
+  sg_hosts* hs = nullptr;
+  int32_t rc = sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (n_hosts && (!host_ipv4 || !host_route_idx || !host_seed))
+      throw Error(SG_ERR_INVALID_ARG, "null host array");
+    hs = new sg_hosts();
+    hs->ctx = ctx;
+    hs->n = n_hosts;
+    hipStream_t st = ctx->stream;
+    const size_t n = n_hosts;
+    SG_HIP(hipMalloc(&hs->route, std::max<size_t>(n * 4, 16)));
+    SG_HIP(hipMalloc(&hs->rng, std::max<size_t>(n * 32, 16)));
+    SG_HIP(hipMalloc(&hs->ctr, std::max<size_t>(n * 8, 16)));
+    uint64_t* d_seed = nullptr;
+    SG_HIP(hipMalloc(&d_seed, std::max<size_t>(n * 8, 16)));
+    std::vector<std::pair<uint32_t, uint32_t>> ips(n);
+    for (uint32_t h = 0; h < n_hosts; h++) ips[h] = {host_ipv4[h], h};
+    std::sort(ips.begin(), ips.end());
+    for (size_t k = 1; k < n; k++)
+      if (ips[k].first == ips[k - 1].first) {
+        (void)hipFree(d_seed);
+        throw Error(SG_ERR_DUPLICATE_IP, "IP address has already been assigned");
+      }
+    if (n) {
+      SG_HIP(hipMemcpyAsync(hs->route, host_route_idx, n * 4, hipMemcpyHostToDevice, st));
+      SG_HIP(hipMemcpyAsync(d_seed, host_seed, n * 8, hipMemcpyHostToDevice, st));
+      SG_HIP(hipMemsetAsync(hs->ctr, 0, n * 8, st));
+      hipLaunchKernelGGL(k_seed_hosts, dim3(grid_for(n, 256)), dim3(256), 0, st, d_seed, n_hosts, hs->rng);
+      SG_CHECK_LAUNCH();
+      uint64_t span = (uint64_t)ips.back().first - ips.front().first + 1;
+      if (span <= 4 * (uint64_t)n + 4096) {
+        hs->ip_base = ips.front().first;
+        hs->dense_span = (uint32_t)span;
+        std::vector<uint32_t> dense(span, NONE);
+        for (auto& p : ips) dense[p.first - hs->ip_base] = p.second;
+        SG_HIP(hipMalloc(&hs->dense, span * 4));
+        SG_HIP(hipMemcpyAsync(hs->dense, dense.data(), span * 4, hipMemcpyHostToDevice, st));
+        SG_HIP(hipStreamSynchronize(st));
+      } else {
+        std::vector<uint32_t> a(n), b(n);
+        for (size_t k = 0; k < n; k++) {
+          a[k] = ips[k].first;
+          b[k] = ips[k].second;
+        }
+        SG_HIP(hipMalloc(&hs->sorted_ip, n * 4));
+        SG_HIP(hipMalloc(&hs->sorted_host, n * 4));
+        SG_HIP(hipMemcpyAsync(hs->sorted_ip, a.data(), n * 4, hipMemcpyHostToDevice, st));
+        SG_HIP(hipMemcpyAsync(hs->sorted_host, b.data(), n * 4, hipMemcpyHostToDevice, st));
+        SG_HIP(hipStreamSynchronize(st));
+      }
+    }
+    SG_HIP(hipStreamSynchronize(st));
+    (void)hipFree(d_seed);
+  });
+  if (rc != SG_OK) {
+    delete hs;
+    return rc;
+  }
+  *out = hs;
+  return SG_OK;
+}
+
+int32_t sg_hosts_get_state(sg_hosts* hs, uint64_t* rng_state, uint64_t* event_ctr) {
+  if (!hs) return SG_ERR_INVALID_ARG;
+  return sg::guarded(hs->ctx, [&] {
+    const size_t n = hs->n;
+    if (!n) return;
+    std::vector<uint64_t> soa(4 * n);
+    SG_HIP(hipMemcpyAsync(soa.data(), hs->rng, n * 32, hipMemcpyDeviceToHost, hs->ctx->stream));
+    if (event_ctr)
+      SG_HIP(hipMemcpyAsync(event_ctr, hs->ctr, n * 8, hipMemcpyDeviceToHost, hs->ctx->stream));
+    SG_HIP(hipStreamSynchronize(hs->ctx->stream));
+    if (rng_state)
+      for (size_t h = 0; h < n; h++)
+        for (int k = 0; k < 4; k++) rng_state[4 * h + k] = soa[k * n + h];
+  });
+}
+
+int32_t sg_hosts_set_state(sg_hosts* hs, const uint64_t* rng_state, const uint64_t* event_ctr) {
+  if (!hs) return SG_ERR_INVALID_ARG;
+  return sg::guarded(hs->ctx, [&] {
+    const size_t n = hs->n;
+    if (!n) return;
+    if (rng_state) {
+      std::vector<uint64_t> soa(4 * n);
+      for (size_t h = 0; h < n; h++)
+        for (int k = 0; k < 4; k++) soa[k * n + h] = rng_state[4 * h + k];
+      SG_HIP(hipMemcpyAsync(hs->rng, soa.data(), n * 32, hipMemcpyHostToDevice, hs->ctx->stream));
+      SG_HIP(hipStreamSynchronize(hs->ctx->stream));
+    }
+    if (event_ctr) {
+      SG_HIP(hipMemcpyAsync(hs->ctr, event_ctr, n * 8, hipMemcpyHostToDevice, hs->ctx->stream));
+      SG_HIP(hipStreamSynchronize(hs->ctx->stream));
+    }
+  });
+}
+
+void sg_hosts_destroy(sg_hosts* hs) {
+  if (!hs) return;
+  if (hs->ctx) (void)hipSetDevice(hs->ctx->device);
+  delete hs;
+}
+
+int32_t sg_deliver_round(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table, const sg_round* round,
+                         const sg_packets* packets, sg_deliveries* out, sg_round_stats* stats) {
+  return sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (!hosts || hosts->ctx != ctx || !table || !round || !packets || !out)
+      throw Error(SG_ERR_INVALID_ARG, "null argument");
+    if (!out->dst_offsets) throw Error(SG_ERR_INVALID_ARG, "null dst_offsets");
+    if (packets->n_packets &&
+        (!packets->src_host || !packets->dst_ipv4 || !packets->payload_len || !packets->send_time_ns ||
+         !out->status || !out->deliver_time_ns || !out->event_id || !out->dst_order ||
+         !table->latency_ns || !table->packet_loss))
+      throw Error(SG_ERR_INVALID_ARG, "null packet or output array");
+    deliver_round(ctx, hosts, table, round, packets, out, stats);
+  });
+}
+
+}  // extern "C"

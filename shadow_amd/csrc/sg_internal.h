@@ -1,0 +1,147 @@
+// sg_internal.h -- host-side runtime shared by the HIP translation units:
+// context, grow-only device workspace, error plumbing.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <deque>
+#include <vector>
+
+#include "../../include/shadow_gpu.h"
+
+namespace sg {
+
+// Status-carrying exception; converted to a status code at the C boundary.
+struct Error : std::runtime_error {
+  int32_t code;
+  uint32_t row, col;
+  Error(int32_t c, const std::string& m, uint32_t r = 0, uint32_t k = 0)
+      : std::runtime_error(m), code(c), row(r), col(k) {}
+};
+
+#define SG_HIP(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) {                                                                 \
+      if (e_ == hipErrorOutOfMemory) throw ::sg::Error(SG_ERR_OOM, std::string(#expr) + ": out of device memory"); \
+      throw ::sg::Error(SG_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    }                                                                                       \
+  } while (0)
+
+#define SG_CHECK_LAUNCH() SG_HIP(hipGetLastError())
+
+// Grow-only device buffer.  Growth is the only path that allocates, so a
+// steady-state round never calls hipMalloc.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* get(size_t count) {
+    size_t bytes = count * sizeof(T);
+    if (bytes == 0) bytes = 16;
+    if (bytes > cap) {
+      release();
+      SG_HIP(hipMalloc(&p, bytes));
+      cap = bytes;
+    }
+    return static_cast<T*>(p);
+  }
+};
+
+// Per-kernel timer: HIP events recorded on the context stream around each
+// launch of an instrumented kernel (bench.py reads the average launch time and
+// the algorithmic work the launch site declares).
+struct KernelTimer {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  double total_ms = 0.0;
+  double work = 0.0;  // algorithmic units (relaxations / bytes), summed over launches
+  uint64_t launches = 0;
+};
+
+}  // namespace sg
+
+struct sg_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  int n_cu = 256;
+  std::string last_error;
+  uint32_t err_row = 0, err_col = 0;
+  // routing workspace
+  sg::DevBuf r_dist, r_dist2, r_flags, r_used, r_err, r_pair_cnt, r_pair_edge, r_map, r_out_lat,
+      r_out_loss, r_misc;
+  // delivery workspace
+  sg::DevBuf d_seg, d_dst, d_cnt, d_cur, d_keys, d_vals, d_keys2, d_vals2, d_misc, d_scan, d_lists;
+  sg::DevBuf m_scratch;
+  // kernel timers (off unless sg_ctx_enable_timers)
+  bool timing = false;
+  std::deque<std::pair<std::string, sg::KernelTimer>> timers;  // deque: stable addresses
+  std::vector<hipEvent_t> event_pool;
+};
+
+namespace sg {
+
+// Run `fn` with the context's device current; map exceptions to status codes.
+template <class F>
+int32_t guarded(sg_ctx* ctx, F&& fn) {
+  if (!ctx) return SG_ERR_INVALID_ARG;
+  try {
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != ctx->device) SG_HIP(hipSetDevice(ctx->device));
+    fn();
+    ctx->last_error.clear();
+    ctx->err_row = ctx->err_col = 0;
+    return SG_OK;
+  } catch (const Error& e) {
+    ctx->last_error = e.what();
+    ctx->err_row = e.row;
+    ctx->err_col = e.col;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    ctx->last_error = "host out of memory";
+    return SG_ERR_OOM;
+  } catch (const std::exception& e) {
+    ctx->last_error = e.what();
+    return SG_ERR_DEVICE;
+  }
+}
+
+inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 1u << 20) {
+  size_t g = (n + block - 1) / block;
+  if (g == 0) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+// Exclusive scan of n u32 values (device, in -> out, out has n+1 entries, out[n] = total).
+void exclusive_scan_u32(sg_ctx* ctx, const uint32_t* d_in, uint32_t* d_out, uint32_t n);
+
+// Read a few scalars back (blocking on the context stream).
+void copy_to_host(sg_ctx* ctx, void* dst, const void* src, size_t bytes);
+
+// RAII bracket for one instrumented launch: `TimedLaunch t(ctx, "k_walk", work);`
+// before the launch; the end event is recorded when `t` goes out of scope.
+struct TimedLaunch {
+  sg_ctx* ctx;
+  KernelTimer* timer = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  TimedLaunch(sg_ctx* c, const char* name, double work);
+  ~TimedLaunch();
+};
+
+}  // namespace sg

@@ -1,0 +1,682 @@
+// sg_routing.hip -- routing-table build on MI355X.
+//
+// Replaces NetworkGraph::compute_shortest_paths (graph/mod.rs:183-228) and
+// NetworkGraph::get_direct_paths (graph/mod.rs:230-252).
+//
+// Shortest paths.  The reference runs petgraph's Dijkstra per used source
+// over (latency u64, loss f32) with the LEFT fold default() + e1 + e2 + ...
+// (graph/mod.rs:195-200, 322-331).  Because edge latency >= 1 ns
+// (graph/mod.rs:105-107) and the f32 fold is monotone, that result equals the
+// fixed point of the source-rooted relaxation
+//     D[s][v] = min(D[s][v], D[s][u] (+) w(u,v))
+// under ANY relaxation order, as long as every update keeps the edge on the
+// right (source-rooted) and the (latency, loss) pair is updated atomically.
+// Floyd-Warshall would re-associate the f32 fold and is not bit-exact for loss.
+//
+// Kernel: batched-source pull relaxation.  A wave owns one destination node v
+// of one 64-source batch; lane = source.  The batch's distance slab is laid out
+// [node][64 sources], so each in-arc (u -> v) costs one coalesced 512-B read of
+// D[u][0..63] and 64 independent relaxations.  In-arcs are read through the
+// scalar path (wave-uniform).  The key is packed: (lat << 30) | f32 bits(loss),
+// so one u64 min is the lexicographic PathProperties comparison and one 64-bit
+// store is an untorn (lat, loss) update -> in-place (Gauss-Seidel) passes.
+// Rows whose keys saturate (latency >= 2^34-1 ns, or unreachable) are redone
+// with a wide (u64 latency, f32 loss) Jacobi kernel.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "sg_device.h"
+#include "sg_internal.h"
+
+struct sg_net {
+  sg_ctx* ctx = nullptr;
+  uint32_t n_nodes = 0, n_edges = 0, n_arcs = 0;
+  bool directed = false;
+  std::vector<uint32_t> gml_id;
+  // GML edge list (device)
+  uint32_t* e_src = nullptr;
+  uint32_t* e_dst = nullptr;
+  uint64_t* e_lat = nullptr;
+  float* e_loss = nullptr;
+  // in-arc CSC without self-loops (device)
+  uint32_t* in_off = nullptr;  // n_nodes + 1
+  uint32_t* in_src = nullptr;
+  uint64_t* in_lat = nullptr;
+  float* in_om = nullptr;  // 1f32 - loss
+  // self-loops
+  uint32_t* self_cnt = nullptr;
+  uint32_t* self_edge = nullptr;
+  ~sg_net() {
+    void* ps[] = {e_src, e_dst, e_lat, e_loss, in_off, in_src, in_lat, in_om, self_cnt, self_edge};
+    for (void* p : ps)
+      if (p) (void)hipFree(p);
+  }
+};
+
+namespace sg {
+
+constexpr int BATCH = 64;         // sources per batch = wave width
+constexpr int RELAX_WAVES = 4;    // waves per block
+constexpr int RELAX_BLOCK = RELAX_WAVES * 64;
+
+// ---------------------------------------------------------------------------
+// Graph upload: CSC of in-arcs (both directions when undirected, petgraph
+// semantics graph/mod.rs:137-152), self-loop census for get_edge_weight(n, n).
+// ---------------------------------------------------------------------------
+__global__ void k_count_arcs(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                             uint32_t m, int directed, uint32_t* __restrict__ indeg,
+                             uint32_t* __restrict__ self_cnt, uint32_t* __restrict__ self_edge) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < m; e += gridDim.x * blockDim.x) {
+    uint32_t s = src[e], d = dst[e];
+    if (s == d) {
+      atomicAdd(&self_cnt[s], 1u);
+      self_edge[s] = e;  // meaningful only when the count ends at 1
+    } else {
+      atomicAdd(&indeg[d], 1u);
+      if (!directed) atomicAdd(&indeg[s], 1u);
+    }
+  }
+}
+
+__global__ void k_scatter_arcs(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                               const uint64_t* __restrict__ lat, const float* __restrict__ loss,
+                               uint32_t m, int directed, uint32_t* __restrict__ cursor,
+                               uint32_t* __restrict__ in_src, uint64_t* __restrict__ in_lat,
+                               float* __restrict__ in_om) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < m; e += gridDim.x * blockDim.x) {
+    uint32_t s = src[e], d = dst[e];
+    if (s == d) continue;  // a self-loop never improves D[s][v] (latency >= 1)
+    float om = __fsub_rn(1.0f, loss[e]);
+    uint32_t p = atomicAdd(&cursor[d], 1u);
+    in_src[p] = s;
+    in_lat[p] = lat[e];
+    in_om[p] = om;
+    if (!directed) {
+      uint32_t q = atomicAdd(&cursor[s], 1u);
+      in_src[q] = d;
+      in_lat[q] = lat[e];
+      in_om[q] = om;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Packed-key batched relaxation.
+// ---------------------------------------------------------------------------
+__global__ void k_init_packed(uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ used,
+                              uint32_t first_row, uint32_t row_end, uint32_t n_batches) {
+  size_t total = (size_t)n_batches * n * BATCH;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t lane = (uint32_t)(i & (BATCH - 1));
+    size_t bv = i / BATCH;
+    uint32_t v = (uint32_t)(bv % n);
+    uint32_t b = (uint32_t)(bv / n);
+    uint32_t row = first_row + b * BATCH + lane;
+    D[i] = (row < row_end && used[row] == v) ? 0ull : KEY_INF;  // PathProperties::default()
+  }
+}
+
+template <int VPW>
+__global__ void __launch_bounds__(RELAX_BLOCK)
+    k_relax_packed(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
+                   const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om,
+                   uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ active,
+                   uint32_t* __restrict__ changed) {
+  const uint32_t b = blockIdx.y;
+  if (!active[b]) return;
+  uint64_t* __restrict__ Db = D + (size_t)b * n * BATCH;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  bool any = false;
+  const uint32_t v0 = (blockIdx.x * RELAX_WAVES + wave) * VPW;
+#pragma unroll 1
+  for (int k = 0; k < VPW; k++) {
+    const uint32_t v = v0 + k;
+    if (v >= n) break;
+    const uint32_t a0 = in_off[v], a1 = in_off[v + 1];
+    const uint64_t cur = Db[(size_t)v * BATCH + lane];
+    uint64_t best = cur;
+    uint32_t a = a0;
+    // 4 independent 512-B row reads in flight per wave
+    for (; a + 4 <= a1; a += 4) {
+      uint32_t u0 = in_src[a], u1 = in_src[a + 1], u2 = in_src[a + 2], u3 = in_src[a + 3];
+      uint64_t k0 = Db[(size_t)u0 * BATCH + lane];
+      uint64_t k1 = Db[(size_t)u1 * BATCH + lane];
+      uint64_t k2 = Db[(size_t)u2 * BATCH + lane];
+      uint64_t k3 = Db[(size_t)u3 * BATCH + lane];
+      uint64_t l0 = min(in_lat[a], LAT_SAT), l1 = min(in_lat[a + 1], LAT_SAT);
+      uint64_t l2 = min(in_lat[a + 2], LAT_SAT), l3 = min(in_lat[a + 3], LAT_SAT);
+      float o0 = in_om[a], o1 = in_om[a + 1], o2 = in_om[a + 2], o3 = in_om[a + 3];
+      uint64_t c0 = k0 == KEY_INF ? KEY_INF : relax_key(k0, l0, o0);
+      uint64_t c1 = k1 == KEY_INF ? KEY_INF : relax_key(k1, l1, o1);
+      uint64_t c2 = k2 == KEY_INF ? KEY_INF : relax_key(k2, l2, o2);
+      uint64_t c3 = k3 == KEY_INF ? KEY_INF : relax_key(k3, l3, o3);
+      best = min(best, min(min(c0, c1), min(c2, c3)));
+    }
+    for (; a < a1; a++) {
+      uint32_t u = in_src[a];
+      uint64_t ku = Db[(size_t)u * BATCH + lane];
+      uint64_t c = ku == KEY_INF ? KEY_INF : relax_key(ku, min(in_lat[a], LAT_SAT), in_om[a]);
+      best = min(best, c);
+    }
+    if (best < cur) {
+      Db[(size_t)v * BATCH + lane] = best;  // one untorn 64-bit (lat, loss) update
+      any = true;
+    }
+  }
+  if (__any(any) && lane == 0) atomicOr(&changed[b], 1u);
+}
+
+// Transposed write-out of a [64 rows x 64 cols] tile.  Diagonal = raw
+// self-loop (graph/mod.rs:210-217).  Saturated keys flag their batch.
+__global__ void __launch_bounds__(256)
+    k_out_packed(const uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ used,
+                 uint32_t n_used, uint32_t first_row, uint32_t row_end, uint32_t out_row0,
+                 const uint32_t* __restrict__ self_edge, const uint64_t* __restrict__ e_lat,
+                 const float* __restrict__ e_loss, uint64_t* __restrict__ out_lat,
+                 float* __restrict__ out_loss, uint32_t* __restrict__ sat) {
+  __shared__ uint64_t tile[64][65];
+  const uint32_t b = blockIdx.y;
+  const uint32_t j0 = blockIdx.x * 64;
+  const uint64_t* __restrict__ Db = D + (size_t)b * n * BATCH;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int c = wave; c < 64; c += 4) {
+    uint32_t j = j0 + c;
+    tile[c][lane] = j < n_used ? Db[(size_t)used[j] * BATCH + lane] : 0ull;
+  }
+  __syncthreads();
+  bool s = false;
+  const uint32_t j = j0 + lane;
+  for (int r = wave; r < 64; r += 4) {
+    uint32_t row = first_row + b * BATCH + r;
+    if (row >= row_end || j >= n_used) continue;
+    size_t o = (size_t)(row - out_row0) * n_used + j;
+    if (row == j) {
+      uint32_t e = self_edge[used[j]];
+      out_lat[o] = e_lat[e];
+      out_loss[o] = e_loss[e];
+    } else {
+      uint64_t k = tile[lane][r];
+      uint64_t lat = key_lat(k);
+      s |= lat >= LAT_SAT;
+      out_lat[o] = lat;
+      out_loss[o] = __uint_as_float(key_loss_bits(k));
+    }
+  }
+  if (__any(s) && lane == 0) atomicOr(&sat[b], 1u);
+}
+
+// ---------------------------------------------------------------------------
+// Wide fallback: u64 latency + f32 loss, Jacobi (double-buffered) so a reader
+// never sees a torn pair.  UINT64_MAX latency = no path yet.
+// ---------------------------------------------------------------------------
+__global__ void k_init_wide(uint64_t* __restrict__ L, float* __restrict__ F, uint32_t n,
+                            const uint32_t* __restrict__ used, const uint32_t* __restrict__ rows,
+                            uint32_t n_rows_total, uint32_t n_batches) {
+  size_t total = (size_t)n_batches * n * BATCH;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t lane = (uint32_t)(i & (BATCH - 1));
+    size_t bv = i / BATCH;
+    uint32_t v = (uint32_t)(bv % n);
+    uint32_t b = (uint32_t)(bv / n);
+    uint32_t slot = b * BATCH + lane;
+    bool src = slot < n_rows_total && used[rows[slot]] == v;
+    L[i] = src ? 0ull : ~0ull;
+    F[i] = 0.0f;
+  }
+}
+
+__global__ void __launch_bounds__(RELAX_BLOCK)
+    k_relax_wide(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
+                 const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om,
+                 const uint64_t* __restrict__ Lc, const float* __restrict__ Fc,
+                 uint64_t* __restrict__ Ln, float* __restrict__ Fn, uint32_t n,
+                 uint32_t* __restrict__ changed) {
+  const uint32_t b = blockIdx.y;
+  const size_t base = (size_t)b * n * BATCH;
+  const int lane = threadIdx.x & 63;
+  const uint32_t v = __builtin_amdgcn_readfirstlane(blockIdx.x * RELAX_WAVES + (threadIdx.x >> 6));
+  if (v >= n) return;
+  uint64_t bl = Lc[base + (size_t)v * BATCH + lane];
+  float bf = Fc[base + (size_t)v * BATCH + lane];
+  const uint64_t l_in = bl;
+  const float f_in = bf;
+  for (uint32_t a = in_off[v]; a < in_off[v + 1]; a++) {
+    uint32_t u = in_src[a];
+    uint64_t lu = Lc[base + (size_t)u * BATCH + lane];
+    if (lu == ~0ull) continue;
+    float fu = Fc[base + (size_t)u * BATCH + lane];
+    uint64_t cl = lu + in_lat[a];
+    float cf = fold_loss(fu, in_om[a]);
+    if (cl < bl || (cl == bl && cf < bf)) {
+      bl = cl;
+      bf = cf;
+    }
+  }
+  Ln[base + (size_t)v * BATCH + lane] = bl;
+  Fn[base + (size_t)v * BATCH + lane] = bf;
+  bool ch = bl != l_in || __float_as_uint(bf) != __float_as_uint(f_in);
+  if (__any(ch) && lane == 0) atomicOr(changed, 1u);
+}
+
+__global__ void k_out_wide(const uint64_t* __restrict__ L, const float* __restrict__ F, uint32_t n,
+                           const uint32_t* __restrict__ used, uint32_t n_used,
+                           const uint32_t* __restrict__ rows, uint32_t n_rows_total, uint32_t out_row0,
+                           const uint32_t* __restrict__ self_edge, const uint64_t* __restrict__ e_lat,
+                           const float* __restrict__ e_loss, uint64_t* __restrict__ out_lat,
+                           float* __restrict__ out_loss, unsigned long long* __restrict__ first_unreach) {
+  const uint32_t slot = blockIdx.y * BATCH + (threadIdx.x & 63);
+  if (slot >= n_rows_total) return;
+  const uint32_t row = rows[slot];
+  const size_t base = (size_t)blockIdx.y * n * BATCH + (threadIdx.x & 63);
+  for (uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6); j < n_used; j += gridDim.x * 4) {
+    size_t o = (size_t)(row - out_row0) * n_used + j;
+    if (row == j) {
+      uint32_t e = self_edge[used[j]];
+      out_lat[o] = e_lat[e];
+      out_loss[o] = e_loss[e];
+      continue;
+    }
+    uint64_t l = L[base + (size_t)used[j] * BATCH];
+    out_lat[o] = l;
+    out_loss[o] = F[base + (size_t)used[j] * BATCH];
+    if (l == ~0ull) atomicMin(first_unreach, (unsigned long long)row * n_used + j);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Self-loop census over the used nodes (graph/mod.rs:210-217): first failing
+// node in order, low bit = "more than one".
+// ---------------------------------------------------------------------------
+__global__ void k_self_check(const uint32_t* __restrict__ used, uint32_t n_used,
+                             const uint32_t* __restrict__ self_cnt,
+                             unsigned long long* __restrict__ first) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n_used; j += gridDim.x * blockDim.x) {
+    uint32_t c = self_cnt[used[j]];
+    if (c != 1) atomicMin(first, ((unsigned long long)j << 1) | (c > 1 ? 1ull : 0ull));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Direct paths (graph/mod.rs:230-252): per used pair, count the edges that
+// petgraph's edges_connecting would yield.
+// ---------------------------------------------------------------------------
+__global__ void k_pair_count(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                             uint32_t m, int directed, const uint32_t* __restrict__ map,
+                             uint32_t n_used, uint32_t row_begin, uint32_t row_end,
+                             uint32_t* __restrict__ cnt, uint32_t* __restrict__ edge) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < m; e += gridDim.x * blockDim.x) {
+    uint32_t iu = map[src[e]], iv = map[dst[e]];
+    if (iu == ~0u || iv == ~0u) continue;
+    if (iu >= row_begin && iu < row_end) {
+      size_t o = (size_t)(iu - row_begin) * n_used + iv;
+      atomicAdd(&cnt[o], 1u);
+      edge[o] = e;
+    }
+    if (!directed && iu != iv && iv >= row_begin && iv < row_end) {
+      size_t o = (size_t)(iv - row_begin) * n_used + iu;
+      atomicAdd(&cnt[o], 1u);
+      edge[o] = e;
+    }
+  }
+}
+
+__global__ void k_pair_out(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ edge,
+                           size_t count, uint32_t n_used, uint32_t row_begin,
+                           const uint64_t* __restrict__ e_lat, const float* __restrict__ e_loss,
+                           uint64_t* __restrict__ out_lat, float* __restrict__ out_loss,
+                           unsigned long long* __restrict__ first) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+       i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t c = cnt[i];
+    if (c != 1) {
+      unsigned long long lin = (unsigned long long)row_begin * n_used + i;
+      atomicMin(first, (lin << 1) | (c > 1 ? 1ull : 0ull));
+      out_lat[i] = 0;
+      out_loss[i] = 0.0f;
+    } else {
+      out_lat[i] = e_lat[edge[i]];
+      out_loss[i] = e_loss[edge[i]];
+    }
+  }
+}
+
+__global__ void k_min_u64(const uint64_t* __restrict__ x, size_t count,
+                          unsigned long long* __restrict__ out) {
+  unsigned long long m = ~0ull;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+       i += (size_t)gridDim.x * blockDim.x)
+    m = min(m, (unsigned long long)x[i]);
+  for (int d = 32; d > 0; d >>= 1) m = min(m, (unsigned long long)__shfl_xor(m, d, 64));
+  if ((threadIdx.x & 63) == 0) atomicMin(out, m);
+}
+
+// ---------------------------------------------------------------------------
+// Host orchestration
+// ---------------------------------------------------------------------------
+static std::string node_name(const sg_net* net, uint32_t idx) {
+  uint32_t id = net->gml_id.empty() ? idx : net->gml_id[idx];
+  return std::to_string(id);
+}
+
+static int env_int(const char* name, int dflt) {
+  const char* s = getenv(name);
+  return s && *s ? atoi(s) : dflt;
+}
+
+template <class T>
+static T* dmalloc(size_t count) {
+  void* p = nullptr;
+  SG_HIP(hipMalloc(&p, std::max<size_t>(count * sizeof(T), 16)));
+  return static_cast<T*>(p);
+}
+
+static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
+  const uint32_t n = g->n_nodes, m = g->n_edges;
+  if (m && (!g->edge_src || !g->edge_dst || !g->edge_latency_ns || !g->edge_packet_loss))
+    throw Error(SG_ERR_INVALID_ARG, "null edge array");
+  for (uint32_t e = 0; e < m; e++) {
+    if (g->edge_src[e] >= n || g->edge_dst[e] >= n)
+      throw Error(SG_ERR_INVALID_ARG, "edge " + std::to_string(e) + " endpoint out of range");
+    float l = g->edge_packet_loss[e];
+    if (!(l >= 0.0f && l <= 1.0f))  // graph/mod.rs:101-103 (NaN rejected too)
+      throw Error(SG_ERR_INVALID_ARG, "Edge 'packet_loss' is not in the range [0,1]");
+    if (g->edge_latency_ns[e] == 0)  // graph/mod.rs:105-107
+      throw Error(SG_ERR_INVALID_ARG, "Edge 'latency' must not be 0");
+  }
+  net->ctx = ctx;
+  net->n_nodes = n;
+  net->n_edges = m;
+  net->directed = g->directed != 0;
+  if (g->node_gml_id) net->gml_id.assign(g->node_gml_id, g->node_gml_id + n);
+  hipStream_t st = ctx->stream;
+  net->e_src = dmalloc<uint32_t>(m);
+  net->e_dst = dmalloc<uint32_t>(m);
+  net->e_lat = dmalloc<uint64_t>(m);
+  net->e_loss = dmalloc<float>(m);
+  net->in_off = dmalloc<uint32_t>((size_t)n + 1);
+  net->self_cnt = dmalloc<uint32_t>(n);
+  net->self_edge = dmalloc<uint32_t>(n);
+  if (m) {
+    SG_HIP(hipMemcpyAsync(net->e_src, g->edge_src, m * 4ull, hipMemcpyHostToDevice, st));
+    SG_HIP(hipMemcpyAsync(net->e_dst, g->edge_dst, m * 4ull, hipMemcpyHostToDevice, st));
+    SG_HIP(hipMemcpyAsync(net->e_lat, g->edge_latency_ns, m * 8ull, hipMemcpyHostToDevice, st));
+    SG_HIP(hipMemcpyAsync(net->e_loss, g->edge_packet_loss, m * 4ull, hipMemcpyHostToDevice, st));
+  }
+  uint32_t* indeg = ctx->r_misc.get<uint32_t>((size_t)n + 1);
+  SG_HIP(hipMemsetAsync(indeg, 0, ((size_t)n + 1) * 4, st));
+  SG_HIP(hipMemsetAsync(net->self_cnt, 0, (size_t)n * 4, st));
+  SG_HIP(hipMemsetAsync(net->self_edge, 0, (size_t)n * 4, st));
+  if (m) {
+    hipLaunchKernelGGL(k_count_arcs, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src,
+                       net->e_dst, m, (int)net->directed, indeg, net->self_cnt, net->self_edge);
+    SG_CHECK_LAUNCH();
+  }
+  exclusive_scan_u32(ctx, indeg, net->in_off, n);
+  uint32_t n_arcs = 0;
+  copy_to_host(ctx, &n_arcs, net->in_off + n, 4);
+  net->n_arcs = n_arcs;
+  net->in_src = dmalloc<uint32_t>(n_arcs);
+  net->in_lat = dmalloc<uint64_t>(n_arcs);
+  net->in_om = dmalloc<float>(n_arcs);
+  if (n_arcs) {
+    uint32_t* cursor = ctx->r_map.get<uint32_t>((size_t)n + 1);
+    SG_HIP(hipMemcpyAsync(cursor, net->in_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_scatter_arcs, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src,
+                       net->e_dst, net->e_lat, net->e_loss, m, (int)net->directed, cursor,
+                       net->in_src, net->in_lat, net->in_om);
+    SG_CHECK_LAUNCH();
+  }
+  SG_HIP(hipStreamSynchronize(st));
+}
+
+static void check_self_loops(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
+                             const uint32_t* h_used) {
+  unsigned long long* first = ctx->r_err.get<unsigned long long>(4);
+  SG_HIP(hipMemsetAsync(first, 0xff, 8, ctx->stream));
+  hipLaunchKernelGGL(k_self_check, dim3(grid_for(n_used, 256, 4096)), dim3(256), 0, ctx->stream,
+                     d_used, n_used, net->self_cnt, first);
+  SG_CHECK_LAUNCH();
+  unsigned long long h = 0;
+  copy_to_host(ctx, &h, first, 8);
+  if (h != ~0ull) {
+    uint32_t j = (uint32_t)(h >> 1);
+    std::string id = node_name(net, h_used[j]);
+    if (h & 1)
+      throw Error(SG_ERR_MULTI_EDGE, "More than one edge connecting node " + id + " to " + id, j, j);
+    throw Error(SG_ERR_NO_EDGE, "No edge connecting node " + id + " to " + id, j, j);
+  }
+}
+
+// Wide recomputation of the listed rows (absolute row indices).
+static void run_wide(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
+                     const std::vector<uint32_t>& rows, uint32_t out_row0, uint64_t* out_lat,
+                     float* out_loss) {
+  hipStream_t st = ctx->stream;
+  const uint32_t n = net->n_nodes;
+  const uint32_t nr = (uint32_t)rows.size();
+  const uint32_t nb = (nr + BATCH - 1) / BATCH;
+  uint32_t* d_rows = ctx->r_misc.get<uint32_t>(nr);
+  SG_HIP(hipMemcpyAsync(d_rows, rows.data(), nr * 4ull, hipMemcpyHostToDevice, st));
+  size_t slab = (size_t)nb * n * BATCH;
+  char* buf = ctx->r_dist2.get<char>(slab * 24);
+  uint64_t* L0 = (uint64_t*)buf;
+  uint64_t* L1 = L0 + slab;
+  float* F0 = (float*)(L1 + slab);
+  float* F1 = F0 + slab;
+  hipLaunchKernelGGL(k_init_wide, dim3(grid_for(slab, 256, 65536)), dim3(256), 0, st, L0, F0, n,
+                     d_used, d_rows, nr, nb);
+  uint32_t* changed = ctx->r_flags.get<uint32_t>(4);
+  for (uint32_t pass = 0;; pass++) {
+    if (pass > n + 2) throw Error(SG_ERR_DEVICE, "wide relaxation did not converge");
+    SG_HIP(hipMemsetAsync(changed, 0, 4, st));
+    TimedLaunch tl(ctx, "relax_wide", (double)nb * BATCH * net->n_arcs);
+    hipLaunchKernelGGL(k_relax_wide, dim3((n + RELAX_WAVES - 1) / RELAX_WAVES, nb), dim3(RELAX_BLOCK),
+                       0, st, net->in_off, net->in_src, net->in_lat, net->in_om, L0, F0, L1, F1, n,
+                       changed);
+    SG_CHECK_LAUNCH();
+    std::swap(L0, L1);
+    std::swap(F0, F1);
+    uint32_t h = 0;
+    copy_to_host(ctx, &h, changed, 4);
+    if (!h) break;
+  }
+  unsigned long long* first = ctx->r_err.get<unsigned long long>(4);
+  SG_HIP(hipMemsetAsync(first, 0xff, 8, st));
+  hipLaunchKernelGGL(k_out_wide, dim3(grid_for(n_used, 4, 1024), nb), dim3(256), 0, st, L0, F0, n,
+                     d_used, n_used, d_rows, nr, out_row0, net->self_edge, net->e_lat, net->e_loss,
+                     out_lat, out_loss, first);
+  SG_CHECK_LAUNCH();
+  unsigned long long h = 0;
+  copy_to_host(ctx, &h, first, 8);
+  if (h != ~0ull) {
+    uint32_t i = (uint32_t)(h / n_used), j = (uint32_t)(h % n_used);
+    throw Error(SG_ERR_UNREACHABLE, "no path from node index " + std::to_string(i) + " to " +
+                                        std::to_string(j) + " (graph must be connected)",
+                i, j);
+  }
+}
+
+static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
+                           uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
+                           float* out_loss) {
+  hipStream_t st = ctx->stream;
+  const uint32_t n = net->n_nodes;
+  const uint32_t n_rows = row_end - row_begin;
+  const uint32_t n_batches = (n_rows + BATCH - 1) / BATCH;
+  // Group size: batches whose slabs (n x 512 B each) are live together.
+  size_t slab_bytes = (size_t)n * BATCH * 8;
+  size_t budget = (size_t)env_int("SG_APSP_GROUP_MB", 2048) << 20;
+  uint32_t group = (uint32_t)std::max<size_t>(1, std::min<size_t>(n_batches, budget / slab_bytes));
+  constexpr int VPW = 4;
+  const uint32_t nvb = (n + RELAX_WAVES * VPW - 1) / (RELAX_WAVES * VPW);
+  uint64_t* D = ctx->r_dist.get<uint64_t>((size_t)group * n * BATCH);
+  uint32_t* flags = ctx->r_flags.get<uint32_t>((size_t)group * 2 + 8);
+  uint32_t* sat = flags + 2 * (size_t)group;
+  std::vector<uint32_t> h_changed(group), h_sat(group);
+  std::vector<uint32_t> wide_rows;
+  for (uint32_t g0 = 0; g0 < n_batches; g0 += group) {
+    const uint32_t gb = std::min(group, n_batches - g0);
+    const uint32_t first_row = row_begin + g0 * BATCH;
+    hipLaunchKernelGGL(k_init_packed, dim3(grid_for((size_t)gb * n * BATCH, 256, 65536)), dim3(256),
+                       0, st, D, n, d_used, first_row, row_end, gb);
+    SG_CHECK_LAUNCH();
+    uint32_t* active = flags;
+    uint32_t* changed = flags + group;
+    SG_HIP(hipMemsetAsync(active, 1, gb * 4ull, st));  // nonzero = active
+    uint32_t n_active = gb;
+    for (uint32_t pass = 0;; pass++) {
+      if (pass > n + 2) throw Error(SG_ERR_DEVICE, "relaxation did not converge");
+      SG_HIP(hipMemsetAsync(changed, 0, gb * 4ull, st));
+      {
+        TimedLaunch tl(ctx, "relax_packed", (double)n_active * BATCH * net->n_arcs);
+        hipLaunchKernelGGL(k_relax_packed<VPW>, dim3(nvb, gb), dim3(RELAX_BLOCK), 0, st, net->in_off,
+                           net->in_src, net->in_lat, net->in_om, D, n, active, changed);
+      }
+      SG_CHECK_LAUNCH();
+      copy_to_host(ctx, h_changed.data(), changed, gb * 4ull);
+      n_active = 0;
+      for (uint32_t b = 0; b < gb; b++) n_active += h_changed[b] != 0;
+      if (!n_active) break;
+      std::swap(active, changed);
+    }
+    SG_HIP(hipMemsetAsync(sat, 0, gb * 4ull, st));
+    TimedLaunch tl(ctx, "out_packed", 12.0 * std::min<uint32_t>(gb * BATCH, row_end - first_row) * n_used);
+    hipLaunchKernelGGL(k_out_packed, dim3((n_used + 63) / 64, gb), dim3(256), 0, st, D, n, d_used,
+                       n_used, first_row, row_end, row_begin, net->self_edge, net->e_lat,
+                       net->e_loss, out_lat, out_loss, sat);
+    SG_CHECK_LAUNCH();
+    copy_to_host(ctx, h_sat.data(), sat, gb * 4ull);
+    for (uint32_t b = 0; b < gb; b++)
+      if (h_sat[b])
+        for (uint32_t r = 0; r < BATCH; r++) {
+          uint32_t row = first_row + b * BATCH + r;
+          if (row < row_end) wide_rows.push_back(row);
+        }
+  }
+  if (!wide_rows.empty()) run_wide(ctx, net, d_used, n_used, wide_rows, row_begin, out_lat, out_loss);
+}
+
+static void direct_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, const uint32_t* h_used,
+                         uint32_t n_used, uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
+                         float* out_loss) {
+  hipStream_t st = ctx->stream;
+  const uint32_t n = net->n_nodes;
+  std::vector<uint32_t> map(n, ~0u);
+  for (uint32_t j = 0; j < n_used; j++) map[h_used[j]] = j;
+  uint32_t* d_map = ctx->r_map.get<uint32_t>(n);
+  SG_HIP(hipMemcpyAsync(d_map, map.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+  size_t count = (size_t)(row_end - row_begin) * n_used;
+  uint32_t* cnt = ctx->r_pair_cnt.get<uint32_t>(count);
+  uint32_t* edge = ctx->r_pair_edge.get<uint32_t>(count);
+  SG_HIP(hipMemsetAsync(cnt, 0, count * 4, st));
+  if (net->n_edges)
+    hipLaunchKernelGGL(k_pair_count, dim3(grid_for(net->n_edges, 256, 8192)), dim3(256), 0, st,
+                       net->e_src, net->e_dst, net->n_edges, (int)net->directed, d_map, n_used,
+                       row_begin, row_end, cnt, edge);
+  unsigned long long* first = ctx->r_err.get<unsigned long long>(4);
+  SG_HIP(hipMemsetAsync(first, 0xff, 8, st));
+  hipLaunchKernelGGL(k_pair_out, dim3(grid_for(count, 256, 65536)), dim3(256), 0, st, cnt, edge,
+                     count, n_used, row_begin, net->e_lat, net->e_loss, out_lat, out_loss, first);
+  SG_CHECK_LAUNCH();
+  unsigned long long h = 0;
+  copy_to_host(ctx, &h, first, 8);
+  if (h != ~0ull) {
+    unsigned long long lin = h >> 1;
+    uint32_t i = (uint32_t)(lin / n_used), j = (uint32_t)(lin % n_used);
+    std::string a = node_name(net, h_used[i]), b = node_name(net, h_used[j]);
+    if (h & 1) throw Error(SG_ERR_MULTI_EDGE, "More than one edge connecting node " + a + " to " + b, i, j);
+    throw Error(SG_ERR_NO_EDGE, "No edge connecting node " + a + " to " + b, i, j);
+  }
+}
+
+}  // namespace sg
+
+extern "C" {
+
+int32_t sg_net_create(sg_ctx* ctx, const sg_graph* g, sg_net** out) {
+  if (!g || !out) return SG_ERR_INVALID_ARG;
+  *out = nullptr;
+  sg_net* net = nullptr;
+  int32_t rc = sg::guarded(ctx, [&] {
+    net = new sg_net();
+    sg::build_net(ctx, g, net);
+  });
+  if (rc != SG_OK) {
+    delete net;
+    return rc;
+  }
+  *out = net;
+  return SG_OK;
+}
+
+void sg_net_destroy(sg_net* net) {
+  if (!net) return;
+  if (net->ctx) (void)hipSetDevice(net->ctx->device);
+  delete net;
+}
+
+int32_t sg_routing_build(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32_t n_used,
+                         uint32_t row_begin, uint32_t row_end, uint32_t flags,
+                         uint64_t* out_latency_ns, float* out_packet_loss) {
+  return sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (!net || net->ctx != ctx) throw Error(SG_ERR_INVALID_ARG, "network belongs to another context");
+    if (row_begin > row_end || row_end > n_used) throw Error(SG_ERR_INVALID_ARG, "bad row range");
+    if (n_used && !nodes) throw Error(SG_ERR_INVALID_ARG, "null node list");
+    if (row_end > row_begin && (!out_latency_ns || !out_packet_loss))
+      throw Error(SG_ERR_INVALID_ARG, "null output");
+    {
+      std::vector<uint8_t> seen(net->n_nodes, 0);
+      for (uint32_t j = 0; j < n_used; j++) {
+        if (nodes[j] >= net->n_nodes) throw Error(SG_ERR_INVALID_ARG, "node index out of range");
+        if (seen[nodes[j]]++) throw Error(SG_ERR_INVALID_ARG, "duplicate node in node list");
+      }
+    }
+    if (n_used == 0) return;
+    hipStream_t st = ctx->stream;
+    uint32_t* d_used = ctx->r_used.get<uint32_t>(n_used);
+    SG_HIP(hipMemcpyAsync(d_used, nodes, (size_t)n_used * 4, hipMemcpyHostToDevice, st));
+    const bool shortest = flags & SG_ROUTE_SHORTEST_PATH;
+    // The reference checks every used node's self-loop (graph/mod.rs:211-217),
+    // whichever rows this call computes.
+    if (shortest) check_self_loops(ctx, net, d_used, n_used, nodes);
+    if (row_end == row_begin) return;
+    const size_t count = (size_t)(row_end - row_begin) * n_used;
+    const bool dev_out = flags & SG_ROUTE_OUT_DEVICE;
+    uint64_t* o_lat = dev_out ? out_latency_ns : ctx->r_out_lat.get<uint64_t>(count);
+    float* o_loss = dev_out ? out_packet_loss : ctx->r_out_loss.get<float>(count);
+    if (shortest)
+      shortest_paths(ctx, net, d_used, n_used, row_begin, row_end, o_lat, o_loss);
+    else
+      direct_paths(ctx, net, d_used, nodes, n_used, row_begin, row_end, o_lat, o_loss);
+    if (!dev_out) {
+      SG_HIP(hipMemcpyAsync(out_latency_ns, o_lat, count * 8, hipMemcpyDeviceToHost, st));
+      SG_HIP(hipMemcpyAsync(out_packet_loss, o_loss, count * 4, hipMemcpyDeviceToHost, st));
+    }
+    SG_HIP(hipStreamSynchronize(st));
+  });
+}
+
+int32_t sg_routing_min_latency(sg_ctx* ctx, const uint64_t* d_latency_ns, size_t count,
+                               uint64_t* out_min) {
+  return sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (!out_min || (count && !d_latency_ns)) throw Error(SG_ERR_INVALID_ARG, "null argument");
+    unsigned long long* m = ctx->r_err.get<unsigned long long>(4);
+    SG_HIP(hipMemsetAsync(m, 0xff, 8, ctx->stream));
+    if (count)
+      hipLaunchKernelGGL(k_min_u64, dim3(grid_for(count, 256, 4096)), dim3(256), 0, ctx->stream,
+                         d_latency_ns, count, m);
+    SG_CHECK_LAUNCH();
+    unsigned long long h = 0;
+    copy_to_host(ctx, &h, m, 8);
+    *out_min = h;
+  });
+}
+
+}  // extern "C"

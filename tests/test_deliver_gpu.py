@@ -1,0 +1,196 @@
+"""GPU parity: one delivery round (HIP) vs the CPU oracle, bit-exact.
+
+Compares per-packet status (delivered / dropped by loss / unknown destination /
+after sim end), deliver time, event id, the destination buckets and their
+EventQueue order, the round minima, and the hosts' RNG streams and event-id
+counters after the round (so consecutive rounds stay in lockstep).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from shadow_amd import ShadowGpuError, _capi, synth
+from shadow_amd.worker import DeviceTable, HostTable, PacketBatch, deliver_round
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _device_table(lat, loss, row_begin=0):
+    import torch
+
+    n_cols = lat.shape[1]
+    dl = torch.from_numpy(np.ascontiguousarray(lat).view(np.int64).ravel()).cuda()
+    df = torch.from_numpy(np.ascontiguousarray(loss).ravel()).cuda()
+    return DeviceTable(dl, df, n_cols, row_begin)
+
+
+def _run_both(oracle, ctx, lat, loss, hosts, pk, round_end, sim_end, boot, rng0=None, ctr0=None):
+    H = hosts["n"]
+    ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    if rng0 is not None:
+        ht.set_state(rng0, ctr0)
+    rng, ctr = ht.get_state()
+    want = oracle.deliver_round(round_end, sim_end, boot, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
+                                hosts["ip"], hosts["route"], lat, loss, rng, ctr)
+    batch = PacketBatch.from_numpy(pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"])
+    out = deliver_round(ht, _device_table(lat, loss), batch, round_end, sim_end, boot)
+    got = out.to_numpy(len(pk["src"]))
+    grng, gctr = ht.get_state()
+    return want, got, (rng, ctr), (grng, gctr), ht
+
+
+def _assert_same(want, got, ost, gst):
+    assert np.array_equal(got["status"], want["status"])
+    assert np.array_equal(got["deliver_time"], want["deliver_time"])
+    assert np.array_equal(got["event_id"], want["event_id"])
+    assert np.array_equal(got["dst_offsets"], want["dst_offsets"])
+    assert np.array_equal(got["dst_order"], want["dst_order"])
+    assert got["delivered"] == want["delivered"]
+    assert got["min_deliver"] == want["min_deliver"] and got["min_lat"] == want["min_lat"]
+    assert np.array_equal(gst[0], ost[0]) and np.array_equal(gst[1], ost[1])
+
+
+def test_seeding_matches_seed_from_u64(oracle, ctx):
+    hosts = synth.make_hosts(50, 5)
+    ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    rng, ctr = ht.get_state()
+    for h in range(50):
+        assert np.array_equal(rng[h], oracle.xoshiro_seed(int(hosts["seed"][h])))
+    assert (ctr == 0).all()
+
+
+def test_golden_round(ctx):
+    z = np.load(os.path.join(GOLD, "deliver_small.npz"))
+    ht = HostTable(z["host_ip"], z["host_route"], z["host_seed"], ctx=ctx)
+    rng, ctr = ht.get_state()
+    assert np.array_equal(rng, z["rng0"]) and np.array_equal(ctr, z["ctr0"])
+    batch = PacketBatch.from_numpy(z["src"], z["dst_ip"], z["payload"], z["send_time"])
+    r = z["round"]
+    out = deliver_round(ht, _device_table(z["tab_lat"], z["tab_loss"]), batch, int(r[0]), int(r[1]), int(r[2]))
+    got = out.to_numpy(len(z["src"]))
+    assert np.array_equal(got["status"], z["status"])
+    assert np.array_equal(got["deliver_time"], z["deliver_time"])
+    assert np.array_equal(got["event_id"], z["event_id"])
+    assert np.array_equal(got["dst_order"], z["dst_order"])
+    assert np.array_equal(got["dst_offsets"], z["dst_offsets"])
+    assert [got["delivered"], got["min_deliver"], got["min_lat"]] == z["stats"].tolist()
+    rng1, ctr1 = ht.get_state()
+    assert np.array_equal(rng1, z["rng1"]) and np.array_equal(ctr1, z["ctr1"])
+
+
+def _world(n_nodes=64, n_hosts=2000, seed=1, lossy=True):
+    from oracle import oracle as O
+
+    g = synth.ring_chords_graph(n_nodes, 6.0, seed=seed)
+    rc, lat, loss, _ = O.shortest_paths(n_nodes, g["src"], g["dst"], g["lat"], g["loss"], False,
+                                        np.arange(n_nodes, dtype=np.uint32), threads=8)
+    assert rc == 0
+    if lossy:
+        loss = loss.copy()
+        loss[::2, 1::3] = np.float32(0.3)
+        loss[5, :] = np.float32(1.0)
+    hosts = synth.make_hosts(n_hosts, n_nodes, general_seed=seed, exact_seeds=n_hosts <= 5000)
+    return lat, loss, hosts
+
+
+T0 = 946684800 * 10**9  # EmulatedTime SIMULATION_START
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_round(oracle, ctx, seed):
+    lat, loss, hosts = _world(seed=seed)
+    start, end = T0 + 10**9, T0 + 10**9 + 10**6
+    pk = synth.make_packets(60000, hosts, start, end, seed=seed, p_unknown_dst=0.01)
+    pk["send_time"][::997] = end + 5 * 10**8  # some at/after sim end
+    want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, end, end + 5 * 10**8, start + 300_000)
+    assert want["delivered"] > 0 and (want["status"] == oracle.ST_DROP_LOSS).any()
+    _assert_same(want, got, ost, gst)
+
+
+def test_hot_destination_big_buckets(oracle, ctx):
+    """Skewed destinations: buckets far above the small-sort and LDS-chunk sizes."""
+    lat, loss, hosts = _world(n_hosts=3000, seed=3)
+    start, end = T0 + 2 * 10**9, T0 + 2 * 10**9 + 10**6
+    pk = synth.make_packets(200000, hosts, start, end, seed=5, hot_dst=11, p_hot=0.15)
+    pk2 = synth.make_packets(200000, hosts, start, end, seed=6, hot_dst=12, p_hot=0.02)
+    want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, end, 2**63, 0)
+    assert np.diff(want["dst_offsets"]).max() > 20000
+    _assert_same(want, got, ost, gst)
+    want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk2, end, 2**63, 0)
+    _assert_same(want, got, ost, gst)
+
+
+def test_equal_times_order_by_source(oracle, ctx):
+    """All packets clamp to round_end: order falls back to (src_host_id, event id)."""
+    lat, loss, hosts = _world(n_hosts=500, seed=4, lossy=False)
+    end = T0 + 10**12  # far beyond send + latency -> every deliver time == round_end
+    pk = synth.make_packets(20000, hosts, T0, T0 + 1000, seed=7)
+    want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, end, 2**63, 0)
+    assert (want["deliver_time"][want["status"] == 0] == end).all()
+    _assert_same(want, got, ost, gst)
+
+
+def test_consecutive_rounds_keep_streams(oracle, ctx):
+    lat, loss, hosts = _world(n_hosts=800, seed=5)
+    ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    rng, ctr = ht.get_state()
+    tab = _device_table(lat, loss)
+    for k in range(3):
+        start, end = T0 + k * 10**6, T0 + (k + 1) * 10**6
+        pk = synth.make_packets(15000, hosts, start, end, seed=20 + k)
+        want = oracle.deliver_round(end, 2**63, 0, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
+                                    hosts["ip"], hosts["route"], lat, loss, rng, ctr)
+        out = deliver_round(ht, tab, PacketBatch.from_numpy(pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"]),
+                            end, 2**63, 0)
+        _assert_same(want, out.to_numpy(15000), (rng, ctr), ht.get_state())
+
+
+def test_edge_cases(oracle, ctx):
+    lat, loss, hosts = _world(n_hosts=40, seed=6)
+    # empty round
+    pk = dict(src=np.zeros(0, np.uint32), dst_ip=np.zeros(0, np.uint32), payload=np.zeros(0, np.uint32),
+              send_time=np.zeros(0, np.uint64))
+    ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    out = deliver_round(ht, _device_table(lat, loss), PacketBatch.from_numpy(**{
+        "src_host": pk["src"], "dst_ipv4": pk["dst_ip"], "payload_len": pk["payload"], "send_time_ns": pk["send_time"]}),
+        T0 + 10, 2**63, 0)
+    assert out.n_delivered == 0 and out.min_deliver_time_ns == 2**64 - 1
+    assert (out.dst_offsets.cpu().numpy() == 0).all()
+    # a single host sending to itself, all acks, all unknown, all after end
+    for kind in ("self", "ack", "unknown", "late"):
+        n = 100
+        src = np.full(n, 3, np.uint32)
+        dst_ip = np.full(n, hosts["ip"][3] if kind == "self" else hosts["ip"][9], np.uint32)
+        if kind == "unknown":
+            dst_ip[:] = 7
+        pay = np.zeros(n, np.uint32) if kind == "ack" else np.full(n, 100, np.uint32)
+        t = np.arange(T0, T0 + n, dtype=np.uint64)
+        sim_end = T0 if kind == "late" else 2**63
+        p = dict(src=src, dst_ip=dst_ip, payload=pay, send_time=t)
+        want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, p, T0 + 10**6, sim_end, 0)
+        _assert_same(want, got, ost, gst)
+
+
+def test_unsorted_sources_rejected(ctx):
+    lat, loss, hosts = _world(n_hosts=10, seed=7)
+    ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    b = PacketBatch.from_numpy([2, 1], hosts["ip"][[0, 0]], [1, 1], [T0, T0])
+    with pytest.raises(ShadowGpuError) as e:
+        deliver_round(ht, _device_table(lat, loss), b, T0 + 10, 2**63, 0)
+    assert e.value.code == _capi.SG_ERR_UNSORTED
+
+
+def test_duplicate_ip_rejected(ctx):
+    with pytest.raises(ShadowGpuError) as e:
+        HostTable([5, 5], [0, 0], [1, 2], ctx=ctx)
+    assert e.value.code == _capi.SG_ERR_DUPLICATE_IP
+
+
+def test_sparse_addresses_use_sorted_lookup(oracle, ctx):
+    lat, loss, hosts = _world(n_hosts=300, seed=8)
+    hosts["ip"] = (np.random.default_rng(1).permutation(2**20)[:300].astype(np.uint32) * 4000 + 7).astype(np.uint32)
+    pk = synth.make_packets(8000, hosts, T0, T0 + 10**6, seed=9, p_unknown_dst=0.05)
+    want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, T0 + 10**6, 2**63, 0)
+    _assert_same(want, got, ost, gst)

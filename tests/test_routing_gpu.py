@@ -1,0 +1,175 @@
+"""GPU parity: routing-table build (HIP) vs the CPU oracle, bit-exact.
+
+Latency must match exactly (u64 ns) and loss bit-for-bit (f32), for every
+used pair, on the reference's own test graphs, the committed golden vectors,
+and seeded random graphs.  Errors must match the reference's error cases.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from shadow_amd import NetworkGraph, ShadowGpuError, _capi, generate_routing_info, synth
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _graph(g, ctx):
+    return NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
+
+
+def _check(oracle, g, used, ctx, shortest=True, rows=None):
+    net = _graph(g, ctx)
+    if rows is None:
+        t = net.compute_shortest_paths(used) if shortest else net.get_direct_paths(used)
+        lat, loss = t.latency_ns, t.packet_loss
+    else:
+        import torch
+
+        r0, r1 = rows
+        nu = len(used)
+        dl = torch.empty((r1 - r0) * nu, dtype=torch.int64, device="cuda")
+        df = torch.empty((r1 - r0) * nu, dtype=torch.float32, device="cuda")
+        net.build_rows_device(used, r0, r1, dl.data_ptr(), df.data_ptr(), shortest)
+        lat = dl.cpu().numpy().view(np.uint64).reshape(r1 - r0, nu)
+        loss = df.cpu().numpy().reshape(r1 - r0, nu)
+    fn = oracle.shortest_paths if shortest else oracle.direct_paths
+    kw = dict(rows=rows, threads=8) if shortest else {}
+    rc, olat, oloss, _ = fn(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], used, **kw)
+    assert rc == 0
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(loss.view(np.uint32), oloss.view(np.uint32))
+    return lat, loss
+
+
+def test_reference_test_shortest_path(ctx):
+    """graph/mod.rs:564-651, through the GML parser like the reference test."""
+    from test_capi_cpu import THREE
+
+    k = json.load(open(os.path.join(GOLD, "reference_kat.json")))["test_shortest_path"]
+    for d in (1, 0):
+        graph = NetworkGraph.parse(THREE.format(d=d), ctx=ctx)
+        n0, n1, n2 = (graph.node_id_to_index(i) for i in range(3))
+        paths = graph.compute_shortest_paths([n0, n1, n2])
+        lookup = lambda a, b: paths[(a, b)].latency_ns
+        want = k["directed_latency" if d else "undirected_latency"]
+        got = [[lookup(a, b) for b in (n0, n1, n2)] for a in (n0, n1, n2)]
+        assert got == want
+        assert len(paths) == 9
+
+
+def test_one_gbit_switch(ctx):
+    from test_capi_cpu import test_parse_one_gbit_switch  # noqa: F401
+
+    text = 'graph [\n  directed 0\n  node [\n    id 0\n  ]\n  edge [\n    source 0\n    target 0\n    latency "1 ms"\n    packet_loss 0.0\n  ]\n]'
+    g = NetworkGraph.parse(text, ctx=ctx)
+    for fn in (g.compute_shortest_paths, g.get_direct_paths):
+        p = fn([0])[(0, 0)]
+        assert p.latency_ns == 1_000_000 and p.packet_loss == 0.0
+    r = generate_routing_info(g, {0}, True)
+    assert r.path(0, 0).latency_ns == 1_000_000 and r.get_smallest_latency_ns() == 1_000_000
+
+
+def test_golden_vectors(ctx):
+    z = np.load(os.path.join(GOLD, "routing_small.npz"))
+    for name in sorted({k.split(".")[0] for k in z.files}):
+        g = dict(n=int(z[f"{name}.n"][0]), src=z[f"{name}.src"], dst=z[f"{name}.dst"], lat=z[f"{name}.lat"],
+                 loss=z[f"{name}.loss"], directed=bool(z[f"{name}.directed"][0]))
+        t = _graph(g, ctx).compute_shortest_paths(z[f"{name}.used"])
+        assert np.array_equal(t.latency_ns, z[f"{name}.out_lat"]), name
+        assert np.array_equal(t.packet_loss.view(np.uint32), z[f"{name}.out_loss"].view(np.uint32)), name
+
+
+@pytest.mark.parametrize("directed", [False, True])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_sparse(oracle, ctx, directed, seed):
+    g = synth.ring_chords_graph(700, 8.0, seed=seed, directed=directed, parallel=0.05)
+    used = np.random.default_rng(seed).permutation(700)[:333].astype(np.uint32)
+    _check(oracle, g, used, ctx)
+
+
+def test_complete_graph(oracle, ctx):
+    g = synth.complete_graph(300, seed=3)
+    _check(oracle, g, np.arange(300, dtype=np.uint32), ctx)
+
+
+def test_heavy_loss_ties(oracle, ctx):
+    """Many equal-latency paths: the loss tie-break decides (graph/mod.rs:305-313)."""
+    g = synth.ring_chords_graph(400, 10.0, seed=9)
+    rng = np.random.default_rng(4)
+    g["lat"] = (rng.integers(1, 4, len(g["lat"])) * 1000).astype(np.uint64)
+    g["loss"] = rng.uniform(0, 0.4, len(g["lat"])).astype(np.float32)
+    g["loss"][rng.random(len(g["loss"])) < 0.1] = np.float32(1.0)
+    _check(oracle, g, np.arange(400, dtype=np.uint32), ctx)
+
+
+def test_wide_fallback_big_latencies(oracle, ctx):
+    """Path latencies beyond 2^34 ns take the u64 kernel; must still be exact."""
+    g = synth.ring_chords_graph(150, 4.0, seed=8, lat_lo_us=2_000_000, lat_hi_us=9_000_000)
+    lat, _ = _check(oracle, g, np.arange(150, dtype=np.uint32), ctx)
+    assert lat.max() >= (1 << 34)
+
+
+def test_huge_edge_latency(oracle, ctx):
+    g = synth.ring_chords_graph(60, 4.0, seed=10)
+    g["lat"][70] = np.uint64(1) << np.uint64(62)
+    _check(oracle, g, np.arange(60, dtype=np.uint32), ctx)
+
+
+def test_row_shards_concatenate(oracle, ctx):
+    g = synth.ring_chords_graph(500, 6.0, seed=12)
+    used = np.arange(0, 500, 2, dtype=np.uint32)
+    full, _ = _check(oracle, g, used, ctx)
+    parts = [_check(oracle, g, used, ctx, rows=(a, b))[0] for a, b in ((0, 70), (70, 71), (71, 250))]
+    assert np.array_equal(np.concatenate(parts), full)
+
+
+def test_direct_paths(oracle, ctx):
+    g = synth.complete_graph(120, seed=5)
+    _check(oracle, g, np.random.default_rng(0).permutation(120).astype(np.uint32), ctx, shortest=False)
+    gd = synth.complete_graph(40, seed=6)
+    # a directed complete graph needs both directions
+    gd2 = dict(n=40, src=np.concatenate([gd["src"], gd["dst"][40:]]), dst=np.concatenate([gd["dst"], gd["src"][40:]]),
+               lat=np.concatenate([gd["lat"], gd["lat"][40:] + 1]), loss=np.concatenate([gd["loss"], gd["loss"][40:]]),
+               directed=True)
+    _check(oracle, gd2, np.arange(40, dtype=np.uint32), ctx, shortest=False)
+
+
+def test_errors_match_reference(oracle, ctx):
+    cases = [  # (n, src, dst, directed, used, shortest, code, pair)
+        (2, [0, 0], [0, 1], False, [0, 1], True, _capi.SG_ERR_NO_EDGE, (1, 1)),
+        (2, [0, 0, 1, 0], [0, 0, 1, 1], False, [0, 1], True, _capi.SG_ERR_MULTI_EDGE, (0, 0)),
+        (2, [0, 1, 0], [0, 1, 1], True, [0, 1], True, _capi.SG_ERR_UNREACHABLE, (1, 0)),
+        (2, [0, 1], [0, 1], False, [0, 1], False, _capi.SG_ERR_NO_EDGE, (0, 1)),
+        (2, [0, 1, 0, 1], [0, 1, 1, 0], False, [0, 1], False, _capi.SG_ERR_MULTI_EDGE, (0, 1)),
+    ]
+    for n, s, d, directed, used, shortest, code, pair in cases:
+        m = len(s)
+        net = NetworkGraph(n, s, d, [5] * m, [0.0] * m, directed, ctx=ctx)
+        with pytest.raises(ShadowGpuError) as e:
+            (net.compute_shortest_paths if shortest else net.get_direct_paths)(used)
+        assert e.value.code == code and e.value.pair == pair, (e.value.code, e.value.pair, str(e.value))
+    # messages name GML ids like the reference
+    text = 'graph [\n  node [\n    id 7\n  ]\n  node [\n    id 9\n  ]\n  edge [\n    source 7\n    target 9\n    latency "1 ms"\n  ]\n  edge [\n    source 7\n    target 7\n    latency "1 ms"\n  ]\n]'
+    g = NetworkGraph.parse(text, ctx=ctx)
+    with pytest.raises(ShadowGpuError, match="No edge connecting node 9 to 9"):
+        g.compute_shortest_paths([0, 1])
+    # unused isolated node is fine
+    net = NetworkGraph(3, [0, 1, 0, 2], [0, 1, 1, 2], [5] * 4, [0.0] * 4, False, ctx=ctx)
+    assert net.compute_shortest_paths([0, 1])[(0, 1)].latency_ns == 5
+
+
+def test_min_latency_device(ctx):
+    import torch
+
+    x = torch.tensor([9, 7, 11, 3 << 40], dtype=torch.int64, device="cuda")
+    g = NetworkGraph(1, [0], [0], [1], [0.0], False, ctx=ctx)
+    assert g.min_latency_device(x.data_ptr(), 4) == 7
+    assert g.min_latency_device(x.data_ptr(), 0) == (1 << 64) - 1
+
+
+def test_empty_used(ctx):
+    g = NetworkGraph(2, [0, 1], [0, 1], [1, 1], [0.0, 0.0], False, ctx=ctx)
+    assert len(g.compute_shortest_paths([])) == 0
