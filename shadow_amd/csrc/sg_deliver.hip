@@ -39,6 +39,7 @@ struct sg_hosts {
   uint32_t* dense = nullptr;
   uint32_t* sorted_ip = nullptr;
   uint32_t* sorted_host = nullptr;
+  uint32_t max_route = 0;  // largest routing-table index of any host
   ~sg_hosts() {
     void* ps[] = {route, rng, ctr, dense, sorted_ip, sorted_host};
     for (void* p : ps)
@@ -485,6 +486,7 @@ int32_t sg_hosts_create(sg_ctx* ctx, uint32_t n_hosts, const uint32_t* host_ipv4
     SG_HIP(hipMalloc(&hs->ctr, std::max<size_t>(n * 8, 16)));
     uint64_t* d_seed = nullptr;
     SG_HIP(hipMalloc(&d_seed, std::max<size_t>(n * 8, 16)));
+    for (uint32_t h = 0; h < n_hosts; h++) hs->max_route = std::max(hs->max_route, host_route_idx[h]);
     std::vector<std::pair<uint32_t, uint32_t>> ips(n);
     for (uint32_t h = 0; h < n_hosts; h++) ips[h] = {host_ipv4[h], h};
     std::sort(ips.begin(), ips.end());
@@ -580,6 +582,8 @@ int32_t sg_deliver_round(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table, co
     if (!hosts || hosts->ctx != ctx || !table || !round || !packets || !out)
       throw Error(SG_ERR_INVALID_ARG, "null argument");
     if (!out->dst_offsets) throw Error(SG_ERR_INVALID_ARG, "null dst_offsets");
+    if (hosts->n && hosts->max_route >= table->n_cols)
+      throw Error(SG_ERR_INVALID_ARG, "a host's routing index is outside the table's columns");
     if (packets->n_packets &&
         (!packets->src_host || !packets->dst_ipv4 || !packets->payload_len || !packets->send_time_ns ||
          !out->status || !out->deliver_time_ns || !out->event_id || !out->dst_order ||
