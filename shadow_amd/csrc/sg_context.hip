@@ -164,11 +164,18 @@ extern "C" {
 
 int32_t sg_abi_version(void) { return SG_ABI_VERSION; }
 
+static thread_local std::string g_create_error;
+
 int32_t sg_ctx_create(int32_t device, sg_ctx** out) {
   if (!out) return SG_ERR_INVALID_ARG;
   *out = nullptr;
   int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return SG_ERR_DEVICE;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || device < 0 || device >= n) {
+    g_create_error = std::string("hipGetDeviceCount: ") + hipGetErrorString(e) + ", devices=" +
+                     std::to_string(n) + ", requested=" + std::to_string(device);
+    return SG_ERR_DEVICE;
+  }
   sg_ctx* ctx = new (std::nothrow) sg_ctx();
   if (!ctx) return SG_ERR_OOM;
   ctx->device = device;
@@ -176,11 +183,12 @@ int32_t sg_ctx_create(int32_t device, sg_ctx** out) {
     SG_HIP(hipSetDevice(device));
     SG_HIP(hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking));
     ctx->stream = ctx->own_stream;
-    hipDeviceProp_t prop;
-    SG_HIP(hipGetDeviceProperties(&prop, device));
-    ctx->n_cu = prop.multiProcessorCount;
+    int cus = 0;
+    SG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    ctx->n_cu = cus;
   });
   if (rc != SG_OK) {
+    g_create_error = ctx->last_error;
     delete ctx;
     return rc;
   }
@@ -215,7 +223,8 @@ int32_t sg_ctx_synchronize(sg_ctx* ctx) {
 }
 
 const char* sg_ctx_last_error(const sg_ctx* ctx) {
-  return ctx ? ctx->last_error.c_str() : "null context";
+  // NULL: the reason the last sg_ctx_create on this thread failed
+  return ctx ? ctx->last_error.c_str() : g_create_error.c_str();
 }
 
 void sg_ctx_last_error_pair(const sg_ctx* ctx, uint32_t* row, uint32_t* col) {

@@ -36,7 +36,8 @@ class Context:
         h = C.c_void_p()
         rc = L.sg_ctx_create(int(device), C.byref(h))
         if rc != _capi.SG_OK:
-            raise ShadowGpuError(rc, f"sg_ctx_create(device={device}) failed with status {rc}")
+            why = (L.sg_ctx_last_error(None) or b"").decode(errors="replace")
+            raise ShadowGpuError(rc, f"sg_ctx_create(device={device}) failed with status {rc}: {why}")
         self.handle = h
         self.device = int(device)
         if stream is not None:
