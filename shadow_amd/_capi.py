@@ -92,6 +92,14 @@ def load(path: str | None = None):
     if _lib is not None:
         return _lib
     path = path or os.environ.get("SHADOW_GPU_LIB", LIB_PATH)
+    # One HIP runtime per process: torch bundles its own libamdhip64.so (soname
+    # libamdhip64.so.7).  If our library loaded first, /opt/rocm's runtime would
+    # come in too and whichever initialised second would see no device.  Loading
+    # torch first lets our NEEDED libamdhip64.so.7 resolve to the loaded copy.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(path):
         raise ShadowGpuUnavailable(
             f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
