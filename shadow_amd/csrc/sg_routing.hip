@@ -515,7 +515,7 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
   constexpr int VPW = 4;
   const uint32_t nvb = (n + RELAX_WAVES * VPW - 1) / (RELAX_WAVES * VPW);
   uint64_t* D = ctx->r_dist.get<uint64_t>((size_t)group * n * BATCH);
-  uint32_t* flags = ctx->r_flags.get<uint32_t>((size_t)group * 3 + 8)  // [active | changed | sat];
+  uint32_t* flags = ctx->r_flags.get<uint32_t>((size_t)group * 3 + 8);  // [active | changed | sat]
   uint32_t* sat = flags + 2 * (size_t)group;
   std::vector<uint32_t> h_changed(group), h_sat(group);
   std::vector<uint32_t> wide_rows;
