@@ -205,6 +205,35 @@ int32_t sg_deliver_round(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table,
                          const sg_round* round, const sg_packets* packets, sg_deliveries* out,
                          sg_round_stats* stats);
 
+/* ---- sharded delivery (one process per GPU, exchange between the calls) ---
+ * Hosts are partitioned over ranks; a rank sends for the hosts whose routing
+ * rows it holds and receives for the hosts it owns.
+ *   1. sg_deliver_source: the send_packet half for this rank's packets
+ *      (same per-packet outputs and RNG/counter updates as sg_deliver_round),
+ *      plus one sg_record per delivered packet, grouped by the destination's
+ *      owner rank host_owner[dst] (send_counts[r] records for rank r, in rank
+ *      order).  Synchronises (the counts are needed for the exchange).
+ *   2. the caller exchanges records (all-to-all, e.g. RCCL over xGMI).
+ *   3. sg_deliver_bucket: the push_packet_to_host half on the owner: bucket
+ *      the received records by local destination slot host_local[dst] and
+ *      order each bucket as the EventQueue pops it (deliver time, src host,
+ *      event id).  dst_order holds indices into `recv`.                     */
+typedef struct sg_record {
+  uint64_t deliver_time_ns;
+  uint64_t order_key; /* (src_host << 32) | k, k = rank among src_host's delivered packets this round */
+  uint64_t event_id;  /* src_host_event_id */
+  uint32_t packet;    /* index in the source rank's sg_packets */
+  uint32_t dst_host;  /* HostId of the destination */
+} sg_record;
+
+int32_t sg_deliver_source(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table, const sg_round* round,
+                          const sg_packets* packets, uint8_t* status, uint64_t* deliver_time_ns,
+                          uint64_t* event_id, const uint32_t* host_owner, uint32_t n_ranks,
+                          sg_record* send, uint32_t* send_counts, sg_round_stats* stats);
+int32_t sg_deliver_bucket(sg_ctx* ctx, const sg_record* recv, uint32_t n_records,
+                          const uint32_t* host_local, uint32_t n_hosts, uint32_t n_local_hosts,
+                          uint32_t* dst_order, uint32_t* dst_offsets);
+
 #ifdef __cplusplus
 }
 #endif

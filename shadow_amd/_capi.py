@@ -35,7 +35,7 @@ EXPORTED = [
     "sg_ctx_read_timer", "sg_gml_parse", "sg_gml_graph",
     "sg_gml_node_index", "sg_gml_destroy", "sg_net_create", "sg_net_destroy", "sg_routing_build",
     "sg_routing_min_latency", "sg_hosts_create", "sg_hosts_get_state", "sg_hosts_set_state",
-    "sg_hosts_destroy", "sg_deliver_round",
+    "sg_hosts_destroy", "sg_deliver_round", "sg_deliver_source", "sg_deliver_bucket",
 ]
 
 
@@ -135,6 +135,9 @@ def load(path: str | None = None):
         "sg_hosts_destroy": (None, [vp]),
         "sg_deliver_round": (i32, [vp, vp, C.POINTER(sg_table), C.POINTER(sg_round), C.POINTER(sg_packets),
                                    C.POINTER(sg_deliveries), C.POINTER(sg_round_stats)]),
+        "sg_deliver_source": (i32, [vp, vp, C.POINTER(sg_table), C.POINTER(sg_round), C.POINTER(sg_packets),
+                                    vp, vp, vp, vp, u32, vp, u32p, C.POINTER(sg_round_stats)]),
+        "sg_deliver_bucket": (i32, [vp, vp, u32, vp, u32, u32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

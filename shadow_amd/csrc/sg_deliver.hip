@@ -23,6 +23,7 @@
 // so the bucket key is (deliver_time, packet index).
 #include <algorithm>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 #include "sg_device.h"
@@ -54,7 +55,7 @@ constexpr int SMALL_BUCKET = 32;
 constexpr int SORT_BLOCK = 256;
 constexpr int SORT_CHUNK = 2048;  // elements sorted in LDS per chunk
 
-enum : uint32_t { ERR_UNSORTED = 1, ERR_SRC_RANGE = 2, ERR_ROUTE_RANGE = 4 };
+enum : uint32_t { ERR_UNSORTED = 1, ERR_SRC_RANGE = 2, ERR_ROUTE_RANGE = 4, ERR_NOT_LOCAL = 8 };
 
 struct HostMap {
   uint32_t ip_base, dense_span, n_sorted;
@@ -205,27 +206,36 @@ __global__ void __launch_bounds__(256) k_walk(WalkArgs a) {
   }
 }
 
+// Bucket entries carry a 128-bit sort key (kt = deliver time, kk = order key)
+// and a value ki (what dst_order reports).  The order key encodes
+// (src_host_id, src_host_event_id) order:
+//   single GPU: kk = packet index (input grouped by ascending source host, and
+//               event ids grow in send order);
+//   sharded:    kk = (src_host << 32) | k, k = the packet's rank among its
+//               host's delivered packets this round.
 __global__ void k_scatter(const uint32_t* __restrict__ dst_host, const uint64_t* __restrict__ deliver,
                           uint32_t P, const uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
-                          uint64_t* __restrict__ kt, uint32_t* __restrict__ ki) {
+                          uint64_t* __restrict__ kt, uint64_t* __restrict__ kk, uint32_t* __restrict__ ki) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < P; i += gridDim.x * blockDim.x) {
     uint32_t d = dst_host[i];
     if (d == NONE) continue;
     uint32_t p = off[d] + atomicAdd(&cur[d], 1u);
     kt[p] = deliver[i];
+    kk[p] = i;
     ki[p] = i;
   }
 }
 
-__device__ __forceinline__ bool key_less(uint64_t ta, uint32_t ia, uint64_t tb, uint32_t ib) {
-  return ta < tb || (ta == tb && ia < ib);
+__device__ __forceinline__ bool key_less(uint64_t ta, uint64_t ka, uint64_t tb, uint64_t kb) {
+  return ta < tb || (ta == tb && ka < kb);
 }
 
 // Thread per destination: insertion sort of a small bucket; big buckets are
 // queued for k_sort_big.
 __global__ void k_sort_small(const uint32_t* __restrict__ off, uint32_t H, uint64_t* __restrict__ kt,
-                             uint32_t* __restrict__ ki, uint32_t* __restrict__ order,
-                             uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
+                             uint64_t* __restrict__ kk, uint32_t* __restrict__ ki,
+                             uint32_t* __restrict__ order, uint32_t* __restrict__ big_list,
+                             uint32_t* __restrict__ big_count) {
   for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < H; h += gridDim.x * blockDim.x) {
     const uint32_t b = off[h], e = off[h + 1];
     if (e - b > SMALL_BUCKET) {
@@ -233,15 +243,17 @@ __global__ void k_sort_small(const uint32_t* __restrict__ off, uint32_t H, uint6
       continue;
     }
     for (uint32_t i = b + 1; i < e; i++) {
-      uint64_t t = kt[i];
+      uint64_t t = kt[i], k = kk[i];
       uint32_t x = ki[i];
       uint32_t j = i;
-      while (j > b && key_less(t, x, kt[j - 1], ki[j - 1])) {
+      while (j > b && key_less(t, k, kt[j - 1], kk[j - 1])) {
         kt[j] = kt[j - 1];
+        kk[j] = kk[j - 1];
         ki[j] = ki[j - 1];
         j--;
       }
       kt[j] = t;
+      kk[j] = k;
       ki[j] = x;
     }
     for (uint32_t i = b; i < e; i++) order[i] = ki[i];
@@ -253,9 +265,10 @@ __global__ void k_sort_small(const uint32_t* __restrict__ off, uint32_t H, uint6
 __global__ void __launch_bounds__(SORT_BLOCK)
     k_sort_big(const uint32_t* __restrict__ off, const uint32_t* __restrict__ big_list,
                const uint32_t* __restrict__ big_count, uint64_t* __restrict__ kt,
-               uint32_t* __restrict__ ki, uint64_t* __restrict__ kt2, uint32_t* __restrict__ ki2,
-               uint32_t* __restrict__ order) {
+               uint64_t* __restrict__ kk, uint32_t* __restrict__ ki, uint64_t* __restrict__ kt2,
+               uint64_t* __restrict__ kk2, uint32_t* __restrict__ ki2, uint32_t* __restrict__ order) {
   __shared__ uint64_t st[SORT_CHUNK];
+  __shared__ uint64_t sk[SORT_CHUNK];
   __shared__ uint32_t si[SORT_CHUNK];
   const uint32_t nbig = *big_count;
   for (uint32_t q = blockIdx.x; q < nbig; q += gridDim.x) {
@@ -267,13 +280,10 @@ __global__ void __launch_bounds__(SORT_BLOCK)
       uint32_t pow2 = 1;
       while (pow2 < cn) pow2 <<= 1;
       for (uint32_t i = threadIdx.x; i < pow2; i += SORT_BLOCK) {
-        if (i < cn) {
-          st[i] = kt[b + c0 + i];
-          si[i] = ki[b + c0 + i];
-        } else {
-          st[i] = ~0ull;
-          si[i] = ~0u;
-        }
+        const bool in = i < cn;
+        st[i] = in ? kt[b + c0 + i] : ~0ull;
+        sk[i] = in ? kk[b + c0 + i] : ~0ull;
+        si[i] = in ? ki[b + c0 + i] : ~0u;
       }
       __syncthreads();
       for (uint32_t k = 2; k <= pow2; k <<= 1) {
@@ -282,11 +292,14 @@ __global__ void __launch_bounds__(SORT_BLOCK)
             uint32_t l = i ^ j;
             if (l > i) {
               bool up = (i & k) == 0;
-              bool sw = up ? key_less(st[l], si[l], st[i], si[i]) : key_less(st[i], si[i], st[l], si[l]);
+              bool sw = up ? key_less(st[l], sk[l], st[i], sk[i]) : key_less(st[i], sk[i], st[l], sk[l]);
               if (sw) {
                 uint64_t tt = st[i];
                 st[i] = st[l];
                 st[l] = tt;
+                uint64_t tk = sk[i];
+                sk[i] = sk[l];
+                sk[l] = tk;
                 uint32_t ii = si[i];
                 si[i] = si[l];
                 si[l] = ii;
@@ -298,28 +311,25 @@ __global__ void __launch_bounds__(SORT_BLOCK)
       }
       for (uint32_t i = threadIdx.x; i < cn; i += SORT_BLOCK) {
         kt[b + c0 + i] = st[i];
+        kk[b + c0 + i] = sk[i];
         ki[b + c0 + i] = si[i];
       }
       __syncthreads();
     }
     // 2. merge runs of width w into the other buffer until one run remains
-    uint64_t* at = kt + b;
-    uint32_t* ai = ki + b;
-    uint64_t* bt = kt2 + b;
-    uint32_t* bi = ki2 + b;
+    uint64_t *at = kt + b, *ak = kk + b, *bt = kt2 + b, *bk = kk2 + b;
+    uint32_t *ai = ki + b, *bi = ki2 + b;
     for (uint32_t w = SORT_CHUNK; w < n; w <<= 1) {
       for (uint32_t p = threadIdx.x; p < n; p += SORT_BLOCK) {
-        // output position p belongs to the pair of runs starting at s
-        const uint32_t s = (p / (2 * w)) * (2 * w);
+        const uint32_t s = (p / (2 * w)) * (2 * w);  // first run of the pair holding output p
         const uint32_t m = min(s + w, n), t = min(s + 2 * w, n);
         const uint32_t k = p - s;  // rank within the merged pair
-        // merge path: find i in run A (s..m) and j = k - i in run B (m..t)
+        // merge path: i elements from run A (s..m), k - i from run B (m..t)
         uint32_t lo = k > (t - m) ? k - (t - m) : 0, hi = min(k, m - s);
         while (lo < hi) {
-          uint32_t i = (lo + hi) >> 1;  // take i from A, k-i from B
+          uint32_t i = (lo + hi) >> 1;
           uint32_t j = k - i;
-          // A[i] < B[j-1] ?  (stable: A wins ties; keys are unique anyway)
-          if (key_less(bt == kt2 + b ? at[s + i] : at[s + i], ai[s + i], at[m + j - 1], ai[m + j - 1]))
+          if (key_less(at[s + i], ak[s + i], at[m + j - 1], ak[m + j - 1]))
             lo = i + 1;
           else
             hi = i;
@@ -331,25 +341,98 @@ __global__ void __launch_bounds__(SORT_BLOCK)
         else if (m + j >= t)
           takeA = true;
         else
-          takeA = !key_less(at[m + j], ai[m + j], at[s + i], ai[s + i]);
-        if (takeA) {
-          bt[p] = at[s + i];
-          bi[p] = ai[s + i];
-        } else {
-          bt[p] = at[m + j];
-          bi[p] = ai[m + j];
-        }
+          takeA = !key_less(at[m + j], ak[m + j], at[s + i], ak[s + i]);
+        const uint32_t src = takeA ? s + i : m + j;
+        bt[p] = at[src];
+        bk[p] = ak[src];
+        bi[p] = ai[src];
       }
       __syncthreads();
-      uint64_t* tt = at;
+      uint64_t* t0 = at;
       at = bt;
-      bt = tt;
-      uint32_t* ti = ai;
+      bt = t0;
+      uint64_t* k0 = ak;
+      ak = bk;
+      bk = k0;
+      uint32_t* i0 = ai;
       ai = bi;
-      bi = ti;
+      bi = i0;
     }
     for (uint32_t p = threadIdx.x; p < n; p += SORT_BLOCK) order[b + p] = ai[p];
     __syncthreads();
+  }
+}
+
+// ---- sharded delivery: pack delivered records by destination owner --------
+constexpr int PACK_BLOCK = 256;
+constexpr uint32_t MAX_RANKS = 64;
+
+__global__ void __launch_bounds__(PACK_BLOCK)
+    k_owner_count(const uint32_t* __restrict__ dst_host, uint32_t P, const uint32_t* __restrict__ owner,
+                  uint32_t n_ranks, uint32_t* __restrict__ block_counts) {
+  __shared__ uint32_t cnt[MAX_RANKS];
+  for (uint32_t r = threadIdx.x; r < n_ranks; r += PACK_BLOCK) cnt[r] = 0;
+  __syncthreads();
+  const uint32_t chunk = (P + gridDim.x - 1) / gridDim.x;
+  const uint32_t i0 = blockIdx.x * chunk, i1 = min(P, i0 + chunk);
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += PACK_BLOCK) {
+    uint32_t d = dst_host[i];
+    if (d != NONE) atomicAdd(&cnt[owner[d]], 1u);
+  }
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < n_ranks; r += PACK_BLOCK) block_counts[r * gridDim.x + blockIdx.x] = cnt[r];
+}
+
+__global__ void __launch_bounds__(PACK_BLOCK)
+    k_owner_scatter(const uint32_t* __restrict__ src_host, const uint32_t* __restrict__ dst_host,
+                    const uint64_t* __restrict__ deliver, const uint64_t* __restrict__ eid,
+                    const uint64_t* __restrict__ ctr_start, uint32_t P, const uint32_t* __restrict__ owner,
+                    uint32_t n_ranks, const uint32_t* __restrict__ block_off, sg_record* __restrict__ send) {
+  __shared__ uint32_t cur[MAX_RANKS];
+  for (uint32_t r = threadIdx.x; r < n_ranks; r += PACK_BLOCK) cur[r] = block_off[r * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const uint32_t chunk = (P + gridDim.x - 1) / gridDim.x;
+  const uint32_t i0 = blockIdx.x * chunk, i1 = min(P, i0 + chunk);
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += PACK_BLOCK) {
+    uint32_t d = dst_host[i];
+    if (d == NONE) continue;
+    uint32_t p = atomicAdd(&cur[owner[d]], 1u);
+    uint32_t s = src_host[i];
+    sg_record r;
+    r.deliver_time_ns = deliver[i];
+    r.order_key = ((uint64_t)s << 32) | (uint32_t)(eid[i] - ctr_start[s]);
+    r.event_id = eid[i];
+    r.packet = i;
+    r.dst_host = d;
+    send[p] = r;
+  }
+}
+
+// ---- sharded delivery: destination side ----------------------------------
+__global__ void k_rec_count(const sg_record* __restrict__ rec, uint32_t n, const uint32_t* __restrict__ local,
+                            uint32_t H, uint32_t* __restrict__ cnt, uint32_t* __restrict__ err) {
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+    uint32_t d = rec[r].dst_host;
+    uint32_t s = d < H ? local[d] : NONE;
+    if (s == NONE) {
+      atomicOr(err, ERR_NOT_LOCAL);
+      continue;
+    }
+    atomicAdd(&cnt[s], 1u);
+  }
+}
+
+__global__ void k_rec_scatter(const sg_record* __restrict__ rec, uint32_t n, const uint32_t* __restrict__ local,
+                              uint32_t H, const uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
+                              uint64_t* __restrict__ kt, uint64_t* __restrict__ kk, uint32_t* __restrict__ ki) {
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+    uint32_t d = rec[r].dst_host;
+    uint32_t s = d < H ? local[d] : NONE;
+    if (s == NONE) continue;
+    uint32_t p = off[s] + atomicAdd(&cur[s], 1u);
+    kt[p] = rec[r].deliver_time_ns;
+    kk[p] = rec[r].order_key;
+    ki[p] = r;
   }
 }
 
@@ -359,100 +442,112 @@ static void fail_flags(uint32_t err) {
     throw Error(SG_ERR_UNSORTED, "packets must be grouped by ascending source host (send order within a host)");
   if (err & ERR_ROUTE_RANGE)
     throw Error(SG_ERR_INVALID_ARG, "a sending host's route row is outside the table shard");
+  if (err & ERR_NOT_LOCAL)
+    throw Error(SG_ERR_INVALID_ARG, "a received record's destination host is not local to this rank");
 }
 
-static void deliver_round(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const sg_round* rd,
-                          const sg_packets* pk, sg_deliveries* out, sg_round_stats* stats) {
+// Sort the buckets described by off[0..n_buckets] (entries in kt/kk/ki) into order.
+static void sort_buckets(sg_ctx* ctx, const uint32_t* off, uint32_t n_buckets, uint32_t n_entries,
+                         uint64_t* kt, uint64_t* kk, uint32_t* ki, uint32_t* order, uint32_t* big_count) {
+  hipStream_t st = ctx->stream;
+  uint32_t* big_list = ctx->d_lists.get<uint32_t>(n_buckets);
+  {
+    TimedLaunch tl(ctx, "sort_small", 24.0 * n_entries + 8.0 * n_buckets);
+    hipLaunchKernelGGL(k_sort_small, dim3(grid_for(n_buckets, 256)), dim3(256), 0, st, off, n_buckets, kt, kk,
+                       ki, order, big_list, big_count);
+  }
+  uint64_t* kt2 = ctx->d_keys2.get<uint64_t>(n_entries);
+  uint64_t* kk2 = ctx->d_keys3.get<uint64_t>(n_entries);
+  uint32_t* ki2 = ctx->d_vals2.get<uint32_t>(n_entries);
+  {
+    TimedLaunch tl(ctx, "sort_big", 0.0);
+    hipLaunchKernelGGL(k_sort_big, dim3(std::min<uint32_t>(std::max(n_buckets, 1u), 2048)), dim3(SORT_BLOCK), 0, st,
+                       off, big_list, big_count, kt, kk, ki, kt2, kk2, ki2, order);
+  }
+  SG_CHECK_LAUNCH();
+}
+
+struct RoundWork {
+  uint32_t *seg_begin, *seg_end, *dst_cnt, *cur, *big_count, *err, *dst_host;
+  uint64_t* ctr_start;
+  unsigned long long* stats;
+};
+
+// Shared source half of a round: segments + walk.  Leaves per-packet
+// dst_host (NONE unless delivered), per-destination counts, stats.
+static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const sg_round* rd,
+                              const sg_packets* pk, uint8_t* status, uint64_t* deliver, uint64_t* eid,
+                              bool want_ctr_start) {
   hipStream_t st = ctx->stream;
   const uint32_t P = pk->n_packets, H = hs->n;
-  // workspace: [seg_begin H][seg_end H][dst_cnt H][cur H][big_count 1][err 1] + stats
+  RoundWork w;
+  // workspace: [seg_begin H][seg_end H][dst_cnt H][cur H][big_count 1][err 1]
   uint32_t* ws = ctx->d_seg.get<uint32_t>(4 * (size_t)H + 8);
-  uint32_t* seg_begin = ws;
-  uint32_t* seg_end = ws + H;
-  uint32_t* dst_cnt = ws + 2 * (size_t)H;
-  uint32_t* cur = ws + 3 * (size_t)H;
-  uint32_t* big_count = ws + 4 * (size_t)H;
-  uint32_t* err = big_count + 1;
-  unsigned long long* dstats = ctx->d_misc.get<unsigned long long>(4);
+  w.seg_begin = ws;
+  w.seg_end = ws + H;
+  w.dst_cnt = ws + 2 * (size_t)H;
+  w.cur = ws + 3 * (size_t)H;
+  w.big_count = ws + 4 * (size_t)H;
+  w.err = w.big_count + 1;
+  w.stats = ctx->d_misc.get<unsigned long long>(4);
+  w.dst_host = ctx->d_dst.get<uint32_t>(P);
+  w.ctr_start = want_ctr_start ? ctx->d_ctr0.get<uint64_t>(H) : nullptr;
   SG_HIP(hipMemsetAsync(ws, 0, (4 * (size_t)H + 8) * 4, st));
-  SG_HIP(hipMemsetAsync(dstats, 0, 8, st));
-  SG_HIP(hipMemsetAsync(dstats + 1, 0xff, 16, st));
-  uint32_t* dst_host = ctx->d_dst.get<uint32_t>(P);
-  uint64_t* kt = ctx->d_keys.get<uint64_t>(P);
-  uint32_t* ki = ctx->d_vals.get<uint32_t>(P);
-  uint32_t* big_list = ctx->d_lists.get<uint32_t>(H);
-  if (P) {
-    {
-      TimedLaunch tl(ctx, "seg_bounds", 4.0 * P + 8.0 * H);
-      hipLaunchKernelGGL(k_seg_bounds, dim3(grid_for(P, 256, 16384)), dim3(256), 0, st, pk->src_host, P,
-                         H, seg_begin, seg_end, err);
-    }
-    WalkArgs a;
-    a.src = pk->src_host;
-    a.dst_ip = pk->dst_ipv4;
-    a.payload = pk->payload_len;
-    a.send = pk->send_time_ns;
-    a.P = P;
-    a.H = H;
-    a.seg_begin = seg_begin;
-    a.seg_end = seg_end;
-    a.route = hs->route;
-    a.rng = hs->rng;
-    a.ctr = hs->ctr;
-    a.map = HostMap{hs->ip_base, hs->dense_span, hs->n, hs->dense, hs->sorted_ip, hs->sorted_host};
-    a.tab_lat = tab->latency_ns;
-    a.tab_loss = tab->packet_loss;
-    a.n_cols = tab->n_cols;
-    a.row_begin = tab->row_begin;
-    a.n_rows = tab->n_rows;
-    a.round_end = rd->round_end_ns;
-    a.sim_end = rd->sim_end_ns;
-    a.bootstrap_end = rd->bootstrap_end_ns;
-    a.status = out->status;
-    a.deliver = out->deliver_time_ns;
-    a.eid = out->event_id;
-    a.dst_host = dst_host;
-    a.dst_cnt = dst_cnt;
-    a.stats = dstats;
-    a.err = err;
-    {
-      // per packet: 20 B in, 12 B path gather, 4 B dst map, 21 B out (status, time, id), 4 B dst scratch;
-      // per host: 8 B segment, 4 B route, 32+32 B RNG, 8+8 B event counter
-      TimedLaunch tl(ctx, "walk", 61.0 * P + 92.0 * H);
-      hipLaunchKernelGGL(k_walk, dim3(grid_for(H, 256)), dim3(256), 0, st, a);
-    }
-    SG_CHECK_LAUNCH();
-  }
+  SG_HIP(hipMemsetAsync(w.stats, 0, 8, st));
+  SG_HIP(hipMemsetAsync(w.stats + 1, 0xff, 16, st));
+  if (w.ctr_start) SG_HIP(hipMemcpyAsync(w.ctr_start, hs->ctr, (size_t)H * 8, hipMemcpyDeviceToDevice, st));
+  if (!P) return w;
   {
-    TimedLaunch tl(ctx, "scan", 8.0 * H);
-    exclusive_scan_u32(ctx, dst_cnt, out->dst_offsets, H);
+    TimedLaunch tl(ctx, "seg_bounds", 4.0 * P + 8.0 * H);
+    hipLaunchKernelGGL(k_seg_bounds, dim3(grid_for(P, 256, 16384)), dim3(256), 0, st, pk->src_host, P, H,
+                       w.seg_begin, w.seg_end, w.err);
   }
-  if (P) {
-    {
-      TimedLaunch tl(ctx, "scatter", 24.0 * P);
-      hipLaunchKernelGGL(k_scatter, dim3(grid_for(P, 256, 16384)), dim3(256), 0, st, dst_host,
-                         out->deliver_time_ns, P, out->dst_offsets, cur, kt, ki);
-    }
-    {
-      TimedLaunch tl(ctx, "sort_small", 16.0 * P + 8.0 * H);
-      hipLaunchKernelGGL(k_sort_small, dim3(grid_for(H, 256)), dim3(256), 0, st, out->dst_offsets, H, kt,
-                         ki, out->dst_order, big_list, big_count);
-    }
-    uint64_t* kt2 = ctx->d_keys2.get<uint64_t>(P);
-    uint32_t* ki2 = ctx->d_vals2.get<uint32_t>(P);
-    {
-      TimedLaunch tl(ctx, "sort_big", 0.0);
-      hipLaunchKernelGGL(k_sort_big, dim3(std::min<uint32_t>(H, 2048)), dim3(SORT_BLOCK), 0, st,
-                         out->dst_offsets, big_list, big_count, kt, ki, kt2, ki2, out->dst_order);
-    }
-    SG_CHECK_LAUNCH();
+  WalkArgs a;
+  a.src = pk->src_host;
+  a.dst_ip = pk->dst_ipv4;
+  a.payload = pk->payload_len;
+  a.send = pk->send_time_ns;
+  a.P = P;
+  a.H = H;
+  a.seg_begin = w.seg_begin;
+  a.seg_end = w.seg_end;
+  a.route = hs->route;
+  a.rng = hs->rng;
+  a.ctr = hs->ctr;
+  a.map = HostMap{hs->ip_base, hs->dense_span, hs->n, hs->dense, hs->sorted_ip, hs->sorted_host};
+  a.tab_lat = tab->latency_ns;
+  a.tab_loss = tab->packet_loss;
+  a.n_cols = tab->n_cols;
+  a.row_begin = tab->row_begin;
+  a.n_rows = tab->n_rows;
+  a.round_end = rd->round_end_ns;
+  a.sim_end = rd->sim_end_ns;
+  a.bootstrap_end = rd->bootstrap_end_ns;
+  a.status = status;
+  a.deliver = deliver;
+  a.eid = eid;
+  a.dst_host = w.dst_host;
+  a.dst_cnt = w.dst_cnt;
+  a.stats = w.stats;
+  a.err = w.err;
+  {
+    // per packet: 20 B in, 12 B path gather, 4 B dst map, 21 B out (status, time, id), 4 B dst scratch;
+    // per host: 8 B segment, 4 B route, 32+32 B RNG, 8+8 B event counter
+    TimedLaunch tl(ctx, "walk", 61.0 * P + 92.0 * H);
+    hipLaunchKernelGGL(k_walk, dim3(grid_for(H, 256)), dim3(256), 0, st, a);
   }
+  SG_CHECK_LAUNCH();
+  return w;
+}
+
+static void finish(sg_ctx* ctx, const RoundWork& w, sg_round_stats* stats) {
   struct {
     unsigned long long s[3];
     uint32_t err;
   } h;
-  SG_HIP(hipMemcpyAsync(h.s, dstats, 24, hipMemcpyDeviceToHost, st));
-  SG_HIP(hipMemcpyAsync(&h.err, err, 4, hipMemcpyDeviceToHost, st));
+  hipStream_t st = ctx->stream;
+  SG_HIP(hipMemcpyAsync(h.s, w.stats, 24, hipMemcpyDeviceToHost, st));
+  SG_HIP(hipMemcpyAsync(&h.err, w.err, 4, hipMemcpyDeviceToHost, st));
   SG_HIP(hipStreamSynchronize(st));
   fail_flags(h.err);
   if (stats) {
@@ -460,6 +555,86 @@ static void deliver_round(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const 
     stats->min_deliver_time_ns = h.s[1];
     stats->min_used_latency_ns = h.s[2];
   }
+}
+
+static void deliver_round(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const sg_round* rd,
+                          const sg_packets* pk, sg_deliveries* out, sg_round_stats* stats) {
+  hipStream_t st = ctx->stream;
+  const uint32_t P = pk->n_packets, H = hs->n;
+  RoundWork w = source_phase(ctx, hs, tab, rd, pk, out->status, out->deliver_time_ns, out->event_id, false);
+  {
+    TimedLaunch tl(ctx, "scan", 8.0 * H);
+    exclusive_scan_u32(ctx, w.dst_cnt, out->dst_offsets, H);
+  }
+  if (P) {
+    uint64_t* kt = ctx->d_keys.get<uint64_t>(P);
+    uint64_t* kk = ctx->d_keys4.get<uint64_t>(P);
+    uint32_t* ki = ctx->d_vals.get<uint32_t>(P);
+    {
+      TimedLaunch tl(ctx, "scatter", 32.0 * P);
+      hipLaunchKernelGGL(k_scatter, dim3(grid_for(P, 256, 16384)), dim3(256), 0, st, w.dst_host,
+                         out->deliver_time_ns, P, out->dst_offsets, w.cur, kt, kk, ki);
+    }
+    sort_buckets(ctx, out->dst_offsets, H, P, kt, kk, ki, out->dst_order, w.big_count);
+  }
+  finish(ctx, w, stats);
+}
+
+static void deliver_source(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const sg_round* rd,
+                           const sg_packets* pk, uint8_t* status, uint64_t* deliver, uint64_t* eid,
+                           const uint32_t* owner, uint32_t n_ranks, sg_record* send, uint32_t* send_counts,
+                           sg_round_stats* stats) {
+  hipStream_t st = ctx->stream;
+  const uint32_t P = pk->n_packets;
+  RoundWork w = source_phase(ctx, hs, tab, rd, pk, status, deliver, eid, true);
+  const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(grid_for(P, PACK_BLOCK * 8), 2048));
+  uint32_t* bc = ctx->d_cnt.get<uint32_t>((size_t)n_ranks * nb + 1);
+  uint32_t* bo = ctx->d_scan.get<uint32_t>((size_t)n_ranks * nb + 1);
+  SG_HIP(hipMemsetAsync(bc, 0, ((size_t)n_ranks * nb + 1) * 4, st));
+  if (P) {
+    TimedLaunch tl(ctx, "pack", 4.0 * P + 32.0 * P);
+    hipLaunchKernelGGL(k_owner_count, dim3(nb), dim3(PACK_BLOCK), 0, st, w.dst_host, P, owner, n_ranks, bc);
+  }
+  exclusive_scan_u32(ctx, bc, bo, n_ranks * nb);
+  if (P) {
+    hipLaunchKernelGGL(k_owner_scatter, dim3(nb), dim3(PACK_BLOCK), 0, st, pk->src_host, w.dst_host, deliver, eid,
+                       w.ctr_start, P, owner, n_ranks, bo, send);
+    SG_CHECK_LAUNCH();
+  }
+  std::vector<uint32_t> starts((size_t)n_ranks * nb + 1);
+  SG_HIP(hipMemcpyAsync(starts.data(), bo, starts.size() * 4, hipMemcpyDeviceToHost, st));
+  finish(ctx, w, stats);  // synchronises the stream
+  for (uint32_t r = 0; r < n_ranks; r++) send_counts[r] = starts[(size_t)(r + 1) * nb] - starts[(size_t)r * nb];
+}
+
+static void deliver_bucket(sg_ctx* ctx, const sg_record* recv, uint32_t n, const uint32_t* local, uint32_t H,
+                           uint32_t n_local, uint32_t* order, uint32_t* offsets) {
+  hipStream_t st = ctx->stream;
+  uint32_t* ws = ctx->d_seg.get<uint32_t>(2 * (size_t)n_local + 8);
+  uint32_t* cnt = ws;
+  uint32_t* cur = ws + n_local;
+  uint32_t* big_count = ws + 2 * (size_t)n_local;
+  uint32_t* err = big_count + 1;
+  SG_HIP(hipMemsetAsync(ws, 0, (2 * (size_t)n_local + 8) * 4, st));
+  if (n) {
+    TimedLaunch tl(ctx, "rec_count", 36.0 * n);
+    hipLaunchKernelGGL(k_rec_count, dim3(grid_for(n, 256, 16384)), dim3(256), 0, st, recv, n, local, H, cnt, err);
+  }
+  exclusive_scan_u32(ctx, cnt, offsets, n_local);
+  if (n) {
+    uint64_t* kt = ctx->d_keys.get<uint64_t>(n);
+    uint64_t* kk = ctx->d_keys4.get<uint64_t>(n);
+    uint32_t* ki = ctx->d_vals.get<uint32_t>(n);
+    {
+      TimedLaunch tl(ctx, "rec_scatter", 56.0 * n);
+      hipLaunchKernelGGL(k_rec_scatter, dim3(grid_for(n, 256, 16384)), dim3(256), 0, st, recv, n, local, H, offsets,
+                         cur, kt, kk, ki);
+    }
+    sort_buckets(ctx, offsets, n_local, n, kt, kk, ki, order, big_count);
+  }
+  uint32_t h_err = 0;
+  copy_to_host(ctx, &h_err, err, 4);
+  fail_flags(h_err);
 }
 
 }  // namespace sg
@@ -590,6 +765,40 @@ int32_t sg_deliver_round(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table, co
          !table->latency_ns || !table->packet_loss))
       throw Error(SG_ERR_INVALID_ARG, "null packet or output array");
     deliver_round(ctx, hosts, table, round, packets, out, stats);
+  });
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int32_t sg_deliver_source(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table, const sg_round* round,
+                          const sg_packets* packets, uint8_t* status, uint64_t* deliver_time_ns,
+                          uint64_t* event_id, const uint32_t* host_owner, uint32_t n_ranks, sg_record* send,
+                          uint32_t* send_counts, sg_round_stats* stats) {
+  return sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (!hosts || hosts->ctx != ctx || !table || !round || !packets || !host_owner || !send_counts)
+      throw Error(SG_ERR_INVALID_ARG, "null argument");
+    if (n_ranks == 0 || n_ranks > MAX_RANKS) throw Error(SG_ERR_INVALID_ARG, "n_ranks must be in [1, 64]");
+    if (hosts->n && hosts->max_route >= table->n_cols)
+      throw Error(SG_ERR_INVALID_ARG, "a host's routing index is outside the table's columns");
+    if (packets->n_packets &&
+        (!packets->src_host || !packets->dst_ipv4 || !packets->payload_len || !packets->send_time_ns || !status ||
+         !deliver_time_ns || !event_id || !send || !table->latency_ns || !table->packet_loss))
+      throw Error(SG_ERR_INVALID_ARG, "null packet or output array");
+    deliver_source(ctx, hosts, table, round, packets, status, deliver_time_ns, event_id, host_owner, n_ranks, send,
+                   send_counts, stats);
+  });
+}
+
+int32_t sg_deliver_bucket(sg_ctx* ctx, const sg_record* recv, uint32_t n_records, const uint32_t* host_local,
+                          uint32_t n_hosts, uint32_t n_local_hosts, uint32_t* dst_order, uint32_t* dst_offsets) {
+  return sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (!host_local || !dst_offsets || (n_records && (!recv || !dst_order)))
+      throw Error(SG_ERR_INVALID_ARG, "null argument");
+    deliver_bucket(ctx, recv, n_records, host_local, n_hosts, n_local_hosts, dst_order, dst_offsets);
   });
 }
 

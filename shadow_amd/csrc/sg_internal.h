@@ -85,7 +85,8 @@ struct sg_ctx {
   sg::DevBuf r_dist, r_dist2, r_flags, r_used, r_err, r_pair_cnt, r_pair_edge, r_map, r_out_lat,
       r_out_loss, r_misc;
   // delivery workspace
-  sg::DevBuf d_seg, d_dst, d_cnt, d_cur, d_keys, d_vals, d_keys2, d_vals2, d_misc, d_scan, d_lists;
+  sg::DevBuf d_seg, d_dst, d_cnt, d_cur, d_keys, d_vals, d_keys2, d_vals2, d_keys3, d_keys4, d_misc,
+      d_scan, d_lists, d_ctr0;
   sg::DevBuf m_scratch;
   // kernel timers (off unless sg_ctx_enable_timers)
   bool timing = false;

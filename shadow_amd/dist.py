@@ -1,0 +1,154 @@
+"""Multi-GPU sharding of the network core: one process per GPU, RCCL over xGMI.
+
+Routing build: source rows are independent problems.  Rank r computes rows
+`row_range(n_used, world, r)`; the graph (a few MB) is replicated.  When a
+replicated table is wanted, the row blocks are all-gathered (equal block sizes,
+padded), otherwise each rank keeps its shard -- which is all delivery needs,
+because a packet only reads its source host's row.
+
+Delivery: hosts are owned by the rank that holds their routing row
+(`HostPartition`).  Each round:
+  1. source phase on every rank (sg_deliver_source): the send_packet half for
+     the packets its hosts sent, records packed by destination owner;
+  2. all-to-all of the per-rank record counts, then of the records
+     (32 B each; torch.distributed "nccl" = RCCL);
+  3. destination phase (sg_deliver_bucket): per-destination EventQueue order.
+The phases are injectable so the exchange logic is testable on CPU (gloo).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+from . import _capi
+from ._capi import check, load
+
+NONE = 0xFFFFFFFF
+RECORD_DTYPE = np.dtype([("deliver_time_ns", "<u8"), ("order_key", "<u8"), ("event_id", "<u8"),
+                         ("packet", "<u4"), ("dst_host", "<u4")])
+assert RECORD_DTYPE.itemsize == 32
+
+
+def row_range(n_used: int, world: int, rank: int):
+    """Contiguous, equal-size (last one short) row block of `rank`."""
+    per = (n_used + world - 1) // max(world, 1)
+    return min(rank * per, n_used), min((rank + 1) * per, n_used), per
+
+
+class HostPartition:
+    """owner[h] = rank holding host h's routing row; local[h] = slot on its owner."""
+
+    def __init__(self, host_route: Sequence[int], n_used: int, world: int):
+        route = np.asarray(host_route, dtype=np.int64)
+        per = (n_used + world - 1) // max(world, 1)
+        self.world = world
+        self.owner = (route // per).astype(np.uint32)
+        self.hosts_of = [np.nonzero(self.owner == r)[0].astype(np.uint32) for r in range(world)]
+        self.local = np.full(len(route), NONE, np.uint32)
+        for r in range(world):
+            self.local[self.hosts_of[r]] = np.arange(len(self.hosts_of[r]), dtype=np.uint32)
+
+    def n_local(self, rank: int) -> int:
+        return len(self.hosts_of[rank])
+
+
+# ---------------------------------------------------------------------------
+# GPU phases (libshadow_gpu.so)
+# ---------------------------------------------------------------------------
+@dataclass
+class SourceResult:
+    status: object           # uint8 device tensor
+    deliver_time_ns: object  # int64 device tensor
+    event_id: object         # int64 device tensor
+    send: object             # int64 device tensor [n, 4] (sg_record)
+    send_counts: List[int]
+    n_delivered: int
+    min_deliver_time_ns: int
+    min_used_latency_ns: int
+
+
+def gpu_source_phase(ctx, hosts, table, packets, round_end_ns, sim_end_ns, bootstrap_end_ns, owner_dev,
+                     n_ranks) -> SourceResult:
+    import torch
+
+    n = len(packets)
+    dev = packets.src_host.device
+    status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    deliver = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    eid = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    send = torch.empty((max(n, 1), 4), dtype=torch.int64, device=dev)
+    counts = (C.c_uint32 * n_ranks)()
+    p = _capi.sg_packets()
+    p.n_packets = n
+    p.src_host, p.dst_ipv4 = packets.src_host.data_ptr(), packets.dst_ipv4.data_ptr()
+    p.payload_len, p.send_time_ns = packets.payload_len.data_ptr(), packets.send_time_ns.data_ptr()
+    r = _capi.sg_round(round_end_ns, sim_end_ns, bootstrap_end_ns)
+    st = _capi.sg_round_stats()
+    t = table.struct()
+    check(ctx.handle, load().sg_deliver_source(ctx.handle, hosts.handle, C.byref(t), C.byref(r), C.byref(p),
+                                               status.data_ptr(), deliver.data_ptr(), eid.data_ptr(),
+                                               owner_dev.data_ptr(), n_ranks, send.data_ptr(), counts,
+                                               C.byref(st)))
+    return SourceResult(status, deliver, eid, send, list(counts), st.n_delivered, st.min_deliver_time_ns,
+                        st.min_used_latency_ns)
+
+
+def gpu_bucket_phase(ctx, recv, n_records: int, local_dev, n_hosts: int, n_local: int):
+    import torch
+
+    dev = local_dev.device
+    order = torch.empty(max(n_records, 1), dtype=torch.int32, device=dev)
+    offsets = torch.empty(n_local + 1, dtype=torch.int32, device=dev)
+    check(ctx.handle, load().sg_deliver_bucket(ctx.handle, recv.data_ptr() if n_records else None, n_records,
+                                               local_dev.data_ptr(), n_hosts, n_local, order.data_ptr(),
+                                               offsets.data_ptr()))
+    return order[:n_records], offsets
+
+
+# ---------------------------------------------------------------------------
+# Exchange
+# ---------------------------------------------------------------------------
+def all_to_all_records(send, send_counts: List[int], dist, group=None):
+    """Counts exchange, then one all_to_all_single of the 32-B records."""
+    import torch
+
+    world = len(send_counts)
+    dev = send.device
+    sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
+    rc = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = [int(x) for x in rc.cpu()]
+    n_recv = sum(recv_counts)
+    recv = torch.empty((max(n_recv, 1), 4), dtype=torch.int64, device=dev)
+    n_send = sum(send_counts)
+    dist.all_to_all_single(recv[:n_recv], send[:n_send], output_split_sizes=recv_counts,
+                           input_split_sizes=list(send_counts), group=group)
+    return recv[:n_recv], recv_counts
+
+
+class ShardedDelivery:
+    """One rank's side of a sharded delivery round (see module docstring)."""
+
+    def __init__(self, ctx, hosts, table, partition: HostPartition, rank: int, world: int, dist=None, group=None,
+                 source_fn: Optional[Callable] = None, bucket_fn: Optional[Callable] = None,
+                 exchange_fn: Optional[Callable] = None, device="cuda"):
+        self.ctx, self.hosts, self.table, self.part = ctx, hosts, table, partition
+        self.rank, self.world, self.dist, self.group = rank, world, dist, group
+        self.source_fn = source_fn or gpu_source_phase
+        self.bucket_fn = bucket_fn or gpu_bucket_phase
+        self.exchange_fn = exchange_fn or (lambda send, counts: all_to_all_records(send, counts, dist, group))
+        import torch
+
+        self.owner_dev = torch.from_numpy(partition.owner.view(np.int32)).to(device)
+        self.local_dev = torch.from_numpy(partition.local.view(np.int32)).to(device)
+
+    def round(self, packets, round_end_ns: int, sim_end_ns: int, bootstrap_end_ns: int = 0):
+        src = self.source_fn(self.ctx, self.hosts, self.table, packets, round_end_ns, sim_end_ns, bootstrap_end_ns,
+                             self.owner_dev, self.world)
+        recv, recv_counts = self.exchange_fn(src.send, src.send_counts)
+        order, offsets = self.bucket_fn(self.ctx, recv, int(sum(recv_counts)), self.local_dev,
+                                        len(self.part.local), self.part.n_local(self.rank))
+        return src, recv, recv_counts, order, offsets

@@ -1,0 +1,153 @@
+"""World-size-2 gloo tests of the sharding logic on CPU.
+
+The exchange code (`shadow_amd.dist.all_to_all_records`, `ShardedDelivery`) and
+the row partition are the real product code; the GPU phases are replaced by
+numpy/oracle stand-ins written here (the kernels themselves are covered by
+tests/test_dist_gpu.py on the GPU box).  The merged result must equal a single
+oracle round over all packets, and gathered row shards the full table.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from shadow_amd import synth
+from shadow_amd.dist import HostPartition, RECORD_DTYPE, ShardedDelivery, SourceResult, row_range
+
+T0 = 946684800 * 10**9
+NONE = 0xFFFFFFFF
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _world(O):
+    g = synth.ring_chords_graph(60, 6.0, seed=2)
+    rc, lat, loss, _ = O.shortest_paths(60, g["src"], g["dst"], g["lat"], g["loss"], False, np.arange(60), threads=2)
+    assert rc == 0
+    loss = loss.copy()
+    loss[::2, 1::2] = np.float32(0.35)
+    hosts = synth.make_hosts(400, 60, general_seed=4)
+    pk = synth.make_packets(12000, hosts, T0, T0 + 10**6, seed=8, p_unknown_dst=0.02)
+    return g, lat, loss, hosts, pk
+
+
+class _Tables:
+    """Stand-in for the device state of one rank (test-side only)."""
+
+    def __init__(self, O, hosts):
+        self.rng = np.stack([O.xoshiro_seed(int(s)) for s in hosts["seed"]]).astype(np.uint64)
+        self.ctr = np.zeros(hosts["n"], np.uint64)
+
+
+def _cpu_source(O, lat, loss, hosts, state, part):
+    def fn(ctx, h, table, packets, round_end, sim_end, boot, owner_dev, n_ranks):
+        src, dst_ip, pay, t = packets
+        ctr0 = state.ctr.copy()
+        res = O.deliver_round(round_end, sim_end, boot, src, dst_ip, pay, t, hosts["ip"], hosts["route"], lat, loss,
+                              state.rng, state.ctr)
+        ip2h = {int(ip): k for k, ip in enumerate(hosts["ip"])}
+        recs = []
+        for i in np.nonzero(res["status"] == O.ST_DELIVERED)[0]:
+            s, d = int(src[i]), ip2h[int(dst_ip[i])]
+            k = int(res["event_id"][i] - ctr0[s])
+            recs.append((int(res["deliver_time"][i]), (s << 32) | k, int(res["event_id"][i]), int(i), d))
+        recs = np.array(recs, dtype=RECORD_DTYPE) if recs else np.zeros(0, RECORD_DTYPE)
+        own = part.owner[recs["dst_host"]]
+        recs = recs[np.argsort(own, kind="stable")]
+        counts = [int((own == r).sum()) for r in range(n_ranks)]
+        send = torch.from_numpy(recs.view(np.int64).reshape(-1, 4).copy())
+        return SourceResult(res["status"], res["deliver_time"], res["event_id"], send, counts, res["delivered"],
+                            res["min_deliver"], res["min_lat"])
+    return fn
+
+
+def _cpu_bucket(part, rank):
+    def fn(ctx, recv, n, local_dev, n_hosts, n_local):
+        rec = recv.numpy().view(RECORD_DTYPE).ravel()[:n]
+        slot = part.local[rec["dst_host"]]
+        assert (part.owner[rec["dst_host"]] == rank).all()
+        order = np.lexsort((rec["order_key"], rec["deliver_time_ns"], slot)).astype(np.uint32)
+        offsets = np.zeros(n_local + 1, np.uint32)
+        np.add.at(offsets, slot + 1, 1)
+        return order, np.cumsum(offsets).astype(np.uint32)
+    return fn
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from oracle import oracle as O
+
+        g, lat, loss, hosts, pk = _world(O)
+        nu = lat.shape[0]
+        # --- routing rows: each rank its block, all-gathered ---
+        r0, r1, per = row_range(nu, world, rank)
+        rc, mine, _, _ = O.shortest_paths(60, g["src"], g["dst"], g["lat"], g["loss"], False, np.arange(60),
+                                          rows=(r0, r1))
+        block = np.zeros((per, nu), np.uint64)
+        block[: r1 - r0] = mine
+        full = torch.zeros(world * per * nu, dtype=torch.int64)
+        dist.all_gather_into_tensor(full, torch.from_numpy(block.view(np.int64).ravel()))
+        gathered = full.numpy().view(np.uint64).reshape(world * per, nu)[:nu]
+        rows_ok = bool(np.array_equal(gathered, lat))
+        # --- sharded delivery ---
+        part = HostPartition(hosts["route"], nu, world)
+        sel = np.nonzero(part.owner[pk["src"]] == rank)[0]
+        state = _Tables(O, hosts)
+        sd = ShardedDelivery(None, None, None, part, rank, world, dist=dist, device="cpu",
+                             source_fn=_cpu_source(O, lat, loss, hosts, state, part),
+                             bucket_fn=_cpu_bucket(part, rank))
+        packets = (pk["src"][sel], pk["dst_ip"][sel], pk["payload"][sel], pk["send_time"][sel])
+        src, recv, recv_counts, order, offsets = sd.round(packets, T0 + 10**6, 2**63, 0)
+        rec = recv.numpy().view(RECORD_DTYPE).ravel()
+        # map records back to global packet indices: sender r's selection
+        sels = [np.nonzero(part.owner[pk["src"]] == r)[0] for r in range(world)]
+        origin = np.repeat(np.arange(world), recv_counts)
+        glob = np.array([sels[origin[k]][rec["packet"][k]] for k in range(len(rec))], np.int64)
+        per_dst = {int(h): glob[order[offsets[s]:offsets[s + 1]]].tolist() for s, h in enumerate(part.hosts_of[rank])}
+        q.put((rank, rows_ok, per_dst, src.status.tolist(), sel.tolist()))
+        dist.destroy_process_group()
+    except Exception as e:  # surface worker failures to the parent
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc(), None, None))
+
+
+def test_two_rank_gloo_exchange_matches_single_round(oracle):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for o in out:
+        assert o[1] != "error", o[2]
+    g, lat, loss, hosts, pk = _world(oracle)
+    rng = np.stack([oracle.xoshiro_seed(int(s)) for s in hosts["seed"]]).astype(np.uint64)
+    ctr = np.zeros(hosts["n"], np.uint64)
+    want = oracle.deliver_round(T0 + 10**6, 2**63, 0, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
+                                hosts["ip"], hosts["route"], lat, loss, rng, ctr)
+    seen = set()
+    for rank, rows_ok, per_dst, status, sel in out:
+        assert rows_ok
+        assert np.array_equal(np.array(status, np.uint8), want["status"][np.array(sel, np.int64)])
+        for h, got in per_dst.items():
+            exp = want["dst_order"][want["dst_offsets"][h]:want["dst_offsets"][h + 1]].tolist()
+            assert got == exp, h
+            seen.add(h)
+    assert seen == set(range(hosts["n"]))

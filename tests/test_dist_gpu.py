@@ -1,0 +1,106 @@
+"""GPU parity of the sharded delivery kernels (sg_deliver_source / sg_deliver_bucket).
+
+W ranks are emulated in one process on one GPU: each rank holds its routing
+row shard and runs the source phase for the hosts it owns; the exchange is a
+concatenation (the all-to-all itself is covered by tests/test_dist_cpu.py with
+gloo).  The result must equal one oracle round over all packets.
+"""
+import numpy as np
+import pytest
+
+from shadow_amd import synth
+from shadow_amd.dist import HostPartition, RECORD_DTYPE, ShardedDelivery, row_range
+from shadow_amd.worker import DeviceTable, HostTable, PacketBatch
+
+pytestmark = pytest.mark.gpu
+T0 = 946684800 * 10**9
+
+
+def _world(oracle, n_nodes=90, n_hosts=1500, seed=3):
+    g = synth.ring_chords_graph(n_nodes, 6.0, seed=seed)
+    used = np.arange(n_nodes, dtype=np.uint32)
+    rc, lat, loss, _ = oracle.shortest_paths(n_nodes, g["src"], g["dst"], g["lat"], g["loss"], False, used, threads=8)
+    assert rc == 0
+    loss = loss.copy()
+    loss[1::2, ::3] = np.float32(0.4)
+    hosts = synth.make_hosts(n_hosts, n_nodes, general_seed=seed)
+    return lat, loss, hosts
+
+
+def _run(oracle, ctx, W, n_packets, hot=None, seed=1):
+    import torch
+
+    lat, loss, hosts = _world(oracle, seed=seed)
+    nu = lat.shape[0]
+    part = HostPartition(hosts["route"], nu, W)
+    start, end = T0 + 10**9, T0 + 10**9 + 10**6
+    pk = synth.make_packets(n_packets, hosts, start, end, seed=seed + 10, p_unknown_dst=0.01,
+                            hot_dst=-1 if hot is None else hot, p_hot=0.0 if hot is None else 0.1)
+    owner_of_pkt = part.owner[pk["src"]]
+    ranks = []
+    for r in range(W):
+        r0, r1, per = row_range(nu, W, r)
+        sel = np.nonzero(owner_of_pkt == r)[0]
+        ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+        dl = torch.from_numpy(np.ascontiguousarray(lat[r0:r1]).view(np.int64).ravel()).cuda()
+        df = torch.from_numpy(np.ascontiguousarray(loss[r0:r1]).ravel()).cuda()
+        table = DeviceTable(dl, df, nu, r0)
+        batch = PacketBatch.from_numpy(pk["src"][sel], pk["dst_ip"][sel], pk["payload"][sel], pk["send_time"][sel])
+        ranks.append(dict(sel=sel, ht=ht, table=table, batch=batch))
+    # source phases
+    sends = []
+    for r, R in enumerate(ranks):
+        sd = ShardedDelivery(ctx, R["ht"], R["table"], part, r, W)
+        src = sd.source_fn(ctx, R["ht"], R["table"], R["batch"], end, 2**63, start + 200_000, sd.owner_dev, W)
+        R["src"], R["sd"] = src, sd
+        sends.append(src)
+    # exchange by concatenation: rank d receives segment d of every sender, in sender order
+    results = []
+    for d, R in enumerate(ranks):
+        parts, origin = [], []
+        for s, src in enumerate(sends):
+            off = int(sum(src.send_counts[:d]))
+            cnt = src.send_counts[d]
+            parts.append(src.send[off:off + cnt])
+            origin += [s] * cnt
+        recv = torch.cat(parts) if parts else torch.empty((0, 4), dtype=torch.int64, device="cuda")
+        order, offsets = R["sd"].bucket_fn(ctx, recv.contiguous(), recv.shape[0], R["sd"].local_dev,
+                                           len(part.local), part.n_local(d))
+        results.append((recv, np.array(origin, np.int64), order, offsets))
+    # oracle over all packets
+    ht0 = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    rng, ctr = ht0.get_state()
+    want = oracle.deliver_round(end, 2**63, start + 200_000, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
+                                hosts["ip"], hosts["route"], lat, loss, rng, ctr)
+    # per-packet outputs + host streams
+    for r, R in enumerate(ranks):
+        sel = R["sel"]
+        assert np.array_equal(R["src"].status[:len(sel)].cpu().numpy(), want["status"][sel])
+        assert np.array_equal(R["src"].deliver_time_ns[:len(sel)].cpu().numpy().view(np.uint64), want["deliver_time"][sel])
+        assert np.array_equal(R["src"].event_id[:len(sel)].cpu().numpy().view(np.uint64), want["event_id"][sel])
+        grng, gctr = R["ht"].get_state()
+        mine = part.hosts_of[r]
+        assert np.array_equal(grng[mine], rng[mine]) and np.array_equal(gctr[mine], ctr[mine])
+    # per-destination order
+    for d, (recv, origin, order, offsets) in enumerate(results):
+        rec = recv.cpu().numpy().view(RECORD_DTYPE).ravel() if recv.shape[0] else np.zeros(0, RECORD_DTYPE)
+        offs = offsets.cpu().numpy().view(np.uint32)
+        ordr = order.cpu().numpy().view(np.uint32)
+        glob = np.array([ranks[origin[k]]["sel"][rec["packet"][k]] for k in range(len(rec))], np.int64)
+        for slot, h in enumerate(part.hosts_of[d]):
+            got = glob[ordr[offs[slot]:offs[slot + 1]]]
+            exp = want["dst_order"][want["dst_offsets"][h]:want["dst_offsets"][h + 1]]
+            assert np.array_equal(got, exp), (d, h)
+        assert np.array_equal(rec["event_id"], want["event_id"][glob])
+        assert np.array_equal(rec["deliver_time_ns"], want["deliver_time"][glob])
+    return want
+
+
+@pytest.mark.parametrize("W", [1, 2, 3, 8])
+def test_sharded_round_matches_single(oracle, ctx, W):
+    want = _run(oracle, ctx, W, 30000)
+    assert want["delivered"] > 0
+
+
+def test_sharded_hot_destination(oracle, ctx):
+    _run(oracle, ctx, 4, 120000, hot=17, seed=5)
