@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output into profiles/ JSON.
+
+  kernel stats : rocprofv3 --kernel-trace --stats --output-format csv -d DIR -- python bench.py ...
+  PMC passes   : rocprofv3 --pmc FETCH_SIZE  --output-format csv -d DIR_F -- python bench.py ...
+                 rocprofv3 --pmc WRITE_SIZE  --output-format csv -d DIR_W -- python bench.py ...
+
+    python tools/pmc_summary.py --stats DIR --fetch DIR_F --write DIR_W -o profiles/pmc_r01.json
+
+Per kernel: average FETCH_SIZE / WRITE_SIZE per dispatch (rocprofv3 reports KB),
+HBM bytes per launch = (FETCH_SIZE * 2 + WRITE_SIZE) * 1024, where the x2 is the
+gfx950 correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE reads half the bytes of
+a wide coalesced stream; calibrated for 16-B/lane loads -- our 8-B/lane gathers
+are uncalibrated, so the raw value is kept beside it).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+KERNELS = {"relax_packed": "k_relax_packed", "out_packed": "k_out_packed", "walk": "k_walk",
+           "scatter": "k_scatter", "sort_small": "k_sort_small", "sort_big": "k_sort_big",
+           "seg_bounds": "k_seg_bounds", "relax_wide": "k_relax_wide"}
+
+
+def _rows(d, pattern):
+    out = []
+    for f in glob.glob(os.path.join(d, "**", pattern), recursive=True):
+        with open(f) as fh:
+            out += list(csv.DictReader(fh))
+    return out
+
+
+def short(name):
+    for k, v in KERNELS.items():
+        if v in name:
+            return k
+    return None
+
+
+def counter_avgs(d, counter):
+    acc = defaultdict(list)
+    for r in _rows(d, "*counter_collection.csv"):
+        if r.get("Counter_Name") != counter:
+            continue
+        k = short(r.get("Kernel_Name", ""))
+        if k:
+            acc[k].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def stats(d):
+    res = {}
+    for r in _rows(d, "*kernel_stats.csv"):
+        k = short(r.get("Name", ""))
+        if k:
+            res[k] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "total_ns": float(r["TotalDurationNs"]),
+                      "pct": float(r.get("Percentage", 0) or 0)}
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stats")
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("-o", "--out", required=True)
+    a = ap.parse_args()
+    out = {}
+    st = stats(a.stats) if a.stats else {}
+    fe = counter_avgs(a.fetch, "FETCH_SIZE") if a.fetch else {}
+    wr = counter_avgs(a.write, "WRITE_SIZE") if a.write else {}
+    for k in sorted(set(st) | set(fe) | set(wr)):
+        e = {}
+        if k in st:
+            e.update(st[k])
+        if k in fe:
+            e["fetch_kb_raw"] = fe[k]
+        if k in wr:
+            e["write_kb"] = wr[k]
+        if k in fe and k in wr:
+            e["hbm_bytes_per_launch"] = (2 * fe[k] + wr[k]) * 1024
+            e["hbm_bytes_per_launch_raw"] = (fe[k] + wr[k]) * 1024
+        out[k] = e
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
