@@ -137,6 +137,12 @@ TimedLaunch::TimedLaunch(sg_ctx* c, const char* name, double work) : ctx(c) {
   SG_HIP(hipEventRecord(e0, ctx->stream));
 }
 
+void timer_add_work(sg_ctx* ctx, const char* name, double work) {
+  if (!ctx->timing) return;
+  for (auto& kv : ctx->timers)
+    if (kv.first == name) kv.second.work += work;
+}
+
 TimedLaunch::~TimedLaunch() {
   if (!timer) return;
   (void)hipEventRecord(e1, ctx->stream);

@@ -83,7 +83,7 @@ struct sg_ctx {
   uint32_t err_row = 0, err_col = 0;
   // routing workspace
   sg::DevBuf r_dist, r_dist2, r_flags, r_used, r_err, r_pair_cnt, r_pair_edge, r_map, r_out_lat,
-      r_out_loss, r_misc;
+      r_out_loss, r_misc, r_dirty, r_work;
   // delivery workspace
   sg::DevBuf d_seg, d_dst, d_cnt, d_cur, d_keys, d_vals, d_keys2, d_vals2, d_keys3, d_keys4, d_misc,
       d_scan, d_lists, d_ctr0;
@@ -134,6 +134,9 @@ void exclusive_scan_u32(sg_ctx* ctx, const uint32_t* d_in, uint32_t* d_out, uint
 
 // Read a few scalars back (blocking on the context stream).
 void copy_to_host(sg_ctx* ctx, void* dst, const void* src, size_t bytes);
+
+// Add algorithmic work to a timer after the fact (e.g. a device-side count).
+void timer_add_work(sg_ctx* ctx, const char* name, double work);
 
 // RAII bracket for one instrumented launch: `TimedLaunch t(ctx, "k_walk", work);`
 // before the launch; the end event is recorded when `t` goes out of scope.

@@ -103,110 +103,160 @@ __global__ void k_scatter_arcs(const uint32_t* __restrict__ src, const uint32_t*
 }
 
 // ---------------------------------------------------------------------------
-// Packed-key batched relaxation.
+// Packed-key batched relaxation, B sources per batch.
+//
+// Slab layout D[batch][node][B] (u64 keys).  With B = 32 a batch's slab is
+// n x 256 B -- 2.56 MB at n = 10k, inside one XCD's 4 MB L2.  A wave owns
+// G = 64 / B destination nodes (one per B-lane group; lane % B = source).
+//
+// XCD-aware 1-D grid: dispatch deals blocks round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md, "Workgroup dispatch"), so block L runs on XCD L % 8.
+// Block L serves batch (L % 8) + 8 * ((L / 8) / nvb) and node chunk
+// (L / 8) % nvb: every block of a batch lands on the same XCD, whose L2 then
+// holds the batch's slab.  Placement changes speed only, never results.
+//
+// Frontier: dirty[batch][node] bytes mark nodes whose key changed in the
+// previous pass (dprev) or earlier in this pass (dcur, read racily).  Arc
+// (u -> v) is relaxed only if u is dirty.  Exactness: every change of u sets
+// dcur[u]; in the next pass every out-neighbour re-reads u (across a kernel
+// boundary, so the value is visible), and the iteration stops only after a
+// pass with no change anywhere -- which is then the fixed point.
 // ---------------------------------------------------------------------------
-__global__ void k_init_packed(uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ used,
-                              uint32_t first_row, uint32_t row_end, uint32_t n_batches) {
-  size_t total = (size_t)n_batches * n * BATCH;
+struct BatchMap {
+  uint32_t nvb, n_batches;
+  __device__ __forceinline__ bool decode(uint32_t L, uint32_t& batch, uint32_t& chunk) const {
+    const uint32_t x = L & 7, k = L >> 3;
+    batch = x + 8 * (k / nvb);
+    chunk = k % nvb;
+    return batch < n_batches;
+  }
+};
+
+template <int B>
+__global__ void k_init_front(uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ used,
+                             uint32_t first_row, uint32_t row_end, uint32_t n_batches) {
+  const size_t total = (size_t)n_batches * n * B;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (size_t)gridDim.x * blockDim.x) {
-    uint32_t lane = (uint32_t)(i & (BATCH - 1));
-    size_t bv = i / BATCH;
-    uint32_t v = (uint32_t)(bv % n);
-    uint32_t b = (uint32_t)(bv / n);
-    uint32_t row = first_row + b * BATCH + lane;
+    const uint32_t s = (uint32_t)(i % B);
+    const size_t bv = i / B;
+    const uint32_t v = (uint32_t)(bv % n);
+    const uint32_t b = (uint32_t)(bv / n);
+    const uint32_t row = first_row + b * B + s;
     D[i] = (row < row_end && used[row] == v) ? 0ull : KEY_INF;  // PathProperties::default()
   }
 }
 
-template <int VPW>
-__global__ void __launch_bounds__(RELAX_BLOCK)
-    k_relax_packed(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
-                   const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om,
-                   uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ active,
-                   uint32_t* __restrict__ changed) {
-  const uint32_t b = blockIdx.y;
-  if (!active[b]) return;
-  uint64_t* __restrict__ Db = D + (size_t)b * n * BATCH;
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  bool any = false;
-  const uint32_t v0 = (blockIdx.x * RELAX_WAVES + wave) * VPW;
-#pragma unroll 1
-  for (int k = 0; k < VPW; k++) {
-    const uint32_t v = v0 + k;
-    if (v >= n) break;
-    const uint32_t a0 = in_off[v], a1 = in_off[v + 1];
-    const uint64_t cur = Db[(size_t)v * BATCH + lane];
-    uint64_t best = cur;
-    uint32_t a = a0;
-    // 4 independent 512-B row reads in flight per wave
-    for (; a + 4 <= a1; a += 4) {
-      uint32_t u0 = in_src[a], u1 = in_src[a + 1], u2 = in_src[a + 2], u3 = in_src[a + 3];
-      uint64_t k0 = Db[(size_t)u0 * BATCH + lane];
-      uint64_t k1 = Db[(size_t)u1 * BATCH + lane];
-      uint64_t k2 = Db[(size_t)u2 * BATCH + lane];
-      uint64_t k3 = Db[(size_t)u3 * BATCH + lane];
-      uint64_t l0 = min(in_lat[a], LAT_SAT), l1 = min(in_lat[a + 1], LAT_SAT);
-      uint64_t l2 = min(in_lat[a + 2], LAT_SAT), l3 = min(in_lat[a + 3], LAT_SAT);
-      float o0 = in_om[a], o1 = in_om[a + 1], o2 = in_om[a + 2], o3 = in_om[a + 3];
-      uint64_t c0 = k0 == KEY_INF ? KEY_INF : relax_key(k0, l0, o0);
-      uint64_t c1 = k1 == KEY_INF ? KEY_INF : relax_key(k1, l1, o1);
-      uint64_t c2 = k2 == KEY_INF ? KEY_INF : relax_key(k2, l2, o2);
-      uint64_t c3 = k3 == KEY_INF ? KEY_INF : relax_key(k3, l3, o3);
-      best = min(best, min(min(c0, c1), min(c2, c3)));
-    }
-    for (; a < a1; a++) {
-      uint32_t u = in_src[a];
-      uint64_t ku = Db[(size_t)u * BATCH + lane];
-      uint64_t c = ku == KEY_INF ? KEY_INF : relax_key(ku, min(in_lat[a], LAT_SAT), in_om[a]);
-      best = min(best, c);
-    }
-    if (best < cur) {
-      Db[(size_t)v * BATCH + lane] = best;  // one untorn 64-bit (lat, loss) update
-      any = true;
-    }
-  }
-  if (__any(any) && lane == 0) atomicOr(&changed[b], 1u);
+template <int B>
+__global__ void k_mark_sources(uint8_t* __restrict__ dirty, uint32_t n, const uint32_t* __restrict__ used,
+                               uint32_t first_row, uint32_t row_end, uint32_t n_batches) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_batches * B) return;
+  const uint32_t b = t / B, row = first_row + t;
+  if (row < row_end) dirty[(size_t)b * n + used[row]] = 1;
 }
 
-// Transposed write-out of a [64 rows x 64 cols] tile.  Diagonal = raw
+template <int B, int VPW>
+__global__ void __launch_bounds__(RELAX_BLOCK)
+    k_relax_front(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
+                  const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om, uint64_t* D,
+                  uint32_t n, BatchMap map, const uint32_t* __restrict__ active,
+                  uint32_t* __restrict__ changed, const uint8_t* dprev, uint8_t* dcur,
+                  unsigned long long* __restrict__ work) {
+  constexpr int G = 64 / B;
+  uint32_t b, chunk;
+  if (!map.decode(blockIdx.x, b, chunk) || !active[b]) return;
+  uint64_t* Db = D + (size_t)b * n * B;
+  const uint8_t* Pf = dprev + (size_t)b * n;
+  uint8_t* Cf = dcur + (size_t)b * n;
+  const int lane = threadIdx.x & 63;
+  const int g = lane / B, s = lane % B;
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint64_t gmask = (B == 64) ? ~0ull : (((1ull << (B & 63)) - 1) << (g * B));
+  bool any = false;
+  uint32_t n_relax = 0;  // dirty arcs relaxed by this lane
+  const uint32_t base = (chunk * RELAX_WAVES + wave) * (G * VPW);
+#pragma unroll 1
+  for (int k = 0; k < VPW; k++) {
+    const uint32_t v = base + k * G + g;
+    const bool valid = v < n;
+    const uint32_t a0 = valid ? in_off[v] : 0, a1 = valid ? in_off[v + 1] : 0;
+    const uint64_t cur = valid ? Db[(size_t)v * B + s] : KEY_INF;
+    uint64_t best = cur;
+    uint32_t a = a0;
+    for (; a + 4 <= a1; a += 4) {  // four arcs' rows in flight per lane group
+      const uint32_t u0 = in_src[a], u1 = in_src[a + 1], u2 = in_src[a + 2], u3 = in_src[a + 3];
+      const bool f0 = Pf[u0] | Cf[u0], f1 = Pf[u1] | Cf[u1], f2 = Pf[u2] | Cf[u2], f3 = Pf[u3] | Cf[u3];
+      uint64_t k0 = KEY_INF, k1 = KEY_INF, k2 = KEY_INF, k3 = KEY_INF;
+      n_relax += (uint32_t)f0 + (uint32_t)f1 + (uint32_t)f2 + (uint32_t)f3;
+      if (f0) k0 = Db[(size_t)u0 * B + s];
+      if (f1) k1 = Db[(size_t)u1 * B + s];
+      if (f2) k2 = Db[(size_t)u2 * B + s];
+      if (f3) k3 = Db[(size_t)u3 * B + s];
+      if (k0 != KEY_INF) best = min(best, relax_key(k0, min(in_lat[a], LAT_SAT), in_om[a]));
+      if (k1 != KEY_INF) best = min(best, relax_key(k1, min(in_lat[a + 1], LAT_SAT), in_om[a + 1]));
+      if (k2 != KEY_INF) best = min(best, relax_key(k2, min(in_lat[a + 2], LAT_SAT), in_om[a + 2]));
+      if (k3 != KEY_INF) best = min(best, relax_key(k3, min(in_lat[a + 3], LAT_SAT), in_om[a + 3]));
+    }
+    for (; a < a1; a++) {
+      const uint32_t u = in_src[a];
+      if (!(Pf[u] | Cf[u])) continue;
+      n_relax++;
+      const uint64_t ku = Db[(size_t)u * B + s];
+      if (ku != KEY_INF) best = min(best, relax_key(ku, min(in_lat[a], LAT_SAT), in_om[a]));
+    }
+    const bool ch = valid && best < cur;
+    if (ch) Db[(size_t)v * B + s] = best;  // one untorn 64-bit (lat, loss) update
+    const uint64_t m = __ballot(ch) & gmask;
+    if (m && s == 0) Cf[v] = 1;
+    any |= ch;
+  }
+  if (__any(any) && lane == 0) atomicOr(&changed[b], 1u);
+  unsigned long long wsum = n_relax;
+  for (int d = 32; d > 0; d >>= 1) wsum += __shfl_xor(wsum, d, 64);
+  if (lane == 0 && wsum) atomicAdd(work, wsum);
+}
+
+// Transposed write-out of [B rows x 64 cols] tiles.  Diagonal = the raw
 // self-loop (graph/mod.rs:210-217).  Saturated keys flag their batch.
+template <int B>
 __global__ void __launch_bounds__(256)
-    k_out_packed(const uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ used,
-                 uint32_t n_used, uint32_t first_row, uint32_t row_end, uint32_t out_row0,
-                 const uint32_t* __restrict__ self_edge, const uint64_t* __restrict__ e_lat,
-                 const float* __restrict__ e_loss, uint64_t* __restrict__ out_lat,
-                 float* __restrict__ out_loss, uint32_t* __restrict__ sat) {
-  __shared__ uint64_t tile[64][65];
+    k_out_front(const uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ used,
+                uint32_t n_used, uint32_t first_row, uint32_t row_end, uint32_t out_row0,
+                const uint32_t* __restrict__ self_edge, const uint64_t* __restrict__ e_lat,
+                const float* __restrict__ e_loss, uint64_t* __restrict__ out_lat,
+                float* __restrict__ out_loss, uint32_t* __restrict__ sat) {
+  constexpr int G = 64 / B;
+  __shared__ uint64_t tile[64][B + 1];
   const uint32_t b = blockIdx.y;
   const uint32_t j0 = blockIdx.x * 64;
-  const uint64_t* __restrict__ Db = D + (size_t)b * n * BATCH;
+  const uint64_t* __restrict__ Db = D + (size_t)b * n * B;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int c = wave; c < 64; c += 4) {
-    uint32_t j = j0 + c;
-    tile[c][lane] = j < n_used ? Db[(size_t)used[j] * BATCH + lane] : 0ull;
+  const int g = lane / B, s = lane % B;
+  for (int c = wave * G + g; c < 64; c += 4 * G) {
+    const uint32_t j = j0 + c;
+    tile[c][s] = j < n_used ? Db[(size_t)used[j] * B + s] : 0ull;
   }
   __syncthreads();
-  bool s = false;
+  bool sflag = false;
   const uint32_t j = j0 + lane;
-  for (int r = wave; r < 64; r += 4) {
-    uint32_t row = first_row + b * BATCH + r;
+  for (int r = wave; r < B; r += 4) {
+    const uint32_t row = first_row + b * B + r;
     if (row >= row_end || j >= n_used) continue;
-    size_t o = (size_t)(row - out_row0) * n_used + j;
+    const size_t o = (size_t)(row - out_row0) * n_used + j;
     if (row == j) {
-      uint32_t e = self_edge[used[j]];
+      const uint32_t e = self_edge[used[j]];
       out_lat[o] = e_lat[e];
       out_loss[o] = e_loss[e];
     } else {
-      uint64_t k = tile[lane][r];
-      uint64_t lat = key_lat(k);
-      s |= lat >= LAT_SAT;
+      const uint64_t kk = tile[lane][r];
+      const uint64_t lat = key_lat(kk);
+      sflag |= lat >= LAT_SAT;
       out_lat[o] = lat;
-      out_loss[o] = __uint_as_float(key_loss_bits(k));
+      out_loss[o] = __uint_as_float(key_loss_bits(kk));
     }
   }
-  if (__any(s) && lane == 0) atomicOr(&sat[b], 1u);
+  if (__any(sflag) && lane == 0) atomicOr(&sat[b], 1u);
 }
 
 // ---------------------------------------------------------------------------
@@ -504,59 +554,80 @@ static void run_wide(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t 
 static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                            uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
                            float* out_loss) {
+  constexpr int B = 32;    // sources per batch: slab = n x 256 B (L2-resident per XCD at 10k nodes)
+  constexpr int VPW = 4;   // destination nodes per lane group, walked sequentially
+  constexpr int G = 64 / B;
   hipStream_t st = ctx->stream;
   const uint32_t n = net->n_nodes;
   const uint32_t n_rows = row_end - row_begin;
-  const uint32_t n_batches = (n_rows + BATCH - 1) / BATCH;
-  // Group size: batches whose slabs (n x 512 B each) are live together.
-  size_t slab_bytes = (size_t)n * BATCH * 8;
-  size_t budget = (size_t)env_int("SG_APSP_GROUP_MB", 2048) << 20;
-  uint32_t group = (uint32_t)std::max<size_t>(1, std::min<size_t>(n_batches, budget / slab_bytes));
-  constexpr int VPW = 4;
-  const uint32_t nvb = (n + RELAX_WAVES * VPW - 1) / (RELAX_WAVES * VPW);
-  uint64_t* D = ctx->r_dist.get<uint64_t>((size_t)group * n * BATCH);
+  const uint32_t n_batches = (n_rows + B - 1) / B;
+  // Group size: batches whose slabs are live together (bounded device memory).
+  const size_t slab_bytes = (size_t)n * B * 8;
+  const size_t budget = (size_t)env_int("SG_APSP_GROUP_MB", 4096) << 20;
+  const uint32_t group = (uint32_t)std::max<size_t>(1, std::min<size_t>(n_batches, budget / slab_bytes));
+  const uint32_t nvb = (n + RELAX_WAVES * G * VPW - 1) / (RELAX_WAVES * G * VPW);
+  uint64_t* D = ctx->r_dist.get<uint64_t>((size_t)group * n * B);
   uint32_t* flags = ctx->r_flags.get<uint32_t>((size_t)group * 3 + 8);  // [active | changed | sat]
   uint32_t* sat = flags + 2 * (size_t)group;
+  uint8_t* dirty = ctx->r_dirty.get<uint8_t>(2 * (size_t)group * n);
+  uint8_t* dirtyA[2] = {dirty, dirty + (size_t)group * n};
+  unsigned long long* work = ctx->r_work.get<unsigned long long>(2);
+  SG_HIP(hipMemsetAsync(work, 0, 8, st));
   std::vector<uint32_t> h_changed(group), h_sat(group);
   std::vector<uint32_t> wide_rows;
   for (uint32_t g0 = 0; g0 < n_batches; g0 += group) {
     const uint32_t gb = std::min(group, n_batches - g0);
-    const uint32_t first_row = row_begin + g0 * BATCH;
-    hipLaunchKernelGGL(k_init_packed, dim3(grid_for((size_t)gb * n * BATCH, 256, 65536)), dim3(256),
-                       0, st, D, n, d_used, first_row, row_end, gb);
+    const uint32_t first_row = row_begin + g0 * B;
+    hipLaunchKernelGGL(k_init_front<B>, dim3(grid_for((size_t)gb * n * B, 256, 65536)), dim3(256), 0, st, D, n,
+                       d_used, first_row, row_end, gb);
+    SG_HIP(hipMemsetAsync(dirty, 0, 2 * (size_t)gb * n, st));
+    dirtyA[1] = dirty + (size_t)gb * n;
+    hipLaunchKernelGGL(k_mark_sources<B>, dim3(grid_for((size_t)gb * B, 256)), dim3(256), 0, st, dirtyA[1], n,
+                       d_used, first_row, row_end, gb);
     SG_CHECK_LAUNCH();
     uint32_t* active = flags;
     uint32_t* changed = flags + group;
     SG_HIP(hipMemsetAsync(active, 1, gb * 4ull, st));  // nonzero = active
-    uint32_t n_active = gb;
+    const BatchMap map{nvb, gb};
+    const uint32_t grid = 8 * nvb * ((gb + 7) / 8);
     for (uint32_t pass = 0;; pass++) {
       if (pass > n + 2) throw Error(SG_ERR_DEVICE, "relaxation did not converge");
+      uint8_t* dcur = dirtyA[pass & 1];
+      const uint8_t* dprev = dirtyA[(pass & 1) ^ 1];
       SG_HIP(hipMemsetAsync(changed, 0, gb * 4ull, st));
+      if (pass) SG_HIP(hipMemsetAsync(dcur, 0, (size_t)gb * n, st));
       {
-        TimedLaunch tl(ctx, "relax_packed", (double)n_active * BATCH * net->n_arcs);
-        hipLaunchKernelGGL(k_relax_packed<VPW>, dim3(nvb, gb), dim3(RELAX_BLOCK), 0, st, net->in_off,
-                           net->in_src, net->in_lat, net->in_om, D, n, active, changed);
+        TimedLaunch tl(ctx, "relax_packed", 0.0);
+        hipLaunchKernelGGL((k_relax_front<B, VPW>), dim3(grid), dim3(RELAX_BLOCK), 0, st, net->in_off,
+                           net->in_src, net->in_lat, net->in_om, D, n, map, active, changed, dprev, dcur, work);
       }
       SG_CHECK_LAUNCH();
       copy_to_host(ctx, h_changed.data(), changed, gb * 4ull);
-      n_active = 0;
+      uint32_t n_active = 0;
       for (uint32_t b = 0; b < gb; b++) n_active += h_changed[b] != 0;
       if (!n_active) break;
       std::swap(active, changed);
     }
     SG_HIP(hipMemsetAsync(sat, 0, gb * 4ull, st));
-    TimedLaunch tl(ctx, "out_packed", 12.0 * std::min<uint32_t>(gb * BATCH, row_end - first_row) * n_used);
-    hipLaunchKernelGGL(k_out_packed, dim3((n_used + 63) / 64, gb), dim3(256), 0, st, D, n, d_used,
-                       n_used, first_row, row_end, row_begin, net->self_edge, net->e_lat,
-                       net->e_loss, out_lat, out_loss, sat);
+    {
+      TimedLaunch tl(ctx, "out_packed", 12.0 * std::min<uint32_t>(gb * B, row_end - first_row) * n_used);
+      hipLaunchKernelGGL(k_out_front<B>, dim3((n_used + 63) / 64, gb), dim3(256), 0, st, D, n, d_used, n_used,
+                         first_row, row_end, row_begin, net->self_edge, net->e_lat, net->e_loss, out_lat,
+                         out_loss, sat);
+    }
     SG_CHECK_LAUNCH();
     copy_to_host(ctx, h_sat.data(), sat, gb * 4ull);
     for (uint32_t b = 0; b < gb; b++)
       if (h_sat[b])
-        for (uint32_t r = 0; r < BATCH; r++) {
-          uint32_t row = first_row + b * BATCH + r;
+        for (uint32_t r = 0; r < B; r++) {
+          uint32_t row = first_row + b * B + r;
           if (row < row_end) wide_rows.push_back(row);
         }
+  }
+  if (ctx->timing) {  // relaxations actually performed (dirty arcs x lanes), for the roofline
+    unsigned long long w = 0;
+    copy_to_host(ctx, &w, work, 8);
+    timer_add_work(ctx, "relax_packed", (double)w);
   }
   if (!wide_rows.empty()) run_wide(ctx, net, d_used, n_used, wide_rows, row_begin, out_lat, out_loss);
 }

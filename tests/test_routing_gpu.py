@@ -90,6 +90,14 @@ def test_random_sparse(oracle, ctx, directed, seed):
     _check(oracle, g, used, ctx)
 
 
+def test_multiple_batch_groups(oracle, ctx, monkeypatch):
+    """A tiny slab budget forces several sequential batch groups (and partial XCD groups)."""
+    monkeypatch.setenv("SG_APSP_GROUP_MB", "1")
+    g = synth.ring_chords_graph(1500, 6.0, seed=13)
+    used = np.random.default_rng(13).permutation(1500)[:700].astype(np.uint32)
+    _check(oracle, g, used, ctx)
+
+
 def test_complete_graph(oracle, ctx):
     g = synth.complete_graph(300, seed=3)
     _check(oracle, g, np.arange(300, dtype=np.uint32), ctx)
