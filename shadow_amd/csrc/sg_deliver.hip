@@ -230,32 +230,57 @@ __device__ __forceinline__ bool key_less(uint64_t ta, uint64_t ka, uint64_t tb, 
   return ta < tb || (ta == tb && ka < kb);
 }
 
-// Thread per destination: insertion sort of a small bucket; big buckets are
-// queued for k_sort_big.
-__global__ void k_sort_small(const uint32_t* __restrict__ off, uint32_t H, uint64_t* __restrict__ kt,
-                             uint64_t* __restrict__ kk, uint32_t* __restrict__ ki,
-                             uint32_t* __restrict__ order, uint32_t* __restrict__ big_list,
-                             uint32_t* __restrict__ big_count) {
-  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < H; h += gridDim.x * blockDim.x) {
-    const uint32_t b = off[h], e = off[h + 1];
-    if (e - b > SMALL_BUCKET) {
-      big_list[atomicAdd(big_count, 1u)] = h;
-      continue;
+// Block of 256 destinations: their buckets are contiguous, so the block loads
+// the whole range into LDS with coalesced reads, each thread insertion-sorts
+// its bucket in LDS, and the block writes dst_order back coalesced.  Buckets
+// above SMALL_BUCKET are queued for k_sort_big; a block whose range does not
+// fit in LDS sorts its small buckets in place in global memory instead.
+constexpr int SMALL_LDS = 3072;  // entries staged per block (60 KB of LDS)
+
+__device__ __forceinline__ void insertion_sort(uint64_t* t_, uint64_t* k_, uint32_t* i_, uint32_t b,
+                                               uint32_t e) {
+  for (uint32_t i = b + 1; i < e; i++) {
+    const uint64_t t = t_[i], k = k_[i];
+    const uint32_t x = i_[i];
+    uint32_t j = i;
+    while (j > b && key_less(t, k, t_[j - 1], k_[j - 1])) {
+      t_[j] = t_[j - 1];
+      k_[j] = k_[j - 1];
+      i_[j] = i_[j - 1];
+      j--;
     }
-    for (uint32_t i = b + 1; i < e; i++) {
-      uint64_t t = kt[i], k = kk[i];
-      uint32_t x = ki[i];
-      uint32_t j = i;
-      while (j > b && key_less(t, k, kt[j - 1], kk[j - 1])) {
-        kt[j] = kt[j - 1];
-        kk[j] = kk[j - 1];
-        ki[j] = ki[j - 1];
-        j--;
-      }
-      kt[j] = t;
-      kk[j] = k;
-      ki[j] = x;
+    t_[j] = t;
+    k_[j] = k;
+    i_[j] = x;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+    k_sort_small(const uint32_t* __restrict__ off, uint32_t H, uint64_t* __restrict__ kt,
+                 uint64_t* __restrict__ kk, uint32_t* __restrict__ ki, uint32_t* __restrict__ order,
+                 uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
+  __shared__ uint64_t st[SMALL_LDS];
+  __shared__ uint64_t sk[SMALL_LDS];
+  __shared__ uint32_t si[SMALL_LDS];
+  const uint32_t h0 = blockIdx.x * 256;
+  const uint32_t h = h0 + threadIdx.x;
+  const uint32_t r0 = off[h0], r1 = off[min(h0 + 256, H)];
+  const bool mine = h < H;
+  const uint32_t b = mine ? off[h] : r1, e = mine ? off[h + 1] : r1;
+  const bool big = e - b > SMALL_BUCKET;
+  if (mine && big) big_list[atomicAdd(big_count, 1u)] = h;
+  if (r1 - r0 <= SMALL_LDS) {
+    for (uint32_t i = r0 + threadIdx.x; i < r1; i += 256) {
+      st[i - r0] = kt[i];
+      sk[i - r0] = kk[i];
+      si[i - r0] = ki[i];
     }
+    __syncthreads();
+    if (mine && !big) insertion_sort(st, sk, si, b - r0, e - r0);
+    __syncthreads();
+    for (uint32_t i = r0 + threadIdx.x; i < r1; i += 256) order[i] = si[i - r0];  // big ranges rewritten later
+  } else if (mine && !big) {
+    insertion_sort(kt, kk, ki, b, e);
     for (uint32_t i = b; i < e; i++) order[i] = ki[i];
   }
 }
@@ -453,7 +478,7 @@ static void sort_buckets(sg_ctx* ctx, const uint32_t* off, uint32_t n_buckets, u
   uint32_t* big_list = ctx->d_lists.get<uint32_t>(n_buckets);
   {
     TimedLaunch tl(ctx, "sort_small", 24.0 * n_entries + 8.0 * n_buckets);
-    hipLaunchKernelGGL(k_sort_small, dim3(grid_for(n_buckets, 256)), dim3(256), 0, st, off, n_buckets, kt, kk,
+    hipLaunchKernelGGL(k_sort_small, dim3((n_buckets + 255) / 256 ? (n_buckets + 255) / 256 : 1), dim3(256), 0, st, off, n_buckets, kt, kk,
                        ki, order, big_list, big_count);
   }
   uint64_t* kt2 = ctx->d_keys2.get<uint64_t>(n_entries);
