@@ -567,12 +567,17 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
   const uint32_t group = (uint32_t)std::max<size_t>(1, std::min<size_t>(n_batches, budget / slab_bytes));
   const uint32_t nvb = (n + RELAX_WAVES * G * VPW - 1) / (RELAX_WAVES * G * VPW);
   uint64_t* D = ctx->r_dist.get<uint64_t>((size_t)group * n * B);
-  uint32_t* flags = ctx->r_flags.get<uint32_t>((size_t)group * 3 + 8);  // [active | changed | sat]
-  uint32_t* sat = flags + 2 * (size_t)group;
+  // per-batch flags: a 3-slot ring of "changed in pass p" arrays, then the saturation flags
+  uint32_t* flags = ctx->r_flags.get<uint32_t>((size_t)group * 4 + 8);
+  uint32_t* ring[3] = {flags, flags + group, flags + 2 * (size_t)group};
+  uint32_t* sat = flags + 3 * (size_t)group;
   uint8_t* dirty = ctx->r_dirty.get<uint8_t>(2 * (size_t)group * n);
   uint8_t* dirtyA[2] = {dirty, dirty + (size_t)group * n};
   unsigned long long* work = ctx->r_work.get<unsigned long long>(2);
   SG_HIP(hipMemsetAsync(work, 0, 8, st));
+  // Passes are issued in chunks; the host reads the convergence flags once per
+  // chunk.  A pass issued after its batch converged exits at once (active == 0).
+  const uint32_t chunk = (uint32_t)std::max(1, env_int("SG_APSP_PASS_CHUNK", 4));
   std::vector<uint32_t> h_changed(group), h_sat(group);
   std::vector<uint32_t> wide_rows;
   for (uint32_t g0 = 0; g0 < n_batches; g0 += group) {
@@ -585,28 +590,31 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
     hipLaunchKernelGGL(k_mark_sources<B>, dim3(grid_for((size_t)gb * B, 256)), dim3(256), 0, st, dirtyA[1], n,
                        d_used, first_row, row_end, gb);
     SG_CHECK_LAUNCH();
-    uint32_t* active = flags;
-    uint32_t* changed = flags + group;
-    SG_HIP(hipMemsetAsync(active, 1, gb * 4ull, st));  // nonzero = active
+    SG_HIP(hipMemsetAsync(ring[2], 1, gb * 4ull, st));  // "changed in pass -1": every batch active
     const BatchMap map{nvb, gb};
     const uint32_t grid = 8 * nvb * ((gb + 7) / 8);
-    for (uint32_t pass = 0;; pass++) {
-      if (pass > n + 2) throw Error(SG_ERR_DEVICE, "relaxation did not converge");
-      uint8_t* dcur = dirtyA[pass & 1];
-      const uint8_t* dprev = dirtyA[(pass & 1) ^ 1];
-      SG_HIP(hipMemsetAsync(changed, 0, gb * 4ull, st));
-      if (pass) SG_HIP(hipMemsetAsync(dcur, 0, (size_t)gb * n, st));
-      {
-        TimedLaunch tl(ctx, "relax_packed", 0.0);
-        hipLaunchKernelGGL((k_relax_front<B, VPW>), dim3(grid), dim3(RELAX_BLOCK), 0, st, net->in_off,
-                           net->in_src, net->in_lat, net->in_om, D, n, map, active, changed, dprev, dcur, work);
+    for (uint32_t pass = 0;;) {
+      uint32_t last = pass;
+      for (uint32_t c = 0; c < chunk; c++, pass++) {
+        if (pass > n + 2 + chunk) throw Error(SG_ERR_DEVICE, "relaxation did not converge");
+        const uint32_t* active = ring[(pass + 2) % 3];
+        uint32_t* changed = ring[pass % 3];
+        uint8_t* dcur = dirtyA[pass & 1];
+        const uint8_t* dprev = dirtyA[(pass & 1) ^ 1];
+        SG_HIP(hipMemsetAsync(changed, 0, gb * 4ull, st));
+        if (pass) SG_HIP(hipMemsetAsync(dcur, 0, (size_t)gb * n, st));
+        {
+          TimedLaunch tl(ctx, "relax_packed", 0.0);
+          hipLaunchKernelGGL((k_relax_front<B, VPW>), dim3(grid), dim3(RELAX_BLOCK), 0, st, net->in_off,
+                             net->in_src, net->in_lat, net->in_om, D, n, map, active, changed, dprev, dcur, work);
+        }
+        SG_CHECK_LAUNCH();
+        last = pass;
       }
-      SG_CHECK_LAUNCH();
-      copy_to_host(ctx, h_changed.data(), changed, gb * 4ull);
+      copy_to_host(ctx, h_changed.data(), ring[last % 3], gb * 4ull);
       uint32_t n_active = 0;
       for (uint32_t b = 0; b < gb; b++) n_active += h_changed[b] != 0;
       if (!n_active) break;
-      std::swap(active, changed);
     }
     SG_HIP(hipMemsetAsync(sat, 0, gb * 4ull, st));
     {
