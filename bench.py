@@ -5,9 +5,12 @@
 
 Primary line (`value`): one routing-table build of the C3 workload (10k-node
 ring + chords, mean degree 8, every node used) -- seconds per
-build, rows sharded across ranks, RCCL all-gather of the row blocks when N > 1.
-`delivery` sub-object: one C4 delivery round (100k hosts, 1M packets) per step,
-packets/s.  Inputs are resident in HBM when the timed region starts.
+build, source rows sharded across ranks (rows are independent units; each rank
+keeps its row block, which is all delivery reads).  The optional RCCL all-gather
+that would replicate the table is timed separately (apsp_detail.allgather_ms).
+`delivery` sub-object: one C4 delivery round (100k hosts, 1M packets per rank)
+per step, packets/s; at N > 1 delivered records go to the destination's owner
+by RCCL all-to-all.  Inputs are resident in HBM when the timed region starts.
 
 Single GPU:  python bench.py [--steps K --warmup W]
 N GPUs:      python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -130,12 +133,15 @@ def main():
     my_loss = full_loss[D.rank * rows * nu:(D.rank + 1) * rows * nu]
 
     def build():
+        # rows are independent units: each rank keeps its row shard (delivery reads only its own rows)
         net.build_rows_device(used, r0, r1, my_lat.data_ptr(), my_loss.data_ptr(), True)
-        if D.dist:
-            D.dist.all_gather_into_tensor(full_lat, my_lat)
-            D.dist.all_gather_into_tensor(full_loss, my_loss)
+
+    def allgather():
+        D.dist.all_gather_into_tensor(full_lat, my_lat)
+        D.dist.all_gather_into_tensor(full_loss, my_loss)
 
     t_build = timed(D, build, a.steps, a.warmup)
+    t_allgather = timed(D, allgather, max(1, a.steps // 2), 1) if D.dist else 0.0
     # instrumented pass: per-kernel device time of the dominant kernel on its stream
     ctx.enable_timers(True)
     build()
@@ -174,10 +180,12 @@ def main():
         "data": "synthetic (seeded ring+chords graph, SURVEY §8d C3)",
         "config": {"workload": "C3 APSP routing build: 10k-node undirected ring+chords graph, mean degree 8, "
                                "latency U[1,100] ms (integer us), loss 0 w.p. 0.8 else U(0,0.02); all nodes used; "
-                               "source rows sharded across ranks" + (", RCCL all-gather" if D.world > 1 else ""),
+                               "source rows sharded across ranks (each rank keeps its row block; the optional RCCL "
+                               "all-gather of the blocks is timed separately in apsp_detail.allgather_ms)",
                    "nodes": a.nodes, "arcs": n_arcs, "parallelism": f"rows{D.world}"},
         "roofline": roofline, "cpu_baseline": cpu,
-        "apsp_detail": {"out_kernel_ms": round(out_ms, 4),
+        "apsp_detail": {"out_kernel_ms": round(out_ms, 4), "allgather_ms": round(t_allgather * 1e3, 4),
+                        "table_bytes": 12 * nu * nu,
                         "fw_equivalent_Tops": round(2.0 * nu * a.nodes ** 2 / t_build / 1e12, 2)},
     }
     if cpu:
@@ -185,25 +193,33 @@ def main():
 
     # ---------------- delivery round (C4) ----------------
     if not a.no_delivery:
+        from shadow_amd.dist import HostPartition, ShardedDelivery
+
         hosts = synth.make_hosts(a.hosts, a.nodes, general_seed=1, exact_seeds=True)
-        # weak scaling: each rank sends a.packets from the hosts whose node rows it owns
-        mine = np.nonzero((hosts["route"] >= r0) & (hosts["route"] < r1))[0]
-        sub = dict(n=len(mine), ip=hosts["ip"][mine], route=hosts["route"][mine], seed=hosts["seed"][mine])
-        pk = synth.make_packets(a.packets, sub, T0 + 10**9, T0 + 10**9 + 10**6, seed=100 + D.rank)
-        src_global = mine[pk["src"]].astype(np.uint32)
+        part = HostPartition(hosts["route"], nu, D.world)
+        mine = part.hosts_of[D.rank]
+        # weak scaling: each rank sends a.packets from the hosts it owns, to destinations anywhere
+        pk = synth.make_packets(a.packets, hosts, T0 + 10**9, T0 + 10**9 + 10**6, seed=100 + D.rank,
+                                src_hosts=mine)
         ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
         table = DeviceTable(my_lat, my_loss, nu, r0)
-        batch = PacketBatch.from_numpy(src_global, pk["dst_ip"], pk["payload"], pk["send_time"])
+        batch = PacketBatch.from_numpy(pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"])
+        src_global = pk["src"]
         out = Deliveries.allocate(a.packets, a.hosts)
         round_end, sim_end = T0 + 10**9 + 10**6, 2**63
+        sharded = ShardedDelivery(ctx, ht, table, part, D.rank, D.world, dist=D.dist) if D.world > 1 else None
 
         def rnd():
-            deliver_round(ht, table, batch, round_end, sim_end, 0, out=out, ctx=ctx)
+            if sharded:
+                sharded.round(batch, round_end, sim_end, 0)
+            else:
+                deliver_round(ht, table, batch, round_end, sim_end, 0, out=out, ctx=ctx)
 
         t_round = timed(D, rnd, a.steps, a.warmup)
         ctx.enable_timers(True)
         rnd()
-        kt = {k: ctx.read_timer(k) for k in ("seg_bounds", "walk", "scan", "scatter", "sort_small", "sort_big")}
+        kt = {k: ctx.read_timer(k) for k in ("seg_bounds", "walk", "scan", "scatter", "sort_small", "sort_big",
+                                             "pack", "rec_count", "rec_scatter")}
         ctx.enable_timers(False)
         walk_ms, walk_n, walk_bytes = kt["walk"]
         walk_s = walk_ms / 1e3 / max(walk_n, 1)
@@ -216,12 +232,15 @@ def main():
             "unit": "packets/s", "higher_is_better": True, "ms_per_round": round(t_round * 1e3, 4),
             "scaling": "weak", "dtype": "u64+f32+f64",
             "config": {"workload": "C4 delivery round: 100k hosts on the C3 graph (node h mod 10k), 1M packets per "
-                                   "rank, src-major, dst uniform != src, 20% zero-payload, send_time U[1 ms round)",
+                                   "rank from the hosts it owns, dst uniform over all hosts != src, 20% zero-payload, "
+                                   "send_time U[1 ms round)" + ("; records exchanged by RCCL all-to-all to the "
+                                                                "destination's owner" if D.world > 1 else ""),
                        "hosts": a.hosts, "packets_per_rank": a.packets},
             "roofline": {"kernel": "k_walk", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmw.get("hbm_bytes_per_launch"),
                          "avg_launch_ms": round(walk_s * 1e3, 4)},
             "round_hbm_GBs": round(round_bytes / t_round / 1e9, 1),
+            "parallelism": f"hosts{D.world}",
             "kernel_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in kt.items()},
         }
         if D.rank == 0 and D.world == 1 and not a.no_cpu:

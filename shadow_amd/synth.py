@@ -155,11 +155,19 @@ def make_hosts(n_hosts: int, n_nodes: int, general_seed: int = 1, exact_seeds: b
 
 
 def make_packets(n_packets: int, hosts, round_start: int, round_end: int, seed: int = 1,
-                 p_ack: float = 0.2, p_unknown_dst: float = 0.0, hot_dst: int = -1, p_hot: float = 0.0):
-    """C4 recipe: grouped by ascending source host, send_time ascending within a host."""
+                 p_ack: float = 0.2, p_unknown_dst: float = 0.0, hot_dst: int = -1, p_hot: float = 0.0,
+                 src_hosts=None):
+    """C4 recipe: grouped by ascending source host, send_time ascending within a host.
+
+    src_hosts: restrict senders to these host ids (a rank's own hosts); destinations stay global.
+    """
     rng = np.random.default_rng(seed)
     H = hosts["n"]
-    src = np.sort(rng.integers(0, H, n_packets)).astype(np.uint32)
+    if src_hosts is None:
+        src = np.sort(rng.integers(0, H, n_packets)).astype(np.uint32)
+    else:
+        src_hosts = np.sort(np.asarray(src_hosts, dtype=np.uint32))
+        src = np.sort(src_hosts[rng.integers(0, len(src_hosts), n_packets)]).astype(np.uint32)
     dst = rng.integers(0, H - 1, n_packets)
     dst = np.where(dst >= src, dst + 1, dst) if H > 1 else np.zeros(n_packets, np.int64)
     if hot_dst >= 0 and p_hot > 0:
