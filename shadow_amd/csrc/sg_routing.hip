@@ -60,6 +60,7 @@ namespace sg {
 constexpr int BATCH = 64;         // sources per batch = wave width
 constexpr int RELAX_WAVES = 4;    // waves per block
 constexpr int RELAX_BLOCK = RELAX_WAVES * 64;
+constexpr int WORK_SHARDS = 64;  // relaxation counter shards (measurement only)
 
 // ---------------------------------------------------------------------------
 // Graph upload: CSC of in-arcs (both directions when undirected, petgraph
@@ -211,10 +212,20 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
     if (m && s == 0) Cf[v] = 1;
     any |= ch;
   }
-  if (__any(any) && lane == 0) atomicOr(&changed[b], 1u);
-  unsigned long long wsum = n_relax;
-  for (int d = 32; d > 0; d >>= 1) wsum += __shfl_xor(wsum, d, 64);
-  if (lane == 0 && wsum) atomicAdd(work, wsum);
+  // every writer stores the same 1: a plain store, no same-address atomic storm
+  if (__any(any) && lane == 0) __hip_atomic_store(&changed[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (work) {  // measurement only (timers on): block reduction, one add per block into a sharded counter
+    __shared__ unsigned long long wblk[RELAX_WAVES];
+    unsigned long long wsum = n_relax;
+    for (int d = 32; d > 0; d >>= 1) wsum += __shfl_xor(wsum, d, 64);
+    if (lane == 0) wblk[wave] = wsum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long t = 0;
+      for (int w = 0; w < RELAX_WAVES; w++) t += wblk[w];
+      if (t) atomicAdd(&work[blockIdx.x & (WORK_SHARDS - 1)], t);
+    }
+  }
 }
 
 // Transposed write-out of [B rows x 64 cols] tiles.  Diagonal = the raw
@@ -573,8 +584,8 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
   uint32_t* sat = flags + 3 * (size_t)group;
   uint8_t* dirty = ctx->r_dirty.get<uint8_t>(2 * (size_t)group * n);
   uint8_t* dirtyA[2] = {dirty, dirty + (size_t)group * n};
-  unsigned long long* work = ctx->r_work.get<unsigned long long>(2);
-  SG_HIP(hipMemsetAsync(work, 0, 8, st));
+  unsigned long long* work = ctx->timing ? ctx->r_work.get<unsigned long long>(WORK_SHARDS) : nullptr;
+  if (work) SG_HIP(hipMemsetAsync(work, 0, WORK_SHARDS * 8, st));
   // Passes are issued in chunks; the host reads the convergence flags once per
   // chunk.  A pass issued after its batch converged exits at once (active == 0).
   const uint32_t chunk = (uint32_t)std::max(1, env_int("SG_APSP_PASS_CHUNK", 4));
@@ -632,10 +643,12 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
           if (row < row_end) wide_rows.push_back(row);
         }
   }
-  if (ctx->timing) {  // relaxations actually performed (dirty arcs x lanes), for the roofline
-    unsigned long long w = 0;
-    copy_to_host(ctx, &w, work, 8);
-    timer_add_work(ctx, "relax_packed", (double)w);
+  if (work) {  // relaxations actually performed (dirty arcs x lanes), for the roofline
+    unsigned long long w[WORK_SHARDS];
+    copy_to_host(ctx, w, work, sizeof(w));
+    double total = 0;
+    for (int k = 0; k < WORK_SHARDS; k++) total += (double)w[k];
+    timer_add_work(ctx, "relax_packed", total);
   }
   if (!wide_rows.empty()) run_wide(ctx, net, d_used, n_used, wide_rows, row_begin, out_lat, out_loss);
 }
