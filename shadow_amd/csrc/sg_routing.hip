@@ -61,6 +61,7 @@ constexpr int BATCH = 64;         // sources per batch = wave width
 constexpr int RELAX_WAVES = 4;    // waves per block
 constexpr int RELAX_BLOCK = RELAX_WAVES * 64;
 constexpr int WORK_SHARDS = 64;  // relaxation counter shards (measurement only)
+constexpr int ARC_CHUNK = 1024;  // in-arcs staged in LDS per block step
 
 // ---------------------------------------------------------------------------
 // Graph upload: CSC of in-arcs (both directions when undirected, petgraph
@@ -165,6 +166,14 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
                   uint32_t* __restrict__ changed, const uint8_t* dprev, uint8_t* dcur,
                   unsigned long long* __restrict__ work) {
   constexpr int G = 64 / B;
+  constexpr int NB = RELAX_WAVES * G * VPW;  // destination nodes per block
+  // Staged in-arcs of the block's nodes: source (bit 31 = source is dirty),
+  // clamped latency, 1 - loss.  Loaded coalesced, so the inner loop's only
+  // global access is the independent distance-row read of each dirty arc.
+  __shared__ uint32_t s_u[ARC_CHUNK];
+  __shared__ uint64_t s_lat[ARC_CHUNK];
+  __shared__ float s_om[ARC_CHUNK];
+  __shared__ unsigned long long wblk[RELAX_WAVES];
   uint32_t b, chunk;
   if (!map.decode(blockIdx.x, b, chunk) || !active[b]) return;
   uint64_t* Db = D + (size_t)b * n * B;
@@ -174,40 +183,66 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
   const int g = lane / B, s = lane % B;
   const uint32_t wave = threadIdx.x >> 6;
   const uint64_t gmask = (B == 64) ? ~0ull : (((1ull << (B & 63)) - 1) << (g * B));
-  bool any = false;
-  uint32_t n_relax = 0;  // dirty arcs relaxed by this lane
-  const uint32_t base = (chunk * RELAX_WAVES + wave) * (G * VPW);
-#pragma unroll 1
+  const uint32_t v0 = chunk * NB;
+  const uint32_t vq = v0 + (wave * G + g) * VPW;  // this lane group's first node
+  uint32_t lo[VPW], hi[VPW];
+  uint64_t cur[VPW], best[VPW];
+#pragma unroll
   for (int k = 0; k < VPW; k++) {
-    const uint32_t v = base + k * G + g;
+    const uint32_t v = vq + k;
     const bool valid = v < n;
-    const uint32_t a0 = valid ? in_off[v] : 0, a1 = valid ? in_off[v + 1] : 0;
-    const uint64_t cur = valid ? Db[(size_t)v * B + s] : KEY_INF;
-    uint64_t best = cur;
-    uint32_t a = a0;
-    for (; a + 4 <= a1; a += 4) {  // four arcs' rows in flight per lane group
-      const uint32_t u0 = in_src[a], u1 = in_src[a + 1], u2 = in_src[a + 2], u3 = in_src[a + 3];
-      const bool f0 = Pf[u0] | Cf[u0], f1 = Pf[u1] | Cf[u1], f2 = Pf[u2] | Cf[u2], f3 = Pf[u3] | Cf[u3];
-      uint64_t k0 = KEY_INF, k1 = KEY_INF, k2 = KEY_INF, k3 = KEY_INF;
-      n_relax += (uint32_t)f0 + (uint32_t)f1 + (uint32_t)f2 + (uint32_t)f3;
-      if (f0) k0 = Db[(size_t)u0 * B + s];
-      if (f1) k1 = Db[(size_t)u1 * B + s];
-      if (f2) k2 = Db[(size_t)u2 * B + s];
-      if (f3) k3 = Db[(size_t)u3 * B + s];
-      if (k0 != KEY_INF) best = min(best, relax_key(k0, min(in_lat[a], LAT_SAT), in_om[a]));
-      if (k1 != KEY_INF) best = min(best, relax_key(k1, min(in_lat[a + 1], LAT_SAT), in_om[a + 1]));
-      if (k2 != KEY_INF) best = min(best, relax_key(k2, min(in_lat[a + 2], LAT_SAT), in_om[a + 2]));
-      if (k3 != KEY_INF) best = min(best, relax_key(k3, min(in_lat[a + 3], LAT_SAT), in_om[a + 3]));
-    }
-    for (; a < a1; a++) {
+    lo[k] = valid ? in_off[v] : 0;
+    hi[k] = valid ? in_off[v + 1] : 0;
+    cur[k] = valid ? Db[(size_t)v * B + s] : KEY_INF;
+    best[k] = cur[k];
+  }
+  const uint32_t a_begin = in_off[v0], a_end = in_off[min(v0 + NB, n)];
+  uint32_t n_relax = 0;
+  for (uint32_t c0 = a_begin; c0 < a_end; c0 += ARC_CHUNK) {
+    const uint32_t c1 = min(c0 + ARC_CHUNK, a_end);
+    for (uint32_t a = c0 + threadIdx.x; a < c1; a += RELAX_BLOCK) {
       const uint32_t u = in_src[a];
-      if (!(Pf[u] | Cf[u])) continue;
-      n_relax++;
-      const uint64_t ku = Db[(size_t)u * B + s];
-      if (ku != KEY_INF) best = min(best, relax_key(ku, min(in_lat[a], LAT_SAT), in_om[a]));
+      const bool f = Pf[u] | Cf[u];
+      s_u[a - c0] = u | (f ? 0x80000000u : 0u);
+      s_lat[a - c0] = min(in_lat[a], LAT_SAT);
+      s_om[a - c0] = in_om[a];
     }
-    const bool ch = valid && best < cur;
-    if (ch) Db[(size_t)v * B + s] = best;  // one untorn 64-bit (lat, loss) update
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < VPW; k++) {
+      uint32_t a = max(lo[k], c0);
+      const uint32_t e = min(hi[k], c1);
+      uint64_t bk = best[k];
+      for (; a + 4 <= e; a += 4) {
+        const uint32_t x0 = s_u[a - c0], x1 = s_u[a + 1 - c0], x2 = s_u[a + 2 - c0], x3 = s_u[a + 3 - c0];
+        uint64_t k0 = KEY_INF, k1 = KEY_INF, k2 = KEY_INF, k3 = KEY_INF;
+        if (x0 >> 31) k0 = Db[(size_t)(x0 & 0x7fffffffu) * B + s];
+        if (x1 >> 31) k1 = Db[(size_t)(x1 & 0x7fffffffu) * B + s];
+        if (x2 >> 31) k2 = Db[(size_t)(x2 & 0x7fffffffu) * B + s];
+        if (x3 >> 31) k3 = Db[(size_t)(x3 & 0x7fffffffu) * B + s];
+        n_relax += (x0 >> 31) + (x1 >> 31) + (x2 >> 31) + (x3 >> 31);
+        if (k0 != KEY_INF) bk = min(bk, relax_key(k0, s_lat[a - c0], s_om[a - c0]));
+        if (k1 != KEY_INF) bk = min(bk, relax_key(k1, s_lat[a + 1 - c0], s_om[a + 1 - c0]));
+        if (k2 != KEY_INF) bk = min(bk, relax_key(k2, s_lat[a + 2 - c0], s_om[a + 2 - c0]));
+        if (k3 != KEY_INF) bk = min(bk, relax_key(k3, s_lat[a + 3 - c0], s_om[a + 3 - c0]));
+      }
+      for (; a < e; a++) {
+        const uint32_t x = s_u[a - c0];
+        if (!(x >> 31)) continue;
+        n_relax++;
+        const uint64_t ku = Db[(size_t)(x & 0x7fffffffu) * B + s];
+        if (ku != KEY_INF) bk = min(bk, relax_key(ku, s_lat[a - c0], s_om[a - c0]));
+      }
+      best[k] = bk;
+    }
+    __syncthreads();
+  }
+  bool any = false;
+#pragma unroll
+  for (int k = 0; k < VPW; k++) {
+    const uint32_t v = vq + k;
+    const bool ch = v < n && best[k] < cur[k];
+    if (ch) Db[(size_t)v * B + s] = best[k];  // one untorn 64-bit (lat, loss) update
     const uint64_t m = __ballot(ch) & gmask;
     if (m && s == 0) Cf[v] = 1;
     any |= ch;
@@ -215,7 +250,6 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
   // every writer stores the same 1: a plain store, no same-address atomic storm
   if (__any(any) && lane == 0) __hip_atomic_store(&changed[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (work) {  // measurement only (timers on): block reduction, one add per block into a sharded counter
-    __shared__ unsigned long long wblk[RELAX_WAVES];
     unsigned long long wsum = n_relax;
     for (int d = 32; d > 0; d >>= 1) wsum += __shfl_xor(wsum, d, 64);
     if (lane == 0) wblk[wave] = wsum;
