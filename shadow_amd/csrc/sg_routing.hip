@@ -158,7 +158,7 @@ __global__ void k_mark_sources(uint8_t* __restrict__ dirty, uint32_t n, const ui
   if (row < row_end) dirty[(size_t)b * n + used[row]] = 1;
 }
 
-template <int B, int VPW>
+template <int B, int VPW, bool XCD, bool FLAGS>
 __global__ void __launch_bounds__(RELAX_BLOCK)
     k_relax_front(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
                   const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om, uint64_t* D,
@@ -175,7 +175,13 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
   __shared__ float s_om[ARC_CHUNK];
   __shared__ unsigned long long wblk[RELAX_WAVES];
   uint32_t b, chunk;
-  if (!map.decode(blockIdx.x, b, chunk) || !active[b]) return;
+  if (XCD) {
+    if (!map.decode(blockIdx.x, b, chunk) || !active[b]) return;
+  } else {
+    b = blockIdx.x / map.nvb;
+    chunk = blockIdx.x % map.nvb;
+    if (b >= map.n_batches || !active[b]) return;
+  }
   uint64_t* Db = D + (size_t)b * n * B;
   const uint8_t* Pf = dprev + (size_t)b * n;
   uint8_t* Cf = dcur + (size_t)b * n;
@@ -202,7 +208,7 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
     const uint32_t c1 = min(c0 + ARC_CHUNK, a_end);
     for (uint32_t a = c0 + threadIdx.x; a < c1; a += RELAX_BLOCK) {
       const uint32_t u = in_src[a];
-      const bool f = Pf[u] | Cf[u];
+      const bool f = !FLAGS || (Pf[u] | Cf[u]);
       s_u[a - c0] = u | (f ? 0x80000000u : 0u);
       s_lat[a - c0] = min(in_lat[a], LAT_SAT);
       s_om[a - c0] = in_om[a];
@@ -596,11 +602,12 @@ static void run_wide(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t 
   }
 }
 
-static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
-                           uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
-                           float* out_loss) {
-  constexpr int B = 32;    // sources per batch: slab = n x 256 B (L2-resident per XCD at 10k nodes)
-  constexpr int VPW = 4;   // destination nodes per lane group, walked sequentially
+template <int B, int VPW, bool XCD, bool FLAGS>
+static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
+                             uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
+                             float* out_loss) {
+  // B = sources per batch (B = 32: slab n x 256 B, L2-resident per XCD at 10k nodes);
+  // VPW = destination nodes per lane group, walked sequentially
   constexpr int G = 64 / B;
   hipStream_t st = ctx->stream;
   const uint32_t n = net->n_nodes;
@@ -637,7 +644,7 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
     SG_CHECK_LAUNCH();
     SG_HIP(hipMemsetAsync(ring[2], 1, gb * 4ull, st));  // "changed in pass -1": every batch active
     const BatchMap map{nvb, gb};
-    const uint32_t grid = 8 * nvb * ((gb + 7) / 8);
+    const uint32_t grid = XCD ? 8 * nvb * ((gb + 7) / 8) : nvb * gb;
     for (uint32_t pass = 0;;) {
       uint32_t last = pass;
       for (uint32_t c = 0; c < chunk; c++, pass++) {
@@ -650,7 +657,7 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
         if (pass) SG_HIP(hipMemsetAsync(dcur, 0, (size_t)gb * n, st));
         {
           TimedLaunch tl(ctx, "relax_packed", 0.0);
-          hipLaunchKernelGGL((k_relax_front<B, VPW>), dim3(grid), dim3(RELAX_BLOCK), 0, st, net->in_off,
+          hipLaunchKernelGGL((k_relax_front<B, VPW, XCD, FLAGS>), dim3(grid), dim3(RELAX_BLOCK), 0, st, net->in_off,
                              net->in_src, net->in_lat, net->in_om, D, n, map, active, changed, dprev, dcur, work);
         }
         SG_CHECK_LAUNCH();
@@ -685,6 +692,29 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
     timer_add_work(ctx, "relax_packed", total);
   }
   if (!wide_rows.empty()) run_wide(ctx, net, d_used, n_used, wide_rows, row_begin, out_lat, out_loss);
+}
+
+// Kernel variant (A/B measurement): SG_APSP_VARIANT = "<B>[x][f]" (x = XCD-aware
+// grid, f = frontier flags); default below.
+static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
+                           uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
+  const char* v = getenv("SG_APSP_VARIANT");
+  std::string var = v && *v ? v : "32xf";
+#define SG_VAR(name, B, VPW, X, F)                                                              \
+  if (var == name) {                                                                            \
+    shortest_paths_t<B, VPW, X, F>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss); \
+    return;                                                                                     \
+  }
+  SG_VAR("32xf", 32, 4, true, true)
+  SG_VAR("32x", 32, 4, true, false)
+  SG_VAR("32f", 32, 4, false, true)
+  SG_VAR("32", 32, 4, false, false)
+  SG_VAR("64xf", 64, 4, true, true)
+  SG_VAR("64x", 64, 4, true, false)
+  SG_VAR("64f", 64, 4, false, true)
+  SG_VAR("64", 64, 4, false, false)
+#undef SG_VAR
+  throw Error(SG_ERR_INVALID_ARG, "unknown SG_APSP_VARIANT " + var);
 }
 
 static void direct_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, const uint32_t* h_used,
