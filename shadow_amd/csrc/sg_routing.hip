@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "sg_device.h"
@@ -149,8 +150,8 @@ __global__ void k_init_front(uint64_t* __restrict__ D, uint32_t n, const uint32_
   }
 }
 
-template <int B>
-__global__ void k_mark_sources(uint8_t* __restrict__ dirty, uint32_t n, const uint32_t* __restrict__ used,
+template <int B, class FT>
+__global__ void k_mark_sources(FT* __restrict__ dirty, uint32_t n, const uint32_t* __restrict__ used,
                                uint32_t first_row, uint32_t row_end, uint32_t n_batches) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_batches * B) return;
@@ -259,6 +260,88 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
     unsigned long long wsum = n_relax;
     for (int d = 32; d > 0; d >>= 1) wsum += __shfl_xor(wsum, d, 64);
     if (lane == 0) wblk[wave] = wsum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long t = 0;
+      for (int w = 0; w < RELAX_WAVES; w++) t += wblk[w];
+      if (t) atomicAdd(&work[blockIdx.x & (WORK_SHARDS - 1)], t);
+    }
+  }
+}
+
+// Wave-per-node relaxation (B = 64: lane = source).  The destination node is
+// wave-uniform, so in-arcs and frontier flags are scalar loads; each dirty
+// arc costs one coalesced 512-B row read.  Clean arcs read the node's own row
+// instead (an L1 hit), keeping the four loads per step branch-free and in
+// flight together.  Linear batch-major grid: all CUs work on the same one or
+// two batches, whose slab rows stay hot in L2 / Infinity Cache.
+template <int VPW, bool FLAGS>
+__global__ void __launch_bounds__(RELAX_BLOCK)
+    k_relax_wave(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
+                 const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om, uint64_t* D,
+                 uint32_t n, uint32_t nvb, uint32_t n_batches, const uint32_t* __restrict__ active,
+                 uint32_t* __restrict__ changed, const uint32_t* dprev, uint32_t* dcur,
+                 unsigned long long* __restrict__ work) {
+  constexpr int B = 64;
+  __shared__ unsigned long long wblk[RELAX_WAVES];
+  const uint32_t b = blockIdx.x / nvb, chunk = blockIdx.x % nvb;
+  if (b >= n_batches || !active[b]) return;
+  uint64_t* Db = D + (size_t)b * n * B;
+  const uint32_t* Pf = dprev + (size_t)b * n;
+  uint32_t* Cf = dcur + (size_t)b * n;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  bool any = false;
+  uint32_t n_relax = 0;  // wave-uniform count of dirty arcs
+  const uint32_t v0 = (chunk * RELAX_WAVES + wave) * VPW;
+#pragma unroll 1
+  for (int k = 0; k < VPW; k++) {
+    const uint32_t v = v0 + k;
+    if (v >= n) break;
+    const uint32_t a0 = in_off[v], a1 = in_off[v + 1];
+    const size_t own = (size_t)v * B + lane;
+    const uint64_t cur = Db[own];
+    uint64_t best = cur;
+    uint32_t a = a0;
+    for (; a + 4 <= a1; a += 4) {
+      const uint32_t u0 = in_src[a], u1 = in_src[a + 1], u2 = in_src[a + 2], u3 = in_src[a + 3];
+      bool f0 = true, f1 = true, f2 = true, f3 = true;
+      if (FLAGS) {
+        f0 = (Pf[u0] | Cf[u0]) != 0;
+        f1 = (Pf[u1] | Cf[u1]) != 0;
+        f2 = (Pf[u2] | Cf[u2]) != 0;
+        f3 = (Pf[u3] | Cf[u3]) != 0;
+        n_relax += (uint32_t)f0 + (uint32_t)f1 + (uint32_t)f2 + (uint32_t)f3;
+      }
+      const uint64_t k0 = Db[f0 ? (size_t)u0 * B + lane : own];
+      const uint64_t k1 = Db[f1 ? (size_t)u1 * B + lane : own];
+      const uint64_t k2 = Db[f2 ? (size_t)u2 * B + lane : own];
+      const uint64_t k3 = Db[f3 ? (size_t)u3 * B + lane : own];
+      const uint64_t c0 = (!f0 || k0 == KEY_INF) ? KEY_INF : relax_key(k0, min(in_lat[a], LAT_SAT), in_om[a]);
+      const uint64_t c1 = (!f1 || k1 == KEY_INF) ? KEY_INF : relax_key(k1, min(in_lat[a + 1], LAT_SAT), in_om[a + 1]);
+      const uint64_t c2 = (!f2 || k2 == KEY_INF) ? KEY_INF : relax_key(k2, min(in_lat[a + 2], LAT_SAT), in_om[a + 2]);
+      const uint64_t c3 = (!f3 || k3 == KEY_INF) ? KEY_INF : relax_key(k3, min(in_lat[a + 3], LAT_SAT), in_om[a + 3]);
+      best = min(best, min(min(c0, c1), min(c2, c3)));
+    }
+    for (; a < a1; a++) {
+      const uint32_t u = in_src[a];
+      const bool f = !FLAGS || (Pf[u] | Cf[u]) != 0;
+      if (FLAGS) n_relax += f;
+      const uint64_t ku = Db[f ? (size_t)u * B + lane : own];
+      const uint64_t c = (!f || ku == KEY_INF) ? KEY_INF : relax_key(ku, min(in_lat[a], LAT_SAT), in_om[a]);
+      best = min(best, c);
+    }
+    if (!FLAGS) n_relax += a1 - a0;
+    const bool ch = best < cur;
+    if (ch) Db[own] = best;  // one untorn 64-bit (lat, loss) update
+    if (__any(ch)) {
+      any = true;
+      if (FLAGS && lane == 0) Cf[v] = 1u;
+    }
+  }
+  if (any && lane == 0) __hip_atomic_store(&changed[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (work) {  // measurement only: lane-relaxations = dirty arcs x 64
+    if (lane == 0) wblk[wave] = (unsigned long long)n_relax * B;
     __syncthreads();
     if (threadIdx.x == 0) {
       unsigned long long t = 0;
@@ -602,12 +685,15 @@ static void run_wide(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t 
   }
 }
 
-template <int B, int VPW, bool XCD, bool FLAGS>
+template <int B, int VPW, bool XCD, bool FLAGS, bool WAVE>
 static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                              uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
                              float* out_loss) {
   // B = sources per batch (B = 32: slab n x 256 B, L2-resident per XCD at 10k nodes);
-  // VPW = destination nodes per lane group, walked sequentially
+  // VPW = destination nodes per lane group, walked sequentially;
+  // WAVE = wave-per-node kernel (B = 64, scalar arc loads, u32 frontier flags)
+  static_assert(!WAVE || B == 64, "wave-per-node kernel needs B = 64");
+  using FT = typename std::conditional<WAVE, uint32_t, uint8_t>::type;
   constexpr int G = 64 / B;
   hipStream_t st = ctx->stream;
   const uint32_t n = net->n_nodes;
@@ -623,8 +709,8 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
   uint32_t* flags = ctx->r_flags.get<uint32_t>((size_t)group * 4 + 8);
   uint32_t* ring[3] = {flags, flags + group, flags + 2 * (size_t)group};
   uint32_t* sat = flags + 3 * (size_t)group;
-  uint8_t* dirty = ctx->r_dirty.get<uint8_t>(2 * (size_t)group * n);
-  uint8_t* dirtyA[2] = {dirty, dirty + (size_t)group * n};
+  FT* dirty = ctx->r_dirty.get<FT>(2 * (size_t)group * n);
+  FT* dirtyA[2] = {dirty, dirty + (size_t)group * n};
   unsigned long long* work = ctx->timing ? ctx->r_work.get<unsigned long long>(WORK_SHARDS) : nullptr;
   if (work) SG_HIP(hipMemsetAsync(work, 0, WORK_SHARDS * 8, st));
   // Passes are issued in chunks; the host reads the convergence flags once per
@@ -637,9 +723,9 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
     const uint32_t first_row = row_begin + g0 * B;
     hipLaunchKernelGGL(k_init_front<B>, dim3(grid_for((size_t)gb * n * B, 256, 65536)), dim3(256), 0, st, D, n,
                        d_used, first_row, row_end, gb);
-    SG_HIP(hipMemsetAsync(dirty, 0, 2 * (size_t)gb * n, st));
+    SG_HIP(hipMemsetAsync(dirty, 0, 2 * (size_t)gb * n * sizeof(FT), st));
     dirtyA[1] = dirty + (size_t)gb * n;
-    hipLaunchKernelGGL(k_mark_sources<B>, dim3(grid_for((size_t)gb * B, 256)), dim3(256), 0, st, dirtyA[1], n,
+    hipLaunchKernelGGL((k_mark_sources<B, FT>), dim3(grid_for((size_t)gb * B, 256)), dim3(256), 0, st, dirtyA[1], n,
                        d_used, first_row, row_end, gb);
     SG_CHECK_LAUNCH();
     SG_HIP(hipMemsetAsync(ring[2], 1, gb * 4ull, st));  // "changed in pass -1": every batch active
@@ -651,14 +737,22 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
         if (pass > n + 2 + chunk) throw Error(SG_ERR_DEVICE, "relaxation did not converge");
         const uint32_t* active = ring[(pass + 2) % 3];
         uint32_t* changed = ring[pass % 3];
-        uint8_t* dcur = dirtyA[pass & 1];
-        const uint8_t* dprev = dirtyA[(pass & 1) ^ 1];
+        FT* dcur = dirtyA[pass & 1];
+        const FT* dprev = dirtyA[(pass & 1) ^ 1];
         SG_HIP(hipMemsetAsync(changed, 0, gb * 4ull, st));
-        if (pass) SG_HIP(hipMemsetAsync(dcur, 0, (size_t)gb * n, st));
+        if (pass) SG_HIP(hipMemsetAsync(dcur, 0, (size_t)gb * n * sizeof(FT), st));
         {
           TimedLaunch tl(ctx, "relax_packed", 0.0);
-          hipLaunchKernelGGL((k_relax_front<B, VPW, XCD, FLAGS>), dim3(grid), dim3(RELAX_BLOCK), 0, st, net->in_off,
-                             net->in_src, net->in_lat, net->in_om, D, n, map, active, changed, dprev, dcur, work);
+          if constexpr (WAVE) {
+            const uint32_t nvw = (n + RELAX_WAVES * VPW - 1) / (RELAX_WAVES * VPW);
+            hipLaunchKernelGGL((k_relax_wave<VPW, FLAGS>), dim3(nvw * gb), dim3(RELAX_BLOCK), 0, st, net->in_off,
+                               net->in_src, net->in_lat, net->in_om, D, n, nvw, gb, active, changed,
+                               (const uint32_t*)dprev, (uint32_t*)dcur, work);
+          } else {
+            hipLaunchKernelGGL((k_relax_front<B, VPW, XCD, FLAGS>), dim3(grid), dim3(RELAX_BLOCK), 0, st,
+                               net->in_off, net->in_src, net->in_lat, net->in_om, D, n, map, active, changed,
+                               (const uint8_t*)dprev, (uint8_t*)dcur, work);
+          }
         }
         SG_CHECK_LAUNCH();
         last = pass;
@@ -700,19 +794,21 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
                            uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
   const char* v = getenv("SG_APSP_VARIANT");
   std::string var = v && *v ? v : "32xf";
-#define SG_VAR(name, B, VPW, X, F)                                                              \
-  if (var == name) {                                                                            \
-    shortest_paths_t<B, VPW, X, F>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss); \
-    return;                                                                                     \
+#define SG_VAR(name, B, VPW, X, F, W)                                                                \
+  if (var == name) {                                                                                 \
+    shortest_paths_t<B, VPW, X, F, W>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss); \
+    return;                                                                                          \
   }
-  SG_VAR("32xf", 32, 4, true, true)
-  SG_VAR("32x", 32, 4, true, false)
-  SG_VAR("32f", 32, 4, false, true)
-  SG_VAR("32", 32, 4, false, false)
-  SG_VAR("64xf", 64, 4, true, true)
-  SG_VAR("64x", 64, 4, true, false)
-  SG_VAR("64f", 64, 4, false, true)
-  SG_VAR("64", 64, 4, false, false)
+  SG_VAR("w64f", 64, 4, false, true, true)
+  SG_VAR("w64", 64, 4, false, false, true)
+  SG_VAR("32xf", 32, 4, true, true, false)
+  SG_VAR("32x", 32, 4, true, false, false)
+  SG_VAR("32f", 32, 4, false, true, false)
+  SG_VAR("32", 32, 4, false, false, false)
+  SG_VAR("64xf", 64, 4, true, true, false)
+  SG_VAR("64x", 64, 4, true, false, false)
+  SG_VAR("64f", 64, 4, false, true, false)
+  SG_VAR("64", 64, 4, false, false, false)
 #undef SG_VAR
   throw Error(SG_ERR_INVALID_ARG, "unknown SG_APSP_VARIANT " + var);
 }
