@@ -140,7 +140,9 @@ def load(path: str | None = None):
         "sg_deliver_bucket": (i32, [vp, vp, u32, vp, u32, u32, vp, vp]),
     }
     for name, (res, args) in sig.items():
-        f = getattr(L, name)
+        f = getattr(L, name, None)
+        if f is None:  # only an older library given via SHADOW_GPU_LIB (A/B tools) lacks symbols
+            continue
         f.restype = res
         f.argtypes = args
     if L.sg_abi_version() != 1:
