@@ -222,16 +222,19 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
       uint64_t bk = best[k];
       for (; a + 4 <= e; a += 4) {
         const uint32_t x0 = s_u[a - c0], x1 = s_u[a + 1 - c0], x2 = s_u[a + 2 - c0], x3 = s_u[a + 3 - c0];
-        uint64_t k0 = KEY_INF, k1 = KEY_INF, k2 = KEY_INF, k3 = KEY_INF;
-        if (x0 >> 31) k0 = Db[(size_t)(x0 & 0x7fffffffu) * B + s];
-        if (x1 >> 31) k1 = Db[(size_t)(x1 & 0x7fffffffu) * B + s];
-        if (x2 >> 31) k2 = Db[(size_t)(x2 & 0x7fffffffu) * B + s];
-        if (x3 >> 31) k3 = Db[(size_t)(x3 & 0x7fffffffu) * B + s];
+        const size_t own = (size_t)(vq + k) * B + s;  // clean arcs re-read the node's own row (L1 hit)
+        const uint64_t k0 = Db[(x0 >> 31) ? (size_t)(x0 & 0x7fffffffu) * B + s : own];
+        const uint64_t k1 = Db[(x1 >> 31) ? (size_t)(x1 & 0x7fffffffu) * B + s : own];
+        const uint64_t k2 = Db[(x2 >> 31) ? (size_t)(x2 & 0x7fffffffu) * B + s : own];
+        const uint64_t k3 = Db[(x3 >> 31) ? (size_t)(x3 & 0x7fffffffu) * B + s : own];
         n_relax += (x0 >> 31) + (x1 >> 31) + (x2 >> 31) + (x3 >> 31);
-        if (k0 != KEY_INF) bk = min(bk, relax_key(k0, s_lat[a - c0], s_om[a - c0]));
-        if (k1 != KEY_INF) bk = min(bk, relax_key(k1, s_lat[a + 1 - c0], s_om[a + 1 - c0]));
-        if (k2 != KEY_INF) bk = min(bk, relax_key(k2, s_lat[a + 2 - c0], s_om[a + 2 - c0]));
-        if (k3 != KEY_INF) bk = min(bk, relax_key(k3, s_lat[a + 3 - c0], s_om[a + 3 - c0]));
+        const uint64_t l0 = s_lat[a - c0], l1 = s_lat[a + 1 - c0], l2 = s_lat[a + 2 - c0], l3 = s_lat[a + 3 - c0];
+        const float o0 = s_om[a - c0], o1 = s_om[a + 1 - c0], o2 = s_om[a + 2 - c0], o3 = s_om[a + 3 - c0];
+        const uint64_t c0k = ((x0 >> 31) && k0 != KEY_INF) ? relax_key(k0, l0, o0) : KEY_INF;
+        const uint64_t c1k = ((x1 >> 31) && k1 != KEY_INF) ? relax_key(k1, l1, o1) : KEY_INF;
+        const uint64_t c2k = ((x2 >> 31) && k2 != KEY_INF) ? relax_key(k2, l2, o2) : KEY_INF;
+        const uint64_t c3k = ((x3 >> 31) && k3 != KEY_INF) ? relax_key(k3, l3, o3) : KEY_INF;
+        bk = min(bk, min(min(c0k, c1k), min(c2k, c3k)));
       }
       for (; a < e; a++) {
         const uint32_t x = s_u[a - c0];
@@ -317,10 +320,15 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
       const uint64_t k1 = Db[f1 ? (size_t)u1 * B + lane : own];
       const uint64_t k2 = Db[f2 ? (size_t)u2 * B + lane : own];
       const uint64_t k3 = Db[f3 ? (size_t)u3 * B + lane : own];
-      const uint64_t c0 = (!f0 || k0 == KEY_INF) ? KEY_INF : relax_key(k0, min(in_lat[a], LAT_SAT), in_om[a]);
-      const uint64_t c1 = (!f1 || k1 == KEY_INF) ? KEY_INF : relax_key(k1, min(in_lat[a + 1], LAT_SAT), in_om[a + 1]);
-      const uint64_t c2 = (!f2 || k2 == KEY_INF) ? KEY_INF : relax_key(k2, min(in_lat[a + 2], LAT_SAT), in_om[a + 2]);
-      const uint64_t c3 = (!f3 || k3 == KEY_INF) ? KEY_INF : relax_key(k3, min(in_lat[a + 3], LAT_SAT), in_om[a + 3]);
+      // arc weights loaded unconditionally, before any use of k*: keeps them off the
+      // critical path (under a condition the compiler serialises them behind the row loads)
+      const uint64_t l0 = min(in_lat[a], LAT_SAT), l1 = min(in_lat[a + 1], LAT_SAT);
+      const uint64_t l2 = min(in_lat[a + 2], LAT_SAT), l3 = min(in_lat[a + 3], LAT_SAT);
+      const float o0 = in_om[a], o1 = in_om[a + 1], o2 = in_om[a + 2], o3 = in_om[a + 3];
+      const uint64_t c0 = (!f0 || k0 == KEY_INF) ? KEY_INF : relax_key(k0, l0, o0);
+      const uint64_t c1 = (!f1 || k1 == KEY_INF) ? KEY_INF : relax_key(k1, l1, o1);
+      const uint64_t c2 = (!f2 || k2 == KEY_INF) ? KEY_INF : relax_key(k2, l2, o2);
+      const uint64_t c3 = (!f3 || k3 == KEY_INF) ? KEY_INF : relax_key(k3, l3, o3);
       best = min(best, min(min(c0, c1), min(c2, c3)));
     }
     for (; a < a1; a++) {
@@ -328,7 +336,9 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
       const bool f = !FLAGS || (Pf[u] | Cf[u]) != 0;
       if (FLAGS) n_relax += f;
       const uint64_t ku = Db[f ? (size_t)u * B + lane : own];
-      const uint64_t c = (!f || ku == KEY_INF) ? KEY_INF : relax_key(ku, min(in_lat[a], LAT_SAT), in_om[a]);
+      const uint64_t l = min(in_lat[a], LAT_SAT);
+      const float o = in_om[a];
+      const uint64_t c = (!f || ku == KEY_INF) ? KEY_INF : relax_key(ku, l, o);
       best = min(best, c);
     }
     if (!FLAGS) n_relax += a1 - a0;
