@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
                  unsigned long long* __restrict__ work) {
   constexpr int B = 64;
   __shared__ unsigned long long wblk[RELAX_WAVES];
-  const uint32_t b = blockIdx.x / nvb, chunk = blockIdx.x % nvb;
+  const uint32_t b = blockIdx.y, chunk = blockIdx.x;  // 2-D grid (chunk, batch)
   if (b >= n_batches || !active[b]) return;
   uint64_t* Db = D + (size_t)b * n * B;
   const uint32_t* Pf = dprev + (size_t)b * n;
@@ -755,7 +755,7 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
           TimedLaunch tl(ctx, "relax_packed", 0.0);
           if constexpr (WAVE) {
             const uint32_t nvw = (n + RELAX_WAVES * VPW - 1) / (RELAX_WAVES * VPW);
-            hipLaunchKernelGGL((k_relax_wave<VPW, FLAGS>), dim3(nvw * gb), dim3(RELAX_BLOCK), 0, st, net->in_off,
+            hipLaunchKernelGGL((k_relax_wave<VPW, FLAGS>), dim3(nvw, gb), dim3(RELAX_BLOCK), 0, st, net->in_off,
                                net->in_src, net->in_lat, net->in_om, D, n, nvw, gb, active, changed,
                                (const uint32_t*)dprev, (uint32_t*)dcur, work);
           } else {
