@@ -361,6 +361,58 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
   }
 }
 
+// Verbatim v1 relaxation kernel (A/B control, variant "v1k").
+template <int VPW>
+__global__ void __launch_bounds__(RELAX_BLOCK)
+    k_relax_v1(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
+                   const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om,
+                   uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ active,
+                   uint32_t* __restrict__ changed) {
+  const uint32_t b = blockIdx.y;
+  if (!active[b]) return;
+  uint64_t* __restrict__ Db = D + (size_t)b * n * BATCH;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  bool any = false;
+  const uint32_t v0 = (blockIdx.x * RELAX_WAVES + wave) * VPW;
+#pragma unroll 1
+  for (int k = 0; k < VPW; k++) {
+    const uint32_t v = v0 + k;
+    if (v >= n) break;
+    const uint32_t a0 = in_off[v], a1 = in_off[v + 1];
+    const uint64_t cur = Db[(size_t)v * BATCH + lane];
+    uint64_t best = cur;
+    uint32_t a = a0;
+    // 4 independent 512-B row reads in flight per wave
+    for (; a + 4 <= a1; a += 4) {
+      uint32_t u0 = in_src[a], u1 = in_src[a + 1], u2 = in_src[a + 2], u3 = in_src[a + 3];
+      uint64_t k0 = Db[(size_t)u0 * BATCH + lane];
+      uint64_t k1 = Db[(size_t)u1 * BATCH + lane];
+      uint64_t k2 = Db[(size_t)u2 * BATCH + lane];
+      uint64_t k3 = Db[(size_t)u3 * BATCH + lane];
+      uint64_t l0 = min(in_lat[a], LAT_SAT), l1 = min(in_lat[a + 1], LAT_SAT);
+      uint64_t l2 = min(in_lat[a + 2], LAT_SAT), l3 = min(in_lat[a + 3], LAT_SAT);
+      float o0 = in_om[a], o1 = in_om[a + 1], o2 = in_om[a + 2], o3 = in_om[a + 3];
+      uint64_t c0 = k0 == KEY_INF ? KEY_INF : relax_key(k0, l0, o0);
+      uint64_t c1 = k1 == KEY_INF ? KEY_INF : relax_key(k1, l1, o1);
+      uint64_t c2 = k2 == KEY_INF ? KEY_INF : relax_key(k2, l2, o2);
+      uint64_t c3 = k3 == KEY_INF ? KEY_INF : relax_key(k3, l3, o3);
+      best = min(best, min(min(c0, c1), min(c2, c3)));
+    }
+    for (; a < a1; a++) {
+      uint32_t u = in_src[a];
+      uint64_t ku = Db[(size_t)u * BATCH + lane];
+      uint64_t c = ku == KEY_INF ? KEY_INF : relax_key(ku, min(in_lat[a], LAT_SAT), in_om[a]);
+      best = min(best, c);
+    }
+    if (best < cur) {
+      Db[(size_t)v * BATCH + lane] = best;  // one untorn 64-bit (lat, loss) update
+      any = true;
+    }
+  }
+  if (__any(any) && lane == 0) atomicOr(&changed[b], 1u);
+}
+
 // Transposed write-out of [B rows x 64 cols] tiles.  Diagonal = the raw
 // self-loop (graph/mod.rs:210-217).  Saturated keys flag their batch.
 template <int B>
@@ -753,7 +805,11 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
         if (pass) SG_HIP(hipMemsetAsync(dcur, 0, (size_t)gb * n * sizeof(FT), st));
         {
           TimedLaunch tl(ctx, "relax_packed", 0.0);
-          if constexpr (WAVE) {
+          if (getenv("SG_APSP_V1K")) {
+            const uint32_t nvb1 = (n + RELAX_WAVES * 4 - 1) / (RELAX_WAVES * 4);
+            hipLaunchKernelGGL(k_relax_v1<4>, dim3(nvb1, gb), dim3(RELAX_BLOCK), 0, st, net->in_off, net->in_src,
+                               net->in_lat, net->in_om, D, n, active, changed);
+          } else if constexpr (WAVE) {
             const uint32_t nvw = (n + RELAX_WAVES * VPW - 1) / (RELAX_WAVES * VPW);
             hipLaunchKernelGGL((k_relax_wave<VPW, FLAGS>), dim3(nvw, gb), dim3(RELAX_BLOCK), 0, st, net->in_off,
                                net->in_src, net->in_lat, net->in_om, D, n, nvw, gb, active, changed,
