@@ -278,25 +278,24 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
 // instead (an L1 hit), keeping the four loads per step branch-free and in
 // flight together.  Linear batch-major grid: all CUs work on the same one or
 // two batches, whose slab rows stay hot in L2 / Infinity Cache.
-template <int VPW, bool FLAGS>
+template <int VPW, bool FLAGS, bool COUNT>
 __global__ void __launch_bounds__(RELAX_BLOCK)
     k_relax_wave(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
-                 const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om, uint64_t* D,
-                 uint32_t n, uint32_t nvb, uint32_t n_batches, const uint32_t* __restrict__ active,
+                 const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om,
+                 uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ active,
                  uint32_t* __restrict__ changed, const uint32_t* dprev, uint32_t* dcur,
                  unsigned long long* __restrict__ work) {
   constexpr int B = 64;
-  __shared__ unsigned long long wblk[RELAX_WAVES];
-  const uint32_t b = blockIdx.y, chunk = blockIdx.x;  // 2-D grid (chunk, batch)
-  if (b >= n_batches || !active[b]) return;
-  uint64_t* Db = D + (size_t)b * n * B;
+  const uint32_t b = blockIdx.y;
+  if (!active[b]) return;
+  uint64_t* __restrict__ Db = D + (size_t)b * n * B;
   const uint32_t* Pf = dprev + (size_t)b * n;
   uint32_t* Cf = dcur + (size_t)b * n;
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   bool any = false;
-  uint32_t n_relax = 0;  // wave-uniform count of dirty arcs
-  const uint32_t v0 = (chunk * RELAX_WAVES + wave) * VPW;
+  uint32_t n_relax = 0;  // wave-uniform count of dirty arcs (COUNT builds only)
+  const uint32_t v0 = (blockIdx.x * RELAX_WAVES + wave) * VPW;
 #pragma unroll 1
   for (int k = 0; k < VPW; k++) {
     const uint32_t v = v0 + k;
@@ -306,22 +305,21 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
     const uint64_t cur = Db[own];
     uint64_t best = cur;
     uint32_t a = a0;
+    // 4 independent 512-B row reads in flight per wave
     for (; a + 4 <= a1; a += 4) {
       const uint32_t u0 = in_src[a], u1 = in_src[a + 1], u2 = in_src[a + 2], u3 = in_src[a + 3];
       bool f0 = true, f1 = true, f2 = true, f3 = true;
-      if (FLAGS) {
+      if (FLAGS) {  // clean sources re-read the node's own row (an L1 hit): branch-free loads
         f0 = (Pf[u0] | Cf[u0]) != 0;
         f1 = (Pf[u1] | Cf[u1]) != 0;
         f2 = (Pf[u2] | Cf[u2]) != 0;
         f3 = (Pf[u3] | Cf[u3]) != 0;
-        n_relax += (uint32_t)f0 + (uint32_t)f1 + (uint32_t)f2 + (uint32_t)f3;
       }
+      if (COUNT) n_relax += (uint32_t)f0 + (uint32_t)f1 + (uint32_t)f2 + (uint32_t)f3;
       const uint64_t k0 = Db[f0 ? (size_t)u0 * B + lane : own];
       const uint64_t k1 = Db[f1 ? (size_t)u1 * B + lane : own];
       const uint64_t k2 = Db[f2 ? (size_t)u2 * B + lane : own];
       const uint64_t k3 = Db[f3 ? (size_t)u3 * B + lane : own];
-      // arc weights loaded unconditionally, before any use of k*: keeps them off the
-      // critical path (under a condition the compiler serialises them behind the row loads)
       const uint64_t l0 = min(in_lat[a], LAT_SAT), l1 = min(in_lat[a + 1], LAT_SAT);
       const uint64_t l2 = min(in_lat[a + 2], LAT_SAT), l3 = min(in_lat[a + 3], LAT_SAT);
       const float o0 = in_om[a], o1 = in_om[a + 1], o2 = in_om[a + 2], o3 = in_om[a + 3];
@@ -334,32 +332,24 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
     for (; a < a1; a++) {
       const uint32_t u = in_src[a];
       const bool f = !FLAGS || (Pf[u] | Cf[u]) != 0;
-      if (FLAGS) n_relax += f;
+      if (COUNT) n_relax += f;
       const uint64_t ku = Db[f ? (size_t)u * B + lane : own];
       const uint64_t l = min(in_lat[a], LAT_SAT);
       const float o = in_om[a];
       const uint64_t c = (!f || ku == KEY_INF) ? KEY_INF : relax_key(ku, l, o);
       best = min(best, c);
     }
-    if (!FLAGS) n_relax += a1 - a0;
-    const bool ch = best < cur;
-    if (ch) Db[own] = best;  // one untorn 64-bit (lat, loss) update
-    if (__any(ch)) {
+    if (best < cur) {
+      Db[own] = best;  // one untorn 64-bit (lat, loss) update
       any = true;
-      if (FLAGS && lane == 0) Cf[v] = 1u;
     }
+    if (FLAGS && __any(best < cur) && lane == 0) Cf[v] = 1u;
   }
-  if (any && lane == 0) __hip_atomic_store(&changed[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (work) {  // measurement only: lane-relaxations = dirty arcs x 64
-    if (lane == 0) wblk[wave] = (unsigned long long)n_relax * B;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned long long t = 0;
-      for (int w = 0; w < RELAX_WAVES; w++) t += wblk[w];
-      if (t) atomicAdd(&work[blockIdx.x & (WORK_SHARDS - 1)], t);
-    }
-  }
+  if (__any(any) && lane == 0) atomicOr(&changed[b], 1u);
+  if (COUNT && lane == 0 && n_relax) atomicAdd(&work[(blockIdx.x + blockIdx.y) & (WORK_SHARDS - 1)],
+                                              (unsigned long long)n_relax * B);
 }
+
 
 // Verbatim v1 relaxation kernel (A/B control, variant "v1k").
 template <int VPW>
@@ -811,9 +801,14 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
                                net->in_lat, net->in_om, D, n, active, changed);
           } else if constexpr (WAVE) {
             const uint32_t nvw = (n + RELAX_WAVES * VPW - 1) / (RELAX_WAVES * VPW);
-            hipLaunchKernelGGL((k_relax_wave<VPW, FLAGS>), dim3(nvw, gb), dim3(RELAX_BLOCK), 0, st, net->in_off,
-                               net->in_src, net->in_lat, net->in_om, D, n, nvw, gb, active, changed,
-                               (const uint32_t*)dprev, (uint32_t*)dcur, work);
+            if (work)
+              hipLaunchKernelGGL((k_relax_wave<VPW, FLAGS, true>), dim3(nvw, gb), dim3(RELAX_BLOCK), 0, st,
+                                 net->in_off, net->in_src, net->in_lat, net->in_om, D, n, active, changed,
+                                 (const uint32_t*)dprev, (uint32_t*)dcur, work);
+            else
+              hipLaunchKernelGGL((k_relax_wave<VPW, FLAGS, false>), dim3(nvw, gb), dim3(RELAX_BLOCK), 0, st,
+                                 net->in_off, net->in_src, net->in_lat, net->in_om, D, n, active, changed,
+                                 (const uint32_t*)dprev, (uint32_t*)dcur, work);
           } else {
             hipLaunchKernelGGL((k_relax_front<B, VPW, XCD, FLAGS>), dim3(grid), dim3(RELAX_BLOCK), 0, st,
                                net->in_off, net->in_src, net->in_lat, net->in_om, D, n, map, active, changed,
