@@ -351,6 +351,98 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
 }
 
 
+// B = 32 sources per batch, two half-waves on adjacent destination nodes.
+// XCD=true: block L runs batch (L % 8) + 8 * ((L / 8) / nvb) so every block of
+// a batch shares an XCD (round-robin dispatch) and its 2.56 MB slab stays in
+// that XCD's 4 MB L2.  Load scheduling as in the wave kernel: weights loaded
+// unconditionally, row loads branch-free (clean arcs re-read the own row).
+template <int VPW, bool XCD, bool FLAGS, bool COUNT>
+__global__ void __launch_bounds__(RELAX_BLOCK)
+    k_relax_half(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
+                 const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om,
+                 uint64_t* __restrict__ D, uint32_t n, uint32_t nvb, uint32_t n_batches,
+                 const uint32_t* __restrict__ active, uint32_t* __restrict__ changed,
+                 const uint32_t* dprev, uint32_t* dcur, unsigned long long* __restrict__ work) {
+  constexpr int B = 32;
+  uint32_t b, chunk;
+  if (XCD) {
+    const uint32_t x = blockIdx.x & 7, q = blockIdx.x >> 3;
+    b = x + 8 * (q / nvb);
+    chunk = q % nvb;
+  } else {
+    b = blockIdx.x / nvb;
+    chunk = blockIdx.x % nvb;
+  }
+  if (b >= n_batches || !active[b]) return;
+  uint64_t* __restrict__ Db = D + (size_t)b * n * B;
+  const uint32_t* Pf = dprev + (size_t)b * n;
+  uint32_t* Cf = dcur + (size_t)b * n;
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 5, s = lane & 31;
+  const uint32_t wave = threadIdx.x >> 6;
+  bool any = false;
+  uint32_t n_relax = 0;
+  const uint32_t v0 = (chunk * RELAX_WAVES + wave) * (2 * VPW);
+#pragma unroll 1
+  for (int k = 0; k < VPW; k++) {
+    const uint32_t v = v0 + 2 * k + g;
+    const bool valid = v < n;
+    const uint32_t a0 = valid ? in_off[v] : 0, a1 = valid ? in_off[v + 1] : 0;
+    const size_t own = valid ? (size_t)v * B + s : (size_t)s;
+    const uint64_t cur = valid ? Db[own] : KEY_INF;
+    uint64_t best = cur;
+    uint32_t a = a0;
+    for (; a + 4 <= a1; a += 4) {
+      const uint32_t u0 = in_src[a], u1 = in_src[a + 1], u2 = in_src[a + 2], u3 = in_src[a + 3];
+      bool f0 = true, f1 = true, f2 = true, f3 = true;
+      if (FLAGS) {
+        f0 = (Pf[u0] | Cf[u0]) != 0;
+        f1 = (Pf[u1] | Cf[u1]) != 0;
+        f2 = (Pf[u2] | Cf[u2]) != 0;
+        f3 = (Pf[u3] | Cf[u3]) != 0;
+      }
+      if (COUNT) n_relax += (uint32_t)f0 + (uint32_t)f1 + (uint32_t)f2 + (uint32_t)f3;
+      const uint64_t k0 = Db[f0 ? (size_t)u0 * B + s : own];
+      const uint64_t k1 = Db[f1 ? (size_t)u1 * B + s : own];
+      const uint64_t k2 = Db[f2 ? (size_t)u2 * B + s : own];
+      const uint64_t k3 = Db[f3 ? (size_t)u3 * B + s : own];
+      const uint64_t l0 = min(in_lat[a], LAT_SAT), l1 = min(in_lat[a + 1], LAT_SAT);
+      const uint64_t l2 = min(in_lat[a + 2], LAT_SAT), l3 = min(in_lat[a + 3], LAT_SAT);
+      const float o0 = in_om[a], o1 = in_om[a + 1], o2 = in_om[a + 2], o3 = in_om[a + 3];
+      const uint64_t c0 = (!f0 || k0 == KEY_INF) ? KEY_INF : relax_key(k0, l0, o0);
+      const uint64_t c1 = (!f1 || k1 == KEY_INF) ? KEY_INF : relax_key(k1, l1, o1);
+      const uint64_t c2 = (!f2 || k2 == KEY_INF) ? KEY_INF : relax_key(k2, l2, o2);
+      const uint64_t c3 = (!f3 || k3 == KEY_INF) ? KEY_INF : relax_key(k3, l3, o3);
+      best = min(best, min(min(c0, c1), min(c2, c3)));
+    }
+    for (; a < a1; a++) {
+      const uint32_t u = in_src[a];
+      const bool f = !FLAGS || (Pf[u] | Cf[u]) != 0;
+      if (COUNT) n_relax += f;
+      const uint64_t ku = Db[f ? (size_t)u * B + s : own];
+      const uint64_t l = min(in_lat[a], LAT_SAT);
+      const float o = in_om[a];
+      const uint64_t c = (!f || ku == KEY_INF) ? KEY_INF : relax_key(ku, l, o);
+      best = min(best, c);
+    }
+    const bool ch = valid && best < cur;
+    if (ch) {
+      Db[own] = best;  // one untorn 64-bit (lat, loss) update
+      any = true;
+    }
+    if (FLAGS) {
+      const uint64_t m = __ballot(ch) >> (32 * g);
+      if ((m & 0xffffffffull) && s == 0) Cf[v] = 1u;
+    }
+  }
+  if (__any(any) && lane == 0) atomicOr(&changed[b], 1u);
+  if (COUNT) {
+    unsigned long long w = n_relax;
+    for (int d = 32; d > 0; d >>= 1) w += __shfl_xor(w, d, 64);
+    if (lane == 0 && w) atomicAdd(&work[blockIdx.x & (WORK_SHARDS - 1)], w);
+  }
+}
+
 // Verbatim v1 relaxation kernel (A/B control, variant "v1k").
 template <int VPW>
 __global__ void __launch_bounds__(RELAX_BLOCK)
@@ -737,7 +829,7 @@ static void run_wide(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t 
   }
 }
 
-template <int B, int VPW, bool XCD, bool FLAGS, bool WAVE>
+template <int B, int VPW, bool XCD, bool FLAGS, bool WAVE, bool HALF = false>
 static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                              uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
                              float* out_loss) {
@@ -745,7 +837,8 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
   // VPW = destination nodes per lane group, walked sequentially;
   // WAVE = wave-per-node kernel (B = 64, scalar arc loads, u32 frontier flags)
   static_assert(!WAVE || B == 64, "wave-per-node kernel needs B = 64");
-  using FT = typename std::conditional<WAVE, uint32_t, uint8_t>::type;
+  static_assert(!HALF || B == 32, "half-wave kernel needs B = 32");
+  using FT = typename std::conditional<WAVE || HALF, uint32_t, uint8_t>::type;
   constexpr int G = 64 / B;
   hipStream_t st = ctx->stream;
   const uint32_t n = net->n_nodes;
@@ -799,6 +892,17 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
             const uint32_t nvb1 = (n + RELAX_WAVES * 4 - 1) / (RELAX_WAVES * 4);
             hipLaunchKernelGGL(k_relax_v1<4>, dim3(nvb1, gb), dim3(RELAX_BLOCK), 0, st, net->in_off, net->in_src,
                                net->in_lat, net->in_om, D, n, active, changed);
+          } else if constexpr (HALF) {
+            const uint32_t nvh = (n + RELAX_WAVES * 2 * VPW - 1) / (RELAX_WAVES * 2 * VPW);
+            const uint32_t gridh = XCD ? 8 * nvh * ((gb + 7) / 8) : nvh * gb;
+            if (work)
+              hipLaunchKernelGGL((k_relax_half<VPW, XCD, FLAGS, true>), dim3(gridh), dim3(RELAX_BLOCK), 0, st,
+                                 net->in_off, net->in_src, net->in_lat, net->in_om, D, n, nvh, gb, active, changed,
+                                 (const uint32_t*)dprev, (uint32_t*)dcur, work);
+            else
+              hipLaunchKernelGGL((k_relax_half<VPW, XCD, FLAGS, false>), dim3(gridh), dim3(RELAX_BLOCK), 0, st,
+                                 net->in_off, net->in_src, net->in_lat, net->in_om, D, n, nvh, gb, active, changed,
+                                 (const uint32_t*)dprev, (uint32_t*)dcur, work);
           } else if constexpr (WAVE) {
             const uint32_t nvw = (n + RELAX_WAVES * VPW - 1) / (RELAX_WAVES * VPW);
             if (work)
@@ -860,6 +964,16 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
     shortest_paths_t<B, VPW, X, F, W>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss); \
     return;                                                                                          \
   }
+#define SG_VARH(name, VPW, X, F)                                                                     \
+  if (var == name) {                                                                                 \
+    shortest_paths_t<32, VPW, X, F, false, true>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, \
+                                                 out_loss);                                          \
+    return;                                                                                          \
+  }
+  SG_VARH("h32x", 4, true, false)
+  SG_VARH("h32xf", 4, true, true)
+  SG_VARH("h32", 4, false, false)
+  SG_VARH("h32xv2", 2, true, false)
   SG_VAR("w64f", 64, 4, false, true, true)
   SG_VAR("w64", 64, 4, false, false, true)
   SG_VAR("32xf", 32, 4, true, true, false)
@@ -871,6 +985,7 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
   SG_VAR("64f", 64, 4, false, true, false)
   SG_VAR("64", 64, 4, false, false, false)
 #undef SG_VAR
+#undef SG_VARH
   throw Error(SG_ERR_INVALID_ARG, "unknown SG_APSP_VARIANT " + var);
 }
 
