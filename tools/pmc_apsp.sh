@@ -4,7 +4,7 @@ set -u
 TAG=$1; shift
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_$TAG; mkdir -p $OUT
-CMD="python3 tools/apsp_variants.py --variants w64 --reps 1"
+CMD="python3 tools/apsp_variants.py --variants ${VARIANT:-w64} --reps 1"
 run() { name=$1; shift; timeout -k 10 200 env "$ENVS" rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o run -- $CMD > $OUT/$name.log 2>&1 || echo "pass $name failed"; }
 ENVS="${1:-X=1}"
 run sq SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU
