@@ -278,15 +278,24 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
 // instead (an L1 hit), keeping the four loads per step branch-free and in
 // flight together.  Linear batch-major grid: all CUs work on the same one or
 // two batches, whose slab rows stay hot in L2 / Infinity Cache.
-template <int VPW, bool FLAGS, bool COUNT>
+template <int VPW, bool FLAGS, bool COUNT, bool XCD = false>
 __global__ void __launch_bounds__(RELAX_BLOCK)
     k_relax_wave(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
                  const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om,
                  uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ active,
                  uint32_t* __restrict__ changed, const uint32_t* dprev, uint32_t* dcur,
-                 unsigned long long* __restrict__ work) {
+                 unsigned long long* __restrict__ work, uint32_t nvb = 0, uint32_t n_batches = 0) {
   constexpr int B = 64;
-  const uint32_t b = blockIdx.y;
+  uint32_t b, chunk;
+  if (XCD) {  // 1-D grid: block L on XCD L % 8 serves batch (L % 8) + 8 * ((L / 8) / nvb)
+    const uint32_t x = blockIdx.x & 7, q = blockIdx.x >> 3;
+    b = x + 8 * (q / nvb);
+    chunk = q % nvb;
+    if (b >= n_batches) return;
+  } else {
+    b = blockIdx.y;
+    chunk = blockIdx.x;
+  }
   if (!active[b]) return;
   uint64_t* __restrict__ Db = D + (size_t)b * n * B;
   const uint32_t* Pf = dprev + (size_t)b * n;
@@ -295,7 +304,7 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   bool any = false;
   uint32_t n_relax = 0;  // wave-uniform count of dirty arcs (COUNT builds only)
-  const uint32_t v0 = (blockIdx.x * RELAX_WAVES + wave) * VPW;
+  const uint32_t v0 = (chunk * RELAX_WAVES + wave) * VPW;
 #pragma unroll 1
   for (int k = 0; k < VPW; k++) {
     const uint32_t v = v0 + k;
@@ -905,14 +914,15 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
                                  (const uint32_t*)dprev, (uint32_t*)dcur, work);
           } else if constexpr (WAVE) {
             const uint32_t nvw = (n + RELAX_WAVES * VPW - 1) / (RELAX_WAVES * VPW);
+            const dim3 gw = XCD ? dim3(8 * nvw * ((gb + 7) / 8)) : dim3(nvw, gb);
             if (work)
-              hipLaunchKernelGGL((k_relax_wave<VPW, FLAGS, true>), dim3(nvw, gb), dim3(RELAX_BLOCK), 0, st,
+              hipLaunchKernelGGL((k_relax_wave<VPW, FLAGS, true, XCD>), gw, dim3(RELAX_BLOCK), 0, st,
                                  net->in_off, net->in_src, net->in_lat, net->in_om, D, n, active, changed,
-                                 (const uint32_t*)dprev, (uint32_t*)dcur, work);
+                                 (const uint32_t*)dprev, (uint32_t*)dcur, work, nvw, gb);
             else
-              hipLaunchKernelGGL((k_relax_wave<VPW, FLAGS, false>), dim3(nvw, gb), dim3(RELAX_BLOCK), 0, st,
+              hipLaunchKernelGGL((k_relax_wave<VPW, FLAGS, false, XCD>), gw, dim3(RELAX_BLOCK), 0, st,
                                  net->in_off, net->in_src, net->in_lat, net->in_om, D, n, active, changed,
-                                 (const uint32_t*)dprev, (uint32_t*)dcur, work);
+                                 (const uint32_t*)dprev, (uint32_t*)dcur, work, nvw, gb);
           } else {
             hipLaunchKernelGGL((k_relax_front<B, VPW, XCD, FLAGS>), dim3(grid), dim3(RELAX_BLOCK), 0, st,
                                net->in_off, net->in_src, net->in_lat, net->in_om, D, n, map, active, changed,
@@ -974,6 +984,9 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
   SG_VARH("h32xf", 4, true, true)
   SG_VARH("h32", 4, false, false)
   SG_VARH("h32xv2", 2, true, false)
+  SG_VAR("w64x", 64, 4, true, false, true)
+  SG_VAR("w64xf", 64, 4, true, true, true)
+  SG_VAR("w64v8", 64, 8, false, false, true)
   SG_VAR("w64f", 64, 4, false, true, true)
   SG_VAR("w64", 64, 4, false, false, true)
   SG_VAR("32xf", 32, 4, true, true, false)
