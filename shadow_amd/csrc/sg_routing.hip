@@ -968,7 +968,7 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                            uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
   const char* v = getenv("SG_APSP_VARIANT");
-  std::string var = v && *v ? v : "32xf";
+  std::string var = v && *v ? v : "w64xv32";
 #define SG_VAR(name, B, VPW, X, F, W)                                                                \
   if (var == name) {                                                                                 \
     shortest_paths_t<B, VPW, X, F, W>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss); \
@@ -987,6 +987,15 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
   SG_VAR("w64x", 64, 4, true, false, true)
   SG_VAR("w64xf", 64, 4, true, true, true)
   SG_VAR("w64v8", 64, 8, false, false, true)
+  SG_VAR("w64v16", 64, 16, false, false, true)
+  SG_VAR("w64v32", 64, 32, false, false, true)
+  SG_VAR("w64xv8", 64, 8, true, false, true)
+  SG_VAR("w64xv16", 64, 16, true, false, true)
+  SG_VAR("w64fv16", 64, 16, false, true, true)
+  SG_VAR("w64v64", 64, 64, false, false, true)
+  SG_VAR("w64v128", 64, 128, false, false, true)
+  SG_VAR("w64xv32", 64, 32, true, false, true)
+  SG_VAR("w64xv64", 64, 64, true, false, true)
   SG_VAR("w64f", 64, 4, false, true, true)
   SG_VAR("w64", 64, 4, false, false, true)
   SG_VAR("32xf", 32, 4, true, true, false)
