@@ -145,15 +145,15 @@ def main():
     # instrumented pass: per-kernel device time of the dominant kernel on its stream
     ctx.enable_timers(True)
     build()
-    relax_ms, relax_launches, relax_work = ctx.read_timer("relax_packed")
-    out_ms, _, _ = ctx.read_timer("out_packed")
+    relax_ms, relax_launches, relax_work = ctx.read_timer("relax")
+    out_ms, _, _ = ctx.read_timer("out")
     ctx.enable_timers(False)
     n_arcs = int(net.edge_src.size * 2 - 2 * np.count_nonzero(net.edge_src == net.edge_dst))
     avg_launch_s = relax_ms / 1e3 / max(relax_launches, 1)
     ops_per_launch = 2.0 * relax_work / max(relax_launches, 1)  # add + min per relaxation
     achieved = ops_per_launch / avg_launch_s / 1e12 if relax_launches else 0.0
-    pm = pmc.get("relax_packed", {})
-    roofline = {"kernel": "k_relax_packed", "bound": "valu", "achieved": round(achieved, 3),
+    pm = pmc.get("relax", {})
+    roofline = {"kernel": "k_relax", "bound": "valu", "achieved": round(achieved, 3),
                 "peak": round(VALU_PEAK_TOPS, 1), "unit": "Tops/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
                 "traffic": pm.get("hbm_bytes_per_launch"),
                 "avg_launch_ms": round(avg_launch_s * 1e3, 4), "launches_per_build": relax_launches,

@@ -12,21 +12,19 @@ namespace sg {
 // ---------------------------------------------------------------------------
 // Packed lexicographic path key.
 // PathProperties (graph/mod.rs:297-313) orders by latency, then packet loss.
-// Loss is a non-negative f32 in [0, 1] whose bit pattern (<= 0x3F800000 < 2^30)
-// is order-preserving, so key = (latency << 30) | bits(loss) compares like
-// PathProperties as one u64 while latency < 2^34 - 1 (17.2 s).  Latency
-// saturates at LAT_SAT; any saturated key marks "overflow or unreachable" and
-// the row falls back to the wide (u64 latency + f32 loss) kernel.
+// Loss is a non-negative f32 in [0, 1], whose bit pattern is order-preserving,
+// so key = (latency u32 << 32) | bits(loss) compares like PathProperties as one
+// u64, and one 64-bit store is an untorn (latency, loss) update.  Latency adds
+// saturate at LAT32_SAT (v_add_u32 clamp); a key whose latency reached
+// LAT32_SAT means "overflow or unreachable" and its row is redone by the wide
+// (u64 latency + f32 loss) kernel.  KEY_INF = (LAT32_SAT, loss 1.0) is a fixed
+// point of relax32: sat(LAT32_SAT + l) = LAT32_SAT and 1 - (1 - 1) * om = 1.
 // ---------------------------------------------------------------------------
-constexpr int LOSS_BITS = 30;
-constexpr uint64_t LOSS_MASK = (1ull << LOSS_BITS) - 1;
-constexpr uint64_t LAT_SAT = (1ull << (64 - LOSS_BITS)) - 1;  // 2^34 - 1
-constexpr uint64_t KEY_INF = ~0ull;                            // (LAT_SAT << 30) | LOSS_MASK
+constexpr uint32_t LAT32_SAT = 0xFFFFFFFFu;
+constexpr uint64_t KEY_INF = 0xFFFFFFFF3F800000ull;
 
-__host__ __device__ __forceinline__ uint64_t key_lat(uint64_t k) { return k >> LOSS_BITS; }
-__host__ __device__ __forceinline__ uint32_t key_loss_bits(uint64_t k) {
-  return (uint32_t)(k & LOSS_MASK);
-}
+__host__ __device__ __forceinline__ uint32_t key_lat(uint64_t k) { return (uint32_t)(k >> 32); }
+__host__ __device__ __forceinline__ uint32_t key_loss_bits(uint64_t k) { return (uint32_t)k; }
 
 // PathProperties::add (graph/mod.rs:322-331) with the edge's (1f32 - loss)
 // precomputed: loss' = 1f32 - (1f32 - a) * (1f32 - e).  The subtraction
@@ -37,13 +35,12 @@ __device__ __forceinline__ float fold_loss(float a, float one_minus_e) {
   return __fsub_rn(1.0f, prod);
 }
 
-// key(u) + edge, latency saturating at LAT_SAT.  edge_lat is pre-clamped to
-// LAT_SAT on upload, so the u64 sum cannot wrap.
-__device__ __forceinline__ uint64_t relax_key(uint64_t ku, uint64_t edge_lat, float edge_om) {
-  uint64_t lat = key_lat(ku) + edge_lat;
-  lat = lat < LAT_SAT ? lat : LAT_SAT;
-  float loss = fold_loss(__uint_as_float(key_loss_bits(ku)), edge_om);
-  return (lat << LOSS_BITS) | (uint64_t)__float_as_uint(loss);
+// key(u) + edge: one saturating u32 add and the three-op f32 fold.  The edge
+// latency is clamped to LAT32_SAT on upload.
+__device__ __forceinline__ uint64_t relax32(uint64_t ku, uint32_t edge_lat, float edge_om) {
+  const uint32_t lat = __builtin_elementwise_add_sat(key_lat(ku), edge_lat);
+  const float loss = fold_loss(__uint_as_float(key_loss_bits(ku)), edge_om);
+  return ((uint64_t)lat << 32) | (uint64_t)__float_as_uint(loss);
 }
 
 // ---------------------------------------------------------------------------

@@ -44,13 +44,20 @@ struct sg_net {
   // in-arc CSC without self-loops (device)
   uint32_t* in_off = nullptr;  // n_nodes + 1
   uint32_t* in_src = nullptr;
-  uint64_t* in_lat = nullptr;
-  float* in_om = nullptr;  // 1f32 - loss
+  uint32_t* in_dst = nullptr;
+  uint64_t* in_lat = nullptr;    // exact latency (wide kernel)
+  uint32_t* in_lat32 = nullptr;  // latency clamped to LAT32_SAT (packed-key kernel)
+  float* in_om = nullptr;        // 1f32 - loss
+  std::vector<uint32_t> h_in_off;  // host copy of in_off
+  // relaxation chunks: chunk c = destination nodes [chunk_v[c], chunk_v[c + 1])
+  uint32_t n_chunks = 0, chunk_nodes = 0, chunk_arcs = 0;
+  uint32_t* chunk_v = nullptr;
   // self-loops
   uint32_t* self_cnt = nullptr;
   uint32_t* self_edge = nullptr;
   ~sg_net() {
-    void* ps[] = {e_src, e_dst, e_lat, e_loss, in_off, in_src, in_lat, in_om, self_cnt, self_edge};
+    void* ps[] = {e_src, e_dst, e_lat, e_loss, in_off, in_src, in_dst, in_lat, in_lat32, in_om, chunk_v, self_cnt,
+                  self_edge};
     for (void* p : ps)
       if (p) (void)hipFree(p);
   }
@@ -59,10 +66,9 @@ struct sg_net {
 namespace sg {
 
 constexpr int BATCH = 64;         // sources per batch = wave width
-constexpr int RELAX_WAVES = 4;    // waves per block
+constexpr int RELAX_WAVES = 4;    // waves per block (wide kernel)
 constexpr int RELAX_BLOCK = RELAX_WAVES * 64;
 constexpr int WORK_SHARDS = 64;  // relaxation counter shards (measurement only)
-constexpr int ARC_CHUNK = 1024;  // in-arcs staged in LDS per block step
 
 // ---------------------------------------------------------------------------
 // Graph upload: CSC of in-arcs (both directions when undirected, petgraph
@@ -86,449 +92,380 @@ __global__ void k_count_arcs(const uint32_t* __restrict__ src, const uint32_t* _
 __global__ void k_scatter_arcs(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
                                const uint64_t* __restrict__ lat, const float* __restrict__ loss,
                                uint32_t m, int directed, uint32_t* __restrict__ cursor,
-                               uint32_t* __restrict__ in_src, uint64_t* __restrict__ in_lat,
+                               uint32_t* __restrict__ in_src, uint32_t* __restrict__ in_dst,
+                               uint64_t* __restrict__ in_lat, uint32_t* __restrict__ in_lat32,
                                float* __restrict__ in_om) {
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < m; e += gridDim.x * blockDim.x) {
     uint32_t s = src[e], d = dst[e];
     if (s == d) continue;  // a self-loop never improves D[s][v] (latency >= 1)
-    float om = __fsub_rn(1.0f, loss[e]);
+    const float om = __fsub_rn(1.0f, loss[e]);
+    const uint64_t l = lat[e];
+    const uint32_t l32 = l < LAT32_SAT ? (uint32_t)l : LAT32_SAT;
     uint32_t p = atomicAdd(&cursor[d], 1u);
     in_src[p] = s;
-    in_lat[p] = lat[e];
+    in_dst[p] = d;
+    in_lat[p] = l;
+    in_lat32[p] = l32;
     in_om[p] = om;
     if (!directed) {
       uint32_t q = atomicAdd(&cursor[s], 1u);
       in_src[q] = d;
-      in_lat[q] = lat[e];
+      in_dst[q] = s;
+      in_lat[q] = l;
+      in_lat32[q] = l32;
       in_om[q] = om;
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// Packed-key batched relaxation, B sources per batch.
+// Batched-source relaxation (the hot kernel).
 //
-// Slab layout D[batch][node][B] (u64 keys).  With B = 32 a batch's slab is
-// n x 256 B -- 2.56 MB at n = 10k, inside one XCD's 4 MB L2.  A wave owns
-// G = 64 / B destination nodes (one per B-lane group; lane % B = source).
+// 64 sources per batch (lane = source).  A batch's distance slab is laid out
+// D[node][64] (u64 keys, 512 B per node), so one in-arc u -> v costs one
+// coalesced 512-B read of D[u][0..63] and 64 independent relaxations.
+//
+// A block owns a chunk of consecutive destination nodes (<= CHUNK_NODES, about
+// CHUNK_ARCS in-arcs; chunk table built per graph).  Its in-arcs are
+// contiguous in the CSC, so the four waves split them into groups of GROUP
+// arcs: per group the arc fields are wave-uniform scalar loads, the GROUP row
+// reads are issued back to back, and each candidate is folded into the
+// destination's LDS row with ds_min_u64 -- no per-node serialisation, hub nodes
+// spread over all waves.  At the end the block compares each LDS row with the
+// node's key at block start and writes improved keys in place (Gauss-Seidel:
+// later blocks of the same pass may already read them).
 //
 // XCD-aware 1-D grid: dispatch deals blocks round-robin over the 8 XCDs
 // (MI355X_MICROARCH.md, "Workgroup dispatch"), so block L runs on XCD L % 8.
-// Block L serves batch (L % 8) + 8 * ((L / 8) / nvb) and node chunk
-// (L / 8) % nvb: every block of a batch lands on the same XCD, whose L2 then
-// holds the batch's slab.  Placement changes speed only, never results.
+// Block L serves batch (L % 8) + 8 * ((L / 8) / n_chunks), chunk (L / 8) %
+// n_chunks: the blocks of one batch share an XCD, whose L2 holds most of the
+// batch's slab.  Placement changes speed only, never results.
 //
-// Frontier: dirty[batch][node] bytes mark nodes whose key changed in the
-// previous pass (dprev) or earlier in this pass (dcur, read racily).  Arc
-// (u -> v) is relaxed only if u is dirty.  Exactness: every change of u sets
-// dcur[u]; in the next pass every out-neighbour re-reads u (across a kernel
-// boundary, so the value is visible), and the iteration stops only after a
-// pass with no change anywhere -- which is then the fixed point.
+// Frontier (FRONT): stamp[batch][node] = p + 2 when the node's key changed in
+// pass p (sources start at 1).  In pass p an arc is relaxed only when its
+// source's stamp >= p + 1, i.e. the source changed in pass p - 1 or earlier in
+// pass p.  Exactness: a value written in pass p is re-read by every out-arc in
+// pass p + 1 (a kernel boundary, so visible), and iteration stops only after a
+// pass with no change anywhere -- then every arc satisfies D[v] <= D[u] (+) w,
+// the fixed point, which is petgraph's Dijkstra result (see header).
 // ---------------------------------------------------------------------------
-struct BatchMap {
-  uint32_t nvb, n_batches;
-  __device__ __forceinline__ bool decode(uint32_t L, uint32_t& batch, uint32_t& chunk) const {
-    const uint32_t x = L & 7, k = L >> 3;
-    batch = x + 8 * (k / nvb);
-    chunk = k % nvb;
-    return batch < n_batches;
-  }
-};
+constexpr int GROUP = 8;           // row reads in flight per wave step
+constexpr int RELAX_THREADS = 256;
+constexpr uint32_t FLAG_STRIDE = 32;  // per-batch pass flags 128 B apart: no two batches share a cache line
 
-template <int B>
-__global__ void k_init_front(uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ used,
-                             uint32_t first_row, uint32_t row_end, uint32_t n_batches) {
-  const size_t total = (size_t)n_batches * n * B;
+// Timing experiments only (tools/ab builds): plain LDS stores instead of ds_min_u64.
+#ifdef SG_EXPERIMENT_NOATOMIC
+#define SG_LDS_MIN(p, v) (*(p) = (v))
+#else
+#define SG_LDS_MIN(p, v) atomicMin((p), (v))
+#endif
+
+// One 8-B key through a buffer descriptor (32-bit per-lane byte offset).  An
+// offset of OOB is outside every slab: the load returns 0 and touches no memory.
+constexpr uint32_t OOB = 0x80000000u;
+__device__ __forceinline__ uint64_t load_key(__amdgpu_buffer_rsrc_t rsrc, uint32_t off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0);
+  return ((uint64_t)v[1] << 32) | v[0];
+}
+
+__global__ void k_init_batch(uint64_t* __restrict__ D, uint32_t* __restrict__ stamp, uint32_t n,
+                             const uint32_t* __restrict__ used, uint32_t first_row, uint32_t row_end,
+                             uint32_t n_batches) {
+  const size_t total = (size_t)n_batches * n * BATCH;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t s = (uint32_t)(i % B);
-    const size_t bv = i / B;
+    const uint32_t s = (uint32_t)(i % BATCH);
+    const size_t bv = i / BATCH;
     const uint32_t v = (uint32_t)(bv % n);
     const uint32_t b = (uint32_t)(bv / n);
-    const uint32_t row = first_row + b * B + s;
-    D[i] = (row < row_end && used[row] == v) ? 0ull : KEY_INF;  // PathProperties::default()
+    const uint32_t row = first_row + b * BATCH + s;
+    const bool src = row < row_end && used[row] == v;
+    D[i] = src ? 0ull : KEY_INF;  // PathProperties::default() at the source
+    if (s == 0) stamp[bv] = 0;
   }
 }
 
-template <int B, class FT>
-__global__ void k_mark_sources(FT* __restrict__ dirty, uint32_t n, const uint32_t* __restrict__ used,
-                               uint32_t first_row, uint32_t row_end, uint32_t n_batches) {
+__global__ void k_stamp_sources(uint32_t* __restrict__ stamp, uint32_t n, const uint32_t* __restrict__ used,
+                                uint32_t first_row, uint32_t row_end, uint32_t n_batches) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_batches * B) return;
-  const uint32_t b = t / B, row = first_row + t;
-  if (row < row_end) dirty[(size_t)b * n + used[row]] = 1;
+  if (t >= n_batches * BATCH) return;
+  const uint32_t row = first_row + t;
+  if (row < row_end) stamp[(size_t)(t / BATCH) * n + used[row]] = 1;
 }
 
-template <int B, int VPW, bool XCD, bool FLAGS>
-__global__ void __launch_bounds__(RELAX_BLOCK)
-    k_relax_front(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
-                  const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om, uint64_t* D,
-                  uint32_t n, BatchMap map, const uint32_t* __restrict__ active,
-                  uint32_t* __restrict__ changed, const uint8_t* dprev, uint8_t* dcur,
-                  unsigned long long* __restrict__ work) {
-  constexpr int G = 64 / B;
-  constexpr int NB = RELAX_WAVES * G * VPW;  // destination nodes per block
-  // Staged in-arcs of the block's nodes: source (bit 31 = source is dirty),
-  // clamped latency, 1 - loss.  Loaded coalesced, so the inner loop's only
-  // global access is the independent distance-row read of each dirty arc.
-  __shared__ uint32_t s_u[ARC_CHUNK];
-  __shared__ uint64_t s_lat[ARC_CHUNK];
-  __shared__ float s_om[ARC_CHUNK];
-  __shared__ unsigned long long wblk[RELAX_WAVES];
-  uint32_t b, chunk;
-  if (XCD) {
-    if (!map.decode(blockIdx.x, b, chunk) || !active[b]) return;
-  } else {
-    b = blockIdx.x / map.nvb;
-    chunk = blockIdx.x % map.nvb;
-    if (b >= map.n_batches || !active[b]) return;
-  }
-  uint64_t* Db = D + (size_t)b * n * B;
-  const uint8_t* Pf = dprev + (size_t)b * n;
-  uint8_t* Cf = dcur + (size_t)b * n;
+// CN = destination nodes per chunk (LDS rows: CN x 512 B); STG = arcs staged
+// per block step (LDS list: STG x 16 B).
+template <int CN, int STG, bool FRONT, bool COUNT>
+__global__ void __launch_bounds__(RELAX_THREADS)
+    k_relax(const uint32_t* __restrict__ chunk_v, uint32_t n_chunks, const uint32_t* __restrict__ in_off,
+            const uint32_t* __restrict__ in_src, const uint32_t* __restrict__ in_dst,
+            const uint32_t* __restrict__ in_lat32, const float* __restrict__ in_om, uint64_t* __restrict__ D,
+            uint32_t n, uint32_t n_batches, const uint32_t* __restrict__ active, uint32_t* __restrict__ changed,
+            uint32_t* __restrict__ stamp, uint32_t pass, unsigned long long* __restrict__ work) {
+  constexpr int WAVES = RELAX_THREADS / 64;
+  constexpr int ROWS = CN / WAVES;  // own rows per wave at flush
+  __shared__ unsigned long long best[CN * BATCH];
+  __shared__ uint4 list[STG];  // staged arcs: (source, LDS byte offset of the destination row, latency, 1 - loss)
+  __shared__ uint32_t n_list;
+  const uint32_t q = blockIdx.x >> 3;
+  const uint32_t b = (blockIdx.x & 7) + 8 * (q / n_chunks);
+  const uint32_t chunk = q % n_chunks;
+  if (b >= n_batches || !active[b * FLAG_STRIDE]) return;
   const int lane = threadIdx.x & 63;
-  const int g = lane / B, s = lane % B;
-  const uint32_t wave = threadIdx.x >> 6;
-  const uint64_t gmask = (B == 64) ? ~0ull : (((1ull << (B & 63)) - 1) << (g * B));
-  const uint32_t v0 = chunk * NB;
-  const uint32_t vq = v0 + (wave * G + g) * VPW;  // this lane group's first node
-  uint32_t lo[VPW], hi[VPW];
-  uint64_t cur[VPW], best[VPW];
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint64_t* Db = D + (size_t)b * n * BATCH;
+  const uint32_t* St = stamp + (size_t)b * n;
+  const uint32_t v0 = chunk_v[chunk], v1 = chunk_v[chunk + 1];
+  const uint32_t a0 = in_off[v0], a1 = in_off[v1];
+  // Rows of the batch slab through a buffer descriptor: a 32-bit per-lane offset,
+  // one VALU op per row address.
+  const __amdgpu_buffer_rsrc_t slab =
+      __builtin_amdgcn_make_buffer_rsrc(Db, 0, (int)(n * BATCH * 8u), 0x00020000);
+  const uint32_t lane8 = lane * 8;
+  bool init = false;
+  uint32_t n_rel = 0, n_cand = 0;
+  for (uint32_t c0 = a0; c0 < a1; c0 += STG) {
+    const uint32_t c1 = min(c0 + STG, a1);
+    if (threadIdx.x == 0) n_list = 0;
+    __syncthreads();
+    // 1. stage the dirty arcs of [c0, c1): coalesced arc reads, gathered stamps,
+    //    wave-ballot compaction (record order inside the list is irrelevant: min
+    //    is commutative)
+    constexpr int PER = STG / RELAX_THREADS;
+    uint32_t ua[PER];
+    bool dirty[PER];
 #pragma unroll
-  for (int k = 0; k < VPW; k++) {
-    const uint32_t v = vq + k;
-    const bool valid = v < n;
-    lo[k] = valid ? in_off[v] : 0;
-    hi[k] = valid ? in_off[v + 1] : 0;
-    cur[k] = valid ? Db[(size_t)v * B + s] : KEY_INF;
-    best[k] = cur[k];
-  }
-  const uint32_t a_begin = in_off[v0], a_end = in_off[min(v0 + NB, n)];
-  uint32_t n_relax = 0;
-  for (uint32_t c0 = a_begin; c0 < a_end; c0 += ARC_CHUNK) {
-    const uint32_t c1 = min(c0 + ARC_CHUNK, a_end);
-    for (uint32_t a = c0 + threadIdx.x; a < c1; a += RELAX_BLOCK) {
-      const uint32_t u = in_src[a];
-      const bool f = !FLAGS || (Pf[u] | Cf[u]);
-      s_u[a - c0] = u | (f ? 0x80000000u : 0u);
-      s_lat[a - c0] = min(in_lat[a], LAT_SAT);
-      s_om[a - c0] = in_om[a];
+    for (int i = 0; i < PER; i++) {
+      const uint32_t a = c0 + threadIdx.x + i * RELAX_THREADS;
+      ua[i] = in_src[min(a, c1 - 1)];
+    }
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+      const uint32_t a = c0 + threadIdx.x + i * RELAX_THREADS;
+      dirty[i] = a < c1 && (!FRONT || St[ua[i]] > pass);
+    }
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+      const uint32_t a = c0 + threadIdx.x + i * RELAX_THREADS;
+      const uint64_t m = __ballot(dirty[i]);
+      if (!m) continue;
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&n_list, (uint32_t)__popcll(m));
+      base = __shfl(base, 0, 64);
+      if (dirty[i]) {
+        const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+        list[pos] = make_uint4(ua[i], (in_dst[a] - v0) * (BATCH * 8), in_lat32[a], __float_as_uint(in_om[a]));
+      }
+    }
+    if (!init) {
+      for (uint32_t i = threadIdx.x; i < CN * BATCH; i += RELAX_THREADS) best[i] = KEY_INF;
     }
     __syncthreads();
+    const uint32_t cnt = n_list;
+    init = true;
+    n_cand += cnt;
+    if (COUNT) n_rel += cnt;
+    // 2. relax: GROUP row reads in flight per wave, candidates folded into LDS rows
+    uint32_t g = GROUP * w;
+    for (; g + GROUP <= cnt; g += GROUP * WAVES) {
+      uint4 r[GROUP];
+      uint64_t k[GROUP];
 #pragma unroll
-    for (int k = 0; k < VPW; k++) {
-      uint32_t a = max(lo[k], c0);
-      const uint32_t e = min(hi[k], c1);
-      uint64_t bk = best[k];
-      for (; a + 4 <= e; a += 4) {
-        const uint32_t x0 = s_u[a - c0], x1 = s_u[a + 1 - c0], x2 = s_u[a + 2 - c0], x3 = s_u[a + 3 - c0];
-        const size_t own = (size_t)(vq + k) * B + s;  // clean arcs re-read the node's own row (L1 hit)
-        const uint64_t k0 = Db[(x0 >> 31) ? (size_t)(x0 & 0x7fffffffu) * B + s : own];
-        const uint64_t k1 = Db[(x1 >> 31) ? (size_t)(x1 & 0x7fffffffu) * B + s : own];
-        const uint64_t k2 = Db[(x2 >> 31) ? (size_t)(x2 & 0x7fffffffu) * B + s : own];
-        const uint64_t k3 = Db[(x3 >> 31) ? (size_t)(x3 & 0x7fffffffu) * B + s : own];
-        n_relax += (x0 >> 31) + (x1 >> 31) + (x2 >> 31) + (x3 >> 31);
-        const uint64_t l0 = s_lat[a - c0], l1 = s_lat[a + 1 - c0], l2 = s_lat[a + 2 - c0], l3 = s_lat[a + 3 - c0];
-        const float o0 = s_om[a - c0], o1 = s_om[a + 1 - c0], o2 = s_om[a + 2 - c0], o3 = s_om[a + 3 - c0];
-        const uint64_t c0k = ((x0 >> 31) && k0 != KEY_INF) ? relax_key(k0, l0, o0) : KEY_INF;
-        const uint64_t c1k = ((x1 >> 31) && k1 != KEY_INF) ? relax_key(k1, l1, o1) : KEY_INF;
-        const uint64_t c2k = ((x2 >> 31) && k2 != KEY_INF) ? relax_key(k2, l2, o2) : KEY_INF;
-        const uint64_t c3k = ((x3 >> 31) && k3 != KEY_INF) ? relax_key(k3, l3, o3) : KEY_INF;
-        bk = min(bk, min(min(c0k, c1k), min(c2k, c3k)));
-      }
-      for (; a < e; a++) {
-        const uint32_t x = s_u[a - c0];
-        if (!(x >> 31)) continue;
-        n_relax++;
-        const uint64_t ku = Db[(size_t)(x & 0x7fffffffu) * B + s];
-        if (ku != KEY_INF) bk = min(bk, relax_key(ku, s_lat[a - c0], s_om[a - c0]));
-      }
-      best[k] = bk;
+      for (int j = 0; j < GROUP; j++) r[j] = list[g + j];
+#pragma unroll
+      for (int j = 0; j < GROUP; j++)
+        k[j] = load_key(slab, r[j].x * (BATCH * 8) + lane8);
+#pragma unroll
+      for (int j = 0; j < GROUP; j++)
+        SG_LDS_MIN((unsigned long long*)((char*)best + r[j].y + lane8),
+                  (unsigned long long)relax32(k[j], r[j].z, __uint_as_float(r[j].w)));
+    }
+    for (; g < cnt; g++) {  // tail: fewer than GROUP records left for this wave
+      const uint4 r = list[g];
+      const uint64_t k = load_key(slab, r.x * (BATCH * 8) + lane8);
+      SG_LDS_MIN((unsigned long long*)((char*)best + r.y + lane8),
+                (unsigned long long)relax32(k, r.z, __uint_as_float(r.w)));
     }
     __syncthreads();
   }
+  if (!n_cand) return;
+  // 3. flush: improved keys are written in place (one untorn 64-bit update each).
+  //    Rows that received no candidate are not read (out-of-range buffer load).
   bool any = false;
+  uint64_t nb[ROWS], cur[ROWS];
 #pragma unroll
-  for (int k = 0; k < VPW; k++) {
-    const uint32_t v = vq + k;
-    const bool ch = v < n && best[k] < cur[k];
-    if (ch) Db[(size_t)v * B + s] = best[k];  // one untorn 64-bit (lat, loss) update
-    const uint64_t m = __ballot(ch) & gmask;
-    if (m && s == 0) Cf[v] = 1;
-    any |= ch;
+  for (int i = 0; i < ROWS; i++) {
+    const uint32_t r = w + WAVES * i;
+    nb[i] = best[r * BATCH + lane];
+    const uint32_t v = min(v0 + r, v1 - 1);
+    cur[i] = load_key(slab, __any(nb[i] != KEY_INF) ? v * (BATCH * 8) + lane8 : OOB);
+  }
+#pragma unroll
+  for (int i = 0; i < ROWS; i++) {
+    const uint32_t v = v0 + w + WAVES * i;
+    const bool ch = v < v1 && nb[i] < cur[i];
+    if (ch) Db[(size_t)v * BATCH + lane] = nb[i];
+    if (__any(ch)) {
+      any = true;
+      if (FRONT && lane == 0) stamp[(size_t)b * n + v] = pass + 2;
+    }
   }
   // every writer stores the same 1: a plain store, no same-address atomic storm
-  if (__any(any) && lane == 0) __hip_atomic_store(&changed[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (work) {  // measurement only (timers on): block reduction, one add per block into a sharded counter
-    unsigned long long wsum = n_relax;
-    for (int d = 32; d > 0; d >>= 1) wsum += __shfl_xor(wsum, d, 64);
-    if (lane == 0) wblk[wave] = wsum;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned long long t = 0;
-      for (int w = 0; w < RELAX_WAVES; w++) t += wblk[w];
-      if (t) atomicAdd(&work[blockIdx.x & (WORK_SHARDS - 1)], t);
-    }
-  }
+  if (any && lane == 0) changed[b * FLAG_STRIDE] = 1u;
+  if (COUNT && threadIdx.x == 0 && n_rel)
+    atomicAdd(&work[blockIdx.x & (WORK_SHARDS - 1)], (unsigned long long)n_rel * BATCH);
 }
 
-// Wave-per-node relaxation (B = 64: lane = source).  The destination node is
-// wave-uniform, so in-arcs and frontier flags are scalar loads; each dirty
-// arc costs one coalesced 512-B row read.  Clean arcs read the node's own row
-// instead (an L1 hit), keeping the four loads per step branch-free and in
-// flight together.  Linear batch-major grid: all CUs work on the same one or
-// two batches, whose slab rows stay hot in L2 / Infinity Cache.
-template <int VPW, bool FLAGS, bool COUNT, bool XCD = false>
-__global__ void __launch_bounds__(RELAX_BLOCK)
-    k_relax_wave(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
-                 const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om,
-                 uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ active,
-                 uint32_t* __restrict__ changed, const uint32_t* dprev, uint32_t* dcur,
-                 unsigned long long* __restrict__ work, uint32_t nvb = 0, uint32_t n_batches = 0) {
-  constexpr int B = 64;
-  uint32_t b, chunk;
-  if (XCD) {  // 1-D grid: block L on XCD L % 8 serves batch (L % 8) + 8 * ((L / 8) / nvb)
-    const uint32_t x = blockIdx.x & 7, q = blockIdx.x >> 3;
-    b = x + 8 * (q / nvb);
-    chunk = q % nvb;
-    if (b >= n_batches) return;
-  } else {
-    b = blockIdx.y;
-    chunk = blockIdx.x;
-  }
-  if (!active[b]) return;
-  uint64_t* __restrict__ Db = D + (size_t)b * n * B;
-  const uint32_t* Pf = dprev + (size_t)b * n;
-  uint32_t* Cf = dcur + (size_t)b * n;
+// Wave-owned destinations: wave w of a block owns NPW consecutive nodes and
+// their best rows in its own LDS slice.  The wave's in-arcs are contiguous;
+// each staging round reads up to 64 * K of them (coalesced), compacts the dirty
+// ones into the wave's LDS list, then relaxes them GROUP at a time with GROUP
+// row reads in flight.  No block barriers and no LDS atomics (64-bit ds_min
+// measured 3x slower than this kernel's whole loop): every wave runs on its own.
+template <int NPW, int K, bool FRONT, bool COUNT>
+__global__ void __launch_bounds__(RELAX_THREADS)
+    k_relax_w(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
+              const uint32_t* __restrict__ in_dst, const uint32_t* __restrict__ in_lat32,
+              const float* __restrict__ in_om, uint64_t* __restrict__ D, uint32_t n, uint32_t n_batches,
+              const uint32_t* __restrict__ active, uint32_t* __restrict__ changed, uint32_t* __restrict__ stamp,
+              uint32_t pass, unsigned long long* __restrict__ work) {
+  constexpr int WAVES = RELAX_THREADS / 64;
+  constexpr int STG_W = 64 * K;
+  __shared__ uint4 lists[WAVES][STG_W];  // (source row byte offset, destination slot, latency, 1 - loss)
+  __shared__ unsigned long long bests[WAVES][NPW * BATCH];
   const int lane = threadIdx.x & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  bool any = false;
-  uint32_t n_relax = 0;  // wave-uniform count of dirty arcs (COUNT builds only)
-  const uint32_t v0 = (chunk * RELAX_WAVES + wave) * VPW;
-#pragma unroll 1
-  for (int k = 0; k < VPW; k++) {
-    const uint32_t v = v0 + k;
-    if (v >= n) break;
-    const uint32_t a0 = in_off[v], a1 = in_off[v + 1];
-    const size_t own = (size_t)v * B + lane;
-    const uint64_t cur = Db[own];
-    uint64_t best = cur;
-    uint32_t a = a0;
-    // 4 independent 512-B row reads in flight per wave
-    for (; a + 4 <= a1; a += 4) {
-      const uint32_t u0 = in_src[a], u1 = in_src[a + 1], u2 = in_src[a + 2], u3 = in_src[a + 3];
-      bool f0 = true, f1 = true, f2 = true, f3 = true;
-      if (FLAGS) {  // clean sources re-read the node's own row (an L1 hit): branch-free loads
-        f0 = (Pf[u0] | Cf[u0]) != 0;
-        f1 = (Pf[u1] | Cf[u1]) != 0;
-        f2 = (Pf[u2] | Cf[u2]) != 0;
-        f3 = (Pf[u3] | Cf[u3]) != 0;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane8 = lane * 8;
+  uint4* list = lists[w];
+  unsigned long long* best = bests[w];
+  // Work items (batch, wave chunk) of the batches b = x (mod 8) go to the blocks
+  // L = x (mod 8), i.e. to XCD x under round-robin dispatch; consecutive items
+  // are consecutive chunks of one batch, so an XCD's resident waves share a slab.
+  const uint32_t x = blockIdx.x & 7;
+  const uint32_t nwc = (n + NPW - 1) / NPW;
+  const uint32_t nbx = n_batches > x ? (n_batches - x + 7) / 8 : 0;
+  const uint32_t items = nbx * nwc;
+  const uint32_t stride = (gridDim.x >> 3) * WAVES;
+  uint32_t n_rel = 0, flagged = ~0u;
+  for (uint32_t it = (blockIdx.x >> 3) * WAVES + w; it < items; it += stride) {
+    const uint32_t b = x + 8 * (it / nwc);
+    const uint32_t vw = (it % nwc) * NPW;
+    if (!active[b * FLAG_STRIDE]) continue;
+    const uint32_t vw1 = min(vw + NPW, n);
+    uint64_t* Db = D + (size_t)b * n * BATCH;
+    const uint32_t* St = stamp + (size_t)b * n;
+    const __amdgpu_buffer_rsrc_t slab =
+        __builtin_amdgcn_make_buffer_rsrc(Db, 0, (int)(n * BATCH * 8u), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < NPW; i++) best[i * BATCH + lane] = KEY_INF;
+    const uint32_t a0 = in_off[vw], a1 = in_off[vw1];
+    uint32_t n_cand = 0;
+    uint32_t run_slot = 0;
+    uint64_t run = KEY_INF;
+    for (uint32_t c0 = a0; c0 < a1; c0 += STG_W) {
+      const uint32_t c1 = min(c0 + STG_W, a1);
+      uint32_t ua[K];
+      bool dirty[K];
+#pragma unroll
+      for (int i = 0; i < K; i++) ua[i] = in_src[min(c0 + lane + 64 * i, c1 - 1)];
+#pragma unroll
+      for (int i = 0; i < K; i++) dirty[i] = c0 + lane + 64 * i < c1 && (!FRONT || St[ua[i]] > pass);
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int i = 0; i < K; i++) {
+        const uint32_t a = min(c0 + lane + 64 * i, c1 - 1);
+        const uint64_t m = __ballot(dirty[i]);
+        if (dirty[i])
+          list[cnt + (uint32_t)__popcll(m & ((1ull << lane) - 1))] =
+              make_uint4(ua[i] * (BATCH * 8), in_dst[a] - vw, in_lat32[a], __float_as_uint(in_om[a]));
+        cnt += (uint32_t)__popcll(m);
       }
-      if (COUNT) n_relax += (uint32_t)f0 + (uint32_t)f1 + (uint32_t)f2 + (uint32_t)f3;
-      const uint64_t k0 = Db[f0 ? (size_t)u0 * B + lane : own];
-      const uint64_t k1 = Db[f1 ? (size_t)u1 * B + lane : own];
-      const uint64_t k2 = Db[f2 ? (size_t)u2 * B + lane : own];
-      const uint64_t k3 = Db[f3 ? (size_t)u3 * B + lane : own];
-      const uint64_t l0 = min(in_lat[a], LAT_SAT), l1 = min(in_lat[a + 1], LAT_SAT);
-      const uint64_t l2 = min(in_lat[a + 2], LAT_SAT), l3 = min(in_lat[a + 3], LAT_SAT);
-      const float o0 = in_om[a], o1 = in_om[a + 1], o2 = in_om[a + 2], o3 = in_om[a + 3];
-      const uint64_t c0 = (!f0 || k0 == KEY_INF) ? KEY_INF : relax_key(k0, l0, o0);
-      const uint64_t c1 = (!f1 || k1 == KEY_INF) ? KEY_INF : relax_key(k1, l1, o1);
-      const uint64_t c2 = (!f2 || k2 == KEY_INF) ? KEY_INF : relax_key(k2, l2, o2);
-      const uint64_t c3 = (!f3 || k3 == KEY_INF) ? KEY_INF : relax_key(k3, l3, o3);
-      best = min(best, min(min(c0, c1), min(c2, c3)));
-    }
-    for (; a < a1; a++) {
-      const uint32_t u = in_src[a];
-      const bool f = !FLAGS || (Pf[u] | Cf[u]) != 0;
-      if (COUNT) n_relax += f;
-      const uint64_t ku = Db[f ? (size_t)u * B + lane : own];
-      const uint64_t l = min(in_lat[a], LAT_SAT);
-      const float o = in_om[a];
-      const uint64_t c = (!f || ku == KEY_INF) ? KEY_INF : relax_key(ku, l, o);
-      best = min(best, c);
-    }
-    if (best < cur) {
-      Db[own] = best;  // one untorn 64-bit (lat, loss) update
-      any = true;
-    }
-    if (FLAGS && __any(best < cur) && lane == 0) Cf[v] = 1u;
-  }
-  if (__any(any) && lane == 0) atomicOr(&changed[b], 1u);
-  if (COUNT && lane == 0 && n_relax) atomicAdd(&work[(blockIdx.x + blockIdx.y) & (WORK_SHARDS - 1)],
-                                              (unsigned long long)n_relax * B);
-}
-
-
-// B = 32 sources per batch, two half-waves on adjacent destination nodes.
-// XCD=true: block L runs batch (L % 8) + 8 * ((L / 8) / nvb) so every block of
-// a batch shares an XCD (round-robin dispatch) and its 2.56 MB slab stays in
-// that XCD's 4 MB L2.  Load scheduling as in the wave kernel: weights loaded
-// unconditionally, row loads branch-free (clean arcs re-read the own row).
-template <int VPW, bool XCD, bool FLAGS, bool COUNT>
-__global__ void __launch_bounds__(RELAX_BLOCK)
-    k_relax_half(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
-                 const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om,
-                 uint64_t* __restrict__ D, uint32_t n, uint32_t nvb, uint32_t n_batches,
-                 const uint32_t* __restrict__ active, uint32_t* __restrict__ changed,
-                 const uint32_t* dprev, uint32_t* dcur, unsigned long long* __restrict__ work) {
-  constexpr int B = 32;
-  uint32_t b, chunk;
-  if (XCD) {
-    const uint32_t x = blockIdx.x & 7, q = blockIdx.x >> 3;
-    b = x + 8 * (q / nvb);
-    chunk = q % nvb;
-  } else {
-    b = blockIdx.x / nvb;
-    chunk = blockIdx.x % nvb;
-  }
-  if (b >= n_batches || !active[b]) return;
-  uint64_t* __restrict__ Db = D + (size_t)b * n * B;
-  const uint32_t* Pf = dprev + (size_t)b * n;
-  uint32_t* Cf = dcur + (size_t)b * n;
-  const int lane = threadIdx.x & 63;
-  const int g = lane >> 5, s = lane & 31;
-  const uint32_t wave = threadIdx.x >> 6;
-  bool any = false;
-  uint32_t n_relax = 0;
-  const uint32_t v0 = (chunk * RELAX_WAVES + wave) * (2 * VPW);
-#pragma unroll 1
-  for (int k = 0; k < VPW; k++) {
-    const uint32_t v = v0 + 2 * k + g;
-    const bool valid = v < n;
-    const uint32_t a0 = valid ? in_off[v] : 0, a1 = valid ? in_off[v + 1] : 0;
-    const size_t own = valid ? (size_t)v * B + s : (size_t)s;
-    const uint64_t cur = valid ? Db[own] : KEY_INF;
-    uint64_t best = cur;
-    uint32_t a = a0;
-    for (; a + 4 <= a1; a += 4) {
-      const uint32_t u0 = in_src[a], u1 = in_src[a + 1], u2 = in_src[a + 2], u3 = in_src[a + 3];
-      bool f0 = true, f1 = true, f2 = true, f3 = true;
-      if (FLAGS) {
-        f0 = (Pf[u0] | Cf[u0]) != 0;
-        f1 = (Pf[u1] | Cf[u1]) != 0;
-        f2 = (Pf[u2] | Cf[u2]) != 0;
-        f3 = (Pf[u3] | Cf[u3]) != 0;
+      n_cand += cnt;
+      // Records arrive in destination order (CSC order, compaction keeps it), so
+      // each destination's candidates form one run, folded in registers; the run
+      // is stored to the destination's LDS row when the destination changes.
+      uint32_t g = 0;
+      for (; g + GROUP <= cnt; g += GROUP) {
+        uint4 r[GROUP];
+        uint64_t k[GROUP];
+#pragma unroll
+        for (int j = 0; j < GROUP; j++) r[j] = list[g + j];
+#pragma unroll
+        for (int j = 0; j < GROUP; j++) k[j] = load_key(slab, r[j].x + lane8);
+#pragma unroll
+        for (int j = 0; j < GROUP; j++) {
+          const uint32_t slot = __builtin_amdgcn_readfirstlane(r[j].y);
+          if (slot != run_slot) {
+            best[run_slot * BATCH + lane] = run;
+            run_slot = slot;
+            run = KEY_INF;
+          }
+          run = min(run, relax32(k[j], r[j].z, __uint_as_float(r[j].w)));
+        }
       }
-      if (COUNT) n_relax += (uint32_t)f0 + (uint32_t)f1 + (uint32_t)f2 + (uint32_t)f3;
-      const uint64_t k0 = Db[f0 ? (size_t)u0 * B + s : own];
-      const uint64_t k1 = Db[f1 ? (size_t)u1 * B + s : own];
-      const uint64_t k2 = Db[f2 ? (size_t)u2 * B + s : own];
-      const uint64_t k3 = Db[f3 ? (size_t)u3 * B + s : own];
-      const uint64_t l0 = min(in_lat[a], LAT_SAT), l1 = min(in_lat[a + 1], LAT_SAT);
-      const uint64_t l2 = min(in_lat[a + 2], LAT_SAT), l3 = min(in_lat[a + 3], LAT_SAT);
-      const float o0 = in_om[a], o1 = in_om[a + 1], o2 = in_om[a + 2], o3 = in_om[a + 3];
-      const uint64_t c0 = (!f0 || k0 == KEY_INF) ? KEY_INF : relax_key(k0, l0, o0);
-      const uint64_t c1 = (!f1 || k1 == KEY_INF) ? KEY_INF : relax_key(k1, l1, o1);
-      const uint64_t c2 = (!f2 || k2 == KEY_INF) ? KEY_INF : relax_key(k2, l2, o2);
-      const uint64_t c3 = (!f3 || k3 == KEY_INF) ? KEY_INF : relax_key(k3, l3, o3);
-      best = min(best, min(min(c0, c1), min(c2, c3)));
+      for (; g < cnt; g++) {
+        const uint4 r = list[g];
+        const uint32_t slot = __builtin_amdgcn_readfirstlane(r.y);
+        if (slot != run_slot) {
+          best[run_slot * BATCH + lane] = run;
+          run_slot = slot;
+          run = KEY_INF;
+        }
+        run = min(run, relax32(load_key(slab, r.x + lane8), r.z, __uint_as_float(r.w)));
+      }
     }
-    for (; a < a1; a++) {
-      const uint32_t u = in_src[a];
-      const bool f = !FLAGS || (Pf[u] | Cf[u]) != 0;
-      if (COUNT) n_relax += f;
-      const uint64_t ku = Db[f ? (size_t)u * B + s : own];
-      const uint64_t l = min(in_lat[a], LAT_SAT);
-      const float o = in_om[a];
-      const uint64_t c = (!f || ku == KEY_INF) ? KEY_INF : relax_key(ku, l, o);
-      best = min(best, c);
+    if (COUNT) n_rel += n_cand;
+    if (!n_cand) continue;
+    best[run_slot * BATCH + lane] = run;
+    // flush: improved keys are written in place (one untorn 64-bit update each).
+    // Rows that received no candidate are not read (out-of-range buffer load).
+    uint64_t nb[NPW], cur[NPW];
+#pragma unroll
+    for (int i = 0; i < NPW; i++) {
+      nb[i] = best[i * BATCH + lane];
+      cur[i] = load_key(slab, __any(nb[i] != KEY_INF) ? min(vw + i, vw1 - 1) * (BATCH * 8) + lane8 : OOB);
     }
-    const bool ch = valid && best < cur;
-    if (ch) {
-      Db[own] = best;  // one untorn 64-bit (lat, loss) update
-      any = true;
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < NPW; i++) {
+      const uint32_t v = vw + i;
+      const bool ch = v < vw1 && nb[i] < cur[i];
+      if (ch) Db[(size_t)v * BATCH + lane] = nb[i];
+      if (__any(ch)) {
+        any = true;
+        if (FRONT && lane == 0) stamp[(size_t)b * n + v] = pass + 2;
+      }
     }
-    if (FLAGS) {
-      const uint64_t m = __ballot(ch) >> (32 * g);
-      if ((m & 0xffffffffull) && s == 0) Cf[v] = 1u;
+    // one flag store per wave and batch (a wave's items run batch by batch)
+    if (any && b != flagged) {
+      if (lane == 0) changed[b * FLAG_STRIDE] = 1u;
+      flagged = b;
     }
   }
-  if (__any(any) && lane == 0) atomicOr(&changed[b], 1u);
-  if (COUNT) {
-    unsigned long long w = n_relax;
-    for (int d = 32; d > 0; d >>= 1) w += __shfl_xor(w, d, 64);
-    if (lane == 0 && w) atomicAdd(&work[blockIdx.x & (WORK_SHARDS - 1)], w);
-  }
+  if (COUNT && lane == 0 && n_rel) atomicAdd(&work[blockIdx.x & (WORK_SHARDS - 1)], (unsigned long long)n_rel * BATCH);
 }
 
-// Verbatim v1 relaxation kernel (A/B control, variant "v1k").
-template <int VPW>
-__global__ void __launch_bounds__(RELAX_BLOCK)
-    k_relax_v1(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
-                   const uint64_t* __restrict__ in_lat, const float* __restrict__ in_om,
-                   uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ active,
-                   uint32_t* __restrict__ changed) {
-  const uint32_t b = blockIdx.y;
-  if (!active[b]) return;
-  uint64_t* __restrict__ Db = D + (size_t)b * n * BATCH;
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  bool any = false;
-  const uint32_t v0 = (blockIdx.x * RELAX_WAVES + wave) * VPW;
-#pragma unroll 1
-  for (int k = 0; k < VPW; k++) {
-    const uint32_t v = v0 + k;
-    if (v >= n) break;
-    const uint32_t a0 = in_off[v], a1 = in_off[v + 1];
-    const uint64_t cur = Db[(size_t)v * BATCH + lane];
-    uint64_t best = cur;
-    uint32_t a = a0;
-    // 4 independent 512-B row reads in flight per wave
-    for (; a + 4 <= a1; a += 4) {
-      uint32_t u0 = in_src[a], u1 = in_src[a + 1], u2 = in_src[a + 2], u3 = in_src[a + 3];
-      uint64_t k0 = Db[(size_t)u0 * BATCH + lane];
-      uint64_t k1 = Db[(size_t)u1 * BATCH + lane];
-      uint64_t k2 = Db[(size_t)u2 * BATCH + lane];
-      uint64_t k3 = Db[(size_t)u3 * BATCH + lane];
-      uint64_t l0 = min(in_lat[a], LAT_SAT), l1 = min(in_lat[a + 1], LAT_SAT);
-      uint64_t l2 = min(in_lat[a + 2], LAT_SAT), l3 = min(in_lat[a + 3], LAT_SAT);
-      float o0 = in_om[a], o1 = in_om[a + 1], o2 = in_om[a + 2], o3 = in_om[a + 3];
-      uint64_t c0 = k0 == KEY_INF ? KEY_INF : relax_key(k0, l0, o0);
-      uint64_t c1 = k1 == KEY_INF ? KEY_INF : relax_key(k1, l1, o1);
-      uint64_t c2 = k2 == KEY_INF ? KEY_INF : relax_key(k2, l2, o2);
-      uint64_t c3 = k3 == KEY_INF ? KEY_INF : relax_key(k3, l3, o3);
-      best = min(best, min(min(c0, c1), min(c2, c3)));
-    }
-    for (; a < a1; a++) {
-      uint32_t u = in_src[a];
-      uint64_t ku = Db[(size_t)u * BATCH + lane];
-      uint64_t c = ku == KEY_INF ? KEY_INF : relax_key(ku, min(in_lat[a], LAT_SAT), in_om[a]);
-      best = min(best, c);
-    }
-    if (best < cur) {
-      Db[(size_t)v * BATCH + lane] = best;  // one untorn 64-bit (lat, loss) update
-      any = true;
-    }
-  }
-  if (__any(any) && lane == 0) atomicOr(&changed[b], 1u);
-}
-
-// Transposed write-out of [B rows x 64 cols] tiles.  Diagonal = the raw
+// Transposed write-out of [64 rows x 64 cols] tiles.  Diagonal = the raw
 // self-loop (graph/mod.rs:210-217).  Saturated keys flag their batch.
-template <int B>
 __global__ void __launch_bounds__(256)
-    k_out_front(const uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ used,
-                uint32_t n_used, uint32_t first_row, uint32_t row_end, uint32_t out_row0,
-                const uint32_t* __restrict__ self_edge, const uint64_t* __restrict__ e_lat,
-                const float* __restrict__ e_loss, uint64_t* __restrict__ out_lat,
-                float* __restrict__ out_loss, uint32_t* __restrict__ sat) {
-  constexpr int G = 64 / B;
-  __shared__ uint64_t tile[64][B + 1];
+    k_out_batch(const uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ used, uint32_t n_used,
+                uint32_t first_row, uint32_t row_end, uint32_t out_row0, const uint32_t* __restrict__ self_edge,
+                const uint64_t* __restrict__ e_lat, const float* __restrict__ e_loss,
+                uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, uint32_t* __restrict__ sat) {
+  __shared__ uint64_t tile[64][BATCH + 1];
   const uint32_t b = blockIdx.y;
   const uint32_t j0 = blockIdx.x * 64;
-  const uint64_t* __restrict__ Db = D + (size_t)b * n * B;
+  const uint64_t* __restrict__ Db = D + (size_t)b * n * BATCH;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane / B, s = lane % B;
-  for (int c = wave * G + g; c < 64; c += 4 * G) {
+  for (int c = wave; c < 64; c += 4) {
     const uint32_t j = j0 + c;
-    tile[c][s] = j < n_used ? Db[(size_t)used[j] * B + s] : 0ull;
+    tile[c][lane] = j < n_used ? Db[(size_t)used[j] * BATCH + lane] : 0ull;
   }
   __syncthreads();
   bool sflag = false;
   const uint32_t j = j0 + lane;
-  for (int r = wave; r < B; r += 4) {
-    const uint32_t row = first_row + b * B + r;
+  for (int r = wave; r < BATCH; r += 4) {
+    const uint32_t row = first_row + b * BATCH + r;
     if (row >= row_end || j >= n_used) continue;
     const size_t o = (size_t)(row - out_row0) * n_used + j;
     if (row == j) {
@@ -537,8 +474,8 @@ __global__ void __launch_bounds__(256)
       out_loss[o] = e_loss[e];
     } else {
       const uint64_t kk = tile[lane][r];
-      const uint64_t lat = key_lat(kk);
-      sflag |= lat >= LAT_SAT;
+      const uint32_t lat = key_lat(kk);
+      sflag |= lat == LAT32_SAT;
       out_lat[o] = lat;
       out_loss[o] = __uint_as_float(key_loss_bits(kk));
     }
@@ -758,17 +695,43 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   copy_to_host(ctx, &n_arcs, net->in_off + n, 4);
   net->n_arcs = n_arcs;
   net->in_src = dmalloc<uint32_t>(n_arcs);
+  net->in_dst = dmalloc<uint32_t>(n_arcs);
   net->in_lat = dmalloc<uint64_t>(n_arcs);
+  net->in_lat32 = dmalloc<uint32_t>(n_arcs);
   net->in_om = dmalloc<float>(n_arcs);
   if (n_arcs) {
     uint32_t* cursor = ctx->r_map.get<uint32_t>((size_t)n + 1);
     SG_HIP(hipMemcpyAsync(cursor, net->in_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(k_scatter_arcs, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src,
                        net->e_dst, net->e_lat, net->e_loss, m, (int)net->directed, cursor,
-                       net->in_src, net->in_lat, net->in_om);
+                       net->in_src, net->in_dst, net->in_lat, net->in_lat32, net->in_om);
     SG_CHECK_LAUNCH();
   }
+  net->h_in_off.resize((size_t)n + 1);
+  copy_to_host(ctx, net->h_in_off.data(), net->in_off, ((size_t)n + 1) * 4);
   SG_HIP(hipStreamSynchronize(st));
+}
+
+// Relaxation chunks: consecutive destination nodes, at most `nodes` of them
+// and about `arcs` in-arcs (a hub node gets a chunk of its own).
+static void ensure_chunks(sg_ctx* ctx, sg_net* net, uint32_t nodes, uint32_t arcs) {
+  if (net->chunk_v && net->chunk_nodes == nodes && net->chunk_arcs == arcs) return;
+  const uint32_t n = net->n_nodes;
+  const std::vector<uint32_t>& off = net->h_in_off;
+  std::vector<uint32_t> cv{0};
+  for (uint32_t v = 0; v < n;) {
+    uint32_t e = v + 1;
+    while (e < n && e - v < nodes && off[e + 1] - off[v] <= arcs) e++;
+    cv.push_back(e);
+    v = e;
+  }
+  if (net->chunk_v) SG_HIP(hipFree(net->chunk_v));
+  net->chunk_v = dmalloc<uint32_t>(cv.size());
+  net->n_chunks = (uint32_t)cv.size() - 1;
+  net->chunk_nodes = nodes;
+  net->chunk_arcs = arcs;
+  SG_HIP(hipMemcpyAsync(net->chunk_v, cv.data(), cv.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
 }
 
 static void check_self_loops(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
@@ -838,109 +801,118 @@ static void run_wide(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t 
   }
 }
 
-template <int B, int VPW, bool XCD, bool FLAGS, bool WAVE, bool HALF = false>
+// WAVE_OWNED: k_relax_w with CN nodes per wave and STG staged arcs per wave;
+// otherwise k_relax with CN nodes per block and STG staged arcs per block.
+template <int CN, int STG, bool FRONT, bool WAVE_OWNED>
 static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
-                             uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
-                             float* out_loss) {
-  // B = sources per batch (B = 32: slab n x 256 B, L2-resident per XCD at 10k nodes);
-  // VPW = destination nodes per lane group, walked sequentially;
-  // WAVE = wave-per-node kernel (B = 64, scalar arc loads, u32 frontier flags)
-  static_assert(!WAVE || B == 64, "wave-per-node kernel needs B = 64");
-  static_assert(!HALF || B == 32, "half-wave kernel needs B = 32");
-  using FT = typename std::conditional<WAVE || HALF, uint32_t, uint8_t>::type;
-  constexpr int G = 64 / B;
+                             uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
   hipStream_t st = ctx->stream;
   const uint32_t n = net->n_nodes;
   const uint32_t n_rows = row_end - row_begin;
-  const uint32_t n_batches = (n_rows + B - 1) / B;
-  // Group size: batches whose slabs are live together (bounded device memory).
-  const size_t slab_bytes = (size_t)n * B * 8;
+  const uint32_t n_batches = (n_rows + BATCH - 1) / BATCH;
+  if (!WAVE_OWNED) ensure_chunks(ctx, net, CN, (uint32_t)env_int("SG_APSP_CHUNK_ARCS", 16 * CN));
+  // Group: batches whose slabs are live together (bounded device memory).
+  const size_t slab_bytes = (size_t)n * BATCH * 8;
   const size_t budget = (size_t)env_int("SG_APSP_GROUP_MB", 4096) << 20;
   const uint32_t group = (uint32_t)std::max<size_t>(1, std::min<size_t>(n_batches, budget / slab_bytes));
-  const uint32_t nvb = (n + RELAX_WAVES * G * VPW - 1) / (RELAX_WAVES * G * VPW);
-  uint64_t* D = ctx->r_dist.get<uint64_t>((size_t)group * n * B);
+  uint64_t* D = ctx->r_dist.get<uint64_t>((size_t)group * n * BATCH);
+  uint32_t* stamp = ctx->r_dirty.get<uint32_t>((size_t)group * n);
   // per-batch flags: a 3-slot ring of "changed in pass p" arrays, then the saturation flags
-  uint32_t* flags = ctx->r_flags.get<uint32_t>((size_t)group * 4 + 8);
-  uint32_t* ring[3] = {flags, flags + group, flags + 2 * (size_t)group};
-  uint32_t* sat = flags + 3 * (size_t)group;
-  FT* dirty = ctx->r_dirty.get<FT>(2 * (size_t)group * n);
-  FT* dirtyA[2] = {dirty, dirty + (size_t)group * n};
+  const size_t fs = (size_t)group * FLAG_STRIDE;
+  uint32_t* flags = ctx->r_flags.get<uint32_t>(fs * 3 + group + 8);
+  uint32_t* ring[3] = {flags, flags + fs, flags + 2 * fs};
+  uint32_t* sat = flags + 3 * fs;
   unsigned long long* work = ctx->timing ? ctx->r_work.get<unsigned long long>(WORK_SHARDS) : nullptr;
   if (work) SG_HIP(hipMemsetAsync(work, 0, WORK_SHARDS * 8, st));
   // Passes are issued in chunks; the host reads the convergence flags once per
   // chunk.  A pass issued after its batch converged exits at once (active == 0).
   const uint32_t chunk = (uint32_t)std::max(1, env_int("SG_APSP_PASS_CHUNK", 4));
-  std::vector<uint32_t> h_changed(group), h_sat(group);
+  std::vector<uint32_t> h_changed(fs), h_sat(group);
   std::vector<uint32_t> wide_rows;
   for (uint32_t g0 = 0; g0 < n_batches; g0 += group) {
     const uint32_t gb = std::min(group, n_batches - g0);
-    const uint32_t first_row = row_begin + g0 * B;
-    hipLaunchKernelGGL(k_init_front<B>, dim3(grid_for((size_t)gb * n * B, 256, 65536)), dim3(256), 0, st, D, n,
-                       d_used, first_row, row_end, gb);
-    SG_HIP(hipMemsetAsync(dirty, 0, 2 * (size_t)gb * n * sizeof(FT), st));
-    dirtyA[1] = dirty + (size_t)gb * n;
-    hipLaunchKernelGGL((k_mark_sources<B, FT>), dim3(grid_for((size_t)gb * B, 256)), dim3(256), 0, st, dirtyA[1], n,
+    const uint32_t first_row = row_begin + g0 * BATCH;
+    hipLaunchKernelGGL(k_init_batch, dim3(grid_for((size_t)gb * n * BATCH, 256, 65536)), dim3(256), 0, st, D,
+                       stamp, n, d_used, first_row, row_end, gb);
+    hipLaunchKernelGGL(k_stamp_sources, dim3(grid_for((size_t)gb * BATCH, 256)), dim3(256), 0, st, stamp, n,
                        d_used, first_row, row_end, gb);
     SG_CHECK_LAUNCH();
-    SG_HIP(hipMemsetAsync(ring[2], 1, gb * 4ull, st));  // "changed in pass -1": every batch active
-    const BatchMap map{nvb, gb};
-    const uint32_t grid = XCD ? 8 * nvb * ((gb + 7) / 8) : nvb * gb;
+    SG_HIP(hipMemsetAsync(ring[2], 1, gb * FLAG_STRIDE * 4ull, st));  // "changed in pass -1": every batch active
+    const uint32_t grid = 8 * net->n_chunks * ((gb + 7) / 8);
+    const bool trace = env_int("SG_APSP_TRACE", 0) != 0;  // per-pass diagnostics on stderr
+    hipEvent_t te0 = nullptr, te1 = nullptr;
+    if (trace) {
+      SG_HIP(hipEventCreate(&te0));
+      SG_HIP(hipEventCreate(&te1));
+    }
+    double trace_prev = 0;
     for (uint32_t pass = 0;;) {
       uint32_t last = pass;
       for (uint32_t c = 0; c < chunk; c++, pass++) {
+        if (trace) SG_HIP(hipEventRecord(te0, st));
         if (pass > n + 2 + chunk) throw Error(SG_ERR_DEVICE, "relaxation did not converge");
         const uint32_t* active = ring[(pass + 2) % 3];
         uint32_t* changed = ring[pass % 3];
-        FT* dcur = dirtyA[pass & 1];
-        const FT* dprev = dirtyA[(pass & 1) ^ 1];
-        SG_HIP(hipMemsetAsync(changed, 0, gb * 4ull, st));
-        if (pass) SG_HIP(hipMemsetAsync(dcur, 0, (size_t)gb * n * sizeof(FT), st));
-        {
-          TimedLaunch tl(ctx, "relax_packed", 0.0);
-          if (getenv("SG_APSP_V1K")) {
-            const uint32_t nvb1 = (n + RELAX_WAVES * 4 - 1) / (RELAX_WAVES * 4);
-            hipLaunchKernelGGL(k_relax_v1<4>, dim3(nvb1, gb), dim3(RELAX_BLOCK), 0, st, net->in_off, net->in_src,
-                               net->in_lat, net->in_om, D, n, active, changed);
-          } else if constexpr (HALF) {
-            const uint32_t nvh = (n + RELAX_WAVES * 2 * VPW - 1) / (RELAX_WAVES * 2 * VPW);
-            const uint32_t gridh = XCD ? 8 * nvh * ((gb + 7) / 8) : nvh * gb;
-            if (work)
-              hipLaunchKernelGGL((k_relax_half<VPW, XCD, FLAGS, true>), dim3(gridh), dim3(RELAX_BLOCK), 0, st,
-                                 net->in_off, net->in_src, net->in_lat, net->in_om, D, n, nvh, gb, active, changed,
-                                 (const uint32_t*)dprev, (uint32_t*)dcur, work);
-            else
-              hipLaunchKernelGGL((k_relax_half<VPW, XCD, FLAGS, false>), dim3(gridh), dim3(RELAX_BLOCK), 0, st,
-                                 net->in_off, net->in_src, net->in_lat, net->in_om, D, n, nvh, gb, active, changed,
-                                 (const uint32_t*)dprev, (uint32_t*)dcur, work);
-          } else if constexpr (WAVE) {
-            const uint32_t nvw = (n + RELAX_WAVES * VPW - 1) / (RELAX_WAVES * VPW);
-            const dim3 gw = XCD ? dim3(8 * nvw * ((gb + 7) / 8)) : dim3(nvw, gb);
-            if (work)
-              hipLaunchKernelGGL((k_relax_wave<VPW, FLAGS, true, XCD>), gw, dim3(RELAX_BLOCK), 0, st,
-                                 net->in_off, net->in_src, net->in_lat, net->in_om, D, n, active, changed,
-                                 (const uint32_t*)dprev, (uint32_t*)dcur, work, nvw, gb);
-            else
-              hipLaunchKernelGGL((k_relax_wave<VPW, FLAGS, false, XCD>), gw, dim3(RELAX_BLOCK), 0, st,
-                                 net->in_off, net->in_src, net->in_lat, net->in_om, D, n, active, changed,
-                                 (const uint32_t*)dprev, (uint32_t*)dcur, work, nvw, gb);
-          } else {
-            hipLaunchKernelGGL((k_relax_front<B, VPW, XCD, FLAGS>), dim3(grid), dim3(RELAX_BLOCK), 0, st,
-                               net->in_off, net->in_src, net->in_lat, net->in_om, D, n, map, active, changed,
-                               (const uint8_t*)dprev, (uint8_t*)dcur, work);
-          }
+        SG_HIP(hipMemsetAsync(changed, 0, gb * FLAG_STRIDE * 4ull, st));
+        if constexpr (WAVE_OWNED) {
+          TimedLaunch tl(ctx, "relax", 0.0);
+          constexpr int NPW = CN;  // nodes per wave
+          // persistent grid: SG_APSP_BLOCKS_PER_CU resident blocks per CU (0 = one block per work item)
+          const int bpc = env_int("SG_APSP_BLOCKS_PER_CU", 0);
+          const uint32_t ncw = (n + 4 * NPW - 1) / (4 * NPW);
+          const uint32_t gridw = bpc > 0 ? 8 * (uint32_t)((ctx->n_cu * bpc + 7) / 8) : 8 * ncw * ((gb + 7) / 8);
+          if (work)
+            hipLaunchKernelGGL((k_relax_w<NPW, STG / 64, FRONT, true>), dim3(gridw), dim3(RELAX_THREADS), 0, st,
+                               net->in_off, net->in_src, net->in_dst, net->in_lat32, net->in_om, D, n, gb,
+                               active, changed, stamp, pass, work);
+          else
+            hipLaunchKernelGGL((k_relax_w<NPW, STG / 64, FRONT, false>), dim3(gridw), dim3(RELAX_THREADS), 0, st,
+                               net->in_off, net->in_src, net->in_dst, net->in_lat32, net->in_om, D, n, gb,
+                               active, changed, stamp, pass, work);
+        } else {
+          TimedLaunch tl(ctx, "relax", 0.0);
+          if (work)
+            hipLaunchKernelGGL((k_relax<CN, STG, FRONT, true>), dim3(grid), dim3(RELAX_THREADS), 0, st, net->chunk_v,
+                               net->n_chunks, net->in_off, net->in_src, net->in_dst, net->in_lat32, net->in_om, D,
+                               n, gb, active, changed, stamp, pass, work);
+          else
+            hipLaunchKernelGGL((k_relax<CN, STG, FRONT, false>), dim3(grid), dim3(RELAX_THREADS), 0, st, net->chunk_v,
+                               net->n_chunks, net->in_off, net->in_src, net->in_dst, net->in_lat32, net->in_om, D,
+                               n, gb, active, changed, stamp, pass, work);
         }
         SG_CHECK_LAUNCH();
         last = pass;
+        if (trace) {
+          SG_HIP(hipEventRecord(te1, st));
+          SG_HIP(hipEventSynchronize(te1));
+          float ms = 0;
+          SG_HIP(hipEventElapsedTime(&ms, te0, te1));
+          unsigned long long w[WORK_SHARDS] = {};
+          if (work) copy_to_host(ctx, w, work, sizeof(w));
+          double tot = 0;
+          for (int k = 0; k < WORK_SHARDS; k++) tot += (double)w[k];
+          std::vector<uint32_t> act(gb * FLAG_STRIDE);
+          copy_to_host(ctx, act.data(), ring[(pass + 2) % 3], gb * FLAG_STRIDE * 4ull);
+          uint32_t na = 0;
+          for (uint32_t b = 0; b < gb; b++) na += act[b * FLAG_STRIDE] != 0;
+          fprintf(stderr, "[apsp] group %u pass %u: %.3f ms, %u active batches, %.3f G lane-relaxations\n", g0, pass,
+                  ms, na, (tot - trace_prev) / 1e9);
+          trace_prev = tot;
+        }
       }
-      copy_to_host(ctx, h_changed.data(), ring[last % 3], gb * 4ull);
+      copy_to_host(ctx, h_changed.data(), ring[last % 3], gb * FLAG_STRIDE * 4ull);
       uint32_t n_active = 0;
-      for (uint32_t b = 0; b < gb; b++) n_active += h_changed[b] != 0;
+      for (uint32_t b = 0; b < gb; b++) n_active += h_changed[b * FLAG_STRIDE] != 0;
       if (!n_active) break;
+    }
+    if (trace) {
+      SG_HIP(hipEventDestroy(te0));
+      SG_HIP(hipEventDestroy(te1));
     }
     SG_HIP(hipMemsetAsync(sat, 0, gb * 4ull, st));
     {
-      TimedLaunch tl(ctx, "out_packed", 12.0 * std::min<uint32_t>(gb * B, row_end - first_row) * n_used);
-      hipLaunchKernelGGL(k_out_front<B>, dim3((n_used + 63) / 64, gb), dim3(256), 0, st, D, n, d_used, n_used,
+      TimedLaunch tl(ctx, "out", 12.0 * std::min<uint32_t>(gb * BATCH, row_end - first_row) * n_used);
+      hipLaunchKernelGGL(k_out_batch, dim3((n_used + 63) / 64, gb), dim3(256), 0, st, D, n, d_used, n_used,
                          first_row, row_end, row_begin, net->self_edge, net->e_lat, net->e_loss, out_lat,
                          out_loss, sat);
     }
@@ -948,67 +920,47 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
     copy_to_host(ctx, h_sat.data(), sat, gb * 4ull);
     for (uint32_t b = 0; b < gb; b++)
       if (h_sat[b])
-        for (uint32_t r = 0; r < B; r++) {
-          uint32_t row = first_row + b * B + r;
+        for (uint32_t r = 0; r < BATCH; r++) {
+          uint32_t row = first_row + b * BATCH + r;
           if (row < row_end) wide_rows.push_back(row);
         }
   }
-  if (work) {  // relaxations actually performed (dirty arcs x lanes), for the roofline
+  if (work) {  // relaxations actually performed (relaxed arcs x lanes), for the roofline
     unsigned long long w[WORK_SHARDS];
     copy_to_host(ctx, w, work, sizeof(w));
     double total = 0;
     for (int k = 0; k < WORK_SHARDS; k++) total += (double)w[k];
-    timer_add_work(ctx, "relax_packed", total);
+    timer_add_work(ctx, "relax", total);
   }
   if (!wide_rows.empty()) run_wide(ctx, net, d_used, n_used, wide_rows, row_begin, out_lat, out_loss);
 }
 
-// Kernel variant (A/B measurement): SG_APSP_VARIANT = "<B>[x][f]" (x = XCD-aware
-// grid, f = frontier flags); default below.
+// A/B measurement knobs: SG_APSP_FRONTIER=0 relaxes every arc every pass;
+// SG_APSP_KERNEL = w (wave-owned nodes) | b (block-owned nodes);
+// SG_APSP_CN nodes per wave (w: 8 | 16) or per block (b: 32 | 64);
+// SG_APSP_STAGE staged arcs per wave (w: 128 | 256) or per block (b: 512 | 1024).
 static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                            uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
-  const char* v = getenv("SG_APSP_VARIANT");
-  std::string var = v && *v ? v : "w64xv32";
-#define SG_VAR(name, B, VPW, X, F, W)                                                                \
-  if (var == name) {                                                                                 \
-    shortest_paths_t<B, VPW, X, F, W>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss); \
+  const bool front = env_int("SG_APSP_FRONTIER", 1) != 0;
+  const char* kv = getenv("SG_APSP_KERNEL");
+  const bool wave = !(kv && kv[0] == 'b');
+  const int cn = env_int("SG_APSP_CN", wave ? 8 : 64), stg = env_int("SG_APSP_STAGE", wave ? 128 : 1024);
+#define SG_SP(W_, CN_, STG_)                                                                          \
+  if (wave == W_ && cn == CN_ && stg == STG_) {                                                      \
+    if (front)                                                                                       \
+      shortest_paths_t<CN_, STG_, true, W_>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss); \
+    else                                                                                             \
+      shortest_paths_t<CN_, STG_, false, W_>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss); \
     return;                                                                                          \
   }
-#define SG_VARH(name, VPW, X, F)                                                                     \
-  if (var == name) {                                                                                 \
-    shortest_paths_t<32, VPW, X, F, false, true>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, \
-                                                 out_loss);                                          \
-    return;                                                                                          \
-  }
-  SG_VARH("h32x", 4, true, false)
-  SG_VARH("h32xf", 4, true, true)
-  SG_VARH("h32", 4, false, false)
-  SG_VARH("h32xv2", 2, true, false)
-  SG_VAR("w64x", 64, 4, true, false, true)
-  SG_VAR("w64xf", 64, 4, true, true, true)
-  SG_VAR("w64v8", 64, 8, false, false, true)
-  SG_VAR("w64v16", 64, 16, false, false, true)
-  SG_VAR("w64v32", 64, 32, false, false, true)
-  SG_VAR("w64xv8", 64, 8, true, false, true)
-  SG_VAR("w64xv16", 64, 16, true, false, true)
-  SG_VAR("w64fv16", 64, 16, false, true, true)
-  SG_VAR("w64v64", 64, 64, false, false, true)
-  SG_VAR("w64v128", 64, 128, false, false, true)
-  SG_VAR("w64xv32", 64, 32, true, false, true)
-  SG_VAR("w64xv64", 64, 64, true, false, true)
-  SG_VAR("w64f", 64, 4, false, true, true)
-  SG_VAR("w64", 64, 4, false, false, true)
-  SG_VAR("32xf", 32, 4, true, true, false)
-  SG_VAR("32x", 32, 4, true, false, false)
-  SG_VAR("32f", 32, 4, false, true, false)
-  SG_VAR("32", 32, 4, false, false, false)
-  SG_VAR("64xf", 64, 4, true, true, false)
-  SG_VAR("64x", 64, 4, true, false, false)
-  SG_VAR("64f", 64, 4, false, true, false)
-  SG_VAR("64", 64, 4, false, false, false)
-#undef SG_VAR
-#undef SG_VARH
-  throw Error(SG_ERR_INVALID_ARG, "unknown SG_APSP_VARIANT " + var);
+  SG_SP(true, 8, 128)
+  SG_SP(true, 8, 256)
+  SG_SP(true, 16, 128)
+  SG_SP(true, 16, 256)
+  SG_SP(false, 32, 512)
+  SG_SP(false, 64, 1024)
+#undef SG_SP
+  throw Error(SG_ERR_INVALID_ARG, "unsupported SG_APSP_KERNEL / SG_APSP_CN / SG_APSP_STAGE");
 }
 
 static void direct_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, const uint32_t* h_used,

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build an experiment library tools/ab/libshadow_gpu_<name>.so with extra -D flags (timing A/B only).
+# usage: bash tools/ab/build_variant.sh NAME "-DSG_EXPERIMENT_X"
+set -e
+NAME=$1; DEFS=$2
+ROOT=$(cd "$(dirname "$0")/../.." && pwd)
+OBJ=/tmp/sg_ab_$NAME; mkdir -p $OBJ
+cd $ROOT/shadow_amd/csrc
+for f in sg_context sg_routing sg_deliver; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -munsafe-fp-atomics $DEFS -c $f.hip -o $OBJ/$f.o &
+done
+g++ -O3 -std=c++17 -fPIC -Wall -c sg_gml.cpp -o $OBJ/sg_gml.o
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/tools/ab/libshadow_gpu_$NAME.so $OBJ/*.o
+echo built tools/ab/libshadow_gpu_$NAME.so

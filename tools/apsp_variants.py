@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""A/B timing of the APSP kernel variants (SG_APSP_VARIANT) on the C3 workload.
+"""A/B timing of APSP build settings on the C3 workload.
 
-Every variant must produce the identical table (checked against the first);
-prints ms per build and the relaxation-kernel statistics per variant.
-    python tools/apsp_variants.py [--nodes 10000] [--variants 32xf,64,...]
+A variant is a set of environment assignments read by the library at each
+build (e.g. "SG_APSP_FRONTIER=0"); variants are separated by ';'.  Every
+variant must produce the identical table (checked against the first); prints
+ms per build and the relaxation-kernel statistics per variant.
+    python tools/apsp_variants.py [--nodes 10000] [--variants "SG_APSP_FRONTIER=1;SG_APSP_FRONTIER=0"]
 """
 import argparse
 import os
@@ -19,8 +21,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nodes", type=int, default=10000)
     ap.add_argument("--degree", type=float, default=8.0)
-    ap.add_argument("--variants", default="64,64x,64f,64xf,32,32x,32f,32xf")
-    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--variants", default="SG_APSP_FRONTIER=1;SG_APSP_FRONTIER=0")
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     import torch
 
@@ -34,26 +37,41 @@ def main():
     lat = torch.empty(n * n, dtype=torch.int64, device="cuda")
     loss = torch.empty(n * n, dtype=torch.float32, device="cuda")
     ref = None
-    for v in a.variants.split(","):
-        os.environ["SG_APSP_VARIANT"] = v
-        net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)  # warm-up
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(a.reps):
-            net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
-        torch.cuda.synchronize()
-        ms = (time.perf_counter() - t0) / a.reps * 1e3
+    base_env = dict(os.environ)
+    variants = a.variants.split(";")
+
+    def set_env(v):
+        os.environ.clear()
+        os.environ.update(base_env)
+        for kv in v.split():
+            k, _, val = kv.partition("=")
+            os.environ[k] = val
+
+    times = {v: [] for v in variants}
+    for _ in range(a.rounds):  # interleaved A/B/A/B...: box-to-box and clock drift hit every variant alike
+        for v in variants:
+            set_env(v)
+            net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)  # warm-up
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.reps):
+                net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
+            torch.cuda.synchronize()
+            times[v].append((time.perf_counter() - t0) / a.reps * 1e3)
+    for v in variants:
+        set_env(v)
         ctx.enable_timers(True)
         net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
-        rms, launches, work = ctx.read_timer("relax_packed")
+        rms, launches, work = ctx.read_timer("relax")
         ctx.enable_timers(False)
         h = (lat[: 64 * n].cpu().numpy().copy(), loss[: 64 * n].cpu().numpy().copy(),
              lat[-64 * n:].cpu().numpy().copy())
         same = "ref" if ref is None else all(np.array_equal(x, y) for x, y in zip(h, ref))
         ref = ref or h
-        print(f"variant {v:5s}: {ms:8.3f} ms/build  relax {rms:8.3f} ms in {launches} launches, "
-              f"{work / 1e9:.3f} G lane-relaxations, {work / max(rms, 1e-9) / 1e6:.1f} G/s  identical={same}",
-              flush=True)
+        ms = float(np.median(times[v]))
+        print(f"variant {v!r}: {ms:8.3f} ms/build (median of {a.rounds}; min {min(times[v]):.3f})  relax {rms:8.3f} ms "
+              f"in {launches} launches, {work / 1e9:.3f} G lane-relaxations, {work / max(rms, 1e-9) / 1e6:.1f} G/s  "
+              f"identical={same}", flush=True)
 
 
 if __name__ == "__main__":

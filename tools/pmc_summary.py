@@ -20,9 +20,10 @@ import json
 import os
 from collections import defaultdict
 
-KERNELS = {"relax_packed": "k_relax_packed", "out_packed": "k_out_packed", "walk": "k_walk",
+# first match wins: k_relax_wide before the k_relax<...> template instances
+KERNELS = {"relax_wide": "k_relax_wide", "relax": "k_relax<", "out": "k_out_batch", "walk": "k_walk",
            "scatter": "k_scatter", "sort_small": "k_sort_small", "sort_big": "k_sort_big",
-           "seg_bounds": "k_seg_bounds", "relax_wide": "k_relax_wide"}
+           "seg_bounds": "k_seg_bounds"}
 
 
 def _rows(d, pattern):
