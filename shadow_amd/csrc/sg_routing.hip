@@ -48,15 +48,12 @@ struct sg_net {
   uint64_t* in_lat = nullptr;    // exact latency (wide kernel)
   uint32_t* in_lat32 = nullptr;  // latency clamped to LAT32_SAT (packed-key kernel)
   float* in_om = nullptr;        // 1f32 - loss
-  std::vector<uint32_t> h_in_off;  // host copy of in_off
-  // relaxation chunks: chunk c = destination nodes [chunk_v[c], chunk_v[c + 1])
-  uint32_t n_chunks = 0, chunk_nodes = 0, chunk_arcs = 0;
-  uint32_t* chunk_v = nullptr;
+  uint4* in_rec = nullptr;       // per in-arc (source, destination, latency32, bits(1f32 - loss))
   // self-loops
   uint32_t* self_cnt = nullptr;
   uint32_t* self_edge = nullptr;
   ~sg_net() {
-    void* ps[] = {e_src, e_dst, e_lat, e_loss, in_off, in_src, in_dst, in_lat, in_lat32, in_om, chunk_v, self_cnt,
+    void* ps[] = {e_src, e_dst, e_lat, e_loss, in_off, in_src, in_dst, in_lat, in_lat32, in_om, in_rec, self_cnt,
                   self_edge};
     for (void* p : ps)
       if (p) (void)hipFree(p);
@@ -94,7 +91,7 @@ __global__ void k_scatter_arcs(const uint32_t* __restrict__ src, const uint32_t*
                                uint32_t m, int directed, uint32_t* __restrict__ cursor,
                                uint32_t* __restrict__ in_src, uint32_t* __restrict__ in_dst,
                                uint64_t* __restrict__ in_lat, uint32_t* __restrict__ in_lat32,
-                               float* __restrict__ in_om) {
+                               float* __restrict__ in_om, uint4* __restrict__ in_rec) {
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < m; e += gridDim.x * blockDim.x) {
     uint32_t s = src[e], d = dst[e];
     if (s == d) continue;  // a self-loop never improves D[s][v] (latency >= 1)
@@ -107,6 +104,7 @@ __global__ void k_scatter_arcs(const uint32_t* __restrict__ src, const uint32_t*
     in_lat[p] = l;
     in_lat32[p] = l32;
     in_om[p] = om;
+    in_rec[p] = make_uint4(s, d, l32, __float_as_uint(om));
     if (!directed) {
       uint32_t q = atomicAdd(&cursor[s], 1u);
       in_src[q] = d;
@@ -114,6 +112,7 @@ __global__ void k_scatter_arcs(const uint32_t* __restrict__ src, const uint32_t*
       in_lat[q] = l;
       in_lat32[q] = l32;
       in_om[q] = om;
+      in_rec[q] = make_uint4(d, s, l32, __float_as_uint(om));
     }
   }
 }
@@ -153,287 +152,187 @@ constexpr int GROUP = 8;           // row reads in flight per wave step
 constexpr int RELAX_THREADS = 256;
 constexpr uint32_t FLAG_STRIDE = 32;  // per-batch pass flags 128 B apart: no two batches share a cache line
 
-// Timing experiments only (tools/ab builds): plain LDS stores instead of ds_min_u64.
-#ifdef SG_EXPERIMENT_NOATOMIC
-#define SG_LDS_MIN(p, v) (*(p) = (v))
-#else
-#define SG_LDS_MIN(p, v) atomicMin((p), (v))
-#endif
-
-// One 8-B key through a buffer descriptor (32-bit per-lane byte offset).  An
-// offset of OOB is outside every slab: the load returns 0 and touches no memory.
-constexpr uint32_t OOB = 0x80000000u;
+// One 8-B key through a buffer descriptor (32-bit per-lane byte offset).
 __device__ __forceinline__ uint64_t load_key(__amdgpu_buffer_rsrc_t rsrc, uint32_t off) {
   const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0);
   return ((uint64_t)v[1] << 32) | v[0];
 }
 
+template <int B>
 __global__ void k_init_batch(uint64_t* __restrict__ D, uint32_t* __restrict__ stamp, uint32_t n,
                              const uint32_t* __restrict__ used, uint32_t first_row, uint32_t row_end,
                              uint32_t n_batches) {
-  const size_t total = (size_t)n_batches * n * BATCH;
+  const size_t total = (size_t)n_batches * n * B;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t s = (uint32_t)(i % BATCH);
-    const size_t bv = i / BATCH;
+    const uint32_t s = (uint32_t)(i % B);
+    const size_t bv = i / B;
     const uint32_t v = (uint32_t)(bv % n);
     const uint32_t b = (uint32_t)(bv / n);
-    const uint32_t row = first_row + b * BATCH + s;
+    const uint32_t row = first_row + b * B + s;
     const bool src = row < row_end && used[row] == v;
     D[i] = src ? 0ull : KEY_INF;  // PathProperties::default() at the source
     if (s == 0) stamp[bv] = 0;
   }
 }
 
+template <int B>
 __global__ void k_stamp_sources(uint32_t* __restrict__ stamp, uint32_t n, const uint32_t* __restrict__ used,
                                 uint32_t first_row, uint32_t row_end, uint32_t n_batches) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_batches * BATCH) return;
+  if (t >= n_batches * B) return;
   const uint32_t row = first_row + t;
-  if (row < row_end) stamp[(size_t)(t / BATCH) * n + used[row]] = 1;
+  if (row < row_end) stamp[(size_t)(t / B) * n + used[row]] = 1;
 }
 
-// CN = destination nodes per chunk (LDS rows: CN x 512 B); STG = arcs staged
-// per block step (LDS list: STG x 16 B).
-template <int CN, int STG, bool FRONT, bool COUNT>
-__global__ void __launch_bounds__(RELAX_THREADS)
-    k_relax(const uint32_t* __restrict__ chunk_v, uint32_t n_chunks, const uint32_t* __restrict__ in_off,
-            const uint32_t* __restrict__ in_src, const uint32_t* __restrict__ in_dst,
-            const uint32_t* __restrict__ in_lat32, const float* __restrict__ in_om, uint64_t* __restrict__ D,
-            uint32_t n, uint32_t n_batches, const uint32_t* __restrict__ active, uint32_t* __restrict__ changed,
-            uint32_t* __restrict__ stamp, uint32_t pass, unsigned long long* __restrict__ work) {
-  constexpr int WAVES = RELAX_THREADS / 64;
-  constexpr int ROWS = CN / WAVES;  // own rows per wave at flush
-  __shared__ unsigned long long best[CN * BATCH];
-  __shared__ uint4 list[STG];  // staged arcs: (source, LDS byte offset of the destination row, latency, 1 - loss)
-  __shared__ uint32_t n_list;
-  const uint32_t q = blockIdx.x >> 3;
-  const uint32_t b = (blockIdx.x & 7) + 8 * (q / n_chunks);
-  const uint32_t chunk = q % n_chunks;
-  if (b >= n_batches || !active[b * FLAG_STRIDE]) return;
-  const int lane = threadIdx.x & 63;
-  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint64_t* Db = D + (size_t)b * n * BATCH;
-  const uint32_t* St = stamp + (size_t)b * n;
-  const uint32_t v0 = chunk_v[chunk], v1 = chunk_v[chunk + 1];
-  const uint32_t a0 = in_off[v0], a1 = in_off[v1];
-  // Rows of the batch slab through a buffer descriptor: a 32-bit per-lane offset,
-  // one VALU op per row address.
-  const __amdgpu_buffer_rsrc_t slab =
-      __builtin_amdgcn_make_buffer_rsrc(Db, 0, (int)(n * BATCH * 8u), 0x00020000);
-  const uint32_t lane8 = lane * 8;
-  bool init = false;
-  uint32_t n_rel = 0, n_cand = 0;
-  for (uint32_t c0 = a0; c0 < a1; c0 += STG) {
-    const uint32_t c1 = min(c0 + STG, a1);
-    if (threadIdx.x == 0) n_list = 0;
+// Active-batch list for the next pass: alist[0] = count, alist[1 + i] = the
+// i-th batch (ascending) whose flag is set.  One block.
+__global__ void __launch_bounds__(1024) k_active_list(const uint32_t* __restrict__ flags, uint32_t gb,
+                                                      uint32_t* __restrict__ alist) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t base;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (uint32_t b0 = 0; b0 < gb; b0 += 1024) {
+    const uint32_t b = b0 + threadIdx.x;
+    const bool on = b < gb && flags[b * FLAG_STRIDE] != 0;
+    const uint64_t m = __ballot(on);
+    if (lane == 0) wsum[wv] = (uint32_t)__popcll(m);
     __syncthreads();
-    // 1. stage the dirty arcs of [c0, c1): coalesced arc reads, gathered stamps,
-    //    wave-ballot compaction (record order inside the list is irrelevant: min
-    //    is commutative)
-    constexpr int PER = STG / RELAX_THREADS;
-    uint32_t ua[PER];
-    bool dirty[PER];
-#pragma unroll
-    for (int i = 0; i < PER; i++) {
-      const uint32_t a = c0 + threadIdx.x + i * RELAX_THREADS;
-      ua[i] = in_src[min(a, c1 - 1)];
-    }
-#pragma unroll
-    for (int i = 0; i < PER; i++) {
-      const uint32_t a = c0 + threadIdx.x + i * RELAX_THREADS;
-      dirty[i] = a < c1 && (!FRONT || St[ua[i]] > pass);
-    }
-#pragma unroll
-    for (int i = 0; i < PER; i++) {
-      const uint32_t a = c0 + threadIdx.x + i * RELAX_THREADS;
-      const uint64_t m = __ballot(dirty[i]);
-      if (!m) continue;
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&n_list, (uint32_t)__popcll(m));
-      base = __shfl(base, 0, 64);
-      if (dirty[i]) {
-        const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-        list[pos] = make_uint4(ua[i], (in_dst[a] - v0) * (BATCH * 8), in_lat32[a], __float_as_uint(in_om[a]));
-      }
-    }
-    if (!init) {
-      for (uint32_t i = threadIdx.x; i < CN * BATCH; i += RELAX_THREADS) best[i] = KEY_INF;
-    }
+    uint32_t off = base;
+    for (int i = 0; i < wv; i++) off += wsum[i];
+    if (on) alist[1 + off + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = b;
     __syncthreads();
-    const uint32_t cnt = n_list;
-    init = true;
-    n_cand += cnt;
-    if (COUNT) n_rel += cnt;
-    // 2. relax: GROUP row reads in flight per wave, candidates folded into LDS rows
-    uint32_t g = GROUP * w;
-    for (; g + GROUP <= cnt; g += GROUP * WAVES) {
-      uint4 r[GROUP];
-      uint64_t k[GROUP];
-#pragma unroll
-      for (int j = 0; j < GROUP; j++) r[j] = list[g + j];
-#pragma unroll
-      for (int j = 0; j < GROUP; j++)
-        k[j] = load_key(slab, r[j].x * (BATCH * 8) + lane8);
-#pragma unroll
-      for (int j = 0; j < GROUP; j++)
-        SG_LDS_MIN((unsigned long long*)((char*)best + r[j].y + lane8),
-                  (unsigned long long)relax32(k[j], r[j].z, __uint_as_float(r[j].w)));
-    }
-    for (; g < cnt; g++) {  // tail: fewer than GROUP records left for this wave
-      const uint4 r = list[g];
-      const uint64_t k = load_key(slab, r.x * (BATCH * 8) + lane8);
-      SG_LDS_MIN((unsigned long long*)((char*)best + r.y + lane8),
-                (unsigned long long)relax32(k, r.z, __uint_as_float(r.w)));
-    }
+    if (threadIdx.x == 0)
+      for (int i = 0; i < 16; i++) base += wsum[i];
     __syncthreads();
   }
-  if (!n_cand) return;
-  // 3. flush: improved keys are written in place (one untorn 64-bit update each).
-  //    Rows that received no candidate are not read (out-of-range buffer load).
-  bool any = false;
-  uint64_t nb[ROWS], cur[ROWS];
-#pragma unroll
-  for (int i = 0; i < ROWS; i++) {
-    const uint32_t r = w + WAVES * i;
-    nb[i] = best[r * BATCH + lane];
-    const uint32_t v = min(v0 + r, v1 - 1);
-    cur[i] = load_key(slab, __any(nb[i] != KEY_INF) ? v * (BATCH * 8) + lane8 : OOB);
-  }
-#pragma unroll
-  for (int i = 0; i < ROWS; i++) {
-    const uint32_t v = v0 + w + WAVES * i;
-    const bool ch = v < v1 && nb[i] < cur[i];
-    if (ch) Db[(size_t)v * BATCH + lane] = nb[i];
-    if (__any(ch)) {
-      any = true;
-      if (FRONT && lane == 0) stamp[(size_t)b * n + v] = pass + 2;
-    }
-  }
-  // every writer stores the same 1: a plain store, no same-address atomic storm
-  if (any && lane == 0) changed[b * FLAG_STRIDE] = 1u;
-  if (COUNT && threadIdx.x == 0 && n_rel)
-    atomicAdd(&work[blockIdx.x & (WORK_SHARDS - 1)], (unsigned long long)n_rel * BATCH);
+  if (threadIdx.x == 0) alist[0] = base;
 }
 
-// Wave-owned destinations: wave w of a block owns NPW consecutive nodes and
-// their best rows in its own LDS slice.  The wave's in-arcs are contiguous;
-// each staging round reads up to 64 * K of them (coalesced), compacts the dirty
-// ones into the wave's LDS list, then relaxes them GROUP at a time with GROUP
-// row reads in flight.  No block barriers and no LDS atomics (64-bit ds_min
-// measured 3x slower than this kernel's whole loop): every wave runs on its own.
-template <int NPW, int K, bool FRONT, bool COUNT>
+// B = sources per batch (64: one row per wave instruction; 32: two rows, one
+// per half-wave, and a 2.5 MB slab at 10k nodes that stays in one XCD's L2).
+template <int B, int NPW, int K, bool FRONT, bool COUNT>
 __global__ void __launch_bounds__(RELAX_THREADS)
-    k_relax_w(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
-              const uint32_t* __restrict__ in_dst, const uint32_t* __restrict__ in_lat32,
-              const float* __restrict__ in_om, uint64_t* __restrict__ D, uint32_t n, uint32_t n_batches,
-              const uint32_t* __restrict__ active, uint32_t* __restrict__ changed, uint32_t* __restrict__ stamp,
-              uint32_t pass, unsigned long long* __restrict__ work) {
+    k_relax_w(const uint32_t* __restrict__ in_off, const uint4* __restrict__ in_rec, uint64_t* __restrict__ D,
+              uint32_t n, const uint32_t* __restrict__ alist, uint32_t* __restrict__ changed,
+              uint32_t* __restrict__ stamp, uint32_t pass, unsigned long long* __restrict__ work) {
   constexpr int WAVES = RELAX_THREADS / 64;
   constexpr int STG_W = 64 * K;
+  constexpr int G = 64 / B;  // rows per wave instruction
+  static_assert(NPW % G == 0, "NPW must be a multiple of the rows per instruction");
   __shared__ uint4 lists[WAVES][STG_W];  // (source row byte offset, destination slot, latency, 1 - loss)
-  __shared__ unsigned long long bests[WAVES][NPW * BATCH];
+  __shared__ unsigned long long bests[WAVES][NPW * B];
   const int lane = threadIdx.x & 63;
+  const uint32_t gh = lane / B, sl = lane % B;  // row group within the instruction, source lane
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t lane8 = lane * 8;
+  const uint32_t lane8 = sl * 8;
   uint4* list = lists[w];
   unsigned long long* best = bests[w];
-  // Work items (batch, wave chunk) of the batches b = x (mod 8) go to the blocks
-  // L = x (mod 8), i.e. to XCD x under round-robin dispatch; consecutive items
-  // are consecutive chunks of one batch, so an XCD's resident waves share a slab.
+  // Work items (active batch, wave chunk): the active batches with list index
+  // i = x (mod 8) go to the blocks L = x (mod 8), i.e. to XCD x under
+  // round-robin dispatch, so the remaining work stays spread over all XCDs as
+  // batches converge; consecutive items are consecutive chunks of one batch, so
+  // an XCD's resident waves share a slab.
   const uint32_t x = blockIdx.x & 7;
   const uint32_t nwc = (n + NPW - 1) / NPW;
-  const uint32_t nbx = n_batches > x ? (n_batches - x + 7) / 8 : 0;
+  const uint32_t n_act = alist[0];
+  const uint32_t nbx = n_act > x ? (n_act - x + 7) / 8 : 0;
   const uint32_t items = nbx * nwc;
   const uint32_t stride = (gridDim.x >> 3) * WAVES;
   uint32_t n_rel = 0, flagged = ~0u;
   for (uint32_t it = (blockIdx.x >> 3) * WAVES + w; it < items; it += stride) {
-    const uint32_t b = x + 8 * (it / nwc);
+    const uint32_t b = alist[1 + x + 8 * (it / nwc)];
     const uint32_t vw = (it % nwc) * NPW;
-    if (!active[b * FLAG_STRIDE]) continue;
     const uint32_t vw1 = min(vw + NPW, n);
-    uint64_t* Db = D + (size_t)b * n * BATCH;
+    uint64_t* Db = D + (size_t)b * n * B;
     const uint32_t* St = stamp + (size_t)b * n;
-    const __amdgpu_buffer_rsrc_t slab =
-        __builtin_amdgcn_make_buffer_rsrc(Db, 0, (int)(n * BATCH * 8u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(Db, 0, (int)(n * B * 8u), 0x00020000);
 #pragma unroll
-    for (int i = 0; i < NPW; i++) best[i * BATCH + lane] = KEY_INF;
+    for (int i = 0; i < NPW * B / 64; i++) best[i * 64 + lane] = KEY_INF;
     const uint32_t a0 = in_off[vw], a1 = in_off[vw1];
     uint32_t n_cand = 0;
-    uint32_t run_slot = 0;
+    uint32_t run_slot = 0;  // per row group: records of one destination form a run
     uint64_t run = KEY_INF;
+    bool prefetched = false;
+    uint64_t cur[NPW / G];
     for (uint32_t c0 = a0; c0 < a1; c0 += STG_W) {
       const uint32_t c1 = min(c0 + STG_W, a1);
-      uint32_t ua[K];
+      uint4 ra[K];
       bool dirty[K];
 #pragma unroll
-      for (int i = 0; i < K; i++) ua[i] = in_src[min(c0 + lane + 64 * i, c1 - 1)];
+      for (int i = 0; i < K; i++) ra[i] = in_rec[min(c0 + lane + 64 * i, c1 - 1)];
 #pragma unroll
-      for (int i = 0; i < K; i++) dirty[i] = c0 + lane + 64 * i < c1 && (!FRONT || St[ua[i]] > pass);
+      for (int i = 0; i < K; i++) dirty[i] = c0 + lane + 64 * i < c1 && (!FRONT || St[ra[i].x] > pass);
       uint32_t cnt = 0;
 #pragma unroll
       for (int i = 0; i < K; i++) {
-        const uint32_t a = min(c0 + lane + 64 * i, c1 - 1);
         const uint64_t m = __ballot(dirty[i]);
         if (dirty[i])
           list[cnt + (uint32_t)__popcll(m & ((1ull << lane) - 1))] =
-              make_uint4(ua[i] * (BATCH * 8), in_dst[a] - vw, in_lat32[a], __float_as_uint(in_om[a]));
+              make_uint4(ra[i].x * (B * 8), ra[i].y - vw, ra[i].z, ra[i].w);
         cnt += (uint32_t)__popcll(m);
       }
       n_cand += cnt;
-      // Records arrive in destination order (CSC order, compaction keeps it), so
-      // each destination's candidates form one run, folded in registers; the run
-      // is stored to the destination's LDS row when the destination changes.
+      if (cnt && !prefetched) {  // this item will flush: fetch its rows now, under the relax loop
+        prefetched = true;
+#pragma unroll
+        for (int i = 0; i < NPW / G; i++)
+          cur[i] = load_key(slab, min(vw + i * G + gh, vw1 - 1) * (B * 8) + lane8);
+      }
+      // Records arrive in destination order (CSC order, compaction keeps it);
+      // row group gh takes records gh, gh + G, ..., so each destination's
+      // candidates form one run per group, folded in registers and merged into
+      // the destination's LDS row (ds_min) when the destination changes.
       uint32_t g = 0;
-      for (; g + GROUP <= cnt; g += GROUP) {
+      for (; g + GROUP * G <= cnt; g += GROUP * G) {
         uint4 r[GROUP];
         uint64_t k[GROUP];
 #pragma unroll
-        for (int j = 0; j < GROUP; j++) r[j] = list[g + j];
+        for (int j = 0; j < GROUP; j++) r[j] = list[g + j * G + gh];
 #pragma unroll
         for (int j = 0; j < GROUP; j++) k[j] = load_key(slab, r[j].x + lane8);
 #pragma unroll
         for (int j = 0; j < GROUP; j++) {
-          const uint32_t slot = __builtin_amdgcn_readfirstlane(r[j].y);
+          const uint32_t slot = G == 1 ? __builtin_amdgcn_readfirstlane(r[j].y) : r[j].y;
           if (slot != run_slot) {
-            best[run_slot * BATCH + lane] = run;
+            atomicMin(&best[run_slot * B + sl], (unsigned long long)run);
             run_slot = slot;
             run = KEY_INF;
           }
           run = min(run, relax32(k[j], r[j].z, __uint_as_float(r[j].w)));
         }
       }
-      for (; g < cnt; g++) {
-        const uint4 r = list[g];
-        const uint32_t slot = __builtin_amdgcn_readfirstlane(r.y);
-        if (slot != run_slot) {
-          best[run_slot * BATCH + lane] = run;
-          run_slot = slot;
-          run = KEY_INF;
+      for (; g < cnt; g += G) {
+        const uint32_t idx = g + gh;
+        if (idx < cnt) {
+          const uint4 r = list[idx];
+          if (r.y != run_slot) {
+            atomicMin(&best[run_slot * B + sl], (unsigned long long)run);
+            run_slot = r.y;
+            run = KEY_INF;
+          }
+          run = min(run, relax32(load_key(slab, r.x + lane8), r.z, __uint_as_float(r.w)));
         }
-        run = min(run, relax32(load_key(slab, r.x + lane8), r.z, __uint_as_float(r.w)));
       }
     }
     if (COUNT) n_rel += n_cand;
     if (!n_cand) continue;
-    best[run_slot * BATCH + lane] = run;
-    // flush: improved keys are written in place (one untorn 64-bit update each).
-    // Rows that received no candidate are not read (out-of-range buffer load).
-    uint64_t nb[NPW], cur[NPW];
-#pragma unroll
-    for (int i = 0; i < NPW; i++) {
-      nb[i] = best[i * BATCH + lane];
-      cur[i] = load_key(slab, __any(nb[i] != KEY_INF) ? min(vw + i, vw1 - 1) * (BATCH * 8) + lane8 : OOB);
-    }
+    atomicMin(&best[run_slot * B + sl], (unsigned long long)run);
+    // flush: improved keys are written in place (one untorn 64-bit update each)
     bool any = false;
 #pragma unroll
-    for (int i = 0; i < NPW; i++) {
-      const uint32_t v = vw + i;
-      const bool ch = v < vw1 && nb[i] < cur[i];
-      if (ch) Db[(size_t)v * BATCH + lane] = nb[i];
-      if (__any(ch)) {
+    for (int i = 0; i < NPW / G; i++) {
+      const uint32_t v = vw + i * G + gh;
+      const uint64_t nb = best[(i * G + gh) * B + sl];
+      const bool ch = v < vw1 && nb < cur[i];
+      if (ch) Db[(size_t)v * B + sl] = nb;
+      const uint64_t m = __ballot(ch);
+      if (m) {
         any = true;
-        if (FRONT && lane == 0) stamp[(size_t)b * n + v] = pass + 2;
+        if (FRONT && sl == 0 && ((m >> (gh * B)) & (B == 64 ? ~0ull : ((1ull << B) - 1))))
+          stamp[(size_t)b * n + v] = pass + 2;
       }
     }
     // one flag store per wave and batch (a wave's items run batch by batch)
@@ -442,30 +341,33 @@ __global__ void __launch_bounds__(RELAX_THREADS)
       flagged = b;
     }
   }
-  if (COUNT && lane == 0 && n_rel) atomicAdd(&work[blockIdx.x & (WORK_SHARDS - 1)], (unsigned long long)n_rel * BATCH);
+  if (COUNT && lane == 0 && n_rel) atomicAdd(&work[blockIdx.x & (WORK_SHARDS - 1)], (unsigned long long)n_rel * B);
 }
 
-// Transposed write-out of [64 rows x 64 cols] tiles.  Diagonal = the raw
+// Transposed write-out of [B rows x 64 cols] tiles.  Diagonal = the raw
 // self-loop (graph/mod.rs:210-217).  Saturated keys flag their batch.
+template <int B>
 __global__ void __launch_bounds__(256)
     k_out_batch(const uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ used, uint32_t n_used,
                 uint32_t first_row, uint32_t row_end, uint32_t out_row0, const uint32_t* __restrict__ self_edge,
                 const uint64_t* __restrict__ e_lat, const float* __restrict__ e_loss,
                 uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, uint32_t* __restrict__ sat) {
-  __shared__ uint64_t tile[64][BATCH + 1];
+  constexpr int G = 64 / B;
+  __shared__ uint64_t tile[64][B + 1];
   const uint32_t b = blockIdx.y;
   const uint32_t j0 = blockIdx.x * 64;
-  const uint64_t* __restrict__ Db = D + (size_t)b * n * BATCH;
+  const uint64_t* __restrict__ Db = D + (size_t)b * n * B;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int c = wave; c < 64; c += 4) {
+  const int gh = lane / B, sl = lane % B;
+  for (int c = wave * G + gh; c < 64; c += 4 * G) {
     const uint32_t j = j0 + c;
-    tile[c][lane] = j < n_used ? Db[(size_t)used[j] * BATCH + lane] : 0ull;
+    tile[c][sl] = j < n_used ? Db[(size_t)used[j] * B + sl] : 0ull;
   }
   __syncthreads();
   bool sflag = false;
   const uint32_t j = j0 + lane;
-  for (int r = wave; r < BATCH; r += 4) {
-    const uint32_t row = first_row + b * BATCH + r;
+  for (int r = wave; r < B; r += 4) {
+    const uint32_t row = first_row + b * B + r;
     if (row >= row_end || j >= n_used) continue;
     const size_t o = (size_t)(row - out_row0) * n_used + j;
     if (row == j) {
@@ -699,39 +601,16 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   net->in_lat = dmalloc<uint64_t>(n_arcs);
   net->in_lat32 = dmalloc<uint32_t>(n_arcs);
   net->in_om = dmalloc<float>(n_arcs);
+  net->in_rec = dmalloc<uint4>(n_arcs);
   if (n_arcs) {
     uint32_t* cursor = ctx->r_map.get<uint32_t>((size_t)n + 1);
     SG_HIP(hipMemcpyAsync(cursor, net->in_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(k_scatter_arcs, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src,
                        net->e_dst, net->e_lat, net->e_loss, m, (int)net->directed, cursor,
-                       net->in_src, net->in_dst, net->in_lat, net->in_lat32, net->in_om);
+                       net->in_src, net->in_dst, net->in_lat, net->in_lat32, net->in_om, net->in_rec);
     SG_CHECK_LAUNCH();
   }
-  net->h_in_off.resize((size_t)n + 1);
-  copy_to_host(ctx, net->h_in_off.data(), net->in_off, ((size_t)n + 1) * 4);
   SG_HIP(hipStreamSynchronize(st));
-}
-
-// Relaxation chunks: consecutive destination nodes, at most `nodes` of them
-// and about `arcs` in-arcs (a hub node gets a chunk of its own).
-static void ensure_chunks(sg_ctx* ctx, sg_net* net, uint32_t nodes, uint32_t arcs) {
-  if (net->chunk_v && net->chunk_nodes == nodes && net->chunk_arcs == arcs) return;
-  const uint32_t n = net->n_nodes;
-  const std::vector<uint32_t>& off = net->h_in_off;
-  std::vector<uint32_t> cv{0};
-  for (uint32_t v = 0; v < n;) {
-    uint32_t e = v + 1;
-    while (e < n && e - v < nodes && off[e + 1] - off[v] <= arcs) e++;
-    cv.push_back(e);
-    v = e;
-  }
-  if (net->chunk_v) SG_HIP(hipFree(net->chunk_v));
-  net->chunk_v = dmalloc<uint32_t>(cv.size());
-  net->n_chunks = (uint32_t)cv.size() - 1;
-  net->chunk_nodes = nodes;
-  net->chunk_arcs = arcs;
-  SG_HIP(hipMemcpyAsync(net->chunk_v, cv.data(), cv.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
 }
 
 static void check_self_loops(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
@@ -801,45 +680,49 @@ static void run_wide(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t 
   }
 }
 
-// WAVE_OWNED: k_relax_w with CN nodes per wave and STG staged arcs per wave;
-// otherwise k_relax with CN nodes per block and STG staged arcs per block.
-template <int CN, int STG, bool FRONT, bool WAVE_OWNED>
+// B sources per batch, NPW destination nodes per wave item, STG arcs staged per
+// wave step, FRONT = stamp frontier.
+template <int B, int NPW, int STG, bool FRONT>
 static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                              uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
   hipStream_t st = ctx->stream;
   const uint32_t n = net->n_nodes;
   const uint32_t n_rows = row_end - row_begin;
-  const uint32_t n_batches = (n_rows + BATCH - 1) / BATCH;
-  if (!WAVE_OWNED) ensure_chunks(ctx, net, CN, (uint32_t)env_int("SG_APSP_CHUNK_ARCS", 16 * CN));
+  const uint32_t n_batches = (n_rows + B - 1) / B;
   // Group: batches whose slabs are live together (bounded device memory).
-  const size_t slab_bytes = (size_t)n * BATCH * 8;
+  const size_t slab_bytes = (size_t)n * B * 8;
   const size_t budget = (size_t)env_int("SG_APSP_GROUP_MB", 4096) << 20;
   const uint32_t group = (uint32_t)std::max<size_t>(1, std::min<size_t>(n_batches, budget / slab_bytes));
-  uint64_t* D = ctx->r_dist.get<uint64_t>((size_t)group * n * BATCH);
+  uint64_t* D = ctx->r_dist.get<uint64_t>((size_t)group * n * B);
   uint32_t* stamp = ctx->r_dirty.get<uint32_t>((size_t)group * n);
-  // per-batch flags: a 3-slot ring of "changed in pass p" arrays, then the saturation flags
+  // per-batch flags: a 3-slot ring of "changed in pass p" arrays, the
+  // saturation flags, the active-batch list
   const size_t fs = (size_t)group * FLAG_STRIDE;
-  uint32_t* flags = ctx->r_flags.get<uint32_t>(fs * 3 + group + 8);
+  uint32_t* flags = ctx->r_flags.get<uint32_t>(fs * 3 + 2 * (size_t)group + 8);
   uint32_t* ring[3] = {flags, flags + fs, flags + 2 * fs};
   uint32_t* sat = flags + 3 * fs;
+  uint32_t* alist = sat + group;
   unsigned long long* work = ctx->timing ? ctx->r_work.get<unsigned long long>(WORK_SHARDS) : nullptr;
   if (work) SG_HIP(hipMemsetAsync(work, 0, WORK_SHARDS * 8, st));
   // Passes are issued in chunks; the host reads the convergence flags once per
-  // chunk.  A pass issued after its batch converged exits at once (active == 0).
+  // chunk.  A pass issued after its batch converged finds it off the active list.
   const uint32_t chunk = (uint32_t)std::max(1, env_int("SG_APSP_PASS_CHUNK", 4));
+  const bool trace = env_int("SG_APSP_TRACE", 0) != 0;  // per-pass diagnostics on stderr
   std::vector<uint32_t> h_changed(fs), h_sat(group);
   std::vector<uint32_t> wide_rows;
   for (uint32_t g0 = 0; g0 < n_batches; g0 += group) {
     const uint32_t gb = std::min(group, n_batches - g0);
-    const uint32_t first_row = row_begin + g0 * BATCH;
-    hipLaunchKernelGGL(k_init_batch, dim3(grid_for((size_t)gb * n * BATCH, 256, 65536)), dim3(256), 0, st, D,
+    const uint32_t first_row = row_begin + g0 * B;
+    hipLaunchKernelGGL(k_init_batch<B>, dim3(grid_for((size_t)gb * n * B, 256, 65536)), dim3(256), 0, st, D,
                        stamp, n, d_used, first_row, row_end, gb);
-    hipLaunchKernelGGL(k_stamp_sources, dim3(grid_for((size_t)gb * BATCH, 256)), dim3(256), 0, st, stamp, n,
+    hipLaunchKernelGGL(k_stamp_sources<B>, dim3(grid_for((size_t)gb * B, 256)), dim3(256), 0, st, stamp, n,
                        d_used, first_row, row_end, gb);
     SG_CHECK_LAUNCH();
     SG_HIP(hipMemsetAsync(ring[2], 1, gb * FLAG_STRIDE * 4ull, st));  // "changed in pass -1": every batch active
-    const uint32_t grid = 8 * net->n_chunks * ((gb + 7) / 8);
-    const bool trace = env_int("SG_APSP_TRACE", 0) != 0;  // per-pass diagnostics on stderr
+    // one wave per work item (active batch, NPW-node chunk); 4 waves per block,
+    // a multiple of 8 blocks (XCD mapping)
+    const uint32_t ncw = (n + 4 * NPW - 1) / (4 * NPW);
+    const uint32_t grid = 8 * ncw * ((gb + 7) / 8);
     hipEvent_t te0 = nullptr, te1 = nullptr;
     if (trace) {
       SG_HIP(hipEventCreate(&te0));
@@ -849,36 +732,20 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
     for (uint32_t pass = 0;;) {
       uint32_t last = pass;
       for (uint32_t c = 0; c < chunk; c++, pass++) {
-        if (trace) SG_HIP(hipEventRecord(te0, st));
         if (pass > n + 2 + chunk) throw Error(SG_ERR_DEVICE, "relaxation did not converge");
+        if (trace) SG_HIP(hipEventRecord(te0, st));
         const uint32_t* active = ring[(pass + 2) % 3];
         uint32_t* changed = ring[pass % 3];
         SG_HIP(hipMemsetAsync(changed, 0, gb * FLAG_STRIDE * 4ull, st));
-        if constexpr (WAVE_OWNED) {
-          TimedLaunch tl(ctx, "relax", 0.0);
-          constexpr int NPW = CN;  // nodes per wave
-          // persistent grid: SG_APSP_BLOCKS_PER_CU resident blocks per CU (0 = one block per work item)
-          const int bpc = env_int("SG_APSP_BLOCKS_PER_CU", 0);
-          const uint32_t ncw = (n + 4 * NPW - 1) / (4 * NPW);
-          const uint32_t gridw = bpc > 0 ? 8 * (uint32_t)((ctx->n_cu * bpc + 7) / 8) : 8 * ncw * ((gb + 7) / 8);
-          if (work)
-            hipLaunchKernelGGL((k_relax_w<NPW, STG / 64, FRONT, true>), dim3(gridw), dim3(RELAX_THREADS), 0, st,
-                               net->in_off, net->in_src, net->in_dst, net->in_lat32, net->in_om, D, n, gb,
-                               active, changed, stamp, pass, work);
-          else
-            hipLaunchKernelGGL((k_relax_w<NPW, STG / 64, FRONT, false>), dim3(gridw), dim3(RELAX_THREADS), 0, st,
-                               net->in_off, net->in_src, net->in_dst, net->in_lat32, net->in_om, D, n, gb,
-                               active, changed, stamp, pass, work);
-        } else {
+        hipLaunchKernelGGL(k_active_list, dim3(1), dim3(1024), 0, st, active, gb, alist);
+        {
           TimedLaunch tl(ctx, "relax", 0.0);
           if (work)
-            hipLaunchKernelGGL((k_relax<CN, STG, FRONT, true>), dim3(grid), dim3(RELAX_THREADS), 0, st, net->chunk_v,
-                               net->n_chunks, net->in_off, net->in_src, net->in_dst, net->in_lat32, net->in_om, D,
-                               n, gb, active, changed, stamp, pass, work);
+            hipLaunchKernelGGL((k_relax_w<B, NPW, STG / 64, FRONT, true>), dim3(grid), dim3(RELAX_THREADS), 0, st,
+                               net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
           else
-            hipLaunchKernelGGL((k_relax<CN, STG, FRONT, false>), dim3(grid), dim3(RELAX_THREADS), 0, st, net->chunk_v,
-                               net->n_chunks, net->in_off, net->in_src, net->in_dst, net->in_lat32, net->in_om, D,
-                               n, gb, active, changed, stamp, pass, work);
+            hipLaunchKernelGGL((k_relax_w<B, NPW, STG / 64, FRONT, false>), dim3(grid), dim3(RELAX_THREADS), 0, st,
+                               net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
         }
         SG_CHECK_LAUNCH();
         last = pass;
@@ -891,10 +758,8 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
           if (work) copy_to_host(ctx, w, work, sizeof(w));
           double tot = 0;
           for (int k = 0; k < WORK_SHARDS; k++) tot += (double)w[k];
-          std::vector<uint32_t> act(gb * FLAG_STRIDE);
-          copy_to_host(ctx, act.data(), ring[(pass + 2) % 3], gb * FLAG_STRIDE * 4ull);
           uint32_t na = 0;
-          for (uint32_t b = 0; b < gb; b++) na += act[b * FLAG_STRIDE] != 0;
+          copy_to_host(ctx, &na, alist, 4);
           fprintf(stderr, "[apsp] group %u pass %u: %.3f ms, %u active batches, %.3f G lane-relaxations\n", g0, pass,
                   ms, na, (tot - trace_prev) / 1e9);
           trace_prev = tot;
@@ -911,8 +776,8 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
     }
     SG_HIP(hipMemsetAsync(sat, 0, gb * 4ull, st));
     {
-      TimedLaunch tl(ctx, "out", 12.0 * std::min<uint32_t>(gb * BATCH, row_end - first_row) * n_used);
-      hipLaunchKernelGGL(k_out_batch, dim3((n_used + 63) / 64, gb), dim3(256), 0, st, D, n, d_used, n_used,
+      TimedLaunch tl(ctx, "out", 12.0 * std::min<uint32_t>(gb * B, row_end - first_row) * n_used);
+      hipLaunchKernelGGL(k_out_batch<B>, dim3((n_used + 63) / 64, gb), dim3(256), 0, st, D, n, d_used, n_used,
                          first_row, row_end, row_begin, net->self_edge, net->e_lat, net->e_loss, out_lat,
                          out_loss, sat);
     }
@@ -920,8 +785,8 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
     copy_to_host(ctx, h_sat.data(), sat, gb * 4ull);
     for (uint32_t b = 0; b < gb; b++)
       if (h_sat[b])
-        for (uint32_t r = 0; r < BATCH; r++) {
-          uint32_t row = first_row + b * BATCH + r;
+        for (uint32_t r = 0; r < B; r++) {
+          uint32_t row = first_row + b * B + r;
           if (row < row_end) wide_rows.push_back(row);
         }
   }
@@ -936,31 +801,27 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 }
 
 // A/B measurement knobs: SG_APSP_FRONTIER=0 relaxes every arc every pass;
-// SG_APSP_KERNEL = w (wave-owned nodes) | b (block-owned nodes);
-// SG_APSP_CN nodes per wave (w: 8 | 16) or per block (b: 32 | 64);
-// SG_APSP_STAGE staged arcs per wave (w: 128 | 256) or per block (b: 512 | 1024).
+// SG_APSP_B sources per batch (32 | 64); SG_APSP_NPW nodes per wave item;
+// SG_APSP_STAGE arcs staged per wave step.
 static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                            uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
   const bool front = env_int("SG_APSP_FRONTIER", 1) != 0;
-  const char* kv = getenv("SG_APSP_KERNEL");
-  const bool wave = !(kv && kv[0] == 'b');
-  const int cn = env_int("SG_APSP_CN", wave ? 8 : 64), stg = env_int("SG_APSP_STAGE", wave ? 128 : 1024);
-#define SG_SP(W_, CN_, STG_)                                                                          \
-  if (wave == W_ && cn == CN_ && stg == STG_) {                                                      \
-    if (front)                                                                                       \
-      shortest_paths_t<CN_, STG_, true, W_>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss); \
-    else                                                                                             \
-      shortest_paths_t<CN_, STG_, false, W_>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss); \
-    return;                                                                                          \
+  const int bsz = env_int("SG_APSP_B", 64), npw = env_int("SG_APSP_NPW", 8), stg = env_int("SG_APSP_STAGE", 128);
+#define SG_SP(B_, NPW_, STG_)                                                                            \
+  if (bsz == B_ && npw == NPW_ && stg == STG_) {                                                        \
+    if (front)                                                                                          \
+      shortest_paths_t<B_, NPW_, STG_, true>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss);  \
+    else                                                                                                \
+      shortest_paths_t<B_, NPW_, STG_, false>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss); \
+    return;                                                                                             \
   }
-  SG_SP(true, 8, 128)
-  SG_SP(true, 8, 256)
-  SG_SP(true, 16, 128)
-  SG_SP(true, 16, 256)
-  SG_SP(false, 32, 512)
-  SG_SP(false, 64, 1024)
+  SG_SP(64, 8, 128)
+  SG_SP(64, 16, 128)
+  SG_SP(32, 8, 128)
+  SG_SP(32, 16, 128)
+  SG_SP(32, 4, 64)
 #undef SG_SP
-  throw Error(SG_ERR_INVALID_ARG, "unsupported SG_APSP_KERNEL / SG_APSP_CN / SG_APSP_STAGE");
+  throw Error(SG_ERR_INVALID_ARG, "unsupported SG_APSP_B / SG_APSP_NPW / SG_APSP_STAGE");
 }
 
 static void direct_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, const uint32_t* h_used,
