@@ -90,20 +90,22 @@ __global__ void k_seed_hosts(const uint64_t* __restrict__ seed, uint32_t n, uint
   }
 }
 
-__global__ void k_seg_bounds(const uint32_t* __restrict__ src, uint32_t P, uint32_t H,
-                             uint32_t* __restrict__ seg_begin, uint32_t* __restrict__ seg_end,
-                             uint32_t* __restrict__ err) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < P; i += gridDim.x * blockDim.x) {
-    uint32_t h = src[i];
-    if (h >= H) {
+// Host CSR over the packets: host_off[h] = first packet whose source is >= h
+// (h = 0..H).  Also checks the grouping (ascending source hosts).
+__global__ void k_host_off(const uint32_t* __restrict__ src, uint32_t P, uint32_t H,
+                           uint32_t* __restrict__ host_off, uint32_t* __restrict__ err) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i <= P; i += gridDim.x * blockDim.x) {
+    const uint32_t s = i < P ? src[i] : H;
+    if (s > H || (i < P && s == H)) {
       atomicOr(err, ERR_SRC_RANGE);
       continue;
     }
-    uint32_t prev = i ? src[i - 1] : NONE;
-    uint32_t next = i + 1 < P ? src[i + 1] : NONE;
-    if (i && prev > h) atomicOr(err, ERR_UNSORTED);
-    if (prev != h) seg_begin[h] = i;
-    if (next != h) seg_end[h] = i + 1;
+    const int64_t prev = i ? (int64_t)min(src[i - 1], H) : -1;
+    if (prev > (int64_t)s) {
+      atomicOr(err, ERR_UNSORTED);
+      continue;
+    }
+    for (int64_t h = prev + 1; h <= (int64_t)s; h++) host_off[h] = i;
   }
 }
 
@@ -113,8 +115,7 @@ struct WalkArgs {
   const uint32_t* payload;
   const uint64_t* send;
   uint32_t P, H;
-  const uint32_t* seg_begin;
-  const uint32_t* seg_end;
+  const uint32_t* host_off;
   const uint32_t* route;
   uint64_t* rng;
   uint64_t* ctr;
@@ -128,81 +129,191 @@ struct WalkArgs {
   uint64_t* eid;
   uint32_t* dst_host;
   uint32_t* dst_cnt;
-  unsigned long long* stats;  // [n_delivered, min_deliver, min_lat]
+  unsigned long long* blk_stats;  // per block: [n_delivered, min_deliver, min_lat] (reduced by k_reduce_stats)
   uint32_t* err;
 };
 
-// One thread per source host: the host's RNG stream is sequential
-// (Host::random_mut, host.rs:645-647), so its packets are walked in send order.
-__global__ void __launch_bounds__(256) k_walk(WalkArgs a) {
-  const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+// A block owns WALK_HOSTS consecutive source hosts; their packets are one
+// contiguous range, processed in chunks of WALK_CHUNK staged in LDS:
+//  1. packet-parallel (all threads, coalesced): send time, destination
+//     resolution (Dns::addr_to_host_id, worker.rs:341), path gather
+//     (latency, loss) -- every independent load in flight at once;
+//  2. host-sequential (one lane per host): the host's packets in send order
+//     against its Xoshiro256++ stream -- only LDS traffic on the serial chain;
+//  3. packet-parallel: coalesced stores of status, arrival time, event id and
+//     destination.
+constexpr int WALK_THREADS = 256;
+constexpr int WALK_HOSTS = 64;
+constexpr int WALK_CHUNK = 1024;
+enum : uint8_t { W_SIM_END = 0, W_NO_DST = 1, W_DRAW = 2, W_PAYLOAD = 4, W_BOOT = 8 };
+
+__global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
+  __shared__ uint64_t s_t[WALK_CHUNK];   // send time -> arrival time
+  __shared__ uint64_t s_l[WALK_CHUNK];   // path latency -> event id
+  __shared__ float s_loss[WALK_CHUNK];   // path packet loss
+  __shared__ uint32_t s_d[WALK_CHUNK];   // destination host -> NONE unless delivered
+  __shared__ uint8_t s_f[WALK_CHUNK];    // W_* flags -> SG_PKT_* status
+  const uint32_t h0 = blockIdx.x * WALK_HOSTS;
+  const uint32_t t = threadIdx.x;
+  const uint32_t p0 = a.host_off[min(h0, a.H)], p1 = a.host_off[min(h0 + WALK_HOSTS, a.H)];
+  // walker lanes: thread t < WALK_HOSTS walks host h0 + t
+  const uint32_t h = h0 + t;
+  const bool walker = t < WALK_HOSTS && h < a.H;
+  uint32_t hb = 0, he = 0;
+  Xoshiro x{0, 0, 0, 0};
+  uint64_t c = 0;
+  if (walker) {
+    hb = a.host_off[h];
+    he = a.host_off[h + 1];
+    if (hb < he) {
+      x = Xoshiro{a.rng[h], a.rng[(size_t)a.H + h], a.rng[2 * (size_t)a.H + h], a.rng[3 * (size_t)a.H + h]};
+      c = a.ctr[h];
+    }
+  }
   unsigned long long nd = 0, mind = ~0ull, minl = ~0ull;
-  if (h < a.H) {
-    const uint32_t b = a.seg_begin[h], e = a.seg_end[h];
-    if (b < e) {
-      const uint32_t r = a.route[h];
-      if (r < a.row_begin || r - a.row_begin >= a.n_rows) {
-        atomicOr(a.err, ERR_ROUTE_RANGE);
-      } else {
-        const size_t row = (size_t)(r - a.row_begin) * a.n_cols;
-        Xoshiro x{a.rng[h], a.rng[(size_t)a.H + h], a.rng[2 * (size_t)a.H + h],
-                  a.rng[3 * (size_t)a.H + h]};
-        uint64_t c = a.ctr[h];
-        for (uint32_t i = b; i < e; i++) {
-          const uint64_t now = a.send[i];
-          uint8_t st;
-          uint64_t t = 0, id = ~0ull;
-          uint32_t d = NONE;
-          if (now >= a.sim_end) {  // worker.rs:332-335
-            st = SG_PKT_SIM_END;
+  for (uint32_t c0 = p0; c0 < p1; c0 += WALK_CHUNK) {
+    const uint32_t c1 = min(c0 + WALK_CHUNK, p1);
+    // 1. packet-parallel gather
+    for (uint32_t i = c0 + t; i < c1; i += WALK_THREADS) {
+      const uint32_t k = i - c0;
+      const uint64_t now = a.send[i];
+      uint8_t f = a.payload[i] > 0 ? W_PAYLOAD : 0;
+      if (now < a.bootstrap_end) f |= W_BOOT;
+      uint32_t d = NONE;
+      uint64_t lat = 0;
+      float loss = 0.0f;
+      if (now < a.sim_end) {  // worker.rs:332-335
+        d = a.map.resolve(a.dst_ip[i]);
+        if (d == NONE) {
+          f |= W_NO_DST;
+        } else {
+          const uint32_t r = a.route[a.src[i]];
+          if (r < a.row_begin || r - a.row_begin >= a.n_rows) {
+            atomicOr(a.err, ERR_ROUTE_RANGE);
+            f |= W_NO_DST;
+            d = NONE;
           } else {
-            d = a.map.resolve(a.dst_ip[i]);  // worker.rs:341
-            if (d == NONE) {
-              st = SG_PKT_DROP_NO_DST;
-            } else {
-              const size_t cell = row + a.route[d];
-              // reliability = f64::from(1.0f32 - loss) (worker.rs:357-359, 526-531)
-              const double rel = (double)__fsub_rn(1.0f, a.tab_loss[cell]);
-              const double chance = x.next_f64();  // worker.rs:360
-              const bool boot = now < a.bootstrap_end;
-              if (!boot && chance >= rel && a.payload[i] > 0) {  // worker.rs:365-368
-                st = SG_PKT_DROP_LOSS;
-                d = NONE;
-              } else {
-                const uint64_t lat = a.tab_lat[cell];  // worker.rs:370
-                t = now + lat;
-                if (t < a.round_end) t = a.round_end;  // worker.rs:381-384
-                id = c++;                              // host.rs:649-653
-                st = SG_PKT_DELIVERED;
-                nd++;
-                mind = min(mind, (unsigned long long)t);
-                minl = min(minl, (unsigned long long)lat);
-                atomicAdd(&a.dst_cnt[d], 1u);
-              }
-            }
+            const size_t cell = (size_t)(r - a.row_begin) * a.n_cols + a.route[d];
+#ifndef SG_EXPERIMENT_NOGATHER
+            lat = a.tab_lat[cell];
+            loss = a.tab_loss[cell];
+#else
+            lat = 1000 + (cell & 1);
+#endif
+            f |= W_DRAW;
           }
-          a.status[i] = st;
-          a.deliver[i] = t;
-          a.eid[i] = id;
-          a.dst_host[i] = d;
         }
-        a.rng[h] = x.s0;
-        a.rng[(size_t)a.H + h] = x.s1;
-        a.rng[2 * (size_t)a.H + h] = x.s2;
-        a.rng[3 * (size_t)a.H + h] = x.s3;
-        a.ctr[h] = c;
+      }
+      s_t[k] = now;
+      s_l[k] = lat;
+      s_loss[k] = loss;
+      s_d[k] = d;
+      s_f[k] = f;
+    }
+    __syncthreads();
+    // 2. host-sequential walk (worker.rs:326-397)
+    if (walker) {
+      const uint32_t b = max(hb, c0), e = min(he, c1);
+      for (uint32_t i = b; i < e; i++) {
+        const uint32_t k = i - c0;
+        const uint8_t f = s_f[k];
+        uint8_t st;
+        uint64_t arr = 0, id = ~0ull;
+        uint32_t d = s_d[k];
+        if (f & W_DRAW) {
+          // reliability = f64::from(1.0f32 - loss) (worker.rs:357-359, 526-531)
+          const double rel = (double)__fsub_rn(1.0f, s_loss[k]);
+          const double chance = x.next_f64();  // worker.rs:360
+          if (!(f & W_BOOT) && chance >= rel && (f & W_PAYLOAD)) {  // worker.rs:365-368
+            st = SG_PKT_DROP_LOSS;
+            d = NONE;
+          } else {
+            const uint64_t lat = s_l[k];  // worker.rs:370
+            arr = s_t[k] + lat;
+            if (arr < a.round_end) arr = a.round_end;  // worker.rs:381-384
+            id = c++;                                  // host.rs:649-653
+            st = SG_PKT_DELIVERED;
+            nd++;
+            mind = min(mind, (unsigned long long)arr);
+            minl = min(minl, (unsigned long long)lat);
+#ifndef SG_EXPERIMENT_NOCNT
+            atomicAdd(&a.dst_cnt[d], 1u);
+#endif
+          }
+        } else {
+          st = (f & W_NO_DST) ? SG_PKT_DROP_NO_DST : SG_PKT_SIM_END;
+          d = NONE;
+        }
+        s_t[k] = arr;
+        s_l[k] = id;
+        s_d[k] = d;
+        s_f[k] = st;
       }
     }
+    __syncthreads();
+    // 3. coalesced stores
+    for (uint32_t i = c0 + t; i < c1; i += WALK_THREADS) {
+      const uint32_t k = i - c0;
+      a.status[i] = s_f[k];
+      a.deliver[i] = s_t[k];
+      a.eid[i] = s_l[k];
+      a.dst_host[i] = s_d[k];
+    }
+    __syncthreads();
+  }
+  if (walker && hb < he) {
+    a.rng[h] = x.s0;
+    a.rng[(size_t)a.H + h] = x.s1;
+    a.rng[2 * (size_t)a.H + h] = x.s2;
+    a.rng[3 * (size_t)a.H + h] = x.s3;
+    a.ctr[h] = c;
+  }
+  if (t < 64) {  // the walkers are wave 0
+    for (int dd = 32; dd > 0; dd >>= 1) {
+      nd += __shfl_xor(nd, dd, 64);
+      mind = min(mind, (unsigned long long)__shfl_xor(mind, dd, 64));
+      minl = min(minl, (unsigned long long)__shfl_xor(minl, dd, 64));
+    }
+    // plain per-block stores: thousands of same-address atomics serialise at the memory
+    if (t == 0) {
+      a.blk_stats[3 * blockIdx.x] = nd;
+      a.blk_stats[3 * blockIdx.x + 1] = mind;
+      a.blk_stats[3 * blockIdx.x + 2] = minl;
+    }
+  }
+}
+
+// Round statistics: sum / min / min over the walk blocks' partials.
+__global__ void __launch_bounds__(1024) k_reduce_stats(const unsigned long long* __restrict__ blk, uint32_t n,
+                                                       unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long r[3][16];
+  unsigned long long nd = 0, mind = ~0ull, minl = ~0ull;
+  for (uint32_t i = threadIdx.x; i < n; i += 1024) {
+    nd += blk[3 * i];
+    mind = min(mind, blk[3 * i + 1]);
+    minl = min(minl, blk[3 * i + 2]);
   }
   for (int d = 32; d > 0; d >>= 1) {
     nd += __shfl_xor(nd, d, 64);
     mind = min(mind, (unsigned long long)__shfl_xor(mind, d, 64));
     minl = min(minl, (unsigned long long)__shfl_xor(minl, d, 64));
   }
-  if ((threadIdx.x & 63) == 0 && nd) {
-    atomicAdd(&a.stats[0], nd);
-    atomicMin(&a.stats[1], mind);
-    atomicMin(&a.stats[2], minl);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    r[0][w] = nd;
+    r[1][w] = mind;
+    r[2][w] = minl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 16; i++) {
+      nd += r[0][i];
+      mind = min(mind, r[1][i]);
+      minl = min(minl, r[2][i]);
+    }
+    out[0] = nd;
+    out[1] = mind;
+    out[2] = minl;
   }
 }
 
@@ -493,7 +604,7 @@ static void sort_buckets(sg_ctx* ctx, const uint32_t* off, uint32_t n_buckets, u
 }
 
 struct RoundWork {
-  uint32_t *seg_begin, *seg_end, *dst_cnt, *cur, *big_count, *err, *dst_host;
+  uint32_t *host_off, *dst_cnt, *cur, *big_count, *err, *dst_host;
   uint64_t* ctr_start;
   unsigned long long* stats;
 };
@@ -506,26 +617,25 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   hipStream_t st = ctx->stream;
   const uint32_t P = pk->n_packets, H = hs->n;
   RoundWork w;
-  // workspace: [seg_begin H][seg_end H][dst_cnt H][cur H][big_count 1][err 1]
+  // workspace: [host_off H+1][dst_cnt H][cur H][big_count 1][err 1]
   uint32_t* ws = ctx->d_seg.get<uint32_t>(4 * (size_t)H + 8);
-  w.seg_begin = ws;
-  w.seg_end = ws + H;
-  w.dst_cnt = ws + 2 * (size_t)H;
-  w.cur = ws + 3 * (size_t)H;
-  w.big_count = ws + 4 * (size_t)H;
+  w.host_off = ws;
+  w.dst_cnt = ws + (size_t)H + 1;
+  w.cur = w.dst_cnt + H;
+  w.big_count = w.cur + H;
   w.err = w.big_count + 1;
   w.stats = ctx->d_misc.get<unsigned long long>(4);
   w.dst_host = ctx->d_dst.get<uint32_t>(P);
   w.ctr_start = want_ctr_start ? ctx->d_ctr0.get<uint64_t>(H) : nullptr;
   SG_HIP(hipMemsetAsync(ws, 0, (4 * (size_t)H + 8) * 4, st));
-  SG_HIP(hipMemsetAsync(w.stats, 0, 8, st));
+  SG_HIP(hipMemsetAsync(w.stats, 0, 8, st));  // P = 0: no walk, no reduction
   SG_HIP(hipMemsetAsync(w.stats + 1, 0xff, 16, st));
   if (w.ctr_start) SG_HIP(hipMemcpyAsync(w.ctr_start, hs->ctr, (size_t)H * 8, hipMemcpyDeviceToDevice, st));
   if (!P) return w;
   {
-    TimedLaunch tl(ctx, "seg_bounds", 4.0 * P + 8.0 * H);
-    hipLaunchKernelGGL(k_seg_bounds, dim3(grid_for(P, 256, 16384)), dim3(256), 0, st, pk->src_host, P, H,
-                       w.seg_begin, w.seg_end, w.err);
+    TimedLaunch tl(ctx, "seg_bounds", 4.0 * P + 4.0 * H);
+    hipLaunchKernelGGL(k_host_off, dim3(grid_for((size_t)P + 1, 256, 16384)), dim3(256), 0, st, pk->src_host, P, H,
+                       w.host_off, w.err);
   }
   WalkArgs a;
   a.src = pk->src_host;
@@ -534,8 +644,7 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   a.send = pk->send_time_ns;
   a.P = P;
   a.H = H;
-  a.seg_begin = w.seg_begin;
-  a.seg_end = w.seg_end;
+  a.host_off = w.host_off;
   a.route = hs->route;
   a.rng = hs->rng;
   a.ctr = hs->ctr;
@@ -553,14 +662,16 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   a.eid = eid;
   a.dst_host = w.dst_host;
   a.dst_cnt = w.dst_cnt;
-  a.stats = w.stats;
+  const uint32_t walk_blocks = (H + WALK_HOSTS - 1) / WALK_HOSTS;
+  a.blk_stats = ctx->d_blk.get<unsigned long long>(3 * (size_t)walk_blocks);
   a.err = w.err;
   {
     // per packet: 20 B in, 12 B path gather, 4 B dst map, 21 B out (status, time, id), 4 B dst scratch;
     // per host: 8 B segment, 4 B route, 32+32 B RNG, 8+8 B event counter
     TimedLaunch tl(ctx, "walk", 61.0 * P + 92.0 * H);
-    hipLaunchKernelGGL(k_walk, dim3(grid_for(H, 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_walk, dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
   }
+  hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(1024), 0, st, a.blk_stats, walk_blocks, w.stats);
   SG_CHECK_LAUNCH();
   return w;
 }

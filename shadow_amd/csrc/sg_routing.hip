@@ -436,7 +436,7 @@ __global__ void __launch_bounds__(RELAX_BLOCK)
   Ln[base + (size_t)v * BATCH + lane] = bl;
   Fn[base + (size_t)v * BATCH + lane] = bf;
   bool ch = bl != l_in || __float_as_uint(bf) != __float_as_uint(f_in);
-  if (__any(ch) && lane == 0) atomicOr(changed, 1u);
+  if (__any(ch) && lane == 0) *changed = 1u;  // plain store: the line stays in L2
 }
 
 __global__ void k_out_wide(const uint64_t* __restrict__ L, const float* __restrict__ F, uint32_t n,
@@ -521,14 +521,28 @@ __global__ void k_pair_out(const uint32_t* __restrict__ cnt, const uint32_t* __r
   }
 }
 
-__global__ void k_min_u64(const uint64_t* __restrict__ x, size_t count,
-                          unsigned long long* __restrict__ out) {
+// Two-stage minimum: per-block partials (plain stores), then one block.
+__global__ void __launch_bounds__(256) k_min_u64(const uint64_t* __restrict__ x, size_t count,
+                                                 unsigned long long* __restrict__ part) {
+  __shared__ unsigned long long wm[4];
   unsigned long long m = ~0ull;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
-       i += (size_t)gridDim.x * blockDim.x)
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x)
     m = min(m, (unsigned long long)x[i]);
   for (int d = 32; d > 0; d >>= 1) m = min(m, (unsigned long long)__shfl_xor(m, d, 64));
-  if ((threadIdx.x & 63) == 0) atomicMin(out, m);
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = min(min(wm[0], wm[1]), min(wm[2], wm[3]));
+}
+
+__global__ void __launch_bounds__(256) k_min_final(const unsigned long long* __restrict__ part, uint32_t n,
+                                                   unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long wm[4];
+  unsigned long long m = ~0ull;
+  for (uint32_t i = threadIdx.x; i < n; i += 256) m = min(m, part[i]);
+  for (int d = 32; d > 0; d >>= 1) m = min(m, (unsigned long long)__shfl_xor(m, d, 64));
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = min(min(wm[0], wm[1]), min(wm[2], wm[3]));
 }
 
 // ---------------------------------------------------------------------------
@@ -932,9 +946,12 @@ int32_t sg_routing_min_latency(sg_ctx* ctx, const uint64_t* d_latency_ns, size_t
     if (!out_min || (count && !d_latency_ns)) throw Error(SG_ERR_INVALID_ARG, "null argument");
     unsigned long long* m = ctx->r_err.get<unsigned long long>(4);
     SG_HIP(hipMemsetAsync(m, 0xff, 8, ctx->stream));
-    if (count)
-      hipLaunchKernelGGL(k_min_u64, dim3(grid_for(count, 256, 4096)), dim3(256), 0, ctx->stream,
-                         d_latency_ns, count, m);
+    if (count) {
+      const unsigned nb = grid_for(count, 256, 2048);
+      unsigned long long* part = ctx->r_misc.get<unsigned long long>(nb);
+      hipLaunchKernelGGL(k_min_u64, dim3(nb), dim3(256), 0, ctx->stream, d_latency_ns, count, part);
+      hipLaunchKernelGGL(k_min_final, dim3(1), dim3(256), 0, ctx->stream, part, nb, m);
+    }
     SG_CHECK_LAUNCH();
     unsigned long long h = 0;
     copy_to_host(ctx, &h, m, 8);
