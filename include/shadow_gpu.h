@@ -68,11 +68,16 @@ int32_t sg_ctx_synchronize(sg_ctx* ctx);
 /* Message and (row, col) of the last failing call on this context. */
 const char* sg_ctx_last_error(const sg_ctx* ctx);
 void sg_ctx_last_error_pair(const sg_ctx* ctx, uint32_t* row, uint32_t* col);
-/* Measurement hooks (bench.py): when enabled, every launch of an instrumented
- * kernel is bracketed by HIP events on the context stream.  read_timer returns
- * the summed device time, the launch count and the algorithmic work declared
- * by the launch sites ("relax": relaxations; "deliver_*": bytes).  Enabling or
- * disabling resets all timers. */
+/* Measurement hooks (bench.py): with bit 0 of `enable` set, every launch of an
+ * instrumented kernel is bracketed by HIP events on the context stream;
+ * bit 1 (SG_TIMERS_COUNT_WORK) additionally runs the counting variant of kernels
+ * whose work is data-dependent (the relaxation kernel counts the lane-
+ * relaxations it performs; slower, so time and count in separate runs).
+ * read_timer returns the summed device time, the launch count and the
+ * algorithmic work ("relax": lane-relaxations; delivery kernels: bytes).
+ * Enabling or disabling resets all timers. */
+#define SG_TIMERS_ON 1
+#define SG_TIMERS_COUNT_WORK 2
 int32_t sg_ctx_enable_timers(sg_ctx* ctx, int32_t enable);
 int32_t sg_ctx_read_timer(sg_ctx* ctx, const char* kernel, double* total_ms, uint64_t* launches,
                           double* work);

@@ -241,7 +241,8 @@ void sg_ctx_last_error_pair(const sg_ctx* ctx, uint32_t* row, uint32_t* col) {
 int32_t sg_ctx_enable_timers(sg_ctx* ctx, int32_t enable) {
   return sg::guarded(ctx, [&] {
     sg::settle_timers(ctx);
-    ctx->timing = enable != 0;
+    ctx->timing = (enable & SG_TIMERS_ON) != 0;
+    ctx->count_work = ctx->timing && (enable & SG_TIMERS_COUNT_WORK) != 0;
     for (auto& kv : ctx->timers) kv.second = sg::KernelTimer();
   });
 }

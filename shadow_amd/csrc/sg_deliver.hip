@@ -128,7 +128,6 @@ struct WalkArgs {
   uint64_t* deliver;
   uint64_t* eid;
   uint32_t* dst_host;
-  uint32_t* dst_cnt;
   unsigned long long* blk_stats;  // per block: [n_delivered, min_deliver, min_lat] (reduced by k_reduce_stats)
   uint32_t* err;
 };
@@ -236,9 +235,6 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
             nd++;
             mind = min(mind, (unsigned long long)arr);
             minl = min(minl, (unsigned long long)lat);
-#ifndef SG_EXPERIMENT_NOCNT
-            atomicAdd(&a.dst_cnt[d], 1u);
-#endif
           }
         } else {
           st = (f & W_NO_DST) ? SG_PKT_DROP_NO_DST : SG_PKT_SIM_END;
@@ -317,36 +313,9 @@ __global__ void __launch_bounds__(1024) k_reduce_stats(const unsigned long long*
   }
 }
 
-// Bucket entries carry a 128-bit sort key (kt = deliver time, kk = order key)
-// and a value ki (what dst_order reports).  The order key encodes
-// (src_host_id, src_host_event_id) order:
-//   single GPU: kk = packet index (input grouped by ascending source host, and
-//               event ids grow in send order);
-//   sharded:    kk = (src_host << 32) | k, k = the packet's rank among its
-//               host's delivered packets this round.
-__global__ void k_scatter(const uint32_t* __restrict__ dst_host, const uint64_t* __restrict__ deliver,
-                          uint32_t P, const uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
-                          uint64_t* __restrict__ kt, uint64_t* __restrict__ kk, uint32_t* __restrict__ ki) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < P; i += gridDim.x * blockDim.x) {
-    uint32_t d = dst_host[i];
-    if (d == NONE) continue;
-    uint32_t p = off[d] + atomicAdd(&cur[d], 1u);
-    kt[p] = deliver[i];
-    kk[p] = i;
-    ki[p] = i;
-  }
-}
-
 __device__ __forceinline__ bool key_less(uint64_t ta, uint64_t ka, uint64_t tb, uint64_t kb) {
   return ta < tb || (ta == tb && ka < kb);
 }
-
-// Block of 256 destinations: their buckets are contiguous, so the block loads
-// the whole range into LDS with coalesced reads, each thread insertion-sorts
-// its bucket in LDS, and the block writes dst_order back coalesced.  Buckets
-// above SMALL_BUCKET are queued for k_sort_big; a block whose range does not
-// fit in LDS sorts its small buckets in place in global memory instead.
-constexpr int SMALL_LDS = 3072;  // entries staged per block (60 KB of LDS)
 
 __device__ __forceinline__ void insertion_sort(uint64_t* t_, uint64_t* k_, uint32_t* i_, uint32_t b,
                                                uint32_t e) {
@@ -363,36 +332,6 @@ __device__ __forceinline__ void insertion_sort(uint64_t* t_, uint64_t* k_, uint3
     t_[j] = t;
     k_[j] = k;
     i_[j] = x;
-  }
-}
-
-__global__ void __launch_bounds__(256)
-    k_sort_small(const uint32_t* __restrict__ off, uint32_t H, uint64_t* __restrict__ kt,
-                 uint64_t* __restrict__ kk, uint32_t* __restrict__ ki, uint32_t* __restrict__ order,
-                 uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
-  __shared__ uint64_t st[SMALL_LDS];
-  __shared__ uint64_t sk[SMALL_LDS];
-  __shared__ uint32_t si[SMALL_LDS];
-  const uint32_t h0 = blockIdx.x * 256;
-  const uint32_t h = h0 + threadIdx.x;
-  const uint32_t r0 = off[h0], r1 = off[min(h0 + 256, H)];
-  const bool mine = h < H;
-  const uint32_t b = mine ? off[h] : r1, e = mine ? off[h + 1] : r1;
-  const bool big = e - b > SMALL_BUCKET;
-  if (mine && big) big_list[atomicAdd(big_count, 1u)] = h;
-  if (r1 - r0 <= SMALL_LDS) {
-    for (uint32_t i = r0 + threadIdx.x; i < r1; i += 256) {
-      st[i - r0] = kt[i];
-      sk[i - r0] = kk[i];
-      si[i - r0] = ki[i];
-    }
-    __syncthreads();
-    if (mine && !big) insertion_sort(st, sk, si, b - r0, e - r0);
-    __syncthreads();
-    for (uint32_t i = r0 + threadIdx.x; i < r1; i += 256) order[i] = si[i - r0];  // big ranges rewritten later
-  } else if (mine && !big) {
-    insertion_sort(kt, kk, ki, b, e);
-    for (uint32_t i = b; i < e; i++) order[i] = ki[i];
   }
 }
 
@@ -544,34 +483,6 @@ __global__ void __launch_bounds__(PACK_BLOCK)
   }
 }
 
-// ---- sharded delivery: destination side ----------------------------------
-__global__ void k_rec_count(const sg_record* __restrict__ rec, uint32_t n, const uint32_t* __restrict__ local,
-                            uint32_t H, uint32_t* __restrict__ cnt, uint32_t* __restrict__ err) {
-  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
-    uint32_t d = rec[r].dst_host;
-    uint32_t s = d < H ? local[d] : NONE;
-    if (s == NONE) {
-      atomicOr(err, ERR_NOT_LOCAL);
-      continue;
-    }
-    atomicAdd(&cnt[s], 1u);
-  }
-}
-
-__global__ void k_rec_scatter(const sg_record* __restrict__ rec, uint32_t n, const uint32_t* __restrict__ local,
-                              uint32_t H, const uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
-                              uint64_t* __restrict__ kt, uint64_t* __restrict__ kk, uint32_t* __restrict__ ki) {
-  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
-    uint32_t d = rec[r].dst_host;
-    uint32_t s = d < H ? local[d] : NONE;
-    if (s == NONE) continue;
-    uint32_t p = off[s] + atomicAdd(&cur[s], 1u);
-    kt[p] = rec[r].deliver_time_ns;
-    kk[p] = rec[r].order_key;
-    ki[p] = r;
-  }
-}
-
 static void fail_flags(uint32_t err) {
   if (err & ERR_SRC_RANGE) throw Error(SG_ERR_INVALID_ARG, "packet source host out of range");
   if (err & ERR_UNSORTED)
@@ -582,52 +493,270 @@ static void fail_flags(uint32_t err) {
     throw Error(SG_ERR_INVALID_ARG, "a received record's destination host is not local to this rank");
 }
 
-// Sort the buckets described by off[0..n_buckets] (entries in kt/kk/ki) into order.
-static void sort_buckets(sg_ctx* ctx, const uint32_t* off, uint32_t n_buckets, uint32_t n_entries,
-                         uint64_t* kt, uint64_t* kk, uint32_t* ki, uint32_t* order, uint32_t* big_count) {
-  hipStream_t st = ctx->stream;
-  uint32_t* big_list = ctx->d_lists.get<uint32_t>(n_buckets);
-  {
-    TimedLaunch tl(ctx, "sort_small", 24.0 * n_entries + 8.0 * n_buckets);
-    hipLaunchKernelGGL(k_sort_small, dim3((n_buckets + 255) / 256 ? (n_buckets + 255) / 256 : 1), dim3(256), 0, st, off, n_buckets, kt, kk,
-                       ki, order, big_list, big_count);
+// ---------------------------------------------------------------------------
+// Destination bucketing without global atomics.
+//
+// Entries (a delivered packet, or a received record) carry a destination slot
+// d, an arrival time t, an order key kk and a value ki.  Result: offsets[d] and
+// order[] = the ki of every entry sorted by (d, t, kk) -- EventQueue order per
+// destination (event.rs:84-155).
+//   1. k_sb_hist    tiles of SB_TILE entries: LDS histogram over super-buckets
+//                   (sb = d >> shift, a contiguous range of 2^shift slots);
+//   2. scan         of the (super-bucket, tile) counts;
+//   3. k_sb_scatter entries to their super-bucket (LDS cursors; order inside a
+//                   super-bucket is irrelevant, step 4 sorts it fully);
+//   4. k_sb_sort    block per super-bucket: per-slot counts and offsets in
+//                   LDS, placement by slot, insertion sort of each slot by
+//                   (t, kk); slots above SMALL_BUCKET entries go to k_sort_big.
+// ---------------------------------------------------------------------------
+constexpr int SB_THREADS = 256;
+constexpr int SB_TILE = 4096;        // entries per hist / scatter block
+constexpr int SB_MAX = 4096;         // super-buckets (LDS histogram bins)
+constexpr int SB_SLOTS_MAX = 1024;   // slots per super-bucket (2^shift)
+constexpr int SB_CAP = 1536;         // entries a super-bucket sorts in LDS
+constexpr int SB_TARGET = 640;       // mean entries per super-bucket
+
+struct PacketEntries {  // single GPU: entries are the round's packets, kk = ki = packet index
+  const uint32_t* dst;
+  const uint64_t* t;
+  __device__ __forceinline__ uint32_t slot(uint32_t e) const { return dst[e]; }
+  __device__ __forceinline__ void get(uint32_t e, uint64_t& tt, uint64_t& kk, uint32_t& ki) const {
+    tt = t[e];
+    kk = e;
+    ki = e;
   }
-  uint64_t* kt2 = ctx->d_keys2.get<uint64_t>(n_entries);
-  uint64_t* kk2 = ctx->d_keys3.get<uint64_t>(n_entries);
-  uint32_t* ki2 = ctx->d_vals2.get<uint32_t>(n_entries);
+};
+
+struct RecordEntries {  // sharded: entries are received records, slot = the destination's local index
+  const sg_record* rec;
+  const uint32_t* local;
+  uint32_t H;
+  uint32_t* err;
+  __device__ __forceinline__ uint32_t slot(uint32_t e) const {
+    const uint32_t d = rec[e].dst_host;
+    const uint32_t s = d < H ? local[d] : NONE;
+    if (s == NONE) atomicOr(err, ERR_NOT_LOCAL);
+    return s;
+  }
+  __device__ __forceinline__ void get(uint32_t e, uint64_t& tt, uint64_t& kk, uint32_t& ki) const {
+    tt = rec[e].deliver_time_ns;
+    kk = rec[e].order_key;
+    ki = e;
+  }
+};
+
+template <class E>
+__global__ void __launch_bounds__(SB_THREADS)
+    k_sb_hist(E src, uint32_t n, uint32_t shift, uint32_t n_sb, uint32_t* __restrict__ tile_hist) {
+  __shared__ uint32_t h[SB_MAX];
+  for (uint32_t i = threadIdx.x; i < n_sb; i += SB_THREADS) h[i] = 0;
+  __syncthreads();
+  const uint32_t e0 = blockIdx.x * SB_TILE, e1 = min(e0 + SB_TILE, n);
+  for (uint32_t e = e0 + threadIdx.x; e < e1; e += SB_THREADS) {
+    const uint32_t d = src.slot(e);
+    if (d != NONE) atomicAdd(&h[d >> shift], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n_sb; i += SB_THREADS) tile_hist[(size_t)i * gridDim.x + blockIdx.x] = h[i];
+}
+
+template <class E>
+__global__ void __launch_bounds__(SB_THREADS)
+    k_sb_scatter(E src, uint32_t n, uint32_t shift, uint32_t n_sb, const uint32_t* __restrict__ tile_off,
+                 uint32_t* __restrict__ rd, uint64_t* __restrict__ rt, uint64_t* __restrict__ rk,
+                 uint32_t* __restrict__ ri) {
+  __shared__ uint32_t cur[SB_MAX];
+  for (uint32_t i = threadIdx.x; i < n_sb; i += SB_THREADS) cur[i] = tile_off[(size_t)i * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const uint32_t e0 = blockIdx.x * SB_TILE, e1 = min(e0 + SB_TILE, n);
+  for (uint32_t e = e0 + threadIdx.x; e < e1; e += SB_THREADS) {
+    const uint32_t d = src.slot(e);
+    if (d == NONE) continue;
+    const uint32_t p = atomicAdd(&cur[d >> shift], 1u);
+    uint64_t tt, kk;
+    uint32_t ki;
+    src.get(e, tt, kk, ki);
+    rd[p] = d;
+    rt[p] = tt;
+    rk[p] = kk;
+    ri[p] = ki;
+  }
+}
+
+// Placement of a super-bucket's entries by slot, then per-slot order by (t, kk).
+template <bool LDS>
+__device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32_t* Ti, uint32_t s0, uint32_t s1,
+                                              uint32_t d0, uint32_t nd, const uint32_t* cnt, uint32_t* cur,
+                                              const uint32_t* __restrict__ rd, const uint64_t* __restrict__ rt,
+                                              const uint64_t* __restrict__ rk, const uint32_t* __restrict__ ri,
+                                              uint64_t* __restrict__ kt, uint64_t* __restrict__ kk,
+                                              uint32_t* __restrict__ ki, uint32_t* __restrict__ order,
+                                              uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
+  for (uint32_t e = s0 + threadIdx.x; e < s1; e += SB_THREADS) {
+    const uint32_t p = atomicAdd(&cur[rd[e] - d0], 1u);
+    Tt[p] = rt[e];
+    Tk[p] = rk[e];
+    Ti[p] = ri[e];
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < nd; j += SB_THREADS) {
+    const uint32_t b = cnt[j], e = cnt[j + 1];
+    if (e - b > (uint32_t)SMALL_BUCKET) {
+      big_list[atomicAdd(big_count, 1u)] = d0 + j;
+      if (LDS)
+        for (uint32_t p = b; p < e; p++) {  // k_sort_big works on the global copy
+          kt[s0 + p] = Tt[p];
+          kk[s0 + p] = Tk[p];
+          ki[s0 + p] = Ti[p];
+        }
+    } else {
+      insertion_sort(Tt, Tk, Ti, b, e);
+    }
+  }
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < s1 - s0; p += SB_THREADS) order[s0 + p] = Ti[p];  // big slots rewritten later
+}
+
+// Block per super-bucket.  Entries of the super-bucket: [s0, s1) of rd/rt/rk/ri.
+// In LDS when they fit (SB_CAP), else sorted in place in the global kt/kk/ki.
+__global__ void __launch_bounds__(SB_THREADS)
+    k_sb_sort(uint32_t shift, uint32_t n_slots, const uint32_t* __restrict__ tile_off, uint32_t n_tiles,
+              const uint32_t* __restrict__ rd, const uint64_t* __restrict__ rt, const uint64_t* __restrict__ rk,
+              const uint32_t* __restrict__ ri, uint64_t* __restrict__ kt, uint64_t* __restrict__ kk,
+              uint32_t* __restrict__ ki, uint32_t* __restrict__ offsets, uint32_t* __restrict__ order,
+              uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
+  __shared__ uint32_t cnt[SB_SLOTS_MAX + 1];
+  __shared__ uint32_t cur[SB_SLOTS_MAX];
+  __shared__ uint32_t wsum[SB_THREADS / 64];
+  __shared__ uint64_t st[SB_CAP];
+  __shared__ uint64_t sk[SB_CAP];
+  __shared__ uint32_t si[SB_CAP];
+  const uint32_t sb = blockIdx.x;
+  const uint32_t s0 = tile_off[(size_t)sb * n_tiles], s1 = tile_off[(size_t)(sb + 1) * n_tiles];
+  const uint32_t d0 = sb << shift, nd = min(1u << shift, n_slots - d0);
+  const uint32_t ns = s1 - s0;
+  const bool lds = ns <= (uint32_t)SB_CAP;
+  for (uint32_t j = threadIdx.x; j <= nd; j += SB_THREADS) cnt[j] = 0;
+  __syncthreads();
+  for (uint32_t e = s0 + threadIdx.x; e < s1; e += SB_THREADS) atomicAdd(&cnt[rd[e] - d0], 1u);
+  __syncthreads();
+  // exclusive scan of cnt[0..nd) (4 slots per thread, nd <= 1024)
+  {
+    const uint32_t j0 = threadIdx.x * 4;
+    uint32_t v[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      v[q] = j0 + q < nd ? cnt[j0 + q] : 0;
+      sum += v[q];
+    }
+    uint32_t incl = sum;
+    const int lane = threadIdx.x & 63;
+    for (int dd = 1; dd < 64; dd <<= 1) {
+      const uint32_t y = __shfl_up(incl, dd, 64);
+      if (lane >= dd) incl += y;
+    }
+    if (lane == 63) wsum[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) base += wsum[w];
+    uint32_t run = base + incl - sum;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (j0 + q < nd) {
+        cnt[j0 + q] = run;
+        cur[j0 + q] = run;
+        run += v[q];
+      }
+    if (j0 < nd && j0 + 4 >= nd) cnt[nd] = run;  // the thread holding the last slot
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < nd; j += SB_THREADS) offsets[d0 + j] = s0 + cnt[j];
+  if (d0 + nd == n_slots && threadIdx.x == 0) offsets[n_slots] = s1;
+  // LDS and global variants as separate inlined bodies: one generic pointer
+  // would turn every access into a flat instruction waiting on both counters
+  if (lds)
+    sb_place_sort<true>(st, sk, si, s0, s1, d0, nd, cnt, cur, rd, rt, rk, ri, kt, kk, ki, order, big_list, big_count);
+  else
+    sb_place_sort<false>(kt + s0, kk + s0, ki + s0, s0, s1, d0, nd, cnt, cur, rd, rt, rk, ri, kt, kk, ki, order,
+                         big_list, big_count);
+}
+
+// Bucket sort of n entries into n_slots destination slots (see above).
+template <class E>
+static void bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32_t* offsets, uint32_t* order,
+                        uint32_t* big_count) {
+  hipStream_t st = ctx->stream;
+  if (n_slots == 0) {
+    SG_HIP(hipMemsetAsync(offsets, 0, 4, st));
+    return;
+  }
+  // 2^shift slots per super-bucket: about SB_TARGET entries each, <= SB_MAX super-buckets
+  uint32_t shift = 0;
+  while (shift < 10 && ((uint64_t)n << (shift + 1)) <= (uint64_t)SB_TARGET * n_slots) shift++;
+  while (((n_slots - 1) >> shift) + 1 > (uint32_t)SB_MAX) shift++;
+  if (shift > 10) throw Error(SG_ERR_INVALID_ARG, "too many destination hosts for one rank");
+  const uint32_t n_sb = ((n_slots - 1) >> shift) + 1;
+  const uint32_t n_tiles = std::max<uint32_t>(1, (n + SB_TILE - 1) / SB_TILE);
+  const size_t nh = (size_t)n_sb * n_tiles;
+  uint32_t* hist = ctx->d_cnt.get<uint32_t>(nh + 1);
+  uint32_t* toff = ctx->d_scan.get<uint32_t>(nh + 1);
+  uint32_t* rd = ctx->d_lists2.get<uint32_t>(n);
+  uint64_t* rt = ctx->d_keys2.get<uint64_t>(n);
+  uint64_t* rk = ctx->d_keys3.get<uint64_t>(n);
+  uint32_t* ri = ctx->d_vals2.get<uint32_t>(n);
+  uint64_t* kt = ctx->d_keys.get<uint64_t>(n);
+  uint64_t* kk = ctx->d_keys4.get<uint64_t>(n);
+  uint32_t* ki = ctx->d_vals.get<uint32_t>(n);
+  uint32_t* big_list = ctx->d_lists.get<uint32_t>(n_slots);
+  {
+    TimedLaunch tl(ctx, "scatter", 56.0 * n);
+    if (n) hipLaunchKernelGGL(k_sb_hist<E>, dim3(n_tiles), dim3(SB_THREADS), 0, st, src, n, shift, n_sb, hist);
+    else SG_HIP(hipMemsetAsync(hist, 0, nh * 4, st));
+    exclusive_scan_u32(ctx, hist, toff, (uint32_t)nh);
+    if (n)
+      hipLaunchKernelGGL(k_sb_scatter<E>, dim3(n_tiles), dim3(SB_THREADS), 0, st, src, n, shift, n_sb, toff, rd, rt,
+                         rk, ri);
+  }
+  {
+    TimedLaunch tl(ctx, "sort_small", 48.0 * n + 4.0 * n_slots);
+    hipLaunchKernelGGL(k_sb_sort, dim3(n_sb), dim3(SB_THREADS), 0, st, shift, n_slots, toff, n_tiles, rd, rt, rk, ri,
+                       kt, kk, ki, offsets, order, big_list, big_count);
+  }
+  uint64_t* kt2 = ctx->d_keys2.get<uint64_t>(n);  // rd/rt are free again
+  uint64_t* kk2 = ctx->d_keys3.get<uint64_t>(n);
+  uint32_t* ki2 = ctx->d_vals2.get<uint32_t>(n);
   {
     TimedLaunch tl(ctx, "sort_big", 0.0);
-    hipLaunchKernelGGL(k_sort_big, dim3(std::min<uint32_t>(std::max(n_buckets, 1u), 2048)), dim3(SORT_BLOCK), 0, st,
-                       off, big_list, big_count, kt, kk, ki, kt2, kk2, ki2, order);
+    hipLaunchKernelGGL(k_sort_big, dim3(std::min<uint32_t>(std::max(n_slots, 1u), 2048)), dim3(SORT_BLOCK), 0, st,
+                       offsets, big_list, big_count, kt, kk, ki, kt2, kk2, ki2, order);
   }
   SG_CHECK_LAUNCH();
 }
 
 struct RoundWork {
-  uint32_t *host_off, *dst_cnt, *cur, *big_count, *err, *dst_host;
+  uint32_t *host_off, *big_count, *err, *dst_host;
   uint64_t* ctr_start;
   unsigned long long* stats;
 };
 
-// Shared source half of a round: segments + walk.  Leaves per-packet
-// dst_host (NONE unless delivered), per-destination counts, stats.
+// Shared source half of a round: host offsets + walk.  Leaves per-packet
+// dst_host (NONE unless delivered) and the round stats.
 static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const sg_round* rd,
                               const sg_packets* pk, uint8_t* status, uint64_t* deliver, uint64_t* eid,
                               bool want_ctr_start) {
   hipStream_t st = ctx->stream;
   const uint32_t P = pk->n_packets, H = hs->n;
   RoundWork w;
-  // workspace: [host_off H+1][dst_cnt H][cur H][big_count 1][err 1]
-  uint32_t* ws = ctx->d_seg.get<uint32_t>(4 * (size_t)H + 8);
+  // workspace: [host_off H+1][big_count 1][err 1]
+  uint32_t* ws = ctx->d_seg.get<uint32_t>((size_t)H + 8);
   w.host_off = ws;
-  w.dst_cnt = ws + (size_t)H + 1;
-  w.cur = w.dst_cnt + H;
-  w.big_count = w.cur + H;
+  w.big_count = ws + (size_t)H + 1;
   w.err = w.big_count + 1;
   w.stats = ctx->d_misc.get<unsigned long long>(4);
   w.dst_host = ctx->d_dst.get<uint32_t>(P);
   w.ctr_start = want_ctr_start ? ctx->d_ctr0.get<uint64_t>(H) : nullptr;
-  SG_HIP(hipMemsetAsync(ws, 0, (4 * (size_t)H + 8) * 4, st));
+  SG_HIP(hipMemsetAsync(ws, 0, ((size_t)H + 8) * 4, st));
   SG_HIP(hipMemsetAsync(w.stats, 0, 8, st));  // P = 0: no walk, no reduction
   SG_HIP(hipMemsetAsync(w.stats + 1, 0xff, 16, st));
   if (w.ctr_start) SG_HIP(hipMemcpyAsync(w.ctr_start, hs->ctr, (size_t)H * 8, hipMemcpyDeviceToDevice, st));
@@ -661,7 +790,6 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   a.deliver = deliver;
   a.eid = eid;
   a.dst_host = w.dst_host;
-  a.dst_cnt = w.dst_cnt;
   const uint32_t walk_blocks = (H + WALK_HOSTS - 1) / WALK_HOSTS;
   a.blk_stats = ctx->d_blk.get<unsigned long long>(3 * (size_t)walk_blocks);
   a.err = w.err;
@@ -695,24 +823,10 @@ static void finish(sg_ctx* ctx, const RoundWork& w, sg_round_stats* stats) {
 
 static void deliver_round(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const sg_round* rd,
                           const sg_packets* pk, sg_deliveries* out, sg_round_stats* stats) {
-  hipStream_t st = ctx->stream;
   const uint32_t P = pk->n_packets, H = hs->n;
   RoundWork w = source_phase(ctx, hs, tab, rd, pk, out->status, out->deliver_time_ns, out->event_id, false);
-  {
-    TimedLaunch tl(ctx, "scan", 8.0 * H);
-    exclusive_scan_u32(ctx, w.dst_cnt, out->dst_offsets, H);
-  }
-  if (P) {
-    uint64_t* kt = ctx->d_keys.get<uint64_t>(P);
-    uint64_t* kk = ctx->d_keys4.get<uint64_t>(P);
-    uint32_t* ki = ctx->d_vals.get<uint32_t>(P);
-    {
-      TimedLaunch tl(ctx, "scatter", 32.0 * P);
-      hipLaunchKernelGGL(k_scatter, dim3(grid_for(P, 256, 16384)), dim3(256), 0, st, w.dst_host,
-                         out->deliver_time_ns, P, out->dst_offsets, w.cur, kt, kk, ki);
-    }
-    sort_buckets(ctx, out->dst_offsets, H, P, kt, kk, ki, out->dst_order, w.big_count);
-  }
+  bucket_sort(ctx, PacketEntries{w.dst_host, out->deliver_time_ns}, P, H, out->dst_offsets, out->dst_order,
+              w.big_count);
   finish(ctx, w, stats);
 }
 
@@ -746,28 +860,11 @@ static void deliver_source(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const
 static void deliver_bucket(sg_ctx* ctx, const sg_record* recv, uint32_t n, const uint32_t* local, uint32_t H,
                            uint32_t n_local, uint32_t* order, uint32_t* offsets) {
   hipStream_t st = ctx->stream;
-  uint32_t* ws = ctx->d_seg.get<uint32_t>(2 * (size_t)n_local + 8);
-  uint32_t* cnt = ws;
-  uint32_t* cur = ws + n_local;
-  uint32_t* big_count = ws + 2 * (size_t)n_local;
-  uint32_t* err = big_count + 1;
-  SG_HIP(hipMemsetAsync(ws, 0, (2 * (size_t)n_local + 8) * 4, st));
-  if (n) {
-    TimedLaunch tl(ctx, "rec_count", 36.0 * n);
-    hipLaunchKernelGGL(k_rec_count, dim3(grid_for(n, 256, 16384)), dim3(256), 0, st, recv, n, local, H, cnt, err);
-  }
-  exclusive_scan_u32(ctx, cnt, offsets, n_local);
-  if (n) {
-    uint64_t* kt = ctx->d_keys.get<uint64_t>(n);
-    uint64_t* kk = ctx->d_keys4.get<uint64_t>(n);
-    uint32_t* ki = ctx->d_vals.get<uint32_t>(n);
-    {
-      TimedLaunch tl(ctx, "rec_scatter", 56.0 * n);
-      hipLaunchKernelGGL(k_rec_scatter, dim3(grid_for(n, 256, 16384)), dim3(256), 0, st, recv, n, local, H, offsets,
-                         cur, kt, kk, ki);
-    }
-    sort_buckets(ctx, offsets, n_local, n, kt, kk, ki, order, big_count);
-  }
+  uint32_t* ws = ctx->d_seg.get<uint32_t>(8);
+  uint32_t* big_count = ws;
+  uint32_t* err = ws + 1;
+  SG_HIP(hipMemsetAsync(ws, 0, 8 * 4, st));
+  bucket_sort(ctx, RecordEntries{recv, local, H, err}, n, n_local, offsets, order, big_count);
   uint32_t h_err = 0;
   copy_to_host(ctx, &h_err, err, 4);
   fail_flags(h_err);

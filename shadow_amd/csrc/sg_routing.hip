@@ -716,7 +716,7 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
   uint32_t* ring[3] = {flags, flags + fs, flags + 2 * fs};
   uint32_t* sat = flags + 3 * fs;
   uint32_t* alist = sat + group;
-  unsigned long long* work = ctx->timing ? ctx->r_work.get<unsigned long long>(WORK_SHARDS) : nullptr;
+  unsigned long long* work = ctx->count_work ? ctx->r_work.get<unsigned long long>(WORK_SHARDS) : nullptr;
   if (work) SG_HIP(hipMemsetAsync(work, 0, WORK_SHARDS * 8, st));
   // Passes are issued in chunks; the host reads the convergence flags once per
   // chunk.  A pass issued after its batch converged finds it off the active list.

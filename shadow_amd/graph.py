@@ -54,9 +54,14 @@ class Context:
     def synchronize(self) -> None:
         check(self.handle, load().sg_ctx_synchronize(self.handle))
 
-    def enable_timers(self, enable: bool = True) -> None:
-        """Per-kernel HIP-event timers on this context's stream (resets them)."""
-        check(self.handle, load().sg_ctx_enable_timers(self.handle, 1 if enable else 0))
+    def enable_timers(self, enable: bool = True, count_work: bool = False) -> None:
+        """Per-kernel HIP-event timers on this context's stream (resets them).
+
+        count_work: run the counting variants of data-dependent kernels (the
+        relaxation kernel's lane-relaxation count); time them in a separate run.
+        """
+        mode = (1 | (2 if count_work else 0)) if enable else 0
+        check(self.handle, load().sg_ctx_enable_timers(self.handle, mode))
 
     def read_timer(self, kernel: str):
         """(total device ms, launches, declared algorithmic work) for one kernel."""

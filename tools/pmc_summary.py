@@ -21,9 +21,10 @@ import os
 from collections import defaultdict
 
 # first match wins: k_relax_wide before the k_relax<...> template instances
-KERNELS = {"relax_wide": "k_relax_wide", "relax": "k_relax<", "out": "k_out_batch", "walk": "k_walk",
-           "scatter": "k_scatter", "sort_small": "k_sort_small", "sort_big": "k_sort_big",
-           "seg_bounds": "k_seg_bounds"}
+KERNELS = {"relax_wide": "k_relax_wide", "relax": "k_relax_w<", "out": "k_out_batch", "walk": "k_walk",
+           "sb_hist": "k_sb_hist", "sb_scatter": "k_sb_scatter", "sb_sort": "k_sb_sort", "sort_big": "k_sort_big",
+           "host_off": "k_host_off", "init": "k_init_batch"}
+VALU_PEAK_OPS_PER_NS = 256 * 4 * 32 * 2.4  # 78.6e3 lane-ops per ns (MI355X_MICROARCH.md chip table)
 
 
 def _rows(d, pattern):
@@ -42,21 +43,28 @@ def short(name):
 
 
 def counter_avgs(d, counter):
-    acc = defaultdict(list)
+    """Average per dispatch of the most-dispatched instantiation of each kernel
+    (bench's one work-counting run uses another template instance)."""
+    acc = defaultdict(lambda: defaultdict(list))
     for r in _rows(d, "*counter_collection.csv"):
         if r.get("Counter_Name") != counter:
             continue
-        k = short(r.get("Kernel_Name", ""))
+        name = r.get("Kernel_Name", "")
+        k = short(name)
         if k:
-            acc[k].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+            acc[k][name].append(float(r["Counter_Value"]))
+    out = {}
+    for k, by_name in acc.items():
+        vals = max(by_name.values(), key=len)
+        out[k] = sum(vals) / len(vals)
+    return out
 
 
 def stats(d):
     res = {}
     for r in _rows(d, "*kernel_stats.csv"):
         k = short(r.get("Name", ""))
-        if k:
+        if k and (k not in res or int(r["Calls"]) > res[k]["calls"]):
             res[k] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "total_ns": float(r["TotalDurationNs"]),
                       "pct": float(r.get("Percentage", 0) or 0)}
     return res
@@ -67,13 +75,15 @@ def main():
     ap.add_argument("--stats")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
+    ap.add_argument("--sq", help="pass with SQ_INSTS_VALU (VALU utilisation)")
     ap.add_argument("-o", "--out", required=True)
     a = ap.parse_args()
     out = {}
     st = stats(a.stats) if a.stats else {}
     fe = counter_avgs(a.fetch, "FETCH_SIZE") if a.fetch else {}
     wr = counter_avgs(a.write, "WRITE_SIZE") if a.write else {}
-    for k in sorted(set(st) | set(fe) | set(wr)):
+    va = counter_avgs(a.sq, "SQ_INSTS_VALU") if a.sq else {}
+    for k in sorted(set(st) | set(fe) | set(wr) | set(va)):
         e = {}
         if k in st:
             e.update(st[k])
@@ -84,6 +94,10 @@ def main():
         if k in fe and k in wr:
             e["hbm_bytes_per_launch"] = (2 * fe[k] + wr[k]) * 1024
             e["hbm_bytes_per_launch_raw"] = (fe[k] + wr[k]) * 1024
+        if k in va:
+            e["valu_insts_per_launch"] = va[k]
+            if k in st and st[k]["avg_ns"] > 0:  # wave instructions x 64 lanes / time / peak
+                e["valu_frac"] = va[k] * 64 / st[k]["avg_ns"] / VALU_PEAK_OPS_PER_NS
         out[k] = e
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
