@@ -114,7 +114,7 @@ def test_heavy_loss_ties(oracle, ctx):
 
 
 def test_wide_fallback_big_latencies(oracle, ctx):
-    """Path latencies beyond 2^34 ns take the u64 kernel; must still be exact."""
+    """Path latencies beyond 2^32 ns take the u64 kernel; must still be exact."""
     g = synth.ring_chords_graph(150, 4.0, seed=8, lat_lo_us=2_000_000, lat_hi_us=9_000_000)
     lat, _ = _check(oracle, g, np.arange(150, dtype=np.uint32), ctx)
     assert lat.max() >= (1 << 34)
