@@ -120,25 +120,16 @@ __global__ void k_scatter_arcs(const uint32_t* __restrict__ src, const uint32_t*
 // ---------------------------------------------------------------------------
 // Batched-source relaxation (the hot kernel).
 //
-// 64 sources per batch (lane = source).  A batch's distance slab is laid out
-// D[node][64] (u64 keys, 512 B per node), so one in-arc u -> v costs one
-// coalesced 512-B read of D[u][0..63] and 64 independent relaxations.
+// B sources per batch (lane = source).  A batch's distance slab is laid out
+// D[node][B] (u64 keys, 8 B x B per node), so one in-arc u -> v costs one
+// coalesced row read of D[u][0..B-1] and B independent relaxations.
 //
-// A block owns a chunk of consecutive destination nodes (<= CHUNK_NODES, about
-// CHUNK_ARCS in-arcs; chunk table built per graph).  Its in-arcs are
-// contiguous in the CSC, so the four waves split them into groups of GROUP
-// arcs: per group the arc fields are wave-uniform scalar loads, the GROUP row
-// reads are issued back to back, and each candidate is folded into the
-// destination's LDS row with ds_min_u64 -- no per-node serialisation, hub nodes
-// spread over all waves.  At the end the block compares each LDS row with the
-// node's key at block start and writes improved keys in place (Gauss-Seidel:
-// later blocks of the same pass may already read them).
-//
-// XCD-aware 1-D grid: dispatch deals blocks round-robin over the 8 XCDs
-// (MI355X_MICROARCH.md, "Workgroup dispatch"), so block L runs on XCD L % 8.
-// Block L serves batch (L % 8) + 8 * ((L / 8) / n_chunks), chunk (L / 8) %
-// n_chunks: the blocks of one batch share an XCD, whose L2 holds most of the
-// batch's slab.  Placement changes speed only, never results.
+// k_relax_w: one wave per work item (active batch, NPW consecutive destination
+// nodes); see the kernel's comment.  XCD-aware 1-D grid: dispatch deals blocks
+// round-robin over the 8 XCDs (MI355X_MICROARCH.md, "Workgroup dispatch"), so
+// block L runs on XCD L % 8, and the items of one batch all go to blocks of one
+// residue: the waves of an XCD share a slab in its L2.  Placement changes speed
+// only, never results.
 //
 // Frontier (FRONT): stamp[batch][node] = p + 2 when the node's key changed in
 // pass p (sources start at 1).  In pass p an arc is relaxed only when its
@@ -148,11 +139,13 @@ __global__ void k_scatter_arcs(const uint32_t* __restrict__ src, const uint32_t*
 // pass with no change anywhere -- then every arc satisfies D[v] <= D[u] (+) w,
 // the fixed point, which is petgraph's Dijkstra result (see header).
 // ---------------------------------------------------------------------------
-constexpr int GROUP = 8;           // row reads in flight per wave step
 constexpr int RELAX_THREADS = 256;
 constexpr uint32_t FLAG_STRIDE = 32;  // per-batch pass flags 128 B apart: no two batches share a cache line
 
-// One 8-B key through a buffer descriptor (32-bit per-lane byte offset).
+// One 8-B key through a buffer descriptor (32-bit per-lane byte offset).  An
+// offset of OOB lies outside every slab: the load returns 0 and moves no data.
+constexpr uint32_t OOB = 0x80000000u;
+constexpr uint32_t PREFETCH_MIN = 16;  // dirty arcs from which an item prefetches all its rows
 __device__ __forceinline__ uint64_t load_key(__amdgpu_buffer_rsrc_t rsrc, uint32_t off) {
   const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0);
   return ((uint64_t)v[1] << 32) | v[0];
@@ -213,7 +206,7 @@ __global__ void __launch_bounds__(1024) k_active_list(const uint32_t* __restrict
 
 // B = sources per batch (64: one row per wave instruction; 32: two rows, one
 // per half-wave, and a 2.5 MB slab at 10k nodes that stays in one XCD's L2).
-template <int B, int NPW, int K, bool FRONT, bool COUNT>
+template <int B, int NPW, int K, int GROUP, bool FRONT, bool COUNT>
 __global__ void __launch_bounds__(RELAX_THREADS)
     k_relax_w(const uint32_t* __restrict__ in_off, const uint4* __restrict__ in_rec, uint64_t* __restrict__ D,
               uint32_t n, const uint32_t* __restrict__ alist, uint32_t* __restrict__ changed,
@@ -249,8 +242,6 @@ __global__ void __launch_bounds__(RELAX_THREADS)
     uint64_t* Db = D + (size_t)b * n * B;
     const uint32_t* St = stamp + (size_t)b * n;
     const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(Db, 0, (int)(n * B * 8u), 0x00020000);
-#pragma unroll
-    for (int i = 0; i < NPW * B / 64; i++) best[i * 64 + lane] = KEY_INF;
     const uint32_t a0 = in_off[vw], a1 = in_off[vw1];
     uint32_t n_cand = 0;
     uint32_t run_slot = 0;  // per row group: records of one destination form a run
@@ -274,8 +265,12 @@ __global__ void __launch_bounds__(RELAX_THREADS)
               make_uint4(ra[i].x * (B * 8), ra[i].y - vw, ra[i].z, ra[i].w);
         cnt += (uint32_t)__popcll(m);
       }
+      if (cnt && !n_cand) {  // first candidates of this item: reset its LDS rows
+#pragma unroll
+        for (int i = 0; i < NPW * B / 64; i++) best[i * 64 + lane] = KEY_INF;
+      }
       n_cand += cnt;
-      if (cnt && !prefetched) {  // this item will flush: fetch its rows now, under the relax loop
+      if (cnt >= PREFETCH_MIN && !prefetched) {  // dense item: fetch its rows now, under the relax loop
         prefetched = true;
 #pragma unroll
         for (int i = 0; i < NPW / G; i++)
@@ -320,12 +315,22 @@ __global__ void __launch_bounds__(RELAX_THREADS)
     if (COUNT) n_rel += n_cand;
     if (!n_cand) continue;
     atomicMin(&best[run_slot * B + sl], (unsigned long long)run);
-    // flush: improved keys are written in place (one untorn 64-bit update each)
+    // flush: improved keys are written in place (one untorn 64-bit update each).
+    // A sparse item reads only the lanes that received a candidate (the others
+    // take an out-of-range offset: no memory traffic, value 0, no change).
+    uint64_t nbv[NPW / G];
+#pragma unroll
+    for (int i = 0; i < NPW / G; i++) nbv[i] = best[(i * G + gh) * B + sl];
+    if (!prefetched) {
+#pragma unroll
+      for (int i = 0; i < NPW / G; i++)
+        cur[i] = load_key(slab, nbv[i] != KEY_INF ? min(vw + i * G + gh, vw1 - 1) * (B * 8) + lane8 : OOB);
+    }
     bool any = false;
 #pragma unroll
     for (int i = 0; i < NPW / G; i++) {
       const uint32_t v = vw + i * G + gh;
-      const uint64_t nb = best[(i * G + gh) * B + sl];
+      const uint64_t nb = nbv[i];
       const bool ch = v < vw1 && nb < cur[i];
       if (ch) Db[(size_t)v * B + sl] = nb;
       const uint64_t m = __ballot(ch);
@@ -346,7 +351,24 @@ __global__ void __launch_bounds__(RELAX_THREADS)
 
 // Transposed write-out of [B rows x 64 cols] tiles.  Diagonal = the raw
 // self-loop (graph/mod.rs:210-217).  Saturated keys flag their batch.
-template <int B>
+// VEC: 16-B stores (two latencies / four losses per lane); needs n_used % 4 == 0
+// so every row starts 16-B aligned.
+__device__ __forceinline__ void out_entry(uint64_t kk, uint32_t row, uint32_t j, const uint32_t* __restrict__ used,
+                                          const uint32_t* __restrict__ self_edge, const uint64_t* __restrict__ e_lat,
+                                          const float* __restrict__ e_loss, uint64_t& lat, float& loss, bool& sflag) {
+  if (row == j) {
+    const uint32_t e = self_edge[used[j]];
+    lat = e_lat[e];
+    loss = e_loss[e];
+  } else {
+    const uint32_t l = key_lat(kk);
+    sflag |= l == LAT32_SAT;
+    lat = l;
+    loss = __uint_as_float(key_loss_bits(kk));
+  }
+}
+
+template <int B, bool VEC>
 __global__ void __launch_bounds__(256)
     k_out_batch(const uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ used, uint32_t n_used,
                 uint32_t first_row, uint32_t row_end, uint32_t out_row0, const uint32_t* __restrict__ self_edge,
@@ -365,21 +387,36 @@ __global__ void __launch_bounds__(256)
   }
   __syncthreads();
   bool sflag = false;
-  const uint32_t j = j0 + lane;
-  for (int r = wave; r < B; r += 4) {
-    const uint32_t row = first_row + b * B + r;
-    if (row >= row_end || j >= n_used) continue;
-    const size_t o = (size_t)(row - out_row0) * n_used + j;
-    if (row == j) {
-      const uint32_t e = self_edge[used[j]];
-      out_lat[o] = e_lat[e];
-      out_loss[o] = e_loss[e];
-    } else {
-      const uint64_t kk = tile[lane][r];
-      const uint32_t lat = key_lat(kk);
-      sflag |= lat == LAT32_SAT;
-      out_lat[o] = lat;
-      out_loss[o] = __uint_as_float(key_loss_bits(kk));
+  const uint32_t rbase = first_row + b * B;
+  if (VEC && j0 + 64 <= n_used) {
+    // lane = (row quarter, 4 columns): each key is read from LDS once, and the
+    // lane stores 32 B of latencies and 16 B of losses
+    for (int r = wave * 4 + (lane >> 4); r < B; r += 16) {
+      const uint32_t row = rbase + r;
+      if (row >= row_end) continue;
+      const uint32_t c = (lane & 15) * 4;
+      uint64_t l0, l1, l2, l3;
+      float4 f;
+      out_entry(tile[c][r], row, j0 + c, used, self_edge, e_lat, e_loss, l0, f.x, sflag);
+      out_entry(tile[c + 1][r], row, j0 + c + 1, used, self_edge, e_lat, e_loss, l1, f.y, sflag);
+      out_entry(tile[c + 2][r], row, j0 + c + 2, used, self_edge, e_lat, e_loss, l2, f.z, sflag);
+      out_entry(tile[c + 3][r], row, j0 + c + 3, used, self_edge, e_lat, e_loss, l3, f.w, sflag);
+      const size_t o = (size_t)(row - out_row0) * n_used + j0 + c;
+      *(ulonglong2*)&out_lat[o] = make_ulonglong2(l0, l1);
+      *(ulonglong2*)&out_lat[o + 2] = make_ulonglong2(l2, l3);
+      *(float4*)&out_loss[o] = f;
+    }
+  } else {
+    const uint32_t j = j0 + lane;
+    for (int r = wave; r < B; r += 4) {
+      const uint32_t row = rbase + r;
+      if (row >= row_end || j >= n_used) continue;
+      const size_t o = (size_t)(row - out_row0) * n_used + j;
+      uint64_t l;
+      float f;
+      out_entry(tile[lane][r], row, j, used, self_edge, e_lat, e_loss, l, f, sflag);
+      out_lat[o] = l;
+      out_loss[o] = f;
     }
   }
   if (__any(sflag) && lane == 0) atomicOr(&sat[b], 1u);
@@ -696,7 +733,7 @@ static void run_wide(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t 
 
 // B sources per batch, NPW destination nodes per wave item, STG arcs staged per
 // wave step, FRONT = stamp frontier.
-template <int B, int NPW, int STG, bool FRONT>
+template <int B, int NPW, int STG, int GR, bool FRONT>
 static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                              uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
   hipStream_t st = ctx->stream;
@@ -755,10 +792,10 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
         {
           TimedLaunch tl(ctx, "relax", 0.0);
           if (work)
-            hipLaunchKernelGGL((k_relax_w<B, NPW, STG / 64, FRONT, true>), dim3(grid), dim3(RELAX_THREADS), 0, st,
+            hipLaunchKernelGGL((k_relax_w<B, NPW, STG / 64, GR, FRONT, true>), dim3(grid), dim3(RELAX_THREADS), 0, st,
                                net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
           else
-            hipLaunchKernelGGL((k_relax_w<B, NPW, STG / 64, FRONT, false>), dim3(grid), dim3(RELAX_THREADS), 0, st,
+            hipLaunchKernelGGL((k_relax_w<B, NPW, STG / 64, GR, FRONT, false>), dim3(grid), dim3(RELAX_THREADS), 0, st,
                                net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
         }
         SG_CHECK_LAUNCH();
@@ -791,9 +828,15 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
     SG_HIP(hipMemsetAsync(sat, 0, gb * 4ull, st));
     {
       TimedLaunch tl(ctx, "out", 12.0 * std::min<uint32_t>(gb * B, row_end - first_row) * n_used);
-      hipLaunchKernelGGL(k_out_batch<B>, dim3((n_used + 63) / 64, gb), dim3(256), 0, st, D, n, d_used, n_used,
-                         first_row, row_end, row_begin, net->self_edge, net->e_lat, net->e_loss, out_lat,
-                         out_loss, sat);
+      const bool vec = n_used % 4 == 0 && ((uintptr_t)out_lat & 15) == 0 && ((uintptr_t)out_loss & 15) == 0;
+      if (vec)
+        hipLaunchKernelGGL((k_out_batch<B, true>), dim3((n_used + 63) / 64, gb), dim3(256), 0, st, D, n, d_used,
+                           n_used, first_row, row_end, row_begin, net->self_edge, net->e_lat, net->e_loss, out_lat,
+                           out_loss, sat);
+      else
+        hipLaunchKernelGGL((k_out_batch<B, false>), dim3((n_used + 63) / 64, gb), dim3(256), 0, st, D, n, d_used,
+                           n_used, first_row, row_end, row_begin, net->self_edge, net->e_lat, net->e_loss, out_lat,
+                           out_loss, sat);
     }
     SG_CHECK_LAUNCH();
     copy_to_host(ctx, h_sat.data(), sat, gb * 4ull);
@@ -816,26 +859,30 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 
 // A/B measurement knobs: SG_APSP_FRONTIER=0 relaxes every arc every pass;
 // SG_APSP_B sources per batch (32 | 64); SG_APSP_NPW nodes per wave item;
-// SG_APSP_STAGE arcs staged per wave step.
+// SG_APSP_STAGE arcs staged per wave step; SG_APSP_GROUP row reads in flight.
 static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                            uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
   const bool front = env_int("SG_APSP_FRONTIER", 1) != 0;
   const int bsz = env_int("SG_APSP_B", 64), npw = env_int("SG_APSP_NPW", 8), stg = env_int("SG_APSP_STAGE", 128);
-#define SG_SP(B_, NPW_, STG_)                                                                            \
-  if (bsz == B_ && npw == NPW_ && stg == STG_) {                                                        \
+  const int gr = env_int("SG_APSP_GROUP", 8);
+#define SG_SP(B_, NPW_, STG_, GR_)                                                                       \
+  if (bsz == B_ && npw == NPW_ && stg == STG_ && gr == GR_) {                                           \
     if (front)                                                                                          \
-      shortest_paths_t<B_, NPW_, STG_, true>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss);  \
+      shortest_paths_t<B_, NPW_, STG_, GR_, true>(ctx, net, d_used, n_used, row_begin, row_end, out_lat,  \
+                                                  out_loss);                                            \
     else                                                                                                \
-      shortest_paths_t<B_, NPW_, STG_, false>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss); \
+      shortest_paths_t<B_, NPW_, STG_, GR_, false>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, \
+                                                   out_loss);                                           \
     return;                                                                                             \
   }
-  SG_SP(64, 8, 128)
-  SG_SP(64, 16, 128)
-  SG_SP(32, 8, 128)
-  SG_SP(32, 16, 128)
-  SG_SP(32, 4, 64)
+  SG_SP(64, 8, 128, 8)
+  SG_SP(64, 8, 128, 16)
+  SG_SP(64, 16, 128, 8)
+  SG_SP(64, 4, 64, 8)
+  SG_SP(32, 8, 128, 8)
+  SG_SP(32, 16, 128, 8)
 #undef SG_SP
-  throw Error(SG_ERR_INVALID_ARG, "unsupported SG_APSP_B / SG_APSP_NPW / SG_APSP_STAGE");
+  throw Error(SG_ERR_INVALID_ARG, "unsupported SG_APSP_B / SG_APSP_NPW / SG_APSP_STAGE / SG_APSP_GROUP");
 }
 
 static void direct_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, const uint32_t* h_used,

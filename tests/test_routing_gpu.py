@@ -181,3 +181,14 @@ def test_min_latency_device(ctx):
 def test_empty_used(ctx):
     g = NetworkGraph(2, [0, 1], [0, 1], [1, 1], [0.0, 0.0], False, ctx=ctx)
     assert len(g.compute_shortest_paths([])) == 0
+
+
+@pytest.mark.parametrize("env", [{"SG_APSP_B": "32"}, {"SG_APSP_FRONTIER": "0"}, {"SG_APSP_NPW": "16"},
+                                 {"SG_APSP_B": "32", "SG_APSP_NPW": "16"}, {"SG_APSP_PASS_CHUNK": "1"}])
+def test_kernel_variants_bit_exact(oracle, ctx, monkeypatch, env):
+    """Every A/B variant of the relaxation kernel (slab width, frontier, item size) is exact."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = synth.ring_chords_graph(900, 7.0, seed=21, parallel=0.03)
+    used = np.random.default_rng(21).permutation(900)[:612].astype(np.uint32)
+    _check(oracle, g, used, ctx)

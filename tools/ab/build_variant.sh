@@ -4,12 +4,15 @@
 set -e
 NAME=$1; DEFS=$2
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
-OBJ=/tmp/sg_ab_$NAME; mkdir -p $OBJ
+OBJ=/tmp/sg_ab_$NAME; rm -rf $OBJ; mkdir -p $OBJ
 cd $ROOT/shadow_amd/csrc
+pids=()
 for f in sg_context sg_routing sg_deliver; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -munsafe-fp-atomics $DEFS -c $f.hip -o $OBJ/$f.o &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=gfx950 -ffp-contract=off \
+    -fno-fast-math -munsafe-fp-atomics $DEFS -c $f.hip -o $OBJ/$f.o &
+  pids+=($!)
 done
 g++ -O3 -std=c++17 -fPIC -Wall -c sg_gml.cpp -o $OBJ/sg_gml.o
-wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/tools/ab/libshadow_gpu_$NAME.so $OBJ/*.o
+for p in "${pids[@]}"; do wait $p; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined -o $ROOT/tools/ab/libshadow_gpu_$NAME.so $OBJ/*.o
 echo built tools/ab/libshadow_gpu_$NAME.so
