@@ -317,24 +317,6 @@ __device__ __forceinline__ bool key_less(uint64_t ta, uint64_t ka, uint64_t tb, 
   return ta < tb || (ta == tb && ka < kb);
 }
 
-__device__ __forceinline__ void insertion_sort(uint64_t* t_, uint64_t* k_, uint32_t* i_, uint32_t b,
-                                               uint32_t e) {
-  for (uint32_t i = b + 1; i < e; i++) {
-    const uint64_t t = t_[i], k = k_[i];
-    const uint32_t x = i_[i];
-    uint32_t j = i;
-    while (j > b && key_less(t, k, t_[j - 1], k_[j - 1])) {
-      t_[j] = t_[j - 1];
-      k_[j] = k_[j - 1];
-      i_[j] = i_[j - 1];
-      j--;
-    }
-    t_[j] = t;
-    k_[j] = k;
-    i_[j] = x;
-  }
-}
-
 // Block per large bucket.  Chunks of SORT_CHUNK are bitonic-sorted in LDS,
 // then merged pairwise (merge path) between two global buffers.
 __global__ void __launch_bounds__(SORT_BLOCK)
@@ -513,10 +495,12 @@ constexpr int SB_THREADS = 256;
 constexpr int SB_TILE = 4096;        // entries per hist / scatter block
 constexpr int SB_MAX = 4096;         // super-buckets (LDS histogram bins)
 constexpr int SB_SLOTS_MAX = 1024;   // slots per super-bucket (2^shift)
-constexpr int SB_CAP = 1536;         // entries a super-bucket sorts in LDS
-constexpr int SB_TARGET = 640;       // mean entries per super-bucket
+constexpr int SB_CAP = 3072;         // entries a super-bucket sorts in LDS
+constexpr int SB_TARGET = 1280;      // mean entries per super-bucket
+constexpr int SBT_THREADS = 512;     // k_sb_sort block
 
 struct PacketEntries {  // single GPU: entries are the round's packets, kk = ki = packet index
+  static constexpr bool KK = false;  // the order key is the value itself
   const uint32_t* dst;
   const uint64_t* t;
   __device__ __forceinline__ uint32_t slot(uint32_t e) const { return dst[e]; }
@@ -528,6 +512,7 @@ struct PacketEntries {  // single GPU: entries are the round's packets, kk = ki 
 };
 
 struct RecordEntries {  // sharded: entries are received records, slot = the destination's local index
+  static constexpr bool KK = true;
   const sg_record* rec;
   const uint32_t* local;
   uint32_t H;
@@ -560,46 +545,119 @@ __global__ void __launch_bounds__(SB_THREADS)
   for (uint32_t i = threadIdx.x; i < n_sb; i += SB_THREADS) tile_hist[(size_t)i * gridDim.x + blockIdx.x] = h[i];
 }
 
+// Exclusive scan of a[0..n) in LDS by the whole block (NT threads, n <= NT * PER);
+// returns the total.  Ends with a barrier.
+template <int NT, int PER>
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* a, uint32_t n, uint32_t* wsum) {
+  const uint32_t j0 = threadIdx.x * PER;
+  uint32_t v[PER], sum = 0;
+#pragma unroll
+  for (int q = 0; q < PER; q++) {
+    v[q] = j0 + q < n ? a[j0 + q] : 0;
+    sum += v[q];
+  }
+  uint32_t incl = sum;
+  const int lane = threadIdx.x & 63;
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const uint32_t y = __shfl_up(incl, dd, 64);
+    if (lane >= dd) incl += y;
+  }
+  if (lane == 63) wsum[threadIdx.x >> 6] = incl;
+  __syncthreads();
+  uint32_t base = 0, total = 0;
+  for (int w = 0; w < NT / 64; w++) {
+    if (w < (int)(threadIdx.x >> 6)) base += wsum[w];
+    total += wsum[w];
+  }
+  uint32_t run = base + incl - sum;
+#pragma unroll
+  for (int q = 0; q < PER; q++)
+    if (j0 + q < n) {
+      a[j0 + q] = run;
+      run += v[q];
+    }
+  __syncthreads();
+  return total;
+}
+
+// Tile -> super-buckets.  The tile is first counting-sorted by super-bucket in
+// LDS, so each super-bucket's entries of the tile leave as one contiguous run
+// (coalesced stores instead of one scattered store per entry and array).
+constexpr int SBS_THREADS = 512;
 template <class E>
-__global__ void __launch_bounds__(SB_THREADS)
+__global__ void __launch_bounds__(SBS_THREADS)
     k_sb_scatter(E src, uint32_t n, uint32_t shift, uint32_t n_sb, const uint32_t* __restrict__ tile_off,
                  uint32_t* __restrict__ rd, uint64_t* __restrict__ rt, uint64_t* __restrict__ rk,
                  uint32_t* __restrict__ ri) {
-  __shared__ uint32_t cur[SB_MAX];
-  for (uint32_t i = threadIdx.x; i < n_sb; i += SB_THREADS) cur[i] = tile_off[(size_t)i * gridDim.x + blockIdx.x];
+  constexpr int PER = SB_TILE / SBS_THREADS;
+  __shared__ uint32_t lcur[SB_MAX];   // local start, then cursor
+  __shared__ uint32_t lbase[SB_MAX];  // global position of the run - local start
+  __shared__ uint32_t sd[SB_TILE];
+  __shared__ uint64_t st_[SB_TILE];
+  __shared__ uint32_t si[SB_TILE];
+  __shared__ uint64_t sk[E::KK ? SB_TILE : 1];
+  __shared__ uint32_t wsum[SBS_THREADS / 64];
+  for (uint32_t i = threadIdx.x; i < n_sb; i += SBS_THREADS) lcur[i] = 0;
   __syncthreads();
   const uint32_t e0 = blockIdx.x * SB_TILE, e1 = min(e0 + SB_TILE, n);
-  for (uint32_t e = e0 + threadIdx.x; e < e1; e += SB_THREADS) {
-    const uint32_t d = src.slot(e);
-    if (d == NONE) continue;
-    const uint32_t p = atomicAdd(&cur[d >> shift], 1u);
+  uint32_t d[PER];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t e = e0 + threadIdx.x + k * SBS_THREADS;
+    d[k] = e < e1 ? src.slot(e) : NONE;
+    if (d[k] != NONE) atomicAdd(&lcur[d[k] >> shift], 1u);
+  }
+  __syncthreads();
+  const uint32_t total = block_exclusive_scan<SBS_THREADS, SB_MAX / SBS_THREADS>(lcur, n_sb, wsum);
+  for (uint32_t i = threadIdx.x; i < n_sb; i += SBS_THREADS)
+    lbase[i] = tile_off[(size_t)i * gridDim.x + blockIdx.x] - lcur[i];
+  __syncthreads();  // lcur is the cursor from here on
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    if (d[k] == NONE) continue;
+    const uint32_t e = e0 + threadIdx.x + k * SBS_THREADS;
+    const uint32_t p = atomicAdd(&lcur[d[k] >> shift], 1u);
     uint64_t tt, kk;
     uint32_t ki;
     src.get(e, tt, kk, ki);
-    rd[p] = d;
-    rt[p] = tt;
-    rk[p] = kk;
-    ri[p] = ki;
+    sd[p] = d[k];
+    st_[p] = tt;
+    si[p] = ki;
+    if (E::KK) sk[p] = kk;
+  }
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < total; p += SBS_THREADS) {
+    const uint32_t dd = sd[p];
+    const uint32_t g = lbase[dd >> shift] + p;
+    rd[g] = dd;
+    rt[g] = st_[p];
+    ri[g] = si[p];
+    if (E::KK) rk[g] = sk[p];
   }
 }
 
 // Placement of a super-bucket's entries by slot, then per-slot order by (t, kk).
-template <bool LDS>
-__device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32_t* Ti, uint32_t s0, uint32_t s1,
-                                              uint32_t d0, uint32_t nd, const uint32_t* cnt, uint32_t* cur,
-                                              const uint32_t* __restrict__ rd, const uint64_t* __restrict__ rt,
-                                              const uint64_t* __restrict__ rk, const uint32_t* __restrict__ ri,
-                                              uint64_t* __restrict__ kt, uint64_t* __restrict__ kk,
-                                              uint32_t* __restrict__ ki, uint32_t* __restrict__ order,
-                                              uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
-  for (uint32_t e = s0 + threadIdx.x; e < s1; e += SB_THREADS) {
-    const uint32_t p = atomicAdd(&cur[rd[e] - d0], 1u);
+// Without KK the order key is the value (ri) itself.
+template <bool LDS, bool KK>
+__device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32_t* Ti, uint16_t* Ts, uint32_t s0,
+                                              uint32_t s1, uint32_t d0, uint32_t nd, const uint32_t* cnt,
+                                              uint32_t* cur, const uint32_t* __restrict__ rd,
+                                              const uint64_t* __restrict__ rt, const uint64_t* __restrict__ rk,
+                                              const uint32_t* __restrict__ ri, uint64_t* __restrict__ kt,
+                                              uint64_t* __restrict__ kk, uint32_t* __restrict__ ki,
+                                              uint32_t* __restrict__ order, uint32_t* __restrict__ big_list,
+                                              uint32_t* __restrict__ big_count) {
+  for (uint32_t e = s0 + threadIdx.x; e < s1; e += SBT_THREADS) {
+    const uint32_t j = rd[e] - d0;
+    const uint32_t p = atomicAdd(&cur[j], 1u);
     Tt[p] = rt[e];
-    Tk[p] = rk[e];
-    Ti[p] = ri[e];
+    const uint32_t v = ri[e];
+    Tk[p] = KK ? rk[e] : (uint64_t)v;
+    Ti[p] = v;
+    Ts[p] = (uint16_t)j;
   }
   __syncthreads();
-  for (uint32_t j = threadIdx.x; j < nd; j += SB_THREADS) {
+  for (uint32_t j = threadIdx.x; j < nd; j += SBT_THREADS) {
     const uint32_t b = cnt[j], e = cnt[j + 1];
     if (e - b > (uint32_t)SMALL_BUCKET) {
       big_list[atomicAdd(big_count, 1u)] = d0 + j;
@@ -609,77 +667,62 @@ __device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32
           kk[s0 + p] = Tk[p];
           ki[s0 + p] = Ti[p];
         }
-    } else {
-      insertion_sort(Tt, Tk, Ti, b, e);
     }
   }
-  __syncthreads();
-  for (uint32_t p = threadIdx.x; p < s1 - s0; p += SB_THREADS) order[s0 + p] = Ti[p];  // big slots rewritten later
+  // Rank sort inside each small slot: entry p goes to slot start + #(entries of
+  // its slot with a smaller (t, kk)); (t, kk) is unique per entry.  One thread
+  // per entry, independent LDS reads -- no serial insertion chain.
+  for (uint32_t p = threadIdx.x; p < s1 - s0; p += SBT_THREADS) {
+    const uint32_t j = Ts[p];
+    const uint32_t b = cnt[j], e = cnt[j + 1];
+    if (e - b > (uint32_t)SMALL_BUCKET) continue;  // k_sort_big writes this slot
+    const uint64_t t = Tt[p], k = Tk[p];
+    uint32_t rank = 0;
+    for (uint32_t q = b; q < e; q++) rank += key_less(Tt[q], Tk[q], t, k);
+    order[s0 + b + rank] = Ti[p];
+  }
 }
 
 // Block per super-bucket.  Entries of the super-bucket: [s0, s1) of rd/rt/rk/ri.
 // In LDS when they fit (SB_CAP), else sorted in place in the global kt/kk/ki.
-__global__ void __launch_bounds__(SB_THREADS)
+template <bool KK>
+__global__ void __launch_bounds__(SBT_THREADS)
     k_sb_sort(uint32_t shift, uint32_t n_slots, const uint32_t* __restrict__ tile_off, uint32_t n_tiles,
               const uint32_t* __restrict__ rd, const uint64_t* __restrict__ rt, const uint64_t* __restrict__ rk,
               const uint32_t* __restrict__ ri, uint64_t* __restrict__ kt, uint64_t* __restrict__ kk,
               uint32_t* __restrict__ ki, uint32_t* __restrict__ offsets, uint32_t* __restrict__ order,
-              uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
+              uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count, uint16_t* __restrict__ slot_spill) {
   __shared__ uint32_t cnt[SB_SLOTS_MAX + 1];
   __shared__ uint32_t cur[SB_SLOTS_MAX];
-  __shared__ uint32_t wsum[SB_THREADS / 64];
+  __shared__ uint32_t wsum[SBT_THREADS / 64];
   __shared__ uint64_t st[SB_CAP];
   __shared__ uint64_t sk[SB_CAP];
   __shared__ uint32_t si[SB_CAP];
+  __shared__ uint16_t ss[SB_CAP];
   const uint32_t sb = blockIdx.x;
   const uint32_t s0 = tile_off[(size_t)sb * n_tiles], s1 = tile_off[(size_t)(sb + 1) * n_tiles];
   const uint32_t d0 = sb << shift, nd = min(1u << shift, n_slots - d0);
   const uint32_t ns = s1 - s0;
   const bool lds = ns <= (uint32_t)SB_CAP;
-  for (uint32_t j = threadIdx.x; j <= nd; j += SB_THREADS) cnt[j] = 0;
+  for (uint32_t j = threadIdx.x; j <= nd; j += SBT_THREADS) cnt[j] = 0;
   __syncthreads();
-  for (uint32_t e = s0 + threadIdx.x; e < s1; e += SB_THREADS) atomicAdd(&cnt[rd[e] - d0], 1u);
+  for (uint32_t e = s0 + threadIdx.x; e < s1; e += SBT_THREADS) atomicAdd(&cnt[rd[e] - d0], 1u);
   __syncthreads();
-  // exclusive scan of cnt[0..nd) (4 slots per thread, nd <= 1024)
-  {
-    const uint32_t j0 = threadIdx.x * 4;
-    uint32_t v[4], sum = 0;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      v[q] = j0 + q < nd ? cnt[j0 + q] : 0;
-      sum += v[q];
-    }
-    uint32_t incl = sum;
-    const int lane = threadIdx.x & 63;
-    for (int dd = 1; dd < 64; dd <<= 1) {
-      const uint32_t y = __shfl_up(incl, dd, 64);
-      if (lane >= dd) incl += y;
-    }
-    if (lane == 63) wsum[threadIdx.x >> 6] = incl;
-    __syncthreads();
-    uint32_t base = 0;
-    for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) base += wsum[w];
-    uint32_t run = base + incl - sum;
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-      if (j0 + q < nd) {
-        cnt[j0 + q] = run;
-        cur[j0 + q] = run;
-        run += v[q];
-      }
-    if (j0 < nd && j0 + 4 >= nd) cnt[nd] = run;  // the thread holding the last slot
-  }
+  // exclusive scan of cnt[0..nd), nd <= SB_SLOTS_MAX
+  const uint32_t tot = block_exclusive_scan<SBT_THREADS, SB_SLOTS_MAX / SBT_THREADS>(cnt, nd, wsum);
+  for (uint32_t j = threadIdx.x; j < nd; j += SBT_THREADS) cur[j] = cnt[j];
+  if (threadIdx.x == 0) cnt[nd] = tot;
   __syncthreads();
-  for (uint32_t j = threadIdx.x; j < nd; j += SB_THREADS) offsets[d0 + j] = s0 + cnt[j];
+  for (uint32_t j = threadIdx.x; j < nd; j += SBT_THREADS) offsets[d0 + j] = s0 + cnt[j];
   if (d0 + nd == n_slots && threadIdx.x == 0) offsets[n_slots] = s1;
   // LDS and global variants as separate inlined bodies: one generic pointer
   // would turn every access into a flat instruction waiting on both counters
   if (lds)
-    sb_place_sort<true>(st, sk, si, s0, s1, d0, nd, cnt, cur, rd, rt, rk, ri, kt, kk, ki, order, big_list, big_count);
+    sb_place_sort<true, KK>(st, sk, si, ss, s0, s1, d0, nd, cnt, cur, rd, rt, rk, ri, kt, kk, ki, order, big_list,
+                            big_count);
   else
-    sb_place_sort<false>(kt + s0, kk + s0, ki + s0, s0, s1, d0, nd, cnt, cur, rd, rt, rk, ri, kt, kk, ki, order,
-                         big_list, big_count);
+    sb_place_sort<false, KK>(kt + s0, kk + s0, ki + s0, slot_spill + s0, s0, s1, d0, nd, cnt, cur, rd, rt, rk, ri,
+                             kt, kk, ki, order, big_list, big_count);
 }
 
 // Bucket sort of n entries into n_slots destination slots (see above).
@@ -709,19 +752,20 @@ static void bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
   uint64_t* kk = ctx->d_keys4.get<uint64_t>(n);
   uint32_t* ki = ctx->d_vals.get<uint32_t>(n);
   uint32_t* big_list = ctx->d_lists.get<uint32_t>(n_slots);
+  uint16_t* spill = ctx->d_spill.get<uint16_t>(n);  // slot index per entry of super-buckets beyond SB_CAP
   {
     TimedLaunch tl(ctx, "scatter", 56.0 * n);
     if (n) hipLaunchKernelGGL(k_sb_hist<E>, dim3(n_tiles), dim3(SB_THREADS), 0, st, src, n, shift, n_sb, hist);
     else SG_HIP(hipMemsetAsync(hist, 0, nh * 4, st));
     exclusive_scan_u32(ctx, hist, toff, (uint32_t)nh);
     if (n)
-      hipLaunchKernelGGL(k_sb_scatter<E>, dim3(n_tiles), dim3(SB_THREADS), 0, st, src, n, shift, n_sb, toff, rd, rt,
+      hipLaunchKernelGGL(k_sb_scatter<E>, dim3(n_tiles), dim3(SBS_THREADS), 0, st, src, n, shift, n_sb, toff, rd, rt,
                          rk, ri);
   }
   {
     TimedLaunch tl(ctx, "sort_small", 48.0 * n + 4.0 * n_slots);
-    hipLaunchKernelGGL(k_sb_sort, dim3(n_sb), dim3(SB_THREADS), 0, st, shift, n_slots, toff, n_tiles, rd, rt, rk, ri,
-                       kt, kk, ki, offsets, order, big_list, big_count);
+    hipLaunchKernelGGL(k_sb_sort<E::KK>, dim3(n_sb), dim3(SBT_THREADS), 0, st, shift, n_slots, toff, n_tiles, rd, rt,
+                       rk, ri, kt, kk, ki, offsets, order, big_list, big_count, spill);
   }
   uint64_t* kt2 = ctx->d_keys2.get<uint64_t>(n);  // rd/rt are free again
   uint64_t* kk2 = ctx->d_keys3.get<uint64_t>(n);

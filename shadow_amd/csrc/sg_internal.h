@@ -86,7 +86,7 @@ struct sg_ctx {
       r_out_loss, r_misc, r_dirty, r_work;
   // delivery workspace
   sg::DevBuf d_seg, d_dst, d_cnt, d_cur, d_keys, d_vals, d_keys2, d_vals2, d_keys3, d_keys4, d_misc,
-      d_scan, d_lists, d_lists2, d_ctr0, d_blk;
+      d_scan, d_lists, d_lists2, d_ctr0, d_blk, d_spill;
   sg::DevBuf m_scratch;
   // kernel timers (off unless sg_ctx_enable_timers)
   bool timing = false;
