@@ -172,42 +172,57 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
   unsigned long long nd = 0, mind = ~0ull, minl = ~0ull;
   for (uint32_t c0 = p0; c0 < p1; c0 += WALK_CHUNK) {
     const uint32_t c1 = min(c0 + WALK_CHUNK, p1);
-    // 1. packet-parallel gather
-    for (uint32_t i = c0 + t; i < c1; i += WALK_THREADS) {
-      const uint32_t k = i - c0;
-      const uint64_t now = a.send[i];
-      uint8_t f = a.payload[i] > 0 ? W_PAYLOAD : 0;
-      if (now < a.bootstrap_end) f |= W_BOOT;
-      uint32_t d = NONE;
+    // 1. packet-parallel gather, PPT packets per thread batched level by level
+    //    (inputs; address map and route rows; destination route; path cell),
+    //    so a thread has at most four dependent round trips per chunk
+    constexpr int PPT = WALK_CHUNK / WALK_THREADS;
+    uint64_t now[PPT];
+    uint32_t ip[PPT], sh[PPT], d[PPT], r[PPT];
+    uint8_t f[PPT];
+#pragma unroll
+    for (int q = 0; q < PPT; q++) {
+      const uint32_t i = min(c0 + t + q * WALK_THREADS, c1 - 1);
+      now[q] = a.send[i];
+      ip[q] = a.dst_ip[i];
+      sh[q] = a.src[i];
+      f[q] = a.payload[i] > 0 ? W_PAYLOAD : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < PPT; q++) {
+      if (now[q] < a.bootstrap_end) f[q] |= W_BOOT;
+      d[q] = now[q] < a.sim_end ? a.map.resolve(ip[q]) : NONE;  // worker.rs:332-335, 341
+      r[q] = a.route[sh[q]];
+    }
+#pragma unroll
+    for (int q = 0; q < PPT; q++) {
+      const bool past_end = !(now[q] < a.sim_end);
+      if (!past_end && d[q] == NONE) f[q] |= W_NO_DST;
+      if (d[q] != NONE && (r[q] < a.row_begin || r[q] - a.row_begin >= a.n_rows)) {
+        atomicOr(a.err, ERR_ROUTE_RANGE);
+        f[q] |= W_NO_DST;
+        d[q] = NONE;
+      }
+      ip[q] = d[q] != NONE ? a.route[d[q]] : 0;  // reuse: the destination's route column
+    }
+#pragma unroll
+    for (int q = 0; q < PPT; q++) {
+      const uint32_t i = c0 + t + q * WALK_THREADS;
       uint64_t lat = 0;
       float loss = 0.0f;
-      if (now < a.sim_end) {  // worker.rs:332-335
-        d = a.map.resolve(a.dst_ip[i]);
-        if (d == NONE) {
-          f |= W_NO_DST;
-        } else {
-          const uint32_t r = a.route[a.src[i]];
-          if (r < a.row_begin || r - a.row_begin >= a.n_rows) {
-            atomicOr(a.err, ERR_ROUTE_RANGE);
-            f |= W_NO_DST;
-            d = NONE;
-          } else {
-            const size_t cell = (size_t)(r - a.row_begin) * a.n_cols + a.route[d];
-#ifndef SG_EXPERIMENT_NOGATHER
-            lat = a.tab_lat[cell];
-            loss = a.tab_loss[cell];
-#else
-            lat = 1000 + (cell & 1);
-#endif
-            f |= W_DRAW;
-          }
-        }
+      if (d[q] != NONE) {
+        const size_t cell = (size_t)(r[q] - a.row_begin) * a.n_cols + ip[q];
+        lat = a.tab_lat[cell];
+        loss = a.tab_loss[cell];
+        f[q] |= W_DRAW;
       }
-      s_t[k] = now;
-      s_l[k] = lat;
-      s_loss[k] = loss;
-      s_d[k] = d;
-      s_f[k] = f;
+      if (i < c1) {
+        const uint32_t k = i - c0;
+        s_t[k] = now[q];
+        s_l[k] = lat;
+        s_loss[k] = loss;
+        s_d[k] = d[q];
+        s_f[k] = f[q];
+      }
     }
     __syncthreads();
     // 2. host-sequential walk (worker.rs:326-397)
