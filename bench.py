@@ -48,6 +48,8 @@ def parse_args():
     p.add_argument("--packets", type=int, default=1000000)
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-delivery", action="store_true")
+    p.add_argument("--no-pack", action="store_true",
+                   help="deliver from the two-array table (no packed path-key copy)")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                    help="PMC summary (HBM bytes per launch) written by tools/pmc_summary.py")
     return p.parse_args()
@@ -217,6 +219,13 @@ def main():
                                 src_hosts=mine)
         ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
         table = DeviceTable(my_lat, my_loss, nu, r0)
+        t_pack = None
+        if not a.no_pack:  # once per routing table, outside the per-round timing (sg_table_pack)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            packed = table.pack(ctx)
+            torch.cuda.synchronize()
+            t_pack = time.perf_counter() - t0 if packed else None
         batch = PacketBatch.from_numpy(pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"])
         src_global = pk["src"]
         out = Deliveries.allocate(a.packets, a.hosts)
@@ -239,7 +248,8 @@ def main():
         walk_s = walk_ms / 1e3 / max(walk_n, 1)
         ach = walk_bytes / max(walk_n, 1) / walk_s / 1e9 if walk_n else 0.0
         total_pkts = D.sum(float(a.packets))
-        round_bytes = 45.0 * a.packets + 84.0 * a.hosts  # SURVEY §8d algorithmic bytes per round
+        # SURVEY §8d algorithmic bytes per round (the packed path key gathers 8 B instead of 12 B)
+        round_bytes = (41.0 if table.path_key is not None else 45.0) * a.packets + 84.0 * a.hosts
         pmw = pmc.get("walk", {})
         delivery = {
             "metric": "packets routed/sec per sim round", "value": round(total_pkts / t_round, 1),
@@ -255,6 +265,8 @@ def main():
                          "avg_launch_ms": round(walk_s * 1e3, 4)},
             "round_hbm_GBs": round(round_bytes / t_round / 1e9, 1),
             "parallelism": f"hosts{D.world}",
+            "path_key_table": table.path_key is not None,
+            "table_pack_ms": round(t_pack * 1e3, 4) if t_pack is not None else None,
             "kernel_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in kt.items()},
         }
         if D.rank == 0 and D.world == 1 and not a.no_cpu:

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 1
+#define SG_ABI_VERSION 2
 
 typedef enum sg_status {
   SG_OK = 0,
@@ -154,14 +154,28 @@ int32_t sg_hosts_get_state(sg_hosts* hosts, uint64_t* rng_state, uint64_t* event
 int32_t sg_hosts_set_state(sg_hosts* hosts, const uint64_t* rng_state, const uint64_t* event_ctr);
 void sg_hosts_destroy(sg_hosts* hosts);
 
-/* Routing-table shard resident on the device (rows [row_begin, row_begin+n_rows)). */
+/* Routing-table shard resident on the device (rows [row_begin, row_begin+n_rows)).
+ * path_key (optional, from sg_table_pack) holds each cell as one u64,
+ * (latency_ns << 32) | bits(packet_loss): the delivery walk then gathers one
+ * 8-byte word per packet instead of two scattered words.  When path_key is
+ * set, latency_ns / packet_loss are not read by the delivery calls and may be
+ * NULL.  NULL = use the two arrays. */
 typedef struct sg_table {
   const uint64_t* latency_ns; /* device, n_rows x n_cols */
   const float* packet_loss;   /* device, n_rows x n_cols */
   uint32_t n_cols;
   uint32_t row_begin;
   uint32_t n_rows;
+  const uint64_t* path_key;   /* device, n_rows x n_cols, or NULL */
 } sg_table;
+
+/* Pack a table's (latency_ns, packet_loss) cells into path_key form
+ * (out_key: device, n_rows x n_cols u64).  *out_packable (host) = 1 if every
+ * latency is below 2^32 ns, else 0 and out_key must not be used (latencies of
+ * 4.29 s and more keep the two-array form).  Synchronises.  Done once per
+ * routing table (the table is immutable for the simulation, network_graph.rs
+ * IpPreviewTable / RoutingInfo are built once in Manager::run). */
+int32_t sg_table_pack(sg_ctx* ctx, const sg_table* table, uint64_t* out_key, uint32_t* out_packable);
 
 /* Round clock (EmulatedTime ns).  round_end = the worker's barrier
  * (worker.rs:262-268); sim_end / bootstrap_end from WorkerShared. */

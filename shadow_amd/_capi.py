@@ -14,6 +14,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "shadow_gpu.h")
 
 # sg_status (include/shadow_gpu.h)
 SG_OK = 0
+SG_ABI_VERSION = 2  # include/shadow_gpu.h
 SG_ERR_NO_EDGE = 1
 SG_ERR_MULTI_EDGE = 2
 SG_ERR_UNREACHABLE = 3
@@ -36,6 +37,7 @@ EXPORTED = [
     "sg_gml_node_index", "sg_gml_destroy", "sg_net_create", "sg_net_destroy", "sg_routing_build",
     "sg_routing_min_latency", "sg_hosts_create", "sg_hosts_get_state", "sg_hosts_set_state",
     "sg_hosts_destroy", "sg_deliver_round", "sg_deliver_source", "sg_deliver_bucket",
+    "sg_table_pack",
 ]
 
 
@@ -61,7 +63,7 @@ class sg_graph(C.Structure):
 
 class sg_table(C.Structure):
     _fields_ = [("latency_ns", C.c_void_p), ("packet_loss", C.c_void_p), ("n_cols", C.c_uint32),
-                ("row_begin", C.c_uint32), ("n_rows", C.c_uint32)]
+                ("row_begin", C.c_uint32), ("n_rows", C.c_uint32), ("path_key", C.c_void_p)]
 
 
 class sg_round(C.Structure):
@@ -138,6 +140,7 @@ def load(path: str | None = None):
         "sg_deliver_source": (i32, [vp, vp, C.POINTER(sg_table), C.POINTER(sg_round), C.POINTER(sg_packets),
                                     vp, vp, vp, vp, u32, vp, u32p, C.POINTER(sg_round_stats)]),
         "sg_deliver_bucket": (i32, [vp, vp, u32, vp, u32, u32, vp, vp]),
+        "sg_table_pack": (i32, [vp, C.POINTER(sg_table), vp, u32p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)
@@ -145,8 +148,11 @@ def load(path: str | None = None):
             continue
         f.restype = res
         f.argtypes = args
-    if L.sg_abi_version() != 1:
-        raise ShadowGpuUnavailable("ABI version mismatch")
+    v = L.sg_abi_version()
+    # an older library given via SHADOW_GPU_LIB (A/B tools) is accepted: v1's
+    # sg_table lacks path_key, which such callers leave NULL
+    if v != SG_ABI_VERSION and not (path != LIB_PATH and v == 1):
+        raise ShadowGpuUnavailable(f"ABI version mismatch: library {v}, bindings {SG_ABI_VERSION}")
     _lib = L
     return L
 

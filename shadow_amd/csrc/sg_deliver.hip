@@ -122,6 +122,7 @@ struct WalkArgs {
   HostMap map;
   const uint64_t* tab_lat;
   const float* tab_loss;
+  const uint64_t* tab_key;  // packed (lat << 32 | bits(loss)) cells, or null
   uint32_t n_cols, row_begin, n_rows;
   uint64_t round_end, sim_end, bootstrap_end;
   uint8_t* status;
@@ -211,8 +212,14 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
       float loss = 0.0f;
       if (d[q] != NONE) {
         const size_t cell = (size_t)(r[q] - a.row_begin) * a.n_cols + ip[q];
-        lat = a.tab_lat[cell];
-        loss = a.tab_loss[cell];
+        if (a.tab_key) {  // one 8-byte gather (uniform branch)
+          const uint64_t k = a.tab_key[cell];
+          lat = k >> 32;
+          loss = __uint_as_float((uint32_t)k);
+        } else {
+          lat = a.tab_lat[cell];
+          loss = a.tab_loss[cell];
+        }
         f[q] |= W_DRAW;
       }
       if (i < c1) {
@@ -839,6 +846,7 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   a.map = HostMap{hs->ip_base, hs->dense_span, hs->n, hs->dense, hs->sorted_ip, hs->sorted_host};
   a.tab_lat = tab->latency_ns;
   a.tab_loss = tab->packet_loss;
+  a.tab_key = tab->path_key;
   a.n_cols = tab->n_cols;
   a.row_begin = tab->row_begin;
   a.n_rows = tab->n_rows;
@@ -853,9 +861,9 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   a.blk_stats = ctx->d_blk.get<unsigned long long>(3 * (size_t)walk_blocks);
   a.err = w.err;
   {
-    // per packet: 20 B in, 12 B path gather, 4 B dst map, 21 B out (status, time, id), 4 B dst scratch;
-    // per host: 8 B segment, 4 B route, 32+32 B RNG, 8+8 B event counter
-    TimedLaunch tl(ctx, "walk", 61.0 * P + 92.0 * H);
+    // per packet: 20 B in, 12 B (8 B packed) path gather, 4 B dst map, 21 B out (status, time, id),
+    // 4 B dst scratch; per host: 8 B segment, 4 B route, 32+32 B RNG, 8+8 B event counter
+    TimedLaunch tl(ctx, "walk", (tab->path_key ? 57.0 : 61.0) * P + 92.0 * H);
     hipLaunchKernelGGL(k_walk, dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
   }
   hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(1024), 0, st, a.blk_stats, walk_blocks, w.stats);
@@ -927,6 +935,34 @@ static void deliver_bucket(sg_ctx* ctx, const sg_record* recv, uint32_t n, const
   uint32_t h_err = 0;
   copy_to_host(ctx, &h_err, err, 4);
   fail_flags(h_err);
+}
+
+// Path-key table: (lat << 32) | bits(loss) per cell, so the walk's path gather
+// is one 8-byte word.  Streaming, coalesced: 12 B in + 8 B out per cell.
+__global__ void __launch_bounds__(256) k_table_pack(const uint64_t* __restrict__ lat, const float* __restrict__ loss,
+                                                    size_t cells, uint64_t* __restrict__ key, uint32_t* wide) {
+  bool over = false;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < cells; i += (size_t)gridDim.x * 256) {
+    const uint64_t l = lat[i];
+    over |= (l >> 32) != 0;
+    key[i] = (l << 32) | __float_as_uint(loss[i]);
+  }
+  if (__any(over) && (threadIdx.x & 63) == 0) *wide = 1;  // rare: one store per wave that saw one
+}
+
+static void table_pack(sg_ctx* ctx, const sg_table* tab, size_t cells, uint64_t* key, uint32_t* packable) {
+  hipStream_t st = ctx->stream;
+  uint32_t* wide = ctx->d_seg.get<uint32_t>(1);
+  SG_HIP(hipMemsetAsync(wide, 0, 4, st));
+  if (cells) {
+    TimedLaunch tl(ctx, "table_pack", 20.0 * cells);
+    hipLaunchKernelGGL(k_table_pack, dim3(grid_for(cells, 256, 8192)), dim3(256), 0, st, tab->latency_ns,
+                       tab->packet_loss, cells, key, wide);
+    SG_CHECK_LAUNCH();
+  }
+  uint32_t h = 0;
+  copy_to_host(ctx, &h, wide, 4);
+  *packable = h ? 0 : 1;
 }
 
 }  // namespace sg
@@ -1054,7 +1090,7 @@ int32_t sg_deliver_round(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table, co
     if (packets->n_packets &&
         (!packets->src_host || !packets->dst_ipv4 || !packets->payload_len || !packets->send_time_ns ||
          !out->status || !out->deliver_time_ns || !out->event_id || !out->dst_order ||
-         !table->latency_ns || !table->packet_loss))
+         (!table->path_key && (!table->latency_ns || !table->packet_loss))))
       throw Error(SG_ERR_INVALID_ARG, "null packet or output array");
     deliver_round(ctx, hosts, table, round, packets, out, stats);
   });
@@ -1077,10 +1113,21 @@ int32_t sg_deliver_source(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table, c
       throw Error(SG_ERR_INVALID_ARG, "a host's routing index is outside the table's columns");
     if (packets->n_packets &&
         (!packets->src_host || !packets->dst_ipv4 || !packets->payload_len || !packets->send_time_ns || !status ||
-         !deliver_time_ns || !event_id || !send || !table->latency_ns || !table->packet_loss))
+         !deliver_time_ns || !event_id || !send || (!table->path_key && (!table->latency_ns || !table->packet_loss))))
       throw Error(SG_ERR_INVALID_ARG, "null packet or output array");
     deliver_source(ctx, hosts, table, round, packets, status, deliver_time_ns, event_id, host_owner, n_ranks, send,
                    send_counts, stats);
+  });
+}
+
+int32_t sg_table_pack(sg_ctx* ctx, const sg_table* table, uint64_t* out_key, uint32_t* out_packable) {
+  return sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (!table || !out_packable) throw Error(SG_ERR_INVALID_ARG, "null argument");
+    const size_t cells = (size_t)table->n_rows * table->n_cols;
+    if (cells && (!out_key || !table->latency_ns || !table->packet_loss))
+      throw Error(SG_ERR_INVALID_ARG, "null table or output array");
+    table_pack(ctx, table, cells, out_key, out_packable);
   });
 }
 

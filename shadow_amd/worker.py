@@ -95,12 +95,29 @@ class DeviceTable:
         self.n_cols = int(n_cols)
         self.row_begin = int(row_begin)
         self.n_rows = latency_ns.numel() // max(self.n_cols, 1)
+        self.path_key = None  # packed (lat << 32 | bits(loss)) cells, set by pack()
+
+    def pack(self, ctx=None) -> bool:
+        """Build the packed path-key copy of the table (sg_table_pack), so a
+        delivery round gathers one 8-byte word per packet.  Returns False and
+        keeps the two-array form when some latency is 2^32 ns or more."""
+        torch = _torch()
+        ctx = ctx or default_context()
+        key = torch.empty(max(self.latency_ns.numel(), 1), dtype=torch.int64, device=self.latency_ns.device)
+        ok = C.c_uint32(0)
+        self.path_key = None
+        t = self.struct()
+        _capi.check(ctx.handle, load().sg_table_pack(ctx.handle, C.byref(t), key.data_ptr(), C.byref(ok)))
+        if ok.value:
+            self.path_key = key
+        return bool(ok.value)
 
     def struct(self) -> _capi.sg_table:
         t = _capi.sg_table()
         t.latency_ns = self.latency_ns.data_ptr()
         t.packet_loss = self.packet_loss.data_ptr()
         t.n_cols, t.row_begin, t.n_rows = self.n_cols, self.row_begin, self.n_rows
+        t.path_key = self.path_key.data_ptr() if self.path_key is not None else None
         return t
 
 

@@ -17,13 +17,29 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
+_PACKED = {"on": False}
+
+
+@pytest.fixture(autouse=True, params=[False, True], ids=["two_array", "path_key"])
+def table_form(request):
+    """Every round runs twice: gathering (latency, loss) from the two arrays,
+    and from the packed path-key table (sg_table_pack)."""
+    _PACKED["on"] = request.param
+    yield request.param
+    _PACKED["on"] = False
+
+
 def _device_table(lat, loss, row_begin=0):
     import torch
 
     n_cols = lat.shape[1]
     dl = torch.from_numpy(np.ascontiguousarray(lat).view(np.int64).ravel()).cuda()
     df = torch.from_numpy(np.ascontiguousarray(loss).ravel()).cuda()
-    return DeviceTable(dl, df, n_cols, row_begin)
+    t = DeviceTable(dl, df, n_cols, row_begin)
+    if _PACKED["on"]:
+        wide = bool((np.asarray(lat, dtype=np.uint64) >> np.uint64(32)).any())
+        assert t.pack() == (not wide)
+    return t
 
 
 def _run_both(oracle, ctx, lat, loss, hosts, pk, round_end, sim_end, boot, rng0=None, ctr0=None):
@@ -193,4 +209,21 @@ def test_sparse_addresses_use_sorted_lookup(oracle, ctx):
     hosts["ip"] = (np.random.default_rng(1).permutation(2**20)[:300].astype(np.uint32) * 4000 + 7).astype(np.uint32)
     pk = synth.make_packets(8000, hosts, T0, T0 + 10**6, seed=9, p_unknown_dst=0.05)
     want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, T0 + 10**6, 2**63, 0)
+    _assert_same(want, got, ost, gst)
+
+
+def test_pack_refuses_wide_latency(oracle, ctx):
+    """A latency of 2^32 ns or more keeps the two-array form (pack returns False)
+    and the round is still exact."""
+    rng = np.random.default_rng(7)
+    hosts = synth.make_hosts(40, 6)
+    lat = rng.integers(1, 1000, size=(6, 6)).astype(np.uint64)
+    lat[:, 3] = np.uint64(1) << np.uint64(33)
+    loss = (rng.random((6, 6), dtype=np.float32) * 0.3).astype(np.float32)
+    t = _device_table(lat, loss)
+    assert not t.pack() and t.path_key is None
+    start, end = T0 + 10**9, T0 + 10**9 + 10**6
+    pk = synth.make_packets(500, hosts, start, end, seed=3)
+    want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, end, end + 10**12, 0)
+    assert want["delivered"] > 0
     _assert_same(want, got, ost, gst)

@@ -45,6 +45,8 @@ def _run(oracle, ctx, W, n_packets, hot=None, seed=1):
         dl = torch.from_numpy(np.ascontiguousarray(lat[r0:r1]).view(np.int64).ravel()).cuda()
         df = torch.from_numpy(np.ascontiguousarray(loss[r0:r1]).ravel()).cuda()
         table = DeviceTable(dl, df, nu, r0)
+        if r % 2:  # odd ranks gather from the packed path-key table (row block offset r0)
+            assert table.pack(ctx)
         batch = PacketBatch.from_numpy(pk["src"][sel], pk["dst_ip"][sel], pk["payload"][sel], pk["send_time"][sel])
         ranks.append(dict(sel=sel, ht=ht, table=table, batch=batch))
     # source phases
