@@ -61,7 +61,11 @@ int32_t sg_abi_version(void);
 /* ---- context ------------------------------------------------------------ */
 int32_t sg_ctx_create(int32_t device, sg_ctx** out);
 void sg_ctx_destroy(sg_ctx* ctx);
-/* Use an existing hipStream_t (e.g. torch's current stream); NULL = the context's own stream. */
+/* Use an existing hipStream_t (e.g. torch's current stream); NULL = the context's own
+ * stream, a blocking stream (ordered with work on the legacy default stream, which is
+ * torch's default stream).  Every entry point launches on this stream and reads
+ * device inputs in stream order: inputs written on some other non-blocking stream
+ * must be complete (or waited for) before the call. */
 int32_t sg_ctx_set_stream(sg_ctx* ctx, void* hip_stream);
 void* sg_ctx_stream(const sg_ctx* ctx);
 int32_t sg_ctx_synchronize(sg_ctx* ctx);

@@ -187,7 +187,10 @@ int32_t sg_ctx_create(int32_t device, sg_ctx** out) {
   ctx->device = device;
   int32_t rc = sg::guarded(ctx, [&] {
     SG_HIP(hipSetDevice(device));
-    SG_HIP(hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking));
+    // a blocking stream: ordered with the legacy default stream, so inputs a
+    // caller produced there (torch's default stream) are complete before our
+    // kernels read them, and our outputs before its later work reads them
+    SG_HIP(hipStreamCreateWithFlags(&ctx->own_stream, hipStreamDefault));
     ctx->stream = ctx->own_stream;
     int cus = 0;
     SG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));

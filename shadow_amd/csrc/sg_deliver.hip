@@ -505,20 +505,31 @@ static void fail_flags(uint32_t err) {
 // order[] = the ki of every entry sorted by (d, t, kk) -- EventQueue order per
 // destination (event.rs:84-155).
 //   1. k_sb_hist    tiles of SB_TILE entries: LDS histogram over super-buckets
-//                   (sb = d >> shift, a contiguous range of 2^shift slots);
+//                   (sb = d / spb, a contiguous range of spb slots, sized so a
+//                   super-bucket's entries fit one sort block's LDS);
 //   2. scan         of the (super-bucket, tile) counts;
 //   3. k_sb_scatter entries to their super-bucket (LDS cursors; order inside a
 //                   super-bucket is irrelevant, step 4 sorts it fully);
 //   4. k_sb_sort    block per super-bucket: per-slot counts and offsets in
-//                   LDS, placement by slot, insertion sort of each slot by
+//                   LDS, placement by slot, rank sort of each slot by
 //                   (t, kk); slots above SMALL_BUCKET entries go to k_sort_big.
 // ---------------------------------------------------------------------------
 constexpr int SB_THREADS = 256;
 constexpr int SB_TILE = 4096;        // entries per hist / scatter block
 constexpr int SB_MAX = 4096;         // super-buckets (LDS histogram bins)
-constexpr int SB_SLOTS_MAX = 1024;   // slots per super-bucket (2^shift)
-constexpr int SB_CAP = 3072;         // entries a super-bucket sorts in LDS
-constexpr int SB_TARGET = 1280;      // mean entries per super-bucket
+constexpr int SB_SLOTS_MAX = 1024;   // slots per super-bucket
+// entries a super-bucket sorts in LDS, and the mean entries per super-bucket
+// aimed for: 14 B of LDS per entry without a separate order key, 22 B with one
+template <bool KK> constexpr int SB_CAP = KK ? 3072 : 4096;
+template <bool KK> constexpr int SB_TARGET = KK ? 2048 : 2560;
+
+// Super-bucket of slot d: d / spb as a multiply-high (exact for d < 2^24,
+// spb < 2^16: magic = ceil(2^40 / spb)).
+struct SbMap {
+  uint64_t magic;
+  uint32_t spb;
+  __device__ __forceinline__ uint32_t of(uint32_t d) const { return (uint32_t)(((uint64_t)d * magic) >> 40); }
+};
 constexpr int SBT_THREADS = 512;     // k_sb_sort block
 
 struct PacketEntries {  // single GPU: entries are the round's packets, kk = ki = packet index
@@ -554,14 +565,14 @@ struct RecordEntries {  // sharded: entries are received records, slot = the des
 
 template <class E>
 __global__ void __launch_bounds__(SB_THREADS)
-    k_sb_hist(E src, uint32_t n, uint32_t shift, uint32_t n_sb, uint32_t* __restrict__ tile_hist) {
+    k_sb_hist(E src, uint32_t n, SbMap sm, uint32_t n_sb, uint32_t* __restrict__ tile_hist) {
   __shared__ uint32_t h[SB_MAX];
   for (uint32_t i = threadIdx.x; i < n_sb; i += SB_THREADS) h[i] = 0;
   __syncthreads();
   const uint32_t e0 = blockIdx.x * SB_TILE, e1 = min(e0 + SB_TILE, n);
   for (uint32_t e = e0 + threadIdx.x; e < e1; e += SB_THREADS) {
     const uint32_t d = src.slot(e);
-    if (d != NONE) atomicAdd(&h[d >> shift], 1u);
+    if (d != NONE) atomicAdd(&h[sm.of(d)], 1u);
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < n_sb; i += SB_THREADS) tile_hist[(size_t)i * gridDim.x + blockIdx.x] = h[i];
@@ -608,7 +619,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* a, uint32_t n
 constexpr int SBS_THREADS = 512;
 template <class E>
 __global__ void __launch_bounds__(SBS_THREADS)
-    k_sb_scatter(E src, uint32_t n, uint32_t shift, uint32_t n_sb, const uint32_t* __restrict__ tile_off,
+    k_sb_scatter(E src, uint32_t n, SbMap sm, uint32_t n_sb, const uint32_t* __restrict__ tile_off,
                  uint32_t* __restrict__ rd, uint64_t* __restrict__ rt, uint64_t* __restrict__ rk,
                  uint32_t* __restrict__ ri) {
   constexpr int PER = SB_TILE / SBS_THREADS;
@@ -627,7 +638,7 @@ __global__ void __launch_bounds__(SBS_THREADS)
   for (int k = 0; k < PER; k++) {
     const uint32_t e = e0 + threadIdx.x + k * SBS_THREADS;
     d[k] = e < e1 ? src.slot(e) : NONE;
-    if (d[k] != NONE) atomicAdd(&lcur[d[k] >> shift], 1u);
+    if (d[k] != NONE) atomicAdd(&lcur[sm.of(d[k])], 1u);
   }
   __syncthreads();
   const uint32_t total = block_exclusive_scan<SBS_THREADS, SB_MAX / SBS_THREADS>(lcur, n_sb, wsum);
@@ -638,7 +649,7 @@ __global__ void __launch_bounds__(SBS_THREADS)
   for (int k = 0; k < PER; k++) {
     if (d[k] == NONE) continue;
     const uint32_t e = e0 + threadIdx.x + k * SBS_THREADS;
-    const uint32_t p = atomicAdd(&lcur[d[k] >> shift], 1u);
+    const uint32_t p = atomicAdd(&lcur[sm.of(d[k])], 1u);
     uint64_t tt, kk;
     uint32_t ki;
     src.get(e, tt, kk, ki);
@@ -650,7 +661,7 @@ __global__ void __launch_bounds__(SBS_THREADS)
   __syncthreads();
   for (uint32_t p = threadIdx.x; p < total; p += SBS_THREADS) {
     const uint32_t dd = sd[p];
-    const uint32_t g = lbase[dd >> shift] + p;
+    const uint32_t g = lbase[sm.of(dd)] + p;
     rd[g] = dd;
     rt[g] = st_[p];
     ri[g] = si[p];
@@ -674,7 +685,8 @@ __device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32
     const uint32_t p = atomicAdd(&cur[j], 1u);
     Tt[p] = rt[e];
     const uint32_t v = ri[e];
-    Tk[p] = KK ? rk[e] : (uint64_t)v;
+    if (KK) Tk[p] = rk[e];
+    else if (!LDS) Tk[p] = v;  // k_sort_big reads the global key
     Ti[p] = v;
     Ts[p] = (uint16_t)j;
   }
@@ -686,7 +698,7 @@ __device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32
       if (LDS)
         for (uint32_t p = b; p < e; p++) {  // k_sort_big works on the global copy
           kt[s0 + p] = Tt[p];
-          kk[s0 + p] = Tk[p];
+          kk[s0 + p] = KK ? Tk[p] : (uint64_t)Ti[p];
           ki[s0 + p] = Ti[p];
         }
     }
@@ -698,9 +710,9 @@ __device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32
     const uint32_t j = Ts[p];
     const uint32_t b = cnt[j], e = cnt[j + 1];
     if (e - b > (uint32_t)SMALL_BUCKET) continue;  // k_sort_big writes this slot
-    const uint64_t t = Tt[p], k = Tk[p];
+    const uint64_t t = Tt[p], k = KK ? Tk[p] : (uint64_t)Ti[p];
     uint32_t rank = 0;
-    for (uint32_t q = b; q < e; q++) rank += key_less(Tt[q], Tk[q], t, k);
+    for (uint32_t q = b; q < e; q++) rank += key_less(Tt[q], KK ? Tk[q] : (uint64_t)Ti[q], t, k);
     order[s0 + b + rank] = Ti[p];
   }
 }
@@ -709,7 +721,7 @@ __device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32
 // In LDS when they fit (SB_CAP), else sorted in place in the global kt/kk/ki.
 template <bool KK>
 __global__ void __launch_bounds__(SBT_THREADS)
-    k_sb_sort(uint32_t shift, uint32_t n_slots, const uint32_t* __restrict__ tile_off, uint32_t n_tiles,
+    k_sb_sort(SbMap sm, uint32_t n_slots, const uint32_t* __restrict__ tile_off, uint32_t n_tiles,
               const uint32_t* __restrict__ rd, const uint64_t* __restrict__ rt, const uint64_t* __restrict__ rk,
               const uint32_t* __restrict__ ri, uint64_t* __restrict__ kt, uint64_t* __restrict__ kk,
               uint32_t* __restrict__ ki, uint32_t* __restrict__ offsets, uint32_t* __restrict__ order,
@@ -717,15 +729,16 @@ __global__ void __launch_bounds__(SBT_THREADS)
   __shared__ uint32_t cnt[SB_SLOTS_MAX + 1];
   __shared__ uint32_t cur[SB_SLOTS_MAX];
   __shared__ uint32_t wsum[SBT_THREADS / 64];
-  __shared__ uint64_t st[SB_CAP];
-  __shared__ uint64_t sk[SB_CAP];
-  __shared__ uint32_t si[SB_CAP];
-  __shared__ uint16_t ss[SB_CAP];
+  constexpr int CAP = SB_CAP<KK>;
+  __shared__ uint64_t st[CAP];
+  __shared__ uint64_t sk[KK ? CAP : 1];
+  __shared__ uint32_t si[CAP];
+  __shared__ uint16_t ss[CAP];
   const uint32_t sb = blockIdx.x;
   const uint32_t s0 = tile_off[(size_t)sb * n_tiles], s1 = tile_off[(size_t)(sb + 1) * n_tiles];
-  const uint32_t d0 = sb << shift, nd = min(1u << shift, n_slots - d0);
+  const uint32_t d0 = sb * sm.spb, nd = min(sm.spb, n_slots - d0);
   const uint32_t ns = s1 - s0;
-  const bool lds = ns <= (uint32_t)SB_CAP;
+  const bool lds = ns <= (uint32_t)CAP;
   for (uint32_t j = threadIdx.x; j <= nd; j += SBT_THREADS) cnt[j] = 0;
   __syncthreads();
   for (uint32_t e = s0 + threadIdx.x; e < s1; e += SBT_THREADS) atomicAdd(&cnt[rd[e] - d0], 1u);
@@ -756,12 +769,15 @@ static void bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
     SG_HIP(hipMemsetAsync(offsets, 0, 4, st));
     return;
   }
-  // 2^shift slots per super-bucket: about SB_TARGET entries each, <= SB_MAX super-buckets
-  uint32_t shift = 0;
-  while (shift < 10 && ((uint64_t)n << (shift + 1)) <= (uint64_t)SB_TARGET * n_slots) shift++;
-  while (((n_slots - 1) >> shift) + 1 > (uint32_t)SB_MAX) shift++;
-  if (shift > 10) throw Error(SG_ERR_INVALID_ARG, "too many destination hosts for one rank");
-  const uint32_t n_sb = ((n_slots - 1) >> shift) + 1;
+  // spb slots per super-bucket: about SB_TARGET entries each, <= SB_MAX super-buckets
+  if (n_slots >= (1u << 24)) throw Error(SG_ERR_INVALID_ARG, "too many destination hosts for one rank");
+  uint64_t spb64 = n ? ((uint64_t)SB_TARGET<E::KK> * n_slots + n - 1) / n : SB_SLOTS_MAX;
+  spb64 = std::min<uint64_t>(std::max<uint64_t>(spb64, (n_slots + SB_MAX - 1) / SB_MAX), SB_SLOTS_MAX);
+  spb64 = std::max<uint64_t>(spb64, 1);
+  if ((n_slots + spb64 - 1) / spb64 > (uint64_t)SB_MAX)
+    throw Error(SG_ERR_INVALID_ARG, "too many destination hosts for one rank");
+  SbMap sm{((1ull << 40) + spb64 - 1) / spb64, (uint32_t)spb64};
+  const uint32_t n_sb = (uint32_t)((n_slots + spb64 - 1) / spb64);
   const uint32_t n_tiles = std::max<uint32_t>(1, (n + SB_TILE - 1) / SB_TILE);
   const size_t nh = (size_t)n_sb * n_tiles;
   uint32_t* hist = ctx->d_cnt.get<uint32_t>(nh + 1);
@@ -777,16 +793,16 @@ static void bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
   uint16_t* spill = ctx->d_spill.get<uint16_t>(n);  // slot index per entry of super-buckets beyond SB_CAP
   {
     TimedLaunch tl(ctx, "scatter", 56.0 * n);
-    if (n) hipLaunchKernelGGL(k_sb_hist<E>, dim3(n_tiles), dim3(SB_THREADS), 0, st, src, n, shift, n_sb, hist);
+    if (n) hipLaunchKernelGGL(k_sb_hist<E>, dim3(n_tiles), dim3(SB_THREADS), 0, st, src, n, sm, n_sb, hist);
     else SG_HIP(hipMemsetAsync(hist, 0, nh * 4, st));
     exclusive_scan_u32(ctx, hist, toff, (uint32_t)nh);
     if (n)
-      hipLaunchKernelGGL(k_sb_scatter<E>, dim3(n_tiles), dim3(SBS_THREADS), 0, st, src, n, shift, n_sb, toff, rd, rt,
+      hipLaunchKernelGGL(k_sb_scatter<E>, dim3(n_tiles), dim3(SBS_THREADS), 0, st, src, n, sm, n_sb, toff, rd, rt,
                          rk, ri);
   }
   {
     TimedLaunch tl(ctx, "sort_small", 48.0 * n + 4.0 * n_slots);
-    hipLaunchKernelGGL(k_sb_sort<E::KK>, dim3(n_sb), dim3(SBT_THREADS), 0, st, shift, n_slots, toff, n_tiles, rd, rt,
+    hipLaunchKernelGGL(k_sb_sort<E::KK>, dim3(n_sb), dim3(SBT_THREADS), 0, st, sm, n_slots, toff, n_tiles, rd, rt,
                        rk, ri, kt, kk, ki, offsets, order, big_list, big_count, spill);
   }
   uint64_t* kt2 = ctx->d_keys2.get<uint64_t>(n);  // rd/rt are free again

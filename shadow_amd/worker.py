@@ -28,6 +28,17 @@ def _torch():
     return torch
 
 
+def _cached(obj, fields, build):
+    """ctypes struct for obj, rebuilt only when one of its tensor fields is replaced
+    (a round loop reuses the same buffers: no per-round data_ptr() / struct setup)."""
+    key = tuple(id(getattr(obj, f)) for f in fields)
+    c = obj.__dict__.get("_c")
+    if c is None or c[0] != key:
+        c = (key, build())
+        obj.__dict__["_c"] = c
+    return c[1]
+
+
 def _dev_u32(x, device):
     torch = _torch()
     if isinstance(x, torch.Tensor):
@@ -112,6 +123,9 @@ class DeviceTable:
             self.path_key = key
         return bool(ok.value)
 
+    def c_struct(self) -> _capi.sg_table:
+        return _cached(self, ("latency_ns", "packet_loss", "path_key"), self.struct)
+
     def struct(self) -> _capi.sg_table:
         t = _capi.sg_table()
         t.latency_ns = self.latency_ns.data_ptr()
@@ -138,6 +152,16 @@ class PacketBatch:
     def __len__(self):
         return int(self.src_host.numel())
 
+    def c_struct(self) -> _capi.sg_packets:
+        def build():
+            p = _capi.sg_packets()
+            p.n_packets = len(self)
+            p.src_host, p.dst_ipv4 = self.src_host.data_ptr(), self.dst_ipv4.data_ptr()
+            p.payload_len, p.send_time_ns = self.payload_len.data_ptr(), self.send_time_ns.data_ptr()
+            return p
+
+        return _cached(self, ("src_host", "dst_ipv4", "payload_len", "send_time_ns"), build)
+
 
 @dataclass
 class Deliveries:
@@ -159,6 +183,16 @@ class Deliveries:
                    torch.empty(max(n_packets, 1), dtype=torch.int32, device=device),
                    torch.empty(n_hosts + 1, dtype=torch.int32, device=device))
 
+    def c_struct(self) -> _capi.sg_deliveries:
+        def build():
+            d = _capi.sg_deliveries()
+            d.status, d.deliver_time_ns = self.status.data_ptr(), self.deliver_time_ns.data_ptr()
+            d.event_id, d.dst_order = self.event_id.data_ptr(), self.dst_order.data_ptr()
+            d.dst_offsets = self.dst_offsets.data_ptr()
+            return d
+
+        return _cached(self, ("status", "deliver_time_ns", "event_id", "dst_order", "dst_offsets"), build)
+
     def to_numpy(self, n_packets: int) -> dict:
         nd = self.n_delivered
         return dict(status=self.status[:n_packets].cpu().numpy(),
@@ -177,16 +211,13 @@ def deliver_round(hosts: HostTable, table: DeviceTable, packets: PacketBatch, ro
     ctx = ctx or hosts.ctx
     n = len(packets)
     out = out or Deliveries.allocate(n, hosts.n, device=packets.src_host.device if n else "cuda")
-    p = _capi.sg_packets()
-    p.n_packets = n
-    p.src_host, p.dst_ipv4 = packets.src_host.data_ptr(), packets.dst_ipv4.data_ptr()
-    p.payload_len, p.send_time_ns = packets.payload_len.data_ptr(), packets.send_time_ns.data_ptr()
-    d = _capi.sg_deliveries()
-    d.status, d.deliver_time_ns, d.event_id = out.status.data_ptr(), out.deliver_time_ns.data_ptr(), out.event_id.data_ptr()
-    d.dst_order, d.dst_offsets = out.dst_order.data_ptr(), out.dst_offsets.data_ptr()
+    if out.status.numel() < n or out.dst_offsets.numel() < hosts.n + 1:
+        raise ValueError("Deliveries buffers are smaller than the round")
+    p = packets.c_struct()
+    d = out.c_struct()
+    t = table.c_struct()
     r = _capi.sg_round(round_end_ns, sim_end_ns, bootstrap_end_ns)
     st = _capi.sg_round_stats()
-    t = table.struct()
     check(ctx.handle, load().sg_deliver_round(ctx.handle, hosts.handle, C.byref(t), C.byref(r), C.byref(p),
                                               C.byref(d), C.byref(st)))
     out.n_delivered = st.n_delivered
