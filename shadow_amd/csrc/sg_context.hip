@@ -192,6 +192,9 @@ int32_t sg_ctx_create(int32_t device, sg_ctx** out) {
     // kernels read them, and our outputs before its later work reads them
     SG_HIP(hipStreamCreateWithFlags(&ctx->own_stream, hipStreamDefault));
     ctx->stream = ctx->own_stream;
+    SG_HIP(hipMalloc(&ctx->round_err, 16));
+    SG_HIP(hipMemset(ctx->round_err, 0, 16));
+    SG_HIP(hipHostMalloc(&ctx->round_ret, sizeof(sg_round_ret), hipHostMallocMapped | hipHostMallocCoherent));
     int cus = 0;
     SG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     ctx->n_cu = cus;
@@ -215,6 +218,8 @@ void sg_ctx_destroy(sg_ctx* ctx) {
       (void)hipEventDestroy(pr.second);
     }
   for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+  if (ctx->round_err) (void)hipFree(ctx->round_err);
+  if (ctx->round_ret) (void)hipHostFree(ctx->round_ret);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }

@@ -155,7 +155,9 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
   __shared__ uint8_t s_f[WALK_CHUNK];    // W_* flags -> SG_PKT_* status
   const uint32_t h0 = blockIdx.x * WALK_HOSTS;
   const uint32_t t = threadIdx.x;
-  const uint32_t p0 = a.host_off[min(h0, a.H)], p1 = a.host_off[min(h0 + WALK_HOSTS, a.H)];
+  // clamped: after a grouping error (flagged by k_host_off) host_off is partly unwritten
+  const uint32_t p0 = min(a.host_off[min(h0, a.H)], a.P);
+  const uint32_t p1 = max(min(a.host_off[min(h0 + WALK_HOSTS, a.H)], a.P), p0);
   // walker lanes: thread t < WALK_HOSTS walks host h0 + t
   const uint32_t h = h0 + t;
   const bool walker = t < WALK_HOSTS && h < a.H;
@@ -163,8 +165,8 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
   Xoshiro x{0, 0, 0, 0};
   uint64_t c = 0;
   if (walker) {
-    hb = a.host_off[h];
-    he = a.host_off[h + 1];
+    hb = min(a.host_off[h], a.P);
+    he = max(min(a.host_off[h + 1], a.P), hb);
     if (hb < he) {
       x = Xoshiro{a.rng[h], a.rng[(size_t)a.H + h], a.rng[2 * (size_t)a.H + h], a.rng[3 * (size_t)a.H + h]};
       c = a.ctr[h];
@@ -301,9 +303,13 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
   }
 }
 
-// Round statistics: sum / min / min over the walk blocks' partials.
+// Round statistics: sum / min / min over the walk blocks' partials, written
+// with the source phase's error flags straight into the context's pinned
+// host-mapped return block.  Clears the flags (for the next round) and the
+// big-slot counter (for this round's bucketing, which runs next).
 __global__ void __launch_bounds__(1024) k_reduce_stats(const unsigned long long* __restrict__ blk, uint32_t n,
-                                                       unsigned long long* __restrict__ out) {
+                                                       uint32_t* __restrict__ err, uint32_t* __restrict__ big_count,
+                                                       sg_round_ret* __restrict__ ret) {
   __shared__ unsigned long long r[3][16];
   unsigned long long nd = 0, mind = ~0ull, minl = ~0ull;
   for (uint32_t i = threadIdx.x; i < n; i += 1024) {
@@ -329,9 +335,12 @@ __global__ void __launch_bounds__(1024) k_reduce_stats(const unsigned long long*
       mind = min(mind, r[1][i]);
       minl = min(minl, r[2][i]);
     }
-    out[0] = nd;
-    out[1] = mind;
-    out[2] = minl;
+    ret->stats[0] = nd;
+    ret->stats[1] = mind;
+    ret->stats[2] = minl;
+    ret->err = *err;
+    *err = 0;
+    *big_count = 0;
   }
 }
 
@@ -817,9 +826,9 @@ static void bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
 }
 
 struct RoundWork {
-  uint32_t *host_off, *big_count, *err, *dst_host;
+  uint32_t *host_off, *big_count, *dst_host;
   uint64_t* ctr_start;
-  unsigned long long* stats;
+  bool walked;  // the walk and the stats kernel ran (P > 0)
 };
 
 // Shared source half of a round: host offsets + walk.  Leaves per-packet
@@ -830,23 +839,24 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   hipStream_t st = ctx->stream;
   const uint32_t P = pk->n_packets, H = hs->n;
   RoundWork w;
-  // workspace: [host_off H+1][big_count 1][err 1]
+  // workspace: [host_off H+1][big_count 1]; k_host_off writes every host_off
+  // entry of well-grouped packets (else it flags an error and the walk clamps),
+  // k_reduce_stats zeroes big_count: no fills on the round's path
   uint32_t* ws = ctx->d_seg.get<uint32_t>((size_t)H + 8);
   w.host_off = ws;
   w.big_count = ws + (size_t)H + 1;
-  w.err = w.big_count + 1;
-  w.stats = ctx->d_misc.get<unsigned long long>(4);
   w.dst_host = ctx->d_dst.get<uint32_t>(P);
   w.ctr_start = want_ctr_start ? ctx->d_ctr0.get<uint64_t>(H) : nullptr;
-  SG_HIP(hipMemsetAsync(ws, 0, ((size_t)H + 8) * 4, st));
-  SG_HIP(hipMemsetAsync(w.stats, 0, 8, st));  // P = 0: no walk, no reduction
-  SG_HIP(hipMemsetAsync(w.stats + 1, 0xff, 16, st));
+  w.walked = P > 0;
   if (w.ctr_start) SG_HIP(hipMemcpyAsync(w.ctr_start, hs->ctr, (size_t)H * 8, hipMemcpyDeviceToDevice, st));
-  if (!P) return w;
+  if (!P) {
+    SG_HIP(hipMemsetAsync(w.big_count, 0, 4, st));
+    return w;
+  }
   {
     TimedLaunch tl(ctx, "seg_bounds", 4.0 * P + 4.0 * H);
     hipLaunchKernelGGL(k_host_off, dim3(grid_for((size_t)P + 1, 256, 16384)), dim3(256), 0, st, pk->src_host, P, H,
-                       w.host_off, w.err);
+                       w.host_off, ctx->round_err);
   }
   WalkArgs a;
   a.src = pk->src_host;
@@ -875,32 +885,33 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   a.dst_host = w.dst_host;
   const uint32_t walk_blocks = (H + WALK_HOSTS - 1) / WALK_HOSTS;
   a.blk_stats = ctx->d_blk.get<unsigned long long>(3 * (size_t)walk_blocks);
-  a.err = w.err;
+  a.err = ctx->round_err;
   {
     // per packet: 20 B in, 12 B (8 B packed) path gather, 4 B dst map, 21 B out (status, time, id),
     // 4 B dst scratch; per host: 8 B segment, 4 B route, 32+32 B RNG, 8+8 B event counter
     TimedLaunch tl(ctx, "walk", (tab->path_key ? 57.0 : 61.0) * P + 92.0 * H);
     hipLaunchKernelGGL(k_walk, dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
   }
-  hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(1024), 0, st, a.blk_stats, walk_blocks, w.stats);
+  hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(1024), 0, st, a.blk_stats, walk_blocks, ctx->round_err,
+                     w.big_count, ctx->round_ret);
   SG_CHECK_LAUNCH();
   return w;
 }
 
 static void finish(sg_ctx* ctx, const RoundWork& w, sg_round_stats* stats) {
-  struct {
-    unsigned long long s[3];
-    uint32_t err;
-  } h;
-  hipStream_t st = ctx->stream;
-  SG_HIP(hipMemcpyAsync(h.s, w.stats, 24, hipMemcpyDeviceToHost, st));
-  SG_HIP(hipMemcpyAsync(&h.err, w.err, 4, hipMemcpyDeviceToHost, st));
-  SG_HIP(hipStreamSynchronize(st));
-  fail_flags(h.err);
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  unsigned long long s[3] = {0, ~0ull, ~0ull};
+  uint32_t err = 0;
+  if (w.walked) {  // written by k_reduce_stats into mapped host memory; the sync made it visible
+    const volatile sg_round_ret* r = ctx->round_ret;
+    for (int i = 0; i < 3; i++) s[i] = r->stats[i];
+    err = r->err;
+  }
+  fail_flags(err);
   if (stats) {
-    stats->n_delivered = h.s[0];
-    stats->min_deliver_time_ns = h.s[1];
-    stats->min_used_latency_ns = h.s[2];
+    stats->n_delivered = s[0];
+    stats->min_deliver_time_ns = s[1];
+    stats->min_used_latency_ns = s[2];
   }
 }
 

@@ -74,6 +74,12 @@ struct KernelTimer {
 
 }  // namespace sg
 
+struct sg_round_ret {
+  unsigned long long stats[3];  // n_delivered, min deliver time, min used latency
+  uint32_t err;
+  uint32_t pad;
+};
+
 struct sg_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -88,6 +94,12 @@ struct sg_ctx {
   sg::DevBuf d_seg, d_dst, d_cnt, d_cur, d_keys, d_vals, d_keys2, d_vals2, d_keys3, d_keys4, d_misc,
       d_scan, d_lists, d_lists2, d_ctr0, d_blk, d_spill;
   sg::DevBuf m_scratch;
+  // Round control: round_err (device, zeroed at creation) collects the source
+  // phase's error flags; the stats kernel hands them to the host and clears
+  // them for the next round.  round_ret (pinned, mapped host memory) receives
+  // the round's stats and error flags straight from that kernel: no copies.
+  uint32_t* round_err = nullptr;
+  sg_round_ret* round_ret = nullptr;
   // kernel timers (off unless sg_ctx_enable_timers)
   bool timing = false;
   bool count_work = false;  // SG_TIMERS_COUNT_WORK

@@ -198,6 +198,20 @@ def test_unsorted_sources_rejected(ctx):
     assert e.value.code == _capi.SG_ERR_UNSORTED
 
 
+def test_error_flags_do_not_leak_into_next_round(oracle, ctx):
+    """The source phase's error flags live in a per-context word the round's
+    stats kernel clears: a rejected round leaves the next one clean and exact."""
+    lat, loss, hosts = _world(n_hosts=200, seed=9)
+    ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    bad = PacketBatch.from_numpy([5, 250], hosts["ip"][[0, 1]], [1, 1], [T0, T0])  # source 250 out of range
+    with pytest.raises(ShadowGpuError):
+        deliver_round(ht, _device_table(lat, loss), bad, T0 + 10, 2**63, 0)
+    start, end = T0 + 10**9, T0 + 10**9 + 10**6
+    pk = synth.make_packets(3000, hosts, start, end, seed=9)
+    want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, end, 2**63, 0)
+    _assert_same(want, got, ost, gst)
+
+
 def test_duplicate_ip_rejected(ctx):
     with pytest.raises(ShadowGpuError) as e:
         HostTable([5, 5], [0, 0], [1, 2], ctx=ctx)
