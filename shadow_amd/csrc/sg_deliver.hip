@@ -147,12 +147,17 @@ constexpr int WALK_HOSTS = 64;
 constexpr int WALK_CHUNK = 1024;
 enum : uint8_t { W_SIM_END = 0, W_NO_DST = 1, W_DRAW = 2, W_PAYLOAD = 4, W_BOOT = 8 };
 
+// PACKED: the path cell is one (lat << 32 | bits(loss)) word, kept whole in
+// LDS (17 B of LDS per staged packet, so every block of a 100k-host round is
+// resident at once); else latency and loss are staged separately (21 B).  The
+// destination stays in the registers of the thread that resolved it: phases 1
+// and 3 map packets to threads identically.
+template <bool PACKED>
 __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
-  __shared__ uint64_t s_t[WALK_CHUNK];   // send time -> arrival time
-  __shared__ uint64_t s_l[WALK_CHUNK];   // path latency -> event id
-  __shared__ float s_loss[WALK_CHUNK];   // path packet loss
-  __shared__ uint32_t s_d[WALK_CHUNK];   // destination host -> NONE unless delivered
-  __shared__ uint8_t s_f[WALK_CHUNK];    // W_* flags -> SG_PKT_* status
+  __shared__ uint64_t s_t[WALK_CHUNK];                  // send time -> arrival time
+  __shared__ uint64_t s_l[WALK_CHUNK];                  // path latency (or cell) -> event id
+  __shared__ float s_loss[PACKED ? 1 : WALK_CHUNK];     // path packet loss (two-array form)
+  __shared__ uint8_t s_f[WALK_CHUNK];                   // W_* flags -> SG_PKT_* status
   const uint32_t h0 = blockIdx.x * WALK_HOSTS;
   const uint32_t t = threadIdx.x;
   // clamped: after a grouping error (flagged by k_host_off) host_off is partly unwritten
@@ -210,14 +215,12 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
 #pragma unroll
     for (int q = 0; q < PPT; q++) {
       const uint32_t i = c0 + t + q * WALK_THREADS;
-      uint64_t lat = 0;
+      uint64_t lat = 0;  // PACKED: the whole cell
       float loss = 0.0f;
       if (d[q] != NONE) {
         const size_t cell = (size_t)(r[q] - a.row_begin) * a.n_cols + ip[q];
-        if (a.tab_key) {  // one 8-byte gather (uniform branch)
-          const uint64_t k = a.tab_key[cell];
-          lat = k >> 32;
-          loss = __uint_as_float((uint32_t)k);
+        if (PACKED) {
+          lat = a.tab_key[cell];  // one 8-byte gather
         } else {
           lat = a.tab_lat[cell];
           loss = a.tab_loss[cell];
@@ -228,8 +231,7 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
         const uint32_t k = i - c0;
         s_t[k] = now[q];
         s_l[k] = lat;
-        s_loss[k] = loss;
-        s_d[k] = d[q];
+        if (!PACKED) s_loss[k] = loss;
         s_f[k] = f[q];
       }
     }
@@ -242,17 +244,17 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
         const uint8_t f = s_f[k];
         uint8_t st;
         uint64_t arr = 0, id = ~0ull;
-        uint32_t d = s_d[k];
         if (f & W_DRAW) {
+          const uint64_t cell = s_l[k];
+          const float loss = PACKED ? __uint_as_float((uint32_t)cell) : s_loss[k];
+          const uint64_t lat = PACKED ? cell >> 32 : cell;
           // reliability = f64::from(1.0f32 - loss) (worker.rs:357-359, 526-531)
-          const double rel = (double)__fsub_rn(1.0f, s_loss[k]);
+          const double rel = (double)__fsub_rn(1.0f, loss);
           const double chance = x.next_f64();  // worker.rs:360
           if (!(f & W_BOOT) && chance >= rel && (f & W_PAYLOAD)) {  // worker.rs:365-368
             st = SG_PKT_DROP_LOSS;
-            d = NONE;
           } else {
-            const uint64_t lat = s_l[k];  // worker.rs:370
-            arr = s_t[k] + lat;
+            arr = s_t[k] + lat;                         // worker.rs:370
             if (arr < a.round_end) arr = a.round_end;  // worker.rs:381-384
             id = c++;                                  // host.rs:649-653
             st = SG_PKT_DELIVERED;
@@ -262,22 +264,25 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
           }
         } else {
           st = (f & W_NO_DST) ? SG_PKT_DROP_NO_DST : SG_PKT_SIM_END;
-          d = NONE;
         }
         s_t[k] = arr;
         s_l[k] = id;
-        s_d[k] = d;
         s_f[k] = st;
       }
     }
     __syncthreads();
-    // 3. coalesced stores
-    for (uint32_t i = c0 + t; i < c1; i += WALK_THREADS) {
-      const uint32_t k = i - c0;
-      a.status[i] = s_f[k];
-      a.deliver[i] = s_t[k];
-      a.eid[i] = s_l[k];
-      a.dst_host[i] = s_d[k];
+    // 3. coalesced stores (the same packet -> thread map as phase 1)
+#pragma unroll
+    for (int q = 0; q < PPT; q++) {
+      const uint32_t i = c0 + t + q * WALK_THREADS;
+      if (i < c1) {
+        const uint32_t k = i - c0;
+        const uint8_t st = s_f[k];
+        a.status[i] = st;
+        a.deliver[i] = s_t[k];
+        a.eid[i] = s_l[k];
+        a.dst_host[i] = st == SG_PKT_DELIVERED ? d[q] : NONE;
+      }
     }
     __syncthreads();
   }
@@ -526,6 +531,7 @@ static void fail_flags(uint32_t err) {
 constexpr int SB_THREADS = 256;
 constexpr int SB_TILE = 4096;        // entries per hist / scatter block
 constexpr int SB_MAX = 4096;         // super-buckets (LDS histogram bins)
+static_assert(SB_MAX + 1 == SB_CTL_STRIDE, "region counters: SB_MAX counts + the overflow flag");
 constexpr int SB_SLOTS_MAX = 1024;   // slots per super-bucket
 // entries a super-bucket sorts in LDS, and the mean entries per super-bucket
 // aimed for: 14 B of LDS per entry without a separate order key, 22 B with one
@@ -625,12 +631,17 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* a, uint32_t n
 // Tile -> super-buckets.  The tile is first counting-sorted by super-bucket in
 // LDS, so each super-bucket's entries of the tile leave as one contiguous run
 // (coalesced stores instead of one scattered store per entry and array).
+// REGION: instead of the (super-bucket, tile) scan, a tile claims each run in
+// its super-bucket's fixed region of `region` entries with one atomic per
+// (tile, super-bucket); a run that would overflow the region is dropped and
+// flagged in ctl[SB_MAX] (the host then reruns the scan path).
 constexpr int SBS_THREADS = 512;
-template <class E>
+constexpr uint32_t RUN_DROPPED = 0xFFFFFFFFu;  // cannot be a valid run base (see below)
+template <class E, bool REGION>
 __global__ void __launch_bounds__(SBS_THREADS)
     k_sb_scatter(E src, uint32_t n, SbMap sm, uint32_t n_sb, const uint32_t* __restrict__ tile_off,
-                 uint32_t* __restrict__ rd, uint64_t* __restrict__ rt, uint64_t* __restrict__ rk,
-                 uint32_t* __restrict__ ri) {
+                 uint32_t* __restrict__ ctl, uint32_t region, uint32_t* __restrict__ rd, uint64_t* __restrict__ rt,
+                 uint64_t* __restrict__ rk, uint32_t* __restrict__ ri) {
   constexpr int PER = SB_TILE / SBS_THREADS;
   __shared__ uint32_t lcur[SB_MAX];   // local start, then cursor
   __shared__ uint32_t lbase[SB_MAX];  // global position of the run - local start
@@ -651,8 +662,25 @@ __global__ void __launch_bounds__(SBS_THREADS)
   }
   __syncthreads();
   const uint32_t total = block_exclusive_scan<SBS_THREADS, SB_MAX / SBS_THREADS>(lcur, n_sb, wsum);
-  for (uint32_t i = threadIdx.x; i < n_sb; i += SBS_THREADS)
-    lbase[i] = tile_off[(size_t)i * gridDim.x + blockIdx.x] - lcur[i];
+  for (uint32_t i = threadIdx.x; i < n_sb; i += SBS_THREADS) {
+    if (REGION) {
+      // the run of super-bucket i: local [lcur[i], lcur[i] + c) -> region slot g..g+c.
+      // A kept base is i * region + g - lcur[i] with lcur[i] <= g + i * region
+      // (i = 0: lcur[0] = 0), never RUN_DROPPED.
+      const uint32_t c = (i + 1 < n_sb ? lcur[i + 1] : total) - lcur[i];
+      uint32_t base = RUN_DROPPED;
+      if (c) {
+        const uint32_t g = atomicAdd(&ctl[i], c);
+        if (g + c <= region)
+          base = i * region + g - lcur[i];
+        else
+          ctl[SB_MAX] = 1u;
+      }
+      lbase[i] = base;
+    } else {
+      lbase[i] = tile_off[(size_t)i * gridDim.x + blockIdx.x] - lcur[i];
+    }
+  }
   __syncthreads();  // lcur is the cursor from here on
 #pragma unroll
   for (int k = 0; k < PER; k++) {
@@ -670,7 +698,9 @@ __global__ void __launch_bounds__(SBS_THREADS)
   __syncthreads();
   for (uint32_t p = threadIdx.x; p < total; p += SBS_THREADS) {
     const uint32_t dd = sd[p];
-    const uint32_t g = lbase[sm.of(dd)] + p;
+    const uint32_t lb = lbase[sm.of(dd)];
+    if (REGION && lb == RUN_DROPPED) continue;
+    const uint32_t g = lb + p;
     rd[g] = dd;
     rt[g] = st_[p];
     ri[g] = si[p];
@@ -681,15 +711,15 @@ __global__ void __launch_bounds__(SBS_THREADS)
 // Placement of a super-bucket's entries by slot, then per-slot order by (t, kk).
 // Without KK the order key is the value (ri) itself.
 template <bool LDS, bool KK>
-__device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32_t* Ti, uint16_t* Ts, uint32_t s0,
-                                              uint32_t s1, uint32_t d0, uint32_t nd, const uint32_t* cnt,
+__device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32_t* Ti, uint16_t* Ts, uint32_t in0,
+                                              uint32_t s0, uint32_t s1, uint32_t d0, uint32_t nd, const uint32_t* cnt,
                                               uint32_t* cur, const uint32_t* __restrict__ rd,
                                               const uint64_t* __restrict__ rt, const uint64_t* __restrict__ rk,
                                               const uint32_t* __restrict__ ri, uint64_t* __restrict__ kt,
                                               uint64_t* __restrict__ kk, uint32_t* __restrict__ ki,
                                               uint32_t* __restrict__ order, uint32_t* __restrict__ big_list,
                                               uint32_t* __restrict__ big_count) {
-  for (uint32_t e = s0 + threadIdx.x; e < s1; e += SBT_THREADS) {
+  for (uint32_t e = in0 + threadIdx.x; e < in0 + (s1 - s0); e += SBT_THREADS) {
     const uint32_t j = rd[e] - d0;
     const uint32_t p = atomicAdd(&cur[j], 1u);
     Tt[p] = rt[e];
@@ -726,15 +756,18 @@ __device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32
   }
 }
 
-// Block per super-bucket.  Entries of the super-bucket: [s0, s1) of rd/rt/rk/ri.
-// In LDS when they fit (SB_CAP), else sorted in place in the global kt/kk/ki.
+// Block per super-bucket: its ns entries are at [in0, in0 + ns) of rd/rt/rk/ri
+// and take positions [s0, s0 + ns) of order[].  In LDS when they fit (SB_CAP),
+// else sorted in place in the global kt/kk/ki.
 template <bool KK>
-__global__ void __launch_bounds__(SBT_THREADS)
-    k_sb_sort(SbMap sm, uint32_t n_slots, const uint32_t* __restrict__ tile_off, uint32_t n_tiles,
-              const uint32_t* __restrict__ rd, const uint64_t* __restrict__ rt, const uint64_t* __restrict__ rk,
-              const uint32_t* __restrict__ ri, uint64_t* __restrict__ kt, uint64_t* __restrict__ kk,
-              uint32_t* __restrict__ ki, uint32_t* __restrict__ offsets, uint32_t* __restrict__ order,
-              uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count, uint16_t* __restrict__ slot_spill) {
+__device__ __forceinline__ void sb_sort_body(uint32_t sb, SbMap sm, uint32_t n_slots, uint32_t in0, uint32_t s0,
+                                             uint32_t ns, const uint32_t* __restrict__ rd,
+                                             const uint64_t* __restrict__ rt, const uint64_t* __restrict__ rk,
+                                             const uint32_t* __restrict__ ri, uint64_t* __restrict__ kt,
+                                             uint64_t* __restrict__ kk, uint32_t* __restrict__ ki,
+                                             uint32_t* __restrict__ offsets, uint32_t* __restrict__ order,
+                                             uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count,
+                                             uint16_t* __restrict__ slot_spill) {
   __shared__ uint32_t cnt[SB_SLOTS_MAX + 1];
   __shared__ uint32_t cur[SB_SLOTS_MAX];
   __shared__ uint32_t wsum[SBT_THREADS / 64];
@@ -743,14 +776,12 @@ __global__ void __launch_bounds__(SBT_THREADS)
   __shared__ uint64_t sk[KK ? CAP : 1];
   __shared__ uint32_t si[CAP];
   __shared__ uint16_t ss[CAP];
-  const uint32_t sb = blockIdx.x;
-  const uint32_t s0 = tile_off[(size_t)sb * n_tiles], s1 = tile_off[(size_t)(sb + 1) * n_tiles];
+  const uint32_t s1 = s0 + ns;
   const uint32_t d0 = sb * sm.spb, nd = min(sm.spb, n_slots - d0);
-  const uint32_t ns = s1 - s0;
   const bool lds = ns <= (uint32_t)CAP;
   for (uint32_t j = threadIdx.x; j <= nd; j += SBT_THREADS) cnt[j] = 0;
   __syncthreads();
-  for (uint32_t e = s0 + threadIdx.x; e < s1; e += SBT_THREADS) atomicAdd(&cnt[rd[e] - d0], 1u);
+  for (uint32_t e = in0 + threadIdx.x; e < in0 + ns; e += SBT_THREADS) atomicAdd(&cnt[rd[e] - d0], 1u);
   __syncthreads();
   // exclusive scan of cnt[0..nd), nd <= SB_SLOTS_MAX
   const uint32_t tot = block_exclusive_scan<SBT_THREADS, SB_SLOTS_MAX / SBT_THREADS>(cnt, nd, wsum);
@@ -762,21 +793,69 @@ __global__ void __launch_bounds__(SBT_THREADS)
   // LDS and global variants as separate inlined bodies: one generic pointer
   // would turn every access into a flat instruction waiting on both counters
   if (lds)
-    sb_place_sort<true, KK>(st, sk, si, ss, s0, s1, d0, nd, cnt, cur, rd, rt, rk, ri, kt, kk, ki, order, big_list,
-                            big_count);
+    sb_place_sort<true, KK>(st, sk, si, ss, in0, s0, s1, d0, nd, cnt, cur, rd, rt, rk, ri, kt, kk, ki, order,
+                            big_list, big_count);
   else
-    sb_place_sort<false, KK>(kt + s0, kk + s0, ki + s0, slot_spill + s0, s0, s1, d0, nd, cnt, cur, rd, rt, rk, ri,
-                             kt, kk, ki, order, big_list, big_count);
+    sb_place_sort<false, KK>(kt + s0, kk + s0, ki + s0, slot_spill + s0, in0, s0, s1, d0, nd, cnt, cur, rd, rt, rk,
+                             ri, kt, kk, ki, order, big_list, big_count);
+}
+
+// Scan path: super-bucket sb's entries are [tile_off[sb, 0], tile_off[sb + 1, 0]).
+template <bool KK>
+__global__ void __launch_bounds__(SBT_THREADS)
+    k_sb_sort(SbMap sm, uint32_t n_slots, const uint32_t* __restrict__ tile_off, uint32_t n_tiles,
+              const uint32_t* __restrict__ rd, const uint64_t* __restrict__ rt, const uint64_t* __restrict__ rk,
+              const uint32_t* __restrict__ ri, uint64_t* __restrict__ kt, uint64_t* __restrict__ kk,
+              uint32_t* __restrict__ ki, uint32_t* __restrict__ offsets, uint32_t* __restrict__ order,
+              uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count, uint16_t* __restrict__ slot_spill) {
+  const uint32_t sb = blockIdx.x;
+  const uint32_t s0 = tile_off[(size_t)sb * n_tiles], s1 = tile_off[(size_t)(sb + 1) * n_tiles];
+  sb_sort_body<KK>(sb, sm, n_slots, s0, s0, s1 - s0, rd, rt, rk, ri, kt, kk, ki, offsets, order, big_list, big_count,
+                   slot_spill);
+}
+
+// Region path: super-bucket sb's entries are [sb * region, sb * region + count[sb])
+// (k_sb_scatter_region); its output position is the sum of the counts before
+// it.  The block does nothing if a region overflowed (the host then reruns the
+// scan path); every block clears a share of the other parity's counters.
+template <bool KK>
+__global__ void __launch_bounds__(SBT_THREADS)
+    k_sb_sort_region(SbMap sm, uint32_t n_slots, uint32_t n_sb, const uint32_t* __restrict__ ctl,
+                     uint32_t* __restrict__ ctl_next, uint32_t region, const uint32_t* __restrict__ rd,
+                     const uint64_t* __restrict__ rt, const uint64_t* __restrict__ rk,
+                     const uint32_t* __restrict__ ri, uint64_t* __restrict__ kt, uint64_t* __restrict__ kk,
+                     uint32_t* __restrict__ ki, uint32_t* __restrict__ offsets, uint32_t* __restrict__ order,
+                     uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count,
+                     uint16_t* __restrict__ slot_spill, sg_round_ret* __restrict__ ret) {
+  __shared__ uint32_t part[SBT_THREADS / 64];
+  for (uint32_t i = blockIdx.x * SBT_THREADS + threadIdx.x; i <= SB_MAX; i += gridDim.x * SBT_THREADS) ctl_next[i] = 0;
+  const uint32_t over = ctl[SB_MAX];
+  if (blockIdx.x == 0 && threadIdx.x == 0) ret->overflow = over;
+  if (over) return;  // uniform across the grid
+  const uint32_t sb = blockIdx.x;
+  uint32_t before = 0;
+  for (uint32_t i = threadIdx.x; i < sb; i += SBT_THREADS) before += ctl[i];
+  for (int dd = 32; dd > 0; dd >>= 1) before += __shfl_xor(before, dd, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = before;
+  __syncthreads();
+  uint32_t s0 = 0;
+  for (int w = 0; w < SBT_THREADS / 64; w++) s0 += part[w];
+  sb_sort_body<KK>(sb, sm, n_slots, sb * region, s0, ctl[sb], rd, rt, rk, ri, kt, kk, ki, offsets, order, big_list,
+                   big_count, slot_spill);
 }
 
 // Bucket sort of n entries into n_slots destination slots (see above).
+// region = true tries the region path (no tile histogram, no scan); it returns
+// true when it did, and the caller must then check round_ret->overflow after
+// synchronising and, if set, call again with region = false (hot destinations
+// that overfill a super-bucket's region; big_count zeroed again first).
 template <class E>
-static void bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32_t* offsets, uint32_t* order,
-                        uint32_t* big_count) {
+static bool bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32_t* offsets, uint32_t* order,
+                        uint32_t* big_count, bool region) {
   hipStream_t st = ctx->stream;
   if (n_slots == 0) {
     SG_HIP(hipMemsetAsync(offsets, 0, 4, st));
-    return;
+    return false;
   }
   // spb slots per super-bucket: about SB_TARGET entries each, <= SB_MAX super-buckets
   if (n_slots >= (1u << 24)) throw Error(SG_ERR_INVALID_ARG, "too many destination hosts for one rank");
@@ -788,31 +867,52 @@ static void bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
   SbMap sm{((1ull << 40) + spb64 - 1) / spb64, (uint32_t)spb64};
   const uint32_t n_sb = (uint32_t)((n_slots + spb64 - 1) / spb64);
   const uint32_t n_tiles = std::max<uint32_t>(1, (n + SB_TILE - 1) / SB_TILE);
-  const size_t nh = (size_t)n_sb * n_tiles;
-  uint32_t* hist = ctx->d_cnt.get<uint32_t>(nh + 1);
-  uint32_t* toff = ctx->d_scan.get<uint32_t>(nh + 1);
-  uint32_t* rd = ctx->d_lists2.get<uint32_t>(n);
-  uint64_t* rt = ctx->d_keys2.get<uint64_t>(n);
-  uint64_t* rk = ctx->d_keys3.get<uint64_t>(n);
-  uint32_t* ri = ctx->d_vals2.get<uint32_t>(n);
+  const char* env = getenv("SG_BUCKET_REGION");
+  region = region && n > 0 && !(env && env[0] == '0');
+  const uint32_t reg = SB_CAP<E::KK>;  // a region is sorted in LDS in one piece
+  const size_t cap = region ? std::max<size_t>((size_t)n_sb * reg, n) : n;
+  uint32_t* rd = ctx->d_lists2.get<uint32_t>(cap);
+  uint64_t* rt = ctx->d_keys2.get<uint64_t>(cap);
+  uint64_t* rk = ctx->d_keys3.get<uint64_t>(E::KK ? cap : 1);
+  uint32_t* ri = ctx->d_vals2.get<uint32_t>(cap);
   uint64_t* kt = ctx->d_keys.get<uint64_t>(n);
   uint64_t* kk = ctx->d_keys4.get<uint64_t>(n);
   uint32_t* ki = ctx->d_vals.get<uint32_t>(n);
   uint32_t* big_list = ctx->d_lists.get<uint32_t>(n_slots);
   uint16_t* spill = ctx->d_spill.get<uint16_t>(n);  // slot index per entry of super-buckets beyond SB_CAP
-  {
-    TimedLaunch tl(ctx, "scatter", 56.0 * n);
-    if (n) hipLaunchKernelGGL(k_sb_hist<E>, dim3(n_tiles), dim3(SB_THREADS), 0, st, src, n, sm, n_sb, hist);
-    else SG_HIP(hipMemsetAsync(hist, 0, nh * 4, st));
-    exclusive_scan_u32(ctx, hist, toff, (uint32_t)nh);
-    if (n)
-      hipLaunchKernelGGL(k_sb_scatter<E>, dim3(n_tiles), dim3(SBS_THREADS), 0, st, src, n, sm, n_sb, toff, rd, rt,
-                         rk, ri);
-  }
-  {
-    TimedLaunch tl(ctx, "sort_small", 48.0 * n + 4.0 * n_slots);
-    hipLaunchKernelGGL(k_sb_sort<E::KK>, dim3(n_sb), dim3(SBT_THREADS), 0, st, sm, n_slots, toff, n_tiles, rd, rt,
-                       rk, ri, kt, kk, ki, offsets, order, big_list, big_count, spill);
+  if (region) {
+    uint32_t* ctl = ctx->sb_ctl + (size_t)ctx->sb_parity * SB_CTL_STRIDE;
+    uint32_t* ctl_next = ctx->sb_ctl + (size_t)(ctx->sb_parity ^ 1) * SB_CTL_STRIDE;
+    ctx->sb_parity ^= 1;
+    {
+      TimedLaunch tl(ctx, "scatter", 32.0 * n);
+      hipLaunchKernelGGL((k_sb_scatter<E, true>), dim3(n_tiles), dim3(SBS_THREADS), 0, st, src, n, sm, n_sb, nullptr,
+                         ctl, reg, rd, rt, rk, ri);
+    }
+    {
+      TimedLaunch tl(ctx, "sort_small", 24.0 * n + 4.0 * n_slots);
+      hipLaunchKernelGGL(k_sb_sort_region<E::KK>, dim3(n_sb), dim3(SBT_THREADS), 0, st, sm, n_slots, n_sb, ctl,
+                         ctl_next, reg, rd, rt, rk, ri, kt, kk, ki, offsets, order, big_list, big_count, spill,
+                         ctx->round_ret);
+    }
+  } else {
+    const size_t nh = (size_t)n_sb * n_tiles;
+    uint32_t* hist = ctx->d_cnt.get<uint32_t>(nh + 1);
+    uint32_t* toff = ctx->d_scan.get<uint32_t>(nh + 1);
+    {
+      TimedLaunch tl(ctx, "scatter", 56.0 * n);
+      if (n) hipLaunchKernelGGL(k_sb_hist<E>, dim3(n_tiles), dim3(SB_THREADS), 0, st, src, n, sm, n_sb, hist);
+      else SG_HIP(hipMemsetAsync(hist, 0, nh * 4, st));
+      exclusive_scan_u32(ctx, hist, toff, (uint32_t)nh);
+      if (n)
+        hipLaunchKernelGGL((k_sb_scatter<E, false>), dim3(n_tiles), dim3(SBS_THREADS), 0, st, src, n, sm, n_sb, toff,
+                           nullptr, 0u, rd, rt, rk, ri);
+    }
+    {
+      TimedLaunch tl(ctx, "sort_small", 48.0 * n + 4.0 * n_slots);
+      hipLaunchKernelGGL(k_sb_sort<E::KK>, dim3(n_sb), dim3(SBT_THREADS), 0, st, sm, n_slots, toff, n_tiles, rd, rt,
+                         rk, ri, kt, kk, ki, offsets, order, big_list, big_count, spill);
+    }
   }
   uint64_t* kt2 = ctx->d_keys2.get<uint64_t>(n);  // rd/rt are free again
   uint64_t* kk2 = ctx->d_keys3.get<uint64_t>(n);
@@ -823,6 +923,7 @@ static void bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
                        offsets, big_list, big_count, kt, kk, ki, kt2, kk2, ki2, order);
   }
   SG_CHECK_LAUNCH();
+  return region;
 }
 
 struct RoundWork {
@@ -890,7 +991,10 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
     // per packet: 20 B in, 12 B (8 B packed) path gather, 4 B dst map, 21 B out (status, time, id),
     // 4 B dst scratch; per host: 8 B segment, 4 B route, 32+32 B RNG, 8+8 B event counter
     TimedLaunch tl(ctx, "walk", (tab->path_key ? 57.0 : 61.0) * P + 92.0 * H);
-    hipLaunchKernelGGL(k_walk, dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
+    if (a.tab_key)
+      hipLaunchKernelGGL(k_walk<true>, dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
+    else
+      hipLaunchKernelGGL(k_walk<false>, dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
   }
   hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(1024), 0, st, a.blk_stats, walk_blocks, ctx->round_err,
                      w.big_count, ctx->round_ret);
@@ -919,9 +1023,14 @@ static void deliver_round(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const 
                           const sg_packets* pk, sg_deliveries* out, sg_round_stats* stats) {
   const uint32_t P = pk->n_packets, H = hs->n;
   RoundWork w = source_phase(ctx, hs, tab, rd, pk, out->status, out->deliver_time_ns, out->event_id, false);
-  bucket_sort(ctx, PacketEntries{w.dst_host, out->deliver_time_ns}, P, H, out->dst_offsets, out->dst_order,
-              w.big_count);
+  const PacketEntries E{w.dst_host, out->deliver_time_ns};
+  const bool region = bucket_sort(ctx, E, P, H, out->dst_offsets, out->dst_order, w.big_count, true);
   finish(ctx, w, stats);
+  if (region && ctx->round_ret->overflow) {  // a hot destination overfilled its region
+    SG_HIP(hipMemsetAsync(w.big_count, 0, 4, ctx->stream));
+    bucket_sort(ctx, E, P, H, out->dst_offsets, out->dst_order, w.big_count, false);
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  }
 }
 
 static void deliver_source(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const sg_round* rd,
@@ -958,10 +1067,17 @@ static void deliver_bucket(sg_ctx* ctx, const sg_record* recv, uint32_t n, const
   uint32_t* big_count = ws;
   uint32_t* err = ws + 1;
   SG_HIP(hipMemsetAsync(ws, 0, 8 * 4, st));
-  bucket_sort(ctx, RecordEntries{recv, local, H, err}, n, n_local, offsets, order, big_count);
+  const RecordEntries E{recv, local, H, err};
+  const bool region = bucket_sort(ctx, E, n, n_local, offsets, order, big_count, true);
   uint32_t h_err = 0;
   copy_to_host(ctx, &h_err, err, 4);
   fail_flags(h_err);
+  if (region && ctx->round_ret->overflow) {  // a hot destination overfilled its region
+    SG_HIP(hipMemsetAsync(ws, 0, 8 * 4, st));
+    bucket_sort(ctx, E, n, n_local, offsets, order, big_count, false);
+    copy_to_host(ctx, &h_err, err, 4);
+    fail_flags(h_err);
+  }
 }
 
 // Path-key table: (lat << 32) | bits(loss) per cell, so the walk's path gather

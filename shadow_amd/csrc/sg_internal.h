@@ -77,7 +77,7 @@ struct KernelTimer {
 struct sg_round_ret {
   unsigned long long stats[3];  // n_delivered, min deliver time, min used latency
   uint32_t err;
-  uint32_t pad;
+  uint32_t overflow;  // a bucketing region overflowed: the scan path must run
 };
 
 struct sg_ctx {
@@ -100,6 +100,10 @@ struct sg_ctx {
   // the round's stats and error flags straight from that kernel: no copies.
   uint32_t* round_err = nullptr;
   sg_round_ret* round_ret = nullptr;
+  // Region bucketing counters, two parities of [SB_MAX counts + overflow flag]
+  // (zeroed at creation; each call's sort kernel clears the other parity).
+  uint32_t* sb_ctl = nullptr;
+  uint32_t sb_parity = 0;
   // kernel timers (off unless sg_ctx_enable_timers)
   bool timing = false;
   bool count_work = false;  // SG_TIMERS_COUNT_WORK
@@ -134,6 +138,9 @@ int32_t guarded(sg_ctx* ctx, F&& fn) {
     return SG_ERR_DEVICE;
   }
 }
+
+// Region bucketing counters per parity: SB_MAX (4096) super-bucket counts + an overflow flag.
+constexpr uint32_t SB_CTL_STRIDE = 4097;
 
 inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 1u << 20) {
   size_t g = (n + block - 1) / block;

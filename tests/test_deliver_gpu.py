@@ -136,6 +136,23 @@ def test_hot_destination_big_buckets(oracle, ctx):
     _assert_same(want, got, ost, gst)
     want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk2, end, 2**63, 0)
     _assert_same(want, got, ost, gst)
+    # a big slot (k_sort_big) whose super-bucket still fits its region (no fallback)
+    pk3 = synth.make_packets(200000, hosts, start, end, seed=7, hot_dst=13, p_hot=0.0025)
+    want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk3, end, 2**63, 0)
+    assert 100 < np.diff(want["dst_offsets"]).max() < 2000
+    _assert_same(want, got, ost, gst)
+
+
+@pytest.mark.parametrize("hot", [False, True])
+def test_scan_path_bucketing(oracle, ctx, monkeypatch, hot):
+    """SG_BUCKET_REGION=0 forces the histogram + scan bucketing path (the
+    region path's fallback) for every round."""
+    monkeypatch.setenv("SG_BUCKET_REGION", "0")
+    lat, loss, hosts = _world(n_hosts=3000, seed=3)
+    start, end = T0 + 2 * 10**9, T0 + 2 * 10**9 + 10**6
+    pk = synth.make_packets(100000, hosts, start, end, seed=8, hot_dst=14 if hot else -1, p_hot=0.1 if hot else 0.0)
+    want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, end, 2**63, 0)
+    _assert_same(want, got, ost, gst)
 
 
 def test_equal_times_order_by_source(oracle, ctx):
