@@ -710,7 +710,45 @@ __global__ void __launch_bounds__(SBS_THREADS)
 
 // Placement of a super-bucket's entries by slot, then per-slot order by (t, kk).
 // Without KK the order key is the value (ri) itself.
-template <bool LDS, bool KK>
+constexpr uint32_t pow2_ceil(uint32_t x) { return x <= 1 ? 1 : 2 * pow2_ceil((x + 1) / 2); }
+static_assert(pow2_ceil(3072) == 4096 && pow2_ceil(4096) == 4096 && pow2_ceil(33) == 64, "pow2_ceil");
+
+// Block-wide bitonic sort of one slot's m entries [b, b + m) of the LDS
+// arrays by (t, key), through an index array (idx, >= next pow2 of m
+// entries); writes the values in order to out[0..m).
+template <bool KK>
+__device__ __forceinline__ void slot_bitonic(const uint64_t* Tt, const uint64_t* Tk, const uint32_t* Ti,
+                                             uint16_t* idx, uint32_t b, uint32_t m, uint32_t* __restrict__ out) {
+  constexpr uint16_t PAD = 0xFFFF;  // sorts last
+  uint32_t M = 1;
+  while (M < m) M <<= 1;
+  for (uint32_t i = threadIdx.x; i < M; i += SBT_THREADS) idx[i] = i < m ? (uint16_t)(b + i) : PAD;
+  __syncthreads();
+  for (uint32_t k = 2; k <= M; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < M; i += SBT_THREADS) {
+        const uint32_t l = i ^ j;
+        if (l <= i) continue;
+        const uint16_t x = idx[i], y = idx[l];
+        // y < x ?
+        const bool y_lt_x = x == PAD ? y != PAD
+                          : y == PAD ? false
+                                     : key_less(Tt[y], KK ? Tk[y] : (uint64_t)Ti[y], Tt[x], KK ? Tk[x] : (uint64_t)Ti[x]);
+        if (y_lt_x == ((i & k) == 0)) {
+          idx[i] = y;
+          idx[l] = x;
+        }
+      }
+      __syncthreads();
+    }
+  for (uint32_t r = threadIdx.x; r < m; r += SBT_THREADS) out[r] = Ti[idx[r]];
+  __syncthreads();
+}
+
+// INBLOCK (LDS only): slots above SMALL_BUCKET are bitonic-sorted by this
+// block too, instead of going to k_sort_big (the region path: a super-bucket
+// always fits LDS there, and no k_sort_big launch is needed).
+template <bool LDS, bool KK, bool INBLOCK = false>
 __device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32_t* Ti, uint16_t* Ts, uint32_t in0,
                                               uint32_t s0, uint32_t s1, uint32_t d0, uint32_t nd, const uint32_t* cnt,
                                               uint32_t* cur, const uint32_t* __restrict__ rd,
@@ -719,6 +757,11 @@ __device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32
                                               uint64_t* __restrict__ kk, uint32_t* __restrict__ ki,
                                               uint32_t* __restrict__ order, uint32_t* __restrict__ big_list,
                                               uint32_t* __restrict__ big_count) {
+  static_assert(LDS || !INBLOCK, "in-block big-slot sort needs the LDS copy");
+  constexpr uint32_t MAX_BIG = SB_CAP<KK> / (SMALL_BUCKET + 1) + 1;
+  __shared__ uint32_t n_big;
+  __shared__ uint16_t bigs[INBLOCK ? MAX_BIG : 1];
+  if (INBLOCK && threadIdx.x == 0) n_big = 0;
   for (uint32_t e = in0 + threadIdx.x; e < in0 + (s1 - s0); e += SBT_THREADS) {
     const uint32_t j = rd[e] - d0;
     const uint32_t p = atomicAdd(&cur[j], 1u);
@@ -733,6 +776,10 @@ __device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32
   for (uint32_t j = threadIdx.x; j < nd; j += SBT_THREADS) {
     const uint32_t b = cnt[j], e = cnt[j + 1];
     if (e - b > (uint32_t)SMALL_BUCKET) {
+      if (INBLOCK) {
+        bigs[atomicAdd(&n_big, 1u)] = (uint16_t)j;
+        continue;
+      }
       big_list[atomicAdd(big_count, 1u)] = d0 + j;
       if (LDS)
         for (uint32_t p = b; p < e; p++) {  // k_sort_big works on the global copy
@@ -754,12 +801,19 @@ __device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32
     for (uint32_t q = b; q < e; q++) rank += key_less(Tt[q], KK ? Tk[q] : (uint64_t)Ti[q], t, k);
     order[s0 + b + rank] = Ti[p];
   }
+  if (INBLOCK) {
+    __syncthreads();  // Ts is free: it becomes the index array
+    for (uint32_t u = 0; u < n_big; u++) {
+      const uint32_t j = bigs[u], b = cnt[j];
+      slot_bitonic<KK>(Tt, Tk, Ti, Ts, b, cnt[j + 1] - b, order + s0 + b);
+    }
+  }
 }
 
 // Block per super-bucket: its ns entries are at [in0, in0 + ns) of rd/rt/rk/ri
 // and take positions [s0, s0 + ns) of order[].  In LDS when they fit (SB_CAP),
 // else sorted in place in the global kt/kk/ki.
-template <bool KK>
+template <bool KK, bool INBLOCK>
 __device__ __forceinline__ void sb_sort_body(uint32_t sb, SbMap sm, uint32_t n_slots, uint32_t in0, uint32_t s0,
                                              uint32_t ns, const uint32_t* __restrict__ rd,
                                              const uint64_t* __restrict__ rt, const uint64_t* __restrict__ rk,
@@ -775,7 +829,7 @@ __device__ __forceinline__ void sb_sort_body(uint32_t sb, SbMap sm, uint32_t n_s
   __shared__ uint64_t st[CAP];
   __shared__ uint64_t sk[KK ? CAP : 1];
   __shared__ uint32_t si[CAP];
-  __shared__ uint16_t ss[CAP];
+  __shared__ uint16_t ss[INBLOCK ? pow2_ceil(CAP) : CAP];  // slot per entry, then the bitonic index array
   const uint32_t s1 = s0 + ns;
   const uint32_t d0 = sb * sm.spb, nd = min(sm.spb, n_slots - d0);
   const bool lds = ns <= (uint32_t)CAP;
@@ -793,9 +847,9 @@ __device__ __forceinline__ void sb_sort_body(uint32_t sb, SbMap sm, uint32_t n_s
   // LDS and global variants as separate inlined bodies: one generic pointer
   // would turn every access into a flat instruction waiting on both counters
   if (lds)
-    sb_place_sort<true, KK>(st, sk, si, ss, in0, s0, s1, d0, nd, cnt, cur, rd, rt, rk, ri, kt, kk, ki, order,
-                            big_list, big_count);
-  else
+    sb_place_sort<true, KK, INBLOCK>(st, sk, si, ss, in0, s0, s1, d0, nd, cnt, cur, rd, rt, rk, ri, kt, kk, ki,
+                                     order, big_list, big_count);
+  else if (!INBLOCK)
     sb_place_sort<false, KK>(kt + s0, kk + s0, ki + s0, slot_spill + s0, in0, s0, s1, d0, nd, cnt, cur, rd, rt, rk,
                              ri, kt, kk, ki, order, big_list, big_count);
 }
@@ -810,7 +864,7 @@ __global__ void __launch_bounds__(SBT_THREADS)
               uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count, uint16_t* __restrict__ slot_spill) {
   const uint32_t sb = blockIdx.x;
   const uint32_t s0 = tile_off[(size_t)sb * n_tiles], s1 = tile_off[(size_t)(sb + 1) * n_tiles];
-  sb_sort_body<KK>(sb, sm, n_slots, s0, s0, s1 - s0, rd, rt, rk, ri, kt, kk, ki, offsets, order, big_list, big_count,
+  sb_sort_body<KK, false>(sb, sm, n_slots, s0, s0, s1 - s0, rd, rt, rk, ri, kt, kk, ki, offsets, order, big_list, big_count,
                    slot_spill);
 }
 
@@ -840,7 +894,7 @@ __global__ void __launch_bounds__(SBT_THREADS)
   __syncthreads();
   uint32_t s0 = 0;
   for (int w = 0; w < SBT_THREADS / 64; w++) s0 += part[w];
-  sb_sort_body<KK>(sb, sm, n_slots, sb * region, s0, ctl[sb], rd, rt, rk, ri, kt, kk, ki, offsets, order, big_list,
+  sb_sort_body<KK, true>(sb, sm, n_slots, sb * region, s0, ctl[sb], rd, rt, rk, ri, kt, kk, ki, offsets, order, big_list,
                    big_count, slot_spill);
 }
 
@@ -913,6 +967,10 @@ static bool bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
       hipLaunchKernelGGL(k_sb_sort<E::KK>, dim3(n_sb), dim3(SBT_THREADS), 0, st, sm, n_slots, toff, n_tiles, rd, rt,
                          rk, ri, kt, kk, ki, offsets, order, big_list, big_count, spill);
     }
+  }
+  if (region) {  // big slots were sorted in-block
+    SG_CHECK_LAUNCH();
+    return true;
   }
   uint64_t* kt2 = ctx->d_keys2.get<uint64_t>(n);  // rd/rt are free again
   uint64_t* kk2 = ctx->d_keys3.get<uint64_t>(n);

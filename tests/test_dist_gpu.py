@@ -27,7 +27,7 @@ def _world(oracle, n_nodes=90, n_hosts=1500, seed=3):
     return lat, loss, hosts
 
 
-def _run(oracle, ctx, W, n_packets, hot=None, seed=1):
+def _run(oracle, ctx, W, n_packets, hot=None, seed=1, p_hot=0.1):
     import torch
 
     lat, loss, hosts = _world(oracle, seed=seed)
@@ -35,7 +35,7 @@ def _run(oracle, ctx, W, n_packets, hot=None, seed=1):
     part = HostPartition(hosts["route"], nu, W)
     start, end = T0 + 10**9, T0 + 10**9 + 10**6
     pk = synth.make_packets(n_packets, hosts, start, end, seed=seed + 10, p_unknown_dst=0.01,
-                            hot_dst=-1 if hot is None else hot, p_hot=0.0 if hot is None else 0.1)
+                            hot_dst=-1 if hot is None else hot, p_hot=0.0 if hot is None else p_hot)
     owner_of_pkt = part.owner[pk["src"]]
     ranks = []
     for r in range(W):
@@ -104,5 +104,9 @@ def test_sharded_round_matches_single(oracle, ctx, W):
     assert want["delivered"] > 0
 
 
-def test_sharded_hot_destination(oracle, ctx):
-    _run(oracle, ctx, 4, 120000, hot=17, seed=5)
+@pytest.mark.parametrize("p_hot", [0.1, 0.01])
+def test_sharded_hot_destination(oracle, ctx, p_hot):
+    # 0.1: the hot slot overfills its region (scan-path fallback); 0.01: a big
+    # slot sorted inside the region path's block
+    want = _run(oracle, ctx, 4, 120000, hot=17, seed=5, p_hot=p_hot)
+    assert np.diff(want["dst_offsets"]).max() > 100
