@@ -35,11 +35,12 @@ struct sg_hosts {
   uint32_t* route = nullptr;  // host -> routing-table index
   uint64_t* rng = nullptr;    // SoA [4][n]
   uint64_t* ctr = nullptr;    // n
-  // address -> host: dense window or sorted table
+  // address -> (host, routing index): dense window or sorted table (the pair
+  // in one 8-byte entry, so resolving a destination is one dependent load)
   uint32_t ip_base = 0, dense_span = 0;
-  uint32_t* dense = nullptr;
+  uint2* dense = nullptr;
   uint32_t* sorted_ip = nullptr;
-  uint32_t* sorted_host = nullptr;
+  uint2* sorted_host = nullptr;
   uint32_t max_route = 0;  // largest routing-table index of any host
   ~sg_hosts() {
     void* ps[] = {route, rng, ctr, dense, sorted_ip, sorted_host};
@@ -59,14 +60,14 @@ enum : uint32_t { ERR_UNSORTED = 1, ERR_SRC_RANGE = 2, ERR_ROUTE_RANGE = 4, ERR_
 
 struct HostMap {
   uint32_t ip_base, dense_span, n_sorted;
-  const uint32_t* dense;
+  const uint2* dense;
   const uint32_t* sorted_ip;
-  const uint32_t* sorted_host;
-  // Dns::addr_to_host_id (dns.rs:174-176)
-  __device__ __forceinline__ uint32_t resolve(uint32_t ip) const {
+  const uint2* sorted_host;
+  // Dns::addr_to_host_id (dns.rs:174-176): (host, its routing index), host = NONE if unknown
+  __device__ __forceinline__ uint2 resolve(uint32_t ip) const {
     if (dense) {
       uint32_t off = ip - ip_base;
-      return off < dense_span ? dense[off] : NONE;
+      return off < dense_span ? dense[off] : make_uint2(NONE, 0);
     }
     uint32_t lo = 0, hi = n_sorted;
     while (lo < hi) {
@@ -76,7 +77,7 @@ struct HostMap {
       else
         hi = mid;
     }
-    return (lo < n_sorted && sorted_ip[lo] == ip) ? sorted_host[lo] : NONE;
+    return (lo < n_sorted && sorted_ip[lo] == ip) ? sorted_host[lo] : make_uint2(NONE, 0);
   }
 };
 
@@ -169,20 +170,19 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
   uint32_t hb = 0, he = 0;
   Xoshiro x{0, 0, 0, 0};
   uint64_t c = 0;
-  if (walker) {
+  if (walker) {  // the stream state loads issue beside the offsets (off the dependent chain)
     hb = min(a.host_off[h], a.P);
     he = max(min(a.host_off[h + 1], a.P), hb);
-    if (hb < he) {
-      x = Xoshiro{a.rng[h], a.rng[(size_t)a.H + h], a.rng[2 * (size_t)a.H + h], a.rng[3 * (size_t)a.H + h]};
-      c = a.ctr[h];
-    }
+    x = Xoshiro{a.rng[h], a.rng[(size_t)a.H + h], a.rng[2 * (size_t)a.H + h], a.rng[3 * (size_t)a.H + h]};
+    c = a.ctr[h];
   }
   unsigned long long nd = 0, mind = ~0ull, minl = ~0ull;
   for (uint32_t c0 = p0; c0 < p1; c0 += WALK_CHUNK) {
     const uint32_t c1 = min(c0 + WALK_CHUNK, p1);
     // 1. packet-parallel gather, PPT packets per thread batched level by level
-    //    (inputs; address map and route rows; destination route; path cell),
-    //    so a thread has at most four dependent round trips per chunk
+    //    (inputs; address map -> (destination, its route column) and the
+    //    source's route row; path cell), so a thread has three dependent round
+    //    trips per chunk
     constexpr int PPT = WALK_CHUNK / WALK_THREADS;
     uint64_t now[PPT];
     uint32_t ip[PPT], sh[PPT], d[PPT], r[PPT];
@@ -198,7 +198,9 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
 #pragma unroll
     for (int q = 0; q < PPT; q++) {
       if (now[q] < a.bootstrap_end) f[q] |= W_BOOT;
-      d[q] = now[q] < a.sim_end ? a.map.resolve(ip[q]) : NONE;  // worker.rs:332-335, 341
+      const uint2 hr = now[q] < a.sim_end ? a.map.resolve(ip[q]) : make_uint2(NONE, 0);  // worker.rs:332-335, 341
+      d[q] = hr.x;
+      ip[q] = hr.y;  // reuse: the destination's route column
       r[q] = a.route[sh[q]];
     }
 #pragma unroll
@@ -210,7 +212,6 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
         f[q] |= W_NO_DST;
         d[q] = NONE;
       }
-      ip[q] = d[q] != NONE ? a.route[d[q]] : 0;  // reuse: the destination's route column
     }
 #pragma unroll
     for (int q = 0; q < PPT; q++) {
@@ -1209,21 +1210,22 @@ int32_t sg_hosts_create(sg_ctx* ctx, uint32_t n_hosts, const uint32_t* host_ipv4
       if (span <= 4 * (uint64_t)n + 4096) {
         hs->ip_base = ips.front().first;
         hs->dense_span = (uint32_t)span;
-        std::vector<uint32_t> dense(span, NONE);
-        for (auto& p : ips) dense[p.first - hs->ip_base] = p.second;
-        SG_HIP(hipMalloc(&hs->dense, span * 4));
-        SG_HIP(hipMemcpyAsync(hs->dense, dense.data(), span * 4, hipMemcpyHostToDevice, st));
+        std::vector<uint2> dense(span, make_uint2(NONE, 0));
+        for (auto& p : ips) dense[p.first - hs->ip_base] = make_uint2(p.second, host_route_idx[p.second]);
+        SG_HIP(hipMalloc(&hs->dense, span * 8));
+        SG_HIP(hipMemcpyAsync(hs->dense, dense.data(), span * 8, hipMemcpyHostToDevice, st));
         SG_HIP(hipStreamSynchronize(st));
       } else {
-        std::vector<uint32_t> a(n), b(n);
+        std::vector<uint32_t> a(n);
+        std::vector<uint2> b(n);
         for (size_t k = 0; k < n; k++) {
           a[k] = ips[k].first;
-          b[k] = ips[k].second;
+          b[k] = make_uint2(ips[k].second, host_route_idx[ips[k].second]);
         }
         SG_HIP(hipMalloc(&hs->sorted_ip, n * 4));
-        SG_HIP(hipMalloc(&hs->sorted_host, n * 4));
+        SG_HIP(hipMalloc(&hs->sorted_host, n * 8));
         SG_HIP(hipMemcpyAsync(hs->sorted_ip, a.data(), n * 4, hipMemcpyHostToDevice, st));
-        SG_HIP(hipMemcpyAsync(hs->sorted_host, b.data(), n * 4, hipMemcpyHostToDevice, st));
+        SG_HIP(hipMemcpyAsync(hs->sorted_host, b.data(), n * 8, hipMemcpyHostToDevice, st));
         SG_HIP(hipStreamSynchronize(st));
       }
     }
