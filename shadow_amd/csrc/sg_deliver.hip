@@ -654,13 +654,21 @@ __global__ void __launch_bounds__(SBS_THREADS)
   for (uint32_t i = threadIdx.x; i < n_sb; i += SBS_THREADS) lcur[i] = 0;
   __syncthreads();
   const uint32_t e0 = blockIdx.x * SB_TILE, e1 = min(e0 + SB_TILE, n);
-  uint32_t d[PER];
+  // every load of the tile up front (one round trip): slot, time, key, value
+  uint32_t d[PER], vi[PER];
+  uint64_t vt[PER], vk[PER];
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t e = e0 + threadIdx.x + k * SBS_THREADS;
-    d[k] = e < e1 ? src.slot(e) : NONE;
-    if (d[k] != NONE) atomicAdd(&lcur[sm.of(d[k])], 1u);
+    d[k] = NONE;
+    if (e < e1) {
+      d[k] = src.slot(e);
+      src.get(e, vt[k], vk[k], vi[k]);
+    }
   }
+#pragma unroll
+  for (int k = 0; k < PER; k++)
+    if (d[k] != NONE) atomicAdd(&lcur[sm.of(d[k])], 1u);
   __syncthreads();
   const uint32_t total = block_exclusive_scan<SBS_THREADS, SB_MAX / SBS_THREADS>(lcur, n_sb, wsum);
   for (uint32_t i = threadIdx.x; i < n_sb; i += SBS_THREADS) {
@@ -686,15 +694,11 @@ __global__ void __launch_bounds__(SBS_THREADS)
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     if (d[k] == NONE) continue;
-    const uint32_t e = e0 + threadIdx.x + k * SBS_THREADS;
     const uint32_t p = atomicAdd(&lcur[sm.of(d[k])], 1u);
-    uint64_t tt, kk;
-    uint32_t ki;
-    src.get(e, tt, kk, ki);
     sd[p] = d[k];
-    st_[p] = tt;
-    si[p] = ki;
-    if (E::KK) sk[p] = kk;
+    st_[p] = vt[k];
+    si[p] = vi[k];
+    if (E::KK) sk[p] = vk[k];
   }
   __syncthreads();
   for (uint32_t p = threadIdx.x; p < total; p += SBS_THREADS) {
@@ -746,34 +750,23 @@ __device__ __forceinline__ void slot_bitonic(const uint64_t* Tt, const uint64_t*
   __syncthreads();
 }
 
-// INBLOCK (LDS only): slots above SMALL_BUCKET are bitonic-sorted by this
-// block too, instead of going to k_sort_big (the region path: a super-bucket
-// always fits LDS there, and no k_sort_big launch is needed).
-template <bool LDS, bool KK, bool INBLOCK = false>
-__device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32_t* Ti, uint16_t* Ts, uint32_t in0,
-                                              uint32_t s0, uint32_t s1, uint32_t d0, uint32_t nd, const uint32_t* cnt,
-                                              uint32_t* cur, const uint32_t* __restrict__ rd,
-                                              const uint64_t* __restrict__ rt, const uint64_t* __restrict__ rk,
-                                              const uint32_t* __restrict__ ri, uint64_t* __restrict__ kt,
-                                              uint64_t* __restrict__ kk, uint32_t* __restrict__ ki,
-                                              uint32_t* __restrict__ order, uint32_t* __restrict__ big_list,
-                                              uint32_t* __restrict__ big_count) {
+// Per-slot order of a placed super-bucket (slot j = entries [cnt[j], cnt[j+1])
+// of Tt/Tk/Ti, Ts = slot per entry): rank sort of small slots; slots above
+// SMALL_BUCKET go to k_sort_big (copied to the global kt/kk/ki when placed in
+// LDS) or, INBLOCK (LDS only), are bitonic-sorted by this block -- the region
+// path, where a super-bucket always fits LDS and no k_sort_big launch is needed.
+template <bool LDS, bool KK, bool INBLOCK>
+__device__ __forceinline__ void slot_orders(uint64_t* Tt, uint64_t* Tk, uint32_t* Ti, uint16_t* Ts, uint32_t s0,
+                                            uint32_t ns, uint32_t d0, uint32_t nd, const uint32_t* cnt,
+                                            uint64_t* __restrict__ kt, uint64_t* __restrict__ kk,
+                                            uint32_t* __restrict__ ki, uint32_t* __restrict__ order,
+                                            uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
   static_assert(LDS || !INBLOCK, "in-block big-slot sort needs the LDS copy");
   constexpr uint32_t MAX_BIG = SB_CAP<KK> / (SMALL_BUCKET + 1) + 1;
   __shared__ uint32_t n_big;
   __shared__ uint16_t bigs[INBLOCK ? MAX_BIG : 1];
   if (INBLOCK && threadIdx.x == 0) n_big = 0;
-  for (uint32_t e = in0 + threadIdx.x; e < in0 + (s1 - s0); e += SBT_THREADS) {
-    const uint32_t j = rd[e] - d0;
-    const uint32_t p = atomicAdd(&cur[j], 1u);
-    Tt[p] = rt[e];
-    const uint32_t v = ri[e];
-    if (KK) Tk[p] = rk[e];
-    else if (!LDS) Tk[p] = v;  // k_sort_big reads the global key
-    Ti[p] = v;
-    Ts[p] = (uint16_t)j;
-  }
-  __syncthreads();
+  __syncthreads();  // placement complete
   for (uint32_t j = threadIdx.x; j < nd; j += SBT_THREADS) {
     const uint32_t b = cnt[j], e = cnt[j + 1];
     if (e - b > (uint32_t)SMALL_BUCKET) {
@@ -793,10 +786,10 @@ __device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32
   // Rank sort inside each small slot: entry p goes to slot start + #(entries of
   // its slot with a smaller (t, kk)); (t, kk) is unique per entry.  One thread
   // per entry, independent LDS reads -- no serial insertion chain.
-  for (uint32_t p = threadIdx.x; p < s1 - s0; p += SBT_THREADS) {
+  for (uint32_t p = threadIdx.x; p < ns; p += SBT_THREADS) {
     const uint32_t j = Ts[p];
     const uint32_t b = cnt[j], e = cnt[j + 1];
-    if (e - b > (uint32_t)SMALL_BUCKET) continue;  // k_sort_big writes this slot
+    if (e - b > (uint32_t)SMALL_BUCKET) continue;  // sorted below / by k_sort_big
     const uint64_t t = Tt[p], k = KK ? Tk[p] : (uint64_t)Ti[p];
     uint32_t rank = 0;
     for (uint32_t q = b; q < e; q++) rank += key_less(Tt[q], KK ? Tk[q] : (uint64_t)Ti[q], t, k);
@@ -811,10 +804,34 @@ __device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32
   }
 }
 
+// Placement of a super-bucket's entries by slot (from the global run arrays at
+// in0), then slot_orders.  Without KK the order key is the value (ri) itself.
+template <bool LDS, bool KK>
+__device__ __forceinline__ void sb_place_sort(uint64_t* Tt, uint64_t* Tk, uint32_t* Ti, uint16_t* Ts, uint32_t in0,
+                                              uint32_t s0, uint32_t s1, uint32_t d0, uint32_t nd, const uint32_t* cnt,
+                                              uint32_t* cur, const uint32_t* __restrict__ rd,
+                                              const uint64_t* __restrict__ rt, const uint64_t* __restrict__ rk,
+                                              const uint32_t* __restrict__ ri, uint64_t* __restrict__ kt,
+                                              uint64_t* __restrict__ kk, uint32_t* __restrict__ ki,
+                                              uint32_t* __restrict__ order, uint32_t* __restrict__ big_list,
+                                              uint32_t* __restrict__ big_count) {
+  for (uint32_t e = in0 + threadIdx.x; e < in0 + (s1 - s0); e += SBT_THREADS) {
+    const uint32_t j = rd[e] - d0;
+    const uint32_t p = atomicAdd(&cur[j], 1u);
+    Tt[p] = rt[e];
+    const uint32_t v = ri[e];
+    if (KK) Tk[p] = rk[e];
+    else if (!LDS) Tk[p] = v;  // k_sort_big reads the global key
+    Ti[p] = v;
+    Ts[p] = (uint16_t)j;
+  }
+  slot_orders<LDS, KK, false>(Tt, Tk, Ti, Ts, s0, s1 - s0, d0, nd, cnt, kt, kk, ki, order, big_list, big_count);
+}
+
 // Block per super-bucket: its ns entries are at [in0, in0 + ns) of rd/rt/rk/ri
 // and take positions [s0, s0 + ns) of order[].  In LDS when they fit (SB_CAP),
 // else sorted in place in the global kt/kk/ki.
-template <bool KK, bool INBLOCK>
+template <bool KK>
 __device__ __forceinline__ void sb_sort_body(uint32_t sb, SbMap sm, uint32_t n_slots, uint32_t in0, uint32_t s0,
                                              uint32_t ns, const uint32_t* __restrict__ rd,
                                              const uint64_t* __restrict__ rt, const uint64_t* __restrict__ rk,
@@ -830,7 +847,7 @@ __device__ __forceinline__ void sb_sort_body(uint32_t sb, SbMap sm, uint32_t n_s
   __shared__ uint64_t st[CAP];
   __shared__ uint64_t sk[KK ? CAP : 1];
   __shared__ uint32_t si[CAP];
-  __shared__ uint16_t ss[INBLOCK ? pow2_ceil(CAP) : CAP];  // slot per entry, then the bitonic index array
+  __shared__ uint16_t ss[CAP];
   const uint32_t s1 = s0 + ns;
   const uint32_t d0 = sb * sm.spb, nd = min(sm.spb, n_slots - d0);
   const bool lds = ns <= (uint32_t)CAP;
@@ -848,9 +865,9 @@ __device__ __forceinline__ void sb_sort_body(uint32_t sb, SbMap sm, uint32_t n_s
   // LDS and global variants as separate inlined bodies: one generic pointer
   // would turn every access into a flat instruction waiting on both counters
   if (lds)
-    sb_place_sort<true, KK, INBLOCK>(st, sk, si, ss, in0, s0, s1, d0, nd, cnt, cur, rd, rt, rk, ri, kt, kk, ki,
-                                     order, big_list, big_count);
-  else if (!INBLOCK)
+    sb_place_sort<true, KK>(st, sk, si, ss, in0, s0, s1, d0, nd, cnt, cur, rd, rt, rk, ri, kt, kk, ki, order,
+                            big_list, big_count);
+  else
     sb_place_sort<false, KK>(kt + s0, kk + s0, ki + s0, slot_spill + s0, in0, s0, s1, d0, nd, cnt, cur, rd, rt, rk,
                              ri, kt, kk, ki, order, big_list, big_count);
 }
@@ -865,7 +882,7 @@ __global__ void __launch_bounds__(SBT_THREADS)
               uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count, uint16_t* __restrict__ slot_spill) {
   const uint32_t sb = blockIdx.x;
   const uint32_t s0 = tile_off[(size_t)sb * n_tiles], s1 = tile_off[(size_t)(sb + 1) * n_tiles];
-  sb_sort_body<KK, false>(sb, sm, n_slots, s0, s0, s1 - s0, rd, rt, rk, ri, kt, kk, ki, offsets, order, big_list, big_count,
+  sb_sort_body<KK>(sb, sm, n_slots, s0, s0, s1 - s0, rd, rt, rk, ri, kt, kk, ki, offsets, order, big_list, big_count,
                    slot_spill);
 }
 
@@ -895,8 +912,53 @@ __global__ void __launch_bounds__(SBT_THREADS)
   __syncthreads();
   uint32_t s0 = 0;
   for (int w = 0; w < SBT_THREADS / 64; w++) s0 += part[w];
-  sb_sort_body<KK, true>(sb, sm, n_slots, sb * region, s0, ctl[sb], rd, rt, rk, ri, kt, kk, ki, offsets, order, big_list,
-                   big_count, slot_spill);
+  const uint32_t in0 = sb * region, ns = ctl[sb];  // ns <= region = SB_CAP (no overflow)
+  constexpr int CAP = SB_CAP<KK>;
+  constexpr int PER = (CAP + SBT_THREADS - 1) / SBT_THREADS;
+  __shared__ uint32_t cnt[SB_SLOTS_MAX + 1];
+  __shared__ uint32_t cur[SB_SLOTS_MAX];
+  __shared__ uint32_t wsum[SBT_THREADS / 64];
+  __shared__ uint64_t st[CAP];
+  __shared__ uint64_t sk[KK ? CAP : 1];
+  __shared__ uint32_t si[CAP];
+  __shared__ uint16_t ss[pow2_ceil(CAP)];  // slot per entry, then the bitonic index array
+  const uint32_t d0 = sb * sm.spb, nd = min(sm.spb, n_slots - d0);
+  // the super-bucket's entries into registers: one global round trip
+  uint32_t vd[PER], vi[PER];
+  uint64_t vt[PER], vk[PER];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t e = threadIdx.x + k * SBT_THREADS;
+    vd[k] = NONE;
+    if (e < ns) {
+      vd[k] = rd[in0 + e] - d0;
+      vt[k] = rt[in0 + e];
+      vi[k] = ri[in0 + e];
+      if (KK) vk[k] = rk[in0 + e];
+    }
+  }
+  for (uint32_t j = threadIdx.x; j <= nd; j += SBT_THREADS) cnt[j] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; k++)
+    if (vd[k] != NONE) atomicAdd(&cnt[vd[k]], 1u);
+  __syncthreads();
+  const uint32_t tot = block_exclusive_scan<SBT_THREADS, SB_SLOTS_MAX / SBT_THREADS>(cnt, nd, wsum);
+  for (uint32_t j = threadIdx.x; j < nd; j += SBT_THREADS) cur[j] = cnt[j];
+  if (threadIdx.x == 0) cnt[nd] = tot;
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < nd; j += SBT_THREADS) offsets[d0 + j] = s0 + cnt[j];
+  if (d0 + nd == n_slots && threadIdx.x == 0) offsets[n_slots] = s0 + ns;
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    if (vd[k] == NONE) continue;
+    const uint32_t p = atomicAdd(&cur[vd[k]], 1u);
+    st[p] = vt[k];
+    if (KK) sk[p] = vk[k];
+    si[p] = vi[k];
+    ss[p] = (uint16_t)vd[k];
+  }
+  slot_orders<true, KK, true>(st, sk, si, ss, s0, ns, d0, nd, cnt, kt, kk, ki, order, big_list, big_count);
 }
 
 // Bucket sort of n entries into n_slots destination slots (see above).
