@@ -7,15 +7,17 @@
 // pops events < end (host.rs:749-758), so no destination can observe a packet
 // of this round before the round ends.
 //
-// Pipeline (all on the context stream):
-//   k_seg_bounds   per packet: per-source-host segment [begin, end), order check
-//   k_walk         per source host: the host's packets in send order --
-//                  resolve dst (Dns::addr_to_host_id), path (latency, loss),
-//                  Xoshiro256++ f64 draw, drop test, arrival time, event id
-//   scan           per-destination counts -> dst_offsets
-//   k_scatter      delivered packets -> destination buckets (unordered)
-//   k_sort_small   thread per destination: order bucket by the EventQueue key
-//   k_sort_big     block per large bucket: LDS bitonic chunks + merge passes
+// Pipeline (all on the context stream, no fills or copies):
+//   k_host_off        per packet: host CSR host_off[h], grouping check
+//   k_walk            block per 64 source hosts: resolve dst (Dns::addr_to_host_id),
+//                     path cell, Xoshiro256++ f64 draw, drop test, arrival time,
+//                     event id -- the host's packets in send order
+//   k_reduce_stats    round minima + error flags -> pinned host-mapped block
+//   k_sb_scatter      delivered packets -> runs in fixed super-bucket regions
+//   k_sb_sort_region  block per super-bucket: dst_offsets, EventQueue order per
+//                     destination (rank sort; LDS bitonic for big ones)
+//   scan-path fallback (a hot destination overfills a region): k_sb_hist, scan,
+//   k_sb_scatter (exact positions), k_sb_sort, k_sort_big.
 // Event order (event.rs:84-155): (time, Packet < Local, src_host_id,
 // src_host_event_id).  Inside a bucket every element is a packet; since the
 // input is grouped by ascending source host in send order and event ids grow
