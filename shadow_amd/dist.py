@@ -129,8 +129,29 @@ def all_to_all_records(send, send_counts: List[int], dist, group=None):
     return recv[:n_recv], recv_counts
 
 
+def gather_round_stats(n_delivered: int, min_deliver: int, min_lat: int, dist, group=None, device="cuda"):
+    """Global round scalars (manager.rs:482 next-event minimum, worker.rs:372
+    lowest used latency, delivered count): one all-gather of every rank's three
+    u64 values (exact for u64; the no-delivery sentinel is UINT64_MAX)."""
+    import torch
+
+    mine = np.array([n_delivered, min_deliver, min_lat], dtype=np.uint64).view(np.int64)
+    t = torch.from_numpy(mine.copy()).to(device)
+    world = dist.get_world_size(group) if dist is not None else 1
+    out = torch.empty(3 * world, dtype=torch.int64, device=device)
+    if dist is None or world == 1:
+        out.copy_(t)
+    else:
+        dist.all_gather_into_tensor(out, t, group=group)
+    allv = out.cpu().numpy().view(np.uint64).reshape(world, 3)
+    return int(allv[:, 0].sum()), int(allv[:, 1].min()), int(allv[:, 2].min())
+
+
 class ShardedDelivery:
-    """One rank's side of a sharded delivery round (see module docstring)."""
+    """One rank's side of a sharded delivery round (see module docstring).
+
+    After round(), last_stats = (delivered, min deliver time, min used latency)
+    over all ranks (gather_round_stats)."""
 
     def __init__(self, ctx, hosts, table, partition: HostPartition, rank: int, world: int, dist=None, group=None,
                  source_fn: Optional[Callable] = None, bucket_fn: Optional[Callable] = None,
@@ -144,6 +165,8 @@ class ShardedDelivery:
 
         self.owner_dev = torch.from_numpy(partition.owner.view(np.int32)).to(device)
         self.local_dev = torch.from_numpy(partition.local.view(np.int32)).to(device)
+        self.device = device
+        self.last_stats = None
 
     def round(self, packets, round_end_ns: int, sim_end_ns: int, bootstrap_end_ns: int = 0):
         src = self.source_fn(self.ctx, self.hosts, self.table, packets, round_end_ns, sim_end_ns, bootstrap_end_ns,
@@ -151,4 +174,6 @@ class ShardedDelivery:
         recv, recv_counts = self.exchange_fn(src.send, src.send_counts)
         order, offsets = self.bucket_fn(self.ctx, recv, int(sum(recv_counts)), self.local_dev,
                                         len(self.part.local), self.part.n_local(self.rank))
+        self.last_stats = gather_round_stats(int(src.n_delivered), int(src.min_deliver_time_ns),
+                                             int(src.min_used_latency_ns), self.dist, self.group, self.device)
         return src, recv, recv_counts, order, offsets

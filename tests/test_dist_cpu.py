@@ -116,12 +116,12 @@ def _worker(rank, world, port, q):
         origin = np.repeat(np.arange(world), recv_counts)
         glob = np.array([sels[origin[k]][rec["packet"][k]] for k in range(len(rec))], np.int64)
         per_dst = {int(h): glob[order[offsets[s]:offsets[s + 1]]].tolist() for s, h in enumerate(part.hosts_of[rank])}
-        q.put((rank, rows_ok, per_dst, src.status.tolist(), sel.tolist()))
+        q.put((rank, rows_ok, per_dst, src.status.tolist(), sel.tolist(), sd.last_stats))
         dist.destroy_process_group()
     except Exception as e:  # surface worker failures to the parent
         import traceback
 
-        q.put((rank, "error", traceback.format_exc(), None, None))
+        q.put((rank, "error", traceback.format_exc(), None, None, None))
 
 
 def test_two_rank_gloo_exchange_matches_single_round(oracle):
@@ -143,8 +143,9 @@ def test_two_rank_gloo_exchange_matches_single_round(oracle):
     want = oracle.deliver_round(T0 + 10**6, 2**63, 0, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
                                 hosts["ip"], hosts["route"], lat, loss, rng, ctr)
     seen = set()
-    for rank, rows_ok, per_dst, status, sel in out:
+    for rank, rows_ok, per_dst, status, sel, stats in out:
         assert rows_ok
+        assert stats == (want["delivered"], want["min_deliver"], want["min_lat"])  # global round scalars
         assert np.array_equal(np.array(status, np.uint8), want["status"][np.array(sel, np.int64)])
         for h, got in per_dst.items():
             exp = want["dst_order"][want["dst_offsets"][h]:want["dst_offsets"][h + 1]].tolist()
