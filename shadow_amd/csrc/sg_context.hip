@@ -195,6 +195,7 @@ int32_t sg_ctx_create(int32_t device, sg_ctx** out) {
     SG_HIP(hipMalloc(&ctx->round_err, 16));
     SG_HIP(hipMemset(ctx->round_err, 0, 16));
     SG_HIP(hipHostMalloc(&ctx->round_ret, sizeof(sg_round_ret), hipHostMallocMapped | hipHostMallocCoherent));
+    SG_HIP(hipHostMalloc(&ctx->apsp_ret, 16, hipHostMallocMapped | hipHostMallocCoherent));
     SG_HIP(hipMalloc(&ctx->sb_ctl, 2 * sg::SB_CTL_STRIDE * 4));
     SG_HIP(hipMemset(ctx->sb_ctl, 0, 2 * sg::SB_CTL_STRIDE * 4));
     int cus = 0;
@@ -223,6 +224,7 @@ void sg_ctx_destroy(sg_ctx* ctx) {
   if (ctx->round_err) (void)hipFree(ctx->round_err);
   if (ctx->sb_ctl) (void)hipFree(ctx->sb_ctl);
   if (ctx->round_ret) (void)hipHostFree(ctx->round_ret);
+  if (ctx->apsp_ret) (void)hipHostFree(ctx->apsp_ret);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }

@@ -104,6 +104,9 @@ struct sg_ctx {
   // (zeroed at creation; each call's sort kernel clears the other parity).
   uint32_t* sb_ctl = nullptr;
   uint32_t sb_parity = 0;
+  // APSP: the active-batch count of the next pass, written by k_active_list
+  // into pinned host-mapped memory at each pass-chunk end
+  uint32_t* apsp_ret = nullptr;
   // kernel timers (off unless sg_ctx_enable_timers)
   bool timing = false;
   bool count_work = false;  // SG_TIMERS_COUNT_WORK

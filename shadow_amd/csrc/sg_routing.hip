@@ -179,9 +179,14 @@ __global__ void k_stamp_sources(uint32_t* __restrict__ stamp, uint32_t n, const 
 }
 
 // Active-batch list for the next pass: alist[0] = count, alist[1 + i] = the
-// i-th batch (ascending) whose flag is set.  One block.
+// i-th batch (ascending) whose flag is set.  One block.  Also zeroes the flag
+// slot the pass will set (`clear`, gb x FLAG_STRIDE words) and, if count_out
+// (pinned host-mapped) is given, reports the count there: no fill and no copy
+// per pass.
 __global__ void __launch_bounds__(1024) k_active_list(const uint32_t* __restrict__ flags, uint32_t gb,
-                                                      uint32_t* __restrict__ alist) {
+                                                      uint32_t* __restrict__ alist, uint32_t* __restrict__ clear,
+                                                      uint32_t* __restrict__ count_out) {
+  for (uint32_t i = threadIdx.x; i < gb * FLAG_STRIDE; i += 1024) clear[i] = 0;
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t base;
   if (threadIdx.x == 0) base = 0;
@@ -201,7 +206,10 @@ __global__ void __launch_bounds__(1024) k_active_list(const uint32_t* __restrict
       for (int i = 0; i < 16; i++) base += wsum[i];
     __syncthreads();
   }
-  if (threadIdx.x == 0) alist[0] = base;
+  if (threadIdx.x == 0) {
+    alist[0] = base;
+    if (count_out) *count_out = base;
+  }
 }
 
 // B = sources per batch (64: one row per wave instruction; 32: two rows, one
@@ -759,7 +767,7 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
   // chunk.  A pass issued after its batch converged finds it off the active list.
   const uint32_t chunk = (uint32_t)std::max(1, env_int("SG_APSP_PASS_CHUNK", 4));
   const bool trace = env_int("SG_APSP_TRACE", 0) != 0;  // per-pass diagnostics on stderr
-  std::vector<uint32_t> h_changed(fs), h_sat(group);
+  std::vector<uint32_t> h_sat(group);
   std::vector<uint32_t> wide_rows;
   for (uint32_t g0 = 0; g0 < n_batches; g0 += group) {
     const uint32_t gb = std::min(group, n_batches - g0);
@@ -780,15 +788,17 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
       SG_HIP(hipEventCreate(&te1));
     }
     double trace_prev = 0;
+    // the active list of pass p (from the flags of pass p - 1) is built by the
+    // pass before it, or at a chunk end, where its count also goes to the host
+    hipLaunchKernelGGL(k_active_list, dim3(1), dim3(1024), 0, st, ring[2], gb, alist, ring[0], nullptr);
     for (uint32_t pass = 0;;) {
-      uint32_t last = pass;
       for (uint32_t c = 0; c < chunk; c++, pass++) {
         if (pass > n + 2 + chunk) throw Error(SG_ERR_DEVICE, "relaxation did not converge");
         if (trace) SG_HIP(hipEventRecord(te0, st));
-        const uint32_t* active = ring[(pass + 2) % 3];
         uint32_t* changed = ring[pass % 3];
-        SG_HIP(hipMemsetAsync(changed, 0, gb * FLAG_STRIDE * 4ull, st));
-        hipLaunchKernelGGL(k_active_list, dim3(1), dim3(1024), 0, st, active, gb, alist);
+        if (c > 0)
+          hipLaunchKernelGGL(k_active_list, dim3(1), dim3(1024), 0, st, ring[(pass + 2) % 3], gb, alist, changed,
+                             nullptr);
         {
           TimedLaunch tl(ctx, "relax", 0.0);
           if (work)
@@ -799,7 +809,6 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
                                net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
         }
         SG_CHECK_LAUNCH();
-        last = pass;
         if (trace) {
           SG_HIP(hipEventRecord(te1, st));
           SG_HIP(hipEventSynchronize(te1));
@@ -816,10 +825,12 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
           trace_prev = tot;
         }
       }
-      copy_to_host(ctx, h_changed.data(), ring[last % 3], gb * FLAG_STRIDE * 4ull);
-      uint32_t n_active = 0;
-      for (uint32_t b = 0; b < gb; b++) n_active += h_changed[b * FLAG_STRIDE] != 0;
-      if (!n_active) break;
+      // active list of the next pass (= batches changed in the last one), its count to the host
+      hipLaunchKernelGGL(k_active_list, dim3(1), dim3(1024), 0, st, ring[(pass + 2) % 3], gb, alist,
+                         ring[pass % 3], ctx->apsp_ret);
+      SG_CHECK_LAUNCH();
+      SG_HIP(hipStreamSynchronize(st));
+      if (*(volatile uint32_t*)ctx->apsp_ret == 0) break;
     }
     if (trace) {
       SG_HIP(hipEventDestroy(te0));
