@@ -410,9 +410,12 @@ __global__ void __launch_bounds__(256)
       out_entry(tile[c + 2][r], row, j0 + c + 2, used, self_edge, e_lat, e_loss, l2, f.z, sflag);
       out_entry(tile[c + 3][r], row, j0 + c + 3, used, self_edge, e_lat, e_loss, l3, f.w, sflag);
       const size_t o = (size_t)(row - out_row0) * n_used + j0 + c;
-      *(ulonglong2*)&out_lat[o] = make_ulonglong2(l0, l1);
-      *(ulonglong2*)&out_lat[o + 2] = make_ulonglong2(l2, l3);
-      *(float4*)&out_loss[o] = f;
+      // write-once streaming output (1.2 GB at 10k): nontemporal 16-B stores
+      typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+      typedef float f32x4 __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store((u64x2){l0, l1}, (u64x2*)&out_lat[o]);
+      __builtin_nontemporal_store((u64x2){l2, l3}, (u64x2*)&out_lat[o + 2]);
+      __builtin_nontemporal_store((f32x4){f.x, f.y, f.z, f.w}, (f32x4*)&out_loss[o]);
     }
   } else {
     const uint32_t j = j0 + lane;
