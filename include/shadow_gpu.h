@@ -48,7 +48,8 @@ typedef enum sg_status {
   SG_ERR_DEVICE = 6,        /* HIP runtime error */
   SG_ERR_PARSE = 7,         /* NetworkGraph::parse / ShadowEdge::try_from (graph/mod.rs:72-181) */
   SG_ERR_UNSORTED = 8,      /* sg_deliver_round: packets not grouped by ascending source host */
-  SG_ERR_DUPLICATE_IP = 9   /* two hosts with one address (IpAssignment::assign_ip, graph/mod.rs:383-394) */
+  SG_ERR_DUPLICATE_IP = 9,  /* two hosts with one address (IpAssignment::assign_ip, graph/mod.rs:383-394) */
+  SG_ERR_CAPACITY = 10      /* a CoDel queue outgrew its ring (sg_codel_create ring_cap) */
 } sg_status;
 
 typedef struct sg_ctx sg_ctx;     /* one HIP device + stream + workspace */
@@ -256,6 +257,59 @@ int32_t sg_deliver_source(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table, c
 int32_t sg_deliver_bucket(sg_ctx* ctx, const sg_record* recv, uint32_t n_records,
                           const uint32_t* host_local, uint32_t n_hosts, uint32_t n_local_hosts,
                           uint32_t* dst_order, uint32_t* dst_offsets);
+
+/* ---- router inbound CoDel queues (one per host) ---------------------------
+ * Router::inbound_packets (router/mod.rs:15-58): each host's CoDelQueue
+ * (router/codel_queue.rs), RFC 8289 with Shadow's TARGET = 10 ms,
+ * INTERVAL = 100 ms, no LIMIT, MTU = 1500 (definitions.h:124).  The queues
+ * and their CoDel state live on the device across calls.  A call runs a batch
+ * of push / pop events: each host's events in its order (hosts are
+ * independent, so the batch runs one device lane per host).
+ *   push(packet, len, now)  = CoDelQueue::push (codel_queue.rs:303-317)
+ *   pop(now) -> packet|none = CoDelQueue::pop  (codel_queue.rs:125-148),
+ *                             dropping as the control law dictates.      */
+typedef struct sg_codel sg_codel;
+enum { SG_CODEL_PUSH = 0, SG_CODEL_POP = 1 };
+enum { SG_CODEL_QUEUED = 0, SG_CODEL_DEQUEUED = 1, SG_CODEL_DROPPED = 2 /* PacketStatus::RouterDropped */ };
+
+/* ring_cap: packets a host's queue may hold (rounded up to a power of two);
+ * a push beyond it fails the call with SG_ERR_CAPACITY (the reference has no
+ * limit, so size it for the workload). */
+int32_t sg_codel_create(sg_ctx* ctx, uint32_t n_hosts, uint32_t ring_cap, sg_codel** out);
+void sg_codel_destroy(sg_codel* q);
+
+typedef struct sg_codel_events { /* device arrays, grouped by ascending host */
+  uint32_t n_events;
+  const uint32_t* host;
+  const uint8_t* kind;     /* SG_CODEL_PUSH | SG_CODEL_POP */
+  const uint64_t* time_ns; /* EmulatedTime of the operation (Worker::current_time) */
+  const uint32_t* packet;  /* push: the caller's packet id (< n_packets below) */
+  const uint32_t* len;     /* push: PacketRc::len() (packet.rs:388-390) */
+} sg_codel_events;
+
+/* pop_result (device, n_events): the popped packet id, UINT32_MAX for an
+ * empty pop and for pushes.  pkt_status (device, n_packets): set to
+ * SG_CODEL_DEQUEUED / SG_CODEL_DROPPED when a packet leaves its queue.
+ * n_dropped (host, may be NULL): packets CoDel dropped in this call. */
+int32_t sg_codel_run(sg_ctx* ctx, sg_codel* q, const sg_codel_events* ev, uint32_t* pop_result,
+                     uint8_t* pkt_status, uint32_t n_packets, uint64_t* n_dropped);
+
+/* Copy the per-host state out of / into the device (host arrays, n_hosts
+ * each; ring_* n_hosts * ring_cap): flags (bit 0 drop mode, bit 1
+ * interval_end set, bit 2 drop_next set), interval_end, drop_next, current /
+ * previous drop count, bytes stored, ring head / tail counters, and the ring
+ * (packet, enqueue time, len).  For checkpoints and tests. */
+typedef struct sg_codel_state {
+  uint8_t* flags;
+  uint64_t *interval_end, *drop_next, *cur_drops, *prev_drops, *bytes;
+  uint32_t *head, *tail;
+  uint32_t* ring_packet;
+  uint64_t* ring_time;
+  uint32_t* ring_len;
+} sg_codel_state;
+uint32_t sg_codel_ring_cap(const sg_codel* q);
+int32_t sg_codel_get_state(sg_codel* q, sg_codel_state* out);
+int32_t sg_codel_set_state(sg_codel* q, const sg_codel_state* in);
 
 #ifdef __cplusplus
 }

@@ -58,6 +58,11 @@ def lib():
         L.sgo_smallest_latency.restype = C.c_uint64
         L.sgo_smallest_latency.argtypes = [u64p, C.c_size_t]
         L.sgo_deliver_round.restype = C.c_int64
+        L.sgo_codel_control_law.argtypes = [C.c_uint64, C.c_uint64]
+        L.sgo_codel_control_law.restype = C.c_uint64
+        L.sgo_codel_run.argtypes = [C.c_uint32, C.c_uint32] + [C.c_void_p] * 11 + [C.c_uint32] + [C.c_void_p] * 7 + [
+            C.c_uint32]
+        L.sgo_codel_run.restype = C.c_int
         L.sgo_deliver_round.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u32p, u32p, u32p, u64p,
                                         C.c_uint32, u32p, u32p, C.c_uint32, u64p, f32p, u64p, u64p, u8p, u64p,
                                         u64p, u32p, u32p, u64p, u64p]
@@ -178,3 +183,48 @@ def deliver_round(round_end, sim_end, bootstrap_end, src_host, dst_ip, payload_l
         raise ValueError("sgo_deliver_round: bad argument")
     return dict(status=status, deliver_time=deliver, event_id=eid, dst_order=order[:nd],
                 dst_offsets=offs, min_deliver=mind.value, min_lat=minl.value, delivered=int(nd))
+
+
+# ---------------------------------------------------------------------------
+# Router inbound CoDel queue (router/codel_queue.rs), one per host
+# ---------------------------------------------------------------------------
+CODEL_TARGET_NS = 10_000_000      # codel_queue.rs:23
+CODEL_INTERVAL_NS = 100_000_000   # codel_queue.rs:28
+CODEL_MTU = 1500                  # definitions.h:124
+CD_DROP, CD_HAS_IEND, CD_HAS_DNEXT = 1, 2, 4
+CD_PUSH, CD_POP = 0, 1
+CD_NONE = 0xFFFFFFFF
+
+
+def codel_control_law(t: int, count: int) -> int:
+    """apply_control_law (codel_queue.rs:285-298)."""
+    return int(lib().sgo_codel_control_law(t, count))
+
+
+def codel_state(n_hosts: int, cap: int) -> dict:
+    """Empty queues (CoDelQueue::new, codel_queue.rs:85-95) in the ring layout the HIP side uses."""
+    return dict(cap=cap, flags=np.zeros(n_hosts, np.uint8), interval_end=np.zeros(n_hosts, np.uint64),
+                drop_next=np.zeros(n_hosts, np.uint64), cur=np.zeros(n_hosts, np.uint64),
+                prev=np.zeros(n_hosts, np.uint64), bytes=np.zeros(n_hosts, np.uint64),
+                head=np.zeros(n_hosts, np.uint32), tail=np.zeros(n_hosts, np.uint32),
+                ring_pkt=np.zeros(n_hosts * cap, np.uint32), ring_ts=np.zeros(n_hosts * cap, np.uint64),
+                ring_len=np.zeros(n_hosts * cap, np.uint32))
+
+
+def codel_run(state: dict, host, kind, time, pkt, length, pkt_status: np.ndarray) -> np.ndarray:
+    """Push/pop events (grouped by ascending host, each host's in order) through the
+    per-host queues; state and pkt_status (1 dequeued, 2 dropped) updated in place.
+    Returns pop_result (the popped packet, or CD_NONE; CD_NONE for pushes)."""
+    host, kind = _arr(host, np.uint32), _arr(kind, np.uint8)
+    time, pkt, length = _arr(time, np.uint64), _arr(pkt, np.uint32), _arr(length, np.uint32)
+    n = len(host)
+    res = np.zeros(max(n, 1), np.uint32)
+    H = len(state["flags"])
+    v = lambda a: a.ctypes.data_as(C.c_void_p)
+    rc = lib().sgo_codel_run(H, state["cap"], v(state["flags"]), v(state["interval_end"]), v(state["drop_next"]),
+                             v(state["cur"]), v(state["prev"]), v(state["bytes"]), v(state["head"]),
+                             v(state["tail"]), v(state["ring_pkt"]), v(state["ring_ts"]), v(state["ring_len"]), n,
+                             v(host), v(kind), v(time), v(pkt), v(length), v(res), v(pkt_status), len(pkt_status))
+    if rc:
+        raise ValueError(f"sgo_codel_run: error {rc}")
+    return res[:n]

@@ -22,6 +22,7 @@
  * Build: make -C oracle   (gcc -O2 -ffp-contract=off: one rounding per f32 op,
  * no FMA, matching Rust's f32 arithmetic in graph/mod.rs:328).
  */
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -626,4 +627,169 @@ int64_t sgo_deliver_round(uint64_t round_end, uint64_t sim_end, uint64_t bootstr
   *min_deliver = mind;
   *min_lat = minl;
   return delivered;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Router inbound CoDel queue (router/codel_queue.rs), one queue per host    */
+/* ------------------------------------------------------------------------- */
+/* State per host (SoA, the same layout as the HIP side):
+ *   flags  bit0 mode == Drop, bit1 interval_end is Some, bit2 drop_next is Some
+ *   interval_end, drop_next (EmulatedTime ns), cur/prev drop counts, bytes
+ *   (total_bytes_stored), and the FIFO as a ring of `cap` slots per host:
+ *   head/tail are running counters, slot = h * cap + (counter % cap).
+ * Events are grouped by ascending host, each host's in its order:
+ *   kind 0 = push(packet, len, now)   (codel_queue.rs:303-317)
+ *   kind 1 = pop(now) -> packet|None  (codel_queue.rs:125-148)
+ * pop_result[e] = the popped packet or UINT32_MAX; pkt_status[packet] = 1 when
+ * it leaves through a pop, 2 when CoDel drops it (RouterDropped). */
+#define CD_TARGET 10000000ull     /* codel_queue.rs:23  10 ms */
+#define CD_INTERVAL 100000000ull  /* codel_queue.rs:28 100 ms */
+#define CD_MTU 1500ull            /* definitions.h:124 CONFIG_MTU */
+#define EMU_MAX (UINT64_MAX - 1)  /* emulated_time.rs:30 EMUTIME_MAX */
+enum { CD_DROP = 1, CD_HAS_IEND = 2, CD_HAS_DNEXT = 4 };
+
+typedef struct {
+  uint8_t flags;
+  uint64_t iend, dnext, cur, prev, bytes;
+  uint32_t head, tail;
+  uint32_t* rpkt;
+  uint64_t* rts;
+  uint32_t* rlen;
+  uint32_t cap;
+  uint8_t* status;
+  uint32_t n_status;
+  int err;
+} cd_q;
+
+static uint64_t cd_sat_add(uint64_t t, uint64_t d) {  /* EmulatedTime::saturating_add */
+  return (t > EMU_MAX - d) ? EMU_MAX : t + d;
+}
+static uint64_t cd_since(uint64_t now, uint64_t t) { return now > t ? now - t : 0; }
+
+/* apply_control_law (codel_queue.rs:285-298): time + round(INTERVAL / sqrt(count)) */
+uint64_t sgo_codel_control_law(uint64_t t, uint64_t count) {
+  const double interval = (double)CD_INTERVAL;
+  const double s = count == 0 ? 1.0 : sqrt((double)count);
+  const double div = interval / s;
+  const uint64_t inc = (uint64_t)round(div);
+  return cd_sat_add(t, inc);
+}
+
+static void cd_drop(cd_q* q, uint32_t pkt) {
+  if (pkt < q->n_status) q->status[pkt] = 2;
+  else q->err = -3;
+}
+
+/* process_standing_delay (:231-262) */
+static int cd_standing(cd_q* q, uint64_t now, uint64_t sd) {
+  if (sd < CD_TARGET || q->bytes <= CD_MTU) {
+    q->flags &= (uint8_t)~CD_HAS_IEND;
+    return 0;
+  }
+  if (q->flags & CD_HAS_IEND) return now >= q->iend;
+  q->iend = cd_sat_add(now, CD_INTERVAL);
+  q->flags |= CD_HAS_IEND;
+  return 0;
+}
+
+/* codel_pop / dodequeue (:204-227): 1 = got (pkt, ok) */
+static int cd_pop_front(cd_q* q, uint64_t now, uint32_t* pkt, int* ok) {
+  if (q->head == q->tail) {
+    q->flags &= (uint8_t)~CD_HAS_IEND;
+    return 0;
+  }
+  const uint32_t slot = q->head % q->cap;
+  q->head++;
+  *pkt = q->rpkt[slot];
+  const uint64_t len = q->rlen[slot];
+  q->bytes = q->bytes > len ? q->bytes - len : 0;
+  *ok = cd_standing(q, now, cd_since(now, q->rts[slot]));
+  return 1;
+}
+
+static int cd_should_drop(const cd_q* q, uint64_t now) { return (q->flags & CD_HAS_DNEXT) && now >= q->dnext; }
+static int cd_dropping_recently(const cd_q* q, uint64_t now) {
+  return (q->flags & CD_HAS_DNEXT) && cd_since(now, q->dnext) < 16 * CD_INTERVAL;
+}
+
+/* pop (:125-148) with drop_from_store_mode (:150-170) and drop_from_drop_mode (:172-201) */
+static uint32_t cd_pop(cd_q* q, uint64_t now) {
+  uint32_t pkt;
+  int ok;
+  if (!cd_pop_front(q, now, &pkt, &ok)) {
+    q->flags &= (uint8_t)~CD_DROP;
+    return UINT32_MAX;
+  }
+  if (!ok) {
+    q->flags &= (uint8_t)~CD_DROP;
+    return pkt;
+  }
+  if (!(q->flags & CD_DROP)) {  /* drop_from_store_mode */
+    cd_drop(q, pkt);
+    uint32_t nxt;
+    int nok;
+    const int has = cd_pop_front(q, now, &nxt, &nok);
+    q->flags |= CD_DROP;
+    const uint64_t delta = q->cur > q->prev ? q->cur - q->prev : 0;
+    q->cur = (cd_dropping_recently(q, now) && delta > 1) ? delta : 1;
+    q->dnext = sgo_codel_control_law(now, q->cur);
+    q->flags |= CD_HAS_DNEXT;
+    q->prev = q->cur;
+    return has ? nxt : UINT32_MAX;
+  }
+  /* drop_from_drop_mode */
+  int has = 1;
+  while (has && (q->flags & CD_DROP) && cd_should_drop(q, now)) {
+    cd_drop(q, pkt);
+    q->cur++;
+    has = cd_pop_front(q, now, &pkt, &ok);
+    if (has && ok)
+      q->dnext = sgo_codel_control_law(q->dnext, q->cur);
+    else
+      q->flags &= (uint8_t)~CD_DROP;
+  }
+  return has ? pkt : UINT32_MAX;
+}
+
+int sgo_codel_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* iend, uint64_t* dnext,
+                  uint64_t* cur, uint64_t* prev, uint64_t* bytes, uint32_t* head, uint32_t* tail,
+                  uint32_t* ring_pkt, uint64_t* ring_ts, uint32_t* ring_len, uint32_t n_events,
+                  const uint32_t* host, const uint8_t* kind, const uint64_t* time, const uint32_t* pkt,
+                  const uint32_t* len, uint32_t* pop_result, uint8_t* pkt_status, uint32_t n_status) {
+  if (!cap) return -1;
+  uint32_t e = 0;
+  for (uint32_t h = 0; h < n_hosts; h++) {
+    cd_q q = {flags[h], iend[h], dnext[h], cur[h], prev[h], bytes[h], head[h], tail[h],
+              ring_pkt + (size_t)h * cap, ring_ts + (size_t)h * cap, ring_len + (size_t)h * cap, cap,
+              pkt_status, n_status, 0};
+    for (; e < n_events && host[e] == h; e++) {
+      pop_result[e] = UINT32_MAX;
+      if (kind[e] == 0) {
+        if (q.tail - q.head >= cap) return -2;  /* the caller's ring is too small (the reference has no limit) */
+        const uint32_t slot = q.tail % cap;
+        q.rpkt[slot] = pkt[e];
+        q.rts[slot] = time[e];
+        q.rlen[slot] = len[e];
+        q.tail++;
+        q.bytes += len[e];
+      } else {
+        const uint32_t p = cd_pop(&q, time[e]);
+        pop_result[e] = p;
+        if (p != UINT32_MAX) {
+          if (p < n_status) pkt_status[p] = 1;
+          else return -3;
+        }
+      }
+      if (q.err) return q.err;
+    }
+    flags[h] = q.flags;
+    iend[h] = q.iend;
+    dnext[h] = q.dnext;
+    cur[h] = q.cur;
+    prev[h] = q.prev;
+    bytes[h] = q.bytes;
+    head[h] = q.head;
+    tail[h] = q.tail;
+  }
+  return e == n_events ? 0 : -4;  /* -4: events not grouped by ascending host (or host >= n_hosts) */
 }

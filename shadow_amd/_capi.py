@@ -24,6 +24,7 @@ SG_ERR_DEVICE = 6
 SG_ERR_PARSE = 7
 SG_ERR_UNSORTED = 8
 SG_ERR_DUPLICATE_IP = 9
+SG_ERR_CAPACITY = 10
 
 SG_ROUTE_SHORTEST_PATH = 0x1
 SG_ROUTE_OUT_DEVICE = 0x2
@@ -37,7 +38,8 @@ EXPORTED = [
     "sg_gml_node_index", "sg_gml_destroy", "sg_net_create", "sg_net_destroy", "sg_routing_build",
     "sg_routing_min_latency", "sg_hosts_create", "sg_hosts_get_state", "sg_hosts_set_state",
     "sg_hosts_destroy", "sg_deliver_round", "sg_deliver_source", "sg_deliver_bucket",
-    "sg_table_pack",
+    "sg_table_pack", "sg_codel_create", "sg_codel_destroy", "sg_codel_run", "sg_codel_ring_cap",
+    "sg_codel_get_state", "sg_codel_set_state",
 ]
 
 
@@ -64,6 +66,16 @@ class sg_graph(C.Structure):
 class sg_table(C.Structure):
     _fields_ = [("latency_ns", C.c_void_p), ("packet_loss", C.c_void_p), ("n_cols", C.c_uint32),
                 ("row_begin", C.c_uint32), ("n_rows", C.c_uint32), ("path_key", C.c_void_p)]
+
+
+class sg_codel_events(C.Structure):
+    _fields_ = [("n_events", C.c_uint32), ("host", C.c_void_p), ("kind", C.c_void_p), ("time_ns", C.c_void_p),
+                ("packet", C.c_void_p), ("len", C.c_void_p)]
+
+
+class sg_codel_state(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("flags", "interval_end", "drop_next", "cur_drops", "prev_drops", "bytes",
+                                          "head", "tail", "ring_packet", "ring_time", "ring_len")]
 
 
 class sg_round(C.Structure):
@@ -141,6 +153,12 @@ def load(path: str | None = None):
                                     vp, vp, vp, vp, u32, vp, u32p, C.POINTER(sg_round_stats)]),
         "sg_deliver_bucket": (i32, [vp, vp, u32, vp, u32, u32, vp, vp]),
         "sg_table_pack": (i32, [vp, C.POINTER(sg_table), vp, u32p]),
+        "sg_codel_create": (i32, [vp, u32, u32, C.POINTER(vp)]),
+        "sg_codel_destroy": (None, [vp]),
+        "sg_codel_run": (i32, [vp, vp, C.POINTER(sg_codel_events), vp, vp, u32, u64p]),
+        "sg_codel_ring_cap": (u32, [vp]),
+        "sg_codel_get_state": (i32, [vp, C.POINTER(sg_codel_state)]),
+        "sg_codel_set_state": (i32, [vp, C.POINTER(sg_codel_state)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)

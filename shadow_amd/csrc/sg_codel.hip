@@ -1,0 +1,421 @@
+// sg_codel.hip -- the routers' inbound CoDel queues, one per host, on the device.
+//
+// Router::inbound_packets (router/mod.rs:15-58) is a CoDelQueue
+// (router/codel_queue.rs): RFC 8289 with Shadow's TARGET = 10 ms and
+// INTERVAL = 100 ms, no LIMIT, "good state" while at most one MTU (1500 B,
+// definitions.h:124) is stored.  A host's queue is a sequential state machine,
+// but hosts are independent: a batch of push / pop events runs one lane per
+// host, k_walk-style -- a block owns 64 consecutive hosts, whose events are one
+// contiguous range staged through LDS in chunks (coalesced loads, per-host
+// sequential processing, coalesced pop results).  The FIFO of each host is a
+// ring of `cap` slots in HBM (packet id, enqueue time, length); the scalar
+// CoDel state is kept in registers for the whole call.
+#include <cmath>
+
+#include "sg_device.h"
+#include "sg_internal.h"
+
+struct sg_codel {
+  sg_ctx* ctx = nullptr;
+  uint32_t n = 0, cap = 0;
+  uint8_t* flags = nullptr;
+  uint64_t *iend = nullptr, *dnext = nullptr, *cur = nullptr, *prev = nullptr, *bytes = nullptr;
+  uint32_t *head = nullptr, *tail = nullptr;
+  uint32_t* ring_pkt = nullptr;
+  uint64_t* ring_ts = nullptr;
+  uint32_t* ring_len = nullptr;
+  unsigned long long* ret = nullptr;  // pinned host-mapped: [dropped, error flags]
+  ~sg_codel() {
+    void* ps[] = {flags, iend, dnext, cur, prev, bytes, head, tail, ring_pkt, ring_ts, ring_len};
+    for (void* p : ps)
+      if (p) (void)hipFree(p);
+    if (ret) (void)hipHostFree(ret);
+  }
+};
+
+namespace sg {
+namespace {
+
+constexpr uint64_t CD_TARGET = 10000000ull;     // codel_queue.rs:23
+constexpr uint64_t CD_INTERVAL = 100000000ull;  // codel_queue.rs:28
+constexpr uint64_t CD_MTU = 1500ull;            // definitions.h:124
+constexpr uint64_t EMU_MAX = ~0ull - 1;         // emulated_time.rs:30 EMUTIME_MAX
+constexpr uint32_t CD_NONE = ~0u;
+enum : uint8_t { F_DROP = 1, F_IEND = 2, F_DNEXT = 4 };
+enum : uint32_t { E_UNSORTED = 1, E_HOST = 2, E_FULL = 16, E_PKT = 32 };
+
+__device__ __forceinline__ uint64_t sat_add(uint64_t t, uint64_t d) { return t > EMU_MAX - d ? EMU_MAX : t + d; }
+__device__ __forceinline__ uint64_t since(uint64_t now, uint64_t t) { return now > t ? now - t : 0; }
+
+// apply_control_law (codel_queue.rs:285-298): time + round(INTERVAL / sqrt(count)), f64
+__device__ __forceinline__ uint64_t control_law(uint64_t t, uint64_t count) {
+  const double s = count == 0 ? 1.0 : sqrt((double)count);
+  return sat_add(t, (uint64_t)round((double)CD_INTERVAL / s));
+}
+
+// One host's queue (registers) + its ring (HBM).
+struct Q {
+  uint8_t flags;
+  uint64_t iend, dnext, cur, prev, bytes;
+  uint32_t head, tail;
+  uint32_t* rp;
+  uint64_t* rt;
+  uint32_t* rl;
+  uint32_t mask;
+  uint8_t* status;
+  uint32_t n_status;
+  uint64_t dropped;
+  uint32_t err;
+
+  __device__ void drop(uint32_t pkt) {  // drop_packet -> RouterDropped
+    if (pkt < n_status) status[pkt] = SG_CODEL_DROPPED;
+    else err |= E_PKT;
+    dropped++;
+  }
+  // process_standing_delay (codel_queue.rs:231-262)
+  __device__ bool standing(uint64_t now, uint64_t sd) {
+    if (sd < CD_TARGET || bytes <= CD_MTU) {
+      flags &= (uint8_t)~F_IEND;
+      return false;
+    }
+    if (flags & F_IEND) return now >= iend;
+    iend = sat_add(now, CD_INTERVAL);
+    flags |= F_IEND;
+    return false;
+  }
+  // codel_pop / dodequeue (codel_queue.rs:204-227)
+  __device__ bool pop_front(uint64_t now, uint32_t& pkt, bool& ok) {
+    if (head == tail) {
+      flags &= (uint8_t)~F_IEND;
+      return false;
+    }
+    const uint32_t slot = head & mask;
+    head++;
+    pkt = rp[slot];
+    const uint64_t len = rl[slot];
+    bytes = bytes > len ? bytes - len : 0;
+    ok = standing(now, since(now, rt[slot]));
+    return true;
+  }
+  __device__ bool should_drop(uint64_t now) const { return (flags & F_DNEXT) && now >= dnext; }
+  __device__ bool dropping_recently(uint64_t now) const {
+    return (flags & F_DNEXT) && since(now, dnext) < 16 * CD_INTERVAL;
+  }
+  // pop (codel_queue.rs:125-148), drop_from_store_mode (:150-170), drop_from_drop_mode (:172-201)
+  __device__ uint32_t pop(uint64_t now) {
+    uint32_t pkt;
+    bool ok;
+    if (!pop_front(now, pkt, ok)) {
+      flags &= (uint8_t)~F_DROP;
+      return CD_NONE;
+    }
+    if (!ok) {
+      flags &= (uint8_t)~F_DROP;
+      return pkt;
+    }
+    if (!(flags & F_DROP)) {
+      drop(pkt);
+      uint32_t nxt;
+      bool nok;
+      const bool has = pop_front(now, nxt, nok);
+      flags |= F_DROP;
+      const uint64_t delta = cur > prev ? cur - prev : 0;
+      cur = (dropping_recently(now) && delta > 1) ? delta : 1;
+      dnext = control_law(now, cur);
+      flags |= F_DNEXT;
+      prev = cur;
+      return has ? nxt : CD_NONE;
+    }
+    bool has = true;
+    while (has && (flags & F_DROP) && should_drop(now)) {
+      drop(pkt);
+      cur++;
+      has = pop_front(now, pkt, ok);
+      if (has && ok)
+        dnext = control_law(dnext, cur);
+      else
+        flags &= (uint8_t)~F_DROP;
+    }
+    return has ? pkt : CD_NONE;
+  }
+  // push (codel_queue.rs:303-317); LIMIT is usize::MAX, the ring is the caller's bound
+  __device__ void push(uint32_t pkt, uint64_t now, uint32_t len) {
+    if (tail - head > mask) {
+      err |= E_FULL;
+      return;
+    }
+    const uint32_t slot = tail & mask;
+    rp[slot] = pkt;
+    rt[slot] = now;
+    rl[slot] = len;
+    tail++;
+    bytes += len;
+  }
+};
+
+struct CodelArgs {
+  const uint32_t* host_off;
+  uint32_t H, E;
+  const uint8_t* kind;
+  const uint64_t* time;
+  const uint32_t* pkt;
+  const uint32_t* len;
+  uint8_t* flags;
+  uint64_t *iend, *dnext, *cur, *prev, *bytes;
+  uint32_t *head, *tail;
+  uint32_t* ring_pkt;
+  uint64_t* ring_ts;
+  uint32_t* ring_len;
+  uint32_t cap;
+  uint32_t* pop_result;
+  uint8_t* status;
+  uint32_t n_status;
+  unsigned long long* blk;  // per block: [dropped, error flags]
+};
+
+constexpr int CD_THREADS = 256;
+constexpr int CD_HOSTS = 64;
+constexpr int CD_CHUNK = 1024;
+
+__global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
+  __shared__ uint64_t s_t[CD_CHUNK];
+  __shared__ uint32_t s_p[CD_CHUNK];  // packet -> pop result
+  __shared__ uint32_t s_l[CD_CHUNK];
+  __shared__ uint8_t s_k[CD_CHUNK];
+  const uint32_t h0 = blockIdx.x * CD_HOSTS, t = threadIdx.x;
+  const uint32_t p0 = min(a.host_off[min(h0, a.H)], a.E);
+  const uint32_t p1 = max(min(a.host_off[min(h0 + CD_HOSTS, a.H)], a.E), p0);
+  const uint32_t h = h0 + t;
+  const bool walker = t < CD_HOSTS && h < a.H;
+  uint32_t hb = 0, he = 0;
+  Q q{};
+  if (walker) {
+    hb = min(a.host_off[h], a.E);
+    he = max(min(a.host_off[h + 1], a.E), hb);
+    q.flags = a.flags[h];
+    q.iend = a.iend[h];
+    q.dnext = a.dnext[h];
+    q.cur = a.cur[h];
+    q.prev = a.prev[h];
+    q.bytes = a.bytes[h];
+    q.head = a.head[h];
+    q.tail = a.tail[h];
+    q.rp = a.ring_pkt + (size_t)h * a.cap;
+    q.rt = a.ring_ts + (size_t)h * a.cap;
+    q.rl = a.ring_len + (size_t)h * a.cap;
+    q.mask = a.cap - 1;
+    q.status = a.status;
+    q.n_status = a.n_status;
+  }
+  for (uint32_t c0 = p0; c0 < p1; c0 += CD_CHUNK) {
+    const uint32_t c1 = min(c0 + CD_CHUNK, p1);
+    for (uint32_t i = c0 + t; i < c1; i += CD_THREADS) {  // 1. coalesced staging
+      const uint32_t k = i - c0;
+      s_t[k] = a.time[i];
+      s_p[k] = a.pkt[i];
+      s_l[k] = a.len[i];
+      s_k[k] = a.kind[i];
+    }
+    __syncthreads();
+    if (walker) {  // 2. each host's events in order
+      const uint32_t b = max(hb, c0), e = min(he, c1);
+      for (uint32_t i = b; i < e; i++) {
+        const uint32_t k = i - c0;
+        uint32_t r = CD_NONE;
+        if (s_k[k] == SG_CODEL_PUSH) {
+          q.push(s_p[k], s_t[k], s_l[k]);
+        } else {
+          r = q.pop(s_t[k]);
+          if (r != CD_NONE) {
+            if (r < q.n_status) q.status[r] = SG_CODEL_DEQUEUED;
+            else q.err |= E_PKT;
+          }
+        }
+        s_p[k] = r;
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = c0 + t; i < c1; i += CD_THREADS) a.pop_result[i] = s_p[i - c0];  // 3. coalesced results
+    __syncthreads();
+  }
+  unsigned long long dropped = 0, err = 0;
+  if (walker) {
+    a.flags[h] = q.flags;
+    a.iend[h] = q.iend;
+    a.dnext[h] = q.dnext;
+    a.cur[h] = q.cur;
+    a.prev[h] = q.prev;
+    a.bytes[h] = q.bytes;
+    a.head[h] = q.head;
+    a.tail[h] = q.tail;
+    dropped = q.dropped;
+    err = q.err;
+  }
+  if (t < 64) {
+    for (int d = 32; d > 0; d >>= 1) {
+      dropped += __shfl_xor(dropped, d, 64);
+      err |= __shfl_xor(err, d, 64);
+    }
+    if (t == 0) {
+      a.blk[2 * blockIdx.x] = dropped;
+      a.blk[2 * blockIdx.x + 1] = err;
+    }
+  }
+}
+
+// Sums the blocks' drop counts, ORs their error flags (and the grouping
+// check's) into the pinned host-mapped return block.
+__global__ void __launch_bounds__(1024) k_codel_reduce(const unsigned long long* __restrict__ blk, uint32_t n,
+                                                       const uint32_t* __restrict__ group_err,
+                                                       unsigned long long* __restrict__ ret) {
+  __shared__ unsigned long long r[2][16];
+  unsigned long long d = 0, e = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += 1024) {
+    d += blk[2 * i];
+    e |= blk[2 * i + 1];
+  }
+  for (int s = 32; s > 0; s >>= 1) {
+    d += __shfl_xor(d, s, 64);
+    e |= __shfl_xor(e, s, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    r[0][threadIdx.x >> 6] = d;
+    r[1][threadIdx.x >> 6] = e;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 16; i++) {
+      d += r[0][i];
+      e |= r[1][i];
+    }
+    ret[0] = d;
+    ret[1] = e | *group_err;
+  }
+}
+
+}  // namespace
+}  // namespace sg
+
+extern "C" {
+
+int32_t sg_codel_create(sg_ctx* ctx, uint32_t n_hosts, uint32_t ring_cap, sg_codel** out) {
+  if (!out) return SG_ERR_INVALID_ARG;
+  *out = nullptr;
+  sg_codel* q = nullptr;
+  int32_t rc = sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (ring_cap == 0 || ring_cap > (1u << 30)) throw Error(SG_ERR_INVALID_ARG, "ring_cap must be in [1, 2^30]");
+    uint32_t cap = 1;
+    while (cap < ring_cap) cap <<= 1;
+    q = new sg_codel();
+    q->ctx = ctx;
+    q->n = n_hosts;
+    q->cap = cap;
+    const size_t n = std::max<uint32_t>(n_hosts, 1), r = n * cap;
+    SG_HIP(hipMalloc(&q->flags, n));
+    SG_HIP(hipMalloc(&q->iend, n * 8));
+    SG_HIP(hipMalloc(&q->dnext, n * 8));
+    SG_HIP(hipMalloc(&q->cur, n * 8));
+    SG_HIP(hipMalloc(&q->prev, n * 8));
+    SG_HIP(hipMalloc(&q->bytes, n * 8));
+    SG_HIP(hipMalloc(&q->head, n * 4));
+    SG_HIP(hipMalloc(&q->tail, n * 4));
+    SG_HIP(hipMalloc(&q->ring_pkt, r * 4));
+    SG_HIP(hipMalloc(&q->ring_ts, r * 8));
+    SG_HIP(hipMalloc(&q->ring_len, r * 4));
+    SG_HIP(hipHostMalloc(&q->ret, 16, hipHostMallocMapped | hipHostMallocCoherent));
+    hipStream_t st = ctx->stream;  // CoDelQueue::new (codel_queue.rs:85-95): empty, Store mode, no times
+    SG_HIP(hipMemsetAsync(q->flags, 0, n, st));
+    void* z8[] = {q->iend, q->dnext, q->cur, q->prev, q->bytes};
+    for (void* p : z8) SG_HIP(hipMemsetAsync(p, 0, n * 8, st));
+    SG_HIP(hipMemsetAsync(q->head, 0, n * 4, st));
+    SG_HIP(hipMemsetAsync(q->tail, 0, n * 4, st));
+    SG_HIP(hipStreamSynchronize(st));
+  });
+  if (rc != SG_OK) {
+    delete q;
+    return rc;
+  }
+  *out = q;
+  return SG_OK;
+}
+
+void sg_codel_destroy(sg_codel* q) {
+  if (!q) return;
+  if (q->ctx) (void)hipSetDevice(q->ctx->device);
+  delete q;
+}
+
+uint32_t sg_codel_ring_cap(const sg_codel* q) { return q ? q->cap : 0; }
+
+int32_t sg_codel_run(sg_ctx* ctx, sg_codel* q, const sg_codel_events* ev, uint32_t* pop_result,
+                     uint8_t* pkt_status, uint32_t n_packets, uint64_t* n_dropped) {
+  return sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (!q || q->ctx != ctx || !ev) throw Error(SG_ERR_INVALID_ARG, "null argument");
+    const uint32_t E = ev->n_events, H = q->n;
+    if (n_dropped) *n_dropped = 0;
+    if (!E) return;
+    if (!ev->host || !ev->kind || !ev->time_ns || !ev->packet || !ev->len || !pop_result ||
+        (n_packets && !pkt_status))
+      throw Error(SG_ERR_INVALID_ARG, "null event or output array");
+    hipStream_t st = ctx->stream;
+    uint32_t* ws = ctx->d_seg.get<uint32_t>((size_t)H + 8);  // [offsets H+1][grouping error]
+    uint32_t* gerr = ws + (size_t)H + 1;
+    SG_HIP(hipMemsetAsync(gerr, 0, 4, st));
+    launch_group_offsets(ctx, ev->host, E, H, ws, gerr);
+    const uint32_t nb = std::max<uint32_t>(1, (H + CD_HOSTS - 1) / CD_HOSTS);
+    CodelArgs a{ws, H, E, ev->kind, ev->time_ns, ev->packet, ev->len, q->flags, q->iend, q->dnext, q->cur,
+                q->prev, q->bytes, q->head, q->tail, q->ring_pkt, q->ring_ts, q->ring_len, q->cap, pop_result,
+                pkt_status, n_packets, ctx->d_blk.get<unsigned long long>(2 * (size_t)nb)};
+    {
+      // per event: 17 B in, 4 B result, ring slot 16 B written (push) or read (pop), 1 B status
+      TimedLaunch tl(ctx, "codel", 38.0 * E + 56.0 * H);
+      hipLaunchKernelGGL(k_codel, dim3(nb), dim3(CD_THREADS), 0, st, a);
+    }
+    hipLaunchKernelGGL(k_codel_reduce, dim3(1), dim3(1024), 0, st, a.blk, nb, gerr, q->ret);
+    SG_CHECK_LAUNCH();
+    SG_HIP(hipStreamSynchronize(st));
+    const volatile unsigned long long* r = q->ret;
+    const uint64_t err = r[1];
+    if (err & E_UNSORTED) throw Error(SG_ERR_UNSORTED, "CoDel events must be grouped by ascending host");
+    if (err & E_HOST) throw Error(SG_ERR_INVALID_ARG, "CoDel event host out of range");
+    if (err & E_FULL) throw Error(SG_ERR_CAPACITY, "a CoDel queue outgrew its ring (raise ring_cap)");
+    if (err & E_PKT) throw Error(SG_ERR_INVALID_ARG, "CoDel packet id >= n_packets");
+    if (n_dropped) *n_dropped = r[0];
+  });
+}
+
+int32_t sg_codel_get_state(sg_codel* q, sg_codel_state* o) {
+  if (!q || !o) return SG_ERR_INVALID_ARG;
+  return sg::guarded(q->ctx, [&] {
+    const size_t n = q->n, r = n * q->cap;
+    hipStream_t st = q->ctx->stream;
+    struct { void* h; const void* d; size_t b; } cp[] = {
+        {o->flags, q->flags, n}, {o->interval_end, q->iend, n * 8}, {o->drop_next, q->dnext, n * 8},
+        {o->cur_drops, q->cur, n * 8}, {o->prev_drops, q->prev, n * 8}, {o->bytes, q->bytes, n * 8},
+        {o->head, q->head, n * 4}, {o->tail, q->tail, n * 4}, {o->ring_packet, q->ring_pkt, r * 4},
+        {o->ring_time, q->ring_ts, r * 8}, {o->ring_len, q->ring_len, r * 4}};
+    for (auto& c : cp)
+      if (c.h && c.b) SG_HIP(hipMemcpyAsync(c.h, c.d, c.b, hipMemcpyDeviceToHost, st));
+    SG_HIP(hipStreamSynchronize(st));
+  });
+}
+
+int32_t sg_codel_set_state(sg_codel* q, const sg_codel_state* in) {
+  if (!q || !in) return SG_ERR_INVALID_ARG;
+  return sg::guarded(q->ctx, [&] {
+    const size_t n = q->n, r = n * q->cap;
+    hipStream_t st = q->ctx->stream;
+    struct { void* d; const void* h; size_t b; } cp[] = {
+        {q->flags, in->flags, n}, {q->iend, in->interval_end, n * 8}, {q->dnext, in->drop_next, n * 8},
+        {q->cur, in->cur_drops, n * 8}, {q->prev, in->prev_drops, n * 8}, {q->bytes, in->bytes, n * 8},
+        {q->head, in->head, n * 4}, {q->tail, in->tail, n * 4}, {q->ring_pkt, in->ring_packet, r * 4},
+        {q->ring_ts, in->ring_time, r * 8}, {q->ring_len, in->ring_len, r * 4}};
+    for (auto& c : cp)
+      if (c.h && c.b) SG_HIP(hipMemcpyAsync(c.d, c.h, c.b, hipMemcpyHostToDevice, st));
+    SG_HIP(hipStreamSynchronize(st));
+  });
+}
+
+}  // extern "C"

@@ -1203,6 +1203,13 @@ static void deliver_bucket(sg_ctx* ctx, const sg_record* recv, uint32_t n, const
   }
 }
 
+void launch_group_offsets(sg_ctx* ctx, const uint32_t* key, uint32_t n, uint32_t n_groups, uint32_t* off,
+                          uint32_t* err) {
+  hipLaunchKernelGGL(k_host_off, dim3(grid_for((size_t)n + 1, 256, 16384)), dim3(256), 0, ctx->stream, key, n,
+                     n_groups, off, err);
+  SG_CHECK_LAUNCH();
+}
+
 // Path-key table: (lat << 32) | bits(loss) per cell, so the walk's path gather
 // is one 8-byte word.  Streaming, coalesced: 12 B in + 8 B out per cell.
 __global__ void __launch_bounds__(256) k_table_pack(const uint64_t* __restrict__ lat, const float* __restrict__ loss,

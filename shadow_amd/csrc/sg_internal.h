@@ -155,6 +155,12 @@ inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 1u << 20) {
 // Exclusive scan of n u32 values (device, in -> out, out has n+1 entries, out[n] = total).
 void exclusive_scan_u32(sg_ctx* ctx, const uint32_t* d_in, uint32_t* d_out, uint32_t n);
 
+// Group offsets of a key array grouped by ascending key (sg_deliver.hip's
+// k_host_off): off[g] = first index whose key >= g, g = 0..n_groups.  err bit
+// 1: not grouped ascending; bit 2: a key >= n_groups.
+void launch_group_offsets(sg_ctx* ctx, const uint32_t* key, uint32_t n, uint32_t n_groups, uint32_t* off,
+                          uint32_t* err);
+
 // Read a few scalars back (blocking on the context stream).
 void copy_to_host(sg_ctx* ctx, void* dst, const void* src, size_t bytes);
 

@@ -1,0 +1,118 @@
+"""Routers' inbound CoDel queues on the device: host-side mirror of
+Router::inbound_packets (src/main/network/router/mod.rs:15-58) and
+CoDelQueue (src/main/network/router/codel_queue.rs).
+
+One queue per host lives on the device across calls.  `CoDelQueues.run`
+applies a batch of push / pop events -- grouped by ascending host, each host's
+in the order the host performed them -- exactly as the reference's
+`CoDelQueue::push(packet, now)` / `CoDelQueue::pop(now)` would, one device
+lane per host.  Every computation is the HIP kernel in libshadow_gpu.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _capi
+from ._capi import check, load
+from .graph import Context, default_context
+
+PUSH, POP = 0, 1                       # SG_CODEL_PUSH / SG_CODEL_POP
+QUEUED, DEQUEUED, DROPPED = 0, 1, 2    # SG_CODEL_* packet status
+NONE = 0xFFFFFFFF
+TARGET_NS = 10_000_000                 # codel_queue.rs:23
+INTERVAL_NS = 100_000_000              # codel_queue.rs:28
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _dev(x, np_dtype, torch_view, device):
+    torch = _torch()
+    if isinstance(x, torch.Tensor):
+        assert x.is_cuda and x.is_contiguous()
+        return x
+    a = np.ascontiguousarray(np.asarray(x, dtype=np_dtype))
+    return torch.from_numpy(a.view(torch_view)).to(device)
+
+
+@dataclass
+class CoDelEvents:
+    """One batch of queue operations (device SoA)."""
+
+    host: "object"     # int32 (u32 bits), grouped by ascending host
+    kind: "object"     # uint8: PUSH / POP
+    time_ns: "object"  # int64 (u64 bits): EmulatedTime of the operation
+    packet: "object"   # int32 (u32 bits): the caller's packet id (pushes)
+    length: "object"   # int32: PacketRc::len() (pushes)
+
+    @classmethod
+    def from_numpy(cls, host, kind, time_ns, packet, length, device="cuda"):
+        return cls(_dev(host, np.uint32, np.int32, device), _dev(kind, np.uint8, np.uint8, device),
+                   _dev(time_ns, np.uint64, np.int64, device), _dev(packet, np.uint32, np.int32, device),
+                   _dev(length, np.uint32, np.int32, device))
+
+    def __len__(self):
+        return int(self.host.numel())
+
+
+class CoDelQueues:
+    """The inbound CoDel queue of every host (sg_codel_*)."""
+
+    def __init__(self, n_hosts: int, ring_cap: int = 4096, ctx: Optional[Context] = None):
+        self.ctx = ctx or default_context()
+        self.n = int(n_hosts)
+        h = C.c_void_p()
+        check(self.ctx.handle, load().sg_codel_create(self.ctx.handle, self.n, int(ring_cap), C.byref(h)))
+        self.handle = h
+        self.cap = int(load().sg_codel_ring_cap(h))
+
+    def run(self, ev: CoDelEvents, pkt_status, n_packets: Optional[int] = None):
+        """Apply the events.  pkt_status (uint8 device tensor indexed by packet id) is
+        set to DEQUEUED / DROPPED as packets leave.  Returns (pop_result int32 device
+        tensor: the popped packet or NONE per event, packets dropped)."""
+        torch = _torch()
+        n = len(ev)
+        res = torch.empty(max(n, 1), dtype=torch.int32, device=ev.host.device)
+        e = _capi.sg_codel_events(n, ev.host.data_ptr(), ev.kind.data_ptr(), ev.time_ns.data_ptr(),
+                                  ev.packet.data_ptr(), ev.length.data_ptr())
+        nd = C.c_uint64()
+        ns = int(pkt_status.numel()) if n_packets is None else int(n_packets)
+        check(self.ctx.handle, load().sg_codel_run(self.ctx.handle, self.handle, C.byref(e), res.data_ptr(),
+                                                   pkt_status.data_ptr(), ns, C.byref(nd)))
+        return res[:n], int(nd.value)
+
+    def get_state(self) -> dict:
+        """Per-host state (the oracle's layout: flags, interval_end, drop_next, cur, prev,
+        bytes, head, tail, ring_pkt, ring_ts, ring_len)."""
+        n, r = self.n, self.n * self.cap
+        st = dict(cap=self.cap, flags=np.zeros(n, np.uint8), interval_end=np.zeros(n, np.uint64),
+                  drop_next=np.zeros(n, np.uint64), cur=np.zeros(n, np.uint64), prev=np.zeros(n, np.uint64),
+                  bytes=np.zeros(n, np.uint64), head=np.zeros(n, np.uint32), tail=np.zeros(n, np.uint32),
+                  ring_pkt=np.zeros(r, np.uint32), ring_ts=np.zeros(r, np.uint64), ring_len=np.zeros(r, np.uint32))
+        check(self.ctx.handle, load().sg_codel_get_state(self.handle, C.byref(self._struct(st))))
+        return st
+
+    def set_state(self, st: dict) -> None:
+        check(self.ctx.handle, load().sg_codel_set_state(self.handle, C.byref(self._struct(st))))
+
+    @staticmethod
+    def _struct(st) -> _capi.sg_codel_state:
+        v = lambda a: a.ctypes.data_as(C.c_void_p)
+        return _capi.sg_codel_state(v(st["flags"]), v(st["interval_end"]), v(st["drop_next"]), v(st["cur"]),
+                                    v(st["prev"]), v(st["bytes"]), v(st["head"]), v(st["tail"]),
+                                    v(st["ring_pkt"]), v(st["ring_ts"]), v(st["ring_len"]))
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                load().sg_codel_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass

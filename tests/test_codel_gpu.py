@@ -1,0 +1,122 @@
+"""GPU parity of the routers' inbound CoDel queues (sg_codel_*) against the
+oracle (router/codel_queue.rs restated; the oracle itself is pinned by the
+reference's unit tests in tests/test_codel_cpu.py).  Bit-exact: pop results,
+packet statuses and the whole per-host state, across consecutive calls."""
+import numpy as np
+import pytest
+
+from shadow_amd import ShadowGpuError, _capi
+from shadow_amd.router import CoDelEvents, CoDelQueues
+
+pytestmark = pytest.mark.gpu
+T0 = 946684800 * 10**9
+MS = 10**6
+KEYS = ("flags", "interval_end", "drop_next", "cur", "prev", "bytes", "head", "tail")
+
+
+def _status(n):
+    import torch
+
+    return torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")
+
+
+def _same_state(O, got, want):
+    for k in KEYS:
+        assert np.array_equal(got[k], want[k]), k
+    cap = want["cap"]
+    for h in range(len(want["head"])):  # live ring slots only
+        for c in range(int(want["head"][h]), int(want["tail"][h])):
+            s = h * cap + (c % cap)
+            assert (got["ring_pkt"][s], got["ring_ts"][s], got["ring_len"][s]) == \
+                (want["ring_pkt"][s], want["ring_ts"][s], want["ring_len"][s])
+
+
+def _run_both(O, q, ostate, gstat, ostat, host, kind, t, pkt, ln):
+    ev = CoDelEvents.from_numpy(host, kind, t, pkt, ln)
+    res, nd = q.run(ev, gstat)
+    before = (ostat == 2).sum()
+    want = O.codel_run(ostate, host, kind, t, pkt, ln, ostat)
+    assert np.array_equal(res.cpu().numpy().view(np.uint32), want)
+    assert np.array_equal(gstat.cpu().numpy()[: len(ostat)], ostat)
+    assert nd == (ostat == 2).sum() - before
+    return want
+
+
+def _stream(rng, H, E, t0, gap_ms, p_pop, n_pkt0=0):
+    host = np.sort(rng.integers(0, H, E)).astype(np.uint32)
+    kind = (rng.random(E) < p_pop).astype(np.uint8)
+    t = np.zeros(E, np.uint64)
+    for h in np.unique(host):
+        idx = np.nonzero(host == h)[0]
+        t[idx] = t0 + np.cumsum(rng.integers(0, gap_ms * MS, len(idx))).astype(np.uint64)
+    pkt = (n_pkt0 + np.arange(E)).astype(np.uint32)
+    ln = rng.integers(40, 1500, E).astype(np.uint32)
+    return host, kind, t, pkt, ln
+
+
+def test_reference_drop_many_sequence(oracle, ctx):
+    """codel_queue.rs:494-534 event by event: state equal after every event."""
+    q = CoDelQueues(1, 64, ctx=ctx)
+    os_ = oracle.codel_state(1, q.cap)
+    gstat, ostat = _status(64), np.zeros(64, np.uint8)
+    start, end = T0 + 1000 * MS, T0 + 1000000 * MS
+    seq = [(0, start)] * 20 + [(1, start + 10 * MS), (1, start + 110 * MS), (1, end)]
+    for i, (k, t) in enumerate(seq):
+        _run_both(oracle, q, os_, gstat, ostat, [0], [k], [t], [i], [1028])
+        _same_state(oracle, q.get_state(), os_)
+    st = q.get_state()
+    assert st["tail"][0] - st["head"][0] == 1 and st["cur"][0] == 16 and not st["flags"][0] & 1
+
+
+@pytest.mark.parametrize("gap_ms,p_pop", [(3, 0.45), (1, 0.3), (20, 0.5)])
+def test_random_streams_over_calls(oracle, ctx, gap_ms, p_pop):
+    """500 hosts, three consecutive calls of 60k events: state carries over."""
+    rng = np.random.default_rng(gap_ms)
+    H, E = 500, 60000
+    q = CoDelQueues(H, 4096, ctx=ctx)
+    os_ = oracle.codel_state(H, q.cap)
+    gstat, ostat = _status(3 * E), np.zeros(3 * E, np.uint8)
+    t0 = T0 + 10**9
+    for c in range(3):
+        ev = _stream(rng, H, E, t0, gap_ms, p_pop, n_pkt0=c * E)
+        _run_both(oracle, q, os_, gstat, ostat, *ev)
+        t0 = int(ev[2].max()) + 1
+    _same_state(oracle, q.get_state(), os_)
+    assert (ostat == 2).any() and (ostat == 1).any()
+
+
+def test_large_single_call(oracle, ctx):
+    """100k hosts, 1M events (the bench shape), one call."""
+    rng = np.random.default_rng(11)
+    H, E = 100000, 1000000
+    q = CoDelQueues(H, 256, ctx=ctx)
+    os_ = oracle.codel_state(H, q.cap)
+    gstat, ostat = _status(E), np.zeros(E, np.uint8)
+    _run_both(oracle, q, os_, gstat, ostat, *_stream(rng, H, E, T0 + 10**9, 30, 0.4))
+    _same_state(oracle, q.get_state(), os_)
+
+
+def test_state_roundtrip_and_empty_call(ctx):
+    q = CoDelQueues(3, 8, ctx=ctx)
+    st = q.get_state()
+    st["flags"][1] = 1
+    st["bytes"][2] = 77
+    q.set_state(st)
+    st2 = q.get_state()
+    assert st2["flags"][1] == 1 and st2["bytes"][2] == 77
+    res, nd = q.run(CoDelEvents.from_numpy([], [], [], [], []), _status(1))
+    assert len(res) == 0 and nd == 0
+
+
+def test_errors(ctx):
+    q = CoDelQueues(4, 2, ctx=ctx)  # ring of 2
+    with pytest.raises(ShadowGpuError) as e:
+        q.run(CoDelEvents.from_numpy([0, 0, 0], [0, 0, 0], [T0] * 3, [0, 1, 2], [100] * 3), _status(8))
+    assert e.value.code == _capi.SG_ERR_CAPACITY
+    q = CoDelQueues(4, 8, ctx=ctx)
+    with pytest.raises(ShadowGpuError) as e:
+        q.run(CoDelEvents.from_numpy([2, 1], [0, 0], [T0] * 2, [0, 1], [100] * 2), _status(8))
+    assert e.value.code == _capi.SG_ERR_UNSORTED
+    with pytest.raises(ShadowGpuError) as e:
+        q.run(CoDelEvents.from_numpy([0, 9], [0, 0], [T0] * 2, [0, 1], [100] * 2), _status(8))
+    assert e.value.code == _capi.SG_ERR_INVALID_ARG

@@ -8,7 +8,8 @@ SRC=/tmp/sg_rev_$NAME; rm -rf $SRC; mkdir -p $SRC
 git -C $ROOT archive $REV shadow_amd/csrc include | tar -x -C $SRC
 cd $SRC/shadow_amd/csrc
 pids=()
-for f in sg_context sg_routing sg_deliver; do
+for f in sg_context sg_routing sg_deliver sg_codel; do
+  [ -f $f.hip ] || continue
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=gfx950 -ffp-contract=off \
     -fno-fast-math -munsafe-fp-atomics -c $f.hip -o $f.o &
   pids+=($!)

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--variants", default="SG_APSP_FRONTIER=1;SG_APSP_FRONTIER=0")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="time only rank 0's source-row block of an N-way row sharding (the per-GPU work at N GPUs)")
     a = ap.parse_args()
     import torch
 
@@ -34,6 +36,7 @@ def main():
     net = NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
     n = a.nodes
     used = np.arange(n, dtype=np.uint32)
+    r1 = (n + a.shard_of - 1) // a.shard_of  # rank 0's rows
     lat = torch.empty(n * n, dtype=torch.int64, device="cuda")
     loss = torch.empty(n * n, dtype=torch.float32, device="cuda")
     ref = None
@@ -51,24 +54,24 @@ def main():
     for _ in range(a.rounds):  # interleaved A/B/A/B...: box-to-box and clock drift hit every variant alike
         for v in variants:
             set_env(v)
-            net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)  # warm-up
+            net.build_rows_device(used, 0, r1, lat.data_ptr(), loss.data_ptr(), True)  # warm-up
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(a.reps):
-                net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
+                net.build_rows_device(used, 0, r1, lat.data_ptr(), loss.data_ptr(), True)
             torch.cuda.synchronize()
             times[v].append((time.perf_counter() - t0) / a.reps * 1e3)
     for v in variants:
         set_env(v)
         ctx.enable_timers(True)
-        net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
+        net.build_rows_device(used, 0, r1, lat.data_ptr(), loss.data_ptr(), True)
         rms, launches, _ = ctx.read_timer("relax")
         ctx.enable_timers(True, count_work=True)
-        net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
+        net.build_rows_device(used, 0, r1, lat.data_ptr(), loss.data_ptr(), True)
         _, _, work = ctx.read_timer("relax")
         ctx.enable_timers(False)
         h = (lat[: 64 * n].cpu().numpy().copy(), loss[: 64 * n].cpu().numpy().copy(),
-             lat[-64 * n:].cpu().numpy().copy())
+             lat[(r1 - 64) * n:r1 * n].cpu().numpy().copy())
         same = "ref" if ref is None else all(np.array_equal(x, y) for x, y in zip(h, ref))
         ref = ref or h
         ms = float(np.median(times[v]))
