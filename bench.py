@@ -48,6 +48,7 @@ def parse_args():
     p.add_argument("--packets", type=int, default=1000000)
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-delivery", action="store_true")
+    p.add_argument("--no-codel", action="store_true", help="skip the router CoDel leg")
     p.add_argument("--no-pack", action="store_true",
                    help="deliver from the two-array table (no packed path-key copy)")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
@@ -113,6 +114,90 @@ def load_pmc(path):
             return json.load(f)
     except (OSError, ValueError):
         return {}
+
+
+SERVICE_NS = 12_000  # 1500 B at 1 Gbit/s: the interface's pop spacing in the CoDel leg
+
+
+def codel_events(offsets, order, deliver_time, payload):
+    """C4 round -> each destination's inbound CoDel stream: pushes at the arrival
+    times (the bucket, in EventQueue order) and a FIFO server popping one packet
+    every SERVICE_NS (s_j = max(a_j, s_{j-1}) + SERVICE_NS); per host in time order,
+    a push before a pop at the same time."""
+    H = len(offsets) - 1
+    cnt = np.diff(offsets.astype(np.int64))
+    host = np.repeat(np.arange(H, dtype=np.int64), cnt)
+    arr = deliver_time[order].astype(np.int64)
+    j = np.arange(len(order), dtype=np.int64) - np.repeat(offsets[:-1].astype(np.int64), cnt)  # rank in bucket
+    # s_j = (j + 1) S + max_{k<=j} (a_k - k S), a running max restarted per host: a per-host
+    # offset above the key range keeps earlier hosts below later ones
+    key = arr - j * SERVICE_NS
+    kmin = int(key.min()) if len(key) else 0
+    shift = host << 41
+    run = np.maximum.accumulate(key - kmin + shift) - shift + kmin if len(key) else key
+    pop_t = run + (j + 1) * SERVICE_NS
+    n = len(order)
+    ev_host = np.concatenate([host, host])
+    ev_time = np.concatenate([arr, pop_t])
+    ev_kind = np.concatenate([np.zeros(n, np.uint8), np.ones(n, np.uint8)])
+    ev_pkt = np.concatenate([order.astype(np.int64), np.zeros(n, np.int64)])
+    ln = 28 + payload[order].astype(np.int64)  # IPv4 + UDP headers + payload (packet.rs:388-390)
+    ev_len = np.concatenate([ln, np.zeros(n, np.int64)])
+    idx = np.lexsort((ev_kind, ev_time, ev_host))
+    return (ev_host[idx].astype(np.uint32), ev_kind[idx], ev_time[idx].astype(np.uint64),
+            ev_pkt[idx].astype(np.uint32), ev_len[idx].astype(np.uint32))
+
+
+def codel_leg(a, D, ctx, torch, out, payload, n_packets, pmc):
+    from shadow_amd.router import CoDelEvents, CoDelQueues
+
+    nd = int(out.n_delivered)
+    offs = out.dst_offsets.cpu().numpy().view(np.uint32)
+    order = out.dst_order[:nd].cpu().numpy().view(np.uint32)
+    dtime = out.deliver_time_ns.cpu().numpy().view(np.uint64)
+    evs = codel_events(offs, order, dtime, np.asarray(payload, np.uint32))
+    E = len(evs[0])
+    H = len(offs) - 1
+    q = CoDelQueues(H, 256, ctx=ctx)
+    ev = CoDelEvents.from_numpy(*evs)
+    status = torch.zeros(max(n_packets, 1), dtype=torch.uint8, device="cuda")
+    state0 = q.get_state()
+
+    def step():
+        q.run(ev, status)
+
+    t = timed(D, step, a.steps, a.warmup)
+    q.set_state(state0)
+    ctx.enable_timers(True)
+    _, n_drop = q.run(ev, status)
+    k_ms, k_n, k_bytes = ctx.read_timer("codel")
+    ctx.enable_timers(False)
+    k_s = k_ms / 1e3 / max(k_n, 1)
+    ach = k_bytes / max(k_n, 1) / k_s / 1e9 if k_n else 0.0
+    pm = pmc.get("codel", {})
+    leg = {
+        "metric": "CoDel queue operations/sec (router inbound, one queue per host)", "unit": "ops/s",
+        "value": round(D.sum(float(E)) / t, 1), "higher_is_better": True, "ms_per_batch": round(t * 1e3, 4),
+        "scaling": "weak", "dtype": "u64+f64",
+        "config": {"workload": "the C4 round's delivered packets pushed into their destinations' CoDel queues at "
+                               "arrival, each interface popping one packet per 12 us (1500 B at 1 Gbit/s)",
+                   "hosts": H, "events": E, "pushes": nd},
+        "roofline": {"kernel": "k_codel", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pm.get("hbm_bytes_per_launch"),
+                     "avg_launch_ms": round(k_s * 1e3, 4)},
+        "dropped": n_drop,
+    }
+    if D.rank == 0 and D.world == 1 and not a.no_cpu:
+        from oracle import oracle as O
+
+        st = O.codel_state(H, q.cap)
+        ost = np.zeros(max(n_packets, 1), np.uint8)
+        t0 = time.perf_counter()
+        O.codel_run(st, *evs, ost)
+        tc = time.perf_counter() - t0
+        leg["cpu_baseline"] = {"value": round(E / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port",
+                               "sample": f"the same {E} events through the C restatement of codel_queue.rs, 1 thread"}
+    return leg
 
 
 def main():
@@ -305,6 +390,8 @@ def main():
                                         "send_packet semantics + per-destination EventQueue order, 1 thread"}
             delivery["speedup_vs_cpu"] = round(delivery["value"] / delivery["cpu_baseline"]["value"], 1)
         result["delivery"] = delivery
+        if not a.no_codel:
+            result["codel"] = codel_leg(a, D, ctx, torch, out, pk["payload"], a.packets, pmc)
 
     if D.rank == 0:
         print(json.dumps(result), flush=True)

@@ -53,11 +53,16 @@ __device__ __forceinline__ uint64_t control_law(uint64_t t, uint64_t count) {
   return sat_add(t, (uint64_t)round((double)CD_INTERVAL / s));
 }
 
-// One host's queue (registers) + its ring (HBM).
+// One host's queue (registers) + its ring (HBM).  The head element is also
+// cached in registers (hp/ht/hl, valid while head < tail): a pop consumes the
+// cache and issues the load of the next element right away, so its latency
+// hides behind the events in between instead of stalling the next pop.
 struct Q {
   uint8_t flags;
   uint64_t iend, dnext, cur, prev, bytes;
   uint32_t head, tail;
+  uint32_t hp, hl;
+  uint64_t ht;
   uint32_t* rp;
   uint64_t* rt;
   uint32_t* rl;
@@ -89,13 +94,21 @@ struct Q {
       flags &= (uint8_t)~F_IEND;
       return false;
     }
-    const uint32_t slot = head & mask;
+    pkt = hp;
+    const uint64_t len = hl, ts = ht;
     head++;
-    pkt = rp[slot];
-    const uint64_t len = rl[slot];
+    load_head();
     bytes = bytes > len ? bytes - len : 0;
-    ok = standing(now, since(now, rt[slot]));
+    ok = standing(now, since(now, ts));
     return true;
+  }
+  __device__ void load_head() {
+    if (head != tail) {
+      const uint32_t slot = head & mask;
+      hp = rp[slot];
+      ht = rt[slot];
+      hl = rl[slot];
+    }
   }
   __device__ bool should_drop(uint64_t now) const { return (flags & F_DNEXT) && now >= dnext; }
   __device__ bool dropping_recently(uint64_t now) const {
@@ -148,6 +161,11 @@ struct Q {
     rp[slot] = pkt;
     rt[slot] = now;
     rl[slot] = len;
+    if (head == tail) {  // the new element is the head
+      hp = pkt;
+      ht = now;
+      hl = len;
+    }
     tail++;
     bytes += len;
   }
@@ -206,6 +224,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
     q.mask = a.cap - 1;
     q.status = a.status;
     q.n_status = a.n_status;
+    q.load_head();
   }
   for (uint32_t c0 = p0; c0 < p1; c0 += CD_CHUNK) {
     const uint32_t c1 = min(c0 + CD_CHUNK, p1);
