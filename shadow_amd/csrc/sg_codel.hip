@@ -11,6 +11,7 @@
 // ring of `cap` slots in HBM (packet id, enqueue time, length); the scalar
 // CoDel state is kept in registers for the whole call.
 #include <cmath>
+#include <vector>
 
 #include "sg_device.h"
 #include "sg_internal.h"
@@ -21,12 +22,10 @@ struct sg_codel {
   uint8_t* flags = nullptr;
   uint64_t *iend = nullptr, *dnext = nullptr, *cur = nullptr, *prev = nullptr, *bytes = nullptr;
   uint32_t *head = nullptr, *tail = nullptr;
-  uint32_t* ring_pkt = nullptr;
-  uint64_t* ring_ts = nullptr;
-  uint32_t* ring_len = nullptr;
+  uint4* ring = nullptr;  // per slot {packet, len, time lo, time hi}: one 16-B access per push / pop
   unsigned long long* ret = nullptr;  // pinned host-mapped: [dropped, error flags]
   ~sg_codel() {
-    void* ps[] = {flags, iend, dnext, cur, prev, bytes, head, tail, ring_pkt, ring_ts, ring_len};
+    void* ps[] = {flags, iend, dnext, cur, prev, bytes, head, tail, ring};
     for (void* p : ps)
       if (p) (void)hipFree(p);
     if (ret) (void)hipHostFree(ret);
@@ -63,9 +62,7 @@ struct Q {
   uint32_t head, tail;
   uint32_t hp, hl;
   uint64_t ht;
-  uint32_t* rp;
-  uint64_t* rt;
-  uint32_t* rl;
+  uint4* ring;
   uint32_t mask;
   uint8_t* status;
   uint32_t n_status;
@@ -105,9 +102,10 @@ struct Q {
   __device__ void load_head() {
     if (head != tail) {
       const uint32_t slot = head & mask;
-      hp = rp[slot];
-      ht = rt[slot];
-      hl = rl[slot];
+      const uint4 r = ring[slot];
+      hp = r.x;
+      hl = r.y;
+      ht = ((uint64_t)r.w << 32) | r.z;
     }
   }
   __device__ bool should_drop(uint64_t now) const { return (flags & F_DNEXT) && now >= dnext; }
@@ -158,9 +156,7 @@ struct Q {
       return;
     }
     const uint32_t slot = tail & mask;
-    rp[slot] = pkt;
-    rt[slot] = now;
-    rl[slot] = len;
+    ring[slot] = make_uint4(pkt, len, (uint32_t)now, (uint32_t)(now >> 32));
     if (head == tail) {  // the new element is the head
       hp = pkt;
       ht = now;
@@ -181,9 +177,7 @@ struct CodelArgs {
   uint8_t* flags;
   uint64_t *iend, *dnext, *cur, *prev, *bytes;
   uint32_t *head, *tail;
-  uint32_t* ring_pkt;
-  uint64_t* ring_ts;
-  uint32_t* ring_len;
+  uint4* ring;
   uint32_t cap;
   uint32_t* pop_result;
   uint8_t* status;
@@ -218,9 +212,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
     q.bytes = a.bytes[h];
     q.head = a.head[h];
     q.tail = a.tail[h];
-    q.rp = a.ring_pkt + (size_t)h * a.cap;
-    q.rt = a.ring_ts + (size_t)h * a.cap;
-    q.rl = a.ring_len + (size_t)h * a.cap;
+    q.ring = a.ring + (size_t)h * a.cap;
     q.mask = a.cap - 1;
     q.status = a.status;
     q.n_status = a.n_status;
@@ -339,9 +331,7 @@ int32_t sg_codel_create(sg_ctx* ctx, uint32_t n_hosts, uint32_t ring_cap, sg_cod
     SG_HIP(hipMalloc(&q->bytes, n * 8));
     SG_HIP(hipMalloc(&q->head, n * 4));
     SG_HIP(hipMalloc(&q->tail, n * 4));
-    SG_HIP(hipMalloc(&q->ring_pkt, r * 4));
-    SG_HIP(hipMalloc(&q->ring_ts, r * 8));
-    SG_HIP(hipMalloc(&q->ring_len, r * 4));
+    SG_HIP(hipMalloc(&q->ring, r * 16));
     SG_HIP(hipHostMalloc(&q->ret, 16, hipHostMallocMapped | hipHostMallocCoherent));
     hipStream_t st = ctx->stream;  // CoDelQueue::new (codel_queue.rs:85-95): empty, Store mode, no times
     SG_HIP(hipMemsetAsync(q->flags, 0, n, st));
@@ -385,7 +375,7 @@ int32_t sg_codel_run(sg_ctx* ctx, sg_codel* q, const sg_codel_events* ev, uint32
     launch_group_offsets(ctx, ev->host, E, H, ws, gerr);
     const uint32_t nb = std::max<uint32_t>(1, (H + CD_HOSTS - 1) / CD_HOSTS);
     CodelArgs a{ws, H, E, ev->kind, ev->time_ns, ev->packet, ev->len, q->flags, q->iend, q->dnext, q->cur,
-                q->prev, q->bytes, q->head, q->tail, q->ring_pkt, q->ring_ts, q->ring_len, q->cap, pop_result,
+                q->prev, q->bytes, q->head, q->tail, q->ring, q->cap, pop_result,
                 pkt_status, n_packets, ctx->d_blk.get<unsigned long long>(2 * (size_t)nb)};
     {
       // per event: 17 B in, 4 B result, ring slot 16 B written (push) or read (pop), 1 B status
@@ -413,11 +403,17 @@ int32_t sg_codel_get_state(sg_codel* q, sg_codel_state* o) {
     struct { void* h; const void* d; size_t b; } cp[] = {
         {o->flags, q->flags, n}, {o->interval_end, q->iend, n * 8}, {o->drop_next, q->dnext, n * 8},
         {o->cur_drops, q->cur, n * 8}, {o->prev_drops, q->prev, n * 8}, {o->bytes, q->bytes, n * 8},
-        {o->head, q->head, n * 4}, {o->tail, q->tail, n * 4}, {o->ring_packet, q->ring_pkt, r * 4},
-        {o->ring_time, q->ring_ts, r * 8}, {o->ring_len, q->ring_len, r * 4}};
+        {o->head, q->head, n * 4}, {o->tail, q->tail, n * 4}};
     for (auto& c : cp)
       if (c.h && c.b) SG_HIP(hipMemcpyAsync(c.h, c.d, c.b, hipMemcpyDeviceToHost, st));
+    std::vector<uint4> ring(r);
+    if (r) SG_HIP(hipMemcpyAsync(ring.data(), q->ring, r * 16, hipMemcpyDeviceToHost, st));
     SG_HIP(hipStreamSynchronize(st));
+    for (size_t i = 0; i < r; i++) {
+      if (o->ring_packet) o->ring_packet[i] = ring[i].x;
+      if (o->ring_len) o->ring_len[i] = ring[i].y;
+      if (o->ring_time) o->ring_time[i] = ((uint64_t)ring[i].w << 32) | ring[i].z;
+    }
   });
 }
 
@@ -429,10 +425,17 @@ int32_t sg_codel_set_state(sg_codel* q, const sg_codel_state* in) {
     struct { void* d; const void* h; size_t b; } cp[] = {
         {q->flags, in->flags, n}, {q->iend, in->interval_end, n * 8}, {q->dnext, in->drop_next, n * 8},
         {q->cur, in->cur_drops, n * 8}, {q->prev, in->prev_drops, n * 8}, {q->bytes, in->bytes, n * 8},
-        {q->head, in->head, n * 4}, {q->tail, in->tail, n * 4}, {q->ring_pkt, in->ring_packet, r * 4},
-        {q->ring_ts, in->ring_time, r * 8}, {q->ring_len, in->ring_len, r * 4}};
+        {q->head, in->head, n * 4}, {q->tail, in->tail, n * 4}};
     for (auto& c : cp)
       if (c.h && c.b) SG_HIP(hipMemcpyAsync(c.d, c.h, c.b, hipMemcpyHostToDevice, st));
+    if (in->ring_packet && in->ring_time && in->ring_len && r) {
+      std::vector<uint4> ring(r);
+      for (size_t i = 0; i < r; i++)
+        ring[i] = make_uint4(in->ring_packet[i], in->ring_len[i], (uint32_t)in->ring_time[i],
+                             (uint32_t)(in->ring_time[i] >> 32));
+      SG_HIP(hipMemcpyAsync(q->ring, ring.data(), r * 16, hipMemcpyHostToDevice, st));
+      SG_HIP(hipStreamSynchronize(st));  // before `ring` goes out of scope
+    }
     SG_HIP(hipStreamSynchronize(st));
   });
 }
