@@ -314,16 +314,24 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
 // Round statistics: sum / min / min over the walk blocks' partials, written
 // with the source phase's error flags straight into the context's pinned
 // host-mapped return block.  Clears the flags (for the next round) and the
-// big-slot counter (for this round's bucketing, which runs next).
-__global__ void __launch_bounds__(1024) k_reduce_stats(const unsigned long long* __restrict__ blk, uint32_t n,
-                                                       uint32_t* __restrict__ err, uint32_t* __restrict__ big_count,
-                                                       sg_round_ret* __restrict__ ret) {
-  __shared__ unsigned long long r[3][16];
+// big-slot counter (for this round's bucketing, which runs next).  One block:
+// k_reduce_stats, or the extra block of the region scatter (StatsJob).
+struct StatsJob {
+  const unsigned long long* blk;  // null: nothing to reduce
+  uint32_t n;
+  uint32_t* err;
+  uint32_t* big_count;
+  sg_round_ret* ret;
+};
+
+template <int NT>
+__device__ __forceinline__ void reduce_stats_block(const StatsJob& j) {
+  __shared__ unsigned long long r[3][NT / 64];
   unsigned long long nd = 0, mind = ~0ull, minl = ~0ull;
-  for (uint32_t i = threadIdx.x; i < n; i += 1024) {
-    nd += blk[3 * i];
-    mind = min(mind, blk[3 * i + 1]);
-    minl = min(minl, blk[3 * i + 2]);
+  for (uint32_t i = threadIdx.x; i < j.n; i += NT) {
+    nd += j.blk[3 * i];
+    mind = min(mind, j.blk[3 * i + 1]);
+    minl = min(minl, j.blk[3 * i + 2]);
   }
   for (int d = 32; d > 0; d >>= 1) {
     nd += __shfl_xor(nd, d, 64);
@@ -338,19 +346,21 @@ __global__ void __launch_bounds__(1024) k_reduce_stats(const unsigned long long*
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int i = 1; i < 16; i++) {
+    for (int i = 1; i < NT / 64; i++) {
       nd += r[0][i];
       mind = min(mind, r[1][i]);
       minl = min(minl, r[2][i]);
     }
-    ret->stats[0] = nd;
-    ret->stats[1] = mind;
-    ret->stats[2] = minl;
-    ret->err = *err;
-    *err = 0;
-    *big_count = 0;
+    j.ret->stats[0] = nd;
+    j.ret->stats[1] = mind;
+    j.ret->stats[2] = minl;
+    j.ret->err = *j.err;
+    *j.err = 0;
+    *j.big_count = 0;
   }
 }
+
+__global__ void __launch_bounds__(1024) k_reduce_stats(StatsJob j) { reduce_stats_block<1024>(j); }
 
 __device__ __forceinline__ bool key_less(uint64_t ta, uint64_t ka, uint64_t tb, uint64_t kb) {
   return ta < tb || (ta == tb && ka < kb);
@@ -644,7 +654,11 @@ template <class E, bool REGION>
 __global__ void __launch_bounds__(SBS_THREADS)
     k_sb_scatter(E src, uint32_t n, SbMap sm, uint32_t n_sb, const uint32_t* __restrict__ tile_off,
                  uint32_t* __restrict__ ctl, uint32_t region, uint32_t* __restrict__ rd, uint64_t* __restrict__ rt,
-                 uint64_t* __restrict__ rk, uint32_t* __restrict__ ri) {
+                 uint64_t* __restrict__ rk, uint32_t* __restrict__ ri, StatsJob stats) {
+  if (stats.blk && blockIdx.x == gridDim.x - 1) {  // the extra block: the round's stats (saves a launch)
+    reduce_stats_block<SBS_THREADS>(stats);
+    return;
+  }
   constexpr int PER = SB_TILE / SBS_THREADS;
   __shared__ uint32_t lcur[SB_MAX];   // local start, then cursor
   __shared__ uint32_t lbase[SB_MAX];  // global position of the run - local start
@@ -970,9 +984,14 @@ __global__ void __launch_bounds__(SBT_THREADS)
 // that overfill a super-bucket's region; big_count zeroed again first).
 template <class E>
 static bool bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32_t* offsets, uint32_t* order,
-                        uint32_t* big_count, bool region) {
+                        uint32_t* big_count, bool region, StatsJob stats = StatsJob{}) {
   hipStream_t st = ctx->stream;
+  auto stats_alone = [&] {  // the round's stats when no region scatter carries them
+    if (stats.blk) hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(1024), 0, st, stats);
+    stats.blk = nullptr;
+  };
   if (n_slots == 0) {
+    stats_alone();
     SG_HIP(hipMemsetAsync(offsets, 0, 4, st));
     return false;
   }
@@ -988,6 +1007,7 @@ static bool bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
   const uint32_t n_tiles = std::max<uint32_t>(1, (n + SB_TILE - 1) / SB_TILE);
   const char* env = getenv("SG_BUCKET_REGION");
   region = region && n > 0 && !(env && env[0] == '0');
+  if (!region) stats_alone();
   const uint32_t reg = SB_CAP<E::KK>;  // a region is sorted in LDS in one piece
   const size_t cap = region ? std::max<size_t>((size_t)n_sb * reg, n) : n;
   uint32_t* rd = ctx->d_lists2.get<uint32_t>(cap);
@@ -1005,8 +1025,8 @@ static bool bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
     ctx->sb_parity ^= 1;
     {
       TimedLaunch tl(ctx, "scatter", 32.0 * n);
-      hipLaunchKernelGGL((k_sb_scatter<E, true>), dim3(n_tiles), dim3(SBS_THREADS), 0, st, src, n, sm, n_sb, nullptr,
-                         ctl, reg, rd, rt, rk, ri);
+      hipLaunchKernelGGL((k_sb_scatter<E, true>), dim3(n_tiles + (stats.blk ? 1 : 0)), dim3(SBS_THREADS), 0, st, src,
+                         n, sm, n_sb, nullptr, ctl, reg, rd, rt, rk, ri, stats);
     }
     {
       TimedLaunch tl(ctx, "sort_small", 24.0 * n + 4.0 * n_slots);
@@ -1025,7 +1045,7 @@ static bool bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
       exclusive_scan_u32(ctx, hist, toff, (uint32_t)nh);
       if (n)
         hipLaunchKernelGGL((k_sb_scatter<E, false>), dim3(n_tiles), dim3(SBS_THREADS), 0, st, src, n, sm, n_sb, toff,
-                           nullptr, 0u, rd, rt, rk, ri);
+                           nullptr, 0u, rd, rt, rk, ri, StatsJob{});
     }
     {
       TimedLaunch tl(ctx, "sort_small", 48.0 * n + 4.0 * n_slots);
@@ -1052,14 +1072,15 @@ static bool bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
 struct RoundWork {
   uint32_t *host_off, *big_count, *dst_host;
   uint64_t* ctr_start;
-  bool walked;  // the walk and the stats kernel ran (P > 0)
+  bool walked;     // the walk ran and its stats reach round_ret (P > 0)
+  StatsJob stats;  // set when the caller launches the stats reduction (fused)
 };
 
 // Shared source half of a round: host offsets + walk.  Leaves per-packet
 // dst_host (NONE unless delivered) and the round stats.
 static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const sg_round* rd,
                               const sg_packets* pk, uint8_t* status, uint64_t* deliver, uint64_t* eid,
-                              bool want_ctr_start) {
+                              bool want_ctr_start, bool fuse_stats = false) {
   hipStream_t st = ctx->stream;
   const uint32_t P = pk->n_packets, H = hs->n;
   RoundWork w;
@@ -1072,6 +1093,7 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   w.dst_host = ctx->d_dst.get<uint32_t>(P);
   w.ctr_start = want_ctr_start ? ctx->d_ctr0.get<uint64_t>(H) : nullptr;
   w.walked = P > 0;
+  w.stats = StatsJob{};
   if (w.ctr_start) SG_HIP(hipMemcpyAsync(w.ctr_start, hs->ctr, (size_t)H * 8, hipMemcpyDeviceToDevice, st));
   if (!P) {
     SG_HIP(hipMemsetAsync(w.big_count, 0, 4, st));
@@ -1119,8 +1141,11 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
     else
       hipLaunchKernelGGL(k_walk<false>, dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
   }
-  hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(1024), 0, st, a.blk_stats, walk_blocks, ctx->round_err,
-                     w.big_count, ctx->round_ret);
+  const StatsJob sj{a.blk_stats, walk_blocks, ctx->round_err, w.big_count, ctx->round_ret};
+  if (fuse_stats)
+    w.stats = sj;
+  else
+    hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(1024), 0, st, sj);
   SG_CHECK_LAUNCH();
   return w;
 }
@@ -1145,9 +1170,9 @@ static void finish(sg_ctx* ctx, const RoundWork& w, sg_round_stats* stats) {
 static void deliver_round(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const sg_round* rd,
                           const sg_packets* pk, sg_deliveries* out, sg_round_stats* stats) {
   const uint32_t P = pk->n_packets, H = hs->n;
-  RoundWork w = source_phase(ctx, hs, tab, rd, pk, out->status, out->deliver_time_ns, out->event_id, false);
+  RoundWork w = source_phase(ctx, hs, tab, rd, pk, out->status, out->deliver_time_ns, out->event_id, false, true);
   const PacketEntries E{w.dst_host, out->deliver_time_ns};
-  const bool region = bucket_sort(ctx, E, P, H, out->dst_offsets, out->dst_order, w.big_count, true);
+  const bool region = bucket_sort(ctx, E, P, H, out->dst_offsets, out->dst_order, w.big_count, true, w.stats);
   finish(ctx, w, stats);
   if (region && ctx->round_ret->overflow) {  // a hot destination overfilled its region
     SG_HIP(hipMemsetAsync(w.big_count, 0, 4, ctx->stream));
