@@ -544,7 +544,8 @@ static void fail_flags(uint32_t err) {
 constexpr int SB_THREADS = 256;
 constexpr int SB_TILE = 4096;        // entries per hist / scatter block
 constexpr int SB_MAX = 4096;         // super-buckets (LDS histogram bins)
-static_assert(SB_MAX + 1 == SB_CTL_STRIDE, "region counters: SB_MAX counts + the overflow flag");
+static_assert(SB_SUB * SB_MAX + 1 == SB_CTL_STRIDE, "region counters: SB_SUB x SB_MAX counts + the overflow flag");
+constexpr uint32_t SB_FLAG = SB_SUB * SB_MAX;  // overflow flag word
 constexpr int SB_SLOTS_MAX = 1024;   // slots per super-bucket
 // entries a super-bucket sorts in LDS, and the mean entries per super-bucket
 // aimed for: 14 B of LDS per entry without a separate order key, 22 B with one
@@ -646,8 +647,11 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* a, uint32_t n
 // (coalesced stores instead of one scattered store per entry and array).
 // REGION: instead of the (super-bucket, tile) scan, a tile claims each run in
 // its super-bucket's fixed region of `region` entries with one atomic per
-// (tile, super-bucket); a run that would overflow the region is dropped and
-// flagged in ctl[SB_MAX] (the host then reruns the scan path).
+// (tile, super-bucket).  The region is split into SB_SUB sub-regions, one per
+// XCD (blockIdx % 8 under round-robin dispatch), each with its own counter, so
+// a counter sees an eighth of the tiles' atomics.  A run that would overflow
+// its sub-region is dropped and flagged in ctl[SB_FLAG] (the host then reruns
+// the scan path).
 constexpr int SBS_THREADS = 512;
 constexpr uint32_t RUN_DROPPED = 0xFFFFFFFFu;  // cannot be a valid run base (see below)
 template <class E, bool REGION>
@@ -689,17 +693,18 @@ __global__ void __launch_bounds__(SBS_THREADS)
   const uint32_t total = block_exclusive_scan<SBS_THREADS, SB_MAX / SBS_THREADS>(lcur, n_sb, wsum);
   for (uint32_t i = threadIdx.x; i < n_sb; i += SBS_THREADS) {
     if (REGION) {
-      // the run of super-bucket i: local [lcur[i], lcur[i] + c) -> region slot g..g+c.
-      // A kept base is i * region + g - lcur[i] with lcur[i] <= g + i * region
-      // (i = 0: lcur[0] = 0), never RUN_DROPPED.
+      // the run of super-bucket i: local [lcur[i], lcur[i] + c) -> sub-region slot g..g+c.
+      // A kept base is i * region + sub * subcap + g - lcur[i] >= 0 (i = 0: lcur[0] = 0;
+      // i > 0: lcur[i] <= SB_TILE <= region), never RUN_DROPPED.
       const uint32_t c = (i + 1 < n_sb ? lcur[i + 1] : total) - lcur[i];
+      const uint32_t sub = blockIdx.x & (SB_SUB - 1), subcap = region / SB_SUB;
       uint32_t base = RUN_DROPPED;
       if (c) {
-        const uint32_t g = atomicAdd(&ctl[i], c);
-        if (g + c <= region)
-          base = i * region + g - lcur[i];
+        const uint32_t g = atomicAdd(&ctl[sub * SB_MAX + i], c);
+        if (g + c <= subcap)
+          base = i * region + sub * subcap + g - lcur[i];
         else
-          ctl[SB_MAX] = 1u;
+          ctl[SB_FLAG] = 1u;
       }
       lbase[i] = base;
     } else {
@@ -902,10 +907,11 @@ __global__ void __launch_bounds__(SBT_THREADS)
                    slot_spill);
 }
 
-// Region path: super-bucket sb's entries are [sb * region, sb * region + count[sb])
-// (k_sb_scatter_region); its output position is the sum of the counts before
-// it.  The block does nothing if a region overflowed (the host then reruns the
-// scan path); every block clears a share of the other parity's counters.
+// Region path: super-bucket sb's entries are SB_SUB runs, sub-region k holding
+// [sb * region + k * subcap, + count[k][sb]) (k_sb_scatter<E, true>); its output
+// position is the sum of all counts of the super-buckets before it.  The block
+// does nothing if a sub-region overflowed (the host then reruns the scan
+// path); every block clears a share of the other parity's counters.
 template <bool KK>
 __global__ void __launch_bounds__(SBT_THREADS)
     k_sb_sort_region(SbMap sm, uint32_t n_slots, uint32_t n_sb, const uint32_t* __restrict__ ctl,
@@ -916,19 +922,29 @@ __global__ void __launch_bounds__(SBT_THREADS)
                      uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count,
                      uint16_t* __restrict__ slot_spill, sg_round_ret* __restrict__ ret) {
   __shared__ uint32_t part[SBT_THREADS / 64];
-  for (uint32_t i = blockIdx.x * SBT_THREADS + threadIdx.x; i <= SB_MAX; i += gridDim.x * SBT_THREADS) ctl_next[i] = 0;
-  const uint32_t over = ctl[SB_MAX];
+  for (uint32_t i = blockIdx.x * SBT_THREADS + threadIdx.x; i <= SB_FLAG; i += gridDim.x * SBT_THREADS)
+    ctl_next[i] = 0;
+  const uint32_t over = ctl[SB_FLAG];
   if (blockIdx.x == 0 && threadIdx.x == 0) ret->overflow = over;
   if (over) return;  // uniform across the grid
-  const uint32_t sb = blockIdx.x;
+  const uint32_t sb = blockIdx.x, subcap = region / SB_SUB;
   uint32_t before = 0;
-  for (uint32_t i = threadIdx.x; i < sb; i += SBT_THREADS) before += ctl[i];
+  for (uint32_t i = threadIdx.x; i < sb; i += SBT_THREADS)  // coalesced per sub-counter array
+#pragma unroll
+    for (int k = 0; k < (int)SB_SUB; k++) before += ctl[k * SB_MAX + i];
   for (int dd = 32; dd > 0; dd >>= 1) before += __shfl_xor(before, dd, 64);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = before;
   __syncthreads();
   uint32_t s0 = 0;
   for (int w = 0; w < SBT_THREADS / 64; w++) s0 += part[w];
-  const uint32_t in0 = sb * region, ns = ctl[sb];  // ns <= region = SB_CAP (no overflow)
+  uint32_t sub_end[SB_SUB];  // running totals of the SB_SUB runs (wave-uniform)
+  uint32_t ns = 0;
+#pragma unroll
+  for (int k = 0; k < (int)SB_SUB; k++) {
+    ns += ctl[k * SB_MAX + sb];
+    sub_end[k] = ns;
+  }
+  const uint32_t in0 = sb * region;  // ns <= region = SB_CAP (no overflow)
   constexpr int CAP = SB_CAP<KK>;
   constexpr int PER = (CAP + SBT_THREADS - 1) / SBT_THREADS;
   __shared__ uint32_t cnt[SB_SLOTS_MAX + 1];
@@ -947,10 +963,18 @@ __global__ void __launch_bounds__(SBT_THREADS)
     const uint32_t e = threadIdx.x + k * SBT_THREADS;
     vd[k] = NONE;
     if (e < ns) {
-      vd[k] = rd[in0 + e] - d0;
-      vt[k] = rt[in0 + e];
-      vi[k] = ri[in0 + e];
-      if (KK) vk[k] = rk[in0 + e];
+      uint32_t sub = 0, start = 0;  // entry e lies in the first run whose running total exceeds it
+#pragma unroll
+      for (int j = 0; j < (int)SB_SUB - 1; j++)
+        if (e >= sub_end[j]) {
+          sub = j + 1;
+          start = sub_end[j];
+        }
+      const uint32_t x = in0 + sub * subcap + (e - start);
+      vd[k] = rd[x] - d0;
+      vt[k] = rt[x];
+      vi[k] = ri[x];
+      if (KK) vk[k] = rk[x];
     }
   }
   for (uint32_t j = threadIdx.x; j <= nd; j += SBT_THREADS) cnt[j] = 0;

@@ -142,8 +142,10 @@ int32_t guarded(sg_ctx* ctx, F&& fn) {
   }
 }
 
-// Region bucketing counters per parity: SB_MAX (4096) super-bucket counts + an overflow flag.
-constexpr uint32_t SB_CTL_STRIDE = 4097;
+// Region bucketing counters per parity: 8 sub-counters (one per XCD) x SB_MAX
+// (4096) super-buckets + an overflow flag.
+constexpr uint32_t SB_SUB = 8;
+constexpr uint32_t SB_CTL_STRIDE = SB_SUB * 4096 + 1;
 
 inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 1u << 20) {
   size_t g = (n + block - 1) / block;
