@@ -258,3 +258,14 @@ def test_pack_refuses_wide_latency(oracle, ctx):
     want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, end, end + 10**12, 0)
     assert want["delivered"] > 0
     _assert_same(want, got, ost, gst)
+
+
+def test_c5_packet_count_round(oracle, ctx):
+    """10M packets in one round (the C5 packet count) over 60k hosts: the region
+    bucketing runs near its super-bucket limit (3750 of 4096)."""
+    lat, loss, hosts = _world(n_nodes=500, n_hosts=60000, seed=21)
+    start, end = T0 + 10**9, T0 + 10**9 + 10**6
+    pk = synth.make_packets(10_000_000, hosts, start, end, seed=21, p_unknown_dst=0.001)
+    want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, end, 2**63, 0)
+    assert want["delivered"] > 9_000_000
+    _assert_same(want, got, ost, gst)

@@ -192,3 +192,13 @@ def test_kernel_variants_bit_exact(oracle, ctx, monkeypatch, env):
     g = synth.ring_chords_graph(900, 7.0, seed=21, parallel=0.03)
     used = np.random.default_rng(21).permutation(900)[:612].astype(np.uint32)
     _check(oracle, g, used, ctx)
+
+
+def test_c5_scale_row_samples(oracle, ctx):
+    """C5 scale: a 50k-node ring + chords graph, mean degree 8, all
+    nodes used.  Row blocks at the start, middle and end of the table, bit-exact
+    against the oracle's Dijkstra rows."""
+    g = synth.ring_chords_graph(50000, 8.0, seed=5)
+    used = np.arange(50000, dtype=np.uint32)
+    for rows in ((0, 128), (25000, 25064), (49936, 50000)):
+        _check(oracle, g, used, ctx, rows=rows)
