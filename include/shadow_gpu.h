@@ -311,6 +311,53 @@ uint32_t sg_codel_ring_cap(const sg_codel* q);
 int32_t sg_codel_get_state(sg_codel* q, sg_codel_state* out);
 int32_t sg_codel_set_state(sg_codel* q, const sg_codel_state* in);
 
+/* ---- inbound pipeline: router CoDel queue -> relay_inet_in (token bucket) --
+ * Host::execute on a Packet event (host.rs:781-786): the packet enters the
+ * router's CoDel queue and the inbound relay is notified; the relay
+ * (relay/mod.rs:72-288) forwards from the queue to the host's internet
+ * interface as its token bucket allows (relay/token_bucket.rs: refill
+ * max(1, bw_down_bytes / 1000) every 1 ms, capacity refill + MTU,
+ * relay/mod.rs:296-309), rescheduling itself when blocked.  A call processes
+ * one host's arrivals (a delivery round's buckets, in EventQueue order) and the
+ * relay's forward tasks up to window_end; later tasks stay pending.  Assumes
+ * Shadow's CPU-delay model is off (host.rs:758-775; its default).           */
+typedef struct sg_inbound sg_inbound;
+/* bw_down_bits (host, n_hosts): each host's bandwidth down (HostInfo, bits/s). */
+int32_t sg_inbound_create(sg_ctx* ctx, uint32_t n_hosts, const uint64_t* bw_down_bits, uint32_t ring_cap,
+                          sg_inbound** out);
+void sg_inbound_destroy(sg_inbound* ib);
+uint32_t sg_inbound_ring_cap(const sg_inbound* ib);
+
+typedef struct sg_inbound_arrivals { /* device arrays, grouped by ascending host, EventQueue order */
+  uint32_t n;
+  const uint32_t* host;
+  const uint64_t* time_ns; /* the Packet event's time (the delivery's arrival), < window_end */
+  const uint32_t* packet;  /* the caller's packet id (< n_packets) */
+  const uint32_t* len;     /* PacketRc::len() */
+} sg_inbound_arrivals;
+
+/* event_ctr (device, n_hosts, may be NULL): each host's event-id counter,
+ * advanced by one per forward task the relay schedules (host.rs:649-653) --
+ * e.g. sg_hosts_event_ctr(hosts).  fwd_time (device, n_packets): the time the
+ * relay pushed the packet to the interface; pkt_status (device, n_packets):
+ * SG_CODEL_DEQUEUED once forwarded, SG_CODEL_DROPPED if CoDel dropped it.
+ * n_dropped (host, may be NULL): CoDel drops in this call. */
+int32_t sg_inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* arr, uint64_t window_end_ns,
+                       uint64_t bootstrap_end_ns, uint64_t sim_end_ns, uint64_t* event_ctr, uint64_t* fwd_time,
+                       uint8_t* pkt_status, uint32_t n_packets, uint64_t* n_dropped);
+
+typedef struct sg_inbound_relay_state { /* host arrays, n_hosts each */
+  uint8_t* flags;          /* bit 0 a forward task is pending, bit 1 it was never queued (>= sim_end),
+                              bit 2 a packet is cached (RelayCached) */
+  uint64_t* task_time;
+  uint32_t *cached_packet, *cached_len;
+  uint64_t *tb_capacity, *tb_balance, *tb_increment, *tb_last_refill;
+} sg_inbound_relay_state;
+int32_t sg_inbound_get_state(sg_inbound* ib, sg_codel_state* queue, sg_inbound_relay_state* relay);
+
+/* The device array of the hosts' event-id counters (Host::event_id_counter). */
+uint64_t* sg_hosts_event_ctr(sg_hosts* hosts);
+
 #ifdef __cplusplus
 }
 #endif

@@ -63,6 +63,11 @@ def lib():
         L.sgo_codel_run.argtypes = [C.c_uint32, C.c_uint32] + [C.c_void_p] * 11 + [C.c_uint32] + [C.c_void_p] * 7 + [
             C.c_uint32]
         L.sgo_codel_run.restype = C.c_int
+        L.sgo_token_bucket_remove.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.sgo_token_bucket_remove.restype = C.c_int
+        L.sgo_inbound_run.argtypes = [C.c_uint32, C.c_uint32] + [C.c_void_p] * 19 + [C.c_uint32] + \
+            [C.c_void_p] * 4 + [C.c_uint64] * 3 + [C.c_void_p] * 3 + [C.c_uint32]
+        L.sgo_inbound_run.restype = C.c_int
         L.sgo_deliver_round.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u32p, u32p, u32p, u64p,
                                         C.c_uint32, u32p, u32p, C.c_uint32, u64p, f32p, u64p, u64p, u8p, u64p,
                                         u64p, u32p, u32p, u64p, u64p]
@@ -228,3 +233,46 @@ def codel_run(state: dict, host, kind, time, pkt, length, pkt_status: np.ndarray
     if rc:
         raise ValueError(f"sgo_codel_run: error {rc}")
     return res[:n]
+
+
+# ---------------------------------------------------------------------------
+# Inbound pipeline: router CoDel queue -> relay_inet_in token bucket
+# ---------------------------------------------------------------------------
+RL_PENDING, RL_NEVER, RL_CACHED = 1, 2, 4
+TB_INTERVAL_NS = 1_000_000   # relay/mod.rs:297
+
+
+def token_bucket_remove(state: np.ndarray, dec: int, now: int):
+    """TokenBucket::conforming_remove_inner on state = u64[5] {capacity, balance,
+    refill_increment, last_refill, refill_interval}: (True, balance) or (False, wait)."""
+    assert state.dtype == np.uint64 and len(state) == 5
+    w = C.c_uint64()
+    ok = lib().sgo_token_bucket_remove(state.ctypes.data_as(C.c_void_p), dec, now, C.byref(w))
+    return (True, int(state[1])) if ok else (False, int(w.value))
+
+
+def inbound_state(bw_down_bits: np.ndarray, cap: int, t0: int = 946684800 * 10**9) -> dict:
+    """Empty router queues + Idle relays with full buckets (Relay::new / create_token_bucket,
+    relay/mod.rs:296-309: refill max(1, B/1000) bytes per 1 ms, capacity refill + MTU)."""
+    n = len(bw_down_bits)
+    st = codel_state(n, cap)
+    refill = np.maximum(1, (np.asarray(bw_down_bits, np.uint64) // np.uint64(8)) // np.uint64(1000)).astype(np.uint64)
+    st.update(rflags=np.zeros(n, np.uint8), task_time=np.zeros(n, np.uint64), cached_pkt=np.zeros(n, np.uint32),
+              cached_len=np.zeros(n, np.uint32), tb_cap=refill + np.uint64(CODEL_MTU), tb_bal=refill + np.uint64(CODEL_MTU),
+              tb_inc=refill, tb_last=np.full(n, t0, np.uint64))
+    return st
+
+
+def inbound_run(st: dict, host, time, pkt, length, window_end: int, bootstrap_end: int, sim_end: int,
+                event_ctr: np.ndarray, fwd_time: np.ndarray, pkt_status: np.ndarray) -> None:
+    host, time = _arr(host, np.uint32), _arr(time, np.uint64)
+    pkt, length = _arr(pkt, np.uint32), _arr(length, np.uint32)
+    v = lambda a: a.ctypes.data_as(C.c_void_p)
+    H = len(st["flags"])
+    rc = lib().sgo_inbound_run(H, st["cap"], *[v(st[k]) for k in (
+        "flags", "interval_end", "drop_next", "cur", "prev", "bytes", "head", "tail", "ring_pkt", "ring_ts",
+        "ring_len", "rflags", "task_time", "cached_pkt", "cached_len", "tb_cap", "tb_bal", "tb_inc", "tb_last")],
+        len(host), v(host), v(time), v(pkt), v(length), window_end, bootstrap_end, sim_end, v(event_ctr),
+        v(fwd_time), v(pkt_status), len(pkt_status))
+    if rc:
+        raise ValueError(f"sgo_inbound_run: error {rc}")

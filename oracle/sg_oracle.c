@@ -793,3 +793,172 @@ int sgo_codel_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* iend
   }
   return e == n_events ? 0 : -4;  /* -4: events not grouped by ascending host (or host >= n_hosts) */
 }
+
+/* ------------------------------------------------------------------------- */
+/* Inbound pipeline: router CoDel queue -> relay_inet_in (token bucket)      */
+/* ------------------------------------------------------------------------- */
+/* Per host, over a window of simulated time (relay/mod.rs, relay/token_bucket.rs,
+ * host.rs:781-786 and :903-924):
+ *   a Packet event at t (the delivery's arrival, EventQueue order) pushes the
+ *   packet into the router's CoDel queue and notifies relay_inet_in; an Idle
+ *   relay schedules its forward task at t (a Local event: after every Packet
+ *   event at t, event.rs:103-112; it takes an event id, host.rs:649-653);
+ *   the task pops the queue until it is empty or the token bucket blocks, and
+ *   then reschedules itself after the conforming duration.
+ * Relay state per host: rflags bit0 Pending, bit1 the pending task was never
+ * queued (at or after sim_end, host.rs:703-709), bit2 a cached packet
+ * (RelayCached); task_time, cached packet/len; token bucket capacity, balance,
+ * refill increment, last refill (1 ms interval, token_bucket.rs:20-60,
+ * relay/mod.rs:296-309).
+ * fwd_time[packet] = the time the relay pushed it to the interface
+ * (RelayForwarded) -- status 1 -- or status 2 when CoDel dropped it. */
+#define TB_INTERVAL 1000000ull /* relay/mod.rs:297 refill every 1 ms */
+enum { RL_PENDING = 1, RL_NEVER = 2, RL_CACHED = 4 };
+
+typedef struct {
+  uint64_t cap, bal, inc, last, interval;
+} tb_t;
+
+/* lazy_refill (token_bucket.rs:124-158): returns the span to the next refill */
+static uint64_t tb_lazy_refill(tb_t* b, uint64_t now) {
+  uint64_t span = now - b->last; /* duration_since: now >= last_refill */
+  if (span >= b->interval) {
+    const uint64_t n = span / b->interval;
+    const uint64_t tokens = (b->inc != 0 && n > UINT64_MAX / b->inc) ? UINT64_MAX : b->inc * n;
+    uint64_t bal = (b->bal > UINT64_MAX - tokens) ? UINT64_MAX : b->bal + tokens;
+    b->bal = bal > b->cap ? b->cap : bal;
+    const uint64_t inc = (n > UINT64_MAX / b->interval) ? UINT64_MAX : b->interval * n;
+    b->last = cd_sat_add(b->last, inc);
+    span = now - b->last;
+  }
+  return b->interval - span;
+}
+
+/* conforming_remove (token_bucket.rs:76-86): 1 and balance -= dec, or 0 and *wait */
+static int tb_remove(tb_t* b, uint64_t dec, uint64_t now, uint64_t* wait) {
+  const uint64_t next = tb_lazy_refill(b, now);
+  if (b->bal >= dec) {
+    b->bal -= dec;
+    return 1;
+  }
+  const uint64_t need = dec > b->bal ? dec - b->bal : 0; /* compute_conforming_duration (:93-118) */
+  const uint64_t nref = need / b->inc + (need % b->inc ? 1 : 0);
+  if (nref == 0) *wait = 0;
+  else if (nref == 1) *wait = next;
+  else {
+    const uint64_t m = nref - 1;
+    const uint64_t extra = (m > UINT64_MAX / b->interval) ? UINT64_MAX : b->interval * m;
+    *wait = next > UINT64_MAX - extra ? UINT64_MAX : next + extra;
+  }
+  return 0;
+}
+
+int sgo_inbound_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* iend, uint64_t* dnext,
+                    uint64_t* cur, uint64_t* prev, uint64_t* bytes, uint32_t* head, uint32_t* tail,
+                    uint32_t* ring_pkt, uint64_t* ring_ts, uint32_t* ring_len, uint8_t* rflags, uint64_t* task_time,
+                    uint32_t* cached_pkt, uint32_t* cached_len, uint64_t* tb_cap, uint64_t* tb_bal,
+                    uint64_t* tb_inc, uint64_t* tb_last, uint32_t n_arr, const uint32_t* host,
+                    const uint64_t* time, const uint32_t* pkt, const uint32_t* len, uint64_t window_end,
+                    uint64_t bootstrap_end, uint64_t sim_end, uint64_t* event_ctr, uint64_t* fwd_time,
+                    uint8_t* pkt_status, uint32_t n_status) {
+  if (!cap) return -1;
+  uint32_t e = 0;
+  for (uint32_t h = 0; h < n_hosts; h++) {
+    cd_q q = {flags[h], iend[h], dnext[h], cur[h], prev[h], bytes[h], head[h], tail[h],
+              ring_pkt + (size_t)h * cap, ring_ts + (size_t)h * cap, ring_len + (size_t)h * cap, cap,
+              pkt_status, n_status, 0};
+    tb_t tb = {tb_cap[h], tb_bal[h], tb_inc[h], tb_last[h], TB_INTERVAL};
+    uint8_t rf = rflags[h];
+    uint64_t tt = task_time[h];
+    uint32_t cp = cached_pkt[h], cl = cached_len[h];
+    uint32_t e1 = e;
+    while (e1 < n_arr && host[e1] == h) e1++;
+    for (;;) {
+      const int has_arr = e < e1;
+      const int has_task = (rf & RL_PENDING) && !(rf & RL_NEVER) && tt < window_end;
+      if (has_arr && time[e] >= window_end) return -5; /* arrivals must precede the window end */
+      if (has_arr && (!has_task || time[e] <= tt)) { /* Packet event (before a Local one at equal time) */
+        const uint64_t now = time[e];
+        if (q.tail - q.head >= cap) return -2;
+        const uint32_t slot = q.tail % cap;
+        q.rpkt[slot] = pkt[e];
+        q.rts[slot] = now;
+        q.rlen[slot] = len[e];
+        q.tail++;
+        q.bytes += len[e];
+        if (!(rf & RL_PENDING)) { /* notify: Idle -> forward_later(ZERO) */
+          event_ctr[h]++;
+          rf |= RL_PENDING;
+          if (now >= sim_end) rf |= RL_NEVER;
+          tt = now;
+        }
+        e++;
+      } else if (has_task) { /* the relay's forward task at tt */
+        const uint64_t now = tt;
+        rf &= (uint8_t)~RL_PENDING; /* run_forward_task: Idle, then forward_now */
+        for (;;) {
+          uint32_t p, l;
+          if (rf & RL_CACHED) {
+            p = cp;
+            l = cl;
+            rf &= (uint8_t)~RL_CACHED;
+          } else {
+            const uint32_t popped = cd_pop(&q, now);
+            if (q.err) return q.err;
+            if (popped == UINT32_MAX) break; /* queue empty: Idle */
+            p = popped;
+            const uint32_t slot = (q.head - 1) % cap; /* the popped element's length */
+            l = q.rlen[slot];
+          }
+          uint64_t wait;
+          if (now >= bootstrap_end && !tb_remove(&tb, l, now, &wait)) {
+            rf |= RL_CACHED; /* RelayCached; forward_later(wait) */
+            cp = p;
+            cl = l;
+            event_ctr[h]++;
+            rf |= RL_PENDING;
+            const uint64_t at = now > UINT64_MAX - wait ? UINT64_MAX : now + wait;
+            if (at >= sim_end) rf |= RL_NEVER;
+            tt = at;
+            break;
+          }
+          if (p < n_status) {
+            pkt_status[p] = 1; /* RelayForwarded -> the interface */
+            fwd_time[p] = now;
+          } else {
+            return -3;
+          }
+        }
+      } else {
+        break;
+      }
+    }
+    if (e != e1) return -4;
+    flags[h] = q.flags;
+    iend[h] = q.iend;
+    dnext[h] = q.dnext;
+    cur[h] = q.cur;
+    prev[h] = q.prev;
+    bytes[h] = q.bytes;
+    head[h] = q.head;
+    tail[h] = q.tail;
+    rflags[h] = rf;
+    task_time[h] = tt;
+    cached_pkt[h] = cp;
+    cached_len[h] = cl;
+    tb_bal[h] = tb.bal;
+    tb_last[h] = tb.last;
+  }
+  return e == n_arr ? 0 : -4;
+}
+
+/* Test hook: TokenBucket::conforming_remove_inner on an explicit state
+ * {capacity, balance, refill_increment, last_refill, refill_interval}.
+ * Returns 1 (ok, balance updated) or 0 (*wait = conforming duration). */
+int sgo_token_bucket_remove(uint64_t* st, uint64_t dec, uint64_t now, uint64_t* wait) {
+  tb_t b = {st[0], st[1], st[2], st[3], st[4]};
+  const int ok = tb_remove(&b, dec, now, wait);
+  st[1] = b.bal;
+  st[3] = b.last;
+  return ok;
+}

@@ -39,7 +39,8 @@ EXPORTED = [
     "sg_routing_min_latency", "sg_hosts_create", "sg_hosts_get_state", "sg_hosts_set_state",
     "sg_hosts_destroy", "sg_deliver_round", "sg_deliver_source", "sg_deliver_bucket",
     "sg_table_pack", "sg_codel_create", "sg_codel_destroy", "sg_codel_run", "sg_codel_ring_cap",
-    "sg_codel_get_state", "sg_codel_set_state",
+    "sg_codel_get_state", "sg_codel_set_state", "sg_inbound_create", "sg_inbound_destroy", "sg_inbound_ring_cap",
+    "sg_inbound_run", "sg_inbound_get_state", "sg_hosts_event_ctr",
 ]
 
 
@@ -76,6 +77,16 @@ class sg_codel_events(C.Structure):
 class sg_codel_state(C.Structure):
     _fields_ = [(k, C.c_void_p) for k in ("flags", "interval_end", "drop_next", "cur_drops", "prev_drops", "bytes",
                                           "head", "tail", "ring_packet", "ring_time", "ring_len")]
+
+
+class sg_inbound_arrivals(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("host", C.c_void_p), ("time_ns", C.c_void_p), ("packet", C.c_void_p),
+                ("len", C.c_void_p)]
+
+
+class sg_inbound_relay_state(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("flags", "task_time", "cached_packet", "cached_len", "tb_capacity",
+                                          "tb_balance", "tb_increment", "tb_last_refill")]
 
 
 class sg_round(C.Structure):
@@ -159,6 +170,12 @@ def load(path: str | None = None):
         "sg_codel_ring_cap": (u32, [vp]),
         "sg_codel_get_state": (i32, [vp, C.POINTER(sg_codel_state)]),
         "sg_codel_set_state": (i32, [vp, C.POINTER(sg_codel_state)]),
+        "sg_inbound_create": (i32, [vp, u32, vp, u32, C.POINTER(vp)]),
+        "sg_inbound_destroy": (None, [vp]),
+        "sg_inbound_ring_cap": (u32, [vp]),
+        "sg_inbound_run": (i32, [vp, vp, C.POINTER(sg_inbound_arrivals), u64, u64, u64, vp, vp, vp, u32, u64p]),
+        "sg_inbound_get_state": (i32, [vp, C.POINTER(sg_codel_state), C.POINTER(sg_inbound_relay_state)]),
+        "sg_hosts_event_ctr": (vp, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)

@@ -41,7 +41,7 @@ constexpr uint64_t CD_MTU = 1500ull;            // definitions.h:124
 constexpr uint64_t EMU_MAX = ~0ull - 1;         // emulated_time.rs:30 EMUTIME_MAX
 constexpr uint32_t CD_NONE = ~0u;
 enum : uint8_t { F_DROP = 1, F_IEND = 2, F_DNEXT = 4 };
-enum : uint32_t { E_UNSORTED = 1, E_HOST = 2, E_FULL = 16, E_PKT = 32 };
+enum : uint32_t { E_UNSORTED = 1, E_HOST = 2, E_FULL = 16, E_PKT = 32, E_WINDOW = 64 };
 
 __device__ __forceinline__ uint64_t sat_add(uint64_t t, uint64_t d) { return t > EMU_MAX - d ? EMU_MAX : t + d; }
 __device__ __forceinline__ uint64_t since(uint64_t now, uint64_t t) { return now > t ? now - t : 0; }
@@ -62,6 +62,7 @@ struct Q {
   uint32_t head, tail;
   uint32_t hp, hl;
   uint64_t ht;
+  uint32_t last_len;  // length of the element pop_front returned last
   uint4* ring;
   uint32_t mask;
   uint8_t* status;
@@ -92,6 +93,7 @@ struct Q {
       return false;
     }
     pkt = hp;
+    last_len = hl;
     const uint64_t len = hl, ts = ht;
     head++;
     load_head();
@@ -304,6 +306,205 @@ __global__ void __launch_bounds__(1024) k_codel_reduce(const unsigned long long*
   }
 }
 
+// ---- inbound pipeline: router CoDel queue -> relay_inet_in ---------------
+// Per host over a window of simulated time (relay/mod.rs:72-288,
+// relay/token_bucket.rs, host.rs:781-786, :919-924): each arrival (a Packet
+// event, in EventQueue order) pushes into the host's CoDel queue and notifies
+// the inbound relay; an Idle relay schedules its forward task at that time (a
+// Local event: after the Packet events of the same time, event.rs:103-112; it
+// takes an event id, host.rs:649-653).  The task pops until the queue is empty
+// or the token bucket blocks, then reschedules itself after the conforming
+// duration.  Tasks at or after the window end stay pending for the next call.
+constexpr uint64_t TB_INTERVAL = 1000000ull;  // relay/mod.rs:297: refill every 1 ms
+enum : uint8_t { R_PENDING = 1, R_NEVER = 2, R_CACHED = 4 };
+
+struct Relay {
+  uint8_t rf;
+  uint64_t tt;  // pending task time
+  uint32_t cp, cl;  // cached packet, its length
+  uint64_t cap, bal, inc, last;  // token bucket (token_bucket.rs:6-12)
+
+  // lazy_refill (token_bucket.rs:124-158): the span to the next refill
+  __device__ uint64_t lazy_refill(uint64_t now) {
+    uint64_t span = now - last;
+    if (span >= TB_INTERVAL) {
+      const uint64_t n = span / TB_INTERVAL;
+      const uint64_t tokens = (inc != 0 && n > ~0ull / inc) ? ~0ull : inc * n;
+      const uint64_t b = bal > ~0ull - tokens ? ~0ull : bal + tokens;
+      bal = b > cap ? cap : b;
+      last = sat_add(last, n > ~0ull / TB_INTERVAL ? ~0ull : TB_INTERVAL * n);
+      span = now - last;
+    }
+    return TB_INTERVAL - span;
+  }
+  // conforming_remove (token_bucket.rs:76-118)
+  __device__ bool remove(uint64_t dec, uint64_t now, uint64_t& wait) {
+    const uint64_t next = lazy_refill(now);
+    if (bal >= dec) {
+      bal -= dec;
+      return true;
+    }
+    const uint64_t need = dec - bal;
+    const uint64_t nref = need / inc + (need % inc ? 1 : 0);
+    if (nref == 1) {
+      wait = next;
+    } else {
+      const uint64_t m = nref - 1;
+      const uint64_t extra = m > ~0ull / TB_INTERVAL ? ~0ull : TB_INTERVAL * m;
+      wait = next > ~0ull - extra ? ~0ull : next + extra;
+    }
+    return false;
+  }
+};
+
+struct InboundArgs {
+  CodelArgs q;  // queues; q.kind unused (every event is an arrival)
+  uint8_t* rflags;
+  uint64_t* task_time;
+  uint32_t *cached_pkt, *cached_len;
+  uint64_t *tb_cap, *tb_bal, *tb_inc, *tb_last;
+  uint64_t window_end, bootstrap_end, sim_end;
+  uint64_t* event_ctr;  // per host, or null
+  uint64_t* fwd_time;   // per packet
+};
+
+// The relay's forward task at `now` (run_forward_task -> forward_until_blocked).
+__device__ void relay_task(Q& q, Relay& r, uint64_t now, uint64_t bootstrap_end, uint64_t sim_end,
+                           uint64_t& ctr_inc, uint64_t* fwd_time) {
+  r.rf &= (uint8_t)~R_PENDING;
+  for (;;) {
+    uint32_t p, l;
+    if (r.rf & R_CACHED) {
+      p = r.cp;
+      l = r.cl;
+      r.rf &= (uint8_t)~R_CACHED;
+    } else {
+      const uint32_t popped = q.pop(now);
+      if (popped == CD_NONE) return;  // empty: Idle
+      p = popped;
+      l = q.last_len;  // the popped element is the last one pop_front returned
+    }
+    uint64_t wait;
+    if (now >= bootstrap_end && !r.remove(l, now, wait)) {  // Worker::is_bootstrapping: no rate limit
+      r.rf |= R_CACHED | R_PENDING;  // RelayCached; forward_later(wait)
+      r.cp = p;
+      r.cl = l;
+      ctr_inc++;
+      r.tt = now > ~0ull - wait ? ~0ull : now + wait;
+      if (r.tt >= sim_end) r.rf |= R_NEVER;
+      return;
+    }
+    if (p < q.n_status) {  // RelayForwarded: pushed to the internet interface
+      q.status[p] = SG_CODEL_DEQUEUED;
+      fwd_time[p] = now;
+    } else {
+      q.err |= E_PKT;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
+  const CodelArgs& a = ia.q;
+  __shared__ uint64_t s_t[CD_CHUNK];
+  __shared__ uint32_t s_p[CD_CHUNK];
+  __shared__ uint32_t s_l[CD_CHUNK];
+  const uint32_t h0 = blockIdx.x * CD_HOSTS, t = threadIdx.x;
+  const uint32_t p0 = min(a.host_off[min(h0, a.H)], a.E);
+  const uint32_t p1 = max(min(a.host_off[min(h0 + CD_HOSTS, a.H)], a.E), p0);
+  const uint32_t h = h0 + t;
+  const bool walker = t < CD_HOSTS && h < a.H;
+  uint32_t hb = 0, he = 0;
+  Q q{};
+  Relay r{};
+  uint64_t ctr_inc = 0;
+  if (walker) {
+    hb = min(a.host_off[h], a.E);
+    he = max(min(a.host_off[h + 1], a.E), hb);
+    q.flags = a.flags[h];
+    q.iend = a.iend[h];
+    q.dnext = a.dnext[h];
+    q.cur = a.cur[h];
+    q.prev = a.prev[h];
+    q.bytes = a.bytes[h];
+    q.head = a.head[h];
+    q.tail = a.tail[h];
+    q.ring = a.ring + (size_t)h * a.cap;
+    q.mask = a.cap - 1;
+    q.status = a.status;
+    q.n_status = a.n_status;
+    q.load_head();
+    r.rf = ia.rflags[h];
+    r.tt = ia.task_time[h];
+    r.cp = ia.cached_pkt[h];
+    r.cl = ia.cached_len[h];
+    r.cap = ia.tb_cap[h];
+    r.bal = ia.tb_bal[h];
+    r.inc = ia.tb_inc[h];
+    r.last = ia.tb_last[h];
+  }
+  auto due = [&](uint64_t before) {  // a pending task earlier than `before` (Packet events go first)
+    return (r.rf & R_PENDING) && !(r.rf & R_NEVER) && r.tt < before;
+  };
+  for (uint32_t c0 = p0; c0 < p1; c0 += CD_CHUNK) {
+    const uint32_t c1 = min(c0 + CD_CHUNK, p1);
+    for (uint32_t i = c0 + t; i < c1; i += CD_THREADS) {
+      const uint32_t k = i - c0;
+      s_t[k] = a.time[i];
+      s_p[k] = a.pkt[i];
+      s_l[k] = a.len[i];
+    }
+    __syncthreads();
+    if (walker) {
+      const uint32_t b = max(hb, c0), e = min(he, c1);
+      for (uint32_t i = b; i < e; i++) {
+        const uint32_t k = i - c0;
+        const uint64_t now = s_t[k];
+        if (now >= ia.window_end) q.err |= E_WINDOW;
+        while (due(now)) relay_task(q, r, r.tt, ia.bootstrap_end, ia.sim_end, ctr_inc, ia.fwd_time);
+        q.push(s_p[k], now, s_l[k]);  // Router::route_incoming_packet
+        if (!(r.rf & R_PENDING)) {    // notify_router_has_packets: Idle -> forward_later(ZERO)
+          ctr_inc++;
+          r.rf |= R_PENDING;
+          if (now >= ia.sim_end) r.rf |= R_NEVER;
+          r.tt = now;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  unsigned long long err = 0, dropped = 0;
+  if (walker) {
+    while (due(ia.window_end)) relay_task(q, r, r.tt, ia.bootstrap_end, ia.sim_end, ctr_inc, ia.fwd_time);
+    a.flags[h] = q.flags;
+    a.iend[h] = q.iend;
+    a.dnext[h] = q.dnext;
+    a.cur[h] = q.cur;
+    a.prev[h] = q.prev;
+    a.bytes[h] = q.bytes;
+    a.head[h] = q.head;
+    a.tail[h] = q.tail;
+    ia.rflags[h] = r.rf;
+    ia.task_time[h] = r.tt;
+    ia.cached_pkt[h] = r.cp;
+    ia.cached_len[h] = r.cl;
+    ia.tb_bal[h] = r.bal;
+    ia.tb_last[h] = r.last;
+    if (ia.event_ctr && ctr_inc) ia.event_ctr[h] += ctr_inc;
+    err = q.err;
+    dropped = q.dropped;
+  }
+  if (t < 64) {
+    for (int d = 32; d > 0; d >>= 1) {
+      dropped += __shfl_xor(dropped, d, 64);
+      err |= __shfl_xor(err, d, 64);
+    }
+    if (t == 0) {
+      a.blk[2 * blockIdx.x] = dropped;
+      a.blk[2 * blockIdx.x + 1] = err;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace sg
 
@@ -356,6 +557,24 @@ void sg_codel_destroy(sg_codel* q) {
 }
 
 uint32_t sg_codel_ring_cap(const sg_codel* q) { return q ? q->cap : 0; }
+
+}  // extern "C"
+
+struct sg_inbound {
+  sg_codel* q = nullptr;
+  uint8_t* rflags = nullptr;
+  uint64_t* task_time = nullptr;
+  uint32_t *cached_pkt = nullptr, *cached_len = nullptr;
+  uint64_t *tb_cap = nullptr, *tb_bal = nullptr, *tb_inc = nullptr, *tb_last = nullptr;
+  ~sg_inbound() {
+    void* ps[] = {rflags, task_time, cached_pkt, cached_len, tb_cap, tb_bal, tb_inc, tb_last};
+    for (void* p : ps)
+      if (p) (void)hipFree(p);
+    sg_codel_destroy(q);
+  }
+};
+
+extern "C" {
 
 int32_t sg_codel_run(sg_ctx* ctx, sg_codel* q, const sg_codel_events* ev, uint32_t* pop_result,
                      uint8_t* pkt_status, uint32_t n_packets, uint64_t* n_dropped) {
@@ -436,6 +655,143 @@ int32_t sg_codel_set_state(sg_codel* q, const sg_codel_state* in) {
       SG_HIP(hipMemcpyAsync(q->ring, ring.data(), r * 16, hipMemcpyHostToDevice, st));
       SG_HIP(hipStreamSynchronize(st));  // before `ring` goes out of scope
     }
+    SG_HIP(hipStreamSynchronize(st));
+  });
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int32_t sg_inbound_create(sg_ctx* ctx, uint32_t n_hosts, const uint64_t* bw_down_bits, uint32_t ring_cap,
+                          sg_inbound** out) {
+  if (!out) return SG_ERR_INVALID_ARG;
+  *out = nullptr;
+  sg_inbound* ib = new (std::nothrow) sg_inbound();
+  if (!ib) return SG_ERR_OOM;
+  int32_t rc = sg_codel_create(ctx, n_hosts, ring_cap, &ib->q);
+  if (rc == SG_OK)
+    rc = sg::guarded(ctx, [&] {
+      using namespace sg;
+      if (n_hosts && !bw_down_bits) throw Error(SG_ERR_INVALID_ARG, "null bandwidth array");
+      const size_t n = std::max<uint32_t>(n_hosts, 1);
+      SG_HIP(hipMalloc(&ib->rflags, n));
+      SG_HIP(hipMalloc(&ib->task_time, n * 8));
+      SG_HIP(hipMalloc(&ib->cached_pkt, n * 4));
+      SG_HIP(hipMalloc(&ib->cached_len, n * 4));
+      SG_HIP(hipMalloc(&ib->tb_cap, n * 8));
+      SG_HIP(hipMalloc(&ib->tb_bal, n * 8));
+      SG_HIP(hipMalloc(&ib->tb_inc, n * 8));
+      SG_HIP(hipMalloc(&ib->tb_last, n * 8));
+      // Relay::new (relay/mod.rs:48-66): Idle, no cached packet, a full bucket
+      std::vector<uint64_t> inc(n), cap(n), last(n, 946684800ull * 1000000000ull);  // EmulatedTime::SIMULATION_START
+      for (uint32_t h = 0; h < n_hosts; h++) {
+        inc[h] = std::max<uint64_t>(1, (bw_down_bits[h] / 8) / 1000);  // create_token_bucket (:296-304)
+        cap[h] = inc[h] + CD_MTU;                                      // + get_burst_allowance (:306-309)
+      }
+      hipStream_t st = ctx->stream;
+      SG_HIP(hipMemsetAsync(ib->rflags, 0, n, st));
+      SG_HIP(hipMemsetAsync(ib->task_time, 0, n * 8, st));
+      SG_HIP(hipMemsetAsync(ib->cached_pkt, 0, n * 4, st));
+      SG_HIP(hipMemsetAsync(ib->cached_len, 0, n * 4, st));
+      SG_HIP(hipMemcpyAsync(ib->tb_cap, cap.data(), n * 8, hipMemcpyHostToDevice, st));
+      SG_HIP(hipMemcpyAsync(ib->tb_bal, cap.data(), n * 8, hipMemcpyHostToDevice, st));
+      SG_HIP(hipMemcpyAsync(ib->tb_inc, inc.data(), n * 8, hipMemcpyHostToDevice, st));
+      SG_HIP(hipMemcpyAsync(ib->tb_last, last.data(), n * 8, hipMemcpyHostToDevice, st));
+      SG_HIP(hipStreamSynchronize(st));
+    });
+  if (rc != SG_OK) {
+    delete ib;
+    return rc;
+  }
+  *out = ib;
+  return SG_OK;
+}
+
+void sg_inbound_destroy(sg_inbound* ib) {
+  if (!ib) return;
+  if (ib->q && ib->q->ctx) (void)hipSetDevice(ib->q->ctx->device);
+  delete ib;
+}
+
+uint32_t sg_inbound_ring_cap(const sg_inbound* ib) { return ib ? ib->q->cap : 0; }
+
+int32_t sg_inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* arr, uint64_t window_end_ns,
+                       uint64_t bootstrap_end_ns, uint64_t sim_end_ns, uint64_t* event_ctr, uint64_t* fwd_time,
+                       uint8_t* pkt_status, uint32_t n_packets, uint64_t* n_dropped) {
+  return sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (!ib || !arr || ib->q->ctx != ctx) throw Error(SG_ERR_INVALID_ARG, "null argument");
+    sg_codel* q = ib->q;
+    const uint32_t E = arr->n, H = q->n;
+    if (n_dropped) *n_dropped = 0;
+    if (E && (!arr->host || !arr->time_ns || !arr->packet || !arr->len))
+      throw Error(SG_ERR_INVALID_ARG, "null arrival array");
+    if (n_packets && (!pkt_status || !fwd_time)) throw Error(SG_ERR_INVALID_ARG, "null output array");
+    if (!H) return;
+    hipStream_t st = ctx->stream;
+    uint32_t* ws = ctx->d_seg.get<uint32_t>((size_t)H + 8);
+    uint32_t* gerr = ws + (size_t)H + 1;
+    SG_HIP(hipMemsetAsync(gerr, 0, 4, st));
+    if (E) {
+      launch_group_offsets(ctx, arr->host, E, H, ws, gerr);
+    } else {
+      SG_HIP(hipMemsetAsync(ws, 0, ((size_t)H + 1) * 4, st));  // no arrivals: pending tasks only
+    }
+    const uint32_t nb = (H + CD_HOSTS - 1) / CD_HOSTS;
+    InboundArgs a;
+    a.q = CodelArgs{ws, H, E, nullptr, arr->time_ns, arr->packet, arr->len, q->flags, q->iend, q->dnext, q->cur,
+                    q->prev, q->bytes, q->head, q->tail, q->ring, q->cap, nullptr, pkt_status, n_packets,
+                    ctx->d_blk.get<unsigned long long>(2 * (size_t)nb)};
+    a.rflags = ib->rflags;
+    a.task_time = ib->task_time;
+    a.cached_pkt = ib->cached_pkt;
+    a.cached_len = ib->cached_len;
+    a.tb_cap = ib->tb_cap;
+    a.tb_bal = ib->tb_bal;
+    a.tb_inc = ib->tb_inc;
+    a.tb_last = ib->tb_last;
+    a.window_end = window_end_ns;
+    a.bootstrap_end = bootstrap_end_ns;
+    a.sim_end = sim_end_ns;
+    a.event_ctr = event_ctr;
+    a.fwd_time = fwd_time;
+    {
+      // per arrival: 16 B in, a 16-B ring record written and read, 9 B out; per host: ~160 B of state
+      TimedLaunch tl(ctx, "inbound", 57.0 * E + 160.0 * H);
+      hipLaunchKernelGGL(k_inbound, dim3(nb), dim3(CD_THREADS), 0, st, a);
+    }
+    hipLaunchKernelGGL(k_codel_reduce, dim3(1), dim3(1024), 0, st, a.q.blk, nb, gerr, q->ret);
+    SG_CHECK_LAUNCH();
+    SG_HIP(hipStreamSynchronize(st));
+    const volatile unsigned long long* r = q->ret;
+    const uint64_t err = r[1];
+    if (err & E_UNSORTED) throw Error(SG_ERR_UNSORTED, "arrivals must be grouped by ascending host");
+    if (err & E_HOST) throw Error(SG_ERR_INVALID_ARG, "arrival host out of range");
+    if (err & E_FULL) throw Error(SG_ERR_CAPACITY, "a CoDel queue outgrew its ring (raise ring_cap)");
+    if (err & E_PKT) throw Error(SG_ERR_INVALID_ARG, "packet id >= n_packets");
+    if (err & E_WINDOW) throw Error(SG_ERR_INVALID_ARG, "an arrival is at or after window_end");
+    if (n_dropped) *n_dropped = r[0];
+  });
+}
+
+int32_t sg_inbound_get_state(sg_inbound* ib, sg_codel_state* queue, sg_inbound_relay_state* o) {
+  if (!ib) return SG_ERR_INVALID_ARG;
+  if (queue) {
+    const int32_t rc = sg_codel_get_state(ib->q, queue);
+    if (rc != SG_OK) return rc;
+  }
+  if (!o) return SG_OK;
+  return sg::guarded(ib->q->ctx, [&] {
+    const size_t n = ib->q->n;
+    hipStream_t st = ib->q->ctx->stream;
+    struct { void* h; const void* d; size_t b; } cp[] = {
+        {o->flags, ib->rflags, n}, {o->task_time, ib->task_time, n * 8}, {o->cached_packet, ib->cached_pkt, n * 4},
+        {o->cached_len, ib->cached_len, n * 4}, {o->tb_capacity, ib->tb_cap, n * 8},
+        {o->tb_balance, ib->tb_bal, n * 8}, {o->tb_increment, ib->tb_inc, n * 8},
+        {o->tb_last_refill, ib->tb_last, n * 8}};
+    for (auto& c : cp)
+      if (c.h && c.b) SG_HIP(hipMemcpyAsync(c.h, c.d, c.b, hipMemcpyDeviceToHost, st));
     SG_HIP(hipStreamSynchronize(st));
   });
 }

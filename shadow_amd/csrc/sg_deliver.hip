@@ -1443,6 +1443,8 @@ int32_t sg_deliver_source(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table, c
   });
 }
 
+uint64_t* sg_hosts_event_ctr(sg_hosts* hosts) { return hosts ? hosts->ctr : nullptr; }
+
 int32_t sg_table_pack(sg_ctx* ctx, const sg_table* table, uint64_t* out_key, uint32_t* out_packable) {
   return sg::guarded(ctx, [&] {
     using namespace sg;

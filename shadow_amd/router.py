@@ -1,6 +1,8 @@
 """Routers' inbound CoDel queues on the device: host-side mirror of
 Router::inbound_packets (src/main/network/router/mod.rs:15-58) and
-CoDelQueue (src/main/network/router/codel_queue.rs).
+CoDelQueue (src/main/network/router/codel_queue.rs); and the inbound pipeline
+(`InboundPipeline`): router queue -> relay_inet_in token bucket
+(src/main/network/relay/mod.rs, relay/token_bucket.rs).
 
 One queue per host lives on the device across calls.  `CoDelQueues.run`
 applies a batch of push / pop events -- grouped by ascending host, each host's
@@ -113,6 +115,61 @@ class CoDelQueues:
         try:
             if getattr(self, "handle", None):
                 load().sg_codel_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+class InboundPipeline:
+    """Every host's router CoDel queue + inbound relay (sg_inbound_*): arrivals (a
+    delivery round's buckets) are pushed and forwarded to the interface as each
+    host's token bucket allows; forward tasks past a window's end stay pending."""
+
+    def __init__(self, bw_down_bits, ring_cap: int = 4096, ctx: Optional[Context] = None):
+        self.ctx = ctx or default_context()
+        bw = np.ascontiguousarray(bw_down_bits, dtype=np.uint64)
+        self.n = len(bw)
+        h = C.c_void_p()
+        check(self.ctx.handle, load().sg_inbound_create(self.ctx.handle, self.n, bw.ctypes.data, int(ring_cap),
+                                                        C.byref(h)))
+        self.handle = h
+        self.cap = int(load().sg_inbound_ring_cap(h))
+
+    def run(self, host, time_ns, packet, length, window_end_ns: int, bootstrap_end_ns: int, sim_end_ns: int,
+            fwd_time, pkt_status, event_ctr_ptr: Optional[int] = None) -> int:
+        """Arrivals as device tensors (int32 host/packet/length, int64 time); fwd_time (int64)
+        and pkt_status (uint8) are indexed by packet id.  Returns the CoDel drops."""
+        n = int(host.numel())
+        a = _capi.sg_inbound_arrivals(n, host.data_ptr(), time_ns.data_ptr(), packet.data_ptr(), length.data_ptr())
+        nd = C.c_uint64()
+        check(self.ctx.handle, load().sg_inbound_run(self.ctx.handle, self.handle, C.byref(a), int(window_end_ns),
+                                                     int(bootstrap_end_ns), int(sim_end_ns),
+                                                     C.c_void_p(event_ctr_ptr or 0), fwd_time.data_ptr(),
+                                                     pkt_status.data_ptr(), int(pkt_status.numel()), C.byref(nd)))
+        return int(nd.value)
+
+    def get_state(self) -> dict:
+        """Queue state (CoDelQueues.get_state layout) + relay state (the oracle's inbound_state keys)."""
+        n = self.n
+        st = dict(cap=self.cap, flags=np.zeros(n, np.uint8), interval_end=np.zeros(n, np.uint64),
+                  drop_next=np.zeros(n, np.uint64), cur=np.zeros(n, np.uint64), prev=np.zeros(n, np.uint64),
+                  bytes=np.zeros(n, np.uint64), head=np.zeros(n, np.uint32), tail=np.zeros(n, np.uint32),
+                  ring_pkt=np.zeros(n * self.cap, np.uint32), ring_ts=np.zeros(n * self.cap, np.uint64),
+                  ring_len=np.zeros(n * self.cap, np.uint32), rflags=np.zeros(n, np.uint8),
+                  task_time=np.zeros(n, np.uint64), cached_pkt=np.zeros(n, np.uint32),
+                  cached_len=np.zeros(n, np.uint32), tb_cap=np.zeros(n, np.uint64), tb_bal=np.zeros(n, np.uint64),
+                  tb_inc=np.zeros(n, np.uint64), tb_last=np.zeros(n, np.uint64))
+        v = lambda k: st[k].ctypes.data_as(C.c_void_p)
+        rs = _capi.sg_inbound_relay_state(v("rflags"), v("task_time"), v("cached_pkt"), v("cached_len"), v("tb_cap"),
+                                          v("tb_bal"), v("tb_inc"), v("tb_last"))
+        check(self.ctx.handle, load().sg_inbound_get_state(self.handle, C.byref(CoDelQueues._struct(st)),
+                                                           C.byref(rs)))
+        return st
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                load().sg_inbound_destroy(self.handle)
                 self.handle = None
         except Exception:
             pass

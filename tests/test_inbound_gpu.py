@@ -1,0 +1,110 @@
+"""GPU parity of the inbound pipeline (sg_inbound_*: router CoDel queue ->
+relay_inet_in token bucket) against the oracle, bit-exact: forward times,
+statuses, event-counter advances and the whole per-host queue + relay state,
+over consecutive windows (pending forward tasks carry over)."""
+import numpy as np
+import pytest
+
+from shadow_amd import ShadowGpuError, _capi
+from shadow_amd.router import InboundPipeline
+
+pytestmark = pytest.mark.gpu
+T0 = 946684800 * 10**9
+MS = 10**6
+QKEYS = ("flags", "interval_end", "drop_next", "cur", "prev", "bytes", "head", "tail")
+RKEYS = ("rflags", "task_time", "tb_cap", "tb_bal", "tb_inc", "tb_last")
+
+
+def _dev(a, np_dtype, torch_dtype):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np_dtype).view(torch_dtype)).cuda()
+
+
+def _arrivals(rng, H, n, t0, t1):
+    host = np.sort(rng.integers(0, H, n)).astype(np.uint32)
+    t = np.sort(rng.integers(t0, t1, n)).astype(np.uint64)
+    order = np.lexsort((t, host))  # per host ascending time (EventQueue order by time)
+    host, t = host[order], t[order]
+    ln = rng.choice(np.array([28, 1476, 600], np.uint32), n)
+    return host, t, ln
+
+
+def _same(O, got, want):
+    for k in QKEYS + RKEYS:
+        assert np.array_equal(got[k], want[k]), k
+    # cached packets only where a packet is cached
+    m = (want["rflags"] & O.RL_CACHED) != 0
+    assert np.array_equal(got["cached_pkt"][m], want["cached_pkt"][m])
+    assert np.array_equal(got["cached_len"][m], want["cached_len"][m])
+
+
+@pytest.mark.parametrize("bw_mbit,boot_ms", [(1000, 0), (10, 0), (1, 0), (10, 40)])
+def test_windows_match_oracle(oracle, ctx, bw_mbit, boot_ms):
+    """300 hosts, 5 windows of 60 ms, 60k arrivals: from unthrottled to heavily
+    throttled (standing queues, CoDel drop mode, tasks pending across windows)."""
+    import torch
+
+    rng = np.random.default_rng(bw_mbit + boot_ms)
+    H, W, per = 300, 60 * MS, 12000
+    bw = rng.integers(bw_mbit * 10**6 // 2, bw_mbit * 10**6 + 1, H).astype(np.uint64)
+    ib = InboundPipeline(bw, 4096, ctx=ctx)
+    ost = oracle.inbound_state(bw, ib.cap)
+    n_pk = 5 * per
+    fwd_g = torch.full((n_pk,), -1, dtype=torch.int64, device="cuda")
+    st_g = torch.zeros(n_pk, dtype=torch.uint8, device="cuda")
+    ctr_g = torch.zeros(H, dtype=torch.int64, device="cuda")
+    fwd_o = np.full(n_pk, np.uint64(2**64 - 1))
+    st_o = np.zeros(n_pk, np.uint8)
+    ctr_o = np.zeros(H, np.uint64)
+    boot, sim_end = T0 + boot_ms * MS, T0 + 10**12
+    for w in range(5):
+        t0, t1 = T0 + w * W, T0 + (w + 1) * W
+        host, t, ln = _arrivals(rng, H, per, t0, t1)
+        pkt = np.arange(w * per, (w + 1) * per, dtype=np.uint32)
+        nd = ib.run(_dev(host, np.uint32, np.int32), _dev(t, np.uint64, np.int64), _dev(pkt, np.uint32, np.int32),
+                    _dev(ln, np.uint32, np.int32), t1, boot, sim_end, fwd_g, st_g, ctr_g.data_ptr())
+        before = int((st_o == 2).sum())
+        oracle.inbound_run(ost, host, t, pkt, ln, t1, boot, sim_end, ctr_o, fwd_o, st_o)
+        assert nd == int((st_o == 2).sum()) - before
+        assert np.array_equal(st_g.cpu().numpy(), st_o)
+        assert np.array_equal(fwd_g.cpu().numpy().view(np.uint64)[st_o == 1], fwd_o[st_o == 1])
+        assert np.array_equal(ctr_g.cpu().numpy().view(np.uint64), ctr_o)
+        _same(oracle, ib.get_state(), ost)
+    if bw_mbit == 1:
+        assert (st_o == 2).any() and (ost["rflags"] & oracle.RL_PENDING).any()
+
+
+def test_empty_window_runs_pending_tasks(oracle, ctx):
+    """A window with no arrivals still runs the forward tasks that fall inside it."""
+    import torch
+
+    bw = np.array([8000, 8000], np.uint64)  # 1 B per ms
+    ib = InboundPipeline(bw, 64, ctx=ctx)
+    ost = oracle.inbound_state(bw, ib.cap)
+    fwd_g = torch.full((8,), -1, dtype=torch.int64, device="cuda")
+    st_g = torch.zeros(8, dtype=torch.uint8, device="cuda")
+    fwd_o, st_o, ctr_o = np.full(8, np.uint64(2**64 - 1)), np.zeros(8, np.uint8), np.zeros(2, np.uint64)
+    host, t, pkt, ln = [0, 0, 1], [T0 + 5 * MS] * 3, [0, 1, 2], [1500, 1500, 1500]
+    args = lambda: (_dev(host, np.uint32, np.int32), _dev(t, np.uint64, np.int64), _dev(pkt, np.uint32, np.int32),
+                    _dev(ln, np.uint32, np.int32))
+    ib.run(*args(), T0 + 10 * MS, 0, T0 + 10**12, fwd_g, st_g)
+    oracle.inbound_run(ost, host, t, pkt, ln, T0 + 10 * MS, 0, T0 + 10**12, ctr_o, fwd_o, st_o)
+    e = [_dev([], np.uint32, np.int32), _dev([], np.uint64, np.int64), _dev([], np.uint32, np.int32),
+         _dev([], np.uint32, np.int32)]
+    ib.run(*e, T0 + 3000 * MS, 0, T0 + 10**12, fwd_g, st_g)
+    oracle.inbound_run(ost, [], [], [], [], T0 + 3000 * MS, 0, T0 + 10**12, ctr_o, fwd_o, st_o)
+    assert np.array_equal(st_g.cpu().numpy(), st_o) and st_o[1] == 1
+    assert np.array_equal(fwd_g.cpu().numpy().view(np.uint64)[st_o == 1], fwd_o[st_o == 1])
+    _same(oracle, ib.get_state(), ost)
+
+
+def test_arrival_after_window_rejected(ctx):
+    import torch
+
+    ib = InboundPipeline(np.array([10**9], np.uint64), 16, ctx=ctx)
+    with pytest.raises(ShadowGpuError) as e:
+        ib.run(_dev([0], np.uint32, np.int32), _dev([T0 + 20 * MS], np.uint64, np.int64),
+               _dev([0], np.uint32, np.int32), _dev([100], np.uint32, np.int32), T0 + 10 * MS, 0, T0 + 10**12,
+               torch.zeros(4, dtype=torch.int64, device="cuda"), torch.zeros(4, dtype=torch.uint8, device="cuda"))
+    assert e.value.code == _capi.SG_ERR_INVALID_ARG
