@@ -200,6 +200,74 @@ def codel_leg(a, D, ctx, torch, out, payload, n_packets, pmc):
     return leg
 
 
+BW_DOWN_BITS = 10**9  # every host's bandwidth down in the inbound leg
+
+
+def inbound_leg(a, D, ctx, torch, out, payload, n_packets, pmc, round_end):
+    """The C4 round's buckets through every destination's inbound pipeline: router
+    CoDel queue -> relay_inet_in token bucket (1 Gbit/s down), one window that holds
+    every arrival."""
+    from shadow_amd.router import InboundPipeline
+
+    nd = int(out.n_delivered)
+    offs = out.dst_offsets.cpu().numpy().view(np.uint32).astype(np.int64)
+    order = out.dst_order[:nd].cpu().numpy().view(np.uint32)
+    dtime = out.deliver_time_ns.cpu().numpy().view(np.uint64)
+    H = len(offs) - 1
+    host = np.repeat(np.arange(H, dtype=np.uint32), np.diff(offs))
+    t = dtime[order]
+    ln = (28 + np.asarray(payload, np.uint32)[order]).astype(np.uint32)
+    window_end = int(t.max()) + 1 if nd else round_end + 1
+    dev = lambda x, dt, tv: torch.from_numpy(np.ascontiguousarray(x, dtype=dt).view(tv)).cuda()
+    args = (dev(host, np.uint32, np.int32), dev(t, np.uint64, np.int64), dev(order, np.uint32, np.int32),
+            dev(ln, np.uint32, np.int32))
+    fwd = torch.full((max(n_packets, 1),), -1, dtype=torch.int64, device="cuda")
+    status = torch.zeros(max(n_packets, 1), dtype=torch.uint8, device="cuda")
+    bw = np.full(H, BW_DOWN_BITS, np.uint64)
+    pipes = [InboundPipeline(bw, 256, ctx=ctx) for _ in range(a.steps + a.warmup + 1)]  # a fresh state per step
+    it = iter(pipes)
+
+    def step():
+        next(it).run(*args, window_end, 0, 2**63, fwd, status)
+
+    t_step = timed(D, step, a.steps, a.warmup)
+    ctx.enable_timers(True)
+    n_drop = next(it).run(*args, window_end, 0, 2**63, fwd, status)
+    k_ms, k_n, k_bytes = ctx.read_timer("inbound")
+    ctx.enable_timers(False)
+    k_s = k_ms / 1e3 / max(k_n, 1)
+    ach = k_bytes / max(k_n, 1) / k_s / 1e9 if k_n else 0.0
+    n_fwd = int((status.cpu().numpy() == 1).sum())
+    leg = {
+        "metric": "inbound arrivals/sec (router CoDel queue -> relay token bucket, per host)", "unit": "arrivals/s",
+        "value": round(D.sum(float(nd)) / t_step, 1), "higher_is_better": True, "ms_per_window": round(t_step * 1e3, 4),
+        "scaling": "weak", "dtype": "u64+f64",
+        "config": {"workload": "the C4 round's delivered packets arriving at their destinations (EventQueue order) "
+                               "through each host's router CoDel queue and a 1 Gbit/s relay_inet_in token bucket, "
+                               "one window holding every arrival", "hosts": H, "arrivals": nd,
+                   "bw_down_bits": BW_DOWN_BITS},
+        "roofline": {"kernel": "k_inbound", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "traffic": pmc.get("inbound", {}).get("hbm_bytes_per_launch"), "avg_launch_ms": round(k_s * 1e3, 4)},
+        "forwarded": n_fwd, "dropped": n_drop,
+    }
+    if D.rank == 0 and D.world == 1 and not a.no_cpu:
+        from oracle import oracle as O
+
+        st = O.inbound_state(bw, pipes[0].cap)
+        ctr = np.zeros(H, np.uint64)
+        ofwd = np.full(max(n_packets, 1), np.uint64(2**64 - 1))
+        ost = np.zeros(max(n_packets, 1), np.uint8)
+        t0 = time.perf_counter()
+        O.inbound_run(st, host, t, order, ln, window_end, 0, 2**63, ctr, ofwd, ost)
+        tc = time.perf_counter() - t0
+        leg["cpu_baseline"] = {"value": round(nd / tc, 1), "unit": "arrivals/s", "cores": 1, "kind": "port",
+                               "sample": f"the same {nd} arrivals through the C restatement (codel_queue.rs + "
+                                         "relay/mod.rs + token_bucket.rs), 1 thread"}
+        leg["parity_vs_cpu"] = bool(np.array_equal(ost, status.cpu().numpy()))
+    return leg
+
+
 def main():
     a = parse_args()
     D = Dist(a.gpus)
@@ -392,6 +460,7 @@ def main():
         result["delivery"] = delivery
         if not a.no_codel:
             result["codel"] = codel_leg(a, D, ctx, torch, out, pk["payload"], a.packets, pmc)
+            result["inbound"] = inbound_leg(a, D, ctx, torch, out, pk["payload"], a.packets, pmc, round_end)
 
     if D.rank == 0:
         print(json.dumps(result), flush=True)

@@ -25,6 +25,7 @@ KERNELS = {"relax_wide": "k_relax_wide", "relax": "k_relax_w<", "out": "k_out_ba
            "sb_hist": "k_sb_hist", "sb_scatter": "k_sb_scatter", "sb_sort_region": "k_sb_sort_region",
            "sb_sort": "k_sb_sort", "sort_big": "k_sort_big", "host_off": "k_host_off", "reduce_stats": "k_reduce_stats",
            "table_pack": "k_table_pack", "codel_reduce": "k_codel_reduce", "codel": "k_codel",
+           "inbound": "k_inbound",
            "init": "k_init_batch"}
 VALU_PEAK_OPS_PER_NS = 256 * 4 * 32 * 2.4  # 78.6e3 lane-ops per ns (MI355X_MICROARCH.md chip table)
 
