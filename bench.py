@@ -319,7 +319,7 @@ def main():
     gather_bytes = ROW_BYTES_PER_RELAX * relax_per_launch
     achieved = gather_bytes / avg_launch_s / 1e9 if relax_launches else 0.0
     pm = pmc.get("relax", {})
-    roofline = {"kernel": "k_relax_w", "bound": "l2", "achieved": round(achieved, 1), "peak": L2_PEAK_GBS,
+    roofline = {"kernel": "k_relax_w2", "bound": "l2", "achieved": round(achieved, 1), "peak": L2_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / L2_PEAK_GBS, 4),
                 "traffic": pm.get("hbm_bytes_per_launch"),
                 "algorithmic_bytes_per_launch": gather_bytes,

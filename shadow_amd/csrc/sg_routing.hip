@@ -357,6 +357,162 @@ __global__ void __launch_bounds__(RELAX_THREADS)
   if (COUNT && lane == 0 && n_rel) atomicAdd(&work[blockIdx.x & (WORK_SHARDS - 1)], (unsigned long long)n_rel * B);
 }
 
+// Two 8-B keys (16 B) through the buffer descriptor; OOB -> zeros, no traffic.
+__device__ __forceinline__ void load_key2(__amdgpu_buffer_rsrc_t rsrc, uint32_t off, uint64_t& k0, uint64_t& k1) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+  k0 = ((uint64_t)v[1] << 32) | v[0];
+  k1 = ((uint64_t)v[3] << 32) | v[2];
+}
+
+// k_relax_w2: the B = 64 relaxation with two sources per lane.  A row (64 keys,
+// 512 B) is read by 32 lanes with 16-B loads, so one wave instruction reads
+// two rows (two arcs, one per half-wave): half the vector-memory instructions
+// per relaxation.  The texture-address unit, 80 % busy in k_relax_w (PMC
+// TA_TA_BUSY), processes one instruction's 64 addresses whatever their width.
+// Same work items, frontier, LDS merge and flush as k_relax_w; a flush writes
+// both keys of a lane with one 16-B store (the row's only writer is this wave,
+// so the unchanged half is rewritten with the value it holds).
+template <int NPW, int K, int GROUP, bool FRONT, bool COUNT>
+__global__ void __launch_bounds__(RELAX_THREADS)
+    k_relax_w2(const uint32_t* __restrict__ in_off, const uint4* __restrict__ in_rec, uint64_t* __restrict__ D,
+               uint32_t n, const uint32_t* __restrict__ alist, uint32_t* __restrict__ changed,
+               uint32_t* __restrict__ stamp, uint32_t pass, unsigned long long* __restrict__ work) {
+  constexpr int B = 64;
+  constexpr int WAVES = RELAX_THREADS / 64;
+  constexpr int STG_W = 64 * K;
+  constexpr int G = 2;  // rows per wave instruction
+  static_assert(NPW % G == 0, "NPW must be even");
+  __shared__ uint4 lists[WAVES][STG_W];
+  __shared__ unsigned long long bests[WAVES][NPW * B];
+  const int lane = threadIdx.x & 63;
+  const uint32_t gh = lane >> 5, sl = lane & 31;  // row group; the lane's sources 2 sl, 2 sl + 1
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane16 = sl * 16;
+  uint4* list = lists[w];
+  unsigned long long* best = bests[w];
+  const uint32_t x = blockIdx.x & 7;
+  const uint32_t nwc = (n + NPW - 1) / NPW;
+  const uint32_t n_act = alist[0];
+  const uint32_t nbx = n_act > x ? (n_act - x + 7) / 8 : 0;
+  const uint32_t items = nbx * nwc;
+  const uint32_t stride = (gridDim.x >> 3) * WAVES;
+  uint32_t n_rel = 0, flagged = ~0u;
+  for (uint32_t it = (blockIdx.x >> 3) * WAVES + w; it < items; it += stride) {
+    const uint32_t b = alist[1 + x + 8 * (it / nwc)];
+    const uint32_t vw = (it % nwc) * NPW;
+    const uint32_t vw1 = min(vw + NPW, n);
+    uint64_t* Db = D + (size_t)b * n * B;
+    const uint32_t* St = stamp + (size_t)b * n;
+    const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(Db, 0, (int)(n * B * 8u), 0x00020000);
+    const uint32_t a0 = in_off[vw], a1 = in_off[vw1];
+    uint32_t n_cand = 0;
+    uint32_t run_slot = 0;
+    uint64_t run0 = KEY_INF, run1 = KEY_INF;
+    bool prefetched = false;
+    uint64_t cur0[NPW / G], cur1[NPW / G];
+    for (uint32_t c0 = a0; c0 < a1; c0 += STG_W) {
+      const uint32_t c1 = min(c0 + STG_W, a1);
+      uint4 ra[K];
+      bool dirty[K];
+#pragma unroll
+      for (int i = 0; i < K; i++) ra[i] = in_rec[min(c0 + lane + 64 * i, c1 - 1)];
+#pragma unroll
+      for (int i = 0; i < K; i++) dirty[i] = c0 + lane + 64 * i < c1 && (!FRONT || St[ra[i].x] > pass);
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int i = 0; i < K; i++) {
+        const uint64_t m = __ballot(dirty[i]);
+        if (dirty[i])
+          list[cnt + (uint32_t)__popcll(m & ((1ull << lane) - 1))] =
+              make_uint4(ra[i].x * (B * 8), ra[i].y - vw, ra[i].z, ra[i].w);
+        cnt += (uint32_t)__popcll(m);
+      }
+      if (cnt && !n_cand) {
+#pragma unroll
+        for (int i = 0; i < NPW * B / 64; i++) best[i * 64 + lane] = KEY_INF;
+      }
+      n_cand += cnt;
+      if (cnt >= PREFETCH_MIN && !prefetched) {
+        prefetched = true;
+#pragma unroll
+        for (int i = 0; i < NPW / G; i++)
+          load_key2(slab, min(vw + i * G + gh, vw1 - 1) * (B * 8) + lane16, cur0[i], cur1[i]);
+      }
+      // half-wave gh takes records gh, gh + 2, ...: each destination's candidates
+      // form one run per half-wave (CSC order)
+      auto fold = [&](const uint4& r, uint64_t k0, uint64_t k1) {
+        if (r.y != run_slot) {
+          atomicMin(&best[run_slot * B + 2 * sl], (unsigned long long)run0);
+          atomicMin(&best[run_slot * B + 2 * sl + 1], (unsigned long long)run1);
+          run_slot = r.y;
+          run0 = run1 = KEY_INF;
+        }
+        const float om = __uint_as_float(r.w);
+        run0 = min(run0, relax32(k0, r.z, om));
+        run1 = min(run1, relax32(k1, r.z, om));
+      };
+      uint32_t g = 0;
+      for (; g + GROUP * G <= cnt; g += GROUP * G) {
+        uint4 r[GROUP];
+        uint64_t k0[GROUP], k1[GROUP];
+#pragma unroll
+        for (int j = 0; j < GROUP; j++) r[j] = list[g + j * G + gh];
+#pragma unroll
+        for (int j = 0; j < GROUP; j++) load_key2(slab, r[j].x + lane16, k0[j], k1[j]);
+#pragma unroll
+        for (int j = 0; j < GROUP; j++) fold(r[j], k0[j], k1[j]);
+      }
+      for (; g < cnt; g += G) {
+        const uint32_t idx = g + gh;
+        if (idx < cnt) {
+          const uint4 r = list[idx];
+          uint64_t k0, k1;
+          load_key2(slab, r.x + lane16, k0, k1);
+          fold(r, k0, k1);
+        }
+      }
+    }
+    if (COUNT) n_rel += n_cand;
+    if (!n_cand) continue;
+    atomicMin(&best[run_slot * B + 2 * sl], (unsigned long long)run0);
+    atomicMin(&best[run_slot * B + 2 * sl + 1], (unsigned long long)run1);
+    uint64_t nb0[NPW / G], nb1[NPW / G];
+#pragma unroll
+    for (int i = 0; i < NPW / G; i++) {
+      nb0[i] = best[(i * G + gh) * B + 2 * sl];
+      nb1[i] = best[(i * G + gh) * B + 2 * sl + 1];
+    }
+    if (!prefetched) {
+#pragma unroll
+      for (int i = 0; i < NPW / G; i++)
+        load_key2(slab,
+                  nb0[i] != KEY_INF || nb1[i] != KEY_INF ? min(vw + i * G + gh, vw1 - 1) * (B * 8) + lane16 : OOB,
+                  cur0[i], cur1[i]);
+    }
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < NPW / G; i++) {
+      const uint32_t v = vw + i * G + gh;
+      const bool c0 = v < vw1 && nb0[i] < cur0[i];
+      const bool c1 = v < vw1 && nb1[i] < cur1[i];
+      if (c0 || c1) {
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        *(u64x2*)&Db[(size_t)v * B + 2 * sl] = (u64x2){c0 ? nb0[i] : cur0[i], c1 ? nb1[i] : cur1[i]};
+      }
+      const uint64_t m = __ballot(c0 || c1);
+      if (m) {
+        any = true;
+        if (FRONT && sl == 0 && ((m >> (gh * 32)) & 0xffffffffull)) stamp[(size_t)b * n + v] = pass + 2;
+      }
+    }
+    if (any && b != flagged) {
+      if (lane == 0) changed[b * FLAG_STRIDE] = 1u;
+      flagged = b;
+    }
+  }
+  if (COUNT && lane == 0 && n_rel) atomicAdd(&work[blockIdx.x & (WORK_SHARDS - 1)], (unsigned long long)n_rel * B);
+}
+
 // Transposed write-out of [B rows x 64 cols] tiles.  Diagonal = the raw
 // self-loop (graph/mod.rs:210-217).  Saturated keys flag their batch.
 // VEC: 16-B stores (two latencies / four losses per lane); needs n_used % 4 == 0
@@ -744,7 +900,7 @@ static void run_wide(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t 
 
 // B sources per batch, NPW destination nodes per wave item, STG arcs staged per
 // wave step, FRONT = stamp frontier.
-template <int B, int NPW, int STG, int GR, bool FRONT>
+template <int B, int NPW, int STG, int GR, bool FRONT, int SPL = 1>
 static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                              uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
   hipStream_t st = ctx->stream;
@@ -804,12 +960,22 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
                              nullptr);
         {
           TimedLaunch tl(ctx, "relax", 0.0);
-          if (work)
-            hipLaunchKernelGGL((k_relax_w<B, NPW, STG / 64, GR, FRONT, true>), dim3(grid), dim3(RELAX_THREADS), 0, st,
-                               net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
-          else
-            hipLaunchKernelGGL((k_relax_w<B, NPW, STG / 64, GR, FRONT, false>), dim3(grid), dim3(RELAX_THREADS), 0, st,
-                               net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
+          if constexpr (SPL == 2) {
+            static_assert(B == 64, "two sources per lane: B = 64");
+            if (work)
+              hipLaunchKernelGGL((k_relax_w2<NPW, STG / 64, GR, FRONT, true>), dim3(grid), dim3(RELAX_THREADS), 0,
+                                 st, net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
+            else
+              hipLaunchKernelGGL((k_relax_w2<NPW, STG / 64, GR, FRONT, false>), dim3(grid), dim3(RELAX_THREADS), 0,
+                                 st, net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
+          } else {
+            if (work)
+              hipLaunchKernelGGL((k_relax_w<B, NPW, STG / 64, GR, FRONT, true>), dim3(grid), dim3(RELAX_THREADS), 0,
+                                 st, net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
+            else
+              hipLaunchKernelGGL((k_relax_w<B, NPW, STG / 64, GR, FRONT, false>), dim3(grid), dim3(RELAX_THREADS), 0,
+                                 st, net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
+          }
         }
         SG_CHECK_LAUNCH();
         if (trace) {
@@ -877,8 +1043,36 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                            uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
   const bool front = env_int("SG_APSP_FRONTIER", 1) != 0;
-  const int bsz = env_int("SG_APSP_B", 64), npw = env_int("SG_APSP_NPW", 8), stg = env_int("SG_APSP_STAGE", 128);
-  const int gr = env_int("SG_APSP_GROUP", 8);
+  const int bsz = env_int("SG_APSP_B", 64);
+  const int spl = env_int("SG_APSP_SPL", bsz == 64 ? 2 : 1);  // sources per lane: 2 = k_relax_w2 (the default)
+  // defaults: the fastest measured configuration of each kernel (tools/apsp_variants.py)
+  const int npw = env_int("SG_APSP_NPW", spl == 2 ? 4 : 8), stg = env_int("SG_APSP_STAGE", spl == 2 ? 64 : 128);
+  const int gr = env_int("SG_APSP_GROUP", spl == 2 ? 3 : 8);
+  if (spl == 2) {
+#define SG_SP2(NPW_, STG_, GR_)                                                                          \
+  if (bsz == 64 && npw == NPW_ && stg == STG_ && gr == GR_) {                                           \
+    if (front)                                                                                          \
+      shortest_paths_t<64, NPW_, STG_, GR_, true, 2>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, \
+                                                     out_loss);                                         \
+    else                                                                                                \
+      shortest_paths_t<64, NPW_, STG_, GR_, false, 2>(ctx, net, d_used, n_used, row_begin, row_end,      \
+                                                      out_lat, out_loss);                               \
+    return;                                                                                             \
+  }
+    SG_SP2(8, 128, 8)
+    SG_SP2(8, 128, 4)
+    SG_SP2(8, 128, 2)
+    SG_SP2(8, 128, 6)
+    SG_SP2(8, 64, 4)
+    SG_SP2(4, 64, 4)
+    SG_SP2(4, 128, 4)
+    SG_SP2(2, 64, 4)
+    SG_SP2(4, 64, 3)
+    SG_SP2(4, 64, 5)
+    SG_SP2(16, 128, 4)
+#undef SG_SP2
+    throw Error(SG_ERR_INVALID_ARG, "unsupported SG_APSP_SPL=2 configuration");
+  }
 #define SG_SP(B_, NPW_, STG_, GR_)                                                                       \
   if (bsz == B_ && npw == NPW_ && stg == STG_ && gr == GR_) {                                           \
     if (front)                                                                                          \

@@ -12,7 +12,7 @@ run lvl SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INST_LEVEL_VMEM SQ_INST
 run tcc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE
 run fetch FETCH_SIZE
 run tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum
-python3 - "$OUT" "${KFILTER:-k_relax_w<}" <<'PY'
+python3 - "$OUT" "${KFILTER:-k_relax_w2<}" <<'PY'
 import csv, glob, sys, collections
 out, kf = sys.argv[1], sys.argv[2]
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
