@@ -119,7 +119,7 @@ def load_pmc(path):
 SERVICE_NS = 12_000  # 1500 B at 1 Gbit/s: the interface's pop spacing in the CoDel leg
 
 
-def codel_events(offsets, order, deliver_time, payload):
+def codel_events(offsets, order, deliver_time, length):
     """C4 round -> each destination's inbound CoDel stream: pushes at the arrival
     times (the bucket, in EventQueue order) and a FIFO server popping one packet
     every SERVICE_NS (s_j = max(a_j, s_{j-1}) + SERVICE_NS); per host in time order,
@@ -141,21 +141,36 @@ def codel_events(offsets, order, deliver_time, payload):
     ev_time = np.concatenate([arr, pop_t])
     ev_kind = np.concatenate([np.zeros(n, np.uint8), np.ones(n, np.uint8)])
     ev_pkt = np.concatenate([order.astype(np.int64), np.zeros(n, np.int64)])
-    ln = 28 + payload[order].astype(np.int64)  # IPv4 + UDP headers + payload (packet.rs:388-390)
+    ln = length[order].astype(np.int64)
     ev_len = np.concatenate([ln, np.zeros(n, np.int64)])
     idx = np.lexsort((ev_kind, ev_time, ev_host))
     return (ev_host[idx].astype(np.uint32), ev_kind[idx], ev_time[idx].astype(np.uint64),
             ev_pkt[idx].astype(np.uint32), ev_len[idx].astype(np.uint32))
 
 
-def codel_leg(a, D, ctx, torch, out, payload, n_packets, pmc):
+def round_buckets(out, payload, sharded):
+    """This rank's destination buckets of the last round: (offsets, order, deliver time
+    and packet length per order index).  Sharded: the received records; their payload
+    is not exchanged, so every length is a full 1476-B data packet."""
+    if sharded is None:
+        nd = int(out.n_delivered)
+        return (out.dst_offsets.cpu().numpy().view(np.uint32), out.dst_order[:nd].cpu().numpy().view(np.uint32),
+                out.deliver_time_ns.cpu().numpy().view(np.uint64),
+                (28 + np.asarray(payload, np.int64)).astype(np.uint32))  # IPv4 + UDP headers (packet.rs:388-390)
+    recv, order, offsets = sharded.last
+    rec = recv.cpu().numpy().view(np.uint64).reshape(-1, 4) if recv.shape[0] else np.zeros((0, 4), np.uint64)
+    order = np.asarray(order.cpu().numpy() if hasattr(order, "cpu") else order).view(np.uint32)
+    offsets = np.asarray(offsets.cpu().numpy() if hasattr(offsets, "cpu") else offsets).view(np.uint32)
+    return offsets, order, rec[:, 0].copy(), np.full(len(rec), 1476, np.uint32)
+
+
+def codel_leg(a, D, ctx, torch, buckets, n_packets, pmc):
     from shadow_amd.router import CoDelEvents, CoDelQueues
 
-    nd = int(out.n_delivered)
-    offs = out.dst_offsets.cpu().numpy().view(np.uint32)
-    order = out.dst_order[:nd].cpu().numpy().view(np.uint32)
-    dtime = out.deliver_time_ns.cpu().numpy().view(np.uint64)
-    evs = codel_events(offs, order, dtime, np.asarray(payload, np.uint32))
+    offs, order, dtime, lens = buckets
+    nd = len(order)
+    n_packets = max(n_packets, len(dtime))
+    evs = codel_events(offs, order, dtime, lens)
     E = len(evs[0])
     H = len(offs) - 1
     q = CoDelQueues(H, 256, ctx=ctx)
@@ -203,20 +218,20 @@ def codel_leg(a, D, ctx, torch, out, payload, n_packets, pmc):
 BW_DOWN_BITS = 10**9  # every host's bandwidth down in the inbound leg
 
 
-def inbound_leg(a, D, ctx, torch, out, payload, n_packets, pmc, round_end):
+def inbound_leg(a, D, ctx, torch, buckets, n_packets, pmc, round_end):
     """The C4 round's buckets through every destination's inbound pipeline: router
     CoDel queue -> relay_inet_in token bucket (1 Gbit/s down), one window that holds
     every arrival."""
     from shadow_amd.router import InboundPipeline
 
-    nd = int(out.n_delivered)
-    offs = out.dst_offsets.cpu().numpy().view(np.uint32).astype(np.int64)
-    order = out.dst_order[:nd].cpu().numpy().view(np.uint32)
-    dtime = out.deliver_time_ns.cpu().numpy().view(np.uint64)
+    offs, order, dtime, lens = buckets
+    offs = offs.astype(np.int64)
+    nd = len(order)
+    n_packets = max(n_packets, len(dtime))
     H = len(offs) - 1
     host = np.repeat(np.arange(H, dtype=np.uint32), np.diff(offs))
     t = dtime[order]
-    ln = (28 + np.asarray(payload, np.uint32)[order]).astype(np.uint32)
+    ln = lens[order].astype(np.uint32)
     window_end = int(t.max()) + 1 if nd else round_end + 1
     dev = lambda x, dt, tv: torch.from_numpy(np.ascontiguousarray(x, dtype=dt).view(tv)).cuda()
     args = (dev(host, np.uint32, np.int32), dev(t, np.uint64, np.int64), dev(order, np.uint32, np.int32),
@@ -459,8 +474,9 @@ def main():
             delivery["speedup_vs_cpu"] = round(delivery["value"] / delivery["cpu_baseline"]["value"], 1)
         result["delivery"] = delivery
         if not a.no_codel:
-            result["codel"] = codel_leg(a, D, ctx, torch, out, pk["payload"], a.packets, pmc)
-            result["inbound"] = inbound_leg(a, D, ctx, torch, out, pk["payload"], a.packets, pmc, round_end)
+            buckets = round_buckets(out, pk["payload"], sharded)
+            result["codel"] = codel_leg(a, D, ctx, torch, buckets, a.packets, pmc)
+            result["inbound"] = inbound_leg(a, D, ctx, torch, buckets, a.packets, pmc, round_end)
 
     if D.rank == 0:
         print(json.dumps(result), flush=True)

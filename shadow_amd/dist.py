@@ -167,6 +167,7 @@ class ShardedDelivery:
         self.local_dev = torch.from_numpy(partition.local.view(np.int32)).to(device)
         self.device = device
         self.last_stats = None
+        self.last = None
 
     def round(self, packets, round_end_ns: int, sim_end_ns: int, bootstrap_end_ns: int = 0):
         src = self.source_fn(self.ctx, self.hosts, self.table, packets, round_end_ns, sim_end_ns, bootstrap_end_ns,
@@ -176,4 +177,5 @@ class ShardedDelivery:
                                         len(self.part.local), self.part.n_local(self.rank))
         self.last_stats = gather_round_stats(int(src.n_delivered), int(src.min_deliver_time_ns),
                                              int(src.min_used_latency_ns), self.dist, self.group, self.device)
+        self.last = (recv, order, offsets)  # this rank's destination buckets of the round
         return src, recv, recv_counts, order, offsets
