@@ -68,6 +68,9 @@ def lib():
         L.sgo_inbound_run.argtypes = [C.c_uint32, C.c_uint32] + [C.c_void_p] * 19 + [C.c_uint32] + \
             [C.c_void_p] * 4 + [C.c_uint64] * 3 + [C.c_void_p] * 3 + [C.c_uint32]
         L.sgo_inbound_run.restype = C.c_int
+        L.sgo_deliver_round_mt.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32] + [C.c_void_p] * 4 + [
+            C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32] + [C.c_void_p] * 11 + [C.c_int]
+        L.sgo_deliver_round_mt.restype = C.c_int64
         L.sgo_deliver_round.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u32p, u32p, u32p, u64p,
                                         C.c_uint32, u32p, u32p, C.c_uint32, u64p, f32p, u64p, u64p, u8p, u64p,
                                         u64p, u32p, u32p, u64p, u64p]
@@ -158,7 +161,7 @@ def smallest_latency(lat: np.ndarray) -> int:
 
 
 def deliver_round(round_end, sim_end, bootstrap_end, src_host, dst_ip, payload_len, send_time,
-                  host_ip, host_row, tab_lat, tab_loss, rng, event_ctr):
+                  host_ip, host_row, tab_lat, tab_loss, rng, event_ctr, threads: int = 1):
     """Worker::send_packet over a round's batch (worker.rs:322-397) + event order (event.rs:84-155).
 
     rng (H x 4 u64) and event_ctr (H u64) are updated in place.
@@ -177,6 +180,16 @@ def deliver_round(round_end, sim_end, bootstrap_end, src_host, dst_ip, payload_l
     order = np.zeros(max(n, 1), np.uint32)
     offs = np.zeros(H + 1, np.uint32)
     mind, minl = C.c_uint64(), C.c_uint64()
+    if threads > 1:  # the multi-threaded restatement (same results; packets grouped by source host)
+        v = lambda a: a.ctypes.data_as(C.c_void_p)
+        nd = lib().sgo_deliver_round_mt(round_end, sim_end, bootstrap_end, n, v(src_host), v(dst_ip), v(payload_len),
+                                        v(send_time), H, v(host_ip), v(host_row), ncols, v(tab_lat), v(tab_loss),
+                                        v(rng), v(event_ctr), v(status), v(deliver), v(eid), v(order), v(offs),
+                                        C.byref(mind), C.byref(minl), int(threads))
+        if nd < 0:
+            raise ValueError("sgo_deliver_round_mt: bad argument")
+        return dict(status=status, deliver_time=deliver, event_id=eid, dst_order=order[:nd],
+                    dst_offsets=offs, min_deliver=mind.value, min_lat=minl.value, delivered=int(nd))
     nd = lib().sgo_deliver_round(round_end, sim_end, bootstrap_end, n, _p(src_host, C.c_uint32),
                                  _p(dst_ip, C.c_uint32), _p(payload_len, C.c_uint32), _p(send_time, C.c_uint64),
                                  H, _p(host_ip, C.c_uint32), _p(host_row, C.c_uint32), ncols,

@@ -962,3 +962,193 @@ int sgo_token_bucket_remove(uint64_t* st, uint64_t dec, uint64_t now, uint64_t* 
   st[3] = b.last;
   return ok;
 }
+
+/* ------------------------------------------------------------------------- */
+/* Multi-threaded deliver_round: the CPU baseline on the host's cores.       */
+/* ------------------------------------------------------------------------- */
+/* The reference runs Worker::send_packet on N worker threads, hosts
+ * round-robin to threads (thread_per_core.rs:62-64), each destination queue
+ * behind a lock.  This restatement gives each thread a contiguous range of
+ * source hosts (a host's packets stay on one thread: its RNG stream is
+ * sequential), then buckets by destination with per-thread histograms and a
+ * parallel per-destination sort.  Results are identical to sgo_deliver_round
+ * (per-host streams are independent; the bucket order is a total order). */
+typedef struct {
+  /* inputs */
+  uint64_t round_end, sim_end, bootstrap_end;
+  const uint32_t *src_host, *dst_ip, *payload_len;
+  const uint64_t* send_time;
+  uint32_t n_hosts, n_cols;
+  const uint32_t* host_row;
+  const uint64_t* tab_lat;
+  const float* tab_loss;
+  const ip_host* map;
+  uint64_t *rng, *event_ctr;
+  /* outputs */
+  uint8_t* status;
+  uint64_t *deliver_time, *event_id;
+  uint32_t* dst_host;
+  uint32_t *dst_offsets, *dst_order;
+  ord_item* tmp;
+  /* partition */
+  uint32_t T;
+  const uint32_t* pkt_begin; /* T + 1 packet boundaries (host-aligned) */
+  uint32_t* hist;            /* T x (n_hosts + 1) */
+  uint64_t *mind, *minl;
+  int64_t* delivered;
+  int err;
+} mt_job;
+
+typedef struct {
+  mt_job* J;
+  uint32_t t;
+  int phase;
+} mt_arg;
+
+static void* mt_worker(void* p) {
+  mt_arg* A = (mt_arg*)p;
+  mt_job* J = A->J;
+  const uint32_t t = A->t, H = J->n_hosts;
+  if (A->phase == 0) { /* send_packet for this thread's hosts, then its destination histogram */
+    uint64_t mind = UINT64_MAX, minl = UINT64_MAX;
+    int64_t nd = 0;
+    uint32_t* hist = J->hist + (size_t)t * (H + 1);
+    for (uint32_t i = J->pkt_begin[t]; i < J->pkt_begin[t + 1]; i++) {
+      const uint32_t s = J->src_host[i];
+      const uint64_t now = J->send_time[i];
+      J->deliver_time[i] = 0;
+      J->event_id[i] = UINT64_MAX;
+      J->dst_host[i] = UINT32_MAX;
+      if (now >= J->sim_end) {
+        J->status[i] = SGO_ST_SIM_END;
+        continue;
+      }
+      ip_host key = {J->dst_ip[i], 0};
+      const ip_host* f = (const ip_host*)bsearch(&key, J->map, H, sizeof(ip_host), cmp_ip);
+      if (!f) {
+        J->status[i] = SGO_ST_DROP_NO_DST;
+        continue;
+      }
+      const uint32_t d = f->host;
+      const size_t cell = (size_t)J->host_row[s] * J->n_cols + J->host_row[d];
+      const double reliability = (double)(1.0f - J->tab_loss[cell]);
+      const double chance = sgo_xoshiro_next_f64(&J->rng[4 * (size_t)s]);
+      if (!(now < J->bootstrap_end) && chance >= reliability && J->payload_len[i] > 0) {
+        J->status[i] = SGO_ST_DROP_LOSS;
+        continue;
+      }
+      const uint64_t delay = J->tab_lat[cell];
+      if (delay < minl) minl = delay;
+      uint64_t tt = now + delay;
+      if (tt < J->round_end) tt = J->round_end;
+      if (tt < mind) mind = tt;
+      J->status[i] = SGO_ST_DELIVERED;
+      J->deliver_time[i] = tt;
+      J->event_id[i] = J->event_ctr[s]++;
+      J->dst_host[i] = d;
+      hist[d]++;
+      nd++;
+    }
+    J->mind[t] = mind;
+    J->minl[t] = minl;
+    J->delivered[t] = nd;
+  } else if (A->phase == 1) { /* scatter this thread's packets to their destination slots */
+    uint32_t* cur = J->hist + (size_t)t * (H + 1); /* now: this thread's start in each bucket */
+    for (uint32_t i = J->pkt_begin[t]; i < J->pkt_begin[t + 1]; i++) {
+      const uint32_t d = J->dst_host[i];
+      if (d == UINT32_MAX) continue;
+      ord_item it = {J->deliver_time[i], J->src_host[i], J->event_id[i], i};
+      J->tmp[cur[d]++] = it;
+    }
+  } else { /* sort destination buckets [t*H/T, (t+1)*H/T) */
+    const uint32_t h0 = (uint32_t)((uint64_t)H * t / J->T), h1 = (uint32_t)((uint64_t)H * (t + 1) / J->T);
+    for (uint32_t h = h0; h < h1; h++) {
+      const uint32_t b = J->dst_offsets[h], e = J->dst_offsets[h + 1];
+      qsort(J->tmp + b, e - b, sizeof(ord_item), cmp_ord);
+      for (uint32_t k = b; k < e; k++) J->dst_order[k] = J->tmp[k].idx;
+    }
+  }
+  return NULL;
+}
+
+static void mt_run(mt_job* J, int phase) {
+  pthread_t th[64];
+  mt_arg args[64];
+  for (uint32_t t = 0; t < J->T; t++) {
+    args[t] = (mt_arg){J, t, phase};
+    if (pthread_create(&th[t], NULL, mt_worker, &args[t])) {
+      mt_worker(&args[t]);
+      th[t] = 0;
+    }
+  }
+  for (uint32_t t = 0; t < J->T; t++)
+    if (th[t]) pthread_join(th[t], NULL);
+}
+
+int64_t sgo_deliver_round_mt(uint64_t round_end, uint64_t sim_end, uint64_t bootstrap_end, uint32_t n_pkts,
+                             const uint32_t* src_host, const uint32_t* dst_ip, const uint32_t* payload_len,
+                             const uint64_t* send_time, uint32_t n_hosts, const uint32_t* host_ip,
+                             const uint32_t* host_row, uint32_t n_cols, const uint64_t* tab_lat,
+                             const float* tab_loss, uint64_t* rng, uint64_t* event_ctr, uint8_t* status,
+                             uint64_t* deliver_time, uint64_t* event_id, uint32_t* dst_order,
+                             uint32_t* dst_offsets, uint64_t* min_deliver, uint64_t* min_lat, int threads) {
+  uint32_t T = threads < 1 ? 1 : (threads > 64 ? 64 : (uint32_t)threads);
+  ip_host* map = (ip_host*)malloc(((size_t)n_hosts + 1) * sizeof(ip_host));
+  uint32_t* dst_host = (uint32_t*)malloc(((size_t)n_pkts + 1) * sizeof(uint32_t));
+  uint32_t* pb = (uint32_t*)malloc((T + 1) * sizeof(uint32_t));
+  uint32_t* hist = (uint32_t*)calloc((size_t)T * (n_hosts + 1), sizeof(uint32_t));
+  uint64_t mind[64], minl[64];
+  int64_t nd[64];
+  if (!map || !dst_host || !pb || !hist) return -1;
+  for (uint32_t h = 0; h < n_hosts; h++) {
+    map[h].ip = host_ip[h];
+    map[h].host = h;
+    if (host_row[h] >= n_cols) return -1;
+  }
+  qsort(map, n_hosts, sizeof(ip_host), cmp_ip);
+  for (uint32_t i = 0; i < n_pkts; i++)
+    if (src_host[i] >= n_hosts || (i && src_host[i] < src_host[i - 1])) return -1;  /* grouped by host */
+  /* T packet ranges of about equal size, cut at host boundaries */
+  pb[0] = 0;
+  for (uint32_t t = 1; t < T; t++) {
+    uint32_t i = (uint32_t)((uint64_t)n_pkts * t / T);
+    if (i < pb[t - 1]) i = pb[t - 1];
+    while (i > 0 && i < n_pkts && src_host[i] == src_host[i - 1]) i++;
+    pb[t] = i;
+  }
+  pb[T] = n_pkts;
+  mt_job J = {round_end, sim_end, bootstrap_end, src_host, dst_ip, payload_len, send_time, n_hosts, n_cols,
+              host_row, tab_lat, tab_loss, map, rng, event_ctr, status, deliver_time, event_id, dst_host,
+              dst_offsets, dst_order, NULL, T, pb, hist, mind, minl, nd, 0};
+  mt_run(&J, 0);
+  /* bucket offsets and each thread's start inside every bucket (thread order = packet order) */
+  int64_t delivered = 0;
+  uint64_t md = UINT64_MAX, ml = UINT64_MAX;
+  for (uint32_t t = 0; t < T; t++) {
+    delivered += nd[t];
+    if (mind[t] < md) md = mind[t];
+    if (minl[t] < ml) ml = minl[t];
+  }
+  uint32_t run = 0;
+  for (uint32_t h = 0; h < n_hosts; h++) {
+    dst_offsets[h] = run;
+    for (uint32_t t = 0; t < T; t++) {
+      const uint32_t c = hist[(size_t)t * (n_hosts + 1) + h];
+      hist[(size_t)t * (n_hosts + 1) + h] = run;
+      run += c;
+    }
+  }
+  dst_offsets[n_hosts] = run;
+  J.tmp = (ord_item*)malloc(((size_t)delivered + 1) * sizeof(ord_item));
+  if (!J.tmp) return -1;
+  mt_run(&J, 1);
+  mt_run(&J, 2);
+  free(J.tmp);
+  free(map);
+  free(dst_host);
+  free(pb);
+  free(hist);
+  *min_deliver = md;
+  *min_lat = ml;
+  return delivered;
+}

@@ -260,3 +260,31 @@ def test_deliver_bootstrap_and_order(oracle):
     # dst host 0 receives pkt1 (0->0, t=20+1000), pkt2 & pkt3 (1->0, t=10+5000): all clamp to round_end
     b, e = r["dst_offsets"][0], r["dst_offsets"][1]
     assert r["dst_order"][b:e].tolist() == [1, 2, 3]  # equal times: by (src_host, event_id)
+
+
+@pytest.mark.parametrize("threads", [2, 7, 16])
+def test_deliver_round_multithreaded_equals_sequential(oracle, threads):
+    """The CPU baseline's multi-threaded restatement (hosts split over threads, per-thread
+    destination histograms, parallel per-destination sort) is identical to the sequential one."""
+    rng = np.random.default_rng(threads)
+    n_nodes = 40
+    g = synth.ring_chords_graph(n_nodes, 5.0, seed=threads)
+    rc, lat, loss, _ = oracle.shortest_paths(n_nodes, g["src"], g["dst"], g["lat"], g["loss"], False,
+                                             np.arange(n_nodes, dtype=np.uint32), threads=4)
+    loss = loss.copy()
+    loss[::3, ::2] = np.float32(0.25)
+    hosts = synth.make_hosts(3000, n_nodes, general_seed=threads, exact_seeds=False)
+    t0 = 946684800 * 10**9
+    pk = synth.make_packets(50000, hosts, t0, t0 + 10**6, seed=threads, p_unknown_dst=0.01)
+    outs = []
+    for th in (1, threads):
+        r = np.stack([oracle.xoshiro_seed(int(s)) for s in hosts["seed"]]).astype(np.uint64)
+        c = np.zeros(len(hosts["seed"]), np.uint64)
+        o = oracle.deliver_round(t0 + 10**6, 2**63, t0 + 200_000, pk["src"], pk["dst_ip"], pk["payload"],
+                                 pk["send_time"], hosts["ip"], hosts["route"], lat, loss, r, c, threads=th)
+        outs.append((o, r, c))
+    (a, ra, ca), (b, rb, cb) = outs
+    for k in ("status", "deliver_time", "event_id", "dst_order", "dst_offsets"):
+        assert np.array_equal(a[k], b[k]), k
+    assert (a["delivered"], a["min_deliver"], a["min_lat"]) == (b["delivered"], b["min_deliver"], b["min_lat"])
+    assert np.array_equal(ra, rb) and np.array_equal(ca, cb)
