@@ -218,6 +218,87 @@ def codel_leg(a, D, ctx, torch, buckets, n_packets, pmc):
 BW_DOWN_BITS = 10**9  # every host's bandwidth down in the inbound leg
 
 
+BW_UP_BITS = 10**9  # every host's bandwidth up in the outbound leg
+HDR_BYTES = 40      # IPv4 + TCP headers: PacketRc::len() = payload + headers
+
+
+def outbound_leg(a, D, ctx, torch, pk, hosts, ht, table, round_end, sharded, pmc):
+    """The C4 round's sends through every source's outbound pipeline: interface fifo ->
+    relay_inet_out token bucket (1 Gbit/s up) -> router -> send_packet, one window holding
+    the round; and the fused round (outbound + delivery of the sent batch)."""
+    from shadow_amd.router import OutboundPipeline
+    from shadow_amd.worker import Deliveries, deliver_round
+
+    n, H = len(pk["src"]), hosts["n"]
+    ln = (pk["payload"] + HDR_BYTES).astype(np.uint32)
+    pkt = np.arange(n, dtype=np.uint32)
+    dev = lambda x, dt, tv: torch.from_numpy(np.ascontiguousarray(x, dtype=dt).view(tv)).cuda()
+    args = (dev(pk["src"], np.uint32, np.int32), dev(pk["send_time"], np.uint64, np.int64),
+            dev(pkt, np.uint32, np.int32), dev(ln, np.uint32, np.int32), dev(pk["payload"], np.uint32, np.int32),
+            dev(pk["dst_ip"], np.uint32, np.int32))
+    fwd = torch.full((max(n, 1),), -1, dtype=torch.int64, device="cuda")
+    status = torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")
+    bw = np.full(H, BW_UP_BITS, np.uint64)
+    n_pipes = 2 * (a.steps + a.warmup) + 1
+    pipes = [OutboundPipeline(hosts["ip"], bw, 64, ctx=ctx) for _ in range(n_pipes)]  # a fresh state per step
+    for p in pipes:
+        p.sent_buffers(n + 4 * H, "cuda")
+    it = iter(pipes)
+
+    def step():
+        return next(it).run(*args, round_end, 0, 2**63, fwd, status)
+
+    t_step = timed(D, step, a.steps, a.warmup)
+    out = Deliveries.allocate(n, H)
+
+    def fused():
+        batch, _ = step()
+        if sharded:
+            sharded.round(batch, round_end, 2**63, 0)
+        else:
+            deliver_round(ht, table, batch, round_end, 2**63, 0, out=out, ctx=ctx)
+
+    t_fused = timed(D, fused, a.steps, a.warmup)
+    ctx.enable_timers(True)
+    batch, _ = step()
+    k_ms, k_n, k_bytes = ctx.read_timer("outbound")
+    c_ms, c_n, _ = ctx.read_timer("out_compact")
+    ctx.enable_timers(False)
+    k_s = k_ms / 1e3 / max(k_n, 1)
+    ach = k_bytes / max(k_n, 1) / k_s / 1e9 if k_n else 0.0
+    leg = {
+        "metric": "outbound sends/sec (interface fifo -> relay token bucket -> send_packet batch, per host)",
+        "unit": "sends/s", "value": round(D.sum(float(n)) / t_step, 1), "higher_is_better": True,
+        "ms_per_window": round(t_step * 1e3, 4), "scaling": "weak", "dtype": "u64",
+        "config": {"workload": "the C4 round's sends (per source host in send order, len = payload + 40 B) through "
+                               "each host's interface and a 1 Gbit/s relay_inet_out token bucket, one window holding "
+                               "the round", "hosts": H, "sends_per_rank": n, "bw_up_bits": BW_UP_BITS},
+        "roofline": {"kernel": "k_outbound", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "traffic": pmc.get("outbound", {}).get("hbm_bytes_per_launch"),
+                     "avg_launch_ms": round(k_s * 1e3, 4)},
+        "compact_ms": round(c_ms / max(c_n, 1), 4),
+        "sent": len(batch),
+        "fused_round": {"ms": round(t_fused * 1e3, 4), "packets_per_s": round(D.sum(float(n)) / t_fused, 1),
+                        "what": "outbound window + delivery round of the sent batch"},
+    }
+    if D.rank == 0 and D.world == 1 and not a.no_cpu:
+        from oracle import oracle as O
+
+        st = O.outbound_state(hosts["ip"], bw, pipes[0].cap)
+        ctr = np.zeros(H, np.uint64)
+        ofwd = np.full(max(n, 1), np.uint64(2**64 - 1))
+        ost = np.zeros(max(n, 1), np.uint8)
+        t0 = time.perf_counter()
+        O.outbound_run(st, pk["src"], pk["send_time"], pkt, ln, pk["payload"], pk["dst_ip"], round_end, 0, 2**63,
+                       ctr, ofwd, ost)
+        tc = time.perf_counter() - t0
+        leg["cpu_baseline"] = {"value": round(n / tc, 1), "unit": "sends/s", "cores": 1, "kind": "port",
+                               "sample": f"the same {n} sends through the C restatement (interface fifo + "
+                                         "relay/mod.rs + token_bucket.rs), 1 thread"}
+    return leg
+
+
 def inbound_leg(a, D, ctx, torch, buckets, n_packets, pmc, round_end):
     """The C4 round's buckets through every destination's inbound pipeline: router
     CoDel queue -> relay_inet_in token bucket (1 Gbit/s down), one window that holds
@@ -479,6 +560,7 @@ def main():
             buckets = round_buckets(out, pk["payload"], sharded)
             result["codel"] = codel_leg(a, D, ctx, torch, buckets, a.packets, pmc)
             result["inbound"] = inbound_leg(a, D, ctx, torch, buckets, a.packets, pmc, round_end)
+            result["outbound"] = outbound_leg(a, D, ctx, torch, pk, hosts, ht, table, round_end, sharded, pmc)
 
     if D.rank == 0:
         print(json.dumps(result), flush=True)

@@ -355,6 +355,78 @@ typedef struct sg_inbound_relay_state { /* host arrays, n_hosts each */
 } sg_inbound_relay_state;
 int32_t sg_inbound_get_state(sg_inbound* ib, sg_codel_state* queue, sg_inbound_relay_state* relay);
 
+/* ---- outbound pipeline: network interface -> relay_inet_out -> router ------
+ * The send side of the relay.  A socket with data joins
+ * its interface's sending queue and relay_inet_out is notified
+ * (Host::notify_socket_has_packets, host.rs:930-945; interface.rs:168-182).
+ * Under the default fifo qdisc the interface pops the socket whose next packet
+ * has the smallest priority (interface.rs:225-260, queuing.rs:16-36), so
+ * packets leave in creation order: a host's sends are one FIFO.  The relay
+ * (relay/mod.rs:111-275) pops and forwards while its token bucket allows
+ * (bw_up: refill max(1, bw_up_bytes / 1000) every 1 ms, capacity refill + MTU,
+ * relay/mod.rs:278-319; no limit while bootstrapping).  A packet addressed to
+ * the host's own address goes back to the interface without using tokens
+ * (is_local, :222-226, :259-264); any other one goes to the router, whose push
+ * is Worker::send_packet at the forward task's time (router/mod.rs:41-43).
+ * Those packets form an sg_packets batch for sg_deliver_round.
+ *
+ * A call processes each host's sends (times < window_end, nondecreasing per
+ * host) and the relay's forward tasks before window_end; later tasks stay
+ * pending.  At equal times a send precedes a forward task (the task that a
+ * notify schedules runs after every send of that instant).  Assumes Shadow's
+ * CPU-delay model is off (host.rs:758-775; its default).                     */
+typedef struct sg_outbound sg_outbound;
+/* host_ipv4, bw_up_bits (host, n_hosts): each host's address and bandwidth up
+ * (HostInfo, bits/s).  ring_cap bounds, per host and call, the packets queued
+ * at the start (a cached one included) plus the call's sends; more fails the
+ * call with SG_ERR_CAPACITY. */
+int32_t sg_outbound_create(sg_ctx* ctx, uint32_t n_hosts, const uint32_t* host_ipv4, const uint64_t* bw_up_bits,
+                           uint32_t ring_cap, sg_outbound** out);
+void sg_outbound_destroy(sg_outbound* ob);
+uint32_t sg_outbound_ring_cap(const sg_outbound* ob);
+
+typedef struct sg_outbound_sends { /* device arrays, grouped by ascending host, interface order */
+  uint32_t n;
+  const uint32_t* host;
+  const uint64_t* time_ns;      /* when the socket handed the packet to the interface, < window_end */
+  const uint32_t* packet;       /* the caller's packet id (< n_packets) */
+  const uint32_t* len;          /* PacketRc::len() (packet.rs:388-390): the bucket's cost */
+  const uint32_t* payload_len;  /* PacketRc::payload_len(): carried into the sent batch */
+  const uint32_t* dst_ipv4;
+} sg_outbound_sends;
+
+enum { SG_OUT_QUEUED = 0, SG_OUT_SENT = 1 /* to the router: Worker::send_packet */,
+       SG_OUT_LOCAL = 2 /* dst == own address: back to the interface */ };
+
+/* The packets this call handed to send_packet, device arrays of capacity
+ * `cap`, grouped by ascending host and in each host's send order: the
+ * sg_packets of a delivery round (src_host, dst_ipv4, payload_len,
+ * send_time_ns), plus the caller's packet id. */
+typedef struct sg_outbound_sent {
+  uint32_t cap;
+  uint32_t *src_host, *dst_ipv4, *payload_len;
+  uint64_t* send_time_ns;
+  uint32_t* packet;
+} sg_outbound_sent;
+
+/* event_ctr (device, n_hosts, may be NULL): advanced by one per forward task
+ * scheduled (host.rs:649-653).  fwd_time / pkt_status (device, n_packets): the
+ * forward time and SG_OUT_SENT / SG_OUT_LOCAL of each packet the relay
+ * forwarded (untouched otherwise).  sent may be NULL; n_sent (host, may be
+ * NULL) receives the count.  SG_ERR_CAPACITY if sent->cap is too small. */
+int32_t sg_outbound_run(sg_ctx* ctx, sg_outbound* ob, const sg_outbound_sends* sends, uint64_t window_end_ns,
+                        uint64_t bootstrap_end_ns, uint64_t sim_end_ns, uint64_t* event_ctr, uint64_t* fwd_time,
+                        uint8_t* pkt_status, uint32_t n_packets, sg_outbound_sent* sent, uint32_t* n_sent);
+
+/* Host arrays: per host the ring head / tail counters and n_hosts * ring_cap
+ * slots (packet, len, payload_len, dst).  A cached packet (relay flags bit 2)
+ * is the slot at head - 1. */
+typedef struct sg_outbound_queue_state {
+  uint32_t *head, *tail;
+  uint32_t *ring_packet, *ring_len, *ring_payload_len, *ring_dst;
+} sg_outbound_queue_state;
+int32_t sg_outbound_get_state(sg_outbound* ob, sg_outbound_queue_state* queue, sg_inbound_relay_state* relay);
+
 /* The device array of the hosts' event-id counters (Host::event_id_counter). */
 uint64_t* sg_hosts_event_ctr(sg_hosts* hosts);
 

@@ -68,6 +68,10 @@ def lib():
         L.sgo_inbound_run.argtypes = [C.c_uint32, C.c_uint32] + [C.c_void_p] * 19 + [C.c_uint32] + \
             [C.c_void_p] * 4 + [C.c_uint64] * 3 + [C.c_void_p] * 3 + [C.c_uint32]
         L.sgo_inbound_run.restype = C.c_int
+        L.sgo_outbound_run.argtypes = [C.c_uint32, C.c_uint32] + [C.c_void_p] * 13 + [C.c_uint32] + \
+            [C.c_void_p] * 6 + [C.c_uint64] * 3 + [C.c_void_p] * 3 + [C.c_uint32] + [C.c_void_p] * 5 + \
+            [C.c_uint32, C.c_void_p]
+        L.sgo_outbound_run.restype = C.c_int
         L.sgo_deliver_round_mt.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32] + [C.c_void_p] * 4 + [
             C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32] + [C.c_void_p] * 11 + [C.c_int]
         L.sgo_deliver_round_mt.restype = C.c_int64
@@ -289,3 +293,41 @@ def inbound_run(st: dict, host, time, pkt, length, window_end: int, bootstrap_en
         v(fwd_time), v(pkt_status), len(pkt_status))
     if rc:
         raise ValueError(f"sgo_inbound_run: error {rc}")
+
+
+# Outbound pipeline: interface FIFO -> relay_inet_out -> router -> send_packet
+def outbound_state(host_ipv4, bw_up_bits: np.ndarray, cap: int, t0: int = 946684800 * 10**9) -> dict:
+    """Empty interface queues + Idle relays with full buckets (Relay::new / create_token_bucket,
+    relay/mod.rs:91-109, :278-319).  `cap` is rounded up to a power of two like the library's."""
+    n = len(bw_up_bits)
+    c = 1
+    while c < cap:
+        c <<= 1
+    refill = np.maximum(1, (np.asarray(bw_up_bits, np.uint64) // np.uint64(8)) // np.uint64(1000)).astype(np.uint64)
+    return dict(cap=c, host_ip=np.ascontiguousarray(host_ipv4, np.uint32), head=np.zeros(n, np.uint32),
+                tail=np.zeros(n, np.uint32), ring_pkt=np.zeros(n * c, np.uint32), ring_len=np.zeros(n * c, np.uint32),
+                ring_dst=np.zeros(n * c, np.uint32), ring_pay=np.zeros(n * c, np.uint32),
+                rflags=np.zeros(n, np.uint8), task_time=np.zeros(n, np.uint64), tb_cap=refill + np.uint64(CODEL_MTU),
+                tb_bal=refill + np.uint64(CODEL_MTU), tb_inc=refill, tb_last=np.full(n, t0, np.uint64))
+
+
+def outbound_run(st: dict, host, time, pkt, length, payload, dst, window_end: int, bootstrap_end: int,
+                 sim_end: int, event_ctr: np.ndarray, fwd_time: np.ndarray, pkt_status: np.ndarray) -> dict:
+    """One window of sends (sgo_outbound_run).  Returns the packets handed to send_packet, in order."""
+    host, time = _arr(host, np.uint32), _arr(time, np.uint64)
+    pkt, length, payload, dst = (_arr(x, np.uint32) for x in (pkt, length, payload, dst))
+    v = lambda a: a.ctypes.data_as(C.c_void_p)
+    H = len(st["head"])
+    cap_out = len(host) + int((st["tail"] - st["head"]).astype(np.uint64).sum()) + H
+    out = dict(src_host=np.zeros(cap_out, np.uint32), dst_ipv4=np.zeros(cap_out, np.uint32),
+               payload_len=np.zeros(cap_out, np.uint32), send_time=np.zeros(cap_out, np.uint64),
+               packet=np.zeros(cap_out, np.uint32))
+    n_out = C.c_uint32()
+    rc = lib().sgo_outbound_run(H, st["cap"], *[v(st[k]) for k in (
+        "host_ip", "head", "tail", "ring_pkt", "ring_len", "ring_dst", "ring_pay", "rflags", "task_time", "tb_cap",
+        "tb_bal", "tb_inc", "tb_last")], len(host), v(host), v(time), v(pkt), v(length), v(payload), v(dst),
+        window_end, bootstrap_end, sim_end, v(event_ctr), v(fwd_time), v(pkt_status), len(pkt_status),
+        *[v(out[k]) for k in ("src_host", "dst_ipv4", "payload_len", "send_time", "packet")], cap_out, C.byref(n_out))
+    if rc:
+        raise ValueError(f"sgo_outbound_run: error {rc}")
+    return {k: a[:n_out.value] for k, a in out.items()}

@@ -952,6 +952,117 @@ int sgo_inbound_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* ie
   return e == n_arr ? 0 : -4;
 }
 
+/* Outbound pipeline: NetworkInterface (fifo qdisc) -> relay_inet_out -> Router
+ * -> Worker::send_packet, per host over a window (relay/mod.rs:111-275,
+ * host.rs:930-945, interface.rs:168-260, router/mod.rs:41-43).  A host's sends
+ * are one FIFO in priority (= creation) order; the relay pops and forwards
+ * while its token bucket allows, a packet to the host's own address goes back
+ * to the interface without tokens, any other is sent at the task's time.  The
+ * FIFO is held as a ring of `cap` slots {packet, len, dst, payload_len}; the
+ * packet the relay caches (next_packet) is the slot at head - 1, and a call's
+ * pushes may not reach the oldest slot it still needs (the library's bound,
+ * -2 here).  Sends at a time precede a forward task at the same time.
+ * Sent packets are appended to out_* (send_packet order: hosts ascending).
+ * Returns 0, or -2 ring full, -3 packet id >= n_status, -4 not grouped,
+ * -5 a send at or after window_end, -6 a host's send times decrease,
+ * -7 more than out_cap sent. */
+int sgo_outbound_run(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip, uint32_t* head, uint32_t* tail,
+                     uint32_t* ring_pkt, uint32_t* ring_len, uint32_t* ring_dst, uint32_t* ring_pay,
+                     uint8_t* rflags, uint64_t* task_time, uint64_t* tb_cap, uint64_t* tb_bal, uint64_t* tb_inc,
+                     uint64_t* tb_last, uint32_t n_sends, const uint32_t* host, const uint64_t* time,
+                     const uint32_t* pkt, const uint32_t* len, const uint32_t* pay, const uint32_t* dst,
+                     uint64_t window_end, uint64_t bootstrap_end, uint64_t sim_end, uint64_t* event_ctr,
+                     uint64_t* fwd_time, uint8_t* pkt_status, uint32_t n_status, uint32_t* out_host,
+                     uint32_t* out_dst, uint32_t* out_pay, uint64_t* out_time, uint32_t* out_pkt, uint32_t out_cap,
+                     uint32_t* n_out) {
+  if (!cap) return -1;
+  uint32_t e = 0, no = 0;
+  *n_out = 0;
+  for (uint32_t h = 0; h < n_hosts; h++) {
+    const size_t base = (size_t)h * cap;
+    tb_t tb = {tb_cap[h], tb_bal[h], tb_inc[h], tb_last[h], TB_INTERVAL};
+    uint8_t rf = rflags[h];
+    uint64_t tt = task_time[h];
+    uint32_t hd = head[h], tl = tail[h];
+    const uint32_t oldest = hd - ((rf & RL_CACHED) ? 1u : 0u);
+    uint32_t e1 = e;
+    while (e1 < n_sends && host[e1] == h) e1++;
+    uint64_t last = 0;
+    for (;;) {
+      const int has_send = e < e1;
+      const int has_task = (rf & RL_PENDING) && !(rf & RL_NEVER) && tt < window_end;
+      if (has_send && time[e] >= window_end) return -5;
+      if (has_send && time[e] < last) return -6;
+      if (has_send && (!has_task || time[e] <= tt)) { /* add_data_source + Relay::notify */
+        const uint64_t now = time[e];
+        last = now;
+        if (tl - oldest >= cap) return -2;
+        const size_t slot = base + tl % cap;
+        ring_pkt[slot] = pkt[e];
+        ring_len[slot] = len[e];
+        ring_dst[slot] = dst[e];
+        ring_pay[slot] = pay[e];
+        tl++;
+        if (!(rf & RL_PENDING)) { /* Idle -> forward_later(ZERO) */
+          event_ctr[h]++;
+          rf |= RL_PENDING;
+          if (now >= sim_end) rf |= RL_NEVER;
+          tt = now;
+        }
+        e++;
+      } else if (has_task) { /* run_forward_task -> forward_until_blocked */
+        const uint64_t now = tt;
+        rf &= (uint8_t)~RL_PENDING;
+        for (;;) {
+          size_t slot;
+          if (rf & RL_CACHED) { /* next_packet.take() */
+            slot = base + (hd - 1) % cap;
+            rf &= (uint8_t)~RL_CACHED;
+          } else {
+            if (hd == tl) break; /* the interface is empty: Idle */
+            slot = base + hd % cap;
+            hd++;
+          }
+          const uint32_t p = ring_pkt[slot];
+          const int local = ring_dst[slot] == host_ip[h]; /* relay/mod.rs:222-226 */
+          uint64_t wait;
+          if (!local && now >= bootstrap_end && !tb_remove(&tb, ring_len[slot], now, &wait)) {
+            rf |= RL_CACHED | RL_PENDING; /* RelayCached; forward_later(wait) */
+            event_ctr[h]++;
+            const uint64_t at = now > UINT64_MAX - wait ? UINT64_MAX : now + wait;
+            if (at >= sim_end) rf |= RL_NEVER;
+            tt = at;
+            break;
+          }
+          if (p >= n_status) return -3;
+          pkt_status[p] = local ? 2 : 1;
+          fwd_time[p] = now;
+          if (!local) { /* Router::push -> Worker::send_packet(now) */
+            if (no >= out_cap) return -7;
+            out_host[no] = h;
+            out_dst[no] = ring_dst[slot];
+            out_pay[no] = ring_pay[slot];
+            out_time[no] = now;
+            out_pkt[no] = p;
+            no++;
+          }
+        }
+      } else {
+        break;
+      }
+    }
+    if (e != e1) return -4;
+    head[h] = hd;
+    tail[h] = tl;
+    rflags[h] = rf;
+    task_time[h] = tt;
+    tb_bal[h] = tb.bal;
+    tb_last[h] = tb.last;
+  }
+  *n_out = no;
+  return e == n_sends ? 0 : -4;
+}
+
 /* Test hook: TokenBucket::conforming_remove_inner on an explicit state
  * {capacity, balance, refill_increment, last_refill, refill_interval}.
  * Returns 1 (ok, balance updated) or 0 (*wait = conforming duration). */

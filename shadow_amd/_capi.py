@@ -40,7 +40,8 @@ EXPORTED = [
     "sg_hosts_destroy", "sg_deliver_round", "sg_deliver_source", "sg_deliver_bucket",
     "sg_table_pack", "sg_codel_create", "sg_codel_destroy", "sg_codel_run", "sg_codel_ring_cap",
     "sg_codel_get_state", "sg_codel_set_state", "sg_inbound_create", "sg_inbound_destroy", "sg_inbound_ring_cap",
-    "sg_inbound_run", "sg_inbound_get_state", "sg_hosts_event_ctr",
+    "sg_inbound_run", "sg_inbound_get_state", "sg_hosts_event_ctr", "sg_outbound_create", "sg_outbound_destroy",
+    "sg_outbound_ring_cap", "sg_outbound_run", "sg_outbound_get_state",
 ]
 
 
@@ -87,6 +88,20 @@ class sg_inbound_arrivals(C.Structure):
 class sg_inbound_relay_state(C.Structure):
     _fields_ = [(k, C.c_void_p) for k in ("flags", "task_time", "cached_packet", "cached_len", "tb_capacity",
                                           "tb_balance", "tb_increment", "tb_last_refill")]
+
+
+class sg_outbound_sends(C.Structure):
+    _fields_ = [("n", C.c_uint32)] + [(k, C.c_void_p) for k in ("host", "time_ns", "packet", "len", "payload_len",
+                                                                  "dst_ipv4")]
+
+
+class sg_outbound_sent(C.Structure):
+    _fields_ = [("cap", C.c_uint32)] + [(k, C.c_void_p) for k in ("src_host", "dst_ipv4", "payload_len",
+                                                                    "send_time_ns", "packet")]
+
+
+class sg_outbound_queue_state(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("head", "tail", "ring_packet", "ring_len", "ring_payload_len", "ring_dst")]
 
 
 class sg_round(C.Structure):
@@ -176,6 +191,12 @@ def load(path: str | None = None):
         "sg_inbound_run": (i32, [vp, vp, C.POINTER(sg_inbound_arrivals), u64, u64, u64, vp, vp, vp, u32, u64p]),
         "sg_inbound_get_state": (i32, [vp, C.POINTER(sg_codel_state), C.POINTER(sg_inbound_relay_state)]),
         "sg_hosts_event_ctr": (vp, [vp]),
+        "sg_outbound_create": (i32, [vp, u32, vp, vp, u32, C.POINTER(vp)]),
+        "sg_outbound_destroy": (None, [vp]),
+        "sg_outbound_ring_cap": (u32, [vp]),
+        "sg_outbound_run": (i32, [vp, vp, C.POINTER(sg_outbound_sends), u64, u64, u64, vp, vp, vp, u32,
+                                  C.POINTER(sg_outbound_sent), C.POINTER(C.c_uint32)]),
+        "sg_outbound_get_state": (i32, [vp, C.POINTER(sg_outbound_queue_state), C.POINTER(sg_inbound_relay_state)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)

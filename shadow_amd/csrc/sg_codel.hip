@@ -505,6 +505,269 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
   }
 }
 
+// ---- outbound pipeline: interface FIFO -> relay_inet_out -> router --------
+// Per host: sends push {packet, len, dst, payload_len} records into a ring
+// (the interface's fifo qdisc); the relay's forward task pops them in order.
+// The packet a blocked relay caches is the slot at head - 1 (never
+// overwritten: a call's pushes may not reach the oldest slot it has to keep),
+// so the records a call forwarded are still in the ring afterwards and
+// k_out_compact gathers the sent batch from there -- no staging copy.
+enum : uint32_t { E_ORDER = 128 };
+
+struct OutboundArgs {
+  const uint32_t* host_off;
+  uint32_t H, E;
+  const uint64_t* time;
+  const uint32_t *pkt, *len, *payload, *dst;
+  const uint32_t* host_ip;
+  uint32_t *head, *tail;
+  uint4* ring;  // {packet, len, dst, payload_len}
+  uint32_t cap;
+  uint8_t* rflags;
+  uint64_t* task_time;
+  uint64_t *tb_cap, *tb_bal, *tb_inc, *tb_last;
+  uint64_t window_end, bootstrap_end, sim_end;
+  uint64_t* event_ctr;
+  uint64_t* fwd_time;
+  uint8_t* status;
+  uint32_t n_status;
+  uint32_t* start;  // per host: the first ring slot this call forwarded from
+  unsigned long long* blk;
+};
+
+struct OutQ {
+  uint32_t head, tail, oldest, mask, ip;
+  uint4* ring;
+  uint4 hr;  // the head record (valid while head < tail), loaded ahead of its pop
+  uint32_t sent;
+  uint32_t err;
+  __device__ void load_head() {
+    if (head != tail) hr = ring[head & mask];
+  }
+};
+
+// The relay's forward task at `now` (run_forward_task -> forward_until_blocked),
+// the interface as its source.
+__device__ void out_task(OutQ& q, Relay& r, uint64_t now, const OutboundArgs& a, uint64_t& ctr_inc) {
+  r.rf &= (uint8_t)~R_PENDING;
+  for (;;) {
+    uint4 rec;
+    if (r.rf & R_CACHED) {  // next_packet.take(): the slot at head - 1
+      rec = q.ring[(q.head - 1) & q.mask];
+      r.rf &= (uint8_t)~R_CACHED;
+    } else {
+      if (q.head == q.tail) return;  // the interface has nothing: Idle
+      rec = q.hr;
+      q.head++;
+      q.load_head();
+    }
+    const bool local = rec.z == q.ip;
+    uint64_t wait;
+    if (!local && now >= a.bootstrap_end && !r.remove(rec.y, now, wait)) {
+      r.rf |= R_CACHED | R_PENDING;  // RelayCached; forward_later(wait)
+      ctr_inc++;
+      r.tt = now > ~0ull - wait ? ~0ull : now + wait;
+      if (r.tt >= a.sim_end) r.rf |= R_NEVER;
+      return;
+    }
+    if (rec.x < a.n_status) {
+      a.status[rec.x] = local ? SG_OUT_LOCAL : SG_OUT_SENT;
+      a.fwd_time[rec.x] = now;
+    } else {
+      q.err |= E_PKT;
+    }
+    q.sent += local ? 0 : 1;
+  }
+}
+
+__global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
+  __shared__ uint64_t s_t[CD_CHUNK];
+  __shared__ uint4 s_r[CD_CHUNK];
+  const uint32_t h0 = blockIdx.x * CD_HOSTS, t = threadIdx.x;
+  const uint32_t p0 = min(a.host_off[min(h0, a.H)], a.E);
+  const uint32_t p1 = max(min(a.host_off[min(h0 + CD_HOSTS, a.H)], a.E), p0);
+  const uint32_t h = h0 + t;
+  const bool walker = t < CD_HOSTS && h < a.H;
+  uint32_t hb = 0, he = 0;
+  OutQ q{};
+  Relay r{};
+  uint64_t ctr_inc = 0, last = 0;
+  if (walker) {
+    hb = min(a.host_off[h], a.E);
+    he = max(min(a.host_off[h + 1], a.E), hb);
+    q.head = a.head[h];
+    q.tail = a.tail[h];
+    q.mask = a.cap - 1;
+    q.ip = a.host_ip[h];
+    q.ring = a.ring + (size_t)h * a.cap;
+    r.rf = a.rflags[h];
+    r.tt = a.task_time[h];
+    r.cap = a.tb_cap[h];
+    r.bal = a.tb_bal[h];
+    r.inc = a.tb_inc[h];
+    r.last = a.tb_last[h];
+    q.oldest = q.head - ((r.rf & R_CACHED) ? 1u : 0u);
+    q.load_head();
+  }
+  auto due = [&](uint64_t before) { return (r.rf & R_PENDING) && !(r.rf & R_NEVER) && r.tt < before; };
+  for (uint32_t c0 = p0; c0 < p1; c0 += CD_CHUNK) {
+    const uint32_t c1 = min(c0 + CD_CHUNK, p1);
+    for (uint32_t i = c0 + t; i < c1; i += CD_THREADS) {
+      const uint32_t k = i - c0;
+      s_t[k] = a.time[i];
+      s_r[k] = make_uint4(a.pkt[i], a.len[i], a.dst[i], a.payload[i]);
+    }
+    __syncthreads();
+    if (walker) {
+      const uint32_t b = max(hb, c0), e = min(he, c1);
+      for (uint32_t i = b; i < e; i++) {
+        const uint32_t k = i - c0;
+        const uint64_t now = s_t[k];
+        if (now >= a.window_end) q.err |= E_WINDOW;
+        if (now < last) q.err |= E_ORDER;
+        last = now;
+        while (due(now)) out_task(q, r, r.tt, a, ctr_inc);
+        if (q.tail - q.oldest >= a.cap) {  // the push would overwrite a slot this call still needs
+          q.err |= E_FULL;
+          continue;
+        }
+        const uint4 rec = s_r[k];
+        q.ring[q.tail & q.mask] = rec;  // NetworkInterface::add_data_source
+        if (q.head == q.tail) q.hr = rec;
+        q.tail++;
+        if (!(r.rf & R_PENDING)) {  // Relay::notify: Idle -> forward_later(ZERO)
+          ctr_inc++;
+          r.rf |= R_PENDING;
+          if (now >= a.sim_end) r.rf |= R_NEVER;
+          r.tt = now;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  unsigned long long err = 0, sent = 0;
+  if (walker) {
+    while (due(a.window_end)) out_task(q, r, r.tt, a, ctr_inc);
+    a.head[h] = q.head;
+    a.tail[h] = q.tail;
+    a.rflags[h] = r.rf;
+    a.task_time[h] = r.tt;
+    a.tb_bal[h] = r.bal;
+    a.tb_last[h] = r.last;
+    a.start[h] = q.oldest;
+    if (a.event_ctr && ctr_inc) a.event_ctr[h] += ctr_inc;
+    err = q.err;
+    sent = q.sent;
+  }
+  if (t < 64) {
+    for (int d = 32; d > 0; d >>= 1) {
+      sent += __shfl_xor(sent, d, 64);
+      err |= __shfl_xor(err, d, 64);
+    }
+    if (t == 0) {
+      a.blk[2 * blockIdx.x] = sent;
+      a.blk[2 * blockIdx.x + 1] = err;
+    }
+  }
+}
+
+// Exclusive prefix of the k_outbound blocks' sent counts (blk[2b]) -> boff[b]:
+// where each block's slice of the sent batch starts.  One block.
+__global__ void __launch_bounds__(1024) k_blk_offsets(const unsigned long long* __restrict__ blk, uint32_t nb,
+                                                      uint32_t* __restrict__ boff) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry;
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < nb; c0 += 1024) {
+    const uint32_t i = c0 + t;
+    const uint32_t v = i < nb ? (uint32_t)blk[2 * i] : 0;
+    uint32_t x = v;  // inclusive wave scan
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t before = carry;
+    for (uint32_t w = 0; w < wv; w++) before += wsum[w];
+    if (i < nb) boff[i] = before + x - v;
+    __syncthreads();
+    if (t == 1023) carry = before + x;
+    __syncthreads();
+  }
+}
+
+// The sent batch: block b owns hosts [64b, 64b + 64), whose forwarded records
+// are ring slots [start, end) per host (end = head, less a packet cached at the
+// end).  The block walks the hosts' slot ranges as one concatenated sequence,
+// 256 slots per step (coalesced within a host's range), skips local packets
+// (a ballot prefix gives each kept record its rank) and writes its slice
+// [boff[b], boff[b] + sent) of the batch with coalesced stores.
+__global__ void __launch_bounds__(256) k_out_compact(uint32_t H, const uint32_t* __restrict__ start,
+                                                     const uint32_t* __restrict__ head,
+                                                     const uint8_t* __restrict__ rflags,
+                                                     const uint32_t* __restrict__ host_ip,
+                                                     const uint4* __restrict__ ring, uint32_t cap,
+                                                     const uint64_t* __restrict__ fwd_time, uint32_t n_status,
+                                                     const uint32_t* __restrict__ boff, sg_outbound_sent out) {
+  __shared__ uint32_t s_off[CD_HOSTS + 1], s_start[CD_HOSTS], s_ip[CD_HOSTS];
+  __shared__ uint32_t wsum[4];
+  const uint32_t h0 = blockIdx.x * CD_HOSTS, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t < 64) {  // one wave: per-host slot counts and their exclusive prefix
+    const uint32_t h = h0 + t;
+    uint32_t len = 0;
+    if (h < H) {
+      const uint32_t st = start[h], end = head[h] - ((rflags[h] & R_CACHED) ? 1u : 0u);
+      len = end - st;
+      s_start[t] = st;
+      s_ip[t] = host_ip[h];
+    }
+    uint32_t x = len;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    s_off[t + 1] = x;
+    if (t == 0) s_off[0] = 0;
+  }
+  __syncthreads();
+  const uint32_t S = s_off[CD_HOSTS], mask = cap - 1;
+  uint32_t o = boff[blockIdx.x];
+  for (uint32_t j0 = 0; j0 < S; j0 += 256) {
+    const uint32_t j = j0 + t;
+    bool keep = false;
+    uint4 rec = make_uint4(0, 0, 0, 0);
+    uint32_t k = 0;
+    if (j < S) {
+      uint32_t lo = 0, hi = CD_HOSTS;  // the host k with s_off[k] <= j < s_off[k + 1]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_off[mid] <= j) lo = mid;
+        else hi = mid;
+      }
+      k = lo;
+      rec = ring[(size_t)(h0 + k) * cap + ((s_start[k] + (j - s_off[k])) & mask)];
+      keep = rec.z != s_ip[k];
+    }
+    const uint64_t m = __ballot(keep);
+    if (lane == 0) wsum[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pos = o + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    for (uint32_t w = 0; w < wv; w++) pos += wsum[w];
+    if (keep && pos < out.cap) {
+      out.src_host[pos] = h0 + k;
+      out.dst_ipv4[pos] = rec.z;
+      out.payload_len[pos] = rec.w;
+      out.send_time_ns[pos] = rec.x < n_status ? fwd_time[rec.x] : 0;
+      out.packet[pos] = rec.x;
+    }
+    o += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+}
+
 }  // namespace
 }  // namespace sg
 
@@ -793,6 +1056,218 @@ int32_t sg_inbound_get_state(sg_inbound* ib, sg_codel_state* queue, sg_inbound_r
     for (auto& c : cp)
       if (c.h && c.b) SG_HIP(hipMemcpyAsync(c.h, c.d, c.b, hipMemcpyDeviceToHost, st));
     SG_HIP(hipStreamSynchronize(st));
+  });
+}
+
+}  // extern "C"
+
+struct sg_outbound {
+  sg_ctx* ctx = nullptr;
+  uint32_t n = 0, cap = 0;
+  uint32_t *host_ip = nullptr, *head = nullptr, *tail = nullptr, *start = nullptr, *off = nullptr;
+  uint4* ring = nullptr;
+  uint8_t* rflags = nullptr;
+  uint64_t *task_time = nullptr, *tb_cap = nullptr, *tb_bal = nullptr, *tb_inc = nullptr, *tb_last = nullptr;
+  unsigned long long* ret = nullptr;  // pinned host-mapped: [sent, error flags]
+  ~sg_outbound() {
+    void* ps[] = {host_ip, head, tail, start, off, ring, rflags, task_time, tb_cap, tb_bal, tb_inc, tb_last};
+    for (void* p : ps)
+      if (p) (void)hipFree(p);
+    if (ret) (void)hipHostFree(ret);
+  }
+};
+
+extern "C" {
+
+int32_t sg_outbound_create(sg_ctx* ctx, uint32_t n_hosts, const uint32_t* host_ipv4, const uint64_t* bw_up_bits,
+                           uint32_t ring_cap, sg_outbound** out) {
+  if (!out) return SG_ERR_INVALID_ARG;
+  *out = nullptr;
+  sg_outbound* ob = nullptr;
+  int32_t rc = sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (ring_cap == 0 || ring_cap > (1u << 30)) throw Error(SG_ERR_INVALID_ARG, "ring_cap must be in [1, 2^30]");
+    if (n_hosts && (!host_ipv4 || !bw_up_bits)) throw Error(SG_ERR_INVALID_ARG, "null address or bandwidth array");
+    uint32_t cap = 1;
+    while (cap < ring_cap) cap <<= 1;
+    ob = new sg_outbound();
+    ob->ctx = ctx;
+    ob->n = n_hosts;
+    ob->cap = cap;
+    const size_t n = std::max<uint32_t>(n_hosts, 1);
+    SG_HIP(hipMalloc(&ob->host_ip, n * 4));
+    SG_HIP(hipMalloc(&ob->head, n * 4));
+    SG_HIP(hipMalloc(&ob->tail, n * 4));
+    SG_HIP(hipMalloc(&ob->start, n * 4));
+    SG_HIP(hipMalloc(&ob->off, ((n + CD_HOSTS - 1) / CD_HOSTS + 1) * 4));  // per k_outbound block
+    SG_HIP(hipMalloc(&ob->ring, n * cap * 16));
+    SG_HIP(hipMalloc(&ob->rflags, n));
+    SG_HIP(hipMalloc(&ob->task_time, n * 8));
+    SG_HIP(hipMalloc(&ob->tb_cap, n * 8));
+    SG_HIP(hipMalloc(&ob->tb_bal, n * 8));
+    SG_HIP(hipMalloc(&ob->tb_inc, n * 8));
+    SG_HIP(hipMalloc(&ob->tb_last, n * 8));
+    SG_HIP(hipHostMalloc(&ob->ret, 16, hipHostMallocMapped | hipHostMallocCoherent));
+    // Relay::new (relay/mod.rs:91-109): Idle, nothing cached, a full bucket;
+    // the interface's queue empty
+    std::vector<uint64_t> inc(n), tcap(n), last(n, 946684800ull * 1000000000ull);  // EmulatedTime::SIMULATION_START
+    for (uint32_t h = 0; h < n_hosts; h++) {
+      inc[h] = std::max<uint64_t>(1, (bw_up_bits[h] / 8) / 1000);  // create_token_bucket (:278-315)
+      tcap[h] = inc[h] + CD_MTU;                                   // + get_burst_allowance (:317-319)
+    }
+    hipStream_t st = ctx->stream;
+    if (n_hosts) SG_HIP(hipMemcpyAsync(ob->host_ip, host_ipv4, (size_t)n_hosts * 4, hipMemcpyHostToDevice, st));
+    SG_HIP(hipMemsetAsync(ob->head, 0, n * 4, st));
+    SG_HIP(hipMemsetAsync(ob->tail, 0, n * 4, st));
+    SG_HIP(hipMemsetAsync(ob->rflags, 0, n, st));
+    SG_HIP(hipMemsetAsync(ob->task_time, 0, n * 8, st));
+    SG_HIP(hipMemcpyAsync(ob->tb_cap, tcap.data(), n * 8, hipMemcpyHostToDevice, st));
+    SG_HIP(hipMemcpyAsync(ob->tb_bal, tcap.data(), n * 8, hipMemcpyHostToDevice, st));
+    SG_HIP(hipMemcpyAsync(ob->tb_inc, inc.data(), n * 8, hipMemcpyHostToDevice, st));
+    SG_HIP(hipMemcpyAsync(ob->tb_last, last.data(), n * 8, hipMemcpyHostToDevice, st));
+    SG_HIP(hipStreamSynchronize(st));
+  });
+  if (rc != SG_OK) {
+    delete ob;
+    return rc;
+  }
+  *out = ob;
+  return SG_OK;
+}
+
+void sg_outbound_destroy(sg_outbound* ob) {
+  if (!ob) return;
+  if (ob->ctx) (void)hipSetDevice(ob->ctx->device);
+  delete ob;
+}
+
+uint32_t sg_outbound_ring_cap(const sg_outbound* ob) { return ob ? ob->cap : 0; }
+
+int32_t sg_outbound_run(sg_ctx* ctx, sg_outbound* ob, const sg_outbound_sends* s, uint64_t window_end_ns,
+                        uint64_t bootstrap_end_ns, uint64_t sim_end_ns, uint64_t* event_ctr, uint64_t* fwd_time,
+                        uint8_t* pkt_status, uint32_t n_packets, sg_outbound_sent* sent, uint32_t* n_sent) {
+  return sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (!ob || !s || ob->ctx != ctx) throw Error(SG_ERR_INVALID_ARG, "null argument");
+    const uint32_t E = s->n, H = ob->n;
+    if (n_sent) *n_sent = 0;
+    if (E && (!s->host || !s->time_ns || !s->packet || !s->len || !s->payload_len || !s->dst_ipv4))
+      throw Error(SG_ERR_INVALID_ARG, "null send array");
+    if (n_packets && (!pkt_status || !fwd_time)) throw Error(SG_ERR_INVALID_ARG, "null output array");
+    if (sent && sent->cap && (!sent->src_host || !sent->dst_ipv4 || !sent->payload_len || !sent->send_time_ns ||
+                              !sent->packet))
+      throw Error(SG_ERR_INVALID_ARG, "null sent-batch array");
+    if (!H) return;
+    hipStream_t st = ctx->stream;
+    uint32_t* ws = ctx->d_seg.get<uint32_t>((size_t)H + 8);
+    uint32_t* gerr = ws + (size_t)H + 1;
+    SG_HIP(hipMemsetAsync(gerr, 0, 4, st));
+    if (E) {
+      launch_group_offsets(ctx, s->host, E, H, ws, gerr);
+    } else {
+      SG_HIP(hipMemsetAsync(ws, 0, ((size_t)H + 1) * 4, st));  // no sends: pending tasks only
+    }
+    const uint32_t nb = (H + CD_HOSTS - 1) / CD_HOSTS;
+    OutboundArgs a;
+    a.host_off = ws;
+    a.H = H;
+    a.E = E;
+    a.time = s->time_ns;
+    a.pkt = s->packet;
+    a.len = s->len;
+    a.payload = s->payload_len;
+    a.dst = s->dst_ipv4;
+    a.host_ip = ob->host_ip;
+    a.head = ob->head;
+    a.tail = ob->tail;
+    a.ring = ob->ring;
+    a.cap = ob->cap;
+    a.rflags = ob->rflags;
+    a.task_time = ob->task_time;
+    a.tb_cap = ob->tb_cap;
+    a.tb_bal = ob->tb_bal;
+    a.tb_inc = ob->tb_inc;
+    a.tb_last = ob->tb_last;
+    a.window_end = window_end_ns;
+    a.bootstrap_end = bootstrap_end_ns;
+    a.sim_end = sim_end_ns;
+    a.event_ctr = event_ctr;
+    a.fwd_time = fwd_time;
+    a.status = pkt_status;
+    a.n_status = n_packets;
+    a.start = ob->start;
+    a.blk = ctx->d_blk.get<unsigned long long>(2 * (size_t)nb);
+    {
+      // per send: 24 B in, a 16-B ring record written and read, 9 B out; per host: ~90 B of state
+      TimedLaunch tl(ctx, "outbound", 65.0 * E + 90.0 * H);
+      hipLaunchKernelGGL(k_outbound, dim3(nb), dim3(CD_THREADS), 0, st, a);
+    }
+    if (sent) {
+      hipLaunchKernelGGL(k_blk_offsets, dim3(1), dim3(1024), 0, st, a.blk, nb, ob->off);
+      sg_outbound_sent o = *sent;
+      TimedLaunch tl(ctx, "out_compact", 0.0);
+      hipLaunchKernelGGL(k_out_compact, dim3(nb), dim3(256), 0, st, H, ob->start, ob->head, ob->rflags, ob->host_ip,
+                         ob->ring, ob->cap, fwd_time, n_packets, ob->off, o);
+    }
+    hipLaunchKernelGGL(k_codel_reduce, dim3(1), dim3(1024), 0, st, a.blk, nb, gerr, ob->ret);
+    SG_CHECK_LAUNCH();
+    SG_HIP(hipStreamSynchronize(st));
+    const volatile unsigned long long* r = ob->ret;
+    const uint64_t err = r[1];
+    if (err & E_UNSORTED) throw Error(SG_ERR_UNSORTED, "sends must be grouped by ascending host");
+    if (err & E_HOST) throw Error(SG_ERR_INVALID_ARG, "send host out of range");
+    if (err & E_ORDER) throw Error(SG_ERR_UNSORTED, "a host's send times must not decrease");
+    if (err & E_FULL) throw Error(SG_ERR_CAPACITY, "an interface queue outgrew its ring (raise ring_cap)");
+    if (err & E_PKT) throw Error(SG_ERR_INVALID_ARG, "packet id >= n_packets");
+    if (err & E_WINDOW) throw Error(SG_ERR_INVALID_ARG, "a send is at or after window_end");
+    const uint64_t ns = r[0];
+    if (n_sent) *n_sent = (uint32_t)ns;
+    if (sent && ns > sent->cap) throw Error(SG_ERR_CAPACITY, "the sent batch exceeds sent->cap");
+  });
+}
+
+int32_t sg_outbound_get_state(sg_outbound* ob, sg_outbound_queue_state* o, sg_inbound_relay_state* rl) {
+  if (!ob) return SG_ERR_INVALID_ARG;
+  return sg::guarded(ob->ctx, [&] {
+    const size_t n = ob->n, r = n * ob->cap;
+    hipStream_t st = ob->ctx->stream;
+    if (o) {
+      struct { void* h; const void* d; size_t b; } cp[] = {{o->head, ob->head, n * 4}, {o->tail, ob->tail, n * 4}};
+      for (auto& c : cp)
+        if (c.h && c.b) SG_HIP(hipMemcpyAsync(c.h, c.d, c.b, hipMemcpyDeviceToHost, st));
+    }
+    if (rl) {
+      struct { void* h; const void* d; size_t b; } cp[] = {
+          {rl->flags, ob->rflags, n}, {rl->task_time, ob->task_time, n * 8}, {rl->tb_capacity, ob->tb_cap, n * 8},
+          {rl->tb_balance, ob->tb_bal, n * 8}, {rl->tb_increment, ob->tb_inc, n * 8},
+          {rl->tb_last_refill, ob->tb_last, n * 8}};
+      for (auto& c : cp)
+        if (c.h && c.b) SG_HIP(hipMemcpyAsync(c.h, c.d, c.b, hipMemcpyDeviceToHost, st));
+    }
+    std::vector<uint4> ring(o ? r : 0);
+    if (o && r) SG_HIP(hipMemcpyAsync(ring.data(), ob->ring, r * 16, hipMemcpyDeviceToHost, st));
+    SG_HIP(hipStreamSynchronize(st));
+    if (o)
+      for (size_t i = 0; i < r; i++) {
+        if (o->ring_packet) o->ring_packet[i] = ring[i].x;
+        if (o->ring_len) o->ring_len[i] = ring[i].y;
+        if (o->ring_dst) o->ring_dst[i] = ring[i].z;
+        if (o->ring_payload_len) o->ring_payload_len[i] = ring[i].w;
+      }
+    // the relay's cached packet is the ring slot at head - 1 (no separate fields)
+    if (rl && (rl->cached_packet || rl->cached_len)) {
+      std::vector<uint32_t> head(n);
+      std::vector<uint8_t> fl(n);
+      SG_HIP(hipMemcpy(head.data(), ob->head, n * 4, hipMemcpyDeviceToHost));
+      SG_HIP(hipMemcpy(fl.data(), ob->rflags, n, hipMemcpyDeviceToHost));
+      for (size_t h = 0; h < n; h++) {
+        uint4 rec = make_uint4(0, 0, 0, 0);
+        if (fl[h] & sg::R_CACHED)
+          SG_HIP(hipMemcpy(&rec, ob->ring + h * ob->cap + ((head[h] - 1) & (ob->cap - 1)), 16, hipMemcpyDeviceToHost));
+        if (rl->cached_packet) rl->cached_packet[h] = rec.x;
+        if (rl->cached_len) rl->cached_len[h] = rec.y;
+      }
+    }
   });
 }
 

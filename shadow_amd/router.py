@@ -2,7 +2,9 @@
 Router::inbound_packets (src/main/network/router/mod.rs:15-58) and
 CoDelQueue (src/main/network/router/codel_queue.rs); and the inbound pipeline
 (`InboundPipeline`): router queue -> relay_inet_in token bucket
-(src/main/network/relay/mod.rs, relay/token_bucket.rs).
+(src/main/network/relay/mod.rs, relay/token_bucket.rs); and the outbound
+pipeline (`OutboundPipeline`): interface fifo -> relay_inet_out token bucket ->
+router -> Worker::send_packet, whose output is a delivery round's PacketBatch.
 
 One queue per host lives on the device across calls.  `CoDelQueues.run`
 applies a batch of push / pop events -- grouped by ascending host, each host's
@@ -170,6 +172,85 @@ class InboundPipeline:
         try:
             if getattr(self, "handle", None):
                 load().sg_inbound_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+class OutboundPipeline:
+    """Every host's network interface (fifo qdisc) + outbound relay (sg_outbound_*):
+    sends enter the interface in creation order; the relay forwards them as the
+    host's token bucket (bw up) allows, packets to the host's own address back to
+    the interface, the rest to the router, i.e. to Worker::send_packet.  The
+    packets sent form the next delivery round's PacketBatch (`run` returns it)."""
+
+    def __init__(self, host_ipv4, bw_up_bits, ring_cap: int = 4096, ctx: Optional[Context] = None):
+        self.ctx = ctx or default_context()
+        ip = np.ascontiguousarray(host_ipv4, dtype=np.uint32)
+        bw = np.ascontiguousarray(bw_up_bits, dtype=np.uint64)
+        assert len(ip) == len(bw)
+        self.n = len(bw)
+        h = C.c_void_p()
+        check(self.ctx.handle, load().sg_outbound_create(self.ctx.handle, self.n, ip.ctypes.data, bw.ctypes.data,
+                                                         int(ring_cap), C.byref(h)))
+        self.handle = h
+        self.cap = int(load().sg_outbound_ring_cap(h))
+        self._sent = None
+
+    def sent_buffers(self, cap: int, device):
+        """Device buffers for the sent batch (grown, then reused across windows)."""
+        import torch
+        if self._sent is None or self._sent["src_host"].numel() < cap:
+            i32 = dict(dtype=torch.int32, device=device)
+            self._sent = dict(src_host=torch.empty(cap, **i32), dst_ipv4=torch.empty(cap, **i32),
+                              payload_len=torch.empty(cap, **i32),
+                              send_time_ns=torch.empty(cap, dtype=torch.int64, device=device),
+                              packet=torch.empty(cap, **i32))
+        return self._sent
+
+    def run(self, host, time_ns, packet, length, payload_len, dst_ipv4, window_end_ns: int, bootstrap_end_ns: int,
+            sim_end_ns: int, fwd_time, pkt_status, event_ctr_ptr: Optional[int] = None, sent_cap: Optional[int] = None):
+        """Sends as device tensors (int32 host/packet/length/payload_len/dst_ipv4, int64 time); fwd_time
+        (int64) and pkt_status (uint8) are indexed by packet id.  Returns (PacketBatch of the packets
+        sent, in send_packet order, and their packet ids), views of buffers reused by the next call."""
+        from .worker import PacketBatch
+        n = int(host.numel())
+        s = _capi.sg_outbound_sends(n, host.data_ptr(), time_ns.data_ptr(), packet.data_ptr(), length.data_ptr(),
+                                    payload_len.data_ptr(), dst_ipv4.data_ptr())
+        cap = int(sent_cap if sent_cap is not None else n + self.n * 4)
+        b = self.sent_buffers(max(cap, 1), fwd_time.device)
+        o = _capi.sg_outbound_sent(cap, *(b[k].data_ptr() for k in ("src_host", "dst_ipv4", "payload_len",
+                                                                     "send_time_ns", "packet")))
+        ns = C.c_uint32()
+        check(self.ctx.handle, load().sg_outbound_run(self.ctx.handle, self.handle, C.byref(s), int(window_end_ns),
+                                                      int(bootstrap_end_ns), int(sim_end_ns),
+                                                      C.c_void_p(event_ctr_ptr or 0), fwd_time.data_ptr(),
+                                                      pkt_status.data_ptr(), int(pkt_status.numel()), C.byref(o),
+                                                      C.byref(ns)))
+        k = ns.value
+        batch = PacketBatch(b["src_host"][:k], b["dst_ipv4"][:k], b["payload_len"][:k], b["send_time_ns"][:k])
+        return batch, b["packet"][:k]
+
+    def get_state(self) -> dict:
+        """Queue + relay state in the oracle's outbound_state layout (cached packet = slot head - 1)."""
+        n, c = self.n, self.cap
+        st = dict(cap=c, head=np.zeros(n, np.uint32), tail=np.zeros(n, np.uint32),
+                  ring_pkt=np.zeros(n * c, np.uint32), ring_len=np.zeros(n * c, np.uint32),
+                  ring_pay=np.zeros(n * c, np.uint32), ring_dst=np.zeros(n * c, np.uint32),
+                  rflags=np.zeros(n, np.uint8), task_time=np.zeros(n, np.uint64), tb_cap=np.zeros(n, np.uint64),
+                  tb_bal=np.zeros(n, np.uint64), tb_inc=np.zeros(n, np.uint64), tb_last=np.zeros(n, np.uint64))
+        v = lambda k: st[k].ctypes.data_as(C.c_void_p)
+        q = _capi.sg_outbound_queue_state(v("head"), v("tail"), v("ring_pkt"), v("ring_len"), v("ring_pay"),
+                                          v("ring_dst"))
+        rs = _capi.sg_inbound_relay_state(v("rflags"), v("task_time"), None, None, v("tb_cap"), v("tb_bal"),
+                                          v("tb_inc"), v("tb_last"))
+        check(self.ctx.handle, load().sg_outbound_get_state(self.handle, C.byref(q), C.byref(rs)))
+        return st
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                load().sg_outbound_destroy(self.handle)
                 self.handle = None
         except Exception:
             pass

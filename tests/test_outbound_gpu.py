@@ -1,0 +1,149 @@
+"""GPU parity of the outbound pipeline (sg_outbound_*: interface fifo ->
+relay_inet_out token bucket -> router -> send_packet) against the oracle,
+bit-exact: statuses, forward times, event-counter advances, the per-host queue
++ relay state, and the sent batch (send_packet order) -- over consecutive
+windows (queued packets and pending tasks carry over); then the sent batch
+runs through sg_deliver_round like any round's packets."""
+import numpy as np
+import pytest
+
+from shadow_amd import ShadowGpuError, _capi, synth
+from shadow_amd.router import OutboundPipeline
+from shadow_amd.worker import DeviceTable, HostTable, deliver_round
+
+pytestmark = pytest.mark.gpu
+T0 = 946684800 * 10**9
+MS = 10**6
+RKEYS = ("head", "tail", "rflags", "task_time", "tb_cap", "tb_bal", "tb_inc", "tb_last")
+
+
+def _dev(a, np_dtype, torch_dtype):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np_dtype).view(torch_dtype)).cuda()
+
+
+def _sends(hosts, n, t0, t1, seed, p_local=0.05):
+    pk = synth.make_packets(n, hosts, t0, t1, seed=seed)
+    rng = np.random.default_rng(seed + 1000)
+    loc = rng.random(n) < p_local
+    dst = np.where(loc, hosts["ip"][pk["src"]], pk["dst_ip"]).astype(np.uint32)
+    ln = (pk["payload"] + 40).astype(np.uint32)  # IPv4 + TCP headers
+    return pk["src"], pk["send_time"], ln, pk["payload"], dst
+
+
+def _live_same(got, want):
+    """Ring slots still needed: [head - cached, tail) per host."""
+    c = want["cap"]
+    lo = want["head"].astype(np.int64) - ((want["rflags"] & 4) != 0)
+    n = want["tail"].astype(np.int64) - lo
+    hh = np.repeat(np.arange(len(n)), n)
+    s = lo[hh] + np.arange(int(n.sum())) - np.repeat(np.cumsum(n) - n, n)
+    i = hh * c + (s % c)
+    for k in ("ring_pkt", "ring_len", "ring_pay", "ring_dst"):
+        assert np.array_equal(got[k][i], want[k][i]), k
+
+
+@pytest.mark.parametrize("bw_mbit,boot_ms", [(1000, 0), (10, 0), (2, 0), (10, 3)])
+def test_windows_match_oracle(oracle, ctx, bw_mbit, boot_ms):
+    """2000 hosts, 5 windows of 2 ms, 40k sends each: unthrottled to heavily throttled
+    (queues and cached packets carried across windows, tasks pending)."""
+    import torch
+
+    H, W, per = 2000, 2 * MS, 40000
+    hosts = synth.make_hosts(H, 64, exact_seeds=False)
+    rng = np.random.default_rng(bw_mbit + boot_ms)
+    bw = rng.integers(bw_mbit * 10**6 // 2, bw_mbit * 10**6 + 1, H).astype(np.uint64)
+    ob = OutboundPipeline(hosts["ip"], bw, 1024, ctx=ctx)
+    ost = oracle.outbound_state(hosts["ip"], bw, ob.cap)
+    n_pk = 5 * per
+    fwd_g = torch.full((n_pk,), -1, dtype=torch.int64, device="cuda")
+    st_g = torch.zeros(n_pk, dtype=torch.uint8, device="cuda")
+    ctr_g = torch.zeros(H, dtype=torch.int64, device="cuda")
+    fwd_o, st_o, ctr_o = np.full(n_pk, np.uint64(2**64 - 1)), np.zeros(n_pk, np.uint8), np.zeros(H, np.uint64)
+    boot, sim_end = T0 + boot_ms * MS, T0 + 10**12
+    total = 0
+    for w in range(5):
+        t0, t1 = T0 + w * W, T0 + (w + 1) * W
+        host, t, ln, pay, dst = _sends(hosts, per, t0, t1, seed=100 * bw_mbit + w)
+        pkt = np.arange(w * per, (w + 1) * per, dtype=np.uint32)
+        batch, ids = ob.run(_dev(host, np.uint32, np.int32), _dev(t, np.uint64, np.int64),
+                            _dev(pkt, np.uint32, np.int32), _dev(ln, np.uint32, np.int32),
+                            _dev(pay, np.uint32, np.int32), _dev(dst, np.uint32, np.int32), t1, boot, sim_end,
+                            fwd_g, st_g, ctr_g.data_ptr())
+        want = oracle.outbound_run(ost, host, t, pkt, ln, pay, dst, t1, boot, sim_end, ctr_o, fwd_o, st_o)
+        assert np.array_equal(st_g.cpu().numpy(), st_o)
+        m = st_o != 0
+        assert np.array_equal(fwd_g.cpu().numpy().view(np.uint64)[m], fwd_o[m])
+        assert np.array_equal(ctr_g.cpu().numpy().view(np.uint64), ctr_o)
+        assert len(batch) == len(want["packet"])
+        assert np.array_equal(batch.src_host.cpu().numpy().view(np.uint32), want["src_host"])
+        assert np.array_equal(batch.dst_ipv4.cpu().numpy().view(np.uint32), want["dst_ipv4"])
+        assert np.array_equal(batch.payload_len.cpu().numpy().view(np.uint32), want["payload_len"])
+        assert np.array_equal(batch.send_time_ns.cpu().numpy().view(np.uint64), want["send_time"])
+        assert np.array_equal(ids.cpu().numpy().view(np.uint32), want["packet"])
+        got = ob.get_state()
+        for k in RKEYS:
+            assert np.array_equal(got[k], ost[k]), k
+        _live_same(got, ost)
+        total += len(want["packet"])
+    assert (st_o == 2).any()
+    if bw_mbit == 2:
+        assert (st_o == 0).any() and (ost["rflags"] & oracle.RL_PENDING).any() and total < n_pk
+
+
+def test_sent_batch_feeds_delivery(oracle, ctx):
+    """Outbound window -> sg_deliver_round on the sent batch, against the oracle chain."""
+    import torch
+
+    from test_deliver_gpu import _world
+
+    lat, loss, hosts = _world(n_hosts=1500, seed=4)
+    H = hosts["n"]
+    bw = np.full(H, 20 * 10**6, np.uint64)
+    start, end = T0 + 10**9, T0 + 10**9 + MS
+    host, t, ln, pay, dst = _sends(hosts, 30000, start, end, seed=7)
+    pkt = np.arange(len(host), dtype=np.uint32)
+    ob = OutboundPipeline(hosts["ip"], bw, 256, ctx=ctx)
+    ost = oracle.outbound_state(hosts["ip"], bw, ob.cap)
+    fwd_g = torch.zeros(len(pkt), dtype=torch.int64, device="cuda")
+    st_g = torch.zeros(len(pkt), dtype=torch.uint8, device="cuda")
+    ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    rng0, ctr0 = ht.get_state()
+    ctr_o = ctr0.copy()
+    batch, ids = ob.run(_dev(host, np.uint32, np.int32), _dev(t, np.uint64, np.int64), _dev(pkt, np.uint32, np.int32),
+                        _dev(ln, np.uint32, np.int32), _dev(pay, np.uint32, np.int32), _dev(dst, np.uint32, np.int32),
+                        end, 0, end + 10**9, fwd_g, st_g, _capi.load().sg_hosts_event_ctr(ht.handle))
+    sent = oracle.outbound_run(ost, host, t, pkt, ln, pay, dst, end, 0, end + 10**9, ctr_o,
+                               np.zeros(len(pkt), np.uint64), np.zeros(len(pkt), np.uint8))
+    lat_t = torch.from_numpy(np.ascontiguousarray(lat).view(np.int64).ravel()).cuda()
+    table = DeviceTable(lat_t, torch.from_numpy(np.ascontiguousarray(loss).ravel()).cuda(), lat.shape[1])
+    assert table.pack()
+    out = deliver_round(ht, table, batch, end, end + 10**9, 0)
+    got = out.to_numpy(len(batch))
+    want = oracle.deliver_round(end, end + 10**9, 0, sent["src_host"], sent["dst_ipv4"], sent["payload_len"],
+                                sent["send_time"], hosts["ip"], hosts["route"], lat, loss, rng0, ctr_o)
+    for k in ("status", "deliver_time", "event_id", "dst_offsets", "dst_order"):
+        assert np.array_equal(got[k], want[k]), k
+    grng, gctr = ht.get_state()
+    assert np.array_equal(grng, rng0) and np.array_equal(gctr, ctr_o)
+    assert want["delivered"] > 0 and len(batch) < len(pkt)
+
+
+def test_sent_capacity_and_order_errors(ctx):
+    import torch
+
+    ob = OutboundPipeline(np.array([10, 11], np.uint32), np.array([10**9, 10**9], np.uint64), 16, ctx=ctx)
+    f = torch.zeros(8, dtype=torch.int64, device="cuda")
+    s = torch.zeros(8, dtype=torch.uint8, device="cuda")
+    args = [_dev([0, 0, 1], np.uint32, np.int32), _dev([T0 + 1, T0 + 2, T0 + 1], np.uint64, np.int64),
+            _dev([0, 1, 2], np.uint32, np.int32), _dev([100] * 3, np.uint32, np.int32),
+            _dev([60] * 3, np.uint32, np.int32), _dev([11, 11, 10], np.uint32, np.int32)]
+    with pytest.raises(ShadowGpuError) as e:
+        ob.run(*args, T0 + MS, 0, T0 + 10**12, f, s, sent_cap=2)
+    assert e.value.code == _capi.SG_ERR_CAPACITY
+    ob = OutboundPipeline(np.array([10, 11], np.uint32), np.array([10**9, 10**9], np.uint64), 16, ctx=ctx)
+    args[1] = _dev([T0 + 2, T0 + 1, T0 + 1], np.uint64, np.int64)
+    with pytest.raises(ShadowGpuError) as e:
+        ob.run(*args, T0 + MS, 0, T0 + 10**12, f, s)
+    assert e.value.code == _capi.SG_ERR_UNSORTED

@@ -26,6 +26,8 @@ KERNELS = {"relax_wide": "k_relax_wide", "relax": "k_relax_w2<", "relax1": "k_re
            "sb_sort": "k_sb_sort", "sort_big": "k_sort_big", "host_off": "k_host_off", "reduce_stats": "k_reduce_stats",
            "table_pack": "k_table_pack", "codel_reduce": "k_codel_reduce", "codel": "k_codel",
            "inbound": "k_inbound",
+           "outbound": "k_outbound",
+           "out_compact": "k_out_compact",
            "init": "k_init_batch"}
 VALU_PEAK_OPS_PER_NS = 256 * 4 * 32 * 2.4  # 78.6e3 lane-ops per ns (MI355X_MICROARCH.md chip table)
 
