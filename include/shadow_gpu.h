@@ -104,6 +104,11 @@ typedef struct sg_graph {
 /* Parse GML text.  On failure returns SG_ERR_PARSE and writes a message into
  * err (if err_len > 0).  Latency unit overflow is reported here. */
 int32_t sg_gml_parse(const char* text, size_t len, sg_gml** out, char* err, size_t err_len);
+/* The same parse on `threads` host threads (0: min(cores, 16), or SG_GML_THREADS).
+ * Results and the error reported are those of the single-threaded parse
+ * (load_network_graph feeds it, graph/mod.rs:498-513). */
+int32_t sg_gml_parse_threads(const char* text, size_t len, uint32_t threads, sg_gml** out, char* err,
+                             size_t err_len);
 /* Borrow the parsed edge list (valid until sg_gml_destroy). */
 int32_t sg_gml_graph(const sg_gml* g, sg_graph* out);
 /* NetworkGraph::node_id_to_index (graph/mod.rs:126-128); SG_ERR_INVALID_ARG if absent. */

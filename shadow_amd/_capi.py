@@ -34,7 +34,7 @@ SG_PKT_DELIVERED, SG_PKT_DROP_LOSS, SG_PKT_DROP_NO_DST, SG_PKT_SIM_END = range(4
 EXPORTED = [
     "sg_abi_version", "sg_ctx_create", "sg_ctx_destroy", "sg_ctx_set_stream", "sg_ctx_stream",
     "sg_ctx_synchronize", "sg_ctx_last_error", "sg_ctx_last_error_pair", "sg_ctx_enable_timers",
-    "sg_ctx_read_timer", "sg_gml_parse", "sg_gml_graph",
+    "sg_ctx_read_timer", "sg_gml_parse", "sg_gml_parse_threads", "sg_gml_graph",
     "sg_gml_node_index", "sg_gml_destroy", "sg_net_create", "sg_net_destroy", "sg_routing_build",
     "sg_routing_min_latency", "sg_hosts_create", "sg_hosts_get_state", "sg_hosts_set_state",
     "sg_hosts_destroy", "sg_deliver_round", "sg_deliver_source", "sg_deliver_bucket",
@@ -162,6 +162,7 @@ def load(path: str | None = None):
         "sg_ctx_enable_timers": (i32, [vp, i32]),
         "sg_ctx_read_timer": (i32, [vp, C.c_char_p, C.POINTER(C.c_double), u64p, C.POINTER(C.c_double)]),
         "sg_gml_parse": (i32, [C.c_char_p, C.c_size_t, C.POINTER(vp), C.c_char_p, C.c_size_t]),
+        "sg_gml_parse_threads": (i32, [C.c_char_p, C.c_size_t, u32, C.POINTER(vp), C.c_char_p, C.c_size_t]),
         "sg_gml_graph": (i32, [vp, C.POINTER(sg_graph)]),
         "sg_gml_node_index": (i32, [vp, u32, u32p]),
         "sg_gml_destroy": (None, [vp]),

@@ -1,4 +1,4 @@
-// sg_gml.cpp -- GML ingest for the network graph (host C++).
+// sg_gml.cpp -- GML ingest for the network graph (host C++, multi-threaded).
 //
 // Mirrors the grammar of src/lib/gml-parser/src/parser.rs (nom) and the edge
 // conversion of ShadowEdge::try_from (src/main/network/graph/mod.rs:72-111),
@@ -8,17 +8,31 @@
 //   * a value is tried as Int (digits only, i32) before Float
 //     (parser.rs:212-230), so `packet_loss 0` is an Int and is rejected as
 //     "not a float" (graph/mod.rs:95-98);
-//   * floats are correctly rounded to f32 (Rust str::parse::<f32> == strtof);
+//   * floats are correctly rounded to f32 (Rust str::parse::<f32>, here
+//     std::from_chars);
 //   * a repeated node id silently re-maps the id to the later node
 //     (graph/mod.rs:157-162).
 // Difference: a latency whose ns value overflows u64 is reported here as a
 // parse error; the reference panics later in PathProperties::from
 // (graph/mod.rs:336 `.unwrap()`).
-#include <cerrno>
-#include <cmath>
+//
+// Speed: no allocation per item -- keys and strings are
+// spans into the text, a block's pairs live in a reused array -- and the
+// body is split over threads.  Each thread starts at a guessed item boundary
+// (a line whose key is `node` / `edge` followed by `[`) and parses whole items
+// up to the next thread's start.  The boundaries are then verified in
+// document order: a chunk that started at a true boundary and ended exactly on
+// the next chunk's start proves that start true; a chunk that overshot (the
+// next guess was inside a string) is continued on the calling thread until it
+// lands on a later guess.  The result, including which error is reported
+// first, is the single-threaded parse's.
+#include <algorithm>
+#include <charconv>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <system_error>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -30,7 +44,20 @@ struct sg_gml {
   std::vector<uint32_t> esrc, edst;
   std::vector<uint64_t> elat;
   std::vector<float> eloss;
-  std::unordered_map<uint32_t, uint32_t> id_to_index;
+  // id -> index: a dense table when the ids are small, else a hash map
+  std::vector<uint32_t> dense;
+  std::unordered_map<uint32_t, uint32_t> sparse;
+  bool lookup(uint32_t id, uint32_t& idx) const {
+    if (!dense.empty()) {
+      if (id >= dense.size() || dense[id] == UINT32_MAX) return false;
+      idx = dense[id];
+      return true;
+    }
+    auto it = sparse.find(id);
+    if (it == sparse.end()) return false;
+    idx = it->second;
+    return true;
+  }
 };
 
 namespace {
@@ -39,31 +66,129 @@ struct ParseError {
   std::string msg;
 };
 
-enum class VT { Int, Float, Str };
+struct Span {
+  const char* p = nullptr;
+  uint32_t n = 0;
+  bool eq(const char* s, uint32_t len) const { return n == len && memcmp(p, s, len) == 0; }
+};
+
+enum VT : uint8_t { V_INT, V_FLOAT, V_STR };
 struct Value {
-  VT t;
+  VT t = V_INT;
+  bool esc = false;  // the string holds \\ or \" escapes (s is the raw text between the quotes)
   int32_t i = 0;
   float f = 0;
-  std::string s;
+  Span s;
+};
+
+std::string unescape(const Span& s, bool esc) {
+  if (!esc) return std::string(s.p, s.n);
+  std::string out;
+  out.reserve(s.n);
+  for (uint32_t k = 0; k < s.n; k++) {
+    if (s.p[k] == '\\' && k + 1 < s.n && (s.p[k + 1] == '\\' || s.p[k + 1] == '"')) k++;
+    out.push_back(s.p[k]);
+  }
+  return out;
+}
+
+inline bool is_space(char c) { return c == ' ' || c == '\t'; }
+inline bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n'; }
+inline bool is_digit(char c) { return c >= '0' && c <= '9'; }
+inline bool is_alpha(char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
+
+// str::parse::<f32> of a recognize_float match [b, e): correctly rounded.
+// Fast path (the usual "0.0123"): up to 19 significant digits and a decimal
+// exponent within +-22 give the correctly rounded double m * 10^e exactly
+// (both operands are exact doubles); its f32 rounding is the decimal's unless
+// the double sits exactly on an f32 rounding midpoint, which goes to the slow
+// path.  The slow path is std::from_chars (correctly rounded too), which in
+// this libstdc++ serialises threads on the locale, hence the fast path.
+bool parse_f32_slow(const char* b, const char* e, float& out) {
+  std::string t;
+  if (b < e && *b == '+') b++;  // from_chars takes no '+'
+  const int neg = (b < e && *b == '-') ? 1 : 0;
+  if (b + neg < e && b[neg] == '.') {  // ".5" / "-.5": from_chars wants a digit first
+    t.assign(neg ? "-0" : "0");
+    t.append(b + neg, e);
+    b = t.data();
+    e = t.data() + t.size();
+  }
+  auto r = std::from_chars(b, e, out, std::chars_format::general);
+  if (r.ptr != e) return false;
+  if (r.ec == std::errc::result_out_of_range) out = strtof(std::string(b, e).c_str(), nullptr);  // +-inf / 0
+  return true;
+}
+
+bool parse_f32(const char* b, const char* e, float& out) {
+  static const double p10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                 1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  const char* q = b;
+  bool neg = false;
+  if (q < e && (*q == '+' || *q == '-')) neg = *q++ == '-';
+  uint64_t m = 0;
+  int nd = 0, e10 = 0;
+  bool seen_dot = false;
+  for (; q < e && (is_digit(*q) || *q == '.'); q++) {
+    if (*q == '.') {
+      seen_dot = true;
+      continue;
+    }
+    if (m == 0 && *q == '0') {  // leading zeros are not significant
+      if (seen_dot) e10--;
+      continue;
+    }
+    if (nd == 19) return parse_f32_slow(b, e, out);
+    m = m * 10 + (uint64_t)(*q - '0');
+    nd++;
+    if (seen_dot) e10--;
+  }
+  if (q < e) {  // [eE][+-]?digits (recognize_float guarantees the shape)
+    q++;
+    bool eneg = false;
+    if (q < e && (*q == '+' || *q == '-')) eneg = *q++ == '-';
+    int x = 0;
+    for (; q < e; q++) {
+      if (x > 100000) return parse_f32_slow(b, e, out);
+      x = x * 10 + (*q - '0');
+    }
+    e10 += eneg ? -x : x;
+  }
+  if (m == 0) {
+    out = neg ? -0.0f : 0.0f;
+    return true;
+  }
+  if (m > (1ull << 53) || e10 < -22 || e10 > 22) return parse_f32_slow(b, e, out);
+  double d = (double)m;
+  d = e10 < 0 ? d / p10[-e10] : d * p10[e10];
+  uint64_t u;
+  memcpy(&u, &d, 8);
+  const int bexp = (int)((u >> 52) & 0x7ff) - 1023;
+  if (bexp < -125 || bexp > 126) return parse_f32_slow(b, e, out);  // f32 subnormal / overflow range
+  if ((u & 0x1fffffffull) == 0x10000000ull) return parse_f32_slow(b, e, out);  // an f32 midpoint
+  out = (float)(neg ? -d : d);
+  return true;
+}
+
+struct KV {
+  Span k;
+  Value v;
 };
 
 struct Parser {
   const char* p;
   const char* end;
+  const char* start;  // the whole text, for byte offsets in messages
 
   bool at_end() const { return p >= end; }
-  static bool is_space(char c) { return c == ' ' || c == '\t'; }
-  static bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n'; }
-  [[noreturn]] void fail(const std::string& m) {
-    throw ParseError{m + " at byte " + std::to_string((size_t)(p - start))};
+  [[noreturn]] void fail(const char* m) {
+    throw ParseError{std::string(m) + " at byte " + std::to_string((size_t)(p - start))};
   }
-  const char* start;
-
   void space0() {
-    while (!at_end() && is_space(*p)) p++;
+    while (p < end && is_space(*p)) p++;
   }
   void multispace0() {
-    while (!at_end() && is_ws(*p)) p++;
+    while (p < end && is_ws(*p)) p++;
   }
   // newline = space0 multispace1 space0 (parser.rs:243-245)
   bool newline() {
@@ -75,62 +200,57 @@ struct Parser {
       p = s;
       return false;
     }
-    space0();
     return true;
   }
-  bool tag(const char* t) {
-    size_t n = strlen(t);
-    if ((size_t)(end - p) >= n && memcmp(p, t, n) == 0) {
-      p += n;
+  bool tag(char c) {
+    if (p < end && *p == c) {
+      p++;
       return true;
     }
     return false;
   }
   // key: [A-Za-z_][A-Za-z0-9_]* (parser.rs:42-49)
-  bool key(std::string& out) {
-    if (at_end() || !(isalpha((unsigned char)*p) || *p == '_')) return false;
+  bool key(Span& out) {
+    if (at_end() || !(is_alpha(*p) || *p == '_')) return false;
     const char* s = p++;
-    while (!at_end() && (isalnum((unsigned char)*p) || *p == '_')) p++;
-    out.assign(s, p);
+    while (p < end && (is_alpha(*p) || is_digit(*p) || *p == '_')) p++;
+    out.p = s;
+    out.n = (uint32_t)(p - s);
     return true;
   }
   // value (parser.rs:212-219): space0 then int|float|string, each followed by newline
   Value value() {
     space0();
-    const char* s = p;
-    // int: digit1 parsed as i32
-    {
+    Value r;
+    {  // int: digit1 parsed as i32
       const char* q = p;
-      while (q < end && isdigit((unsigned char)*q)) q++;
+      while (q < end && is_digit(*q)) q++;
       if (q > p) {
-        std::string digits(p, q);
-        errno = 0;
-        char* e = nullptr;
-        long long v = strtoll(digits.c_str(), &e, 10);
-        bool ok = errno == 0 && v <= INT32_MAX;
+        int64_t v = 0;
+        bool ok = q - p <= 10;
+        for (const char* d = p; ok && d < q; d++) v = v * 10 + (*d - '0');
+        ok = ok && v <= INT32_MAX;
         const char* save = p;
         p = q;
         if (ok && newline()) {
-          Value r;
-          r.t = VT::Int;
+          r.t = V_INT;
           r.i = (int32_t)v;
           return r;
         }
         p = save;
       }
     }
-    // float: nom recognize_float: [+-]? (digits (. digits?)? | . digits) ([eE][+-]?digits)?
-    {
+    {  // float: nom recognize_float: [+-]? (digits (. digits?)? | . digits) ([eE][+-]?digits)?
       const char* q = p;
       if (q < end && (*q == '+' || *q == '-')) q++;
       const char* d0 = q;
-      while (q < end && isdigit((unsigned char)*q)) q++;
-      bool int_part = q > d0;
+      while (q < end && is_digit(*q)) q++;
+      const bool int_part = q > d0;
       bool frac = false;
       if (q < end && *q == '.') {
         const char* f0 = q + 1;
         const char* f = f0;
-        while (f < end && isdigit((unsigned char)*f)) f++;
+        while (f < end && is_digit(*f)) f++;
         if (int_part || f > f0) {
           frac = f > f0;
           q = f;
@@ -141,216 +261,410 @@ struct Parser {
           const char* x = q + 1;
           if (x < end && (*x == '+' || *x == '-')) x++;
           const char* x0 = x;
-          while (x < end && isdigit((unsigned char)*x)) x++;
+          while (x < end && is_digit(*x)) x++;
           if (x > x0) q = x;
         }
-        std::string txt(p, q);
         const char* save = p;
+        float f = 0;
+        const bool ok = parse_f32(p, q, f);
         p = q;
-        if (newline()) {
-          Value r;
-          r.t = VT::Float;
-          r.f = strtof(txt.c_str(), nullptr);  // correctly rounded, as str::parse::<f32>
+        if (ok && newline()) {
+          r.t = V_FLOAT;
+          r.f = f;
           return r;
         }
         p = save;
       }
     }
-    // string: "..." with \\ and \" escapes (parser.rs:233-242)
-    if (!at_end() && *p == '"') {
-      p++;
-      std::string out;
-      while (!at_end() && *p != '"') {
+    if (!at_end() && *p == '"') {  // string: "..." with \\ and \" escapes (parser.rs:233-242)
+      const char* s = ++p;
+      bool esc = false;
+      while (p < end && *p != '"') {
         if (*p == '\\' && p + 1 < end && (p[1] == '\\' || p[1] == '"')) {
-          out.push_back(p[1]);
+          esc = true;
           p += 2;
         } else {
-          out.push_back(*p++);
+          p++;
         }
       }
       if (at_end()) fail("unterminated string");
+      r.s.p = s;
+      r.s.n = (uint32_t)(p - s);
       p++;
       if (!newline()) fail("expected newline after string");
-      Value r;
-      r.t = VT::Str;
-      r.s = std::move(out);
+      r.t = V_STR;
+      r.esc = esc;
       return r;
     }
-    p = s;
     fail("expected a value");
   }
   // node/edge body: space0 "[" newline many_till((key, value), "]") newline
-  std::unordered_map<std::string, Value> block() {
+  void block(std::vector<KV>& kv) {
     space0();
-    if (!tag("[")) fail("expected '['");
+    if (!tag('[')) fail("expected '['");
     if (!newline()) fail("expected newline after '['");
-    std::unordered_map<std::string, Value> kv;
-    size_t count = 0;
+    kv.clear();
     for (;;) {
-      if (tag("]")) break;
-      std::string k;
-      if (!key(k)) fail("expected key or ']'");
-      Value v = value();
-      count++;
-      kv[k] = std::move(v);
+      if (tag(']')) break;
+      KV e;
+      if (!key(e.k)) fail("expected key or ']'");
+      e.v = value();
+      kv.push_back(e);
     }
-    if (kv.size() != count) fail("Duplicate keys are not supported");
+    for (size_t a = 1; a < kv.size(); a++)
+      for (size_t b = 0; b < a; b++)
+        if (kv[a].k.n == kv[b].k.n && memcmp(kv[a].k.p, kv[b].k.p, kv[a].k.n) == 0)
+          fail("Duplicate keys are not supported");
     if (!newline()) fail("expected newline after ']'");
-    return kv;
   }
 };
 
-// Time::<TimePrefix>::from_str (units.rs:411-438): returns (value, ns factor).
-struct TimeVal {
-  uint64_t value;
-  uint64_t factor;
-};
-
-TimeVal parse_time(const std::string& s_in, const char* what) {
-  // regex ^([+-]?[0-9\.]*)\s*(.*)$ ; both groups trimmed
-  size_t i = 0;
-  if (i < s_in.size() && (s_in[i] == '+' || s_in[i] == '-')) i++;
-  while (i < s_in.size() && (isdigit((unsigned char)s_in[i]) || s_in[i] == '.')) i++;
-  auto trim = [](std::string x) {
-    size_t a = 0, b = x.size();
-    while (a < b && isspace((unsigned char)x[a])) a++;
-    while (b > a && isspace((unsigned char)x[b - 1])) b--;
-    return x.substr(a, b - a);
-  };
-  std::string num = trim(s_in.substr(0, i)), unit = trim(s_in.substr(i));
-  const std::string pre = std::string("Edge '") + what + "' is not a valid unit: ";
-  // TimePrefix::from_str (units.rs:233-251); "" -> default Sec (:227-231)
-  uint64_t factor;
-  if (unit.empty())
-    factor = 1000000000ull;
-  else if (unit == "ns" || unit == "nanosecond" || unit == "nanoseconds")
-    factor = 1;
-  else if (unit == "us" || unit == "\xce\xbcs" || unit == "microsecond" || unit == "microseconds")
-    factor = 1000;
-  else if (unit == "ms" || unit == "millisecond" || unit == "milliseconds")
-    factor = 1000000;
-  else if (unit == "s" || unit == "sec" || unit == "secs" || unit == "second" || unit == "seconds")
-    factor = 1000000000ull;
-  else if (unit == "m" || unit == "min" || unit == "mins" || unit == "minute" || unit == "minutes")
-    factor = 60000000000ull;
-  else if (unit == "h" || unit == "hr" || unit == "hrs" || unit == "hour" || unit == "hours")
-    factor = 3600000000000ull;
-  else
-    throw ParseError{pre + "Unit was not one of (ns|nanosecond|nanoseconds|us|\xce\xbcs|microsecond|"
-                           "microseconds|ms|millisecond|milliseconds|s|sec|secs|second|seconds|m|min|"
-                           "mins|minute|minutes|h|hr|hrs|hour|hours)"};
-  // u64::from_str: optional '+', decimal digits only, no overflow
-  std::string digits = num;
-  if (!digits.empty() && digits[0] == '+') digits = digits.substr(1);
-  if (digits.empty()) throw ParseError{pre + "cannot parse integer from empty string"};
-  for (char c : digits)
-    if (!isdigit((unsigned char)c)) throw ParseError{pre + "invalid digit found in string"};
-  unsigned __int128 v = 0;
-  for (char c : digits) {
-    v = v * 10 + (unsigned)(c - '0');
-    if (v > UINT64_MAX) throw ParseError{pre + "number too large to fit in target type"};
-  }
-  return TimeVal{(uint64_t)v, factor};
+const KV* find(const std::vector<KV>& kv, const char* k) {
+  const uint32_t n = (uint32_t)strlen(k);
+  for (const KV& e : kv)
+    if (e.k.eq(k, n)) return &e;
+  return nullptr;
 }
 
-void parse_into(const char* text, size_t len, sg_gml* g) {
+// Time::<TimePrefix>::from_str (units.rs:411-438): the value and its ns
+// factor, or a message in err.
+bool parse_time(const char* s, size_t len, const char* what, uint64_t& value, uint64_t& factor, std::string& err) {
+  // regex ^([+-]?[0-9\.]*)\s*(.*)$ ; both groups trimmed
+  size_t i = 0;
+  if (i < len && (s[i] == '+' || s[i] == '-')) i++;
+  while (i < len && (is_digit(s[i]) || s[i] == '.')) i++;
+  auto trim = [](const char*& a, const char*& b) {
+    while (a < b && isspace((unsigned char)*a)) a++;
+    while (b > a && isspace((unsigned char)b[-1])) b--;
+  };
+  const char *n0 = s, *n1 = s + i, *u0 = s + i, *u1 = s + len;
+  trim(n0, n1);
+  trim(u0, u1);
+  const size_t ul = (size_t)(u1 - u0);
+  auto is = [&](const char* w) { return ul == strlen(w) && memcmp(u0, w, ul) == 0; };
+  auto fail = [&](const char* m) {
+    err = std::string("Edge '") + what + "' is not a valid unit: " + m;
+    return false;
+  };
+  // TimePrefix::from_str (units.rs:233-251); "" -> default Sec (:227-231)
+  if (ul == 0)
+    factor = 1000000000ull;
+  else if (is("ns") || is("nanosecond") || is("nanoseconds"))
+    factor = 1;
+  else if (is("us") || is("\xce\xbcs") || is("microsecond") || is("microseconds"))
+    factor = 1000;
+  else if (is("ms") || is("millisecond") || is("milliseconds"))
+    factor = 1000000;
+  else if (is("s") || is("sec") || is("secs") || is("second") || is("seconds"))
+    factor = 1000000000ull;
+  else if (is("m") || is("min") || is("mins") || is("minute") || is("minutes"))
+    factor = 60000000000ull;
+  else if (is("h") || is("hr") || is("hrs") || is("hour") || is("hours"))
+    factor = 3600000000000ull;
+  else
+    return fail("Unit was not one of (ns|nanosecond|nanoseconds|us|\xce\xbcs|microsecond|"
+                "microseconds|ms|millisecond|milliseconds|s|sec|secs|second|seconds|m|min|"
+                "mins|minute|minutes|h|hr|hrs|hour|hours)");
+  // u64::from_str: optional '+', decimal digits only, no overflow
+  if (n0 < n1 && *n0 == '+') n0++;
+  if (n0 == n1) return fail("cannot parse integer from empty string");
+  for (const char* d = n0; d < n1; d++)
+    if (!is_digit(*d)) return fail("invalid digit found in string");
+  unsigned __int128 v = 0;
+  for (const char* d = n0; d < n1; d++) {
+    v = v * 10 + (unsigned)(*d - '0');
+    if (v > UINT64_MAX) return fail("number too large to fit in target type");
+  }
+  value = (uint64_t)v;
+  return true;
+}
+
+// A string value's text: the span itself, or its unescaped copy in `buf`.
+inline std::pair<const char*, size_t> text_of(const Value& v, std::string& buf) {
+  if (!v.esc) return {v.s.p, v.s.n};
+  buf = unescape(v.s, true);
+  return {buf.data(), buf.size()};
+}
+
+// ShadowEdge::try_from (graph/mod.rs:72-111): latency (ns) and loss, or a message.
+bool edge_convert(const std::vector<KV>& kv, uint64_t& lat_ns, float& loss, std::string& err) {
+  const KV* l = find(kv, "latency");
+  if (!l) return err = "Edge 'latency' was not provided", false;
+  if (l->v.t != V_STR) return err = "Edge 'latency' is not a string", false;
+  uint64_t lv, lf;
+  std::string buf;
+  auto lt = text_of(l->v, buf);
+  if (!parse_time(lt.first, lt.second, "latency", lv, lf, err)) return false;
+  if (const KV* j = find(kv, "jitter")) {
+    if (j->v.t != V_STR) return err = "Edge 'jitter' is not a string", false;
+    uint64_t jv, jf;
+    auto jt = text_of(j->v, buf);
+    if (!parse_time(jt.first, jt.second, "jitter", jv, jf, err)) return false;  // parsed, then unused
+  }
+  loss = 0.0f;
+  if (const KV* pl = find(kv, "packet_loss")) {
+    if (pl->v.t != V_FLOAT) return err = "Edge 'packet_loss' is not a float", false;
+    loss = pl->v.f;
+  }
+  if (loss < 0.0f || loss > 1.0f) return err = "Edge 'packet_loss' is not in the range [0,1]", false;
+  if (lv == 0) return err = "Edge 'latency' must not be 0", false;
+  const unsigned __int128 ns = (unsigned __int128)lv * lf;
+  if (ns > UINT64_MAX)  // reference: convert(Nano).unwrap() panics (graph/mod.rs:336)
+    return err = "Edge 'latency': The resulting value is outside of the bounds [0, 18446744073709551615]", false;
+  lat_ns = (uint64_t)ns;
+  return true;
+}
+
+// One run of top-level items, in document order.
+struct Chunk {
+  enum Stop { LIMIT, END, ERROR };
+  Stop stop = LIMIT;
+  const char* endp = nullptr;     // where parsing stopped (LIMIT: at or past the limit)
+  std::string err;                // ERROR: the syntax-phase message
+  std::vector<int64_t> node_id;   // -1: no id
+  std::vector<uint8_t> node_bad;  // 1: host_bandwidth_down not a string, 2: ..._up
+  std::vector<uint32_t> esrc_id, edst_id;
+  std::vector<uint64_t> elat;
+  std::vector<float> eloss;
+  int64_t conv_err = -1;  // the first edge (chunk-local) whose conversion failed
+  std::string conv_msg;
+  std::vector<std::string> others;  // top-level keys other than node / edge / directed
+  int n_directed = 0;
+  bool directed = false;
+};
+
+// Parse top-level items from P.p until the limit (an item starting at or past
+// it is left alone), the graph's closing "]", or an error.
+void parse_items(Parser P, const char* limit, Chunk& c) {
+  std::vector<KV> kv;
+  kv.reserve(16);
+  try {
+    for (;;) {
+      if (P.p >= limit) {
+        c.stop = Chunk::LIMIT;
+        break;
+      }
+      if (P.tag(']')) {
+        c.stop = Chunk::END;
+        break;
+      }
+      Span k;
+      if (!P.key(k)) P.fail("expected key or ']'");
+      if (k.eq("node", 4)) {
+        P.block(kv);
+        const KV* id = find(kv, "id");  // parser.rs:160-164
+        if (id && id->v.t != V_INT) P.fail("Incorrect 'id' type");
+        c.node_id.push_back(id ? (int64_t)(uint32_t)id->v.i : -1);
+        uint8_t bad = 0;  // ShadowNode::try_from (graph/mod.rs:28-60)
+        const KV* bd = find(kv, "host_bandwidth_down");
+        const KV* bu = find(kv, "host_bandwidth_up");
+        if (bd && bd->v.t != V_STR)
+          bad = 1;
+        else if (bu && bu->v.t != V_STR)
+          bad = 2;
+        c.node_bad.push_back(bad);
+      } else if (k.eq("edge", 4)) {
+        P.block(kv);
+        const KV* s = find(kv, "source");  // parser.rs:190-202
+        const KV* t = find(kv, "target");
+        if (!s) P.fail("'source' doesn't exist");
+        if (s->v.t != V_INT) P.fail("Incorrect 'source' type");
+        if (!t) P.fail("'target' doesn't exist");
+        if (t->v.t != V_INT) P.fail("Incorrect 'target' type");
+        c.esrc_id.push_back((uint32_t)s->v.i);
+        c.edst_id.push_back((uint32_t)t->v.i);
+        uint64_t lat = 0;
+        float loss = 0;
+        if (c.conv_err < 0 && !edge_convert(kv, lat, loss, c.conv_msg)) c.conv_err = (int64_t)c.elat.size();
+        c.elat.push_back(lat);
+        c.eloss.push_back(loss);
+      } else if (k.eq("directed", 8)) {
+        const Value v = P.value();
+        if (v.t != V_INT) P.fail("Value was not an integer");
+        if (v.i != 0 && v.i != 1) P.fail("Bool must be 0 or 1");
+        c.directed = v.i == 1;
+        c.n_directed++;
+      } else {
+        (void)P.value();
+        c.others.emplace_back(k.p, k.n);
+      }
+    }
+  } catch (const ParseError& e) {
+    c.stop = Chunk::ERROR;
+    c.err = e.msg;
+  }
+  c.endp = P.p;
+}
+
+// The next guessed item boundary after q: the first non-blank text of a line
+// is `node` or `edge`, then blanks and '['.
+const char* resync(const char* q, const char* end) {
+  while (q < end) {
+    const char* nl = (const char*)memchr(q, '\n', (size_t)(end - q));
+    if (!nl) return end;
+    const char* k = nl + 1;
+    while (k < end && is_space(*k)) k++;
+    if (end - k >= 5 && (memcmp(k, "node", 4) == 0 || memcmp(k, "edge", 4) == 0)) {
+      const char* b = k + 4;
+      while (b < end && is_space(*b)) b++;
+      if (b < end && *b == '[') return k;
+    }
+    q = nl + 1;
+  }
+  return end;
+}
+
+unsigned default_threads() {
+  if (const char* e = getenv("SG_GML_THREADS")) return (unsigned)std::max(1, atoi(e));
+  const unsigned h = std::thread::hardware_concurrency();
+  return std::max(1u, std::min(h ? h : 1u, 16u));  // a GPU's CPU share on the box
+}
+
+void parse_into(const char* text, size_t len, unsigned threads, sg_gml* g) {
   Parser P{text, text + len, text};
   // gml (parser.rs:67-143)
   P.multispace0();
-  if (!P.tag("graph")) P.fail("expected 'graph'");
+  if ((size_t)(P.end - P.p) < 5 || memcmp(P.p, "graph", 5) != 0) P.fail("expected 'graph'");
+  P.p += 5;
   P.space0();
-  if (!P.tag("[")) P.fail("expected '['");
+  if (!P.tag('[')) P.fail("expected '['");
   if (!P.newline()) P.fail("expected newline");
-  std::vector<std::unordered_map<std::string, Value>> nodes, edges;
-  std::unordered_map<std::string, int> others;
-  int n_directed = 0;
-  for (;;) {
-    if (P.tag("]")) break;
-    std::string k;
-    if (!P.key(k)) P.fail("expected key or ']'");
-    if (k == "node") {
-      nodes.push_back(P.block());
-      auto it = nodes.back().find("id");  // parser.rs:160-164
-      if (it != nodes.back().end() && it->second.t != VT::Int) P.fail("Incorrect 'id' type");
-    } else if (k == "edge") {
-      edges.push_back(P.block());
-      auto& kv = edges.back();  // parser.rs:190-202
-      auto s = kv.find("source"), t = kv.find("target");
-      if (s == kv.end()) P.fail("'source' doesn't exist");
-      if (s->second.t != VT::Int) P.fail("Incorrect 'source' type");
-      if (t == kv.end()) P.fail("'target' doesn't exist");
-      if (t->second.t != VT::Int) P.fail("Incorrect 'target' type");
-    } else if (k == "directed") {
-      Value v = P.value();
-      if (v.t != VT::Int) P.fail("Value was not an integer");
-      if (v.i != 0 && v.i != 1) P.fail("Bool must be 0 or 1");
-      g->directed = v.i == 1;
-      n_directed++;
-    } else {
-      (void)P.value();
-      if (others[k]++) P.fail("Duplicate keys are not supported");
+  const char* body = P.p;
+  const char* end = text + len;
+  const size_t body_len = (size_t)(end - body);
+  // chunk starts: s[0] = body (a true boundary), then guesses; 1 MiB or more each
+  size_t T = body_len < ((size_t)4 << 20) ? 1 : std::min<size_t>(threads, body_len >> 20);
+  T = std::max<size_t>(T, 1);
+  std::vector<const char*> s(T + 1);
+  s[0] = body;
+  for (size_t i = 1; i < T; i++) s[i] = std::max(s[i - 1], resync(body + body_len * i / T, end));
+  s[T] = end + 1;  // past the text: the last chunk runs to the graph's "]"
+  std::vector<Chunk> ch(T);
+  auto run = [&](size_t i) { parse_items(Parser{s[i], end, text}, s[i + 1], ch[i]); };
+  if (T == 1) {
+    run(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (size_t i = 1; i < T; i++) pool.emplace_back(run, i);
+    run(0);
+    for (auto& t : pool) t.join();
+  }
+  // verify the chain in document order; an overshooting chunk goes on here
+  std::vector<Chunk> seq;
+  seq.reserve(T + 4);
+  for (size_t i = 0;;) {
+    seq.push_back(std::move(ch[i]));
+    while (seq.back().stop == Chunk::LIMIT && seq.back().endp != s[i + 1]) {
+      // overshot s[i + 1] (a guess inside a string): continue to the first later guess
+      size_t j = i + 1;
+      while (j < T && s[j] < seq.back().endp) j++;
+      Chunk more;
+      parse_items(Parser{seq.back().endp, end, text}, s[j], more);
+      seq.push_back(std::move(more));
+      i = j - 1;
     }
+    if (seq.back().stop != Chunk::LIMIT) break;
+    if (++i >= T) break;  // landed exactly on s[i]: chunk i parsed from a true boundary
+  }
+  // the syntax phase fails on the first error in document order
+  for (auto& c : seq)
+    if (c.stop == Chunk::ERROR) throw ParseError{c.err};
+  int n_directed = 0;
+  std::vector<const std::string*> others;
+  for (auto& c : seq) {
+    n_directed += c.n_directed;
+    if (c.n_directed) g->directed = c.directed;
+    for (auto& o : c.others) others.push_back(&o);
   }
   if (n_directed > 1) throw ParseError{"The 'directed' key must only be specified once"};
-  // nodes (parser.rs:146-170; ShadowNode::try_from graph/mod.rs:28-60)
-  for (auto& kv : nodes) {
-    auto it = kv.find("id");
-    if (it == kv.end()) throw ParseError{"Node 'id' was not provided"};
-    for (const char* bw : {"host_bandwidth_down", "host_bandwidth_up"}) {
-      auto b = kv.find(bw);
-      if (b != kv.end() && b->second.t != VT::Str)
-        throw ParseError{std::string("Node '") + bw + "' is not a string"};
+  std::sort(others.begin(), others.end(), [](const std::string* a, const std::string* b) { return *a < *b; });
+  for (size_t k = 1; k < others.size(); k++)
+    if (*others[k] == *others[k - 1]) throw ParseError{"Duplicate keys are not supported"};
+  // nodes (ShadowNode::try_from, graph/mod.rs:28-60), in order
+  size_t n_nodes = 0, n_edges = 0;
+  for (auto& c : seq) {
+    for (size_t k = 0; k < c.node_id.size(); k++) {
+      if (c.node_id[k] < 0) throw ParseError{"Node 'id' was not provided"};
+      if (c.node_bad[k] == 1) throw ParseError{"Node 'host_bandwidth_down' is not a string"};
+      if (c.node_bad[k] == 2) throw ParseError{"Node 'host_bandwidth_up' is not a string"};
     }
-    uint32_t id = (uint32_t)it->second.i;
-    uint32_t idx = (uint32_t)g->node_id.size();
-    g->node_id.push_back(id);
-    g->id_to_index[id] = idx;  // later duplicate wins (graph/mod.rs:157-162)
+    n_nodes += c.node_id.size();
+    n_edges += c.elat.size();
   }
-  // edges: ShadowEdge::try_from order (graph/mod.rs:72-111), then endpoint lookup (:164-175)
-  for (auto& kv : edges) {
-    auto l = kv.find("latency");
-    if (l == kv.end()) throw ParseError{"Edge 'latency' was not provided"};
-    if (l->second.t != VT::Str) throw ParseError{"Edge 'latency' is not a string"};
-    TimeVal lat = parse_time(l->second.s, "latency");
-    auto j = kv.find("jitter");
-    if (j != kv.end()) {
-      if (j->second.t != VT::Str) throw ParseError{"Edge 'jitter' is not a string"};
-      (void)parse_time(j->second.s, "jitter");  // parsed, then unused
-    }
-    float loss = 0.0f;
-    auto pl = kv.find("packet_loss");
-    if (pl != kv.end()) {
-      if (pl->second.t != VT::Float) throw ParseError{"Edge 'packet_loss' is not a float"};
-      loss = pl->second.f;
-    }
-    if (loss < 0.0f || loss > 1.0f) throw ParseError{"Edge 'packet_loss' is not in the range [0,1]"};
-    if (lat.value == 0) throw ParseError{"Edge 'latency' must not be 0"};
-    unsigned __int128 ns = (unsigned __int128)lat.value * lat.factor;
-    if (ns > UINT64_MAX)  // reference: convert(Nano).unwrap() panics (graph/mod.rs:336)
-      throw ParseError{"Edge 'latency': The resulting value is outside of the bounds [0, 18446744073709551615]"};
-    uint32_t sid = (uint32_t)kv["source"].i, tid = (uint32_t)kv["target"].i;
-    auto si = g->id_to_index.find(sid);
-    if (si == g->id_to_index.end()) throw ParseError{"Edge source " + std::to_string(sid) + " doesn't exist"};
-    auto ti = g->id_to_index.find(tid);
-    if (ti == g->id_to_index.end()) throw ParseError{"Edge target " + std::to_string(tid) + " doesn't exist"};
-    g->esrc.push_back(si->second);
-    g->edst.push_back(ti->second);
-    g->elat.push_back((uint64_t)ns);
-    g->eloss.push_back(loss);
+  g->node_id.resize(n_nodes);
+  uint32_t max_id = 0;
+  {
+    size_t o = 0;
+    for (auto& c : seq)
+      for (int64_t id : c.node_id) {
+        g->node_id[o++] = (uint32_t)id;
+        max_id = std::max(max_id, (uint32_t)id);
+      }
   }
+  // id -> index, a later duplicate winning (graph/mod.rs:157-162)
+  if (n_nodes && (uint64_t)max_id < 4 * (uint64_t)n_nodes + 1024) {
+    g->dense.assign((size_t)max_id + 1, UINT32_MAX);
+    for (uint32_t k = 0; k < n_nodes; k++) g->dense[g->node_id[k]] = k;
+  } else {
+    g->sparse.reserve(n_nodes);
+    for (uint32_t k = 0; k < n_nodes; k++) g->sparse[g->node_id[k]] = k;
+  }
+  // edges: conversion, then endpoint lookup (graph/mod.rs:164-175), in order;
+  // chunks run on threads, the first failure in document order wins
+  g->esrc.resize(n_edges);
+  g->edst.resize(n_edges);
+  g->elat.resize(n_edges);
+  g->eloss.resize(n_edges);
+  std::vector<size_t> eoff(seq.size() + 1, 0);
+  for (size_t k = 0; k < seq.size(); k++) eoff[k + 1] = eoff[k] + seq[k].elat.size();
+  std::vector<std::string> first_err(seq.size());
+  auto link = [&](size_t k) {
+    const Chunk& c = seq[k];
+    const size_t o = eoff[k], n = c.elat.size();
+    for (size_t e = 0; e < n; e++) {
+      if ((int64_t)e == c.conv_err) {
+        first_err[k] = c.conv_msg;
+        return;
+      }
+      uint32_t si, ti;
+      if (!g->lookup(c.esrc_id[e], si)) {
+        first_err[k] = "Edge source " + std::to_string(c.esrc_id[e]) + " doesn't exist";
+        return;
+      }
+      if (!g->lookup(c.edst_id[e], ti)) {
+        first_err[k] = "Edge target " + std::to_string(c.edst_id[e]) + " doesn't exist";
+        return;
+      }
+      g->esrc[o + e] = si;
+      g->edst[o + e] = ti;
+      g->elat[o + e] = c.elat[e];
+      g->eloss[o + e] = c.eloss[e];
+    }
+  };
+  if (seq.size() == 1) {
+    link(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (size_t k = 1; k < seq.size(); k++) pool.emplace_back(link, k);
+    link(0);
+    for (auto& t : pool) t.join();
+  }
+  for (auto& m : first_err)
+    if (!m.empty()) throw ParseError{m};
 }
 
 }  // namespace
 
 extern "C" {
 
-int32_t sg_gml_parse(const char* text, size_t len, sg_gml** out, char* err, size_t err_len) {
+int32_t sg_gml_parse_threads(const char* text, size_t len, uint32_t threads, sg_gml** out, char* err,
+                             size_t err_len) {
   if (!out || (!text && len)) return SG_ERR_INVALID_ARG;
   *out = nullptr;
   sg_gml* g = new (std::nothrow) sg_gml();
   if (!g) return SG_ERR_OOM;
   try {
-    parse_into(text ? text : "", len, g);
+    parse_into(text ? text : "", len, threads ? threads : default_threads(), g);
   } catch (const ParseError& e) {
     if (err && err_len) {
       strncpy(err, e.msg.c_str(), err_len - 1);
@@ -361,9 +675,16 @@ int32_t sg_gml_parse(const char* text, size_t len, sg_gml** out, char* err, size
   } catch (const std::bad_alloc&) {
     delete g;
     return SG_ERR_OOM;
+  } catch (const std::system_error&) {  // no thread could be started
+    delete g;
+    return SG_ERR_OOM;
   }
   *out = g;
   return SG_OK;
+}
+
+int32_t sg_gml_parse(const char* text, size_t len, sg_gml** out, char* err, size_t err_len) {
+  return sg_gml_parse_threads(text, len, 0, out, err, err_len);
 }
 
 int32_t sg_gml_graph(const sg_gml* g, sg_graph* out) {
@@ -381,10 +702,7 @@ int32_t sg_gml_graph(const sg_gml* g, sg_graph* out) {
 
 int32_t sg_gml_node_index(const sg_gml* g, uint32_t gml_id, uint32_t* out_index) {
   if (!g || !out_index) return SG_ERR_INVALID_ARG;
-  auto it = g->id_to_index.find(gml_id);
-  if (it == g->id_to_index.end()) return SG_ERR_INVALID_ARG;
-  *out_index = it->second;
-  return SG_OK;
+  return g->lookup(gml_id, *out_index) ? SG_OK : SG_ERR_INVALID_ARG;
 }
 
 void sg_gml_destroy(sg_gml* g) { delete g; }

@@ -227,13 +227,14 @@ class NetworkGraph:
             pass
 
     @classmethod
-    def parse(cls, graph_text: str, ctx: Optional[Context] = None) -> "NetworkGraph":
-        """NetworkGraph::parse (graph/mod.rs:134-181); raises ShadowGpuError(SG_ERR_PARSE)."""
+    def parse(cls, graph_text, ctx: Optional[Context] = None, threads: int = 0) -> "NetworkGraph":
+        """NetworkGraph::parse (graph/mod.rs:134-181); raises ShadowGpuError(SG_ERR_PARSE).
+        graph_text: str or bytes (UTF-8).  threads: host threads for the parse (0 = min(cores, 16))."""
         L = load()
-        raw = graph_text.encode()
+        raw = graph_text.encode() if isinstance(graph_text, str) else bytes(graph_text)
         h = C.c_void_p()
         err = C.create_string_buffer(512)
-        rc = L.sg_gml_parse(raw, len(raw), C.byref(h), err, len(err))
+        rc = L.sg_gml_parse_threads(raw, len(raw), int(threads), C.byref(h), err, len(err))
         if rc != _capi.SG_OK:
             raise ShadowGpuError(rc, err.value.decode(errors="replace") or f"parse status {rc}")
         try:
@@ -246,6 +247,28 @@ class NetworkGraph:
                        bool(g.directed), arr(g.node_gml_id, n, np.uint32), ctx)
         finally:
             L.sg_gml_destroy(h)
+
+    @classmethod
+    def from_file(cls, path, compression: Optional[str] = None, ctx: Optional[Context] = None,
+                  threads: int = 0) -> "NetworkGraph":
+        """load_network_graph + NetworkGraph::parse (graph/mod.rs:483-513): a GML file, plain or
+        xz-compressed (compression="xz", as lzma_rs::xz_decompress; here the system liblzma
+        through Python's lzma module).  The text must be UTF-8 (String::from_utf8)."""
+        import os
+
+        path = os.path.expanduser(str(path))  # tilde_expansion
+        if compression is None:
+            with open(path, "rb") as f:
+                raw = f.read()
+        elif compression == "xz":
+            import lzma
+
+            with lzma.open(path, "rb", format=lzma.FORMAT_XZ) as f:
+                raw = f.read()
+        else:
+            raise ValueError(f"unknown compression {compression!r} (configuration.rs:985-988: xz)")
+        raw.decode("utf-8")  # Err(FromUtf8Error) in the reference
+        return cls.parse(raw, ctx=ctx, threads=threads)
 
     def node_id_to_index(self, node_id: int) -> Optional[int]:
         return self._id_to_index.get(int(node_id))
