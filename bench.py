@@ -49,6 +49,7 @@ def parse_args():
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-delivery", action="store_true")
     p.add_argument("--no-codel", action="store_true", help="skip the router CoDel leg")
+    p.add_argument("--no-gml", action="store_true", help="skip the GML ingest leg")
     p.add_argument("--no-pack", action="store_true",
                    help="deliver from the two-array table (no packed path-key copy)")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
@@ -364,6 +365,34 @@ def inbound_leg(a, D, ctx, torch, buckets, n_packets, pmc, round_end):
     return leg
 
 
+GML_NODES = 50000  # 10k-50k-node graphs
+
+
+def gml_leg(a, NetworkGraph, synth):
+    """GML ingest (NetworkGraph::parse, graph/mod.rs:134-181) of a 50k-node graph: the
+    host C++ parser on the box's CPU share, and on one thread."""
+    g = synth.ring_chords_graph(GML_NODES, a.degree, seed=1)
+    raw = synth.graph_to_gml(g).encode()
+    th = min(16, os.cpu_count() or 1)
+
+    def best(threads, reps=3):
+        t = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            p = NetworkGraph.parse(raw, threads=threads)
+            t.append(time.perf_counter() - t0)
+        assert p.n_nodes == g["n"] and np.array_equal(p.edge_latency_ns, g["lat"])
+        return min(t)
+
+    t_many, t_one = best(th), best(1)
+    mb = len(raw) / 1e6
+    return {"metric": "GML ingest MB/s (parse + edge conversion + id lookup)", "unit": "MB/s",
+            "value": round(mb / t_many, 1), "higher_is_better": True, "ms": round(t_many * 1e3, 2), "threads": th,
+            "single_thread": {"value": round(mb / t_one, 1), "ms": round(t_one * 1e3, 2)},
+            "config": {"workload": f"{GML_NODES}-node ring+chords GML (synth.graph_to_gml), mean degree {a.degree}",
+                       "bytes": len(raw), "nodes": int(g["n"]), "edges": int(len(g["src"]))}}
+
+
 def main():
     a = parse_args()
     D = Dist(a.gpus)
@@ -455,6 +484,8 @@ def main():
     }
     if cpu:
         result["apsp_detail"]["speedup_vs_cpu"] = round(cpu["value"] / t_build, 1)
+    if D.rank == 0 and not a.no_gml:
+        result["gml_ingest"] = gml_leg(a, NetworkGraph, synth)
 
     # ---------------- delivery round (C4) ----------------
     if not a.no_delivery:
