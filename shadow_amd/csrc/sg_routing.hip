@@ -372,20 +372,24 @@ __device__ __forceinline__ void load_key2(__amdgpu_buffer_rsrc_t rsrc, uint32_t 
 // Same work items, frontier, LDS merge and flush as k_relax_w; a flush writes
 // both keys of a lane with one 16-B store (the row's only writer is this wave,
 // so the unchanged half is rewritten with the value it holds).
-template <int NPW, int K, int GROUP, bool FRONT, bool COUNT>
+// B = 32 (SG_APSP_B=32): 16 lanes per row, four rows per wave instruction, and
+// a 2.5 MB slab at 10k nodes that fits one XCD's 4 MB L2.
+template <int B, int NPW, int K, int GROUP, bool FRONT, bool COUNT>
 __global__ void __launch_bounds__(RELAX_THREADS)
     k_relax_w2(const uint32_t* __restrict__ in_off, const uint4* __restrict__ in_rec, uint64_t* __restrict__ D,
                uint32_t n, const uint32_t* __restrict__ alist, uint32_t* __restrict__ changed,
                uint32_t* __restrict__ stamp, uint32_t pass, unsigned long long* __restrict__ work) {
-  constexpr int B = 64;
+  static_assert(B == 64 || B == 32, "B = 64 or 32");
   constexpr int WAVES = RELAX_THREADS / 64;
   constexpr int STG_W = 64 * K;
-  constexpr int G = 2;  // rows per wave instruction
-  static_assert(NPW % G == 0, "NPW must be even");
+  constexpr int LPR = B / 2;   // lanes per row
+  constexpr int G = 64 / LPR;  // rows per wave instruction
+  constexpr uint64_t ROW_MASK = LPR == 64 ? ~0ull : (1ull << LPR) - 1;
+  static_assert(NPW % G == 0, "NPW must be a multiple of the rows per instruction");
   __shared__ uint4 lists[WAVES][STG_W];
   __shared__ unsigned long long bests[WAVES][NPW * B];
   const int lane = threadIdx.x & 63;
-  const uint32_t gh = lane >> 5, sl = lane & 31;  // row group; the lane's sources 2 sl, 2 sl + 1
+  const uint32_t gh = lane / LPR, sl = lane % LPR;  // row group; the lane's sources 2 sl, 2 sl + 1
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane16 = sl * 16;
   uint4* list = lists[w];
@@ -502,7 +506,7 @@ __global__ void __launch_bounds__(RELAX_THREADS)
       const uint64_t m = __ballot(c0 || c1);
       if (m) {
         any = true;
-        if (FRONT && sl == 0 && ((m >> (gh * 32)) & 0xffffffffull)) stamp[(size_t)b * n + v] = pass + 2;
+        if (FRONT && sl == 0 && ((m >> (gh * LPR)) & ROW_MASK)) stamp[(size_t)b * n + v] = pass + 2;
       }
     }
     if (any && b != flagged) {
@@ -961,12 +965,11 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
         {
           TimedLaunch tl(ctx, "relax", 0.0);
           if constexpr (SPL == 2) {
-            static_assert(B == 64, "two sources per lane: B = 64");
             if (work)
-              hipLaunchKernelGGL((k_relax_w2<NPW, STG / 64, GR, FRONT, true>), dim3(grid), dim3(RELAX_THREADS), 0,
+              hipLaunchKernelGGL((k_relax_w2<B, NPW, STG / 64, GR, FRONT, true>), dim3(grid), dim3(RELAX_THREADS), 0,
                                  st, net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
             else
-              hipLaunchKernelGGL((k_relax_w2<NPW, STG / 64, GR, FRONT, false>), dim3(grid), dim3(RELAX_THREADS), 0,
+              hipLaunchKernelGGL((k_relax_w2<B, NPW, STG / 64, GR, FRONT, false>), dim3(grid), dim3(RELAX_THREADS), 0,
                                  st, net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
           } else {
             if (work)
@@ -1044,32 +1047,37 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
                            uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
   const bool front = env_int("SG_APSP_FRONTIER", 1) != 0;
   const int bsz = env_int("SG_APSP_B", 64);
-  const int spl = env_int("SG_APSP_SPL", bsz == 64 ? 2 : 1);  // sources per lane: 2 = k_relax_w2 (the default)
+  const int spl = env_int("SG_APSP_SPL", 2);  // sources per lane: 2 = k_relax_w2 (the default)
   // defaults: the fastest measured configuration of each kernel (tools/apsp_variants.py)
   const int npw = env_int("SG_APSP_NPW", spl == 2 ? 4 : 8), stg = env_int("SG_APSP_STAGE", spl == 2 ? 64 : 128);
   const int gr = env_int("SG_APSP_GROUP", spl == 2 ? 3 : 8);
   if (spl == 2) {
-#define SG_SP2(NPW_, STG_, GR_)                                                                          \
-  if (bsz == 64 && npw == NPW_ && stg == STG_ && gr == GR_) {                                           \
+#define SG_SP2(B_, NPW_, STG_, GR_)                                                                      \
+  if (bsz == B_ && npw == NPW_ && stg == STG_ && gr == GR_) {                                           \
     if (front)                                                                                          \
-      shortest_paths_t<64, NPW_, STG_, GR_, true, 2>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, \
+      shortest_paths_t<B_, NPW_, STG_, GR_, true, 2>(ctx, net, d_used, n_used, row_begin, row_end, out_lat, \
                                                      out_loss);                                         \
     else                                                                                                \
-      shortest_paths_t<64, NPW_, STG_, GR_, false, 2>(ctx, net, d_used, n_used, row_begin, row_end,      \
+      shortest_paths_t<B_, NPW_, STG_, GR_, false, 2>(ctx, net, d_used, n_used, row_begin, row_end,      \
                                                       out_lat, out_loss);                               \
     return;                                                                                             \
   }
-    SG_SP2(8, 128, 8)
-    SG_SP2(8, 128, 4)
-    SG_SP2(8, 128, 2)
-    SG_SP2(8, 128, 6)
-    SG_SP2(8, 64, 4)
-    SG_SP2(4, 64, 4)
-    SG_SP2(4, 128, 4)
-    SG_SP2(2, 64, 4)
-    SG_SP2(4, 64, 3)
-    SG_SP2(4, 64, 5)
-    SG_SP2(16, 128, 4)
+    SG_SP2(64, 8, 128, 8)
+    SG_SP2(64, 8, 128, 4)
+    SG_SP2(64, 8, 128, 2)
+    SG_SP2(64, 8, 128, 6)
+    SG_SP2(64, 8, 64, 4)
+    SG_SP2(64, 4, 64, 4)
+    SG_SP2(64, 4, 128, 4)
+    SG_SP2(64, 2, 64, 4)
+    SG_SP2(64, 4, 64, 3)
+    SG_SP2(64, 4, 64, 5)
+    SG_SP2(64, 16, 128, 4)
+    SG_SP2(32, 4, 64, 3)
+    SG_SP2(32, 4, 64, 2)
+    SG_SP2(32, 8, 64, 3)
+    SG_SP2(32, 8, 128, 3)
+    SG_SP2(32, 4, 128, 3)
 #undef SG_SP2
     throw Error(SG_ERR_INVALID_ARG, "unsupported SG_APSP_SPL=2 configuration");
   }
