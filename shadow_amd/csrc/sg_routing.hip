@@ -536,58 +536,77 @@ __device__ __forceinline__ void out_entry(uint64_t kk, uint32_t row, uint32_t j,
   }
 }
 
-template <int B, bool VEC>
+// TPB column tiles per block: the global loads of tile t + 1 are issued into
+// registers before tile t is written out, so a block's reads and writes overlap.
+template <int B, bool VEC, int TPB>
 __global__ void __launch_bounds__(256)
     k_out_batch(const uint64_t* __restrict__ D, uint32_t n, const uint32_t* __restrict__ used, uint32_t n_used,
                 uint32_t first_row, uint32_t row_end, uint32_t out_row0, const uint32_t* __restrict__ self_edge,
                 const uint64_t* __restrict__ e_lat, const float* __restrict__ e_loss,
                 uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, uint32_t* __restrict__ sat) {
   constexpr int G = 64 / B;
+  constexpr int CPW = 64 / (4 * G);  // tile columns (nodes) each lane loads
   __shared__ uint64_t tile[64][B + 1];
   const uint32_t b = blockIdx.y;
-  const uint32_t j0 = blockIdx.x * 64;
   const uint64_t* __restrict__ Db = D + (size_t)b * n * B;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int gh = lane / B, sl = lane % B;
-  for (int c = wave * G + gh; c < 64; c += 4 * G) {
-    const uint32_t j = j0 + c;
-    tile[c][sl] = j < n_used ? Db[(size_t)used[j] * B + sl] : 0ull;
-  }
-  __syncthreads();
+  uint64_t pre[CPW];
+  auto load_tile = [&](uint32_t j0) {
+    uint32_t node[CPW];
+#pragma unroll
+    for (int k = 0; k < CPW; k++) {
+      const uint32_t j = j0 + wave * G + gh + k * 4 * G;
+      node[k] = j < n_used ? used[j] : ~0u;
+    }
+#pragma unroll
+    for (int k = 0; k < CPW; k++) pre[k] = node[k] != ~0u ? Db[(size_t)node[k] * B + sl] : 0ull;
+  };
   bool sflag = false;
   const uint32_t rbase = first_row + b * B;
-  if (VEC && j0 + 64 <= n_used) {
-    // lane = (row quarter, 4 columns): each key is read from LDS once, and the
-    // lane stores 32 B of latencies and 16 B of losses
-    for (int r = wave * 4 + (lane >> 4); r < B; r += 16) {
-      const uint32_t row = rbase + r;
-      if (row >= row_end) continue;
-      const uint32_t c = (lane & 15) * 4;
-      uint64_t l0, l1, l2, l3;
-      float4 f;
-      out_entry(tile[c][r], row, j0 + c, used, self_edge, e_lat, e_loss, l0, f.x, sflag);
-      out_entry(tile[c + 1][r], row, j0 + c + 1, used, self_edge, e_lat, e_loss, l1, f.y, sflag);
-      out_entry(tile[c + 2][r], row, j0 + c + 2, used, self_edge, e_lat, e_loss, l2, f.z, sflag);
-      out_entry(tile[c + 3][r], row, j0 + c + 3, used, self_edge, e_lat, e_loss, l3, f.w, sflag);
-      const size_t o = (size_t)(row - out_row0) * n_used + j0 + c;
-      // write-once streaming output (1.2 GB at 10k): nontemporal 16-B stores
-      typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-      typedef float f32x4 __attribute__((ext_vector_type(4)));
-      __builtin_nontemporal_store((u64x2){l0, l1}, (u64x2*)&out_lat[o]);
-      __builtin_nontemporal_store((u64x2){l2, l3}, (u64x2*)&out_lat[o + 2]);
-      __builtin_nontemporal_store((f32x4){f.x, f.y, f.z, f.w}, (f32x4*)&out_loss[o]);
-    }
-  } else {
-    const uint32_t j = j0 + lane;
-    for (int r = wave; r < B; r += 4) {
-      const uint32_t row = rbase + r;
-      if (row >= row_end || j >= n_used) continue;
-      const size_t o = (size_t)(row - out_row0) * n_used + j;
-      uint64_t l;
-      float f;
-      out_entry(tile[lane][r], row, j, used, self_edge, e_lat, e_loss, l, f, sflag);
-      out_lat[o] = l;
-      out_loss[o] = f;
+  const uint32_t jb = blockIdx.x * TPB * 64;
+  load_tile(jb);
+  for (int t = 0; t < TPB; t++) {
+    const uint32_t j0 = jb + t * 64;
+    if (j0 >= n_used) break;
+    if (t) __syncthreads();  // the previous tile's write-out has read the LDS tile
+#pragma unroll
+    for (int k = 0; k < CPW; k++) tile[wave * G + gh + k * 4 * G][sl] = pre[k];
+    __syncthreads();
+    if (t + 1 < TPB && j0 + 64 < n_used) load_tile(j0 + 64);
+    if (VEC && j0 + 64 <= n_used) {
+      // lane = (row quarter, 4 columns): each key is read from LDS once, and the
+      // lane stores 32 B of latencies and 16 B of losses
+      for (int r = wave * 4 + (lane >> 4); r < B; r += 16) {
+        const uint32_t row = rbase + r;
+        if (row >= row_end) continue;
+        const uint32_t c = (lane & 15) * 4;
+        uint64_t l0, l1, l2, l3;
+        float4 f;
+        out_entry(tile[c][r], row, j0 + c, used, self_edge, e_lat, e_loss, l0, f.x, sflag);
+        out_entry(tile[c + 1][r], row, j0 + c + 1, used, self_edge, e_lat, e_loss, l1, f.y, sflag);
+        out_entry(tile[c + 2][r], row, j0 + c + 2, used, self_edge, e_lat, e_loss, l2, f.z, sflag);
+        out_entry(tile[c + 3][r], row, j0 + c + 3, used, self_edge, e_lat, e_loss, l3, f.w, sflag);
+        const size_t o = (size_t)(row - out_row0) * n_used + j0 + c;
+        // write-once streaming output (1.2 GB at 10k): nontemporal 16-B stores
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        typedef float f32x4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store((u64x2){l0, l1}, (u64x2*)&out_lat[o]);
+        __builtin_nontemporal_store((u64x2){l2, l3}, (u64x2*)&out_lat[o + 2]);
+        __builtin_nontemporal_store((f32x4){f.x, f.y, f.z, f.w}, (f32x4*)&out_loss[o]);
+      }
+    } else {
+      const uint32_t j = j0 + lane;
+      for (int r = wave; r < B; r += 4) {
+        const uint32_t row = rbase + r;
+        if (row >= row_end || j >= n_used) continue;
+        const size_t o = (size_t)(row - out_row0) * n_used + j;
+        uint64_t l;
+        float f;
+        out_entry(tile[lane][r], row, j, used, self_edge, e_lat, e_loss, l, f, sflag);
+        out_lat[o] = l;
+        out_loss[o] = f;
+      }
     }
   }
   if (__any(sflag) && lane == 0) atomicOr(&sat[b], 1u);
@@ -930,6 +949,8 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
   // chunk.  A pass issued after its batch converged finds it off the active list.
   const uint32_t chunk = (uint32_t)std::max(1, env_int("SG_APSP_PASS_CHUNK", 4));
   const bool trace = env_int("SG_APSP_TRACE", 0) != 0;  // per-pass diagnostics on stderr
+  int out_tpb = env_int("SG_APSP_OUT_TPB", 1);  // column tiles per write-out block: 1 | 2 | 4 (1 measured best)
+  out_tpb = out_tpb == 4 ? 4 : out_tpb == 2 ? 2 : 1;
   std::vector<uint32_t> h_sat(group);
   std::vector<uint32_t> wide_rows;
   for (uint32_t g0 = 0; g0 < n_batches; g0 += group) {
@@ -944,7 +965,10 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
     // one wave per work item (active batch, NPW-node chunk); 4 waves per block,
     // a multiple of 8 blocks (XCD mapping)
     const uint32_t ncw = (n + 4 * NPW - 1) / (4 * NPW);
-    const uint32_t grid = 8 * ncw * ((gb + 7) / 8);
+    // Sized for the active batches the host last saw (every batch at first; a
+    // converged batch never becomes active again, so it is an upper bound for
+    // the chunk): a tail pass with few active batches launches few blocks.
+    uint32_t n_act_seen = gb;
     hipEvent_t te0 = nullptr, te1 = nullptr;
     if (trace) {
       SG_HIP(hipEventCreate(&te0));
@@ -955,6 +979,7 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
     // pass before it, or at a chunk end, where its count also goes to the host
     hipLaunchKernelGGL(k_active_list, dim3(1), dim3(1024), 0, st, ring[2], gb, alist, ring[0], nullptr);
     for (uint32_t pass = 0;;) {
+      const uint32_t grid = 8 * ncw * ((n_act_seen + 7) / 8);
       for (uint32_t c = 0; c < chunk; c++, pass++) {
         if (pass > n + 2 + chunk) throw Error(SG_ERR_DEVICE, "relaxation did not converge");
         if (trace) SG_HIP(hipEventRecord(te0, st));
@@ -1002,7 +1027,8 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
                          ring[pass % 3], ctx->apsp_ret);
       SG_CHECK_LAUNCH();
       SG_HIP(hipStreamSynchronize(st));
-      if (*(volatile uint32_t*)ctx->apsp_ret == 0) break;
+      n_act_seen = *(volatile uint32_t*)ctx->apsp_ret;
+      if (n_act_seen == 0) break;
     }
     if (trace) {
       SG_HIP(hipEventDestroy(te0));
@@ -1012,14 +1038,19 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
     {
       TimedLaunch tl(ctx, "out", 12.0 * std::min<uint32_t>(gb * B, row_end - first_row) * n_used);
       const bool vec = n_used % 4 == 0 && ((uintptr_t)out_lat & 15) == 0 && ((uintptr_t)out_loss & 15) == 0;
-      if (vec)
-        hipLaunchKernelGGL((k_out_batch<B, true>), dim3((n_used + 63) / 64, gb), dim3(256), 0, st, D, n, d_used,
-                           n_used, first_row, row_end, row_begin, net->self_edge, net->e_lat, net->e_loss, out_lat,
-                           out_loss, sat);
-      else
-        hipLaunchKernelGGL((k_out_batch<B, false>), dim3((n_used + 63) / 64, gb), dim3(256), 0, st, D, n, d_used,
-                           n_used, first_row, row_end, row_begin, net->self_edge, net->e_lat, net->e_loss, out_lat,
-                           out_loss, sat);
+      const uint32_t tpb = out_tpb;
+      const dim3 og((n_used + 64 * tpb - 1) / (64 * tpb), gb);
+#define SG_OUT(V_, T_)                                                                                          \
+  hipLaunchKernelGGL((k_out_batch<B, V_, T_>), og, dim3(256), 0, st, D, n, d_used, n_used, first_row, row_end, \
+                     row_begin, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat)
+      // (the grid above is sized for tpb: every branch launches TPB = tpb)
+      if (vec && tpb == 4) SG_OUT(true, 4);
+      else if (vec && tpb == 2) SG_OUT(true, 2);
+      else if (vec) SG_OUT(true, 1);
+      else if (tpb == 4) SG_OUT(false, 4);
+      else if (tpb == 2) SG_OUT(false, 2);
+      else SG_OUT(false, 1);
+#undef SG_OUT
     }
     SG_CHECK_LAUNCH();
     copy_to_host(ctx, h_sat.data(), sat, gb * 4ull);

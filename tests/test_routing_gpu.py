@@ -188,7 +188,9 @@ def test_empty_used(ctx):
                                  {"SG_APSP_SPL": "1", "SG_APSP_NPW": "16"}, {"SG_APSP_SPL": "1", "SG_APSP_FRONTIER": "0"},
                                  {"SG_APSP_NPW": "8", "SG_APSP_STAGE": "128", "SG_APSP_GROUP": "8"},
                                  {"SG_APSP_NPW": "16", "SG_APSP_STAGE": "128", "SG_APSP_GROUP": "4"},
-                                 {"SG_APSP_B": "32", "SG_APSP_SPL": "1", "SG_APSP_NPW": "16"}, {"SG_APSP_PASS_CHUNK": "1"}])
+                                 {"SG_APSP_B": "32", "SG_APSP_SPL": "1", "SG_APSP_NPW": "16"}, {"SG_APSP_PASS_CHUNK": "1"},
+                                 {"SG_APSP_OUT_TPB": "1"}, {"SG_APSP_OUT_TPB": "4"},
+                                 {"SG_APSP_OUT_TPB": "4", "SG_APSP_B": "32"}])
 def test_kernel_variants_bit_exact(oracle, ctx, monkeypatch, env):
     """Every A/B variant of the relaxation kernel (slab width, frontier, item size) is exact."""
     for k, v in env.items():

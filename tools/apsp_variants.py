@@ -66,6 +66,7 @@ def main():
         ctx.enable_timers(True)
         net.build_rows_device(used, 0, r1, lat.data_ptr(), loss.data_ptr(), True)
         rms, launches, _ = ctx.read_timer("relax")
+        oms, _, _ = ctx.read_timer("out")
         ctx.enable_timers(True, count_work=True)
         net.build_rows_device(used, 0, r1, lat.data_ptr(), loss.data_ptr(), True)
         _, _, work = ctx.read_timer("relax")
@@ -76,7 +77,7 @@ def main():
         ref = ref or h
         ms = float(np.median(times[v]))
         print(f"variant {v!r}: {ms:8.3f} ms/build (median of {a.rounds}; min {min(times[v]):.3f})  relax {rms:8.3f} ms "
-              f"in {launches} launches, {work / 1e9:.3f} G lane-relaxations, {work / max(rms, 1e-9) / 1e6:.1f} G/s  "
+              f"in {launches} launches, out {oms:.3f} ms, {work / 1e9:.3f} G lane-relaxations, {work / max(rms, 1e-9) / 1e6:.1f} G/s  "
               f"identical={same}", flush=True)
 
 
