@@ -46,6 +46,13 @@ def parse_args():
     p.add_argument("--degree", type=float, default=8.0)
     p.add_argument("--hosts", type=int, default=100000)
     p.add_argument("--packets", type=int, default=1000000)
+    p.add_argument("--config", choices=("c3c4", "c5"), default="c3c4",
+                   help="c3c4 (default): the C3 routing build + C4 delivery round (weak scaling, 1M packets per "
+                        "rank); c5: SURVEY 8d C5, a 50k-node graph and 10M packets per round in total, split "
+                        "over the ranks (strong scaling)")
+    p.add_argument("--cpu-rows", type=int, default=0,
+                   help="time the CPU routing baseline on the first K source rows and scale to all rows "
+                        "(0 = every row)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-delivery", action="store_true")
     p.add_argument("--no-codel", action="store_true", help="skip the router CoDel leg")
@@ -54,7 +61,10 @@ def parse_args():
                    help="deliver from the two-array table (no packed path-key copy)")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                    help="PMC summary (HBM bytes per launch) written by tools/pmc_summary.py")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.config == "c5":
+        a.nodes, a.hosts, a.packets = 50000, 100000, 10000000
+    return a
 
 
 class Dist:
@@ -107,6 +117,10 @@ def timed(D, fn, steps, warmup):
     torch.cuda.synchronize()
     D.barrier()
     return D.max(time.perf_counter() - t0) / steps
+
+
+def _pow2(x):
+    return 1 << max(0, int(x) - 1).bit_length()
 
 
 def load_pmc(path):
@@ -174,7 +188,7 @@ def codel_leg(a, D, ctx, torch, buckets, n_packets, pmc):
     evs = codel_events(offs, order, dtime, lens)
     E = len(evs[0])
     H = len(offs) - 1
-    q = CoDelQueues(H, 256, ctx=ctx)
+    q = CoDelQueues(H, max(256, _pow2(int(np.diff(offs).max(initial=0)))), ctx=ctx)
     ev = CoDelEvents.from_numpy(*evs)
     status = torch.zeros(max(n_packets, 1), dtype=torch.uint8, device="cuda")
     state0 = q.get_state()
@@ -241,7 +255,8 @@ def outbound_leg(a, D, ctx, torch, pk, hosts, ht, table, round_end, sharded, pmc
     status = torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")
     bw = np.full(H, BW_UP_BITS, np.uint64)
     n_pipes = 2 * (a.steps + a.warmup) + 1
-    pipes = [OutboundPipeline(hosts["ip"], bw, 64, ctx=ctx) for _ in range(n_pipes)]  # a fresh state per step
+    cap = max(64, _pow2(int(np.bincount(pk["src"], minlength=H).max(initial=0))))  # deepest interface queue
+    pipes = [OutboundPipeline(hosts["ip"], bw, cap, ctx=ctx) for _ in range(n_pipes)]  # a fresh state per step
     for p in pipes:
         p.sent_buffers(n + 4 * H, "cuda")
     it = iter(pipes)
@@ -321,7 +336,8 @@ def inbound_leg(a, D, ctx, torch, buckets, n_packets, pmc, round_end):
     fwd = torch.full((max(n_packets, 1),), -1, dtype=torch.int64, device="cuda")
     status = torch.zeros(max(n_packets, 1), dtype=torch.uint8, device="cuda")
     bw = np.full(H, BW_DOWN_BITS, np.uint64)
-    pipes = [InboundPipeline(bw, 256, ctx=ctx) for _ in range(a.steps + a.warmup + 1)]  # a fresh state per step
+    cap = max(256, _pow2(int(np.diff(offs).max(initial=0))))  # the deepest router queue
+    pipes = [InboundPipeline(bw, cap, ctx=ctx) for _ in range(a.steps + a.warmup + 1)]  # a fresh state per step
     it = iter(pipes)
 
     def step():
@@ -403,7 +419,10 @@ def main():
     ctx = Context(D.local, stream=torch.cuda.current_stream().cuda_stream)
     pmc = load_pmc(a.pmc_json)
 
-    # ---------------- routing-table build (C3) ----------------
+    c5 = a.config == "c5"
+    if c5:  # 10M packets per round in total, split over the ranks
+        a.packets = (a.packets + D.world - 1) // D.world
+    # ---------------- routing-table build (C3 / C5) ----------------
     g = synth.ring_chords_graph(a.nodes, a.degree, seed=1)
     net = NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
     used = np.arange(a.nodes, dtype=np.uint32)
@@ -457,20 +476,24 @@ def main():
         from oracle import oracle as O  # the checker, timed as the CPU baseline
 
         threads = min(16, os.cpu_count() or 1)
+        k = nu if a.cpu_rows <= 0 else min(a.cpu_rows, nu)
         t0 = time.perf_counter()
-        rc, _, _, _ = O.shortest_paths(g["n"], g["src"], g["dst"], g["lat"], g["loss"], False, used, threads=threads)
-        t_cpu = time.perf_counter() - t0
+        rc, _, _, _ = O.shortest_paths(g["n"], g["src"], g["dst"], g["lat"], g["loss"], False, used, rows=(0, k),
+                                       threads=threads)
+        t_cpu = (time.perf_counter() - t0) * nu / k
         assert rc == 0
+        what = f"all {nu} sources" if k == nu else f"the first {k} of {nu} sources, scaled by {nu}/{k}"
         cpu = {"value": round(t_cpu, 4), "unit": "s", "cores": threads, "kind": "port",
-               "sample": f"all {nu} sources (binary-heap Dijkstra, dense output, no HashMap materialisation) "
+               "sample": f"{what} (binary-heap Dijkstra, dense output, no HashMap materialisation) "
                          f"on the same graph, {threads} threads"}
 
     result = {
         "metric": METRIC, "value": round(t_build, 6), "unit": "s", "n_gpus": D.world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(t_build * 1e3, 4), "higher_is_better": False,
         "scaling": "strong", "vs_baseline": None, "dtype": "u64+f32",
-        "data": "synthetic (seeded ring+chords graph, SURVEY §8d C3)",
-        "config": {"workload": "C3 APSP routing build: 10k-node undirected ring+chords graph, mean degree 8, "
+        "data": f"synthetic (seeded ring+chords graph, SURVEY §8d {'C5' if c5 else 'C3'})",
+        "config": {"workload": f"{'C5' if c5 else 'C3'} APSP routing build: {a.nodes // 1000}k-node undirected "
+                               "ring+chords graph, mean degree 8, "
                                "latency U[1,100] ms (integer us), loss 0 w.p. 0.8 else U(0,0.02); all nodes used; "
                                "source rows sharded across ranks (each rank keeps its row block; the optional RCCL "
                                "all-gather of the blocks is timed separately in apsp_detail.allgather_ms)",
@@ -553,9 +576,11 @@ def main():
         delivery = {
             "metric": "packets routed/sec per sim round", "value": round(total_pkts / t_round, 1),
             "unit": "packets/s", "higher_is_better": True, "ms_per_round": round(t_round * 1e3, 4),
-            "scaling": "weak", "dtype": "u64+f32+f64",
-            "config": {"workload": "C4 delivery round: 100k hosts on the C3 graph (node h mod 10k), 1M packets per "
-                                   "rank from the hosts it owns, dst uniform over all hosts != src, 20% zero-payload, "
+            "scaling": "strong" if c5 else "weak", "dtype": "u64+f32+f64",
+            "config": {"workload": f"{'C5' if c5 else 'C4'} delivery round: {a.hosts // 1000}k hosts on the "
+                                   f"{a.nodes // 1000}k-node graph (node h mod {a.nodes // 1000}k), {a.packets} "
+                                   "packets per rank from the hosts it owns, dst uniform over all hosts != src, "
+                                   "20% zero-payload, "
                                    "send_time U[1 ms round)" + ("; records exchanged by RCCL all-to-all to the "
                                                                 "destination's owner" if D.world > 1 else ""),
                        "hosts": a.hosts, "packets_per_rank": a.packets},

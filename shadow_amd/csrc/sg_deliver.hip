@@ -55,6 +55,7 @@ namespace sg {
 
 constexpr uint32_t NONE = ~0u;
 constexpr int SMALL_BUCKET = 32;
+constexpr uint32_t INBLOCK_RANK_MAX = 256;  // region path: rank sort up to this many entries per slot
 constexpr int SORT_BLOCK = 256;
 constexpr int SORT_CHUNK = 2048;  // elements sorted in LDS per chunk
 
@@ -783,14 +784,19 @@ __device__ __forceinline__ void slot_orders(uint64_t* Tt, uint64_t* Tk, uint32_t
                                             uint32_t* __restrict__ ki, uint32_t* __restrict__ order,
                                             uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
   static_assert(LDS || !INBLOCK, "in-block big-slot sort needs the LDS copy");
-  constexpr uint32_t MAX_BIG = SB_CAP<KK> / (SMALL_BUCKET + 1) + 1;
+  // In-block (region path), slots up to INBLOCK_RANK_MAX are rank-sorted too:
+  // a slot's rank sort runs in parallel with every other slot's, where each
+  // bitonic slot takes the whole block through log2(m)^2 / 2 barriers in turn
+  // (C5: about 100 entries per destination, 1.9 ms of bitonic slots per round).
+  constexpr uint32_t SMALL = INBLOCK ? INBLOCK_RANK_MAX : SMALL_BUCKET;
+  constexpr uint32_t MAX_BIG = SB_CAP<KK> / (SMALL + 1) + 1;
   __shared__ uint32_t n_big;
   __shared__ uint16_t bigs[INBLOCK ? MAX_BIG : 1];
   if (INBLOCK && threadIdx.x == 0) n_big = 0;
   __syncthreads();  // placement complete
   for (uint32_t j = threadIdx.x; j < nd; j += SBT_THREADS) {
     const uint32_t b = cnt[j], e = cnt[j + 1];
-    if (e - b > (uint32_t)SMALL_BUCKET) {
+    if (e - b > SMALL) {
       if (INBLOCK) {
         bigs[atomicAdd(&n_big, 1u)] = (uint16_t)j;
         continue;
@@ -810,7 +816,7 @@ __device__ __forceinline__ void slot_orders(uint64_t* Tt, uint64_t* Tk, uint32_t
   for (uint32_t p = threadIdx.x; p < ns; p += SBT_THREADS) {
     const uint32_t j = Ts[p];
     const uint32_t b = cnt[j], e = cnt[j + 1];
-    if (e - b > (uint32_t)SMALL_BUCKET) continue;  // sorted below / by k_sort_big
+    if (e - b > SMALL) continue;  // sorted below / by k_sort_big
     const uint64_t t = Tt[p], k = KK ? Tk[p] : (uint64_t)Ti[p];
     uint32_t rank = 0;
     for (uint32_t q = b; q < e; q++) rank += key_less(Tt[q], KK ? Tk[q] : (uint64_t)Ti[q], t, k);

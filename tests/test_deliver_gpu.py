@@ -143,6 +143,18 @@ def test_hot_destination_big_buckets(oracle, ctx):
     _assert_same(want, got, ost, gst)
 
 
+def test_slots_around_inblock_rank_limit(oracle, ctx):
+    """About 256 entries per destination: the region path rank-sorts the slots up
+    to INBLOCK_RANK_MAX (256) and bitonic-sorts the ones above it, in one block."""
+    lat, loss, hosts = _world(n_hosts=3000, seed=9)
+    start, end = T0 + 10**9, T0 + 10**9 + 10**6
+    pk = synth.make_packets(800000, hosts, start, end, seed=9)
+    want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, end, 2**63, 0)
+    sizes = np.diff(want["dst_offsets"])
+    assert (sizes > 256).any() and ((sizes > 32) & (sizes <= 256)).any()
+    _assert_same(want, got, ost, gst)
+
+
 @pytest.mark.parametrize("hot", [False, True])
 def test_scan_path_bucketing(oracle, ctx, monkeypatch, hot):
     """SG_BUCKET_REGION=0 forces the histogram + scan bucketing path (the
