@@ -77,14 +77,24 @@ class Dist:
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         if self.world != n_gpus:
             raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={self.world}")
+        # more ranks than GPUs (a rehearsal of the N-rank path on a smaller box) share devices
+        self.local %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(self.local)
         self.dist = None
         if self.world > 1:
             import torch.distributed as dist
 
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            # SG_BENCH_BACKEND=gloo: rehearse the N-rank path with more ranks than GPUs
+            # (RCCL refuses two ranks on one device); collectives are host-staged, so its
+            # timings are not measurements
+            self.backend = os.environ.get("SG_BENCH_BACKEND", "nccl")
+            if self.backend == "gloo":
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
             self.dist = dist
+        self.coll_dev = "cpu" if self.dist and self.backend == "gloo" else "cuda"
 
     def barrier(self):
         if self.dist:
@@ -93,14 +103,14 @@ class Dist:
     def max(self, x: float) -> float:
         if not self.dist:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.coll_dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
     def sum(self, x: float) -> float:
         if not self.dist:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.coll_dev)
         self.dist.all_reduce(t)
         return float(t.item())
 
@@ -439,6 +449,12 @@ def main():
         net.build_rows_device(used, r0, r1, my_lat.data_ptr(), my_loss.data_ptr(), True)
 
     def allgather():
+        if D.coll_dev == "cpu":  # gloo rehearsal: host-staged
+            for full, mine in ((full_lat, my_lat), (full_loss, my_loss)):
+                host = full.cpu()
+                D.dist.all_gather_into_tensor(host, mine.cpu())
+                full.copy_(host)
+            return
         D.dist.all_gather_into_tensor(full_lat, my_lat)
         D.dist.all_gather_into_tensor(full_loss, my_loss)
 

@@ -111,11 +111,20 @@ def gpu_bucket_phase(ctx, recv, n_records: int, local_dev, n_hosts: int, n_local
 # ---------------------------------------------------------------------------
 # Exchange
 # ---------------------------------------------------------------------------
+def _host_staged(dist, group, dev) -> bool:
+    """gloo moves host tensors only: device tensors go through host copies (the
+    multi-rank rehearsal on a box with fewer GPUs than ranks; RCCL needs none)."""
+    return dev.type != "cpu" and dist.get_backend(group) == "gloo"
+
+
 def all_to_all_records(send, send_counts: List[int], dist, group=None):
     """Counts exchange, then one all_to_all_single of the 32-B records."""
     import torch
 
     world = len(send_counts)
+    if _host_staged(dist, group, send.device):
+        recv, counts = all_to_all_records(send.cpu(), send_counts, dist, group)
+        return recv.to(send.device), counts
     dev = send.device
     sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
     rc = torch.empty(world, dtype=torch.int64, device=dev)
@@ -141,6 +150,10 @@ def gather_round_stats(n_delivered: int, min_deliver: int, min_lat: int, dist, g
     out = torch.empty(3 * world, dtype=torch.int64, device=device)
     if dist is None or world == 1:
         out.copy_(t)
+    elif _host_staged(dist, group, out.device):
+        host = out.cpu()
+        dist.all_gather_into_tensor(host, t.cpu(), group=group)
+        out.copy_(host)
     else:
         dist.all_gather_into_tensor(out, t, group=group)
     allv = out.cpu().numpy().view(np.uint64).reshape(world, 3)
