@@ -57,6 +57,7 @@ def parse_args():
     p.add_argument("--no-delivery", action="store_true")
     p.add_argument("--no-codel", action="store_true", help="skip the router CoDel leg")
     p.add_argument("--no-gml", action="store_true", help="skip the GML ingest leg")
+    p.add_argument("--no-c2", action="store_true", help="skip the C2 (1,200-node complete graph) leg")
     p.add_argument("--no-pack", action="store_true",
                    help="deliver from the two-array table (no packed path-key copy)")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
@@ -419,6 +420,63 @@ def gml_leg(a, NetworkGraph, synth):
                        "bytes": len(raw), "nodes": int(g["n"]), "edges": int(len(g["src"]))}}
 
 
+C2_NODES = 1200  # Tor-style complete graph, use_shortest_path: true
+
+
+def c2_leg(a, ctx, torch, NetworkGraph, synth, with_cpu):
+    """C2 (BASELINE configs[1]): a 1,200-node complete undirected GML graph (about 720k
+    edges), every node used -- GML parse on the host, then the routing-table build on
+    one GPU (shortest paths; the direct-path table beside it).  CPU baseline: the oracle's
+    Dijkstra on the box's CPU share; its rows double as a parity check of the GPU table."""
+    g = synth.complete_graph(C2_NODES, seed=1)
+    raw = synth.graph_to_gml(g).encode()
+    t0 = time.perf_counter()
+    net = NetworkGraph.parse(raw, ctx=ctx)
+    t_parse = time.perf_counter() - t0
+    n = net.n_nodes
+    used = np.arange(n, dtype=np.uint32)
+    lat = torch.empty(n * n, dtype=torch.int64, device="cuda")
+    loss = torch.empty(n * n, dtype=torch.float32, device="cuda")
+
+    def per_build(shortest):
+        for _ in range(a.warmup):
+            net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), shortest)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), shortest)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / a.steps
+
+    t_direct = per_build(False)
+    t_build = per_build(True)  # the table left in lat/loss is the shortest-path one
+    ctx.enable_timers(True)
+    net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
+    relax_ms, launches, _ = ctx.read_timer("relax")
+    ctx.enable_timers(False)
+    leg = {"metric": "APSP routing build (s) @1.2k-node complete graph", "unit": "s", "value": round(t_build, 6),
+           "higher_is_better": False, "direct_paths_s": round(t_direct, 6), "gml_parse_s": round(t_parse, 4),
+           "relax_ms": round(relax_ms, 4), "relax_launches": launches,
+           "config": {"workload": f"C2: {n}-node complete undirected graph from GML ({len(raw)} bytes), latency "
+                                  "U[1,300] ms, self-loops U[1,10] ms, loss 0 w.p. 0.8 else U(0,0.02); every node "
+                                  "used; use_shortest_path true", "nodes": n, "edges": int(len(g["src"]))}}
+    if with_cpu:
+        from oracle import oracle as O  # the checker, timed as the CPU baseline
+
+        th = min(16, os.cpu_count() or 1)
+        t0 = time.perf_counter()
+        rc, olat, oloss, _ = O.shortest_paths(n, g["src"], g["dst"], g["lat"], g["loss"], False, used, threads=th)
+        tc = time.perf_counter() - t0
+        assert rc == 0
+        leg["cpu_baseline"] = {"value": round(tc, 4), "unit": "s", "cores": th, "kind": "port",
+                               "sample": f"all {n} sources (binary-heap Dijkstra, dense output), {th} threads"}
+        leg["speedup_vs_cpu"] = round(tc / t_build, 1)
+        leg["parity_vs_cpu"] = bool(
+            np.array_equal(lat.cpu().numpy().view(np.uint64).reshape(n, n), olat)
+            and np.array_equal(loss.cpu().numpy().view(np.uint32).reshape(n, n), oloss.view(np.uint32)))
+    return leg
+
+
 def main():
     a = parse_args()
     D = Dist(a.gpus)
@@ -525,6 +583,8 @@ def main():
         result["apsp_detail"]["speedup_vs_cpu"] = round(cpu["value"] / t_build, 1)
     if D.rank == 0 and not a.no_gml:
         result["gml_ingest"] = gml_leg(a, NetworkGraph, synth)
+    if D.rank == 0 and not a.no_c2:
+        result["c2"] = c2_leg(a, ctx, torch, NetworkGraph, synth, D.world == 1 and not a.no_cpu)
 
     # ---------------- delivery round (C4) ----------------
     if not a.no_delivery:

@@ -240,17 +240,28 @@ __global__ void __launch_bounds__(RELAX_THREADS)
   const uint32_t nwc = (n + NPW - 1) / NPW;
   const uint32_t n_act = alist[0];
   const uint32_t nbx = n_act > x ? (n_act - x + 7) / 8 : 0;
-  const uint32_t items = nbx * nwc;
+  constexpr uint32_t nseg = 1;  // (segments: k_relax_w2 only)
+  // nseg > 1 (dense graphs): an item is one of nseg segments of a node chunk's
+  // in-arcs, so a chunk's thousands of arcs are relaxed by nseg waves at once;
+  // the segments' waves share rows and merge by 64-bit atomic min (the packed
+  // key's order is the PathProperties order)
+  const uint32_t items = nbx * nwc * nseg;
   const uint32_t stride = (gridDim.x >> 3) * WAVES;
   uint32_t n_rel = 0, flagged = ~0u;
   for (uint32_t it = (blockIdx.x >> 3) * WAVES + w; it < items; it += stride) {
-    const uint32_t b = alist[1 + x + 8 * (it / nwc)];
-    const uint32_t vw = (it % nwc) * NPW;
+    const uint32_t b = alist[1 + x + 8 * (it / (nwc * nseg))];
+    const uint32_t ci = it % (nwc * nseg);
+    const uint32_t vw = (ci / nseg) * NPW, seg = ci % nseg;
     const uint32_t vw1 = min(vw + NPW, n);
     uint64_t* Db = D + (size_t)b * n * B;
     const uint32_t* St = stamp + (size_t)b * n;
     const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(Db, 0, (int)(n * B * 8u), 0x00020000);
-    const uint32_t a0 = in_off[vw], a1 = in_off[vw1];
+    uint32_t a0 = in_off[vw], a1 = in_off[vw1];
+    if (nseg > 1) {
+      const uint32_t per = (a1 - a0 + nseg - 1) / nseg;
+      a0 = min(a1, a0 + seg * per);
+      a1 = min(a1, a0 + per);
+    }
     uint32_t n_cand = 0;
     uint32_t run_slot = 0;  // per row group: records of one destination form a run
     uint64_t run = KEY_INF;
@@ -378,7 +389,7 @@ template <int B, int NPW, int K, int GROUP, bool FRONT, bool COUNT>
 __global__ void __launch_bounds__(RELAX_THREADS)
     k_relax_w2(const uint32_t* __restrict__ in_off, const uint4* __restrict__ in_rec, uint64_t* __restrict__ D,
                uint32_t n, const uint32_t* __restrict__ alist, uint32_t* __restrict__ changed,
-               uint32_t* __restrict__ stamp, uint32_t pass, unsigned long long* __restrict__ work) {
+               uint32_t* __restrict__ stamp, uint32_t pass, unsigned long long* __restrict__ work, uint32_t nseg) {
   static_assert(B == 64 || B == 32, "B = 64 or 32");
   constexpr int WAVES = RELAX_THREADS / 64;
   constexpr int STG_W = 64 * K;
@@ -398,17 +409,27 @@ __global__ void __launch_bounds__(RELAX_THREADS)
   const uint32_t nwc = (n + NPW - 1) / NPW;
   const uint32_t n_act = alist[0];
   const uint32_t nbx = n_act > x ? (n_act - x + 7) / 8 : 0;
-  const uint32_t items = nbx * nwc;
+  // nseg > 1 (dense graphs): an item is one of nseg segments of a node chunk's
+  // in-arcs, so a chunk's thousands of arcs are relaxed by nseg waves at once;
+  // the segments' waves share rows and merge by 64-bit atomic min (the packed
+  // key's order is the PathProperties order)
+  const uint32_t items = nbx * nwc * nseg;
   const uint32_t stride = (gridDim.x >> 3) * WAVES;
   uint32_t n_rel = 0, flagged = ~0u;
   for (uint32_t it = (blockIdx.x >> 3) * WAVES + w; it < items; it += stride) {
-    const uint32_t b = alist[1 + x + 8 * (it / nwc)];
-    const uint32_t vw = (it % nwc) * NPW;
+    const uint32_t b = alist[1 + x + 8 * (it / (nwc * nseg))];
+    const uint32_t ci = it % (nwc * nseg);
+    const uint32_t vw = (ci / nseg) * NPW, seg = ci % nseg;
     const uint32_t vw1 = min(vw + NPW, n);
     uint64_t* Db = D + (size_t)b * n * B;
     const uint32_t* St = stamp + (size_t)b * n;
     const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(Db, 0, (int)(n * B * 8u), 0x00020000);
-    const uint32_t a0 = in_off[vw], a1 = in_off[vw1];
+    uint32_t a0 = in_off[vw], a1 = in_off[vw1];
+    if (nseg > 1) {
+      const uint32_t per = (a1 - a0 + nseg - 1) / nseg;
+      a0 = min(a1, a0 + seg * per);
+      a1 = min(a1, a0 + per);
+    }
     uint32_t n_cand = 0;
     uint32_t run_slot = 0;
     uint64_t run0 = KEY_INF, run1 = KEY_INF;
@@ -497,9 +518,13 @@ __global__ void __launch_bounds__(RELAX_THREADS)
 #pragma unroll
     for (int i = 0; i < NPW / G; i++) {
       const uint32_t v = vw + i * G + gh;
-      const bool c0 = v < vw1 && nb0[i] < cur0[i];
-      const bool c1 = v < vw1 && nb1[i] < cur1[i];
-      if (c0 || c1) {
+      bool c0 = v < vw1 && nb0[i] < cur0[i];
+      bool c1 = v < vw1 && nb1[i] < cur1[i];
+      if (nseg > 1) {  // other segments' waves write this row too
+        unsigned long long* k = (unsigned long long*)&Db[(size_t)v * B + 2 * sl];
+        if (c0) c0 = nb0[i] < atomicMin(k, (unsigned long long)nb0[i]);
+        if (c1) c1 = nb1[i] < atomicMin(k + 1, (unsigned long long)nb1[i]);
+      } else if (c0 || c1) {
         typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
         *(u64x2*)&Db[(size_t)v * B + 2 * sl] = (u64x2){c0 ? nb0[i] : cur0[i], c1 ? nb1[i] : cur1[i]};
       }
@@ -949,6 +974,12 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
   // chunk.  A pass issued after its batch converged finds it off the active list.
   const uint32_t chunk = (uint32_t)std::max(1, env_int("SG_APSP_PASS_CHUNK", 4));
   const bool trace = env_int("SG_APSP_TRACE", 0) != 0;  // per-pass diagnostics on stderr
+  // in-arc segments per relaxation item (k_relax_w2): one per ~SEG_ARCS arcs of a
+  // node chunk, so dense graphs (C2: ~4800 arcs per chunk) fill the chip
+  constexpr uint32_t SEG_ARCS = 1200;  // C2 (1,200-node complete graph): 4 segments, measured best (of 1-16)
+  const double chunk_arcs = n ? (double)net->n_arcs * NPW / n : 0.0;
+  const uint32_t nseg = SPL == 2 ? (uint32_t)std::min(16, std::max(1, env_int("SG_APSP_SEG",
+                                       (int)std::lround(chunk_arcs / SEG_ARCS)))) : 1u;
   int out_tpb = env_int("SG_APSP_OUT_TPB", 1);  // column tiles per write-out block: 1 | 2 | 4 (1 measured best)
   out_tpb = out_tpb == 4 ? 4 : out_tpb == 2 ? 2 : 1;
   std::vector<uint32_t> h_sat(group);
@@ -991,11 +1022,13 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
           TimedLaunch tl(ctx, "relax", 0.0);
           if constexpr (SPL == 2) {
             if (work)
-              hipLaunchKernelGGL((k_relax_w2<B, NPW, STG / 64, GR, FRONT, true>), dim3(grid), dim3(RELAX_THREADS), 0,
-                                 st, net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
+              hipLaunchKernelGGL((k_relax_w2<B, NPW, STG / 64, GR, FRONT, true>), dim3(grid * nseg),
+                                 dim3(RELAX_THREADS), 0, st, net->in_off, net->in_rec, D, n, alist, changed, stamp,
+                                 pass, work, nseg);
             else
-              hipLaunchKernelGGL((k_relax_w2<B, NPW, STG / 64, GR, FRONT, false>), dim3(grid), dim3(RELAX_THREADS), 0,
-                                 st, net->in_off, net->in_rec, D, n, alist, changed, stamp, pass, work);
+              hipLaunchKernelGGL((k_relax_w2<B, NPW, STG / 64, GR, FRONT, false>), dim3(grid * nseg),
+                                 dim3(RELAX_THREADS), 0, st, net->in_off, net->in_rec, D, n, alist, changed, stamp,
+                                 pass, work, nseg);
           } else {
             if (work)
               hipLaunchKernelGGL((k_relax_w<B, NPW, STG / 64, GR, FRONT, true>), dim3(grid), dim3(RELAX_THREADS), 0,

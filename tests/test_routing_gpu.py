@@ -190,7 +190,8 @@ def test_empty_used(ctx):
                                  {"SG_APSP_NPW": "16", "SG_APSP_STAGE": "128", "SG_APSP_GROUP": "4"},
                                  {"SG_APSP_B": "32", "SG_APSP_SPL": "1", "SG_APSP_NPW": "16"}, {"SG_APSP_PASS_CHUNK": "1"},
                                  {"SG_APSP_OUT_TPB": "1"}, {"SG_APSP_OUT_TPB": "4"},
-                                 {"SG_APSP_OUT_TPB": "4", "SG_APSP_B": "32"}])
+                                 {"SG_APSP_OUT_TPB": "4", "SG_APSP_B": "32"}, {"SG_APSP_SEG": "3"},
+                                 {"SG_APSP_SEG": "4", "SG_APSP_B": "32"}, {"SG_APSP_SEG": "16", "SG_APSP_PASS_CHUNK": "1"}])
 def test_kernel_variants_bit_exact(oracle, ctx, monkeypatch, env):
     """Every A/B variant of the relaxation kernel (slab width, frontier, item size) is exact."""
     for k, v in env.items():
@@ -198,6 +199,24 @@ def test_kernel_variants_bit_exact(oracle, ctx, monkeypatch, env):
     g = synth.ring_chords_graph(900, 7.0, seed=21, parallel=0.03)
     used = np.random.default_rng(21).permutation(900)[:612].astype(np.uint32)
     _check(oracle, g, used, ctx)
+
+
+def test_c2_scale_from_gml(oracle, ctx):
+    """C2: a 1,200-node complete undirected graph (about 720k edges)
+    parsed from GML text, every node used.  The full shortest-path table is
+    bit-exact against the oracle, and so is the direct-path table
+    (use_shortest_path: false)."""
+    g = synth.complete_graph(1200, seed=2)  # dense: the relaxation splits chunks into ~9 arc segments
+    net = NetworkGraph.parse(synth.graph_to_gml(g), ctx=ctx)
+    assert net.n_nodes == 1200 and len(net.edge_src) == len(g["src"])
+    used = np.arange(1200, dtype=np.uint32)
+    for fn, ofn in ((net.compute_shortest_paths, oracle.shortest_paths), (net.get_direct_paths, oracle.direct_paths)):
+        t = fn(used)
+        kw = dict(threads=8) if ofn is oracle.shortest_paths else {}
+        rc, olat, oloss, _ = ofn(g["n"], g["src"], g["dst"], g["lat"], g["loss"], False, used, **kw)
+        assert rc == 0
+        assert np.array_equal(t.latency_ns, olat)
+        assert np.array_equal(t.packet_loss.view(np.uint32), oloss.view(np.uint32))
 
 
 def test_c5_scale_row_samples(oracle, ctx):
