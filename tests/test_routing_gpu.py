@@ -201,6 +201,24 @@ def test_kernel_variants_bit_exact(oracle, ctx, monkeypatch, env):
     _check(oracle, g, used, ctx)
 
 
+@pytest.mark.parametrize("nseg", ["2", "5"])
+def test_arc_segments_directed_dense(oracle, ctx, monkeypatch, nseg):
+    """Arc segments (atomic-min flush) on a directed, nearly complete graph with
+    parallel arcs, used-subset rows."""
+    monkeypatch.setenv("SG_APSP_SEG", nseg)
+    g = synth.complete_graph(160, seed=11)
+    rng = np.random.default_rng(11)
+    extra = rng.integers(0, 160, (4000, 2)).astype(np.uint32)
+    extra = extra[extra[:, 0] != extra[:, 1]]
+    gd = dict(n=160, directed=True,
+              src=np.concatenate([g["src"], g["dst"][160:], extra[:, 0]]),
+              dst=np.concatenate([g["dst"], g["src"][160:], extra[:, 1]]),
+              lat=np.concatenate([g["lat"], g["lat"][160:][::-1], rng.integers(1, 400, len(extra)).astype(np.uint64) * 10**6]),
+              loss=np.concatenate([g["loss"], g["loss"][160:][::-1], np.full(len(extra), np.float32(0.01))]))
+    used = rng.permutation(160)[:131].astype(np.uint32)
+    _check(oracle, gd, used, ctx)
+
+
 def test_c2_scale_from_gml(oracle, ctx):
     """C2: a 1,200-node complete undirected graph (about 720k edges)
     parsed from GML text, every node used.  The full shortest-path table is
