@@ -56,6 +56,11 @@ __device__ __forceinline__ uint64_t control_law(uint64_t t, uint64_t count) {
 // cached in registers (hp/ht/hl, valid while head < tail): a pop consumes the
 // cache and issues the load of the next element right away, so its latency
 // hides behind the events in between instead of stalling the next pop.
+// LDS views (address space 3: ds_* instructions, not flat ones)
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+typedef __attribute__((address_space(3))) const uint64_t lds_u64;
+typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+
 struct Q {
   uint8_t flags;
   uint64_t iend, dnext, cur, prev, bytes;
@@ -65,6 +70,26 @@ struct Q {
   uint32_t last_len;  // length of the element pop_front returned last
   uint4* ring;
   uint32_t mask;
+  // Staged window: the elements this host pushed since begin_window() are the
+  // push events of its staged range, in order, so the head element is read
+  // from LDS there instead of from the ring in HBM (the ring is still written:
+  // what is left at the end of the window lives on in HBM).
+  bool win;
+  uint32_t t0, wb, cn, ci;  // tail at window start; host's first staged event; pushes located; last one's index
+  lds_u32 *wp, *wl;
+  lds_u64* wt;
+  lds_u8* wk;  // event kinds (push = SG_CODEL_PUSH), or null: every event is a push
+  __device__ void begin_window(lds_u32* p, lds_u32* l, lds_u64* t, lds_u8* k, uint32_t first) {
+    win = true;
+    t0 = tail;
+    wb = first;
+    cn = 0;
+    ci = first - 1;
+    wp = p;
+    wl = l;
+    wt = t;
+    wk = k;
+  }
   uint8_t* status;
   uint32_t n_status;
   uint64_t dropped;
@@ -102,13 +127,27 @@ struct Q {
     return true;
   }
   __device__ void load_head() {
-    if (head != tail) {
-      const uint32_t slot = head & mask;
-      const uint4 r = ring[slot];
-      hp = r.x;
-      hl = r.y;
-      ht = ((uint64_t)r.w << 32) | r.z;
+    if (head == tail) return;
+    const uint32_t j = head - t0;  // the j-th push of the window (modular)
+    if (win && j < tail - t0) {
+      uint32_t k = wb + j;
+      if (wk) {  // locate the j-th push event (the head only moves forward)
+        while (cn <= j) {
+          ci++;
+          cn += wk[ci] == SG_CODEL_PUSH;
+        }
+        k = ci;
+      }
+      hp = wp[k];
+      hl = wl[k];
+      ht = wt[k];
+      return;
     }
+    const uint32_t slot = head & mask;
+    const uint4 r = ring[slot];
+    hp = r.x;
+    hl = r.y;
+    ht = ((uint64_t)r.w << 32) | r.z;
   }
   __device__ bool should_drop(uint64_t now) const { return (flags & F_DNEXT) && now >= dnext; }
   __device__ bool dropping_recently(uint64_t now) const {
@@ -196,6 +235,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
   __shared__ uint32_t s_p[CD_CHUNK];  // packet -> pop result
   __shared__ uint32_t s_l[CD_CHUNK];
   __shared__ uint8_t s_k[CD_CHUNK];
+  __shared__ uint32_t s_r[CD_CHUNK];  // pop results (s_p keeps the pushed packets for the window)
   const uint32_t h0 = blockIdx.x * CD_HOSTS, t = threadIdx.x;
   const uint32_t p0 = min(a.host_off[min(h0, a.H)], a.E);
   const uint32_t p1 = max(min(a.host_off[min(h0 + CD_HOSTS, a.H)], a.E), p0);
@@ -232,23 +272,45 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
     __syncthreads();
     if (walker) {  // 2. each host's events in order
       const uint32_t b = max(hb, c0), e = min(he, c1);
+      q.begin_window((lds_u32*)s_p, (lds_u32*)s_l, (lds_u64*)s_t, (lds_u8*)s_k, b - c0);
+      // the next event's fields are read while this one is processed (the
+      // walker's time is its chain of dependent LDS reads and queue updates)
+      uint8_t nk = 0;
+      uint64_t nt = 0;
+      uint32_t np = 0, nl = 0;
+      if (b < e) {
+        nk = s_k[b - c0];
+        nt = s_t[b - c0];
+        np = s_p[b - c0];
+        nl = s_l[b - c0];
+      }
       for (uint32_t i = b; i < e; i++) {
         const uint32_t k = i - c0;
+        const uint8_t kind = nk;
+        const uint64_t now = nt;
+        const uint32_t pkt = np, len = nl;
+        if (i + 1 < e) {
+          nk = s_k[k + 1];
+          nt = s_t[k + 1];
+          np = s_p[k + 1];
+          nl = s_l[k + 1];
+        }
         uint32_t r = CD_NONE;
-        if (s_k[k] == SG_CODEL_PUSH) {
-          q.push(s_p[k], s_t[k], s_l[k]);
+        if (kind == SG_CODEL_PUSH) {
+          q.push(pkt, now, len);
         } else {
-          r = q.pop(s_t[k]);
+          r = q.pop(now);
           if (r != CD_NONE) {
             if (r < q.n_status) q.status[r] = SG_CODEL_DEQUEUED;
             else q.err |= E_PKT;
           }
         }
-        s_p[k] = r;
+        s_r[k] = r;
       }
+      q.win = false;  // the next chunk's staging overwrites the window
     }
     __syncthreads();
-    for (uint32_t i = c0 + t; i < c1; i += CD_THREADS) a.pop_result[i] = s_p[i - c0];  // 3. coalesced results
+    for (uint32_t i = c0 + t; i < c1; i += CD_THREADS) a.pop_result[i] = s_r[i - c0];  // 3. coalesced results
     __syncthreads();
   }
   unsigned long long dropped = 0, err = 0;
@@ -456,12 +518,22 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
     __syncthreads();
     if (walker) {
       const uint32_t b = max(hb, c0), e = min(he, c1);
+      q.win = false;  // the tasks first run by this chunk pop the previous chunk's elements from HBM
+      q.begin_window((lds_u32*)s_p, (lds_u32*)s_l, (lds_u64*)s_t, nullptr, b - c0);
+      uint64_t nt = b < e ? s_t[b - c0] : 0;  // the next arrival's fields, read ahead
+      uint32_t np = b < e ? s_p[b - c0] : 0, nl = b < e ? s_l[b - c0] : 0;
       for (uint32_t i = b; i < e; i++) {
         const uint32_t k = i - c0;
-        const uint64_t now = s_t[k];
+        const uint64_t now = nt;
+        const uint32_t pkt = np, len = nl;
+        if (i + 1 < e) {
+          nt = s_t[k + 1];
+          np = s_p[k + 1];
+          nl = s_l[k + 1];
+        }
         if (now >= ia.window_end) q.err |= E_WINDOW;
         while (due(now)) relay_task(q, r, r.tt, ia.bootstrap_end, ia.sim_end, ctr_inc, ia.fwd_time);
-        q.push(s_p[k], now, s_l[k]);  // Router::route_incoming_packet
+        q.push(pkt, now, len);  // Router::route_incoming_packet
         if (!(r.rf & R_PENDING)) {    // notify_router_has_packets: Idle -> forward_later(ZERO)
           ctr_inc++;
           r.rf |= R_PENDING;
