@@ -546,6 +546,11 @@ def main():
                 "avg_launch_ms": round(avg_launch_s * 1e3, 4), "launches_per_build": relax_launches,
                 "lane_relaxations_per_launch": relax_per_launch,
                 "valu_frac_pmc": pm.get("valu_frac")}
+    if pm.get("hbm_bytes_per_launch") and relax_launches:
+        # the same launches against HBM: PMC bytes per launch over the launch time
+        hbm = pm["hbm_bytes_per_launch"] / avg_launch_s / 1e9
+        roofline["hbm_view"] = {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": round(hbm / HBM_PEAK_GBS, 4)}
 
     cpu = None
     if D.rank == 0 and D.world == 1 and not a.no_cpu:
