@@ -130,12 +130,40 @@ def all_to_all_records(send, send_counts: List[int], dist, group=None):
     rc = torch.empty(world, dtype=torch.int64, device=dev)
     dist.all_to_all_single(rc, sc, group=group)
     recv_counts = [int(x) for x in rc.cpu()]
+    return _records_all_to_all(send, send_counts, recv_counts, dist, group), recv_counts
+
+
+def exchange_round(send, send_counts: List[int], stats, rank: int, dist, group=None):
+    """The round's one host round trip: an all-gather of every rank's row
+    [delivered, min deliver time, min used latency, counts to each rank] (u64),
+    so the round scalars ride with the counts exchange, then the records'
+    all_to_all_single.  Returns (recv, recv_counts, global stats)."""
+    import torch
+
+    world = len(send_counts)
+    if _host_staged(dist, group, send.device):
+        recv, counts, g = exchange_round(send.cpu(), send_counts, stats, rank, dist, group)
+        return recv.to(send.device), counts, g
+    dev = send.device
+    mine = np.array([*stats, *send_counts], dtype=np.uint64).view(np.int64)
+    out = torch.empty(world * (3 + world), dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(out, torch.from_numpy(mine.copy()).to(dev), group=group)
+    allv = out.cpu().numpy().view(np.uint64).reshape(world, 3 + world)
+    recv_counts = [int(allv[r, 3 + rank]) for r in range(world)]
+    g = (int(allv[:, 0].sum()), int(allv[:, 1].min()), int(allv[:, 2].min()))
+    return _records_all_to_all(send, send_counts, recv_counts, dist, group), recv_counts, g
+
+
+def _records_all_to_all(send, send_counts: List[int], recv_counts: List[int], dist, group):
+    import torch
+
+    dev = send.device
     n_recv = sum(recv_counts)
     recv = torch.empty((max(n_recv, 1), 4), dtype=torch.int64, device=dev)
     n_send = sum(send_counts)
     dist.all_to_all_single(recv[:n_recv], send[:n_send], output_split_sizes=recv_counts,
                            input_split_sizes=list(send_counts), group=group)
-    return recv[:n_recv], recv_counts
+    return recv[:n_recv]
 
 
 def gather_round_stats(n_delivered: int, min_deliver: int, min_lat: int, dist, group=None, device="cuda"):
@@ -173,7 +201,7 @@ class ShardedDelivery:
         self.rank, self.world, self.dist, self.group = rank, world, dist, group
         self.source_fn = source_fn or gpu_source_phase
         self.bucket_fn = bucket_fn or gpu_bucket_phase
-        self.exchange_fn = exchange_fn or (lambda send, counts: all_to_all_records(send, counts, dist, group))
+        self.exchange_fn = exchange_fn  # None: exchange_round (counts and round scalars in one all-gather)
         import torch
 
         self.owner_dev = torch.from_numpy(partition.owner.view(np.int32)).to(device)
@@ -185,10 +213,14 @@ class ShardedDelivery:
     def round(self, packets, round_end_ns: int, sim_end_ns: int, bootstrap_end_ns: int = 0):
         src = self.source_fn(self.ctx, self.hosts, self.table, packets, round_end_ns, sim_end_ns, bootstrap_end_ns,
                              self.owner_dev, self.world)
-        recv, recv_counts = self.exchange_fn(src.send, src.send_counts)
+        stats = (int(src.n_delivered), int(src.min_deliver_time_ns), int(src.min_used_latency_ns))
+        if self.exchange_fn is None:
+            recv, recv_counts, self.last_stats = exchange_round(src.send, src.send_counts, stats, self.rank,
+                                                                self.dist, self.group)
+        else:
+            recv, recv_counts = self.exchange_fn(src.send, src.send_counts)
+            self.last_stats = gather_round_stats(*stats, self.dist, self.group, self.device)
         order, offsets = self.bucket_fn(self.ctx, recv, int(sum(recv_counts)), self.local_dev,
                                         len(self.part.local), self.part.n_local(self.rank))
-        self.last_stats = gather_round_stats(int(src.n_delivered), int(src.min_deliver_time_ns),
-                                             int(src.min_used_latency_ns), self.dist, self.group, self.device)
         self.last = (recv, order, offsets)  # this rank's destination buckets of the round
         return src, recv, recv_counts, order, offsets
