@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 2
+#define SG_ABI_VERSION 3
 
 typedef enum sg_status {
   SG_OK = 0,
@@ -49,7 +49,9 @@ typedef enum sg_status {
   SG_ERR_PARSE = 7,         /* NetworkGraph::parse / ShadowEdge::try_from (graph/mod.rs:72-181) */
   SG_ERR_UNSORTED = 8,      /* sg_deliver_round: packets not grouped by ascending source host */
   SG_ERR_DUPLICATE_IP = 9,  /* two hosts with one address (IpAssignment::assign_ip, graph/mod.rs:383-394) */
-  SG_ERR_CAPACITY = 10      /* a CoDel queue outgrew its ring (sg_codel_create ring_cap) */
+  SG_ERR_CAPACITY = 10,     /* a CoDel queue outgrew its ring (sg_codel_create ring_cap) */
+  SG_ERR_TIME_OVERFLOW = 11 /* send time + latency past EMUTIME_MAX: EmulatedTime + SimulationTime
+                               panics in the reference (emulated_time.rs:121-126, worker.rs:381) */
 } sg_status;
 
 typedef struct sg_ctx sg_ctx;     /* one HIP device + stream + workspace */
@@ -147,6 +149,65 @@ int32_t sg_routing_build(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32
 int32_t sg_routing_min_latency(sg_ctx* ctx, const uint64_t* d_latency_ns, size_t count,
                                uint64_t* out_min);
 
+/* ---- host-side dense RoutingInfo (graph/mod.rs:432-481) ------------------
+ * RoutingInfo<u32> keyed by GML node id, as generate_routing_info builds it
+ * (sim_config.rs:411-448), stored dense: row-major latency / loss arrays in
+ * pinned host memory owned by the object and an id -> row map.  It replaces the
+ * reference's two n_used^2 HashMaps (compute_shortest_paths', graph/mod.rs:190-208,
+ * and the id remap's, sim_config.rs:423-445) and answers RoutingInfo::path and
+ * the WorkerShared lookups with array reads.  Lookups are read-only and safe
+ * from any number of threads; packet counters are atomic.                    */
+typedef struct sg_routing_info sg_routing_info;
+/* node_ids: the used GML node ids (the table's row / column order).  Allocates
+ * the n_used^2 table (pinned when a HIP device is present).  SG_ERR_INVALID_ARG
+ * for a duplicate id. */
+int32_t sg_routing_info_create(uint32_t n_used, const uint32_t* node_ids, sg_routing_info** out);
+void sg_routing_info_destroy(sg_routing_info* ri);
+/* Build the whole table: nodes[i] = the petgraph index of node_ids[i]
+ * (NetworkGraph::node_id_to_index, graph/mod.rs:126-128).  Results and errors
+ * are sg_routing_build's over all rows; row blocks are built on the device and
+ * copied into the object while the next block builds.  Also computes
+ * get_smallest_latency_ns. */
+int32_t sg_routing_info_fill(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32_t flags, sg_routing_info* ri);
+/* Rows [row_begin, row_end) from host arrays (e.g. row shards gathered from
+ * other ranks' sg_routing_build). */
+int32_t sg_routing_info_set_rows(sg_routing_info* ri, uint32_t row_begin, uint32_t row_end,
+                                 const uint64_t* latency_ns, const float* packet_loss);
+/* Zero-copy view: cell (i, j) = path(node_ids[i] -> node_ids[j]). */
+typedef struct sg_routing_view {
+  uint32_t n;
+  const uint32_t* node_ids;
+  const uint64_t* latency_ns;
+  const float* packet_loss;
+  uint32_t pinned;
+} sg_routing_view;
+int32_t sg_routing_info_view(const sg_routing_info* ri, sg_routing_view* out);
+/* Row of a GML node id (SG_ERR_INVALID_ARG if absent). */
+int32_t sg_routing_info_index(const sg_routing_info* ri, uint32_t node_id, uint32_t* row);
+/* RoutingInfo::path(start, end) (graph/mod.rs:448-450): 1 = Some (outputs
+ * written when non-NULL), 0 = None. */
+int32_t sg_routing_info_path(const sg_routing_info* ri, uint32_t start, uint32_t end, uint64_t* latency_ns,
+                             float* packet_loss);
+/* RoutingInfo::get_smallest_latency_ns (graph/mod.rs:478-480): 1 = Some, 0 = None. */
+int32_t sg_routing_info_smallest_latency(const sg_routing_info* ri, uint64_t* out);
+/* RoutingInfo::increment_packet_count (graph/mod.rs:453-460): saturating, thread
+ * safe; SG_ERR_INVALID_ARG for an unknown pair (its caller unwraps, worker.rs:538-542). */
+int32_t sg_routing_info_increment_packet_count(sg_routing_info* ri, uint32_t start, uint32_t end);
+uint64_t sg_routing_info_packet_count(const sg_routing_info* ri, uint32_t start, uint32_t end);
+/* IpAssignment (graph/mod.rs:354-430): the assigned addresses (host byte order,
+ * u32::from(Ipv4Addr)) and their GML node ids; SG_ERR_DUPLICATE_IP for a repeat. */
+int32_t sg_routing_info_set_addresses(sg_routing_info* ri, uint32_t n_addrs, const uint32_t* ipv4,
+                                      const uint32_t* node_id);
+/* WorkerShared::latency / reliability / is_routable (worker.rs:517-555) as the C
+ * exports worker_getLatency / worker_isRoutable take them (worker.rs:651-684):
+ * addresses in network byte order.  latency / reliability return SG_OK, or
+ * SG_ERR_INVALID_ARG where the reference's Option is None (worker_getLatency
+ * unwraps it: a panic).  reliability = 1f32 - loss.  is_routable: 1 when both
+ * addresses are assigned (the graph is connected), else 0. */
+int32_t sg_worker_get_latency(const sg_routing_info* ri, uint32_t src_be, uint32_t dst_be, uint64_t* latency_ns);
+int32_t sg_worker_get_reliability(const sg_routing_info* ri, uint32_t src_be, uint32_t dst_be, float* reliability);
+int32_t sg_worker_is_routable(const sg_routing_info* ri, uint32_t src_be, uint32_t dst_be);
+
 /* ---- packet delivery ------------------------------------------------------ */
 /*
  * Host table.  host_ipv4[h] = the host's address (host byte order, as
@@ -229,7 +290,12 @@ typedef struct sg_round_stats {
 } sg_round_stats;
 
 /* Run one round.  Updates the hosts' RNG streams and event counters on the
- * device.  `stats` (host) may be NULL for a fully asynchronous call. */
+ * device.  `stats` (host) may be NULL for a fully asynchronous call.
+ * A batch that is not grouped by ascending source host (SG_ERR_UNSORTED), names
+ * a host out of range, or comes from a host whose route row is outside the
+ * table shard (SG_ERR_INVALID_ARG) is rejected whole: no host's RNG stream or
+ * event counter changes and no output is written.  SG_ERR_TIME_OVERFLOW (the
+ * reference panics) leaves the hosts' state undefined. */
 int32_t sg_deliver_round(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table,
                          const sg_round* round, const sg_packets* packets, sg_deliveries* out,
                          sg_round_stats* stats);

@@ -190,6 +190,8 @@ def deliver_round(round_end, sim_end, bootstrap_end, src_host, dst_ip, payload_l
                                         v(send_time), H, v(host_ip), v(host_row), ncols, v(tab_lat), v(tab_loss),
                                         v(rng), v(event_ctr), v(status), v(deliver), v(eid), v(order), v(offs),
                                         C.byref(mind), C.byref(minl), int(threads))
+        if nd == -2:
+            raise OverflowError("send time + latency overflows EmulatedTime (emulated_time.rs:121-126 panics)")
         if nd < 0:
             raise ValueError("sgo_deliver_round_mt: bad argument")
         return dict(status=status, deliver_time=deliver, event_id=eid, dst_order=order[:nd],
@@ -201,6 +203,8 @@ def deliver_round(round_end, sim_end, bootstrap_end, src_host, dst_ip, payload_l
                                  _p(event_ctr, C.c_uint64), _p(status, C.c_uint8), _p(deliver, C.c_uint64),
                                  _p(eid, C.c_uint64), _p(order, C.c_uint32), _p(offs, C.c_uint32),
                                  C.byref(mind), C.byref(minl))
+    if nd == -2:
+        raise OverflowError("send time + latency overflows EmulatedTime (emulated_time.rs:121-126 panics)")
     if nd < 0:
         raise ValueError("sgo_deliver_round: bad argument")
     return dict(status=status, deliver_time=deliver, event_id=eid, dst_order=order[:nd],

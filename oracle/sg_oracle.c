@@ -544,7 +544,9 @@ static int cmp_ord(const void* a, const void* b) {
  * EventQueue pops them: (time, src_host_id, src_host_event_id); dst_offsets
  * (n_hosts+1); min_deliver = min next-event time (worker.rs:388), min_lat =
  * min used latency (worker.rs:372); UINT64_MAX when nothing was delivered.
- * Returns the number of delivered packets, or -1 on a bad argument.
+ * Returns the number of delivered packets, -1 on a bad argument, or -2 when a
+ * delivered packet's send time + latency overflows EmulatedTime (the reference
+ * panics).
  */
 int64_t sgo_deliver_round(uint64_t round_end, uint64_t sim_end, uint64_t bootstrap_end,
                           uint32_t n_pkts, const uint32_t* src_host, const uint32_t* dst_ip,
@@ -594,6 +596,13 @@ int64_t sgo_deliver_round(uint64_t round_end, uint64_t sim_end, uint64_t bootstr
     uint64_t delay = tab_lat[cell];
     if (delay < minl) minl = delay;
     uint64_t t = now + delay;
+    /* EmulatedTime + SimulationTime: checked_add(..).unwrap() and EMUTIME_MAX = u64::MAX - 1
+       (emulated_time.rs:30,98-100,121-126) -- a panic in the reference */
+    if (t < now || t == UINT64_MAX) {
+      free(map);
+      free(dst_host);
+      return -2;
+    }
     if (t < round_end) t = round_end;
     if (t < mind) mind = t;
     status[i] = SGO_ST_DELIVERED;
@@ -1151,6 +1160,10 @@ static void* mt_worker(void* p) {
       const uint64_t delay = J->tab_lat[cell];
       if (delay < minl) minl = delay;
       uint64_t tt = now + delay;
+      if (tt < now || tt == UINT64_MAX) { /* EmulatedTime overflow: a panic in the reference */
+        J->err = 1;
+        tt = UINT64_MAX - 1;
+      }
       if (tt < J->round_end) tt = J->round_end;
       if (tt < mind) mind = tt;
       J->status[i] = SGO_ST_DELIVERED;
@@ -1232,6 +1245,13 @@ int64_t sgo_deliver_round_mt(uint64_t round_end, uint64_t sim_end, uint64_t boot
               host_row, tab_lat, tab_loss, map, rng, event_ctr, status, deliver_time, event_id, dst_host,
               dst_offsets, dst_order, NULL, T, pb, hist, mind, minl, nd, 0};
   mt_run(&J, 0);
+  if (J.err) {
+    free(map);
+    free(dst_host);
+    free(pb);
+    free(hist);
+    return -2;
+  }
   /* bucket offsets and each thread's start inside every bucket (thread order = packet order) */
   int64_t delivered = 0;
   uint64_t md = UINT64_MAX, ml = UINT64_MAX;

@@ -14,7 +14,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "shadow_gpu.h")
 
 # sg_status (include/shadow_gpu.h)
 SG_OK = 0
-SG_ABI_VERSION = 2  # include/shadow_gpu.h
+SG_ABI_VERSION = 3  # include/shadow_gpu.h
 SG_ERR_NO_EDGE = 1
 SG_ERR_MULTI_EDGE = 2
 SG_ERR_UNREACHABLE = 3
@@ -25,6 +25,7 @@ SG_ERR_PARSE = 7
 SG_ERR_UNSORTED = 8
 SG_ERR_DUPLICATE_IP = 9
 SG_ERR_CAPACITY = 10
+SG_ERR_TIME_OVERFLOW = 11
 
 SG_ROUTE_SHORTEST_PATH = 0x1
 SG_ROUTE_OUT_DEVICE = 0x2
@@ -42,6 +43,10 @@ EXPORTED = [
     "sg_codel_get_state", "sg_codel_set_state", "sg_inbound_create", "sg_inbound_destroy", "sg_inbound_ring_cap",
     "sg_inbound_run", "sg_inbound_get_state", "sg_hosts_event_ctr", "sg_outbound_create", "sg_outbound_destroy",
     "sg_outbound_ring_cap", "sg_outbound_run", "sg_outbound_get_state",
+    "sg_routing_info_create", "sg_routing_info_destroy", "sg_routing_info_fill", "sg_routing_info_set_rows",
+    "sg_routing_info_view", "sg_routing_info_index", "sg_routing_info_path", "sg_routing_info_smallest_latency",
+    "sg_routing_info_increment_packet_count", "sg_routing_info_packet_count", "sg_routing_info_set_addresses",
+    "sg_worker_get_latency", "sg_worker_get_reliability", "sg_worker_is_routable",
 ]
 
 
@@ -102,6 +107,11 @@ class sg_outbound_sent(C.Structure):
 
 class sg_outbound_queue_state(C.Structure):
     _fields_ = [(k, C.c_void_p) for k in ("head", "tail", "ring_packet", "ring_len", "ring_payload_len", "ring_dst")]
+
+
+class sg_routing_view(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("node_ids", C.c_void_p), ("latency_ns", C.c_void_p), ("packet_loss", C.c_void_p),
+                ("pinned", C.c_uint32)]
 
 
 class sg_round(C.Structure):
@@ -170,6 +180,20 @@ def load(path: str | None = None):
         "sg_net_destroy": (None, [vp]),
         "sg_routing_build": (i32, [vp, vp, vp, u32, u32, u32, u32, vp, vp]),
         "sg_routing_min_latency": (i32, [vp, vp, C.c_size_t, u64p]),
+        "sg_routing_info_create": (i32, [u32, vp, C.POINTER(vp)]),
+        "sg_routing_info_destroy": (None, [vp]),
+        "sg_routing_info_fill": (i32, [vp, vp, vp, u32, vp]),
+        "sg_routing_info_set_rows": (i32, [vp, u32, u32, vp, vp]),
+        "sg_routing_info_view": (i32, [vp, C.POINTER(sg_routing_view)]),
+        "sg_routing_info_index": (i32, [vp, u32, C.POINTER(C.c_uint32)]),
+        "sg_routing_info_path": (i32, [vp, u32, u32, u64p, C.POINTER(C.c_float)]),
+        "sg_routing_info_smallest_latency": (i32, [vp, u64p]),
+        "sg_routing_info_increment_packet_count": (i32, [vp, u32, u32]),
+        "sg_routing_info_packet_count": (u64, [vp, u32, u32]),
+        "sg_routing_info_set_addresses": (i32, [vp, u32, vp, vp]),
+        "sg_worker_get_latency": (i32, [vp, u32, u32, u64p]),
+        "sg_worker_get_reliability": (i32, [vp, u32, u32, C.POINTER(C.c_float)]),
+        "sg_worker_is_routable": (i32, [vp, u32, u32]),
         "sg_hosts_create": (i32, [vp, u32, vp, vp, vp, C.POINTER(vp)]),
         "sg_hosts_get_state": (i32, [vp, vp, vp]),
         "sg_hosts_set_state": (i32, [vp, vp, vp]),

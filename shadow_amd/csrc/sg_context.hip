@@ -224,6 +224,11 @@ void sg_ctx_destroy(sg_ctx* ctx) {
   if (ctx->round_err) (void)hipFree(ctx->round_err);
   if (ctx->sb_ctl) (void)hipFree(ctx->sb_ctl);
   if (ctx->round_ret) (void)hipHostFree(ctx->round_ret);
+  if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
+  for (int b = 0; b < 2; b++) {
+    if (ctx->stage_done[b]) (void)hipEventDestroy(ctx->stage_done[b]);
+    if (ctx->stage_copied[b]) (void)hipEventDestroy(ctx->stage_copied[b]);
+  }
   if (ctx->apsp_ret) (void)hipHostFree(ctx->apsp_ret);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;

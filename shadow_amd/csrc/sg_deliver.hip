@@ -59,7 +59,9 @@ constexpr uint32_t INBLOCK_RANK_MAX = 256;  // region path: rank sort up to this
 constexpr int SORT_BLOCK = 256;
 constexpr int SORT_CHUNK = 2048;  // elements sorted in LDS per chunk
 
-enum : uint32_t { ERR_UNSORTED = 1, ERR_SRC_RANGE = 2, ERR_ROUTE_RANGE = 4, ERR_NOT_LOCAL = 8 };
+enum : uint32_t { ERR_UNSORTED = 1, ERR_SRC_RANGE = 2, ERR_ROUTE_RANGE = 4, ERR_NOT_LOCAL = 8, ERR_TIME_OVERFLOW = 16 };
+// flags that reject a whole batch before any host state changes (raised by k_host_off)
+constexpr uint32_t ERR_BATCH = ERR_UNSORTED | ERR_SRC_RANGE | ERR_ROUTE_RANGE;
 
 struct HostMap {
   uint32_t ip_base, dense_span, n_sorted;
@@ -95,9 +97,14 @@ __global__ void k_seed_hosts(const uint64_t* __restrict__ seed, uint32_t n, uint
 }
 
 // Host CSR over the packets: host_off[h] = first packet whose source is >= h
-// (h = 0..H).  Also checks the grouping (ascending source hosts).
+// (h = 0..H).  Also checks the grouping (ascending source hosts) and, when
+// `route` is given, that every sending host's route row lies in the table shard
+// [row_begin, row_begin + n_rows): a batch failing either check is rejected by
+// the walk before it touches any host's RNG stream or event counter.
 __global__ void k_host_off(const uint32_t* __restrict__ src, uint32_t P, uint32_t H,
-                           uint32_t* __restrict__ host_off, uint32_t* __restrict__ err) {
+                           uint32_t* __restrict__ host_off, uint32_t* __restrict__ err,
+                           const uint32_t* __restrict__ route = nullptr, uint32_t row_begin = 0,
+                           uint32_t n_rows = 0) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i <= P; i += gridDim.x * blockDim.x) {
     const uint32_t s = i < P ? src[i] : H;
     if (s > H || (i < P && s == H)) {
@@ -108,6 +115,10 @@ __global__ void k_host_off(const uint32_t* __restrict__ src, uint32_t P, uint32_
     if (prev > (int64_t)s) {
       atomicOr(err, ERR_UNSORTED);
       continue;
+    }
+    if (route && i < P && (int64_t)s != prev) {  // first packet of host s
+      const uint32_t r = route[s];
+      if (r < row_begin || r - row_begin >= n_rows) atomicOr(err, ERR_ROUTE_RANGE);
     }
     for (int64_t h = prev + 1; h <= (int64_t)s; h++) host_off[h] = i;
   }
@@ -164,7 +175,18 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
   __shared__ uint8_t s_f[WALK_CHUNK];                   // W_* flags -> SG_PKT_* status
   const uint32_t h0 = blockIdx.x * WALK_HOSTS;
   const uint32_t t = threadIdx.x;
-  // clamped: after a grouping error (flagged by k_host_off) host_off is partly unwritten
+  if (*a.err & ERR_BATCH) {
+    // rejected batch (k_host_off): no host state changes; every packet's
+    // destination slot reads NONE so the bucketing that follows stays in bounds
+    for (uint32_t i = blockIdx.x * WALK_THREADS + t; i < a.P; i += gridDim.x * WALK_THREADS) a.dst_host[i] = NONE;
+    if (t == 0) {
+      a.blk_stats[3 * blockIdx.x] = 0;
+      a.blk_stats[3 * blockIdx.x + 1] = ~0ull;
+      a.blk_stats[3 * blockIdx.x + 2] = ~0ull;
+    }
+    return;
+  }
+  // clamped (defensive: k_host_off wrote every entry of an accepted batch)
   const uint32_t p0 = min(a.host_off[min(h0, a.H)], a.P);
   const uint32_t p1 = max(min(a.host_off[min(h0 + WALK_HOSTS, a.H)], a.P), p0);
   // walker lanes: thread t < WALK_HOSTS walks host h0 + t
@@ -204,7 +226,7 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
       const uint2 hr = now[q] < a.sim_end ? a.map.resolve(ip[q]) : make_uint2(NONE, 0);  // worker.rs:332-335, 341
       d[q] = hr.x;
       ip[q] = hr.y;  // reuse: the destination's route column
-      r[q] = a.route[sh[q]];
+      r[q] = a.route[min(sh[q], a.H - 1)];  // sh < H in an accepted batch
     }
 #pragma unroll
     for (int q = 0; q < PPT; q++) {
@@ -258,7 +280,11 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
           if (!(f & W_BOOT) && chance >= rel && (f & W_PAYLOAD)) {  // worker.rs:365-368
             st = SG_PKT_DROP_LOSS;
           } else {
-            arr = s_t[k] + lat;                         // worker.rs:370
+            arr = s_t[k] + lat;  // worker.rs:381; EmulatedTime + SimulationTime panics past EMUTIME_MAX
+            if (arr < lat || arr == ~0ull) {  // (emulated_time.rs:121-126): a failed call here
+              atomicOr(a.err, ERR_TIME_OVERFLOW);
+              arr = ~0ull - 1;
+            }
             if (arr < a.round_end) arr = a.round_end;  // worker.rs:381-384
             id = c++;                                  // host.rs:649-653
             st = SG_PKT_DELIVERED;
@@ -521,6 +547,10 @@ static void fail_flags(uint32_t err) {
     throw Error(SG_ERR_UNSORTED, "packets must be grouped by ascending source host (send order within a host)");
   if (err & ERR_ROUTE_RANGE)
     throw Error(SG_ERR_INVALID_ARG, "a sending host's route row is outside the table shard");
+  if (err & ERR_TIME_OVERFLOW)
+    throw Error(SG_ERR_TIME_OVERFLOW,
+                "send time + path latency overflows EmulatedTime (the reference panics, emulated_time.rs:121-126); "
+                "host RNG streams and event counters are not restored");
   if (err & ERR_NOT_LOCAL)
     throw Error(SG_ERR_INVALID_ARG, "a received record's destination host is not local to this rank");
 }
@@ -1115,7 +1145,7 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   const uint32_t P = pk->n_packets, H = hs->n;
   RoundWork w;
   // workspace: [host_off H+1][big_count 1]; k_host_off writes every host_off
-  // entry of well-grouped packets (else it flags an error and the walk clamps),
+  // entry of well-grouped packets (else it flags an error and the walk skips),
   // k_reduce_stats zeroes big_count: no fills on the round's path
   uint32_t* ws = ctx->d_seg.get<uint32_t>((size_t)H + 8);
   w.host_off = ws;
@@ -1132,7 +1162,7 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   {
     TimedLaunch tl(ctx, "seg_bounds", 4.0 * P + 4.0 * H);
     hipLaunchKernelGGL(k_host_off, dim3(grid_for((size_t)P + 1, 256, 16384)), dim3(256), 0, st, pk->src_host, P, H,
-                       w.host_off, ctx->round_err);
+                       w.host_off, ctx->round_err, hs->route, tab->row_begin, tab->n_rows);
   }
   WalkArgs a;
   a.src = pk->src_host;

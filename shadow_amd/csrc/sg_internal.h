@@ -9,6 +9,7 @@
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <atomic>
 #include <deque>
 #include <vector>
 
@@ -72,6 +73,14 @@ struct KernelTimer {
   uint64_t launches = 0;
 };
 
+// Per-source LDS-resident shortest paths (sg_sssp.hip).
+bool sssp_lds_fits(uint32_t n_nodes);
+void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_arc, uint32_t n, uint32_t n_arcs,
+                     const uint32_t* d_used, uint32_t n_used, uint32_t row_begin, uint32_t row_end,
+                     const uint32_t* self_edge, const uint64_t* e_lat, const float* e_loss, uint64_t* out_lat,
+                     float* out_loss, uint32_t* sat_row, uint32_t delta, unsigned long long* work,
+                     unsigned long long* diag);
+
 }  // namespace sg
 
 struct sg_round_ret {
@@ -94,6 +103,11 @@ struct sg_ctx {
   sg::DevBuf d_seg, d_dst, d_cnt, d_cur, d_keys, d_vals, d_keys2, d_vals2, d_keys3, d_keys4, d_misc,
       d_scan, d_lists, d_lists2, d_ctr0, d_blk, d_spill;
   sg::DevBuf m_scratch;
+  // sg_routing_info_fill: double-buffered device row blocks, copied to the host
+  // on copy_stream while the next block computes
+  sg::DevBuf r_stage_lat[2], r_stage_loss[2];
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t stage_done[2] = {nullptr, nullptr}, stage_copied[2] = {nullptr, nullptr};
   // Round control: round_err (device, zeroed at creation) collects the source
   // phase's error flags; the stats kernel hands them to the host and clears
   // them for the next round.  round_ret (pinned, mapped host memory) receives
@@ -112,6 +126,63 @@ struct sg_ctx {
   bool count_work = false;  // SG_TIMERS_COUNT_WORK
   std::deque<std::pair<std::string, sg::KernelTimer>> timers;  // deque: stable addresses
   std::vector<hipEvent_t> event_pool;
+};
+
+// Device-resident network graph (sg_routing.hip builds it).
+struct sg_net {
+  sg_ctx* ctx = nullptr;
+  uint32_t n_nodes = 0, n_edges = 0, n_arcs = 0;
+  bool directed = false;
+  std::vector<uint32_t> gml_id;
+  // GML edge list (device)
+  uint32_t* e_src = nullptr;
+  uint32_t* e_dst = nullptr;
+  uint64_t* e_lat = nullptr;
+  float* e_loss = nullptr;
+  // in-arc CSC without self-loops (device)
+  uint32_t* in_off = nullptr;  // n_nodes + 1
+  uint32_t* in_src = nullptr;
+  uint32_t* in_dst = nullptr;
+  uint64_t* in_lat = nullptr;    // exact latency (wide kernel)
+  uint32_t* in_lat32 = nullptr;  // latency clamped to LAT32_SAT (packed-key kernel)
+  float* in_om = nullptr;        // 1f32 - loss
+  uint4* in_rec = nullptr;       // per in-arc (source, destination, latency32, bits(1f32 - loss))
+  // out-arc CSR without self-loops (device), for the per-source LDS search
+  // (sg_sssp.hip): out_arc = 3 u32 per arc (head node, latency32, bits(1f32 - loss))
+  uint32_t* out_off = nullptr;  // n_nodes + 1
+  uint32_t* out_arc = nullptr;
+  uint64_t arc_lat_sum = 0;     // sum of the arcs' latency32, for the default bucket width
+  // self-loops
+  uint32_t* self_cnt = nullptr;
+  uint32_t* self_edge = nullptr;
+  ~sg_net() {
+    void* ps[] = {e_src, e_dst, e_lat, e_loss, in_off, in_src, in_dst, in_lat, in_lat32, in_om, in_rec, out_off,
+                  out_arc, self_cnt, self_edge};
+    for (void* p : ps)
+      if (p) (void)hipFree(p);
+  }
+};
+
+// Host-resident dense RoutingInfo (sg_route_info.hip).
+struct sg_routing_info {
+  uint32_t n = 0;
+  std::vector<uint32_t> node_ids;
+  uint64_t* lat = nullptr;  // n x n, pinned when a device was present at creation
+  float* loss = nullptr;
+  bool pinned = false;
+  bool filled = false;
+  uint64_t min_lat = UINT64_MAX;
+  // GML id -> row: dense window [id_base, id_base + id_span) or sorted (id, row) pairs
+  uint32_t id_base = 0, id_span = 0;
+  std::vector<uint32_t> id_dense;
+  std::vector<std::pair<uint32_t, uint32_t>> id_sorted;
+  // address (host byte order) -> row (IpAssignment::get_node, then the id map)
+  uint32_t ip_base = 0, ip_span = 0;
+  std::vector<uint32_t> ip_dense;
+  std::vector<std::pair<uint32_t, uint32_t>> ip_sorted;
+  // increment_packet_count: n x n saturating counters, allocated on first use
+  std::atomic<uint64_t*> counters{nullptr};
+  ~sg_routing_info();
 };
 
 namespace sg {
@@ -178,5 +249,13 @@ struct TimedLaunch {
   TimedLaunch(sg_ctx* c, const char* name, double work);
   ~TimedLaunch();
 };
+
+// Per-source LDS-resident shortest paths (sg_sssp.hip).
+bool sssp_lds_fits(uint32_t n_nodes);
+void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_arc, uint32_t n, uint32_t n_arcs,
+                     const uint32_t* d_used, uint32_t n_used, uint32_t row_begin, uint32_t row_end,
+                     const uint32_t* self_edge, const uint64_t* e_lat, const float* e_loss, uint64_t* out_lat,
+                     float* out_loss, uint32_t* sat_row, uint32_t delta, unsigned long long* work,
+                     unsigned long long* diag);
 
 }  // namespace sg

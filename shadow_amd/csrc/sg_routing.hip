@@ -13,15 +13,29 @@
 // right (source-rooted) and the (latency, loss) pair is updated atomically.
 // Floyd-Warshall would re-associate the f32 fold and is not bit-exact for loss.
 //
-// Kernel: batched-source pull relaxation.  A wave owns one destination node v
-// of one 64-source batch; lane = source.  The batch's distance slab is laid out
-// [node][64 sources], so each in-arc (u -> v) costs one coalesced 512-B read of
-// D[u][0..63] and 64 independent relaxations.  In-arcs are read through the
-// scalar path (wave-uniform).  The key is packed: (lat << 30) | f32 bits(loss),
-// so one u64 min is the lexicographic PathProperties comparison and one 64-bit
-// store is an untorn (lat, loss) update -> in-place (Gauss-Seidel) passes.
-// Rows whose keys saturate (latency >= 2^34-1 ns, or unreachable) are redone
-// with a wide (u64 latency, f32 loss) Jacobi kernel.
+// Two kernels compute the same fixed point:
+//  * sg_sssp.hip k_sssp_lds (graphs up to ~10.9k nodes, the default there): one
+//    workgroup per source, the source's whole distance row in LDS, an
+//    asynchronous delta-stepping work queue; about 1.05x Dijkstra's relaxations.
+//  * k_relax_w2 below (larger graphs): batched-source pull relaxation.  A wave
+//    owns a few destination nodes of one 64-source batch; lane = source.  The
+//    batch's distance slab is laid out [node][64 sources], so each in-arc
+//    (u -> v) costs one coalesced 512-B read of D[u][0..63] and 64 independent
+//    relaxations.
+// Both use the packed key (latency u32 << 32) | f32 bits(loss) (sg_device.h), so
+// one u64 min is the lexicographic PathProperties comparison.  Latency adds
+// saturate at LAT32_SAT = 2^32 - 1 ns; rows holding a saturated key (a path of
+// 4.29 s or more, or an unreachable node) are redone by the wide (u64 latency,
+// f32 loss) Jacobi kernel k_relax_wide.
+//
+// In-place (Gauss-Seidel) updates in k_relax_w2.  A flush writes a lane's two
+// keys with one 16-B store while other waves may gather the same row with 16-B
+// loads.  Each key is one aligned 8-B half of that store.  MI355X_MICROARCH.md
+// records untorn 16-B halves on gfx950 as observed, not architecturally
+// guaranteed; the exactness argument needs only that each aligned 8-B key is
+// read whole (a 64-bit access), which is how the vector memory path moves
+// aligned dwordx2 halves.  Dense graphs (arc segments) flush with 64-bit
+// atomicMin instead.  The LDS kernel updates keys with 64-bit LDS atomics.
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -30,35 +44,6 @@
 
 #include "sg_device.h"
 #include "sg_internal.h"
-
-struct sg_net {
-  sg_ctx* ctx = nullptr;
-  uint32_t n_nodes = 0, n_edges = 0, n_arcs = 0;
-  bool directed = false;
-  std::vector<uint32_t> gml_id;
-  // GML edge list (device)
-  uint32_t* e_src = nullptr;
-  uint32_t* e_dst = nullptr;
-  uint64_t* e_lat = nullptr;
-  float* e_loss = nullptr;
-  // in-arc CSC without self-loops (device)
-  uint32_t* in_off = nullptr;  // n_nodes + 1
-  uint32_t* in_src = nullptr;
-  uint32_t* in_dst = nullptr;
-  uint64_t* in_lat = nullptr;    // exact latency (wide kernel)
-  uint32_t* in_lat32 = nullptr;  // latency clamped to LAT32_SAT (packed-key kernel)
-  float* in_om = nullptr;        // 1f32 - loss
-  uint4* in_rec = nullptr;       // per in-arc (source, destination, latency32, bits(1f32 - loss))
-  // self-loops
-  uint32_t* self_cnt = nullptr;
-  uint32_t* self_edge = nullptr;
-  ~sg_net() {
-    void* ps[] = {e_src, e_dst, e_lat, e_loss, in_off, in_src, in_dst, in_lat, in_lat32, in_om, in_rec, self_cnt,
-                  self_edge};
-    for (void* p : ps)
-      if (p) (void)hipFree(p);
-  }
-};
 
 namespace sg {
 
@@ -113,6 +98,40 @@ __global__ void k_scatter_arcs(const uint32_t* __restrict__ src, const uint32_t*
       in_lat32[q] = l32;
       in_om[q] = om;
       in_rec[q] = make_uint4(d, s, l32, __float_as_uint(om));
+    }
+  }
+}
+
+// Out-arc CSR (tail-grouped) for the per-source search: the same arcs as the
+// CSC, both directions when undirected, self-loops dropped.
+__global__ void k_count_out(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst, uint32_t m,
+                            int directed, uint32_t* __restrict__ outdeg) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < m; e += gridDim.x * blockDim.x) {
+    const uint32_t s = src[e], d = dst[e];
+    if (s == d) continue;
+    atomicAdd(&outdeg[s], 1u);
+    if (!directed) atomicAdd(&outdeg[d], 1u);
+  }
+}
+
+__global__ void k_scatter_out(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                              const uint64_t* __restrict__ lat, const float* __restrict__ loss, uint32_t m,
+                              int directed, uint32_t* __restrict__ cursor, uint32_t* __restrict__ out_arc) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < m; e += gridDim.x * blockDim.x) {
+    const uint32_t s = src[e], d = dst[e];
+    if (s == d) continue;
+    const uint32_t om = __float_as_uint(__fsub_rn(1.0f, loss[e]));
+    const uint64_t l = lat[e];
+    const uint32_t l32 = l < LAT32_SAT ? (uint32_t)l : LAT32_SAT;
+    uint32_t p = atomicAdd(&cursor[s], 1u);
+    out_arc[3 * (size_t)p] = d;
+    out_arc[3 * (size_t)p + 1] = l32;
+    out_arc[3 * (size_t)p + 2] = om;
+    if (!directed) {
+      p = atomicAdd(&cursor[d], 1u);
+      out_arc[3 * (size_t)p] = s;
+      out_arc[3 * (size_t)p + 1] = l32;
+      out_arc[3 * (size_t)p + 2] = om;
     }
   }
 }
@@ -868,6 +887,13 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   net->in_lat32 = dmalloc<uint32_t>(n_arcs);
   net->in_om = dmalloc<float>(n_arcs);
   net->in_rec = dmalloc<uint4>(n_arcs);
+  net->out_off = dmalloc<uint32_t>((size_t)n + 1);
+  net->out_arc = dmalloc<uint32_t>((size_t)n_arcs * 3);
+  for (uint32_t e = 0; e < m; e++)
+    if (g->edge_src[e] != g->edge_dst[e]) {
+      const uint64_t l = std::min<uint64_t>(g->edge_latency_ns[e], LAT32_SAT);
+      net->arc_lat_sum += net->directed ? l : 2 * l;
+    }
   if (n_arcs) {
     uint32_t* cursor = ctx->r_map.get<uint32_t>((size_t)n + 1);
     SG_HIP(hipMemcpyAsync(cursor, net->in_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
@@ -875,6 +901,16 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
                        net->e_dst, net->e_lat, net->e_loss, m, (int)net->directed, cursor,
                        net->in_src, net->in_dst, net->in_lat, net->in_lat32, net->in_om, net->in_rec);
     SG_CHECK_LAUNCH();
+    SG_HIP(hipMemsetAsync(indeg, 0, ((size_t)n + 1) * 4, st));
+    hipLaunchKernelGGL(k_count_out, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst, m,
+                       (int)net->directed, indeg);
+    exclusive_scan_u32(ctx, indeg, net->out_off, n);
+    SG_HIP(hipMemcpyAsync(cursor, net->out_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_scatter_out, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst,
+                       net->e_lat, net->e_loss, m, (int)net->directed, cursor, net->out_arc);
+    SG_CHECK_LAUNCH();
+  } else {
+    SG_HIP(hipMemsetAsync(net->out_off, 0, ((size_t)n + 1) * 4, st));
   }
   SG_HIP(hipStreamSynchronize(st));
 }
@@ -955,6 +991,10 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
   const uint32_t n = net->n_nodes;
   const uint32_t n_rows = row_end - row_begin;
   const uint32_t n_batches = (n_rows + B - 1) / B;
+  // slab byte offsets are 32-bit (buffer descriptors; OOB = 0x80000000)
+  if ((uint64_t)n * B * 8 >= 0x80000000ull)
+    throw Error(SG_ERR_INVALID_ARG, "graph too large for the slab kernel's 32-bit slab offsets (" +
+                                        std::to_string(n) + " nodes)");
   // Group: batches whose slabs are live together (bounded device memory).
   const size_t slab_bytes = (size_t)n * B * 8;
   const size_t budget = (size_t)env_int("SG_APSP_GROUP_MB", 4096) << 20;
@@ -1107,8 +1147,63 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 // A/B measurement knobs: SG_APSP_FRONTIER=0 relaxes every arc every pass;
 // SG_APSP_B sources per batch (32 | 64); SG_APSP_NPW nodes per wave item;
 // SG_APSP_STAGE arcs staged per wave step; SG_APSP_GROUP row reads in flight.
+// Per-source LDS-resident search (sg_sssp.hip) for graphs that fit a CU's LDS.
+// Bucket width: SG_APSP_DELTA (ns), else half the mean arc latency.
+static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
+                               uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
+  hipStream_t st = ctx->stream;
+  const uint32_t rows = row_end - row_begin;
+  uint32_t* sat = ctx->r_flags.get<uint32_t>(rows);
+  SG_HIP(hipMemsetAsync(sat, 0, rows * 4ull, st));
+  unsigned long long* work = ctx->count_work ? ctx->r_work.get<unsigned long long>(WORK_SHARDS) : nullptr;
+  if (work) SG_HIP(hipMemsetAsync(work, 0, WORK_SHARDS * 8, st));
+  const double mean = net->n_arcs ? (double)net->arc_lat_sum / net->n_arcs : 1.0;
+  const char* ds = getenv("SG_APSP_DELTA");
+  double dd = ds && *ds ? atof(ds) : 0.5 * mean;
+  const uint32_t delta = (uint32_t)std::min(4294967295.0, std::max(1.0, dd));
+  // SG_SSSP_DIAG=1 (with counting timers): per-row cycle and phase statistics on stderr
+  const bool diag_on = work && env_int("SG_SSSP_DIAG", 0) != 0;
+  const uint32_t n_diag = std::min<uint32_t>(rows, 4096);
+  unsigned long long* diag = diag_on ? ctx->r_misc.get<unsigned long long>((size_t)n_diag * 8) : nullptr;
+  if (diag) SG_HIP(hipMemsetAsync(diag, 0, (size_t)n_diag * 64, st));
+  {
+    TimedLaunch tl(ctx, "sssp", 0.0);
+    launch_sssp_lds(ctx, net->out_off, net->out_arc, net->n_nodes, net->n_arcs, d_used, n_used, row_begin,
+                    row_end, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work, diag);
+  }
+  if (diag) {
+    std::vector<unsigned long long> h((size_t)n_diag * 8);
+    copy_to_host(ctx, h.data(), diag, h.size() * 8);
+    double a[5] = {0, 0, 0, 0, 0};
+    for (uint32_t r = 0; r < n_diag; r++)
+      for (int k = 0; k < 5; k++) a[k] += (double)h[(size_t)r * 8 + k];
+    fprintf(stderr, "[sssp] delta %u ns, %u rows: mean search %.0f cyc, output %.0f cyc, %.1f wave pops, %.1f buckets, "
+            "%.0f relaxations (%.2f x arcs)\n", delta, n_diag, a[0] / n_diag, a[1] / n_diag, a[2] / n_diag,
+            a[3] / n_diag, a[4] / n_diag, a[4] / n_diag / std::max(1u, net->n_arcs));
+  }
+  std::vector<uint32_t> h_sat(rows);
+  copy_to_host(ctx, h_sat.data(), sat, rows * 4ull);
+  std::vector<uint32_t> wide_rows;
+  for (uint32_t r = 0; r < rows; r++)
+    if (h_sat[r]) wide_rows.push_back(row_begin + r);
+  if (work) {
+    unsigned long long w[WORK_SHARDS];
+    copy_to_host(ctx, w, work, sizeof(w));
+    double total = 0;
+    for (int k = 0; k < WORK_SHARDS; k++) total += (double)w[k];
+    timer_add_work(ctx, "sssp", total);
+  }
+  if (!wide_rows.empty()) run_wide(ctx, net, d_used, n_used, wide_rows, row_begin, out_lat, out_loss);
+}
+
 static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                            uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
+  // SG_APSP_LDS=0 forces the batched-source slab kernel
+  if (env_int("SG_APSP_LDS", 1) != 0 && sssp_lds_fits(net->n_nodes) &&
+      (uint64_t)net->n_arcs * 12 < (1ull << 31)) {
+    shortest_paths_lds(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss);
+    return;
+  }
   const bool front = env_int("SG_APSP_FRONTIER", 1) != 0;
   // dense graphs (more than ~600 in-arcs per node: C2's complete graph) relax
   // faster in 32-source batches with arc segments (3.49 vs 3.66 ms at C2)
@@ -1266,6 +1361,84 @@ int32_t sg_routing_build(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32
       SG_HIP(hipMemcpyAsync(out_packet_loss, o_loss, count * 4, hipMemcpyDeviceToHost, st));
     }
     SG_HIP(hipStreamSynchronize(st));
+  });
+}
+
+// The whole table into a host RoutingInfo (sg_route_info.hip): row blocks are
+// built into one of two device staging buffers and copied to the object's
+// pinned host arrays on a second stream while the next block builds.
+int32_t sg_routing_info_fill(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32_t flags, sg_routing_info* ri) {
+  return sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (!net || net->ctx != ctx) throw Error(SG_ERR_INVALID_ARG, "network belongs to another context");
+    if (!ri) throw Error(SG_ERR_INVALID_ARG, "null routing info");
+    const uint32_t n_used = ri->n;
+    if (n_used && !nodes) throw Error(SG_ERR_INVALID_ARG, "null node list");
+    {
+      std::vector<uint8_t> seen(net->n_nodes, 0);
+      for (uint32_t j = 0; j < n_used; j++) {
+        if (nodes[j] >= net->n_nodes) throw Error(SG_ERR_INVALID_ARG, "node index out of range");
+        if (seen[nodes[j]]++) throw Error(SG_ERR_INVALID_ARG, "duplicate node in node list");
+      }
+    }
+    ri->filled = false;
+    ri->min_lat = UINT64_MAX;
+    if (n_used == 0) {
+      ri->filled = true;
+      return;
+    }
+    hipStream_t st = ctx->stream;
+    uint32_t* d_used = ctx->r_used.get<uint32_t>(n_used);
+    SG_HIP(hipMemcpyAsync(d_used, nodes, (size_t)n_used * 4, hipMemcpyHostToDevice, st));
+    const bool shortest = flags & SG_ROUTE_SHORTEST_PATH;
+    if (shortest) check_self_loops(ctx, net, d_used, n_used, nodes);
+    if (!ctx->copy_stream) {
+      SG_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+      for (int b = 0; b < 2; b++) {
+        SG_HIP(hipEventCreateWithFlags(&ctx->stage_done[b], hipEventDisableTiming));
+        SG_HIP(hipEventCreateWithFlags(&ctx->stage_copied[b], hipEventDisableTiming));
+      }
+    }
+    // blocks of about 1/8 of the table (at least 64 rows, whole 64-row batches)
+    uint32_t rows = (uint32_t)std::max(64, env_int("SG_RI_BLOCK_ROWS", (int)((n_used + 7) / 8)));
+    rows = std::min(n_used, (rows + 63) / 64 * 64);
+    uint64_t* slat[2];
+    float* sloss[2];
+    for (int b = 0; b < 2; b++) {
+      slat[b] = ctx->r_stage_lat[b].get<uint64_t>((size_t)rows * n_used);
+      sloss[b] = ctx->r_stage_loss[b].get<float>((size_t)rows * n_used);
+    }
+    const unsigned nbm = grid_for((size_t)rows * n_used, 256, 2048);
+    uint64_t m = UINT64_MAX;
+    int k = 0;
+    for (uint32_t r0 = 0; r0 < n_used; r0 += rows, k++) {
+      const uint32_t r1 = std::min(n_used, r0 + rows), b = k & 1;
+      if (k >= 2) SG_HIP(hipStreamWaitEvent(st, ctx->stage_copied[b], 0));  // block k - 2 left this buffer
+      if (shortest)
+        shortest_paths(ctx, net, d_used, n_used, r0, r1, slat[b], sloss[b]);
+      else
+        direct_paths(ctx, net, d_used, nodes, n_used, r0, r1, slat[b], sloss[b]);
+      const size_t cells = (size_t)(r1 - r0) * n_used;
+      // (workspace fetched after the build, which may grow these buffers)
+      unsigned long long* dmin = ctx->r_err.get<unsigned long long>(4);
+      unsigned long long* part = ctx->r_misc.get<unsigned long long>(nbm);
+      hipLaunchKernelGGL(k_min_u64, dim3(nbm), dim3(256), 0, st, slat[b], cells, part);
+      hipLaunchKernelGGL(k_min_final, dim3(1), dim3(256), 0, st, part, nbm, dmin);
+      SG_CHECK_LAUNCH();
+      SG_HIP(hipEventRecord(ctx->stage_done[b], st));
+      SG_HIP(hipStreamWaitEvent(ctx->copy_stream, ctx->stage_done[b], 0));
+      SG_HIP(hipMemcpyAsync(ri->lat + (size_t)r0 * n_used, slat[b], cells * 8, hipMemcpyDeviceToHost,
+                            ctx->copy_stream));
+      SG_HIP(hipMemcpyAsync(ri->loss + (size_t)r0 * n_used, sloss[b], cells * 4, hipMemcpyDeviceToHost,
+                            ctx->copy_stream));
+      SG_HIP(hipEventRecord(ctx->stage_copied[b], ctx->copy_stream));
+      unsigned long long h = 0;
+      copy_to_host(ctx, &h, dmin, 8);  // (the next block's build starts after this sync; the copy runs on)
+      m = std::min<uint64_t>(m, h);
+    }
+    SG_HIP(hipStreamSynchronize(ctx->copy_stream));
+    ri->min_lat = m;
+    ri->filled = true;
   });
 }
 

@@ -314,33 +314,132 @@ class NetworkGraph:
 
 
 # ---------------------------------------------------------------------------
-# RoutingInfo (graph/mod.rs:432-481) keyed by GML node id, dense storage
+# RoutingInfo (graph/mod.rs:432-481) keyed by GML node id: a dense host table
+# owned by libshadow_gpu (sg_routing_info, sg_route_info.hip)
 # ---------------------------------------------------------------------------
 class RoutingInfo:
-    def __init__(self, node_ids: Sequence[int], latency_ns: np.ndarray, packet_loss: np.ndarray):
-        self.node_ids = [int(x) for x in node_ids]
-        self.index = {n: i for i, n in enumerate(self.node_ids)}
-        self.latency_ns = latency_ns
-        self.packet_loss = packet_loss
-        self.packet_counters = np.zeros(latency_ns.shape, np.uint64)
+    """RoutingInfo<u32>: path(start, end), get_smallest_latency_ns and the packet
+    counters, over a dense (latency u64, loss f32) table in pinned host memory.
+    `latency_ns` / `packet_loss` are zero-copy [n x n] views (row = source, in
+    `node_ids` order), valid while this object lives.  With addresses attached
+    (set_addresses) it also answers WorkerShared::latency / reliability /
+    is_routable (worker.rs:517-555)."""
+
+    def __init__(self, node_ids: Sequence[int], latency_ns: Optional[np.ndarray] = None,
+                 packet_loss: Optional[np.ndarray] = None):
+        L = load()
+        ids = np.ascontiguousarray(node_ids, dtype=np.uint32)
+        h = C.c_void_p()
+        rc = L.sg_routing_info_create(len(ids), ids.ctypes.data, C.byref(h))
+        if rc != _capi.SG_OK:
+            raise ShadowGpuError(rc, "sg_routing_info_create failed (duplicate node id?)")
+        self.handle = h
+        self.node_ids = [int(x) for x in ids]
+        self.n = len(ids)
+        if latency_ns is not None:
+            self.set_rows(0, np.asarray(latency_ns, np.uint64), np.asarray(packet_loss, np.float32))
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            load().sg_routing_info_destroy(h)
+            self.handle = None
+
+    def fill(self, graph: "NetworkGraph", nodes: Sequence[int], use_shortest_paths: bool = True) -> None:
+        """sg_routing_info_fill: the whole table from the GPU (nodes = petgraph indices of node_ids)."""
+        idx = np.ascontiguousarray(nodes, dtype=np.uint32)
+        assert len(idx) == self.n
+        flags = _capi.SG_ROUTE_SHORTEST_PATH if use_shortest_paths else 0
+        check(graph.ctx.handle, load().sg_routing_info_fill(graph.ctx.handle, graph._ensure_net(), idx.ctypes.data,
+                                                             flags, self.handle))
+
+    def set_rows(self, row_begin: int, latency_ns: np.ndarray, packet_loss: np.ndarray) -> None:
+        lat = np.ascontiguousarray(latency_ns, np.uint64).reshape(-1, self.n)
+        loss = np.ascontiguousarray(packet_loss, np.float32).reshape(-1, self.n)
+        rc = load().sg_routing_info_set_rows(self.handle, int(row_begin), int(row_begin) + lat.shape[0],
+                                             lat.ctypes.data, loss.ctypes.data)
+        if rc != _capi.SG_OK:
+            raise ShadowGpuError(rc, "sg_routing_info_set_rows: bad row range")
+
+    def _view(self):
+        v = _capi.sg_routing_view()
+        load().sg_routing_info_view(self.handle, C.byref(v))
+        return v
+
+    @property
+    def latency_ns(self) -> np.ndarray:
+        v = self._view()
+        if not self.n:
+            return np.zeros((0, 0), np.uint64)
+        buf = (C.c_uint64 * (self.n * self.n)).from_address(v.latency_ns)
+        return np.frombuffer(buf, dtype=np.uint64).reshape(self.n, self.n)
+
+    @property
+    def packet_loss(self) -> np.ndarray:
+        v = self._view()
+        if not self.n:
+            return np.zeros((0, 0), np.float32)
+        buf = (C.c_float * (self.n * self.n)).from_address(v.packet_loss)
+        return np.frombuffer(buf, dtype=np.float32).reshape(self.n, self.n)
+
+    @property
+    def pinned(self) -> bool:
+        return bool(self._view().pinned)
+
+    def index(self, node_id: int) -> Optional[int]:
+        r = C.c_uint32()
+        return int(r.value) if load().sg_routing_info_index(self.handle, int(node_id), C.byref(r)) == 0 else None
 
     def path(self, start: int, end: int) -> Optional[PathProperties]:
-        i, j = self.index.get(int(start)), self.index.get(int(end))
-        if i is None or j is None:
+        """graph/mod.rs:448-450."""
+        lat, loss = C.c_uint64(), C.c_float()
+        if not load().sg_routing_info_path(self.handle, int(start), int(end), C.byref(lat), C.byref(loss)):
             return None
-        return PathProperties(int(self.latency_ns[i, j]), np.float32(self.packet_loss[i, j]))
+        return PathProperties(int(lat.value), np.float32(loss.value))
 
     def increment_packet_count(self, start: int, end: int) -> None:
-        i, j = self.index[int(start)], self.index[int(end)]
-        if self.packet_counters[i, j] != np.iinfo(np.uint64).max:  # saturating_add
-            self.packet_counters[i, j] += np.uint64(1)
+        """graph/mod.rs:453-460 (saturating; the reference's caller unwraps an unknown pair)."""
+        rc = load().sg_routing_info_increment_packet_count(self.handle, int(start), int(end))
+        if rc != _capi.SG_OK:
+            raise KeyError((start, end))
+
+    def packet_count(self, start: int, end: int) -> int:
+        return int(load().sg_routing_info_packet_count(self.handle, int(start), int(end)))
 
     def get_smallest_latency_ns(self) -> Optional[int]:
-        return int(self.latency_ns.min()) if self.latency_ns.size else None
+        """graph/mod.rs:478-480: min over every entry, self pairs included."""
+        out = C.c_uint64()
+        return int(out.value) if load().sg_routing_info_smallest_latency(self.handle, C.byref(out)) else None
+
+    # -- WorkerShared lookups (worker.rs:517-555), addresses as host-order u32 ----
+    def set_addresses(self, ipv4: Sequence[int], node_ids: Sequence[int]) -> None:
+        ips = np.ascontiguousarray(ipv4, np.uint32)
+        ids = np.ascontiguousarray(node_ids, np.uint32)
+        rc = load().sg_routing_info_set_addresses(self.handle, len(ips), ips.ctypes.data, ids.ctypes.data)
+        if rc != _capi.SG_OK:
+            raise ShadowGpuError(rc, "IP address has already been assigned")
+
+    @staticmethod
+    def _be(ip: int) -> int:
+        return int.from_bytes(int(ip).to_bytes(4, "big"), "little")  # in_addr_t: network byte order
+
+    def latency(self, src_ip: int, dst_ip: int) -> Optional[int]:
+        out = C.c_uint64()
+        rc = load().sg_worker_get_latency(self.handle, self._be(src_ip), self._be(dst_ip), C.byref(out))
+        return int(out.value) if rc == _capi.SG_OK else None
+
+    def reliability(self, src_ip: int, dst_ip: int) -> Optional[np.float32]:
+        out = C.c_float()
+        rc = load().sg_worker_get_reliability(self.handle, self._be(src_ip), self._be(dst_ip), C.byref(out))
+        return np.float32(out.value) if rc == _capi.SG_OK else None
+
+    def is_routable(self, src_ip: int, dst_ip: int) -> bool:
+        return bool(load().sg_worker_is_routable(self.handle, self._be(src_ip), self._be(dst_ip)))
 
 
 def generate_routing_info(graph: NetworkGraph, node_ids: Iterable[int], use_shortest_paths: bool) -> RoutingInfo:
-    """sim_config.rs:411-448: used GML ids -> indices, build, remap back to ids."""
+    """sim_config.rs:411-448: used GML ids -> petgraph indices, build straight into
+    the dense host RoutingInfo keyed by the ids (no HashMap, no remap pass)."""
     ids = list(node_ids)
     idx = []
     for x in ids:
@@ -348,13 +447,14 @@ def generate_routing_info(graph: NetworkGraph, node_ids: Iterable[int], use_shor
         if i is None:
             raise KeyError(f"node id {x} not in graph")
         idx.append(i)
+    # an id that maps to an index twice collapses in the reference's HashMap; ids are unique here
+    ri = RoutingInfo([graph.node_index_to_id(i) for i in idx])
     try:
-        t = graph.compute_shortest_paths(idx) if use_shortest_paths else graph.get_direct_paths(idx)
+        ri.fill(graph, idx, use_shortest_paths)
     except ShadowGpuError as e:
         what = "shortest paths" if use_shortest_paths else "the direct paths"
         raise ShadowGpuError(e.code, f"Failed to compute {what} between graph nodes: {e}", e.pair) from None
-    # an id that maps to an index twice collapses in the reference's HashMap; ids are unique here
-    return RoutingInfo([graph.node_index_to_id(i) for i in idx], t.latency_ns, t.packet_loss)
+    return ri
 
 
 # ---------------------------------------------------------------------------

@@ -227,17 +227,112 @@ def test_unsorted_sources_rejected(ctx):
     assert e.value.code == _capi.SG_ERR_UNSORTED
 
 
-def test_error_flags_do_not_leak_into_next_round(oracle, ctx):
-    """The source phase's error flags live in a per-context word the round's
-    stats kernel clears: a rejected round leaves the next one clean and exact."""
+@pytest.mark.parametrize("kind", ["src_range", "unsorted", "route_range"])
+def test_rejected_batch_leaves_hosts_unchanged(oracle, ctx, kind):
+    """A rejected batch is all-or-nothing: no host's RNG stream or event counter
+    moves, the error flags are cleared for the next round, and the next
+    round on the SAME host table is exact."""
     lat, loss, hosts = _world(n_hosts=200, seed=9)
     ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
-    bad = PacketBatch.from_numpy([5, 250], hosts["ip"][[0, 1]], [1, 1], [T0, T0])  # source 250 out of range
-    with pytest.raises(ShadowGpuError):
-        deliver_round(ht, _device_table(lat, loss), bad, T0 + 10, 2**63, 0)
     start, end = T0 + 10**9, T0 + 10**9 + 10**6
+    # a good round first, so the state is not the seed state
+    pk0 = synth.make_packets(2000, hosts, T0, T0 + 10**6, seed=3)
+    deliver_round(ht, _device_table(lat, loss), PacketBatch.from_numpy(pk0["src"], pk0["dst_ip"], pk0["payload"],
+                                                                    pk0["send_time"]), T0 + 10**6, 2**63, 0)
+    rng0, ctr0 = ht.get_state()
+    table = _device_table(lat, loss)
+    if kind == "src_range":  # hosts 0..4 send, then source 250 (out of range)
+        src = np.array([0, 1, 2, 3, 4, 250], np.uint32)
+    elif kind == "unsorted":  # 0..4 are well grouped, then host 1 again
+        src = np.array([0, 1, 2, 3, 4, 1], np.uint32)
+    else:  # a table shard holding rows [0, 5): host 7's route row 7 is outside it
+        src = np.array([0, 1, 2, 3, 4, 7], np.uint32)
+        keep = hosts["route"] < 5
+        assert keep[:5].all() and not keep[7]
+        import torch
+        table = DeviceTable(torch.from_numpy(np.ascontiguousarray(lat[:5]).view(np.int64).ravel()).cuda(),
+                            torch.from_numpy(np.ascontiguousarray(loss[:5]).ravel()).cuda(), lat.shape[1], 0)
+    dst = hosts["ip"][(src + 1) % hosts["n"]]
+    bad = PacketBatch.from_numpy(src, dst, np.ones(len(src), np.uint32), np.full(len(src), T0 + 2 * 10**6, np.uint64))
+    with pytest.raises(ShadowGpuError) as e:
+        deliver_round(ht, table, bad, T0 + 3 * 10**6, 2**63, 0)
+    assert e.value.code == (_capi.SG_ERR_UNSORTED if kind == "unsorted" else _capi.SG_ERR_INVALID_ARG)
+    rng1, ctr1 = ht.get_state()
+    assert np.array_equal(rng1, rng0) and np.array_equal(ctr1, ctr0), "a rejected batch changed host state"
     pk = synth.make_packets(3000, hosts, start, end, seed=9)
+    want = oracle.deliver_round(end, 2**63, 0, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
+                                hosts["ip"], hosts["route"], lat, loss, rng0.copy(), ctr0.copy())
+    out = deliver_round(ht, _device_table(lat, loss),
+                        PacketBatch.from_numpy(pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"]), end, 2**63, 0)
+    got = out.to_numpy(len(pk["src"]))
+    for k in ("status", "deliver_time", "event_id", "dst_offsets", "dst_order"):
+        assert np.array_equal(got[k], want[k]), k
+
+
+def test_arrival_time_overflow_is_an_error(oracle, ctx):
+    """send time + latency past EMUTIME_MAX (u64::MAX - 1): EmulatedTime + SimulationTime
+    panics in the reference (emulated_time.rs:121-126, worker.rs:381); here the call
+    fails with SG_ERR_TIME_OVERFLOW and the oracle raises OverflowError."""
+    hosts = synth.make_hosts(4, 2)
+    lat = np.full((2, 2), 10**6, np.uint64)
+    loss = np.zeros((2, 2), np.float32)
+    for t_send, bad in ((2**64 - 10**6 - 2, False), (2**64 - 10**6 - 1, True), (2**64 - 10, True)):
+        src = np.array([0], np.uint32)
+        dst = hosts["ip"][[1]]
+        ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+        rng, ctr = ht.get_state()
+        b = PacketBatch.from_numpy(src, dst, [100], np.array([t_send], np.uint64))
+        if bad:
+            with pytest.raises(OverflowError):
+                oracle.deliver_round(0, 2**64 - 1, 0, src, dst, [100], [t_send], hosts["ip"], hosts["route"], lat,
+                                     loss, rng, ctr)
+            with pytest.raises(ShadowGpuError) as e:
+                deliver_round(ht, _device_table(lat, loss), b, 0, 2**64 - 1, 0)
+            assert e.value.code == _capi.SG_ERR_TIME_OVERFLOW
+        else:
+            want = oracle.deliver_round(0, 2**64 - 1, 0, src, dst, [100], [t_send], hosts["ip"], hosts["route"],
+                                        lat, loss, rng, ctr)
+            got = deliver_round(ht, _device_table(lat, loss), b, 0, 2**64 - 1, 0).to_numpy(1)
+            assert int(got["deliver_time"][0]) == int(want["deliver_time"][0]) == 2**64 - 2
+
+
+@pytest.fixture(scope="module")
+def c4_world(ctx):
+    """The C4 workload: the 10k-node C3 table built on the GPU once,
+    100k hosts (node h mod 10k), 1M packets."""
+    import time
+
+    import torch
+
+    from shadow_amd import NetworkGraph
+
+    t0 = time.perf_counter()
+    g = synth.ring_chords_graph(10000, 8.0, seed=1)
+    net = NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
+    n = 10000
+    used = np.arange(n, dtype=np.uint32)
+    dl = torch.empty(n * n, dtype=torch.int64, device="cuda")
+    df = torch.empty(n * n, dtype=torch.float32, device="cuda")
+    net.build_rows_device(used, 0, n, dl.data_ptr(), df.data_ptr(), True)
+    lat = dl.cpu().numpy().view(np.uint64).reshape(n, n)
+    loss = df.cpu().numpy().reshape(n, n)
+    del dl, df
+    hosts = synth.make_hosts(100000, n, general_seed=1, exact_seeds=True)
+    start, end = T0 + 10**9, T0 + 10**9 + 10**6
+    pk = synth.make_packets(1_000_000, hosts, start, end, seed=100)
+    print(f"[c4_world] built in {time.perf_counter() - t0:.1f} s", flush=True)
+    return lat, loss, hosts, pk, end
+
+
+def test_c4_full_round(oracle, ctx, c4_world):
+    """The C4 round at full size: exact against the CPU restatement in every output."""
+    import time
+
+    lat, loss, hosts, pk, end = c4_world
+    t0 = time.perf_counter()
     want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, end, 2**63, 0)
+    print(f"[c4] round + oracle in {time.perf_counter() - t0:.1f} s", flush=True)
+    assert want["delivered"] > 700_000
     _assert_same(want, got, ost, gst)
 
 

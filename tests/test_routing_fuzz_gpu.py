@@ -10,6 +10,13 @@ from shadow_amd import NetworkGraph
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["lds", "slab"])
+def apsp_kernel(request, monkeypatch):
+    """Both shortest-path kernels: the per-source LDS search and the slab relaxation."""
+    monkeypatch.setenv("SG_APSP_LDS", "1" if request.param == "lds" else "0")
+    return request.param
+
+
 def _random_graph(n, avg_deg, directed, seed):
     rng = np.random.default_rng(seed)
     m = int(n * avg_deg / (1 if directed else 2))

@@ -16,6 +16,15 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
+@pytest.fixture(autouse=True, params=["lds", "slab"])
+def apsp_kernel(request, monkeypatch):
+    """Every routing test runs on both shortest-path kernels: the per-source
+    LDS-resident search (sg_sssp.hip, the default up to ~10.9k nodes) and the
+    batched-source slab relaxation (k_relax_w2, larger graphs)."""
+    monkeypatch.setenv("SG_APSP_LDS", "1" if request.param == "lds" else "0")
+    return request.param
+
+
 def _graph(g, ctx):
     return NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
 
@@ -192,8 +201,10 @@ def test_empty_used(ctx):
                                  {"SG_APSP_OUT_TPB": "1"}, {"SG_APSP_OUT_TPB": "4"},
                                  {"SG_APSP_OUT_TPB": "4", "SG_APSP_B": "32"}, {"SG_APSP_SEG": "3"},
                                  {"SG_APSP_SEG": "4", "SG_APSP_B": "32"}, {"SG_APSP_SEG": "16", "SG_APSP_PASS_CHUNK": "1"}])
-def test_kernel_variants_bit_exact(oracle, ctx, monkeypatch, env):
-    """Every A/B variant of the relaxation kernel (slab width, frontier, item size) is exact."""
+def test_kernel_variants_bit_exact(oracle, ctx, monkeypatch, env, apsp_kernel):
+    """Every A/B variant of the slab relaxation kernel (slab width, frontier, item size) is exact."""
+    if apsp_kernel == "lds":
+        pytest.skip("slab-kernel knobs")
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     g = synth.ring_chords_graph(900, 7.0, seed=21, parallel=0.03)
@@ -202,9 +213,11 @@ def test_kernel_variants_bit_exact(oracle, ctx, monkeypatch, env):
 
 
 @pytest.mark.parametrize("nseg", ["2", "5"])
-def test_arc_segments_directed_dense(oracle, ctx, monkeypatch, nseg):
+def test_arc_segments_directed_dense(oracle, ctx, monkeypatch, nseg, apsp_kernel):
     """Arc segments (atomic-min flush) on a directed, nearly complete graph with
-    parallel arcs, used-subset rows."""
+    parallel arcs, used-subset rows (the LDS search: a dense directed graph)."""
+    if apsp_kernel == "lds" and nseg != "2":
+        pytest.skip("one LDS run is enough")
     monkeypatch.setenv("SG_APSP_SEG", nseg)
     g = synth.complete_graph(160, seed=11)
     rng = np.random.default_rng(11)
@@ -245,3 +258,101 @@ def test_c5_scale_row_samples(oracle, ctx):
     used = np.arange(50000, dtype=np.uint32)
     for rows in ((0, 128), (25000, 25064), (49936, 50000)):
         _check(oracle, g, used, ctx, rows=rows)
+
+
+@pytest.fixture(scope="module")
+def c3_oracle(oracle):
+    g = synth.ring_chords_graph(10000, 8.0, seed=1)
+    used = np.arange(10000, dtype=np.uint32)
+    rc, olat, oloss, _ = oracle.shortest_paths(g["n"], g["src"], g["dst"], g["lat"], g["loss"], False, used,
+                                               threads=min(16, os.cpu_count() or 1))
+    assert rc == 0
+    return g, used, olat, oloss
+
+
+def test_c3_full_table(c3_oracle, ctx):
+    """The headline C3 build (bench.py `value`): the 10k-node ring + chords graph,
+    all 10^8 (latency, loss) cells bit-exact against the oracle's Dijkstra."""
+    g, used, olat, oloss = c3_oracle
+    _check_full(g, used, olat, oloss, ctx)
+
+
+def _check_full(g, used, olat, oloss, ctx):
+    import torch
+
+    net = _graph(g, ctx)
+    n = len(used)
+    dl = torch.empty(n * n, dtype=torch.int64, device="cuda")
+    df = torch.empty(n * n, dtype=torch.float32, device="cuda")
+    net.build_rows_device(used, 0, n, dl.data_ptr(), df.data_ptr(), True)
+    lat = dl.cpu().numpy().view(np.uint64).reshape(n, n)
+    bad = np.argwhere(lat != olat)
+    assert len(bad) == 0, f"{len(bad)} latency cells differ, first {bad[:3].tolist()}"
+    loss = df.cpu().numpy().view(np.uint32).reshape(n, n)
+    bad = np.argwhere(loss != oloss.view(np.uint32))
+    assert len(bad) == 0, f"{len(bad)} loss cells differ, first {bad[:3].tolist()}"
+
+
+@pytest.mark.parametrize("delta", ["1", "1000", "3000000", "40000000", "4000000000"])
+def test_lds_bucket_widths(oracle, ctx, monkeypatch, delta, apsp_kernel):
+    """The LDS search's bucket width changes the relaxation order only: from
+    1 ns (Dijkstra-like, many buckets) to 4 s (one bucket, chaotic Bellman-Ford),
+    on a tie-heavy lossy graph, directed and undirected."""
+    if apsp_kernel == "slab":
+        pytest.skip("LDS knob")
+    monkeypatch.setenv("SG_APSP_DELTA", delta)
+    for directed in (False, True):
+        g = synth.ring_chords_graph(700, 6.0, seed=31, directed=directed, parallel=0.05)
+        g["lat"] = (g["lat"] // 10**7 + 1) * 10**7  # coarse latencies: many equal-latency paths
+        g["loss"] = np.where(np.arange(len(g["loss"])) % 3 == 0, np.float32(0.05), g["loss"]).astype(np.float32)
+        used = np.random.default_rng(31).permutation(700)[:500].astype(np.uint32)
+        _check(oracle, g, used, ctx)
+
+
+@pytest.mark.parametrize("n", [10900, 11200])
+def test_lds_size_limit(oracle, ctx, n):
+    """Node counts just inside and just past the LDS-resident search's limit (the
+    second runs on the slab kernel): sampled rows exact."""
+    g = synth.ring_chords_graph(n, 8.0, seed=7)
+    used = np.arange(n, dtype=np.uint32)
+    for rows in ((0, 64), (n - 64, n)):
+        _check(oracle, g, used, ctx, rows=rows)
+
+
+@pytest.mark.parametrize("block_rows", ["64", "1000", "20000"])
+def test_routing_info_fill_c3(c3_oracle, ctx, monkeypatch, block_rows, apsp_kernel):
+    """sg_routing_info_fill: the whole C3 table straight into the dense host
+    RoutingInfo, row blocks copied while the next builds (generate_routing_info,
+    sim_config.rs:411-448, in a shuffled used-id order as a HashSet yields them)."""
+    if apsp_kernel == "slab" and block_rows != "1000":
+        pytest.skip("one slab-kernel run is enough")
+    monkeypatch.setenv("SG_RI_BLOCK_ROWS", block_rows)
+    g, used, olat, oloss = c3_oracle
+    net = _graph(g, ctx)
+    order = np.random.default_rng(3).permutation(10000)
+    ri = generate_routing_info(net, order.tolist(), True)
+    assert ri.pinned
+    lat, loss = ri.latency_ns, ri.packet_loss
+    assert np.array_equal(lat, olat[np.ix_(order, order)])
+    assert np.array_equal(loss.view(np.uint32), oloss.view(np.uint32)[np.ix_(order, order)])
+    assert ri.get_smallest_latency_ns() == int(olat.min())
+    rng = np.random.default_rng(5)
+    for a, b in rng.integers(0, 10000, (200, 2)):
+        p = ri.path(int(a), int(b))
+        assert p.latency_ns == int(olat[a, b]) and np.float32(p.packet_loss).view(np.uint32) == oloss.view(np.uint32)[a, b]
+
+
+def test_routing_info_direct_and_errors(oracle, ctx):
+    """Direct paths into the host RoutingInfo, and a failing build leaves a usable
+    error (the reference's Err from get_edge_weight, graph/mod.rs:256-293)."""
+    g = synth.complete_graph(90, seed=4)
+    net = _graph(g, ctx)
+    ri = generate_routing_info(net, range(90), False)
+    rc, olat, oloss, _ = oracle.direct_paths(g["n"], g["src"], g["dst"], g["lat"], g["loss"], False,
+                                             np.arange(90, dtype=np.uint32))
+    assert rc == 0 and np.array_equal(ri.latency_ns, olat)
+    keep = ~((g["src"] == 5) & (g["dst"] == 5))  # node 5 loses its self-loop
+    g2 = dict(g, src=g["src"][keep], dst=g["dst"][keep], lat=g["lat"][keep], loss=g["loss"][keep])
+    with pytest.raises(ShadowGpuError) as e:
+        generate_routing_info(_graph(g2, ctx), range(90), True)
+    assert e.value.code == _capi.SG_ERR_NO_EDGE
