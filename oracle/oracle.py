@@ -117,6 +117,30 @@ def shortest_paths(n_nodes, src, dst, lat, loss, directed, used, rows=None, thre
     return rc, out_lat, out_loss, (ea.value, eb.value)
 
 
+def routing_faithful(n_nodes, src, dst, lat, loss, directed, used, rows=None, node_ids=None, threads=1,
+                     read_back=True):
+    """The reference's routing build cost for cost (sg_faithful.c): petgraph-style
+    Dijkstra with a SipHash score map, the nodes.contains filter, per-source and
+    global HashMaps, the self-loop override and the id remap (graph/mod.rs:183-228,
+    sim_config.rs:411-448), for source rows [0, rows).  Returns (rc, lat, loss,
+    phase seconds [dijkstra+filter+per-source maps, global collect, self pairs, remap])."""
+    src, dst = _arr(src, np.uint32), _arr(dst, np.uint32)
+    lat, loss = _arr(lat, np.uint64), _arr(loss, np.float32)
+    used = _arr(used, np.uint32)
+    nu = len(used)
+    k = nu if rows is None else int(rows)
+    ids = _arr(np.arange(n_nodes) if node_ids is None else node_ids, np.uint32)
+    out_lat = np.zeros((k, nu), np.uint64) if read_back else None
+    out_loss = np.zeros((k, nu), np.float32) if read_back else None
+    ph = (C.c_double * 4)()
+    rc = lib().sgo_routing_faithful(n_nodes, len(src), _p(src, C.c_uint32), _p(dst, C.c_uint32),
+                                    _p(lat, C.c_uint64), _p(loss, C.c_float), int(bool(directed)),
+                                    _p(used, C.c_uint32), nu, k, _p(ids, C.c_uint32), int(threads), ph,
+                                    _p(out_lat, C.c_uint64) if read_back else None,
+                                    _p(out_loss, C.c_float) if read_back else None)
+    return rc, out_lat, out_loss, list(ph)
+
+
 def direct_paths(n_nodes, src, dst, lat, loss, directed, used):
     """NetworkGraph::get_direct_paths (graph/mod.rs:230-252), dense output."""
     src, dst = _arr(src, np.uint32), _arr(dst, np.uint32)

@@ -151,7 +151,6 @@ struct sg_net {
   // (sg_sssp.hip): out_arc = 3 u32 per arc (head node, latency32, bits(1f32 - loss))
   uint32_t* out_off = nullptr;  // n_nodes + 1
   uint32_t* out_arc = nullptr;
-  uint64_t arc_lat_sum = 0;     // sum of the arcs' latency32, for the default bucket width
   // self-loops
   uint32_t* self_cnt = nullptr;
   uint32_t* self_edge = nullptr;

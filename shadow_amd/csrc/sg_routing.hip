@@ -889,11 +889,6 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   net->in_rec = dmalloc<uint4>(n_arcs);
   net->out_off = dmalloc<uint32_t>((size_t)n + 1);
   net->out_arc = dmalloc<uint32_t>((size_t)n_arcs * 3);
-  for (uint32_t e = 0; e < m; e++)
-    if (g->edge_src[e] != g->edge_dst[e]) {
-      const uint64_t l = std::min<uint64_t>(g->edge_latency_ns[e], LAT32_SAT);
-      net->arc_lat_sum += net->directed ? l : 2 * l;
-    }
   if (n_arcs) {
     uint32_t* cursor = ctx->r_map.get<uint32_t>((size_t)n + 1);
     SG_HIP(hipMemcpyAsync(cursor, net->in_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
@@ -1147,8 +1142,12 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 // A/B measurement knobs: SG_APSP_FRONTIER=0 relaxes every arc every pass;
 // SG_APSP_B sources per batch (32 | 64); SG_APSP_NPW nodes per wave item;
 // SG_APSP_STAGE arcs staged per wave step; SG_APSP_GROUP row reads in flight.
-// Per-source LDS-resident search (sg_sssp.hip) for graphs that fit a CU's LDS.
-// Bucket width: SG_APSP_DELTA (ns), else half the mean arc latency.
+// Per-source LDS-resident search (sg_sssp.hip) for sparse graphs that fit a CU's
+// LDS.  Bucket width: SG_APSP_DELTA (ns), else one bucket (chaotic relaxation
+// over the asynchronous queue): at C3 it measured fastest (5.10 ms against
+// 5.6 ms at 100 ms buckets and 6.2 ms at 50 ms), for 2.5x Dijkstra's
+// relaxations against 1.06x at 50 ms -- the search is bound by its critical
+// path, not by its relaxation count.
 static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                                uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
   hipStream_t st = ctx->stream;
@@ -1157,9 +1156,8 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   SG_HIP(hipMemsetAsync(sat, 0, rows * 4ull, st));
   unsigned long long* work = ctx->count_work ? ctx->r_work.get<unsigned long long>(WORK_SHARDS) : nullptr;
   if (work) SG_HIP(hipMemsetAsync(work, 0, WORK_SHARDS * 8, st));
-  const double mean = net->n_arcs ? (double)net->arc_lat_sum / net->n_arcs : 1.0;
   const char* ds = getenv("SG_APSP_DELTA");
-  double dd = ds && *ds ? atof(ds) : 0.5 * mean;
+  double dd = ds && *ds ? atof(ds) : 4294967295.0;
   const uint32_t delta = (uint32_t)std::min(4294967295.0, std::max(1.0, dd));
   // SG_SSSP_DIAG=1 (with counting timers): per-row cycle and phase statistics on stderr
   const bool diag_on = work && env_int("SG_SSSP_DIAG", 0) != 0;
@@ -1174,9 +1172,12 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   if (diag) {
     std::vector<unsigned long long> h((size_t)n_diag * 8);
     copy_to_host(ctx, h.data(), diag, h.size() * 8);
-    double a[5] = {0, 0, 0, 0, 0};
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t r = 0; r < n_diag; r++)
-      for (int k = 0; k < 5; k++) a[k] += (double)h[(size_t)r * 8 + k];
+      for (int k = 0; k < 8; k++) a[k] += (double)h[(size_t)r * 8 + k];
+    fprintf(stderr, "[sssp] per-wave cycles summed over a row's 16 waves: claim+wait %.0f, pop %.0f, steps %.0f "
+            "(per pop: %.0f, %.0f)\n", a[5] / n_diag, a[6] / n_diag, a[7] / n_diag, a[6] / std::max(1.0, a[2]),
+            a[7] / std::max(1.0, a[2]));
     fprintf(stderr, "[sssp] delta %u ns, %u rows: mean search %.0f cyc, output %.0f cyc, %.1f wave pops, %.1f buckets, "
             "%.0f relaxations (%.2f x arcs)\n", delta, n_diag, a[0] / n_diag, a[1] / n_diag, a[2] / n_diag,
             a[3] / n_diag, a[4] / n_diag, a[4] / n_diag / std::max(1u, net->n_arcs));
@@ -1198,8 +1199,12 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
 
 static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                            uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
-  // SG_APSP_LDS=0 forces the batched-source slab kernel
-  if (env_int("SG_APSP_LDS", 1) != 0 && sssp_lds_fits(net->n_nodes) &&
+  // SG_APSP_LDS=0 forces the batched-source slab kernel.  The LDS search takes
+  // sparse graphs (mean out-degree <= 64); on dense ones the slab kernel shares
+  // each arc record among 64 sources (C2, 1,200-node complete graph: 3.6 ms
+  // against 6.8-9.2 ms for the LDS search).
+  const bool sparse = net->n_nodes && net->n_arcs <= 64ull * net->n_nodes;
+  if (env_int("SG_APSP_LDS", 1) != 0 && sparse && sssp_lds_fits(net->n_nodes) &&
       (uint64_t)net->n_arcs * 12 < (1ull << 31)) {
     shortest_paths_lds(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss);
     return;

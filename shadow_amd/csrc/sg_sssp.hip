@@ -2,37 +2,46 @@
 //
 // Replaces, for graphs whose node count fits a CU's LDS (about 11k nodes), the
 // per-source petgraph::algo::dijkstra of NetworkGraph::compute_shortest_paths
-// (graph/mod.rs:190-208).  One workgroup owns one source row: its keys
-// key[v] = (latency u32 << 32) | bits(loss) live in LDS for the whole search,
-// the graph's out-arcs are read from L2 (one 12-B record per relaxation), and
-// the finished row is written straight into the caller's row-major table.
+// (graph/mod.rs:190-208).  One workgroup owns one source row: its keys live in
+// LDS for the whole search, the graph's out-arcs are read from L2 (one 12-B
+// record per relaxation), and the finished row is written straight into the
+// caller's row-major table.
 //
 // Why not the batched-source slab kernel (sg_routing.hip k_relax_w2) here: a
 // 64-source batch gathers whole 512-B rows, and Bellman-Ford re-gathers a row
 // whenever any of its 64 sources improved it -- about 10x the n_used * arcs
 // relaxations of Dijkstra at C3.  A per-source search relaxes only what its own
-// frontier improved, and with the near/far bucket order below it does about
-// 1.1-1.3x Dijkstra's relaxations.
+// frontier improved: with delta-stepping buckets about 1.05-1.4x Dijkstra's
+// relaxations (SG_SSSP_DIAG reports it).
 //
 // Exactness.  Edge latency >= 1 ns (graph/mod.rs:105-107) and the f32 loss fold
 // is monotone, so petgraph's Dijkstra result is the unique fixed point of the
 // source-rooted relaxation key[v] = min(key[v], key[u] (+) w(u, v)) with the
-// edge applied on the right (sg_device.h relax32); any relaxation order reaches
-// it.  LDS 64-bit atomic min keeps each (latency, loss) update whole.  Keys whose
-// latency saturates at LAT32_SAT (>= 4.29 s, or unreachable) are never
-// propagated and flag the row for the wide kernel (sg_routing.hip run_wide), as
-// in the slab kernel.
+// edge applied on the right (sg_device.h fold_loss); any relaxation order
+// reaches it.  Keys whose latency saturates at LAT32_SAT (>= 4.29 s, or
+// unreachable) are never propagated and flag the row for the wide kernel
+// (sg_routing.hip run_wide), as in the slab kernel.
+//
+// Flagged key.  key = (latency u32 << 32) | (bits(loss) << 1) | dirty.  Loss is
+// in [0, 1], so bits(loss) < 2^31 and the 64-bit integer order of the key is the
+// PathProperties order (latency, then loss), the flag ranking last.  A candidate
+// carries dirty = 1, so one 64-bit LDS atomic min both relaxes and tests the
+// flag: the node improved iff the returned key's (latency, loss) is larger, and
+// it must be queued iff the returned key was clean.  An equal candidate never
+// replaces a key (its flag is 1, the stored one 0 or 1), so "improved" means
+// strictly better.  A pop clears the flag with one atomic AND whose return value
+// is the key to relax with; an improvement that lands after it finds the flag
+// clear and queues the node again.
 //
 // Work order: an asynchronous work queue per workgroup, with delta-stepping
 // buckets (bucket width `delta`; one workgroup barrier per bucket, none per hop).
-//   * dirty[v] (LDS bitmap) is set when key[v] improves and cleared when v is
-//     popped.  A node becomes dirty once per improvement episode; an improvement
-//     that makes it dirty with latency below `split` also appends it to the
-//     queue, so the queue never holds a node twice.
+//   * A node is dirty from an improvement until it is popped; a node that
+//     becomes dirty with latency below `split` is also appended to the queue,
+//     so the queue never holds a node twice.
 //   * The queue is an LDS ring of u16 node ids with head / tail counters.  A
 //     wave claims up to 64 entries (CAS on head), relaxes their out-arcs and
-//     appends what it improved (add on tail, then the slot writes; a popped slot
-//     not yet written reads as EMPTY and is waited for).  `busy` counts the
+//     appends what it improved (add on tail, then the slot writes; a claimed
+//     slot not yet written reads as EMPTY and is waited for).  `busy` counts the
 //     waves holding claimed entries; head and busy share one 64-bit LDS word,
 //     so a claim is one CAS and a failed claim attempt changes nothing.
 //   * Quiescence (busy == 0 and head == tail, read in that order) is stable: no
@@ -40,6 +49,11 @@
 //     the dirty nodes left are those at or beyond `split`.  split = (smallest
 //     dirty latency) + delta, the dirty nodes below it are queued, and the
 //     waves go on.  No dirty node left: the search is done.
+//   * Relaxing a popped node: when the largest out-degree among the wave's
+//     entries is at most LANE_DEG_MAX, each lane walks its own node's arcs, eight
+//     loads in flight (no cross-lane bookkeeping on the dependent chain);
+//     otherwise the wave expands the entries' arcs into consecutive slots
+//     (owner by scatter + max-scan) and relaxes SSSP_K chunks of 64 at once.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -49,12 +63,24 @@
 
 namespace sg {
 
-constexpr int SSSP_THREADS = 1024;
+constexpr int SSSP_THREADS = 1024;  // the largest workgroup (SG_SSSP_THREADS selects 512 or 1024)
 constexpr int SSSP_WAVES = SSSP_THREADS / 64;
-constexpr int SSSP_K = 4;  // arc chunks (64 slots each) a wave handles at once
-// static LDS of k_sssp_lds: ctl[8] + red[SSSP_WAVES] (u32), own[SSSP_WAVES][64 * SSSP_K] (u8)
+constexpr int SSSP_K = 4;            // expansion path: chunks of 64 arc slots a wave handles at once
+// lane path: arcs a lane has in flight (template LA: 8 or 16, SG_SSSP_LANE_ARCS);
+// used up to out-degree lane_deg_max (SG_SSSP_LANE_DEG, default 32)
+// static LDS of k_sssp_lds: ctl[8] + red[SSSP_WAVES] (u32), hb (u64), own[SSSP_WAVES][64 * SSSP_K] (u8)
 constexpr size_t SSSP_STATIC_LDS = 4 * (8 + SSSP_WAVES) + 16 + SSSP_WAVES * 64 * SSSP_K;
 constexpr size_t LDS_PER_CU = 160 * 1024;
+
+constexpr uint64_t FKEY_INF = ((uint64_t)LAT32_SAT << 32) | ((uint64_t)0x3F800000u << 1);  // (SAT, 1.0), clean
+__device__ __forceinline__ uint32_t fkey_lat(uint64_t k) { return (uint32_t)(k >> 32); }
+__device__ __forceinline__ uint32_t fkey_loss_bits(uint64_t k) { return ((uint32_t)k >> 1) & 0x7FFFFFFFu; }
+// key(u) (+) edge (graph/mod.rs:322-331), flagged dirty
+__device__ __forceinline__ uint64_t frelax(uint64_t ku, uint32_t edge_lat, float edge_om) {
+  const uint32_t lat = __builtin_elementwise_add_sat(fkey_lat(ku), edge_lat);
+  const float loss = fold_loss(__uint_as_float(fkey_loss_bits(ku)), edge_om);
+  return ((uint64_t)lat << 32) | ((uint64_t)__float_as_uint(loss) << 1) | 1ull;
+}
 
 // Inclusive scans across a wave64 with DPP (row shifts, then the row broadcasts
 // of lanes 15 and 31): sum and max of u32.
@@ -77,88 +103,93 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
   return v;
 }
 
-// LDS bitmap updates.  Relaxed: a wave's LDS operations reach the LDS in issue
-// order, and the order that matters (min on key[v], then the dirty bit; the
-// dirty clear, then the key read) is kept by a control dependence and by a
-// compiler fence.  A workgroup-scope acquire/release would also drain every
-// outstanding global load (vmcnt(0)) on gfx950.
-__device__ __forceinline__ uint32_t lds_fetch_or(uint32_t* p, uint32_t m) {
-  return __hip_atomic_fetch_or(p, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_clear_bits(uint32_t* p, uint32_t m) {
-  (void)__hip_atomic_fetch_and(p, ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Append the flagged lanes' node ids to an LDS list (one counter add per wave).
-__device__ __forceinline__ void wave_append(bool flag, uint32_t node, uint16_t* list, uint32_t* counter,
-                                            int lane) {
-  const uint64_t m = __ballot(flag);
-  if (!m) return;
-  const int leader = __ffsll((unsigned long long)m) - 1;
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-  base = __shfl(base, leader);
-  if (flag) list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)node;
-}
-
-// Queue capacity: a power of two >= n + 1024.  At most n nodes are queued (one
+// Queue capacity: n + 1024 rounded up to 64.  At most n nodes are queued (one
 // entry per dirty node) and at most 16 waves x 64 claimed slots are still being
-// read, so a slot is never reused while its last entry is unread.
-__host__ __device__ inline uint32_t sssp_ring_cap(uint32_t n) {
-  uint32_t c = 1024;
-  while (c < n + 1024) c <<= 1;
-  return c;
-}
+// read, so a slot is never reused while its last entry is unread.  Slot of a
+// counter c: c mod cap by a multiply-high and one correction (cap < 2^17).
+__host__ __device__ inline uint32_t sssp_ring_cap(uint32_t n) { return (n + 1024 + 63) / 64 * 64; }
+struct RingMod {
+  uint32_t cap, m;  // m = floor(2^32 / cap)
+  __device__ __forceinline__ uint32_t operator()(uint32_t c) const {
+    uint32_t r = c - __umulhi(c, m) * cap;  // in [0, 2 cap)
+    return r >= cap ? r - cap : r;
+  }
+};
 constexpr uint16_t RING_EMPTY = 0xFFFF;
 
-// LDS bytes the kernel needs for n nodes (dynamic part).
+// Queue the flagged lanes' nodes (NK candidates per lane): one tail add per call.
+template <int NK>
+__device__ __forceinline__ void append_q(const bool* app, const uint32_t* v, uint16_t* ring, uint32_t* tail,
+                                         const RingMod& slot_of, int lane) {
+  const uint64_t lt = (1ull << lane) - 1;
+  uint64_t mq[NK];  // (NK <= 16)
+  uint32_t tot = 0;
+#pragma unroll
+  for (int c = 0; c < NK; c++) {
+    mq[c] = __ballot(app[c]);
+    tot += (uint32_t)__popcll(mq[c]);
+  }
+  if (!tot) return;
+  uint32_t b = 0;
+  if (lane == 0) b = atomicAdd(tail, tot);
+  b = __builtin_amdgcn_readfirstlane(b);
+#pragma unroll
+  for (int c = 0; c < NK; c++) {
+    if (app[c]) ring[slot_of(b + (uint32_t)__popcll(mq[c] & lt))] = (uint16_t)v[c];
+    b += (uint32_t)__popcll(mq[c]);
+  }
+}
+
+// LDS bytes the kernel needs for n nodes (dynamic part): keys, staged out-arc
+// offsets, the queue ring.
 size_t sssp_lds_bytes(uint32_t n) {
-  const size_t words = (n + 31) / 32;
-  return (size_t)n * 8 + words * 4 + (size_t)sssp_ring_cap(n) * 2;
+  return (size_t)n * 8 + (((size_t)n + 1) * 4 + 7) / 8 * 8 + (size_t)sssp_ring_cap(n) * 2;
 }
 
 // One workgroup per source row i in [row_begin, row_end): source used[i].
 // out_arc: 3 u32 per out-arc (destination, latency clamped to LAT32_SAT,
 // bits(1f32 - loss)), grouped by tail node (out_off).
-template <bool COUNT>
-__global__ void __launch_bounds__(SSSP_THREADS)
+template <bool COUNT, int NT, int LA>
+__global__ void __launch_bounds__(NT)
     k_sssp_lds(const uint32_t* __restrict__ out_off, const uint32_t* __restrict__ out_arc, uint32_t n,
                uint32_t n_arcs, const uint32_t* __restrict__ used, uint32_t n_used, uint32_t row_begin,
                uint32_t out_row0, const uint32_t* __restrict__ self_edge, const uint64_t* __restrict__ e_lat,
                const float* __restrict__ e_loss, uint64_t* __restrict__ out_lat, float* __restrict__ out_loss,
                uint32_t* __restrict__ sat_row, uint32_t delta, int vec_out, unsigned long long* __restrict__ work,
-               unsigned long long* __restrict__ diag) {
+               unsigned long long* __restrict__ diag, uint32_t claim, uint32_t idle_sleep,
+               uint32_t lane_deg_max) {
+  constexpr int NW = NT / 64;
   extern __shared__ __align__(16) unsigned char smem[];
-  const uint32_t W = (n + 31) / 32;
-  const uint32_t cap = sssp_ring_cap(n), cmask = cap - 1;
-  uint64_t* key = (uint64_t*)smem;
-  uint32_t* dirty = (uint32_t*)(key + n);
-  uint16_t* ring = (uint16_t*)(dirty + W);
+  const uint32_t cap = sssp_ring_cap(n);
+  const RingMod slot_of{cap, (uint32_t)(0x100000000ull / cap)};
+  unsigned long long* key = (unsigned long long*)smem;
+  uint32_t* off = (uint32_t*)(key + n);  // out_off staged in LDS (n + 1)
+  uint16_t* ring = (uint16_t*)(smem + (size_t)n * 8 + (((size_t)n + 1) * 4 + 7) / 8 * 8);
   __shared__ uint32_t ctl[8];  // TAIL
   constexpr int TAIL = 1;
   // (head << 32) | busy in one word: a claim advances head and counts its wave
   // busy in one CAS, so a failed claim attempt never touches busy
   __shared__ unsigned long long hb;
-  __shared__ uint8_t own[SSSP_WAVES][64 * SSSP_K];
-  __shared__ uint32_t red[SSSP_WAVES];
+  __shared__ uint8_t own[NW][64 * SSSP_K];
+  __shared__ uint32_t red[NW];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // COUNT diagnostics of the first 4096 rows: cycle stamps, pops, bucket advances, relaxations
   const bool dg = COUNT && diag && blockIdx.x < 4096 && tid == 0;
   const unsigned long long c_start = dg ? clock64() : 0;
   uint32_t n_adv = 0, n_pops = 0;
+  unsigned long long cyc_claim = 0, cyc_pop = 0, cyc_steps = 0;  // per wave, COUNT diagnostics
   const uint32_t row = row_begin + blockIdx.x;
   const uint32_t src = used[row];
-  for (uint32_t v = tid; v < n; v += SSSP_THREADS) key[v] = KEY_INF;
-  for (uint32_t w = tid; w < W; w += SSSP_THREADS) dirty[w] = 0;
-  for (uint32_t i = tid; i < cap; i += SSSP_THREADS) ring[i] = RING_EMPTY;
-  for (int i = tid; i < SSSP_WAVES * 64 * SSSP_K; i += SSSP_THREADS) (&own[0][0])[i] = 0;
+  for (uint32_t v = tid; v < n; v += NT) key[v] = FKEY_INF;
+  for (uint32_t v = tid; v <= n; v += NT) off[v] = out_off[v];
+  for (uint32_t i = tid; i < cap; i += NT) ring[i] = RING_EMPTY;
+  for (int i = tid; i < NW * 64 * SSSP_K; i += NT) (&own[0][0])[i] = 0;
   if (tid < 8) ctl[tid] = 0;
   if (tid == 0) hb = 0;
   __syncthreads();
   if (tid == 0) {
-    key[src] = 0;  // PathProperties::default()
-    dirty[src >> 5] = 1u << (src & 31);
+    key[src] = 1ull;  // PathProperties::default(), dirty and queued
     ring[0] = (uint16_t)src;
     ctl[TAIL] = 1;
   }
@@ -172,24 +203,31 @@ __global__ void __launch_bounds__(SSSP_THREADS)
   const uint32_t max_adv = 4u * n + 64u;
   bool gave_up = false;
   uint8_t* ow = own[wv];
-  const uint64_t lt = (1ull << lane) - 1;
-  // spin budget per wave (sleeps of ~64 cycles): a safety valve against a
+  // spin budget per wave (sleeps of ~128 cycles): a safety valve against a
   // queue bug, never reached by a correct search; past it the wave leaves and
   // the row goes to the wide kernel
   uint32_t spins = 0;
   constexpr uint32_t SPIN_MAX = 1u << 22;
   auto ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+  // relax one candidate into key[v]; true when v became dirty below split (to be queued)
+  auto offer = [&](bool valid, uint32_t v, uint64_t cand) -> bool {
+    if (!valid || fkey_lat(cand) == LAT32_SAT) return false;  // saturated keys are never propagated
+    const uint64_t old = __hip_atomic_fetch_min(&key[v], (unsigned long long)cand, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+    return (old >> 1) > (cand >> 1) && !(old & 1ull) && fkey_lat(cand) < split;
+  };
   __syncthreads();
 
   for (;;) {
-    // ---- claim up to 64 queued entries
+    // ---- claim up to `claim` queued entries
+    const unsigned long long tc0 = (COUNT && diag) ? clock64() : 0;
     uint32_t h = 0, k = 0;
     if (lane == 0) {
       for (;;) {
         const unsigned long long w = __hip_atomic_load(&hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const uint32_t hh = (uint32_t)(w >> 32), t = ld(&ctl[TAIL]);
         if (t == hh) break;
-        const uint32_t kk = min(64u, t - hh);
+        const uint32_t kk = min(claim, t - hh);
         const unsigned long long nw = ((unsigned long long)(hh + kk) << 32) | ((w & 0xFFFFFFFFull) + 1);
         if (atomicCAS(&hb, w, nw) == w) {
           h = hh;
@@ -212,71 +250,56 @@ __global__ void __launch_bounds__(SSSP_THREADS)
           gave_up = true;
           break;
         }
+        for (uint32_t z = 0; z < idle_sleep; z++) __builtin_amdgcn_s_sleep(8);  // ~512 cycles each
         __builtin_amdgcn_s_sleep(2);
         continue;
       }
       // ---- quiescent: every wave is here.  Next bucket, or done.
       __syncthreads();
       uint32_t m = LAT32_SAT;
-      for (uint32_t w = tid; w < W; w += SSSP_THREADS) {
-        uint32_t bits = dirty[w];
-        while (bits) {
-          const uint32_t v = w * 32 + (uint32_t)__builtin_ctz(bits);
-          bits &= bits - 1;
-          m = min(m, key_lat(key[v]));
-        }
+      for (uint32_t v = tid; v < n; v += NT) {
+        const uint64_t kv = key[v];
+        if (kv & 1ull) m = min(m, fkey_lat(kv));
       }
       for (int d = 32; d > 0; d >>= 1) m = min(m, (uint32_t)__shfl_xor(m, d));
       if (lane == 0) red[wv] = m;
       __syncthreads();
       m = red[0];
-      for (int w = 1; w < SSSP_WAVES; w++) m = min(m, red[w]);
+      for (int w = 1; w < NW; w++) m = min(m, red[w]);
       if (m == LAT32_SAT) break;  // nothing dirty (saturated keys are never marked dirty)
       if (++n_adv > max_adv) {
         gave_up = true;
         break;
       }
       split = m + delta >= m ? min(m + delta, LAT32_SAT) : LAT32_SAT;
-      for (uint32_t w0 = wv * 64; w0 < W; w0 += SSSP_THREADS) {  // queue the dirty nodes below split
-        const uint32_t w = w0 + lane;
-        uint32_t bits = w < W ? dirty[w] : 0u;
-        for (;;) {
-          const bool has = bits != 0;
-          if (!__ballot(has)) break;
-          const uint32_t v = has ? w * 32 + (uint32_t)__builtin_ctz(bits) : 0u;
-          bits &= bits - 1;
-          const bool q2 = has && key_lat(key[v]) < split;
-          const uint64_t mq = __ballot(q2);
-          if (mq) {
-            uint32_t b = 0;
-            if (lane == 0) b = atomicAdd(&ctl[TAIL], (uint32_t)__popcll(mq));
-            b = __builtin_amdgcn_readfirstlane(b);
-            if (q2) ring[(b + (uint32_t)__popcll(mq & lt)) & cmask] = (uint16_t)v;
-          }
-        }
+      for (uint32_t v0 = wv * 64; v0 < n; v0 += NT) {  // queue the dirty nodes below split
+        const uint32_t v = v0 + lane;
+        uint64_t kv = v < n ? key[v] : 0ull;
+        const bool q2 = (kv & 1ull) && fkey_lat(kv) < split;
+        append_q<1>(&q2, &v, ring, &ctl[TAIL], slot_of, lane);
       }
       __syncthreads();
       continue;
     }
     if (COUNT) n_pops++;
+    const unsigned long long tc1 = (COUNT && diag) ? clock64() : 0;
     // ---- pop the claimed entries (a slot claimed before its writer stored it reads EMPTY)
     const bool on = lane < (int)k;
     uint32_t u = 0, a0 = 0, a1 = 0;
     uint64_t ku = 0;
     bool stuck = false;
     if (on) {
-      volatile uint16_t* slot = &ring[(h + lane) & cmask];
+      volatile uint16_t* slot = &ring[slot_of(h + lane)];
       uint16_t x;
       uint32_t sp = 0;
       while ((x = *slot) == RING_EMPTY && ++sp < SPIN_MAX) __builtin_amdgcn_s_sleep(0);
       stuck = x == RING_EMPTY;
       *slot = RING_EMPTY;
       u = stuck ? src : x;
-      a0 = out_off[u];
-      a1 = out_off[u + 1];
-      lds_clear_bits(&dirty[u >> 5], 1u << (u & 31));  // before the key read (see header)
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      ku = key[u];
+      a0 = off[u];
+      a1 = off[u + 1];
+      // clear the dirty flag; the returned key is the one to relax with (see header)
+      ku = __hip_atomic_fetch_and(&key[u], ~1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~1ull;
     }
     if (__any(stuck)) {
       if (lane == 0) atomicSub(&hb, 1ull);
@@ -284,89 +307,84 @@ __global__ void __launch_bounds__(SSSP_THREADS)
       break;
     }
     const uint32_t deg = a1 - a0;
-    const uint32_t incl = wave_incl_sum(deg);
-    const uint32_t base = incl - deg;
-    const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
-    if (COUNT) n_rel += T;
-    uint32_t carry = 0;  // 1 + the owner lane of the previous slot
-    // NK chunks of 64 slots, straight-line (no per-chunk branch: a branch join
-    // would make the compiler drain every load before the next is issued)
-    auto step = [&](uint32_t t0, auto nk_c) {
-      constexpr int NK = decltype(nk_c)::value;
-      // owner lane of each slot: heads scatter 1 + their lane at their first slot, a max-scan fills the rest
-      if (deg && base >= t0 && base - t0 < 64u * NK) ow[base - t0] = (uint8_t)(lane + 1);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      uint32_t v[NK], lat[NK], om[NK], o[NK];
-      uint64_t cand[NK];
-      bool valid[NK], imp[NK], app[NK];
+    const uint32_t dmax = __builtin_amdgcn_readlane(wave_incl_max(deg), 63);
+    const unsigned long long tc2 = (COUNT && diag) ? clock64() : 0;
+    if (dmax <= lane_deg_max) {
+      // ---- lane path: each lane walks its own node's arcs, LANE_ARCS loads in flight
+      if (COUNT) n_rel += __builtin_amdgcn_readlane(wave_incl_sum(deg), 63);
+      for (uint32_t j0 = 0; j0 < dmax; j0 += LA) {
+        uint32_t v[LA], lat[LA], om[LA];
+        bool valid[LA], app[LA];
 #pragma unroll
-      for (int c = 0; c < NK; c++) {
-        const uint32_t hd = ow[c * 64 + lane];
-        ow[c * 64 + lane] = 0;
-        const uint32_t m = max(wave_incl_max(hd), carry);
-        carry = __builtin_amdgcn_readlane(m, 63);
-        o[c] = m - 1;
-      }
-#pragma unroll
-      for (int c = 0; c < NK; c++) {
-        const uint32_t sl = t0 + c * 64 + lane;
-        valid[c] = sl < T;
-        const uint32_t a = __shfl(a0, (int)o[c]) + sl - __shfl(base, (int)o[c]);
-        const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid[c] ? a * 12u : 0x80000000u, 0, 0);
-        v[c] = r[0];
-        lat[c] = r[1];
-        om[c] = r[2];
-      }
-#pragma unroll
-      for (int c = 0; c < NK; c++) {
-        const uint32_t klo = __shfl((uint32_t)ku, (int)o[c]), khi = __shfl((uint32_t)(ku >> 32), (int)o[c]);
-        cand[c] = relax32(((uint64_t)khi << 32) | klo, lat[c], __uint_as_float(om[c]));
-        // a saturated key is never propagated (see header); an invalid slot offers KEY_INF
-        if (!valid[c] || key_lat(cand[c]) == LAT32_SAT) cand[c] = KEY_INF;
-      }
-#pragma unroll
-      for (int c = 0; c < NK; c++) {
-        const uint64_t old = __hip_atomic_fetch_min((unsigned long long*)&key[valid[c] ? v[c] : 0],
-                                                    (unsigned long long)cand[c], __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
-        imp[c] = cand[c] < old;
-      }
-      uint32_t tot = 0;
-      uint64_t mq[NK];
-#pragma unroll
-      for (int c = 0; c < NK; c++) {
-        app[c] = false;
-        if (imp[c]) {  // issued after the min returned (control dependence): see header
-          const uint32_t bit = 1u << (v[c] & 31);
-          app[c] = !(lds_fetch_or(&dirty[v[c] >> 5], bit) & bit) && key_lat(cand[c]) < split;
+        for (int c = 0; c < LA; c++) {
+          valid[c] = j0 + c < deg;
+          const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid[c] ? (a0 + j0 + c) * 12u : 0x80000000u,
+                                                              0, 0);
+          v[c] = r[0];
+          lat[c] = r[1];
+          om[c] = r[2];
         }
-        mq[c] = __ballot(app[c]);
-        tot += (uint32_t)__popcll(mq[c]);
-      }
-      if (tot) {
-        uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(&ctl[TAIL], tot);
-        b = __builtin_amdgcn_readfirstlane(b);
 #pragma unroll
-        for (int c = 0; c < NK; c++) {
-          if (app[c]) ring[(b + (uint32_t)__popcll(mq[c] & lt)) & cmask] = (uint16_t)v[c];
-          b += (uint32_t)__popcll(mq[c]);
-        }
+        for (int c = 0; c < LA; c++) app[c] = offer(valid[c], v[c], frelax(ku, lat[c], __uint_as_float(om[c])));
+        append_q<LA>(app, v, ring, &ctl[TAIL], slot_of, lane);
       }
-    };
-    for (uint32_t t0 = 0; t0 < T; t0 += 64 * SSSP_K) {
-      if (T - t0 > 64) step(t0, std::integral_constant<int, SSSP_K>{});
-      else step(t0, std::integral_constant<int, 1>{});
+    } else {
+      // ---- expansion path (high out-degree): arcs of the 64 entries in consecutive slots
+      const uint32_t incl = wave_incl_sum(deg);
+      const uint32_t base = incl - deg;
+      const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+      if (COUNT) n_rel += T;
+      uint32_t carry = 0;  // 1 + the owner lane of the previous slot
+      for (uint32_t t0 = 0; t0 < T; t0 += 64 * SSSP_K) {
+        // owner lane of each slot: heads scatter 1 + their lane at their first slot, a max-scan fills the rest
+        if (deg && base >= t0 && base - t0 < 64u * SSSP_K) ow[base - t0] = (uint8_t)(lane + 1);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t v[SSSP_K], lat[SSSP_K], om[SSSP_K], o[SSSP_K];
+        bool valid[SSSP_K], app[SSSP_K];
+#pragma unroll
+        for (int c = 0; c < SSSP_K; c++) {
+          const uint32_t hd = ow[c * 64 + lane];
+          ow[c * 64 + lane] = 0;
+          const uint32_t mx = max(wave_incl_max(hd), carry);
+          carry = __builtin_amdgcn_readlane(mx, 63);
+          o[c] = mx - 1;
+        }
+#pragma unroll
+        for (int c = 0; c < SSSP_K; c++) {
+          const uint32_t sl = t0 + c * 64 + lane;
+          valid[c] = sl < T;
+          const uint32_t a = __shfl(a0, (int)o[c]) + sl - __shfl(base, (int)o[c]);
+          const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid[c] ? a * 12u : 0x80000000u, 0, 0);
+          v[c] = r[0];
+          lat[c] = r[1];
+          om[c] = r[2];
+        }
+#pragma unroll
+        for (int c = 0; c < SSSP_K; c++) {
+          const uint32_t klo = __shfl((uint32_t)ku, (int)o[c]), khi = __shfl((uint32_t)(ku >> 32), (int)o[c]);
+          app[c] = offer(valid[c], v[c], frelax(((uint64_t)khi << 32) | klo, lat[c], __uint_as_float(om[c])));
+        }
+        append_q<SSSP_K>(app, v, ring, &ctl[TAIL], slot_of, lane);
+      }
     }
     // release the claim after this wave's appends (LDS keeps a wave's operations in order)
     if (lane == 0) atomicSub(&hb, 1ull);
+    if (COUNT && diag) {
+      const unsigned long long tc3 = clock64();
+      cyc_claim += tc1 - tc0;
+      cyc_pop += tc2 - tc1;
+      cyc_steps += tc3 - tc2;
+    }
   }
   if (COUNT && lane == 0 && n_rel) atomicAdd(&work[blockIdx.x & 63], (unsigned long long)n_rel);
   if (COUNT && diag && blockIdx.x < 4096 && lane == 0) {
     if (n_rel) atomicAdd(&diag[blockIdx.x * 8 + 4], (unsigned long long)n_rel);
     if (n_pops) atomicAdd(&diag[blockIdx.x * 8 + 2], (unsigned long long)n_pops);
+    atomicAdd(&diag[blockIdx.x * 8 + 5], cyc_claim);
+    atomicAdd(&diag[blockIdx.x * 8 + 6], cyc_pop);
+    atomicAdd(&diag[blockIdx.x * 8 + 7], cyc_steps);
   }
   const unsigned long long c_search = dg ? clock64() : 0;
 
@@ -379,16 +397,16 @@ __global__ void __launch_bounds__(SSSP_THREADS)
       l = e_lat[e];
       f = e_loss[e];
     } else {
-      const uint64_t k = key[used[j]];
-      sat |= key_lat(k) == LAT32_SAT;
-      l = key_lat(k);
-      f = __uint_as_float(key_loss_bits(k));
+      const uint64_t kk = key[used[j]];
+      sat |= fkey_lat(kk) == LAT32_SAT;
+      l = fkey_lat(kk);
+      f = __uint_as_float(fkey_loss_bits(kk));
     }
   };
   if (vec_out) {  // n_used % 4 == 0, 16-B aligned rows: 16-B nontemporal stores
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     typedef float f32x4 __attribute__((ext_vector_type(4)));
-    for (uint32_t j = tid * 4; j < n_used; j += SSSP_THREADS * 4) {
+    for (uint32_t j = tid * 4; j < n_used; j += NT * 4) {
       uint64_t l0, l1, l2, l3;
       float f0, f1, f2, f3;
       entry(j, l0, f0);
@@ -400,7 +418,7 @@ __global__ void __launch_bounds__(SSSP_THREADS)
       __builtin_nontemporal_store((f32x4){f0, f1, f2, f3}, (f32x4*)&out_loss[orow + j]);
     }
   } else {
-    for (uint32_t j = tid; j < n_used; j += SSSP_THREADS) {
+    for (uint32_t j = tid; j < n_used; j += NT) {
       uint64_t l;
       float f;
       entry(j, l, f);
@@ -431,21 +449,35 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
   const size_t lds = sssp_lds_bytes(n);
   if (!sssp_lds_fits(n)) throw Error(SG_ERR_INVALID_ARG, "graph too large for the LDS-resident search");
   if ((uint64_t)n_arcs * 12 >= (1ull << 31)) throw Error(SG_ERR_INVALID_ARG, "too many arcs for 32-bit offsets");
+  // entries a wave claims at once (SG_SSSP_CLAIM, 1..64)
+  const char* cs = getenv("SG_SSSP_CLAIM");
+  const uint32_t claim = (uint32_t)std::min(64, std::max(1, cs && *cs ? atoi(cs) : 64));
   const int vec = n_used % 4 == 0 && ((uintptr_t)out_lat & 15) == 0 && ((uintptr_t)out_loss & 15) == 0;
   const uint32_t rows = row_end - row_begin;
   if (!rows) return;
+  const char* ts = getenv("SG_SSSP_THREADS");
+  const int nt = ts && atoi(ts) == 512 ? 512 : 1024;
+  const char* ss = getenv("SG_SSSP_SLEEP");  // idle back-off, units of ~512 cycles
+  const uint32_t idle_sleep = ss && *ss ? (uint32_t)std::max(0, atoi(ss)) : 0u;
+  const char* ls = getenv("SG_SSSP_LANE_DEG");
+  const uint32_t lane_deg = ls && *ls ? (uint32_t)std::max(0, atoi(ls)) : 32u;
+  const char* la = getenv("SG_SSSP_LANE_ARCS");
+  const int la16 = la && atoi(la) == 16;
+  auto go = [&](auto kern) {
+    SG_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(LDS_PER_CU - SSSP_STATIC_LDS)));
+    hipLaunchKernelGGL(kern, dim3(rows), dim3(nt), lds, ctx->stream, out_off, out_arc, n, n_arcs, d_used, n_used,
+                       row_begin, row_begin, self_edge, e_lat, e_loss, out_lat, out_loss, sat_row, delta, vec, work,
+                       diag, claim, idle_sleep, lane_deg);
+  };
   if (work) {
-    SG_HIP(hipFuncSetAttribute((const void*)k_sssp_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)(LDS_PER_CU - SSSP_STATIC_LDS)));
-    hipLaunchKernelGGL(k_sssp_lds<true>, dim3(rows), dim3(SSSP_THREADS), lds, ctx->stream, out_off, out_arc, n,
-                       n_arcs, d_used, n_used, row_begin, row_begin, self_edge, e_lat, e_loss, out_lat, out_loss,
-                       sat_row, delta, vec, work, diag);
+    if (nt == 512) go(k_sssp_lds<true, 512, 8>);
+    else if (la16) go(k_sssp_lds<true, 1024, 16>);
+    else go(k_sssp_lds<true, 1024, 8>);
   } else {
-    SG_HIP(hipFuncSetAttribute((const void*)k_sssp_lds<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)(LDS_PER_CU - SSSP_STATIC_LDS)));
-    hipLaunchKernelGGL(k_sssp_lds<false>, dim3(rows), dim3(SSSP_THREADS), lds, ctx->stream, out_off, out_arc, n,
-                       n_arcs, d_used, n_used, row_begin, row_begin, self_edge, e_lat, e_loss, out_lat, out_loss,
-                       sat_row, delta, vec, work, diag);
+    if (nt == 512) go(k_sssp_lds<false, 512, 8>);
+    else if (la16) go(k_sssp_lds<false, 1024, 16>);
+    else go(k_sssp_lds<false, 1024, 8>);
   }
   SG_CHECK_LAUNCH();
 }

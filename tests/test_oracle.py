@@ -288,3 +288,19 @@ def test_deliver_round_multithreaded_equals_sequential(oracle, threads):
         assert np.array_equal(a[k], b[k]), k
     assert (a["delivered"], a["min_deliver"], a["min_lat"]) == (b["delivered"], b["min_deliver"], b["min_lat"])
     assert np.array_equal(ra, rb) and np.array_equal(ca, cb)
+
+
+@pytest.mark.parametrize("directed", [False, True])
+def test_faithful_routing_build_matches_dense(oracle, directed):
+    """The reference-cost CPU baseline (SipHash maps, contains filter, global map,
+    id remap; sg_faithful.c) builds the same table as the dense restatement."""
+    g = synth.ring_chords_graph(300, 6.0, seed=4, directed=directed, parallel=0.02)
+    used = np.random.default_rng(4).permutation(300)[:220].astype(np.uint32)
+    ids = (np.arange(300) * 7 + 3).astype(np.uint32)
+    rc, lat, loss, _ = oracle.shortest_paths(300, g["src"], g["dst"], g["lat"], g["loss"], directed, used, threads=2)
+    assert rc == 0
+    rc2, flat, floss, ph = oracle.routing_faithful(300, g["src"], g["dst"], g["lat"], g["loss"], directed, used,
+                                                   rows=150, node_ids=ids, threads=3)
+    assert rc2 == 0 and all(t >= 0 for t in ph)
+    assert np.array_equal(flat, lat[:150])
+    assert np.array_equal(floss.view(np.uint32), loss[:150].view(np.uint32))
