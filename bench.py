@@ -33,7 +33,34 @@ HBM_PEAK_GBS = 8000.0
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 # L2: 4 MiB per XCD, ~34.5 TB/s aggregate (MI355X_MICROARCH.md, "L2 (per XCD)")
 L2_PEAK_GBS = 34500.0
-ROW_BYTES_PER_RELAX = 8  # one 8-B packed key gathered per lane-relaxation (512-B row per 64 sources)
+ROW_BYTES_PER_RELAX = 8  # slab kernel: one 8-B packed key gathered per lane-relaxation (512-B row per 64 sources)
+ARC_BYTES_PER_RELAX = 12  # LDS search: one 12-B out-arc record (head, latency, 1 - loss) read per relaxation
+FAITHFUL_ROWS = 400  # sources in the reference-faithful CPU sample (~10 s of CPU work at C3 on 16 threads)
+
+
+def _cpu_info():
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    # the CPU share this process may use: the GPU box grants 16 logical CPUs per GPU (a
+    # quota, while all of the host's CPUs stay visible) and says so in OMP_NUM_THREADS
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or visible
+    return {"nproc": min(share, visible), "nproc_visible": visible, "cpu_model": model}
+
+
+CPU_INFO = _cpu_info()
+# the reference's pools: rayon's global pool for APSP = all logical CPUs; the worker
+# threads = the physical cores (manager.rs:254-261).  Both are the CPU share here:
+# more threads than the share only time-slice on it (r02: 256 threads on the 16-CPU
+# share took 1.55 s for the dense C3 baseline, 16 threads 1.17 s).
+CPU_THREADS = CPU_INFO["nproc"]
 T0 = 946684800 * 10**9  # EmulatedTime SIMULATION_START
 
 
@@ -236,7 +263,7 @@ def codel_leg(a, D, ctx, torch, buckets, n_packets, pmc):
         t0 = time.perf_counter()
         O.codel_run(st, *evs, ost)
         tc = time.perf_counter() - t0
-        leg["cpu_baseline"] = {"value": round(E / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port",
+        leg["cpu_baseline"] = {"value": round(E / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port", **CPU_INFO,
                                "sample": f"the same {E} events through the C restatement of codel_queue.rs, 1 thread"}
     return leg
 
@@ -320,7 +347,7 @@ def outbound_leg(a, D, ctx, torch, pk, hosts, ht, table, round_end, sharded, pmc
         O.outbound_run(st, pk["src"], pk["send_time"], pkt, ln, pk["payload"], pk["dst_ip"], round_end, 0, 2**63,
                        ctr, ofwd, ost)
         tc = time.perf_counter() - t0
-        leg["cpu_baseline"] = {"value": round(n / tc, 1), "unit": "sends/s", "cores": 1, "kind": "port",
+        leg["cpu_baseline"] = {"value": round(n / tc, 1), "unit": "sends/s", "cores": 1, "kind": "port", **CPU_INFO,
                                "sample": f"the same {n} sends through the C restatement (interface fifo + "
                                          "relay/mod.rs + token_bucket.rs), 1 thread"}
     return leg
@@ -385,7 +412,7 @@ def inbound_leg(a, D, ctx, torch, buckets, n_packets, pmc, round_end):
         t0 = time.perf_counter()
         O.inbound_run(st, host, t, order, ln, window_end, 0, 2**63, ctr, ofwd, ost)
         tc = time.perf_counter() - t0
-        leg["cpu_baseline"] = {"value": round(nd / tc, 1), "unit": "arrivals/s", "cores": 1, "kind": "port",
+        leg["cpu_baseline"] = {"value": round(nd / tc, 1), "unit": "arrivals/s", "cores": 1, "kind": "port", **CPU_INFO,
                                "sample": f"the same {nd} arrivals through the C restatement (codel_queue.rs + "
                                          "relay/mod.rs + token_bucket.rs), 1 thread"}
         leg["parity_vs_cpu"] = bool(np.array_equal(ost, status.cpu().numpy()))
@@ -463,12 +490,12 @@ def c2_leg(a, ctx, torch, NetworkGraph, synth, with_cpu):
     if with_cpu:
         from oracle import oracle as O  # the checker, timed as the CPU baseline
 
-        th = min(16, os.cpu_count() or 1)
+        th = CPU_THREADS
         t0 = time.perf_counter()
         rc, olat, oloss, _ = O.shortest_paths(n, g["src"], g["dst"], g["lat"], g["loss"], False, used, threads=th)
         tc = time.perf_counter() - t0
         assert rc == 0
-        leg["cpu_baseline"] = {"value": round(tc, 4), "unit": "s", "cores": th, "kind": "port",
+        leg["cpu_baseline"] = {"value": round(tc, 4), "unit": "s", "cores": th, "kind": "port", **CPU_INFO,
                                "sample": f"all {n} sources (binary-heap Dijkstra, dense output), {th} threads"}
         leg["speedup_vs_cpu"] = round(tc / t_build, 1)
         leg["parity_vs_cpu"] = bool(
@@ -520,53 +547,122 @@ def main():
 
     t_build = timed(D, build, a.steps, a.warmup)
     t_allgather = timed(D, allgather, max(1, a.steps // 2), 1) if D.dist else 0.0
-    # instrumented passes on the kernel's own stream: HIP-event launch times, then
-    # (separately, the counting variant is slower) the lane-relaxations performed
+    # instrumented build on the kernel's own stream: HIP-event launch times, then
+    # (separately, the counting variant is slower) the relaxations performed
     ctx.enable_timers(True)
     build()
-    relax_ms, relax_launches, _ = ctx.read_timer("relax")
-    out_ms, _, out_bytes = ctx.read_timer("out")
+    timers = {k: ctx.read_timer(k) for k in ("sssp", "relax", "out", "relax_wide")}
     ctx.enable_timers(True, count_work=True)
     build()
-    _, _, relax_work = ctx.read_timer("relax")
+    works = {k: ctx.read_timer(k)[2] for k in ("sssp", "relax")}
     ctx.enable_timers(False)
     n_arcs = int(net.edge_src.size * 2 - 2 * np.count_nonzero(net.edge_src == net.edge_dst))
-    avg_launch_s = relax_ms / 1e3 / max(relax_launches, 1)
-    relax_per_launch = relax_work / max(relax_launches, 1)
-    # bound: the 512-B key rows every relaxed in-arc gathers from the batch slab,
-    # served by L2 / Infinity Cache (the slab is on chip; HBM traffic is the
-    # PMC "traffic" figure)
-    gather_bytes = ROW_BYTES_PER_RELAX * relax_per_launch
-    achieved = gather_bytes / avg_launch_s / 1e9 if relax_launches else 0.0
-    pm = pmc.get("relax", {})
-    roofline = {"kernel": "k_relax_w2", "bound": "l2", "achieved": round(achieved, 1), "peak": L2_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / L2_PEAK_GBS, 4),
-                "traffic": pm.get("hbm_bytes_per_launch"),
-                "algorithmic_bytes_per_launch": gather_bytes,
-                "avg_launch_ms": round(avg_launch_s * 1e3, 4), "launches_per_build": relax_launches,
-                "lane_relaxations_per_launch": relax_per_launch,
-                "valu_frac_pmc": pm.get("valu_frac")}
-    if pm.get("hbm_bytes_per_launch") and relax_launches:
-        # the same launches against HBM: PMC bytes per launch over the launch time
-        hbm = pm["hbm_bytes_per_launch"] / avg_launch_s / 1e9
-        roofline["hbm_view"] = {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": round(hbm / HBM_PEAK_GBS, 4)}
+    rows_mine = r1 - r0
+    dijkstra_relax = float(rows_mine) * n_arcs  # per-source Dijkstra: every arc of every source once
+    lds = timers["sssp"][1] > 0
+    pm = pmc.get("sssp" if lds else "relax", {})
+    if lds:
+        # k_sssp_lds, one launch per build: a 12-B arc record gathered from L2 per
+        # relaxation; its HBM traffic is the 12-B (latency, loss) cell per table entry
+        k_ms, k_n, _ = timers["sssp"]
+        k_s = k_ms / 1e3 / max(k_n, 1)
+        relax_per_launch = works["sssp"] / max(k_n, 1)
+        gather_bytes = ARC_BYTES_PER_RELAX * relax_per_launch
+        out_bytes = 12.0 * rows_mine * nu / max(k_n, 1)
+        achieved = gather_bytes / k_s / 1e9 if k_n else 0.0
+        roofline = {"kernel": "k_sssp_lds", "bound": "l2", "achieved": round(achieved, 1), "peak": L2_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / L2_PEAK_GBS, 4), "traffic": pm.get("hbm_bytes_per_launch"),
+                    "algorithmic_bytes_per_launch": gather_bytes + out_bytes,
+                    "avg_launch_ms": round(k_s * 1e3, 4), "launches_per_build": k_n,
+                    "relaxations_per_launch": relax_per_launch,
+                    "redundancy_vs_dijkstra": round(relax_per_launch * max(k_n, 1) / max(dijkstra_relax, 1.0), 3),
+                    "valu_frac_pmc": pm.get("valu_frac"),
+                    "hbm_view": {"achieved": round(out_bytes / k_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(out_bytes / k_s / 1e9 / HBM_PEAK_GBS, 4),
+                                 "what": "the row-major table written (12 B per cell)"}}
+    else:
+        relax_ms, relax_launches, _ = timers["relax"]
+        avg_launch_s = relax_ms / 1e3 / max(relax_launches, 1)
+        relax_per_launch = works["relax"] / max(relax_launches, 1)
+        # the 512-B key rows every relaxed in-arc gathers from the batch slab (L2 / Infinity Cache)
+        gather_bytes = ROW_BYTES_PER_RELAX * relax_per_launch
+        achieved = gather_bytes / avg_launch_s / 1e9 if relax_launches else 0.0
+        roofline = {"kernel": "k_relax_w2", "bound": "l2", "achieved": round(achieved, 1), "peak": L2_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / L2_PEAK_GBS, 4), "traffic": pm.get("hbm_bytes_per_launch"),
+                    "algorithmic_bytes_per_launch": gather_bytes,
+                    "avg_launch_ms": round(avg_launch_s * 1e3, 4), "launches_per_build": relax_launches,
+                    "lane_relaxations_per_launch": relax_per_launch,
+                    "redundancy_vs_dijkstra": round(relax_per_launch * relax_launches / max(dijkstra_relax, 1.0), 3),
+                    "valu_frac_pmc": pm.get("valu_frac")}
+        if pm.get("hbm_bytes_per_launch") and relax_launches:
+            hbm = pm["hbm_bytes_per_launch"] / avg_launch_s / 1e9
+            roofline["hbm_view"] = {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": round(hbm / HBM_PEAK_GBS, 4)}
+    # the batched-source slab kernel on the same rows, for comparison (the default above 10.9k nodes)
+    t_slab = None
+    if lds:
+        os.environ["SG_APSP_LDS"] = "0"
+        t_slab = timed(D, build, max(1, a.steps // 2), 1)
+        os.environ.pop("SG_APSP_LDS")
+
+    # end to end: the whole table into the dense host RoutingInfo (sg_routing_info_fill:
+    # row blocks built on the GPU, copied into pinned host memory while the next builds)
+    e2e = None
+    if D.world == 1:
+        from shadow_amd import RoutingInfo
+
+        ri = RoutingInfo(np.arange(nu, dtype=np.uint32))
+        ri.fill(net, used, True)  # warm-up (and the pinned pages touched once)
+        torch.cuda.synchronize()
+        reps = max(1, a.steps // 2)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ri.fill(net, used, True)
+        t_e2e = (time.perf_counter() - t0) / reps
+        same = bool(np.array_equal(ri.latency_ns[: r1 - r0], my_lat.cpu().numpy().view(np.uint64).reshape(-1, nu)[
+                    : r1 - r0]))
+        e2e = {"ms": round(t_e2e * 1e3, 3), "pinned": ri.pinned, "table_bytes": 12 * nu * nu,
+               "d2h_GBs": round(12.0 * nu * nu / t_e2e / 1e9, 1), "same_as_device_table": same,
+               "what": "sg_routing_info_fill: kernel + D2H of the whole table into the dense host RoutingInfo"}
+        del ri
 
     cpu = None
+    parity = None
+    cpu_faithful = None
     if D.rank == 0 and D.world == 1 and not a.no_cpu:
         from oracle import oracle as O  # the checker, timed as the CPU baseline
 
-        threads = min(16, os.cpu_count() or 1)
+        threads = CPU_THREADS
         k = nu if a.cpu_rows <= 0 else min(a.cpu_rows, nu)
         t0 = time.perf_counter()
-        rc, _, _, _ = O.shortest_paths(g["n"], g["src"], g["dst"], g["lat"], g["loss"], False, used, rows=(0, k),
-                                       threads=threads)
+        rc, olat, oloss, _ = O.shortest_paths(g["n"], g["src"], g["dst"], g["lat"], g["loss"], False, used,
+                                              rows=(0, k), threads=threads)
         t_cpu = (time.perf_counter() - t0) * nu / k
         assert rc == 0
+        # parity at the headline size: the GPU's rows [0, k) against the CPU's, every cell
+        glat = my_lat.cpu().numpy().view(np.uint64).reshape(-1, nu)[:k]
+        gloss = my_loss.cpu().numpy().view(np.uint32).reshape(-1, nu)[:k]
+        parity = bool(np.array_equal(glat, olat) and np.array_equal(gloss, oloss.view(np.uint32)))
+        del olat, oloss, glat, gloss
         what = f"all {nu} sources" if k == nu else f"the first {k} of {nu} sources, scaled by {nu}/{k}"
-        cpu = {"value": round(t_cpu, 4), "unit": "s", "cores": threads, "kind": "port",
+        cpu = {"value": round(t_cpu, 4), "unit": "s", "cores": threads, "kind": "port", **CPU_INFO,
                "sample": f"{what} (binary-heap Dijkstra, dense output, no HashMap materialisation) "
                          f"on the same graph, {threads} threads"}
+        # the reference's own cost: SipHash score maps, nodes.contains filter, per-source and
+        # global HashMaps, self pairs, the id remap (oracle/sg_faithful.c), on a bounded sample
+        kf = min(nu, FAITHFUL_ROWS)
+        rcf, _, _, ph = O.routing_faithful(g["n"], g["src"], g["dst"], g["lat"], g["loss"], False, used, rows=kf,
+                                           threads=threads, read_back=False)
+        assert rcf == 0
+        t_f = sum(ph) * nu / kf
+        cpu_faithful = {"value": round(t_f, 3), "unit": "s", "cores": threads, "kind": "port", **CPU_INFO,
+                        "phases_s": {"dijkstra_filter_per_source_maps": round(ph[0] * nu / kf, 3),
+                                     "global_collect": round(ph[1] * nu / kf, 3),
+                                     "self_pairs": round(ph[2] * nu / kf, 4),
+                                     "id_remap_map": round(ph[3] * nu / kf, 3)},
+                        "sample": f"the first {kf} of {nu} sources through the reference's own steps "
+                                  "(graph/mod.rs:183-228, sim_config.rs:411-448), each phase scaled by "
+                                  f"{nu}/{kf}, {threads} threads"}
 
     result = {
         "metric": METRIC, "value": round(t_build, 6), "unit": "s", "n_gpus": D.world, "steps": a.steps,
@@ -580,14 +676,22 @@ def main():
                                "all-gather of the blocks is timed separately in apsp_detail.allgather_ms)",
                    "nodes": a.nodes, "arcs": n_arcs, "parallelism": f"rows{D.world}"},
         "roofline": roofline, "cpu_baseline": cpu,
-        "apsp_detail": {"out_kernel_ms": round(out_ms, 4),
-                        "out_kernel_GBs": round(out_bytes / max(out_ms, 1e-9) / 1e6, 1),
+        "parity_vs_cpu": parity,
+        "apsp_detail": {"kernel": roofline["kernel"],
+                        "slab_kernel_ms": round(t_slab * 1e3, 4) if t_slab else None,
+                        "out_kernel_ms": round(timers["out"][0], 4),
+                        "wide_rows_ms": round(timers["relax_wide"][0], 4),
                         "allgather_ms": round(t_allgather * 1e3, 4),
                         "table_bytes": 12 * nu * nu,
-                        "fw_equivalent_Tops": round(2.0 * nu * a.nodes ** 2 / t_build / 1e12, 2)},
+                        "end_to_end": e2e,
+                        "cpu_baseline_faithful": cpu_faithful},
     }
     if cpu:
         result["apsp_detail"]["speedup_vs_cpu"] = round(cpu["value"] / t_build, 1)
+    if cpu_faithful:
+        result["apsp_detail"]["speedup_vs_cpu_faithful"] = round(cpu_faithful["value"] / t_build, 1)
+        if e2e:
+            result["apsp_detail"]["speedup_vs_cpu_faithful_end_to_end"] = round(cpu_faithful["value"] / (e2e["ms"] / 1e3), 1)
     if D.rank == 0 and not a.no_gml:
         result["gml_ingest"] = gml_leg(a, NetworkGraph, synth)
     if D.rank == 0 and not a.no_c2:
@@ -684,13 +788,27 @@ def main():
             loss_h = my_loss.cpu().numpy().reshape(-1, nu)[: r1 - r0]
             rng0 = np.stack([O.xoshiro_seed(int(s)) for s in hosts["seed"]]).astype(np.uint64)
             ctr0 = np.zeros(a.hosts, np.uint64)
-            th = min(16, os.cpu_count() or 1)  # the box's CPU share (16 per GPU)
+            th = CPU_THREADS  # the box's CPU share (16 logical CPUs per GPU)
+            orng, octr = rng0.copy(), ctr0.copy()
             t0 = time.perf_counter()
-            O.deliver_round(round_end, sim_end, 0, src_global, pk["dst_ip"], pk["payload"], pk["send_time"],
-                            hosts["ip"], hosts["route"], lat_h, loss_h, rng0, ctr0, threads=th)
+            wr = O.deliver_round(round_end, sim_end, 0, src_global, pk["dst_ip"], pk["payload"], pk["send_time"],
+                                 hosts["ip"], hosts["route"], lat_h, loss_h, orng, octr, threads=th)
             tc = time.perf_counter() - t0
+            # parity at the benchmarked size: the same round from the seed state on the GPU,
+            # every per-packet output, the buckets, the minima and the hosts' RNG / counters
+            ht.set_state(rng0, ctr0)
+            st = deliver_round(ht, table, batch, round_end, sim_end, 0, out=out, ctx=ctx)
+            got = out.to_numpy(a.packets)
+            grng, gctr = ht.get_state()
+            same = all(np.array_equal(got[k], wr[k]) for k in ("status", "deliver_time", "event_id", "dst_order",
+                                                                "dst_offsets"))
+            same = same and got["delivered"] == wr["delivered"] and got["min_deliver"] == wr["min_deliver"]
+            same = same and got["min_lat"] == wr["min_lat"]
+            same = same and np.array_equal(grng, orng) and np.array_equal(gctr, octr)
+            delivery["parity_vs_cpu"] = bool(same)
+            del st
             delivery["cpu_baseline"] = {"value": round(a.packets / tc, 1), "unit": "packets/s", "cores": th,
-                                        "kind": "port", "sample": f"one full round of {a.packets} packets, "
+                                        "kind": "port", **CPU_INFO, "sample": f"one full round of {a.packets} packets, "
                                         "send_packet semantics + per-destination EventQueue order; source hosts "
                                         f"split over {th} threads as Shadow's workers split hosts"}
             delivery["speedup_vs_cpu"] = round(delivery["value"] / delivery["cpu_baseline"]["value"], 1)
