@@ -135,6 +135,15 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def gather(self, xs):
+        """Every rank's list of floats (rank order)."""
+        if not self.dist:
+            return [list(xs)]
+        t = self.torch.tensor(list(xs), dtype=self.torch.float64, device=self.coll_dev)
+        out = self.torch.empty(self.world * len(xs), dtype=self.torch.float64, device=self.coll_dev)
+        self.dist.all_gather_into_tensor(out, t)
+        return out.cpu().view(self.world, len(xs)).tolist()
+
     def sum(self, x: float) -> float:
         if not self.dist:
             return x
@@ -729,6 +738,13 @@ def main():
                 deliver_round(ht, table, batch, round_end, sim_end, 0, out=out, ctx=ctx)
 
         t_round = timed(D, rnd, a.steps, a.warmup)
+        per_rank = None
+        if sharded:  # load balance of the host partition: packets sent, records sent / received per rank
+            _, recv_l, _ = sharded.last
+            mine_c = [float(a.packets), float(sum(sharded.last_send_counts)), float(recv_l.shape[0])]
+            allc = D.gather(mine_c)
+            per_rank = {"packets": [int(x[0]) for x in allc], "records_sent": [int(x[1]) for x in allc],
+                        "records_received": [int(x[2]) for x in allc]}
         t_pcie = None
         if D.world == 1:
             # the boundary takes device buffers; a caller holding the packet log in host memory
@@ -768,13 +784,16 @@ def main():
                                    f"{a.nodes // 1000}k-node graph (node h mod {a.nodes // 1000}k), {a.packets} "
                                    "packets per rank from the hosts it owns, dst uniform over all hosts != src, "
                                    "20% zero-payload, "
-                                   "send_time U[1 ms round)" + ("; records exchanged by RCCL all-to-all to the "
-                                                                "destination's owner" if D.world > 1 else ""),
+                                   "send_time U[1 ms round)" + (
+                                       ("; records exchanged by RCCL all-to-all to the destination's owner"
+                                        if D.coll_dev == "cuda" else "; records exchanged by a host-staged gloo "
+                                        "all-to-all (a rehearsal: not a measurement)") if D.world > 1 else ""),
                        "hosts": a.hosts, "packets_per_rank": a.packets},
             "roofline": {"kernel": "k_walk", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmw.get("hbm_bytes_per_launch"),
                          "avg_launch_ms": round(walk_s * 1e3, 4)},
             "round_hbm_GBs": round(round_bytes / t_round / 1e9, 1),
+            "per_rank": per_rank,
             "parallelism": f"hosts{D.world}",
             "path_key_table": table.path_key is not None,
             "pcie_inclusive_ms_per_round": round(t_pcie * 1e3, 4) if t_pcie is not None else None,

@@ -209,11 +209,13 @@ class ShardedDelivery:
         self.device = device
         self.last_stats = None
         self.last = None
+        self.last_send_counts = None
 
     def round(self, packets, round_end_ns: int, sim_end_ns: int, bootstrap_end_ns: int = 0):
         src = self.source_fn(self.ctx, self.hosts, self.table, packets, round_end_ns, sim_end_ns, bootstrap_end_ns,
                              self.owner_dev, self.world)
         stats = (int(src.n_delivered), int(src.min_deliver_time_ns), int(src.min_used_latency_ns))
+        self.last_send_counts = list(src.send_counts)
         if self.exchange_fn is None:
             recv, recv_counts, self.last_stats = exchange_round(src.send, src.send_counts, stats, self.rank,
                                                                 self.dist, self.group)

@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""The multi-GPU code path over real RCCL on one GPU (world size 1, backend "nccl").
+
+Run as a child process by tests/test_rccl_gpu.py (RCCL needs a process of its
+own per rank; two ranks cannot share a device).  It drives, on device tensors:
+  * the APSP row-block all-gather (all_gather_into_tensor, as bench.py does),
+  * ShardedDelivery.round: sg_deliver_source, exchange_round (the all-gather of
+    counts and round scalars, then all_to_all_single of the records) and
+    sg_deliver_bucket,
+and checks them against the single-GPU path (sg_routing_build, deliver_round).
+Prints one JSON line: ok, and the exchange's timings.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+T0 = 946684800 * 10**9
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+
+    from shadow_amd import Context, NetworkGraph, synth
+    from shadow_amd.dist import RECORD_DTYPE, HostPartition, ShardedDelivery, exchange_round
+    from shadow_amd.worker import DeviceTable, HostTable, PacketBatch, deliver_round
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+    ctx = Context(0, stream=torch.cuda.current_stream().cuda_stream)
+
+    # ---- APSP rows + the RCCL all-gather of the row blocks
+    n = 600
+    g = synth.ring_chords_graph(n, 6.0, seed=9)
+    net = NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
+    used = np.arange(n, dtype=np.uint32)
+    mine_lat = torch.empty(n * n, dtype=torch.int64, device="cuda")
+    mine_loss = torch.empty(n * n, dtype=torch.float32, device="cuda")
+    net.build_rows_device(used, 0, n, mine_lat.data_ptr(), mine_loss.data_ptr(), True)
+    full_lat = torch.empty_like(mine_lat)
+    full_loss = torch.empty_like(mine_loss)
+    dist.all_gather_into_tensor(full_lat, mine_lat)
+    dist.all_gather_into_tensor(full_loss, mine_loss)
+    torch.cuda.synchronize()
+    ref = net.compute_shortest_paths(used)
+    assert np.array_equal(full_lat.cpu().numpy().view(np.uint64).reshape(n, n), ref.latency_ns)
+    assert np.array_equal(full_loss.cpu().numpy().view(np.uint32).reshape(n, n), ref.packet_loss.view(np.uint32))
+
+    # ---- a sharded delivery round through RCCL vs the single-GPU round
+    hosts = synth.make_hosts(4000, n, general_seed=9)
+    start, end = T0 + 10**9, T0 + 10**9 + 10**6
+    pk = synth.make_packets(200000, hosts, start, end, seed=9, p_unknown_dst=0.01)
+    table = DeviceTable(full_lat, full_loss, n, 0)
+    batch = PacketBatch.from_numpy(pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"])
+    part = HostPartition(hosts["route"], n, 1)
+    ht_s = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    sd = ShardedDelivery(ctx, ht_s, table, part, 0, 1, dist=dist)
+    src, recv, recv_counts, order, offsets = sd.round(batch, end, 2**63, start + 100_000)
+    ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    out = deliver_round(ht, table, batch, end, 2**63, start + 100_000)
+    want = out.to_numpy(len(pk["src"]))
+    P = len(pk["src"])
+    assert np.array_equal(src.status[:P].cpu().numpy(), want["status"])
+    assert np.array_equal(src.deliver_time_ns[:P].cpu().numpy().view(np.uint64), want["deliver_time"])
+    assert np.array_equal(src.event_id[:P].cpu().numpy().view(np.uint64), want["event_id"])
+    rec = recv.cpu().numpy().view(RECORD_DTYPE).ravel()
+    glob = rec["packet"].astype(np.int64)[order.cpu().numpy().view(np.uint32)]
+    assert np.array_equal(glob, want["dst_order"].astype(np.int64))
+    assert np.array_equal(offsets.cpu().numpy().view(np.uint32), want["dst_offsets"])
+    assert sd.last_stats == (want["delivered"], want["min_deliver"], want["min_lat"])
+    g1, g2 = ht_s.get_state(), ht.get_state()
+    assert np.array_equal(g1[0], g2[0]) and np.array_equal(g1[1], g2[1])
+
+    # ---- timings: the whole sharded round, and exchange_round alone (its one host sync)
+    reps = 20
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sd.round(batch, end, 2**63, start + 100_000)
+    torch.cuda.synchronize()
+    t_round = (time.perf_counter() - t0) / reps
+    stats = (int(src.n_delivered), int(src.min_deliver_time_ns), int(src.min_used_latency_ns))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        exchange_round(src.send, src.send_counts, stats, 0, dist)
+    torch.cuda.synchronize()
+    t_ex = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        deliver_round(ht, table, batch, end, 2**63, start + 100_000, out=out)
+    torch.cuda.synchronize()
+    t_single = (time.perf_counter() - t0) / reps
+    print(json.dumps({"ok": True, "backend": dist.get_backend(), "packets": P, "records": int(sum(recv_counts)),
+                      "sharded_round_ms": round(t_round * 1e3, 4), "exchange_round_ms": round(t_ex * 1e3, 4),
+                      "single_gpu_round_ms": round(t_single * 1e3, 4)}), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
