@@ -107,6 +107,7 @@ struct sg_ctx {
   // on copy_stream while the next block computes
   sg::DevBuf r_stage_lat[2], r_stage_loss[2];
   hipStream_t copy_stream = nullptr;
+  bool in_fill = false;  // inside sg_routing_info_fill (selects the row-block kernel symbols)
   hipEvent_t stage_done[2] = {nullptr, nullptr}, stage_copied[2] = {nullptr, nullptr};
   // Round control: round_err (device, zeroed at creation) collects the source
   // phase's error flags; the stats kernel hands them to the host and clears

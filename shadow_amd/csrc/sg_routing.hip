@@ -1419,10 +1419,17 @@ int32_t sg_routing_info_fill(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, ui
     for (uint32_t r0 = 0; r0 < n_used; r0 += rows, k++) {
       const uint32_t r1 = std::min(n_used, r0 + rows), b = k & 1;
       if (k >= 2) SG_HIP(hipStreamWaitEvent(st, ctx->stage_copied[b], 0));  // block k - 2 left this buffer
-      if (shortest)
-        shortest_paths(ctx, net, d_used, n_used, r0, r1, slat[b], sloss[b]);
-      else
-        direct_paths(ctx, net, d_used, nodes, n_used, r0, r1, slat[b], sloss[b]);
+      ctx->in_fill = true;
+      try {
+        if (shortest)
+          shortest_paths(ctx, net, d_used, n_used, r0, r1, slat[b], sloss[b]);
+        else
+          direct_paths(ctx, net, d_used, nodes, n_used, r0, r1, slat[b], sloss[b]);
+      } catch (...) {
+        ctx->in_fill = false;
+        throw;
+      }
+      ctx->in_fill = false;
       const size_t cells = (size_t)(r1 - r0) * n_used;
       // (workspace fetched after the build, which may grow these buffers)
       unsigned long long* dmin = ctx->r_err.get<unsigned long long>(4);

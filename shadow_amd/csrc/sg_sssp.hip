@@ -149,7 +149,9 @@ size_t sssp_lds_bytes(uint32_t n) {
 // One workgroup per source row i in [row_begin, row_end): source used[i].
 // out_arc: 3 u32 per out-arc (destination, latency clamped to LAT32_SAT,
 // bits(1f32 - loss)), grouped by tail node (out_off).
-template <bool COUNT, int NT, int LA>
+// PART: 0 for a routing build, 1 for sg_routing_info_fill's row blocks (the same
+// code; a separate symbol so per-kernel profiles do not mix whole builds with blocks)
+template <bool COUNT, int NT, int LA, int PART>
 __global__ void __launch_bounds__(NT)
     k_sssp_lds(const uint32_t* __restrict__ out_off, const uint32_t* __restrict__ out_arc, uint32_t n,
                uint32_t n_arcs, const uint32_t* __restrict__ used, uint32_t n_used, uint32_t row_begin,
@@ -471,13 +473,15 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
                        diag, claim, idle_sleep, lane_deg);
   };
   if (work) {
-    if (nt == 512) go(k_sssp_lds<true, 512, 8>);
-    else if (la16) go(k_sssp_lds<true, 1024, 16>);
-    else go(k_sssp_lds<true, 1024, 8>);
+    if (nt == 512) go(k_sssp_lds<true, 512, 8, 0>);
+    else if (la16) go(k_sssp_lds<true, 1024, 16, 0>);
+    else go(k_sssp_lds<true, 1024, 8, 0>);
+  } else if (ctx->in_fill) {
+    go(k_sssp_lds<false, 1024, 8, 1>);
   } else {
-    if (nt == 512) go(k_sssp_lds<false, 512, 8>);
-    else if (la16) go(k_sssp_lds<false, 1024, 16>);
-    else go(k_sssp_lds<false, 1024, 8>);
+    if (nt == 512) go(k_sssp_lds<false, 512, 8, 0>);
+    else if (la16) go(k_sssp_lds<false, 1024, 16, 0>);
+    else go(k_sssp_lds<false, 1024, 8, 0>);
   }
   SG_CHECK_LAUNCH();
 }
