@@ -10,7 +10,10 @@
 // sequential processing, coalesced pop results).  The FIFO of each host is a
 // ring of `cap` slots in HBM (packet id, enqueue time, length); the scalar
 // CoDel state is kept in registers for the whole call.
+#include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "sg_device.h"
@@ -59,7 +62,7 @@ __device__ __forceinline__ uint64_t control_law(uint64_t t, uint64_t count) {
 // LDS views (address space 3: ds_* instructions, not flat ones)
 typedef __attribute__((address_space(3))) const uint32_t lds_u32;
 typedef __attribute__((address_space(3))) const uint64_t lds_u64;
-typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+typedef __attribute__((address_space(3))) const uint16_t lds_u16;
 
 struct Q {
   uint8_t flags;
@@ -67,6 +70,7 @@ struct Q {
   uint32_t head, tail;
   uint32_t hp, hl;
   uint64_t ht;
+  bool hv;            // hp/hl/ht hold the element at head
   uint32_t last_len;  // length of the element pop_front returned last
   uint4* ring;
   uint32_t mask;
@@ -75,20 +79,18 @@ struct Q {
   // from LDS there instead of from the ring in HBM (the ring is still written:
   // what is left at the end of the window lives on in HBM).
   bool win;
-  uint32_t t0, wb, cn, ci;  // tail at window start; host's first staged event; pushes located; last one's index
+  uint32_t t0, wb;  // tail at window start; host's first staged event
   lds_u32 *wp, *wl;
   lds_u64* wt;
-  lds_u8* wk;  // event kinds (push = SG_CODEL_PUSH), or null: every event is a push
-  __device__ void begin_window(lds_u32* p, lds_u32* l, lds_u64* t, lds_u8* k, uint32_t first) {
+  lds_u16* wi;  // the staged index of the window's j-th push, or null: every event is a push
+  __device__ void begin_window(lds_u32* p, lds_u32* l, lds_u64* t, lds_u16* pi, uint32_t first) {
     win = true;
     t0 = tail;
     wb = first;
-    cn = 0;
-    ci = first - 1;
     wp = p;
     wl = l;
     wt = t;
-    wk = k;
+    wi = pi;
   }
   uint8_t* status;
   uint32_t n_status;
@@ -127,17 +129,11 @@ struct Q {
     return true;
   }
   __device__ void load_head() {
-    if (head == tail) return;
+    hv = head != tail;
+    if (!hv) return;
     const uint32_t j = head - t0;  // the j-th push of the window (modular)
     if (win && j < tail - t0) {
-      uint32_t k = wb + j;
-      if (wk) {  // locate the j-th push event (the head only moves forward)
-        while (cn <= j) {
-          ci++;
-          cn += wk[ci] == SG_CODEL_PUSH;
-        }
-        k = ci;
-      }
+      const uint32_t k = wi ? wi[j] : wb + j;
       hp = wp[k];
       hl = wl[k];
       ht = wt[k];
@@ -202,6 +198,7 @@ struct Q {
       hp = pkt;
       ht = now;
       hl = len;
+      hv = true;
     }
     tail++;
     bytes += len;
@@ -224,18 +221,68 @@ struct CodelArgs {
   uint8_t* status;
   uint32_t n_status;
   unsigned long long* blk;  // per block: [dropped, error flags]
+  unsigned long long* bdiag = nullptr;  // SG_LANE_DIAG: per block [start, end, walk cycles, most events of a lane]
 };
 
-constexpr int CD_THREADS = 256;
+// One wave per block: the walkers are the whole block.  The staging loads are
+// unrolled (CD_UNROLL per array in flight per lane) so one wave moves a chunk
+// in two rounds of latency.  Blocks with idle helper waves held occupancy
+// (VGPRs) without walking: at C4 only 1024 of the 1563 blocks were resident,
+// and the kernels ran in two rounds (SG_LANE_DIAG).
+constexpr int CD_THREADS = 64;
+constexpr int CD_UNROLL = 8;
 constexpr int CD_HOSTS = 64;
 constexpr int CD_CHUNK = 1024;
+constexpr int CD_OUT_CHUNK = 896;  // k_outbound: 24 B per send, 21 KB, 7 blocks per CU
+static_assert(CD_THREADS == CD_HOSTS, "a block is its walkers");
+
+// Chunk [c0, c1) staged by the block: ld(i, u) loads element i into slot u of
+// the lane's registers, st(k, u) stores slot u to LDS index k.  Indices past
+// c1 load element c1 - 1 (always valid, unconditional loads: no branch for the
+// compiler to drain each load at) and are not stored.
+template <typename LD, typename ST>
+__device__ __forceinline__ void stage_chunk(uint32_t c0, uint32_t c1, LD&& ld, ST&& st) {
+  const uint32_t t = threadIdx.x;
+  for (uint32_t base = c0; base < c1; base += CD_THREADS * CD_UNROLL) {
+#pragma unroll
+    for (int u = 0; u < CD_UNROLL; u++) ld(min(base + u * CD_THREADS + t, c1 - 1), u);
+#pragma unroll
+    for (int u = 0; u < CD_UNROLL; u++) {
+      const uint32_t i = base + u * CD_THREADS + t;
+      if (i < c1) st(i - c0, u);
+    }
+  }
+}
+
+// SG_LANE_DIAG: a block's start and end on the 100 MHz wall clock (comparable
+// across CUs), the cycles its walkers spent walking, and its busiest lane's events
+__device__ __forceinline__ void lane_diag_store(unsigned long long* d, uint64_t t0, uint64_t walk, uint32_t ev) {
+  if (!d) return;
+  if (threadIdx.x < 64) {
+    for (int o = 32; o > 0; o >>= 1) {
+      walk = max(walk, (uint64_t)__shfl_xor((unsigned long long)walk, o, 64));
+      ev = max(ev, (uint32_t)__shfl_xor(ev, o, 64));
+    }
+    if (threadIdx.x == 0) {
+      unsigned long long* q = d + 4 * (size_t)blockIdx.x;
+      q[0] = t0;
+      q[1] = wall_clock64();
+      q[2] = walk;
+      q[3] = ev;
+    }
+  }
+}
 
 __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
+  const uint64_t d_t0 = a.bdiag ? wall_clock64() : 0;
+  uint64_t d_walk = 0;
+  // staged chunk: 22 KB, so 7 one-wave blocks fit a CU (1792 >= the 1563 blocks of a 100k-host call)
   __shared__ uint64_t s_t[CD_CHUNK];
-  __shared__ uint32_t s_p[CD_CHUNK];  // packet -> pop result
+  __shared__ uint32_t s_p[CD_CHUNK];  // pushed packet; a pop event's slot receives its result
   __shared__ uint32_t s_l[CD_CHUNK];
-  __shared__ uint8_t s_k[CD_CHUNK];
-  __shared__ uint32_t s_r[CD_CHUNK];  // pop results (s_p keeps the pushed packets for the window)
+  __shared__ uint16_t s_pp[CD_CHUNK + 1];  // pushes before each staged event (kind k = s_pp[k + 1] - s_pp[k])
+  __shared__ uint16_t s_pi[CD_CHUNK];      // staged index of the chunk's r-th push
+  __shared__ uint16_t s_qi[CD_CHUNK];      // staged index of the chunk's r-th pop
   const uint32_t h0 = blockIdx.x * CD_HOSTS, t = threadIdx.x;
   const uint32_t p0 = min(a.host_off[min(h0, a.H)], a.E);
   const uint32_t p1 = max(min(a.host_off[min(h0 + CD_HOSTS, a.H)], a.E), p0);
@@ -260,57 +307,102 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
     q.n_status = a.n_status;
     q.load_head();
   }
+  const uint64_t lt = (1ull << t) - 1;  // lanes below this one
   for (uint32_t c0 = p0; c0 < p1; c0 += CD_CHUNK) {
     const uint32_t c1 = min(c0 + CD_CHUNK, p1);
-    for (uint32_t i = c0 + t; i < c1; i += CD_THREADS) {  // 1. coalesced staging
-      const uint32_t k = i - c0;
-      s_t[k] = a.time[i];
-      s_p[k] = a.pkt[i];
-      s_l[k] = a.len[i];
-      s_k[k] = a.kind[i];
-    }
-    __syncthreads();
-    if (walker) {  // 2. each host's events in order
-      const uint32_t b = max(hb, c0), e = min(he, c1);
-      q.begin_window((lds_u32*)s_p, (lds_u32*)s_l, (lds_u64*)s_t, (lds_u8*)s_k, b - c0);
-      // the next event's fields are read while this one is processed (the
-      // walker's time is its chain of dependent LDS reads and queue updates)
-      uint8_t nk = 0;
-      uint64_t nt = 0;
-      uint32_t np = 0, nl = 0;
-      if (b < e) {
-        nk = s_k[b - c0];
-        nt = s_t[b - c0];
-        np = s_p[b - c0];
-        nl = s_l[b - c0];
-      }
-      for (uint32_t i = b; i < e; i++) {
-        const uint32_t k = i - c0;
-        const uint8_t kind = nk;
-        const uint64_t now = nt;
-        const uint32_t pkt = np, len = nl;
-        if (i + 1 < e) {
-          nk = s_k[k + 1];
-          nt = s_t[k + 1];
-          np = s_p[k + 1];
-          nl = s_l[k + 1];
+    {  // 1. coalesced staging, and the chunk's push and pop lists by ballot (the block is one wave)
+      uint32_t run = 0;
+      for (uint32_t base = c0; base < c1; base += CD_THREADS * CD_UNROLL) {
+        uint64_t rt[CD_UNROLL];
+        uint32_t rp[CD_UNROLL], rl[CD_UNROLL];
+        uint8_t rk[CD_UNROLL];
+#pragma unroll
+        for (int u = 0; u < CD_UNROLL; u++) {
+          const uint32_t i = min(base + u * CD_THREADS + t, c1 - 1);
+          rt[u] = a.time[i];
+          rp[u] = a.pkt[i];
+          rl[u] = a.len[i];
+          rk[u] = a.kind[i];
         }
-        uint32_t r = CD_NONE;
-        if (kind == SG_CODEL_PUSH) {
-          q.push(pkt, now, len);
-        } else {
-          r = q.pop(now);
-          if (r != CD_NONE) {
-            if (r < q.n_status) q.status[r] = SG_CODEL_DEQUEUED;
-            else q.err |= E_PKT;
+#pragma unroll
+        for (int u = 0; u < CD_UNROLL; u++) {
+          const uint32_t i = base + u * CD_THREADS + t;
+          const bool in = i < c1, push = in && rk[u] == SG_CODEL_PUSH;
+          const uint64_t m = __ballot(push);
+          const uint32_t rank = run + (uint32_t)__popcll(m & lt);
+          if (in) {
+            const uint32_t k = i - c0;
+            s_t[k] = rt[u];
+            s_p[k] = rp[u];
+            s_l[k] = rl[u];
+            s_pp[k] = (uint16_t)rank;
+            if (push) s_pi[rank] = (uint16_t)k;
+            else s_qi[k - rank] = (uint16_t)k;
           }
+          run += (uint32_t)__popcll(m);
         }
-        s_r[k] = r;
       }
-      q.win = false;  // the next chunk's staging overwrites the window
+      if (t == 0) s_pp[c1 - c0] = (uint16_t)run;
     }
     __syncthreads();
-    for (uint32_t i = c0 + t; i < c1; i += CD_THREADS) a.pop_result[i] = s_r[i - c0];  // 3. coalesced results
+    if (walker) {
+      // 2. each host's pops in order.  A host's pushes between two pops only
+      // append (tail, bytes): they are accounted at the next pop, the elements
+      // read from the staged window, and the ring is written at the chunk's end
+      // for the elements still queued -- the walk's steps are the pops alone.
+      const uint64_t d_w0 = a.bdiag ? clock64() : 0;
+      // this host's staged range [kb, ke) (empty when its events lie outside the chunk)
+      const uint32_t b = max(hb, c0), e = min(he, c1);
+      const uint32_t kb = b < e ? b - c0 : 0, ke = b < e ? e - c0 : 0;
+      const uint32_t pb = kb < ke ? s_pp[kb] : 0, pe = kb < ke ? s_pp[ke] : 0;
+      const uint32_t rb = kb - pb, re = ke - pe;  // this host's pop ranks [rb, re)
+      lds_u16* wi = (lds_u16*)s_pi + pb;
+      q.begin_window((lds_u32*)s_p, (lds_u32*)s_l, (lds_u64*)s_t, wi, kb);
+      uint32_t seen = 0;  // window pushes accounted
+      auto account = [&](uint32_t upto) {  // the window's pushes [seen, upto) enter the queue
+        for (; seen < upto; seen++) q.bytes += s_l[wi[seen]];
+        q.tail = q.t0 + upto;
+        if (q.tail - q.head > q.mask + 1u) q.err |= E_FULL;  // a push found the ring full
+        if (!q.hv) q.load_head();
+      };
+      // the next pop's staged index and fields are read a step ahead, its
+      // successor's index two steps ahead
+      uint32_t k1 = rb < re ? s_qi[rb] : 0, k2 = rb + 1 < re ? s_qi[rb + 1] : 0;
+      uint64_t t1 = rb < re ? s_t[k1] : 0;
+      uint32_t pp1 = rb < re ? s_pp[k1] : 0;
+      for (uint32_t r = rb; r < re; r++) {
+        const uint32_t k = k1, pp = pp1;
+        const uint64_t now = t1;
+        k1 = k2;
+        if (r + 1 < re) {
+          t1 = s_t[k1];
+          pp1 = s_pp[k1];
+        }
+        if (r + 2 < re) k2 = s_qi[r + 2];
+        account(pp - pb);
+        const uint32_t res = q.pop(now);
+        if (res != CD_NONE) {
+          if (res < q.n_status) q.status[res] = SG_CODEL_DEQUEUED;
+          else q.err |= E_PKT;
+        }
+        s_p[k] = res;  // a pop's packet slot is read by no one else
+      }
+      account(pe - pb);
+      // the window's elements still queued live on in the ring
+      const uint32_t w0 = q.head - q.t0 <= q.tail - q.t0 ? q.head - q.t0 : 0;
+      for (uint32_t j = w0; j < q.tail - q.t0; j++) {
+        const uint32_t k = wi[j];
+        const uint64_t tk = s_t[k];
+        q.ring[(q.t0 + j) & q.mask] = make_uint4(s_p[k], s_l[k], (uint32_t)tk, (uint32_t)(tk >> 32));
+      }
+      if (a.bdiag) d_walk += clock64() - d_w0;
+      q.win = false;  // the next chunk's staging overwrites the window (the head stays cached)
+    }
+    __syncthreads();
+    for (uint32_t i = c0 + t; i < c1; i += CD_THREADS) {  // 3. coalesced results (CD_NONE for a push)
+      const uint32_t k = i - c0;
+      a.pop_result[i] = s_pp[k + 1] != s_pp[k] ? CD_NONE : s_p[k];
+    }
     __syncthreads();
   }
   unsigned long long dropped = 0, err = 0;
@@ -326,6 +418,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
     dropped = q.dropped;
     err = q.err;
   }
+  lane_diag_store(a.bdiag, d_t0, d_walk, he - hb);
   if (t < 64) {
     for (int d = 32; d > 0; d >>= 1) {
       dropped += __shfl_xor(dropped, d, 64);
@@ -466,6 +559,8 @@ __device__ void relay_task(Q& q, Relay& r, uint64_t now, uint64_t bootstrap_end,
 }
 
 __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
+  const uint64_t d_t0 = ia.q.bdiag ? wall_clock64() : 0;
+  uint64_t d_walk = 0;
   const CodelArgs& a = ia.q;
   __shared__ uint64_t s_t[CD_CHUNK];
   __shared__ uint32_t s_p[CD_CHUNK];
@@ -509,15 +604,26 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
   };
   for (uint32_t c0 = p0; c0 < p1; c0 += CD_CHUNK) {
     const uint32_t c1 = min(c0 + CD_CHUNK, p1);
-    for (uint32_t i = c0 + t; i < c1; i += CD_THREADS) {
-      const uint32_t k = i - c0;
-      s_t[k] = a.time[i];
-      s_p[k] = a.pkt[i];
-      s_l[k] = a.len[i];
+    {
+      uint64_t rt[CD_UNROLL];
+      uint32_t rp[CD_UNROLL], rl[CD_UNROLL];
+      stage_chunk(
+          c0, c1,
+          [&](uint32_t i, int u) {
+            rt[u] = a.time[i];
+            rp[u] = a.pkt[i];
+            rl[u] = a.len[i];
+          },
+          [&](uint32_t k, int u) {
+            s_t[k] = rt[u];
+            s_p[k] = rp[u];
+            s_l[k] = rl[u];
+          });
     }
     __syncthreads();
     if (walker) {
       const uint32_t b = max(hb, c0), e = min(he, c1);
+      const uint64_t d_w0 = a.bdiag ? clock64() : 0;
       q.win = false;  // the tasks first run by this chunk pop the previous chunk's elements from HBM
       q.begin_window((lds_u32*)s_p, (lds_u32*)s_l, (lds_u64*)s_t, nullptr, b - c0);
       uint64_t nt = b < e ? s_t[b - c0] : 0;  // the next arrival's fields, read ahead
@@ -541,6 +647,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
           r.tt = now;
         }
       }
+      if (a.bdiag) d_walk += clock64() - d_w0;
     }
     __syncthreads();
   }
@@ -565,6 +672,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
     err = q.err;
     dropped = q.dropped;
   }
+  lane_diag_store(a.bdiag, d_t0, d_walk, he - hb);
   if (t < 64) {
     for (int d = 32; d > 0; d >>= 1) {
       dropped += __shfl_xor(dropped, d, 64);
@@ -605,16 +713,39 @@ struct OutboundArgs {
   uint32_t n_status;
   uint32_t* start;  // per host: the first ring slot this call forwarded from
   unsigned long long* blk;
+  unsigned long long* bdiag = nullptr;  // as CodelArgs::bdiag
 };
 
 struct OutQ {
   uint32_t head, tail, oldest, mask, ip;
   uint4* ring;
   uint4 hr;  // the head record (valid while head < tail), loaded ahead of its pop
+  uint4 cr;  // the relay's cached record (valid while R_CACHED): the slot at head - 1
   uint32_t sent;
   uint32_t err;
+  // Staged window: the records pushed since begin_window() are the chunk's
+  // send records wb, wb + 1, ... in LDS, so a head pushed there is read from
+  // LDS instead of being re-read from the ring this lane just wrote (a forward
+  // task pops back to back: each HBM re-read was a full round trip on the chain).
+  bool win;
+  uint32_t t0, wb;
+  const __attribute__((address_space(3))) uint4* wr;
+  __device__ void begin_window(const __attribute__((address_space(3))) uint4* r, uint32_t first) {
+    win = true;
+    t0 = tail;
+    wb = first;
+    wr = r;
+  }
   __device__ void load_head() {
-    if (head != tail) hr = ring[head & mask];
+    if (head == tail) return;
+    const uint32_t j = head - t0;
+    if (win && j < tail - t0) {
+      const __attribute__((address_space(3))) uint32_t* w =
+          (const __attribute__((address_space(3))) uint32_t*)(wr + wb + j);
+      hr = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      hr = ring[head & mask];
+    }
   }
 };
 
@@ -625,7 +756,7 @@ __device__ void out_task(OutQ& q, Relay& r, uint64_t now, const OutboundArgs& a,
   for (;;) {
     uint4 rec;
     if (r.rf & R_CACHED) {  // next_packet.take(): the slot at head - 1
-      rec = q.ring[(q.head - 1) & q.mask];
+      rec = q.cr;
       r.rf &= (uint8_t)~R_CACHED;
     } else {
       if (q.head == q.tail) return;  // the interface has nothing: Idle
@@ -637,6 +768,7 @@ __device__ void out_task(OutQ& q, Relay& r, uint64_t now, const OutboundArgs& a,
     uint64_t wait;
     if (!local && now >= a.bootstrap_end && !r.remove(rec.y, now, wait)) {
       r.rf |= R_CACHED | R_PENDING;  // RelayCached; forward_later(wait)
+      q.cr = rec;
       ctr_inc++;
       r.tt = now > ~0ull - wait ? ~0ull : now + wait;
       if (r.tt >= a.sim_end) r.rf |= R_NEVER;
@@ -653,8 +785,10 @@ __device__ void out_task(OutQ& q, Relay& r, uint64_t now, const OutboundArgs& a,
 }
 
 __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
-  __shared__ uint64_t s_t[CD_CHUNK];
-  __shared__ uint4 s_r[CD_CHUNK];
+  const uint64_t d_t0 = a.bdiag ? wall_clock64() : 0;
+  uint64_t d_walk = 0;
+  __shared__ uint64_t s_t[CD_OUT_CHUNK];
+  __shared__ uint4 s_r[CD_OUT_CHUNK];
   const uint32_t h0 = blockIdx.x * CD_HOSTS, t = threadIdx.x;
   const uint32_t p0 = min(a.host_off[min(h0, a.H)], a.E);
   const uint32_t p1 = max(min(a.host_off[min(h0 + CD_HOSTS, a.H)], a.E), p0);
@@ -679,19 +813,31 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
     r.inc = a.tb_inc[h];
     r.last = a.tb_last[h];
     q.oldest = q.head - ((r.rf & R_CACHED) ? 1u : 0u);
+    if (r.rf & R_CACHED) q.cr = q.ring[(q.head - 1) & q.mask];
     q.load_head();
   }
   auto due = [&](uint64_t before) { return (r.rf & R_PENDING) && !(r.rf & R_NEVER) && r.tt < before; };
-  for (uint32_t c0 = p0; c0 < p1; c0 += CD_CHUNK) {
-    const uint32_t c1 = min(c0 + CD_CHUNK, p1);
-    for (uint32_t i = c0 + t; i < c1; i += CD_THREADS) {
-      const uint32_t k = i - c0;
-      s_t[k] = a.time[i];
-      s_r[k] = make_uint4(a.pkt[i], a.len[i], a.dst[i], a.payload[i]);
+  for (uint32_t c0 = p0; c0 < p1; c0 += CD_OUT_CHUNK) {
+    const uint32_t c1 = min(c0 + CD_OUT_CHUNK, p1);
+    {
+      uint64_t rt[CD_UNROLL];
+      uint4 rr[CD_UNROLL];
+      stage_chunk(
+          c0, c1,
+          [&](uint32_t i, int u) {
+            rt[u] = a.time[i];
+            rr[u] = make_uint4(a.pkt[i], a.len[i], a.dst[i], a.payload[i]);
+          },
+          [&](uint32_t k, int u) {
+            s_t[k] = rt[u];
+            s_r[k] = rr[u];
+          });
     }
     __syncthreads();
     if (walker) {
       const uint32_t b = max(hb, c0), e = min(he, c1);
+      const uint64_t d_w0 = a.bdiag ? clock64() : 0;
+      q.begin_window((const __attribute__((address_space(3))) uint4*)s_r, b - c0);
       for (uint32_t i = b; i < e; i++) {
         const uint32_t k = i - c0;
         const uint64_t now = s_t[k];
@@ -714,6 +860,8 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
           r.tt = now;
         }
       }
+      if (a.bdiag) d_walk += clock64() - d_w0;
+      q.win = false;  // the next chunk's staging overwrites the window
     }
     __syncthreads();
   }
@@ -731,6 +879,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
     err = q.err;
     sent = q.sent;
   }
+  lane_diag_store(a.bdiag, d_t0, d_walk, he - hb);
   if (t < 64) {
     for (int d = 32; d > 0; d >>= 1) {
       sent += __shfl_xor(sent, d, 64);
@@ -909,6 +1058,47 @@ struct sg_inbound {
   }
 };
 
+// SG_LANE_DIAG=1: per-block timing of the lane-per-host kernels on stderr (a
+// diagnostic: a synchronous copy after the launch; never set in a measured run)
+unsigned long long* lane_diag_alloc(uint32_t nb) {
+  const char* e = getenv("SG_LANE_DIAG");
+  if (!e || atoi(e) == 0) return nullptr;
+  unsigned long long* d = nullptr;
+  SG_HIP(hipMalloc(&d, (size_t)nb * 32));
+  SG_HIP(hipMemset(d, 0, (size_t)nb * 32));
+  return d;
+}
+void lane_diag_report(hipStream_t st, const char* name, unsigned long long* d, uint32_t nb) {
+  if (!d) return;
+  std::vector<unsigned long long> h((size_t)nb * 4);
+  SG_HIP(hipStreamSynchronize(st));
+  SG_HIP(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+  (void)hipFree(d);
+  uint64_t t_min = ~0ull, t_max = 0, s_max = 0;
+  std::vector<double> dur(nb), walk(nb), ev(nb);
+  for (uint32_t b = 0; b < nb; b++) {
+    t_min = std::min<uint64_t>(t_min, h[4 * b]);
+    t_max = std::max<uint64_t>(t_max, h[4 * b + 1]);
+  }
+  for (uint32_t b = 0; b < nb; b++) {
+    s_max = std::max<uint64_t>(s_max, h[4 * b] - t_min);
+    dur[b] = (h[4 * b + 1] - h[4 * b]) * 0.01;  // 100 MHz -> us
+    walk[b] = h[4 * b + 2] / 2400.0;              // shader clock cycles -> us at ~2.4 GHz
+    ev[b] = (double)h[4 * b + 3];
+  }
+  auto q = [](std::vector<double> v, double f) {
+    std::sort(v.begin(), v.end());
+    return v[(size_t)std::min<double>(v.size() - 1, f * v.size())];
+  };
+  double mw = 0, me = 0;
+  for (uint32_t b = 0; b < nb; b++) mw += walk[b] / nb, me += ev[b] / nb;
+  fprintf(stderr,
+          "[lane] %s: %u blocks, span %.2f us, last start +%.2f us; block us p50 %.2f p90 %.2f max %.2f; "
+          "walk us (busiest lane) mean %.2f max %.2f; busiest-lane events mean %.1f max %.0f\n",
+          name, nb, (t_max - t_min) * 0.01, s_max * 0.01, q(dur, 0.5), q(dur, 0.9), q(dur, 1.0), mw, q(walk, 1.0), me,
+          q(ev, 1.0));
+}
+
 extern "C" {
 
 int32_t sg_codel_run(sg_ctx* ctx, sg_codel* q, const sg_codel_events* ev, uint32_t* pop_result,
@@ -931,11 +1121,13 @@ int32_t sg_codel_run(sg_ctx* ctx, sg_codel* q, const sg_codel_events* ev, uint32
     CodelArgs a{ws, H, E, ev->kind, ev->time_ns, ev->packet, ev->len, q->flags, q->iend, q->dnext, q->cur,
                 q->prev, q->bytes, q->head, q->tail, q->ring, q->cap, pop_result,
                 pkt_status, n_packets, ctx->d_blk.get<unsigned long long>(2 * (size_t)nb)};
+    a.bdiag = lane_diag_alloc(nb);
     {
       // per event: 17 B in, 4 B result, ring slot 16 B written (push) or read (pop), 1 B status
       TimedLaunch tl(ctx, "codel", 38.0 * E + 56.0 * H);
       hipLaunchKernelGGL(k_codel, dim3(nb), dim3(CD_THREADS), 0, st, a);
     }
+    lane_diag_report(st, "k_codel", a.bdiag, nb);
     hipLaunchKernelGGL(k_codel_reduce, dim3(1), dim3(1024), 0, st, a.blk, nb, gerr, q->ret);
     SG_CHECK_LAUNCH();
     SG_HIP(hipStreamSynchronize(st));
@@ -1093,9 +1285,11 @@ int32_t sg_inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* a
     a.fwd_time = fwd_time;
     {
       // per arrival: 16 B in, a 16-B ring record written and read, 9 B out; per host: ~160 B of state
+      a.q.bdiag = lane_diag_alloc(nb);
       TimedLaunch tl(ctx, "inbound", 57.0 * E + 160.0 * H);
       hipLaunchKernelGGL(k_inbound, dim3(nb), dim3(CD_THREADS), 0, st, a);
     }
+    lane_diag_report(st, "k_inbound", a.q.bdiag, nb);
     hipLaunchKernelGGL(k_codel_reduce, dim3(1), dim3(1024), 0, st, a.q.blk, nb, gerr, q->ret);
     SG_CHECK_LAUNCH();
     SG_HIP(hipStreamSynchronize(st));
@@ -1271,9 +1465,11 @@ int32_t sg_outbound_run(sg_ctx* ctx, sg_outbound* ob, const sg_outbound_sends* s
     a.blk = ctx->d_blk.get<unsigned long long>(2 * (size_t)nb);
     {
       // per send: 24 B in, a 16-B ring record written and read, 9 B out; per host: ~90 B of state
+      a.bdiag = lane_diag_alloc(nb);
       TimedLaunch tl(ctx, "outbound", 65.0 * E + 90.0 * H);
       hipLaunchKernelGGL(k_outbound, dim3(nb), dim3(CD_THREADS), 0, st, a);
     }
+    lane_diag_report(st, "k_outbound", a.bdiag, nb);
     if (sent) {
       hipLaunchKernelGGL(k_blk_offsets, dim3(1), dim3(1024), 0, st, a.blk, nb, ob->off);
       sg_outbound_sent o = *sent;
