@@ -55,6 +55,28 @@ class HostPartition:
         return len(self.hosts_of[rank])
 
 
+class Workspace:
+    """Round buffers kept across rounds: `get` returns the first `n` elements of a
+    cached tensor, reallocated only when a round needs more.  Reuse across rounds
+    is stream-ordered: every kernel runs on the current stream, and the blocking
+    collectives (async_op=False) make that stream wait for RCCL's."""
+
+    def __init__(self):
+        self._t = {}
+
+    def get(self, name, n, dtype, device, cols=None, pinned=False):
+        import torch
+
+        shape = (n,) if cols is None else (n, cols)
+        t = self._t.get(name)
+        if t is None or t.shape[0] < n or t.dtype != dtype or str(t.device) != str(device):
+            cap = max(n, 1) if t is None else max(n, 1, t.shape[0] + t.shape[0] // 2)
+            full = (cap,) if cols is None else (cap, cols)
+            t = torch.empty(full, dtype=dtype, device=device, pin_memory=pinned)
+            self._t[name] = t
+        return t[:n] if shape[0] else t[:0]
+
+
 # ---------------------------------------------------------------------------
 # GPU phases (libshadow_gpu.so)
 # ---------------------------------------------------------------------------
@@ -71,15 +93,17 @@ class SourceResult:
 
 
 def gpu_source_phase(ctx, hosts, table, packets, round_end_ns, sim_end_ns, bootstrap_end_ns, owner_dev,
-                     n_ranks) -> SourceResult:
+                     n_ranks, ws: Optional[Workspace] = None) -> SourceResult:
     import torch
 
     n = len(packets)
     dev = packets.src_host.device
-    status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
-    deliver = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
-    eid = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
-    send = torch.empty((max(n, 1), 4), dtype=torch.int64, device=dev)
+    if ws is None:
+        ws = Workspace()
+    status = ws.get("status", max(n, 1), torch.uint8, dev)
+    deliver = ws.get("deliver", max(n, 1), torch.int64, dev)
+    eid = ws.get("eid", max(n, 1), torch.int64, dev)
+    send = ws.get("send", max(n, 1), torch.int64, dev, cols=4)
     counts = (C.c_uint32 * n_ranks)()
     p = _capi.sg_packets()
     p.n_packets = n
@@ -96,12 +120,15 @@ def gpu_source_phase(ctx, hosts, table, packets, round_end_ns, sim_end_ns, boots
                         st.min_used_latency_ns)
 
 
-def gpu_bucket_phase(ctx, recv, n_records: int, local_dev, n_hosts: int, n_local: int):
+def gpu_bucket_phase(ctx, recv, n_records: int, local_dev, n_hosts: int, n_local: int,
+                     ws: Optional[Workspace] = None):
     import torch
 
     dev = local_dev.device
-    order = torch.empty(max(n_records, 1), dtype=torch.int32, device=dev)
-    offsets = torch.empty(n_local + 1, dtype=torch.int32, device=dev)
+    if ws is None:
+        ws = Workspace()
+    order = ws.get("order", max(n_records, 1), torch.int32, dev)
+    offsets = ws.get("offsets", n_local + 1, torch.int32, dev)
     check(ctx.handle, load().sg_deliver_bucket(ctx.handle, recv.data_ptr() if n_records else None, n_records,
                                                local_dev.data_ptr(), n_hosts, n_local, order.data_ptr(),
                                                offsets.data_ptr()))
@@ -133,11 +160,13 @@ def all_to_all_records(send, send_counts: List[int], dist, group=None):
     return _records_all_to_all(send, send_counts, recv_counts, dist, group), recv_counts
 
 
-def exchange_round(send, send_counts: List[int], stats, rank: int, dist, group=None):
+def exchange_round(send, send_counts: List[int], stats, rank: int, dist, group=None,
+                   ws: Optional[Workspace] = None):
     """The round's one host round trip: an all-gather of every rank's row
     [delivered, min deliver time, min used latency, counts to each rank] (u64),
     so the round scalars ride with the counts exchange, then the records'
-    all_to_all_single.  Returns (recv, recv_counts, global stats)."""
+    all_to_all_single.  The row goes up and the gathered rows come back through
+    pinned host buffers.  Returns (recv, recv_counts, global stats)."""
     import torch
 
     world = len(send_counts)
@@ -145,21 +174,33 @@ def exchange_round(send, send_counts: List[int], stats, rank: int, dist, group=N
         recv, counts, g = exchange_round(send.cpu(), send_counts, stats, rank, dist, group)
         return recv.to(send.device), counts, g
     dev = send.device
-    mine = np.array([*stats, *send_counts], dtype=np.uint64).view(np.int64)
-    out = torch.empty(world * (3 + world), dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(out, torch.from_numpy(mine.copy()).to(dev), group=group)
-    allv = out.cpu().numpy().view(np.uint64).reshape(world, 3 + world)
+    if ws is None:
+        ws = Workspace()
+    w = 3 + world
+    pinned = dev.type != "cpu"
+    mine_h = ws.get("x_mine_h", w, torch.int64, "cpu", pinned=pinned)
+    mine_h.numpy()[:] = np.array([*stats, *send_counts], dtype=np.uint64).view(np.int64)
+    mine_d = ws.get("x_mine_d", w, torch.int64, dev)
+    mine_d.copy_(mine_h, non_blocking=True)
+    out = ws.get("x_out_d", world * w, torch.int64, dev)
+    dist.all_gather_into_tensor(out, mine_d, group=group)
+    out_h = ws.get("x_out_h", world * w, torch.int64, "cpu", pinned=pinned)
+    out_h.copy_(out, non_blocking=True)
+    if pinned:
+        torch.cuda.current_stream(dev).synchronize()
+    allv = out_h.numpy().view(np.uint64).reshape(world, w)
     recv_counts = [int(allv[r, 3 + rank]) for r in range(world)]
     g = (int(allv[:, 0].sum()), int(allv[:, 1].min()), int(allv[:, 2].min()))
-    return _records_all_to_all(send, send_counts, recv_counts, dist, group), recv_counts, g
+    return _records_all_to_all(send, send_counts, recv_counts, dist, group, ws), recv_counts, g
 
 
-def _records_all_to_all(send, send_counts: List[int], recv_counts: List[int], dist, group):
+def _records_all_to_all(send, send_counts: List[int], recv_counts: List[int], dist, group,
+                        ws: Optional[Workspace] = None):
     import torch
 
     dev = send.device
     n_recv = sum(recv_counts)
-    recv = torch.empty((max(n_recv, 1), 4), dtype=torch.int64, device=dev)
+    recv = (ws or Workspace()).get("x_recv", max(n_recv, 1), torch.int64, dev, cols=4)
     n_send = sum(send_counts)
     dist.all_to_all_single(recv[:n_recv], send[:n_send], output_split_sizes=recv_counts,
                            input_split_sizes=list(send_counts), group=group)
@@ -199,8 +240,11 @@ class ShardedDelivery:
                  exchange_fn: Optional[Callable] = None, device="cuda"):
         self.ctx, self.hosts, self.table, self.part = ctx, hosts, table, partition
         self.rank, self.world, self.dist, self.group = rank, world, dist, group
-        self.source_fn = source_fn or gpu_source_phase
-        self.bucket_fn = bucket_fn or gpu_bucket_phase
+        import functools
+
+        self.ws = Workspace()  # the round's buffers, reused round after round
+        self.source_fn = source_fn or functools.partial(gpu_source_phase, ws=self.ws)
+        self.bucket_fn = bucket_fn or functools.partial(gpu_bucket_phase, ws=self.ws)
         self.exchange_fn = exchange_fn  # None: exchange_round (counts and round scalars in one all-gather)
         import torch
 
@@ -212,13 +256,15 @@ class ShardedDelivery:
         self.last_send_counts = None
 
     def round(self, packets, round_end_ns: int, sim_end_ns: int, bootstrap_end_ns: int = 0):
+        """One round.  The returned tensors are views of buffers the next round
+        overwrites (copy what must outlive it)."""
         src = self.source_fn(self.ctx, self.hosts, self.table, packets, round_end_ns, sim_end_ns, bootstrap_end_ns,
                              self.owner_dev, self.world)
         stats = (int(src.n_delivered), int(src.min_deliver_time_ns), int(src.min_used_latency_ns))
         self.last_send_counts = list(src.send_counts)
         if self.exchange_fn is None:
             recv, recv_counts, self.last_stats = exchange_round(src.send, src.send_counts, stats, self.rank,
-                                                                self.dist, self.group)
+                                                                self.dist, self.group, ws=self.ws)
         else:
             recv, recv_counts = self.exchange_fn(src.send, src.send_counts)
             self.last_stats = gather_round_stats(*stats, self.dist, self.group, self.device)

@@ -99,9 +99,27 @@ def main():
         deliver_round(ht, table, batch, end, 2**63, start + 100_000, out=out)
     torch.cuda.synchronize()
     t_single = (time.perf_counter() - t0) / reps
+    # the sharded round's phases one at a time (each call returns synchronised)
+    from shadow_amd.dist import gpu_bucket_phase, gpu_source_phase
+    ph = {"source": 0.0, "exchange": 0.0, "bucket": 0.0}
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        s = gpu_source_phase(ctx, ht_s, table, batch, end, 2**63, start + 100_000, sd.owner_dev, 1)
+        t1 = time.perf_counter()
+        rv, rc, _ = exchange_round(s.send, s.send_counts, (int(s.n_delivered), int(s.min_deliver_time_ns),
+                                                           int(s.min_used_latency_ns)), 0, dist)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        gpu_bucket_phase(ctx, rv, int(sum(rc)), sd.local_dev, len(part.local), part.n_local(0))
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        ph["source"] += (t1 - t0) / reps
+        ph["exchange"] += (t2 - t1) / reps
+        ph["bucket"] += (t3 - t2) / reps
     print(json.dumps({"ok": True, "backend": dist.get_backend(), "packets": P, "records": int(sum(recv_counts)),
                       "sharded_round_ms": round(t_round * 1e3, 4), "exchange_round_ms": round(t_ex * 1e3, 4),
-                      "single_gpu_round_ms": round(t_single * 1e3, 4)}), flush=True)
+                      "single_gpu_round_ms": round(t_single * 1e3, 4),
+                      "phases_ms": {k: round(v * 1e3, 4) for k, v in ph.items()}}), flush=True)
     dist.destroy_process_group()
 
 
