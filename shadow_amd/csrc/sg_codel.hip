@@ -478,13 +478,19 @@ struct Relay {
   uint64_t tt;  // pending task time
   uint32_t cp, cl;  // cached packet, its length
   uint64_t cap, bal, inc, last;  // token bucket (token_bucket.rs:6-12)
+  uint64_t n_max;                 // u64::MAX / inc (inc != 0): the refill count past which tokens saturate
 
+  // inc is fixed for the call: the one u64 division by it happens here, not on every refill
+  __device__ void set_inc(uint64_t v) {
+    inc = v;
+    n_max = v ? ~0ull / v : ~0ull;
+  }
   // lazy_refill (token_bucket.rs:124-158): the span to the next refill
   __device__ uint64_t lazy_refill(uint64_t now) {
     uint64_t span = now - last;
     if (span >= TB_INTERVAL) {
       const uint64_t n = span / TB_INTERVAL;
-      const uint64_t tokens = (inc != 0 && n > ~0ull / inc) ? ~0ull : inc * n;
+      const uint64_t tokens = (inc != 0 && n > n_max) ? ~0ull : inc * n;
       const uint64_t b = bal > ~0ull - tokens ? ~0ull : bal + tokens;
       bal = b > cap ? cap : b;
       last = sat_add(last, n > ~0ull / TB_INTERVAL ? ~0ull : TB_INTERVAL * n);
@@ -500,7 +506,8 @@ struct Relay {
       return true;
     }
     const uint64_t need = dec - bal;
-    const uint64_t nref = need / inc + (need % inc ? 1 : 0);
+    const uint64_t qn = need / inc;
+    const uint64_t nref = qn + (need - qn * inc ? 1 : 0);
     if (nref == 1) {
       wait = next;
     } else {
@@ -596,7 +603,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
     r.cl = ia.cached_len[h];
     r.cap = ia.tb_cap[h];
     r.bal = ia.tb_bal[h];
-    r.inc = ia.tb_inc[h];
+    r.set_inc(ia.tb_inc[h]);
     r.last = ia.tb_last[h];
   }
   auto due = [&](uint64_t before) {  // a pending task earlier than `before` (Packet events go first)
@@ -810,7 +817,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
     r.tt = a.task_time[h];
     r.cap = a.tb_cap[h];
     r.bal = a.tb_bal[h];
-    r.inc = a.tb_inc[h];
+    r.set_inc(a.tb_inc[h]);
     r.last = a.tb_last[h];
     q.oldest = q.head - ((r.rf & R_CACHED) ? 1u : 0u);
     if (r.rf & R_CACHED) q.cr = q.ring[(q.head - 1) & q.mask];

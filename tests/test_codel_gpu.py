@@ -85,6 +85,43 @@ def test_random_streams_over_calls(oracle, ctx, gap_ms, p_pop):
     assert (ostat == 2).any() and (ostat == 1).any()
 
 
+def test_queue_deeper_than_a_chunk(oracle, ctx):
+    """One host's queue grows past a staged chunk (1024 events) and drains in later
+    chunks: its elements are read back from the ring in HBM, which the kernel
+    writes only for what outlives each chunk.  Then push/pop cycles wrap the ring
+    indices several times.  Neighbour hosts have a few events each."""
+    rng = np.random.default_rng(5)
+    cap = 4096
+    q = CoDelQueues(3, cap, ctx=ctx)
+    os_ = oracle.codel_state(3, q.cap)
+    n_pkt = 40000
+    gstat, ostat = _status(n_pkt), np.zeros(n_pkt, np.uint8)
+    t0 = T0 + 10**9
+    # host 1: 2500 pushes 1 us apart, then 2500 pops 2 ms apart (drop mode), in one call
+    h1_kind = np.r_[np.zeros(2500, np.uint8), np.ones(2500, np.uint8)]
+    h1_t = np.r_[t0 + np.arange(2500) * 1000, t0 + 3 * MS + np.arange(2500) * 2 * MS].astype(np.uint64)
+    host = np.r_[np.zeros(3, np.uint32), np.ones(5000, np.uint32), np.full(3, 2, np.uint32)]
+    kind = np.r_[np.array([0, 1, 1], np.uint8), h1_kind, np.array([0, 0, 1], np.uint8)]
+    t = np.r_[t0 + np.arange(3) * MS, h1_t, t0 + np.arange(3) * MS].astype(np.uint64)
+    pkt = np.arange(len(host), dtype=np.uint32)
+    ln = rng.integers(40, 1500, len(host)).astype(np.uint32)
+    _run_both(oracle, q, os_, gstat, ostat, host, kind, t, pkt, ln)
+    _same_state(oracle, q.get_state(), os_)
+    # wrap: calls of bursts (push 600, pop 400) on host 1, queue depth stepping up and down
+    tn, p0 = int(t.max()) + MS, len(host)
+    for c in range(12):
+        k = np.r_[np.zeros(600, np.uint8), np.ones(400 if c % 3 else 900, np.uint8)]
+        tt = (tn + np.arange(len(k)) * 50_000).astype(np.uint64)
+        hh = np.ones(len(k), np.uint32)
+        pp = (p0 + np.arange(len(k))).astype(np.uint32)
+        _run_both(oracle, q, os_, gstat, ostat, hh, k, tt, pp, rng.integers(40, 1500, len(k)).astype(np.uint32))
+        tn, p0 = int(tt.max()) + MS, p0 + len(k)
+    _same_state(oracle, q.get_state(), os_)
+    st = q.get_state()
+    assert int(st["tail"][1]) > 2 * cap  # the ring indices wrapped
+    assert (ostat == 2).any() and (ostat == 1).any()
+
+
 def test_large_single_call(oracle, ctx):
     """100k hosts, 1M events (the bench shape), one call."""
     rng = np.random.default_rng(11)
