@@ -11,6 +11,7 @@
 #include <string>
 #include <atomic>
 #include <deque>
+#include <memory>
 #include <vector>
 
 #include "../../include/shadow_gpu.h"
@@ -73,13 +74,6 @@ struct KernelTimer {
   uint64_t launches = 0;
 };
 
-// Per-source LDS-resident shortest paths (sg_sssp.hip).
-bool sssp_lds_fits(uint32_t n_nodes);
-void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_arc, uint32_t n, uint32_t n_arcs,
-                     const uint32_t* d_used, uint32_t n_used, uint32_t row_begin, uint32_t row_end,
-                     const uint32_t* self_edge, const uint64_t* e_lat, const float* e_loss, uint64_t* out_lat,
-                     float* out_loss, uint32_t* sat_row, uint32_t delta, unsigned long long* work,
-                     unsigned long long* diag);
 
 }  // namespace sg
 
@@ -129,6 +123,20 @@ struct sg_ctx {
   std::vector<hipEvent_t> event_pool;
 };
 
+// A two-phase plan for the LDS search over rows [row_begin, row_end) of a used
+// list (sg_routing.hip sssp_plan): seed rows first, then every other row bounded
+// by a seed out-neighbour's finished row.  Device arrays: [seed rows][other
+// rows][their seed's row][the arc latency to it].
+struct sg_sssp_plan {
+  std::vector<uint32_t> used;
+  int mode = 0;  // seed selection (SG_SSSP_SEED_MODE)
+  uint32_t row_begin = 0, row_end = 0, n_seed = 0, n_other = 0;
+  uint32_t* d = nullptr;
+  ~sg_sssp_plan() {
+    if (d) (void)hipFree(d);
+  }
+};
+
 // Device-resident network graph (sg_routing.hip builds it).
 struct sg_net {
   sg_ctx* ctx = nullptr;
@@ -155,6 +163,9 @@ struct sg_net {
   // self-loops
   uint32_t* self_cnt = nullptr;
   uint32_t* self_edge = nullptr;
+  // host copy of the out-arc heads and latencies (for sssp plans), and the plans
+  std::vector<uint32_t> h_out_off, h_out_head, h_out_lat;
+  std::deque<std::unique_ptr<sg_sssp_plan>> plans;
   ~sg_net() {
     void* ps[] = {e_src, e_dst, e_lat, e_loss, in_off, in_src, in_dst, in_lat, in_lat32, in_om, in_rec, out_off,
                   out_arc, self_cnt, self_edge};
@@ -250,12 +261,18 @@ struct TimedLaunch {
   ~TimedLaunch();
 };
 
-// Per-source LDS-resident shortest paths (sg_sssp.hip).
+// Per-source LDS-resident shortest paths (sg_sssp.hip).  Rows [row_begin,
+// row_end) of the table, one workgroup each; or, with blk_rows, the n_blk rows
+// listed there (absolute, within [row_begin, row_end)).  ub_row / ub_w (per
+// workgroup, optional): the row of an out-neighbour s' already in the table
+// (~0u: none) and the arc latency s -> s'; the search starts every key at the
+// bound (w + D[s'][v]) + 1 instead of infinity (see sg_sssp.hip "Bounds").
 bool sssp_lds_fits(uint32_t n_nodes);
 void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_arc, uint32_t n, uint32_t n_arcs,
                      const uint32_t* d_used, uint32_t n_used, uint32_t row_begin, uint32_t row_end,
                      const uint32_t* self_edge, const uint64_t* e_lat, const float* e_loss, uint64_t* out_lat,
                      float* out_loss, uint32_t* sat_row, uint32_t delta, unsigned long long* work,
-                     unsigned long long* diag);
+                     unsigned long long* diag, const uint32_t* blk_rows = nullptr, uint32_t n_blk = 0,
+                     const uint32_t* ub_row = nullptr, const uint32_t* ub_w = nullptr);
 
 }  // namespace sg

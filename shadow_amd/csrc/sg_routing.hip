@@ -37,6 +37,7 @@
 // aligned dwordx2 halves.  Dense graphs (arc segments) flush with 64-bit
 // atomicMin instead.  The LDS kernel updates keys with 64-bit LDS atomics.
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -1148,8 +1149,138 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 // 5.6 ms at 100 ms buckets and 6.2 ms at 50 ms), for 2.5x Dijkstra's
 // relaxations against 1.06x at 50 ms -- the search is bound by its critical
 // path, not by its relaxation count.
-static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
-                               uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
+// Seeds and bounds for the LDS search (sg_sssp.hip "Bounds").  For an arc
+// s -> s' and any node v, w(s, s') + D[s'][v] is the latency of a real path, so
+// it bounds D[s][v] from above; a search whose keys start just above those
+// bounds rejects every slower candidate at its first atomic min (no queueing, no
+// pop) and reaches the same fixed point.  Phase 1 runs a maximal set of rows no
+// two of which are joined by an arc (greedy in row order, out-arcs); phase 2
+// runs every other row, each bounded by the row of its lowest-latency seed
+// out-neighbour (one exists by construction).  Cached per (used list, range).
+static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h_used, uint32_t n_used,
+                                     uint32_t row_begin, uint32_t row_end) {
+  const int mode = env_int("SG_SSSP_SEED_MODE", 1);
+  for (auto& p : net->plans)
+    if (p->mode == mode && p->row_begin == row_begin && p->row_end == row_end && p->used.size() == n_used &&
+        std::equal(p->used.begin(), p->used.end(), h_used))
+      return p.get();
+  const uint32_t n = net->n_nodes;
+  if (net->h_out_off.empty()) {
+    std::vector<uint32_t> arc((size_t)net->n_arcs * 3);
+    net->h_out_off.resize((size_t)n + 1);
+    copy_to_host(ctx, net->h_out_off.data(), net->out_off, ((size_t)n + 1) * 4);
+    if (net->n_arcs) copy_to_host(ctx, arc.data(), net->out_arc, arc.size() * 4);
+    net->h_out_head.resize(net->n_arcs);
+    net->h_out_lat.resize(net->n_arcs);
+    for (size_t a = 0; a < net->n_arcs; a++) {
+      net->h_out_head[a] = arc[3 * a];
+      net->h_out_lat[a] = arc[3 * a + 1];
+    }
+  }
+  const uint32_t* off = net->h_out_off.data();
+  const uint32_t *head = net->h_out_head.data(), *lat = net->h_out_lat.data();
+  const uint32_t rows = row_end - row_begin;
+  std::vector<uint32_t> rel(n, ~0u);  // node -> its row in range, relative
+  for (uint32_t r = 0; r < rows; r++) rel[h_used[row_begin + r]] = r;
+  std::vector<uint8_t> seed(rows, 0);
+  std::vector<uint32_t> seeds, others, ub_row, ub_w;
+  if (mode == 1) {
+    // greedy dominating set: a seed covers itself and every row with an arc to it;
+    // take the row covering the most uncovered rows, lazily re-scored (max-heap)
+    std::vector<uint32_t> in_off(rows + 1, 0), in_row;
+    for (uint32_t r = 0; r < rows; r++) {
+      const uint32_t s = h_used[row_begin + r];
+      for (uint32_t a = off[s]; a < off[s + 1]; a++)
+        if (rel[head[a]] != ~0u) in_off[rel[head[a]] + 1]++;
+    }
+    for (uint32_t r = 0; r < rows; r++) in_off[r + 1] += in_off[r];
+    in_row.resize(in_off[rows]);
+    {
+      std::vector<uint32_t> cur(in_off.begin(), in_off.end() - 1);
+      for (uint32_t r = 0; r < rows; r++) {
+        const uint32_t s = h_used[row_begin + r];
+        for (uint32_t a = off[s]; a < off[s + 1]; a++)
+          if (rel[head[a]] != ~0u) in_row[cur[rel[head[a]]]++] = r;
+      }
+    }
+    std::vector<uint8_t> covered(rows, 0);
+    auto gain = [&](uint32_t v) {
+      uint32_t g = !covered[v];
+      for (uint32_t k = in_off[v]; k < in_off[v + 1]; k++) g += !covered[in_row[k]];
+      return g;
+    };
+    std::vector<std::pair<uint32_t, uint32_t>> heap;  // (gain, ~row): ties to the lower row
+    heap.reserve(rows);
+    for (uint32_t r = 0; r < rows; r++) heap.push_back({gain(r), ~r});
+    std::make_heap(heap.begin(), heap.end());
+    while (!heap.empty()) {
+      std::pop_heap(heap.begin(), heap.end());
+      const auto [g, nr] = heap.back();
+      heap.pop_back();
+      const uint32_t v = ~nr, gv = gain(v);
+      if (gv == 0) continue;
+      if (gv < g) {  // stale score: re-insert with the current one
+        heap.push_back({gv, nr});
+        std::push_heap(heap.begin(), heap.end());
+        continue;
+      }
+      seed[v] = 1;
+      covered[v] = 1;
+      for (uint32_t k = in_off[v]; k < in_off[v + 1]; k++) covered[in_row[k]] = 1;
+    }
+    for (uint32_t r = 0; r < rows; r++)
+      if (seed[r]) seeds.push_back(row_begin + r);
+  } else {
+    // maximal independent set in row order
+    for (uint32_t r = 0; r < rows; r++) {
+      const uint32_t s = h_used[row_begin + r];
+      bool has = false;
+      for (uint32_t a = off[s]; a < off[s + 1] && !has; a++) has = rel[head[a]] != ~0u && seed[rel[head[a]]];
+      if (!has) {
+        seed[r] = 1;
+        seeds.push_back(row_begin + r);
+      }
+    }
+  }
+  for (uint32_t r = 0; r < rows; r++) {
+    if (seed[r]) continue;
+    const uint32_t s = h_used[row_begin + r];
+    uint32_t best = ~0u, bw = ~0u;
+    for (uint32_t a = off[s]; a < off[s + 1]; a++) {
+      const uint32_t q = rel[head[a]];
+      if (q != ~0u && seed[q] && lat[a] < bw) {
+        bw = lat[a];
+        best = row_begin + q;
+      }
+    }
+    others.push_back(row_begin + r);
+    ub_row.push_back(best);  // (a seed out-neighbour exists: r was not made a seed)
+    ub_w.push_back(best == ~0u ? 0u : bw);
+  }
+  auto p = std::make_unique<sg_sssp_plan>();
+  p->used.assign(h_used, h_used + n_used);
+  p->mode = mode;
+  p->row_begin = row_begin;
+  p->row_end = row_end;
+  p->n_seed = (uint32_t)seeds.size();
+  p->n_other = (uint32_t)others.size();
+  std::vector<uint32_t> all;
+  all.reserve(seeds.size() + 3 * others.size());
+  all.insert(all.end(), seeds.begin(), seeds.end());
+  all.insert(all.end(), others.begin(), others.end());
+  all.insert(all.end(), ub_row.begin(), ub_row.end());
+  all.insert(all.end(), ub_w.begin(), ub_w.end());
+  SG_HIP(hipMalloc(&p->d, std::max<size_t>(all.size() * 4, 16)));
+  SG_HIP(hipMemcpyAsync(p->d, all.data(), all.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  net->plans.push_front(std::move(p));
+  if (net->plans.size() > 16) net->plans.pop_back();
+  return net->plans.front().get();
+}
+
+static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, const uint32_t* h_used,
+                               uint32_t n_used, uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
+                               float* out_loss) {
   hipStream_t st = ctx->stream;
   const uint32_t rows = row_end - row_begin;
   uint32_t* sat = ctx->r_flags.get<uint32_t>(rows);
@@ -1164,7 +1295,28 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   const uint32_t n_diag = std::min<uint32_t>(rows, 4096);
   unsigned long long* diag = diag_on ? ctx->r_misc.get<unsigned long long>((size_t)n_diag * 8) : nullptr;
   if (diag) SG_HIP(hipMemsetAsync(diag, 0, (size_t)n_diag * 64, st));
-  {
+  // Two phases (sssp_plan) when the rows fill the CUs many times over: with a
+  // few rows per CU the phase boundary costs more than the bounds save (2,000
+  // nodes: 0.41 against 0.39 ms).  SG_SSSP_SEEDS=0 never, =2 always.
+  const int seeds_env = env_int("SG_SSSP_SEEDS", 1);
+  const bool two_phase = h_used && seeds_env != 0 && (seeds_env == 2 || rows >= 16u * 256u);
+  const sg_sssp_plan* plan = two_phase ? sssp_plan(ctx, net, h_used, n_used, row_begin, row_end) : nullptr;
+  if (plan && plan->n_other) {
+    const uint32_t* pd = plan->d;
+    const uint32_t ns = plan->n_seed, no = plan->n_other;
+    {
+      TimedLaunch tl(ctx, "sssp", 0.0);
+      launch_sssp_lds(ctx, net->out_off, net->out_arc, net->n_nodes, net->n_arcs, d_used, n_used, row_begin,
+                      row_end, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work, nullptr,
+                      pd, ns);
+    }
+    {
+      TimedLaunch tl(ctx, "sssp_bounded", 0.0);
+      launch_sssp_lds(ctx, net->out_off, net->out_arc, net->n_nodes, net->n_arcs, d_used, n_used, row_begin,
+                      row_end, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work, diag,
+                      pd + ns, no, pd + ns + no, pd + ns + 2 * (size_t)no);
+    }
+  } else {
     TimedLaunch tl(ctx, "sssp", 0.0);
     launch_sssp_lds(ctx, net->out_off, net->out_arc, net->n_nodes, net->n_arcs, d_used, n_used, row_begin,
                     row_end, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work, diag);
@@ -1197,8 +1349,9 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   if (!wide_rows.empty()) run_wide(ctx, net, d_used, n_used, wide_rows, row_begin, out_lat, out_loss);
 }
 
-static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
-                           uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
+static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, const uint32_t* h_used,
+                           uint32_t n_used, uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
+                           float* out_loss) {
   // SG_APSP_LDS=0 forces the batched-source slab kernel.  The LDS search takes
   // sparse graphs (mean out-degree <= 64); on dense ones the slab kernel shares
   // each arc record among 64 sources (C2, 1,200-node complete graph: 3.6 ms
@@ -1206,7 +1359,7 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uin
   const bool sparse = net->n_nodes && net->n_arcs <= 64ull * net->n_nodes;
   if (env_int("SG_APSP_LDS", 1) != 0 && sparse && sssp_lds_fits(net->n_nodes) &&
       (uint64_t)net->n_arcs * 12 < (1ull << 31)) {
-    shortest_paths_lds(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss);
+    shortest_paths_lds(ctx, net, d_used, h_used, n_used, row_begin, row_end, out_lat, out_loss);
     return;
   }
   const bool front = env_int("SG_APSP_FRONTIER", 1) != 0;
@@ -1358,7 +1511,7 @@ int32_t sg_routing_build(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32
     uint64_t* o_lat = dev_out ? out_latency_ns : ctx->r_out_lat.get<uint64_t>(count);
     float* o_loss = dev_out ? out_packet_loss : ctx->r_out_loss.get<float>(count);
     if (shortest)
-      shortest_paths(ctx, net, d_used, n_used, row_begin, row_end, o_lat, o_loss);
+      shortest_paths(ctx, net, d_used, nodes, n_used, row_begin, row_end, o_lat, o_loss);
     else
       direct_paths(ctx, net, d_used, nodes, n_used, row_begin, row_end, o_lat, o_loss);
     if (!dev_out) {
@@ -1422,7 +1575,7 @@ int32_t sg_routing_info_fill(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, ui
       ctx->in_fill = true;
       try {
         if (shortest)
-          shortest_paths(ctx, net, d_used, n_used, r0, r1, slat[b], sloss[b]);
+          shortest_paths(ctx, net, d_used, nodes, n_used, r0, r1, slat[b], sloss[b]);
         else
           direct_paths(ctx, net, d_used, nodes, n_used, r0, r1, slat[b], sloss[b]);
       } catch (...) {

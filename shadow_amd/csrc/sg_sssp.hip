@@ -159,7 +159,8 @@ __global__ void __launch_bounds__(NT)
                const float* __restrict__ e_loss, uint64_t* __restrict__ out_lat, float* __restrict__ out_loss,
                uint32_t* __restrict__ sat_row, uint32_t delta, int vec_out, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ diag, uint32_t claim, uint32_t idle_sleep,
-               uint32_t lane_deg_max) {
+               uint32_t lane_deg_max, const uint32_t* __restrict__ blk_rows,
+               const uint32_t* __restrict__ ub_row, const uint32_t* __restrict__ ub_w) {
   constexpr int NW = NT / 64;
   extern __shared__ __align__(16) unsigned char smem[];
   const uint32_t cap = sssp_ring_cap(n);
@@ -181,7 +182,7 @@ __global__ void __launch_bounds__(NT)
   const unsigned long long c_start = dg ? clock64() : 0;
   uint32_t n_adv = 0, n_pops = 0;
   unsigned long long cyc_claim = 0, cyc_pop = 0, cyc_steps = 0;  // per wave, COUNT diagnostics
-  const uint32_t row = row_begin + blockIdx.x;
+  const uint32_t row = blk_rows ? blk_rows[blockIdx.x] : row_begin + blockIdx.x;
   const uint32_t src = used[row];
   for (uint32_t v = tid; v < n; v += NT) key[v] = FKEY_INF;
   for (uint32_t v = tid; v <= n; v += NT) off[v] = out_off[v];
@@ -190,6 +191,18 @@ __global__ void __launch_bounds__(NT)
   if (tid < 8) ctl[tid] = 0;
   if (tid == 0) hb = 0;
   __syncthreads();
+  if (ub_row) {  // Bounds: keys start just above a known path's latency (clean)
+    const uint32_t sr = ub_row[blockIdx.x];
+    if (sr != ~0u) {
+      const uint64_t w = ub_w[blockIdx.x];
+      const uint64_t* srow = out_lat + (size_t)(sr - out_row0) * n_used;
+      for (uint32_t j = tid; j < n_used; j += NT) {
+        const uint64_t ub = srow[j] + w;  // w < 2^32 and srow[j] <= u64::MAX: wrap means >= 2^64
+        if (ub >= w && ub + 1 < LAT32_SAT) key[used[j]] = ((ub + 1) << 32) | ((uint64_t)0x3F800000u << 1);
+      }
+    }
+    __syncthreads();
+  }
   if (tid == 0) {
     key[src] = 1ull;  // PathProperties::default(), dirty and queued
     ring[0] = (uint16_t)src;
@@ -428,7 +441,7 @@ __global__ void __launch_bounds__(NT)
       out_loss[orow + j] = f;
     }
   }
-  if (__any(sat) && lane == 0) sat_row[blockIdx.x] = 1u;
+  if (__any(sat) && lane == 0) sat_row[row - row_begin] = 1u;
   if (dg) {
     diag[blockIdx.x * 8 + 0] = c_search - c_start;
     diag[blockIdx.x * 8 + 1] = clock64() - c_search;
@@ -447,7 +460,8 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
                      const uint32_t* d_used, uint32_t n_used, uint32_t row_begin, uint32_t row_end,
                      const uint32_t* self_edge, const uint64_t* e_lat, const float* e_loss, uint64_t* out_lat,
                      float* out_loss, uint32_t* sat_row, uint32_t delta, unsigned long long* work,
-                     unsigned long long* diag) {
+                     unsigned long long* diag, const uint32_t* blk_rows, uint32_t n_blk, const uint32_t* ub_row,
+                     const uint32_t* ub_w) {
   const size_t lds = sssp_lds_bytes(n);
   if (!sssp_lds_fits(n)) throw Error(SG_ERR_INVALID_ARG, "graph too large for the LDS-resident search");
   if ((uint64_t)n_arcs * 12 >= (1ull << 31)) throw Error(SG_ERR_INVALID_ARG, "too many arcs for 32-bit offsets");
@@ -455,7 +469,7 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
   const char* cs = getenv("SG_SSSP_CLAIM");
   const uint32_t claim = (uint32_t)std::min(64, std::max(1, cs && *cs ? atoi(cs) : 64));
   const int vec = n_used % 4 == 0 && ((uintptr_t)out_lat & 15) == 0 && ((uintptr_t)out_loss & 15) == 0;
-  const uint32_t rows = row_end - row_begin;
+  const uint32_t rows = blk_rows ? n_blk : row_end - row_begin;
   if (!rows) return;
   const char* ts = getenv("SG_SSSP_THREADS");
   const int nt = ts && atoi(ts) == 512 ? 512 : 1024;
@@ -470,7 +484,7 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
                                (int)(LDS_PER_CU - SSSP_STATIC_LDS)));
     hipLaunchKernelGGL(kern, dim3(rows), dim3(nt), lds, ctx->stream, out_off, out_arc, n, n_arcs, d_used, n_used,
                        row_begin, row_begin, self_edge, e_lat, e_loss, out_lat, out_loss, sat_row, delta, vec, work,
-                       diag, claim, idle_sleep, lane_deg);
+                       diag, claim, idle_sleep, lane_deg, blk_rows, ub_row, ub_w);
   };
   if (work) {
     if (nt == 512) go(k_sssp_lds<true, 512, 8, 0>);

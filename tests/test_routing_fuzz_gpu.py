@@ -10,11 +10,13 @@ from shadow_amd import NetworkGraph
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["lds", "slab"])
+@pytest.fixture(autouse=True, params=["lds", "lds_bounded", "slab"])
 def apsp_kernel(request, monkeypatch):
-    """Both shortest-path kernels: the per-source LDS search and the slab relaxation."""
-    monkeypatch.setenv("SG_APSP_LDS", "1" if request.param == "lds" else "0")
-    return request.param
+    """Both shortest-path kernels: the per-source LDS search (also in its forced
+    two-phase form, seed rows then bounded rows) and the slab relaxation."""
+    monkeypatch.setenv("SG_APSP_LDS", "0" if request.param == "slab" else "1")
+    monkeypatch.setenv("SG_SSSP_SEEDS", "2" if request.param == "lds_bounded" else "1")
+    return "lds" if request.param.startswith("lds") else request.param
 
 
 def _random_graph(n, avg_deg, directed, seed):

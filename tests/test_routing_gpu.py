@@ -16,13 +16,16 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(autouse=True, params=["lds", "slab"])
+@pytest.fixture(autouse=True, params=["lds", "lds_bounded", "slab"])
 def apsp_kernel(request, monkeypatch):
     """Every routing test runs on both shortest-path kernels: the per-source
     LDS-resident search (sg_sssp.hip, the default up to ~10.9k nodes) and the
-    batched-source slab relaxation (k_relax_w2, larger graphs)."""
-    monkeypatch.setenv("SG_APSP_LDS", "1" if request.param == "lds" else "0")
-    return request.param
+    batched-source slab relaxation (k_relax_w2, larger graphs).  lds_bounded
+    forces the LDS search's two phases (seed rows, then rows whose keys start
+    at a seed neighbour's bounds), which the default uses from 4,096 rows on."""
+    monkeypatch.setenv("SG_APSP_LDS", "0" if request.param == "slab" else "1")
+    monkeypatch.setenv("SG_SSSP_SEEDS", "2" if request.param == "lds_bounded" else "1")
+    return "lds" if request.param.startswith("lds") else request.param
 
 
 def _graph(g, ctx):

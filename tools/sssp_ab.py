@@ -44,6 +44,10 @@ def main():
             net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
+        ctx.enable_timers(True)
+        net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
+        tm = {k: round(ctx.read_timer(k)[0], 4) for k in ("sssp", "sssp_bounded", "relax", "relax_wide")}
+        ctx.enable_timers(False)
         h = (lat.view(torch.int64).sum().item(), loss.view(torch.int32).to(torch.int64).sum().item())
         if first is None:
             first = (lat.clone(), loss.clone())
@@ -51,7 +55,7 @@ def main():
         else:
             same = bool(torch.equal(first[0], lat) and torch.equal(first[1].view(torch.int32), loss.view(torch.int32)))
         print(json.dumps({"setting": st, "n": n, "ms_median": round(float(np.median(ts)), 4),
-                          "ms_min": round(min(ts), 4), "same_as_first": same, "checksum": h}), flush=True)
+                          "ms_min": round(min(ts), 4), "timers_ms": tm, "same_as_first": same, "checksum": h}), flush=True)
         for k, v in old.items():
             if v is None:
                 os.environ.pop(k, None)
