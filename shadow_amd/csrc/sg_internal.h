@@ -123,14 +123,19 @@ struct sg_ctx {
   std::vector<hipEvent_t> event_pool;
 };
 
-// A two-phase plan for the LDS search over rows [row_begin, row_end) of a used
-// list (sg_routing.hip sssp_plan): seed rows first, then every other row bounded
-// by a seed out-neighbour's finished row.  Device arrays: [seed rows][other
-// rows][their seed's row][the arc latency to it].
+// A phased plan for the LDS search over rows [row_begin, row_end) of a used
+// list (sg_routing.hip sssp_plan): phase 0 rows from infinity, then rows bounded
+// by out-neighbours finished in earlier phases.  Device arrays per phase: [rows]
+// [SSSP_KB_MAX bound rows per row][their arc latencies].
 struct sg_sssp_plan {
   std::vector<uint32_t> used;
-  int mode = 0;  // seed selection (SG_SSSP_SEED_MODE)
-  uint32_t row_begin = 0, row_end = 0, n_seed = 0, n_other = 0;
+  int mode = 0;  // the settings it was built for (phases, bounds per row)
+  uint32_t row_begin = 0, row_end = 0;
+  struct Phase {
+    uint32_t n = 0;                       // rows in the phase
+    size_t rows = 0, ub_row = 0, ub_w = 0;  // offsets into d (u32): row list, bound rows, bound latencies
+  };
+  std::vector<Phase> phases;
   uint32_t* d = nullptr;
   ~sg_sssp_plan() {
     if (d) (void)hipFree(d);
@@ -264,9 +269,11 @@ struct TimedLaunch {
 // Per-source LDS-resident shortest paths (sg_sssp.hip).  Rows [row_begin,
 // row_end) of the table, one workgroup each; or, with blk_rows, the n_blk rows
 // listed there (absolute, within [row_begin, row_end)).  ub_row / ub_w (per
-// workgroup, optional): the row of an out-neighbour s' already in the table
-// (~0u: none) and the arc latency s -> s'; the search starts every key at the
-// bound (w + D[s'][v]) + 1 instead of infinity (see sg_sssp.hip "Bounds").
+// workgroup, SSSP_KB_MAX each, optional): rows of out-neighbours s' already in
+// the table (~0u: none) and the arc latencies s -> s'; the search starts every
+// key at min over them of (w + D[s'][v]) + 1 instead of infinity.  The bound
+// rows must be final before the launch (an earlier launch on the stream).
+constexpr int SSSP_KB_MAX = 4;  // bound rows per bounded search (sg_sssp.hip SSSP_KB)
 bool sssp_lds_fits(uint32_t n_nodes);
 void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_arc, uint32_t n, uint32_t n_arcs,
                      const uint32_t* d_used, uint32_t n_used, uint32_t row_begin, uint32_t row_end,

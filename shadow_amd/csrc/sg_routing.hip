@@ -1149,17 +1149,22 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 // 5.6 ms at 100 ms buckets and 6.2 ms at 50 ms), for 2.5x Dijkstra's
 // relaxations against 1.06x at 50 ms -- the search is bound by its critical
 // path, not by its relaxation count.
-// Seeds and bounds for the LDS search (sg_sssp.hip "Bounds").  For an arc
+// Phases and bounds for the LDS search (sg_sssp.hip "Bounds").  For an arc
 // s -> s' and any node v, w(s, s') + D[s'][v] is the latency of a real path, so
 // it bounds D[s][v] from above; a search whose keys start just above those
 // bounds rejects every slower candidate at its first atomic min (no queueing, no
-// pop) and reaches the same fixed point.  Phase 1 runs a maximal set of rows no
-// two of which are joined by an arc (greedy in row order, out-arcs); phase 2
-// runs every other row, each bounded by the row of its lowest-latency seed
-// out-neighbour (one exists by construction).  Cached per (used list, range).
+// pop) and reaches the same fixed point.  Phase 0 is a greedy dominating set of
+// the rows (row u is covered by a chosen v when u == v or u has an arc to v) and
+// runs from infinity; each later phase but the last is a dominating set of the
+// rows left; the last phase takes the rest.  A row of phase p >= 1 is bounded by
+// its SSSP_KB_MAX lowest-latency out-neighbours in phases < p (phase 0 dominates,
+// so it has one).  Each phase is one launch: a kernel boundary publishes the
+// rows the next phase reads.  Cached per (used list, range, settings).
 static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h_used, uint32_t n_used,
                                      uint32_t row_begin, uint32_t row_end) {
-  const int mode = env_int("SG_SSSP_SEED_MODE", 1);
+  const int n_phase = std::max(2, std::min(6, env_int("SG_SSSP_PHASES", 3)));
+  const int kb = std::max(1, std::min(SSSP_KB_MAX, env_int("SG_SSSP_BOUNDS", 1)));
+  const int mode = n_phase * 16 + kb;
   for (auto& p : net->plans)
     if (p->mode == mode && p->row_begin == row_begin && p->row_end == row_end && p->used.size() == n_used &&
         std::equal(p->used.begin(), p->used.end(), h_used))
@@ -1182,94 +1187,101 @@ static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h
   const uint32_t rows = row_end - row_begin;
   std::vector<uint32_t> rel(n, ~0u);  // node -> its row in range, relative
   for (uint32_t r = 0; r < rows; r++) rel[h_used[row_begin + r]] = r;
-  std::vector<uint8_t> seed(rows, 0);
-  std::vector<uint32_t> seeds, others, ub_row, ub_w;
-  if (mode == 1) {
-    // greedy dominating set: a seed covers itself and every row with an arc to it;
-    // take the row covering the most uncovered rows, lazily re-scored (max-heap)
-    std::vector<uint32_t> in_off(rows + 1, 0), in_row;
+  // in-arcs among the rows: in_row[in_off[v] ..] = the rows u with an arc u -> v
+  std::vector<uint32_t> in_off(rows + 1, 0), in_row;
+  for (uint32_t r = 0; r < rows; r++) {
+    const uint32_t s = h_used[row_begin + r];
+    for (uint32_t a = off[s]; a < off[s + 1]; a++)
+      if (rel[head[a]] != ~0u) in_off[rel[head[a]] + 1]++;
+  }
+  for (uint32_t r = 0; r < rows; r++) in_off[r + 1] += in_off[r];
+  in_row.resize(in_off[rows]);
+  {
+    std::vector<uint32_t> cur(in_off.begin(), in_off.end() - 1);
     for (uint32_t r = 0; r < rows; r++) {
       const uint32_t s = h_used[row_begin + r];
       for (uint32_t a = off[s]; a < off[s + 1]; a++)
-        if (rel[head[a]] != ~0u) in_off[rel[head[a]] + 1]++;
+        if (rel[head[a]] != ~0u) in_row[cur[rel[head[a]]]++] = r;
     }
-    for (uint32_t r = 0; r < rows; r++) in_off[r + 1] += in_off[r];
-    in_row.resize(in_off[rows]);
-    {
-      std::vector<uint32_t> cur(in_off.begin(), in_off.end() - 1);
-      for (uint32_t r = 0; r < rows; r++) {
-        const uint32_t s = h_used[row_begin + r];
-        for (uint32_t a = off[s]; a < off[s + 1]; a++)
-          if (rel[head[a]] != ~0u) in_row[cur[rel[head[a]]]++] = r;
-      }
-    }
+  }
+  std::vector<int> phase(rows, -1);
+  for (int ph = 0; ph + 1 < n_phase; ph++) {
+    // greedy dominating set of the rows still unassigned (lazily re-scored max-heap)
     std::vector<uint8_t> covered(rows, 0);
+    auto live = [&](uint32_t u) { return phase[u] < 0 && !covered[u]; };
     auto gain = [&](uint32_t v) {
-      uint32_t g = !covered[v];
-      for (uint32_t k = in_off[v]; k < in_off[v + 1]; k++) g += !covered[in_row[k]];
+      uint32_t g = live(v);
+      for (uint32_t k = in_off[v]; k < in_off[v + 1]; k++) g += live(in_row[k]);
       return g;
     };
     std::vector<std::pair<uint32_t, uint32_t>> heap;  // (gain, ~row): ties to the lower row
-    heap.reserve(rows);
-    for (uint32_t r = 0; r < rows; r++) heap.push_back({gain(r), ~r});
+    for (uint32_t r = 0; r < rows; r++)
+      if (phase[r] < 0) heap.push_back({gain(r), ~r});
     std::make_heap(heap.begin(), heap.end());
+    std::vector<uint32_t> chosen;
     while (!heap.empty()) {
       std::pop_heap(heap.begin(), heap.end());
       const auto [g, nr] = heap.back();
       heap.pop_back();
       const uint32_t v = ~nr, gv = gain(v);
       if (gv == 0) continue;
-      if (gv < g) {  // stale score: re-insert with the current one
+      if (gv < g) {
         heap.push_back({gv, nr});
         std::push_heap(heap.begin(), heap.end());
         continue;
       }
-      seed[v] = 1;
+      chosen.push_back(v);
       covered[v] = 1;
       for (uint32_t k = in_off[v]; k < in_off[v + 1]; k++) covered[in_row[k]] = 1;
     }
-    for (uint32_t r = 0; r < rows; r++)
-      if (seed[r]) seeds.push_back(row_begin + r);
-  } else {
-    // maximal independent set in row order
-    for (uint32_t r = 0; r < rows; r++) {
-      const uint32_t s = h_used[row_begin + r];
-      bool has = false;
-      for (uint32_t a = off[s]; a < off[s + 1] && !has; a++) has = rel[head[a]] != ~0u && seed[rel[head[a]]];
-      if (!has) {
-        seed[r] = 1;
-        seeds.push_back(row_begin + r);
-      }
-    }
+    for (uint32_t v : chosen) phase[v] = ph;
   }
-  for (uint32_t r = 0; r < rows; r++) {
-    if (seed[r]) continue;
-    const uint32_t s = h_used[row_begin + r];
-    uint32_t best = ~0u, bw = ~0u;
-    for (uint32_t a = off[s]; a < off[s + 1]; a++) {
-      const uint32_t q = rel[head[a]];
-      if (q != ~0u && seed[q] && lat[a] < bw) {
-        bw = lat[a];
-        best = row_begin + q;
-      }
-    }
-    others.push_back(row_begin + r);
-    ub_row.push_back(best);  // (a seed out-neighbour exists: r was not made a seed)
-    ub_w.push_back(best == ~0u ? 0u : bw);
-  }
+  for (uint32_t r = 0; r < rows; r++)
+    if (phase[r] < 0) phase[r] = n_phase - 1;
   auto p = std::make_unique<sg_sssp_plan>();
   p->used.assign(h_used, h_used + n_used);
   p->mode = mode;
   p->row_begin = row_begin;
   p->row_end = row_end;
-  p->n_seed = (uint32_t)seeds.size();
-  p->n_other = (uint32_t)others.size();
   std::vector<uint32_t> all;
-  all.reserve(seeds.size() + 3 * others.size());
-  all.insert(all.end(), seeds.begin(), seeds.end());
-  all.insert(all.end(), others.begin(), others.end());
-  all.insert(all.end(), ub_row.begin(), ub_row.end());
-  all.insert(all.end(), ub_w.begin(), ub_w.end());
+  std::vector<std::pair<uint32_t, uint32_t>> cand;  // (arc latency, row)
+  for (int ph = 0; ph < n_phase; ph++) {
+    std::vector<uint32_t> list, ubr, ubw;
+    for (uint32_t r = 0; r < rows; r++) {
+      if (phase[r] != ph) continue;
+      list.push_back(row_begin + r);
+      if (ph == 0) continue;
+      const uint32_t s = h_used[row_begin + r];
+      cand.clear();
+      for (uint32_t a = off[s]; a < off[s + 1]; a++) {
+        const uint32_t q = rel[head[a]];
+        if (q != ~0u && phase[q] < ph) cand.push_back({lat[a], row_begin + q});
+      }
+      std::sort(cand.begin(), cand.end());
+      int k = 0;
+      for (size_t c = 0; c < cand.size() && k < kb; c++) {  // distinct rows (parallel arcs: the lowest)
+        bool dup = false;
+        for (int i = 0; i < k; i++) dup |= ubr[ubr.size() - k + i] == cand[c].second;
+        if (dup) continue;
+        ubr.push_back(cand[c].second);
+        ubw.push_back(cand[c].first);
+        k++;
+      }
+      for (; k < SSSP_KB_MAX; k++) {
+        ubr.push_back(~0u);
+        ubw.push_back(0u);
+      }
+    }
+    sg_sssp_plan::Phase P;
+    P.n = (uint32_t)list.size();
+    P.rows = all.size();
+    all.insert(all.end(), list.begin(), list.end());
+    P.ub_row = all.size();
+    all.insert(all.end(), ubr.begin(), ubr.end());
+    P.ub_w = all.size();
+    all.insert(all.end(), ubw.begin(), ubw.end());
+    if (P.n) p->phases.push_back(P);
+  }
   SG_HIP(hipMalloc(&p->d, std::max<size_t>(all.size() * 4, 16)));
   SG_HIP(hipMemcpyAsync(p->d, all.data(), all.size() * 4, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
@@ -1301,20 +1313,15 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   const int seeds_env = env_int("SG_SSSP_SEEDS", 1);
   const bool two_phase = h_used && seeds_env != 0 && (seeds_env == 2 || rows >= 16u * 256u);
   const sg_sssp_plan* plan = two_phase ? sssp_plan(ctx, net, h_used, n_used, row_begin, row_end) : nullptr;
-  if (plan && plan->n_other) {
-    const uint32_t* pd = plan->d;
-    const uint32_t ns = plan->n_seed, no = plan->n_other;
-    {
-      TimedLaunch tl(ctx, "sssp", 0.0);
+  if (plan && plan->phases.size() > 1) {
+    for (size_t ph = 0; ph < plan->phases.size(); ph++) {
+      const auto& P = plan->phases[ph];
+      const bool bounded = ph > 0;
+      TimedLaunch tl(ctx, bounded ? "sssp_bounded" : "sssp", 0.0);
       launch_sssp_lds(ctx, net->out_off, net->out_arc, net->n_nodes, net->n_arcs, d_used, n_used, row_begin,
-                      row_end, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work, nullptr,
-                      pd, ns);
-    }
-    {
-      TimedLaunch tl(ctx, "sssp_bounded", 0.0);
-      launch_sssp_lds(ctx, net->out_off, net->out_arc, net->n_nodes, net->n_arcs, d_used, n_used, row_begin,
-                      row_end, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work, diag,
-                      pd + ns, no, pd + ns + no, pd + ns + 2 * (size_t)no);
+                      row_end, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work,
+                      ph + 1 == plan->phases.size() ? diag : nullptr, plan->d + P.rows, P.n,
+                      bounded ? plan->d + P.ub_row : nullptr, bounded ? plan->d + P.ub_w : nullptr);
     }
   } else {
     TimedLaunch tl(ctx, "sssp", 0.0);

@@ -54,6 +54,18 @@
 //     loads in flight (no cross-lane bookkeeping on the dependent chain);
 //     otherwise the wave expands the entries' arcs into consecutive slots
 //     (owner by scatter + max-scan) and relaxes SSSP_K chunks of 64 at once.
+//
+// Bounds (ub_row / ub_w).  For an arc s -> s' whose row D[s'] is already in the
+// table, w(s, s') + D[s'][v] is the latency of a real path from s, so it bounds
+// D[s][v] from above.  A bounded search starts key[v] at (that bound + 1, loss
+// 1.0, clean) instead of infinity: still above the optimum, so the fixed point
+// and the proof above are unchanged, but every candidate slower than the bound
+// loses its first atomic min and is never queued.  sg_routing.hip sssp_plan
+// orders the rows in phases, one launch each, so the bound rows of a phase are
+// final (an earlier launch) before any search reads them.  A one-launch variant
+// with per-row flags (searches reading rows other workgroups had just published)
+// was tried: with an L2 write-back before each flag it matched bit for bit and
+// saved 3 %, without it the table came out wrong, so it was dropped.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -66,10 +78,12 @@ namespace sg {
 constexpr int SSSP_THREADS = 1024;  // the largest workgroup (SG_SSSP_THREADS selects 512 or 1024)
 constexpr int SSSP_WAVES = SSSP_THREADS / 64;
 constexpr int SSSP_K = 4;            // expansion path: chunks of 64 arc slots a wave handles at once
-// lane path: arcs a lane has in flight (template LA: 8 or 16, SG_SSSP_LANE_ARCS);
-// used up to out-degree lane_deg_max (SG_SSSP_LANE_DEG, default 32)
+constexpr int SSSP_KB = SSSP_KB_MAX;  // bound rows per bounded search (sg_routing.hip sssp_plan)
 // static LDS of k_sssp_lds: ctl[8] + red[SSSP_WAVES] (u32), hb (u64), own[SSSP_WAVES][64 * SSSP_K] (u8)
 constexpr size_t SSSP_STATIC_LDS = 4 * (8 + SSSP_WAVES) + 16 + SSSP_WAVES * 64 * SSSP_K;
+// lane path: arcs a lane has in flight (template LA: 8 or 16, SG_SSSP_LANE_ARCS);
+// used up to out-degree lane_deg_max (SG_SSSP_LANE_DEG, default 32)
+
 constexpr size_t LDS_PER_CU = 160 * 1024;
 
 constexpr uint64_t FKEY_INF = ((uint64_t)LAT32_SAT << 32) | ((uint64_t)0x3F800000u << 1);  // (SAT, 1.0), clean
@@ -191,14 +205,27 @@ __global__ void __launch_bounds__(NT)
   if (tid < 8) ctl[tid] = 0;
   if (tid == 0) hb = 0;
   __syncthreads();
-  if (ub_row) {  // Bounds: keys start just above a known path's latency (clean)
-    const uint32_t sr = ub_row[blockIdx.x];
-    if (sr != ~0u) {
-      const uint64_t w = ub_w[blockIdx.x];
-      const uint64_t* srow = out_lat + (size_t)(sr - out_row0) * n_used;
+  if (ub_row) {  // Bounds: keys start just above the shortest of up to SSSP_KB known paths (clean)
+    const uint64_t* srow[SSSP_KB];
+    uint64_t w[SSSP_KB];
+    int nb = 0;
+#pragma unroll
+    for (int k = 0; k < SSSP_KB; k++) {
+      const uint32_t sr = ub_row[(size_t)blockIdx.x * SSSP_KB + k];
+      w[k] = ub_w[(size_t)blockIdx.x * SSSP_KB + k];
+      srow[k] = sr != ~0u ? out_lat + (size_t)(sr - out_row0) * n_used : nullptr;
+      nb += sr != ~0u;
+    }
+    if (nb) {
       for (uint32_t j = tid; j < n_used; j += NT) {
-        const uint64_t ub = srow[j] + w;  // w < 2^32 and srow[j] <= u64::MAX: wrap means >= 2^64
-        if (ub >= w && ub + 1 < LAT32_SAT) key[used[j]] = ((ub + 1) << 32) | ((uint64_t)0x3F800000u << 1);
+        uint64_t m = ~0ull;
+#pragma unroll
+        for (int k = 0; k < SSSP_KB; k++) {
+          if (!srow[k]) continue;
+          const uint64_t ub = srow[k][j] + w[k];  // w < 2^32: a wrap means >= 2^64
+          if (ub >= w[k]) m = min(m, ub);
+        }
+        if (m + 1 < LAT32_SAT) key[used[j]] = ((m + 1) << 32) | ((uint64_t)0x3F800000u << 1);
       }
     }
     __syncthreads();
