@@ -560,7 +560,7 @@ def main():
     # (separately, the counting variant is slower) the relaxations performed
     ctx.enable_timers(True)
     build()
-    timers = {k: ctx.read_timer(k) for k in ("sssp", "relax", "out", "relax_wide")}
+    timers = {k: ctx.read_timer(k) for k in ("sssp", "sssp_bounded", "relax", "out", "relax_wide")}
     ctx.enable_timers(True, count_work=True)
     build()
     works = {k: ctx.read_timer(k)[2] for k in ("sssp", "relax")}
@@ -571,9 +571,12 @@ def main():
     lds = timers["sssp"][1] > 0
     pm = pmc.get("sssp" if lds else "relax", {})
     if lds:
-        # k_sssp_lds, one launch per build: a 12-B arc record gathered from L2 per
-        # relaxation; its HBM traffic is the 12-B (latency, loss) cell per table entry
-        k_ms, k_n, _ = timers["sssp"]
+        # k_sssp_lds: a 12-B arc record gathered from L2 per relaxation; its HBM
+        # traffic is the 12-B (latency, loss) cell per table entry.  A build is one
+        # launch, or three (the bounded phases, timer sssp_bounded): per-launch
+        # figures average over all of them, as rocprof's kernel average does
+        k_ms = timers["sssp"][0] + timers["sssp_bounded"][0]
+        k_n = timers["sssp"][1] + timers["sssp_bounded"][1]
         k_s = k_ms / 1e3 / max(k_n, 1)
         relax_per_launch = works["sssp"] / max(k_n, 1)
         gather_bytes = ARC_BYTES_PER_RELAX * relax_per_launch
@@ -583,6 +586,8 @@ def main():
                     "unit": "GB/s", "frac": round(achieved / L2_PEAK_GBS, 4), "traffic": pm.get("hbm_bytes_per_launch"),
                     "algorithmic_bytes_per_launch": gather_bytes + out_bytes,
                     "avg_launch_ms": round(k_s * 1e3, 4), "launches_per_build": k_n,
+                    "phase_ms": {"unbounded": round(timers["sssp"][0], 4),
+                                 "bounded": round(timers["sssp_bounded"][0], 4)},
                     "relaxations_per_launch": relax_per_launch,
                     "redundancy_vs_dijkstra": round(relax_per_launch * max(k_n, 1) / max(dijkstra_relax, 1.0), 3),
                     "valu_frac_pmc": pm.get("valu_frac"),
@@ -609,10 +614,15 @@ def main():
                                     "frac": round(hbm / HBM_PEAK_GBS, 4)}
     # the batched-source slab kernel on the same rows, for comparison (the default above 10.9k nodes)
     t_slab = None
+    t_unbounded = None
     if lds:
         os.environ["SG_APSP_LDS"] = "0"
         t_slab = timed(D, build, max(1, a.steps // 2), 1)
         os.environ.pop("SG_APSP_LDS")
+        # and the LDS search in one launch with every key from infinity (no bound rows)
+        os.environ["SG_SSSP_SEEDS"] = "0"
+        t_unbounded = timed(D, build, max(1, a.steps // 2), 1)
+        os.environ.pop("SG_SSSP_SEEDS")
 
     # end to end: the whole table into the dense host RoutingInfo (sg_routing_info_fill:
     # row blocks built on the GPU, copied into pinned host memory while the next builds)
@@ -705,6 +715,7 @@ def main():
         "parity_vs_cpu": parity,
         "apsp_detail": {"kernel": roofline["kernel"],
                         "slab_kernel_ms": round(t_slab * 1e3, 4) if t_slab else None,
+                        "unbounded_one_launch_ms": round(t_unbounded * 1e3, 4) if t_unbounded else None,
                         "out_kernel_ms": round(timers["out"][0], 4),
                         "wide_rows_ms": round(timers["relax_wide"][0], 4),
                         "allgather_ms": round(t_allgather * 1e3, 4),
