@@ -859,6 +859,25 @@ def main():
                                         "send_packet semantics + per-destination EventQueue order; source hosts "
                                         f"split over {th} threads as Shadow's workers split hosts"}
             delivery["speedup_vs_cpu"] = round(delivery["value"] / delivery["cpu_baseline"]["value"], 1)
+            # the reference's own per-packet costs on the same round (oracle/sg_faithful.c): SipHash
+            # Dns / IpAssignment / RoutingInfo lookups (a map of every node pair), the global
+            # RwLock'd packet counter, a mutex'd binary heap per destination queue
+            frng, fctr = rng0.copy(), ctr0.copy()
+            fr = O.deliver_faithful(round_end, sim_end, 0, src_global, pk["dst_ip"], pk["payload"], pk["send_time"],
+                                    hosts["ip"], hosts["route"], lat_h, loss_h, frng, fctr, threads=th)
+            fsame = all(np.array_equal(fr[k], wr[k]) for k in ("status", "deliver_time", "event_id", "dst_order",
+                                                               "dst_offsets"))
+            fsame = fsame and np.array_equal(frng, orng) and np.array_equal(fctr, octr)
+            delivery["cpu_baseline_faithful"] = {
+                "value": round(a.packets / fr["round_s"], 1), "unit": "packets/s", "cores": th, "kind": "port",
+                **CPU_INFO, "setup_s": round(fr["setup_s"], 2), "matches_dense_cpu": bool(fsame),
+                "sample": f"the same round of {a.packets} packets through Worker::send_packet on the reference's "
+                          "structures (worker.rs:322-397, :517-607; graph/mod.rs:354-456; dns.rs:176): "
+                          f"{nu}x{nu} node-pair SipHash map, hosts round-robin over {th} threads; setup_s = "
+                          "building the maps (startup in the reference), not in the value"}
+            delivery["speedup_vs_cpu_faithful"] = round(delivery["value"] / delivery["cpu_baseline_faithful"]["value"],
+                                                        1)
+            del fr
         result["delivery"] = delivery
         if not a.no_codel:
             buckets = round_buckets(out, pk["payload"], sharded)

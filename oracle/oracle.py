@@ -75,6 +75,9 @@ def lib():
         L.sgo_deliver_round_mt.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32] + [C.c_void_p] * 4 + [
             C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32] + [C.c_void_p] * 11 + [C.c_int]
         L.sgo_deliver_round_mt.restype = C.c_int64
+        L.sgo_deliver_faithful.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32] + [C.c_void_p] * 4 + [
+            C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32] + [C.c_void_p] * 11 + [C.c_int, C.c_void_p, C.c_void_p]
+        L.sgo_deliver_faithful.restype = C.c_int64
         L.sgo_deliver_round.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u32p, u32p, u32p, u64p,
                                         C.c_uint32, u32p, u32p, C.c_uint32, u64p, f32p, u64p, u64p, u8p, u64p,
                                         u64p, u32p, u32p, u64p, u64p]
@@ -233,6 +236,38 @@ def deliver_round(round_end, sim_end, bootstrap_end, src_host, dst_ip, payload_l
         raise ValueError("sgo_deliver_round: bad argument")
     return dict(status=status, deliver_time=deliver, event_id=eid, dst_order=order[:nd],
                 dst_offsets=offs, min_deliver=mind.value, min_lat=minl.value, delivered=int(nd))
+
+
+def deliver_faithful(round_end, sim_end, bootstrap_end, src_host, dst_ip, payload_len, send_time,
+                     host_ip, host_node, tab_lat, tab_loss, rng, event_ctr, threads: int = 1):
+    """The reference's delivery round cost for cost (sg_faithful.c sgo_deliver_faithful):
+    Worker::send_packet with SipHash Dns / IpAssignment / RoutingInfo lookups, the
+    global RwLock'd packet counter and a mutex'd binary heap per destination queue,
+    hosts round-robin over `threads` workers.  host_node[h] = host h's node, a row and
+    column of the n x n table.  rng / event_ctr are updated in place.  Returns the
+    deliver_round dict plus setup_s (building the maps) and round_s (the round)."""
+    src_host, dst_ip = _arr(src_host, np.uint32), _arr(dst_ip, np.uint32)
+    payload_len, send_time = _arr(payload_len, np.uint32), _arr(send_time, np.uint64)
+    host_ip, host_node = _arr(host_ip, np.uint32), _arr(host_node, np.uint32)
+    tab_lat, tab_loss = _arr(tab_lat, np.uint64), _arr(tab_loss, np.float32)
+    assert rng.dtype == np.uint64 and rng.flags.c_contiguous and event_ctr.dtype == np.uint64
+    n, H = len(src_host), len(host_ip)
+    nn = tab_lat.shape[-1]
+    assert tab_lat.size == nn * nn
+    status, deliver, eid = np.zeros(n, np.uint8), np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+    order, offs = np.zeros(max(n, 1), np.uint32), np.zeros(H + 1, np.uint32)
+    mind, minl, ts, tr = C.c_uint64(), C.c_uint64(), C.c_double(), C.c_double()
+    v = lambda a: a.ctypes.data_as(C.c_void_p)
+    nd = lib().sgo_deliver_faithful(round_end, sim_end, bootstrap_end, n, v(src_host), v(dst_ip), v(payload_len),
+                                    v(send_time), H, v(host_ip), v(host_node), nn, v(tab_lat), v(tab_loss), v(rng),
+                                    v(event_ctr), v(status), v(deliver), v(eid), v(order), v(offs), C.byref(mind),
+                                    C.byref(minl), int(threads), C.byref(ts), C.byref(tr))
+    if nd == -2:
+        raise OverflowError("send time + latency overflows EmulatedTime (emulated_time.rs:121-126 panics)")
+    if nd < 0:
+        raise ValueError("sgo_deliver_faithful: bad argument")
+    return dict(status=status, deliver_time=deliver, event_id=eid, dst_order=order[:nd], dst_offsets=offs,
+                min_deliver=mind.value, min_lat=minl.value, delivered=int(nd), setup_s=ts.value, round_s=tr.value)
 
 
 # ---------------------------------------------------------------------------

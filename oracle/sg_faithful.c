@@ -25,6 +25,8 @@
  * 7 top hash bits, as hashbrown keeps them) and SipHash-1-3 over the key's bytes
  * (u32 writes; std's RandomState keys are random per map, fixed here).
  * Results are identical to sgo_shortest_paths (tests/test_oracle.py).
+ *
+ * sgo_deliver_faithful (below) does the same for the delivery round.
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -414,5 +416,304 @@ int sgo_routing_faithful(uint32_t n, uint32_t m, const uint32_t* esrc, const uin
   free(A.off);
   free(A.dst);
   free(A.edge);
+  return rc;
+}
+
+/* ========================================================================== */
+/* The reference's delivery round, cost for cost                               */
+/* ========================================================================== */
+/*
+ * Worker::send_packet (worker.rs:322-397) on the reference's data structures:
+ *  - Dns::addr_to_host_id (dns.rs:176-178): HashMap<Ipv4Addr, Record> lookup;
+ *  - WorkerShared::reliability and ::latency (worker.rs:517-535): each does two
+ *    IpAssignment::get_node lookups (HashMap<IpAddr, u32>, graph/mod.rs:391-393)
+ *    and a RoutingInfo::path lookup (HashMap<(u32, u32), PathProperties> holding
+ *    every node pair, graph/mod.rs:445-447);
+ *  - increment_packet_count (worker.rs:541-546, graph/mod.rs:449-456): two more
+ *    get_node lookups, then a write lock on one global RwLock<HashMap<(u32, u32),
+ *    u64>> and an entry update;
+ *  - push_packet_to_host (worker.rs:597-607): HashMap<HostId, Arc<Mutex<
+ *    EventQueue>>> lookup, the queue's mutex, a BinaryHeap push (event_queue.rs:
+ *    31-37) ordered as Event (event.rs:84-155: time, then source host, then the
+ *    source's event id).
+ * Worker threads take hosts round-robin (thread_per_core.rs:62-64); a host's
+ * packets run in order on its thread.  The maps are built before the round
+ * (untimed: the reference builds them at startup); the round is timed.  The
+ * per-destination heaps are popped afterwards (untimed) into dst_order /
+ * dst_offsets, so tests compare the whole round with sgo_deliver_round.
+ * Keys are hashed as 4 or 8 bytes (std also hashes an IpAddr's discriminant).
+ */
+double sgo_xoshiro_next_f64(uint64_t s[4]);
+/* statuses as sg_oracle.c SGO_ST_* (PacketStatus outcomes of send_packet) */
+enum { SGO_ST_DELIVERED_F = 0, SGO_ST_DROP_LOSS_F = 1, SGO_ST_NO_DST_F = 2, SGO_ST_SIM_END_F = 3 };
+
+typedef struct {
+  uint64_t time, eid;
+  uint32_t src, pkt;
+} fev;
+static inline int fev_lt(const fev* a, const fev* b) {
+  if (a->time != b->time) return a->time < b->time;
+  if (a->src != b->src) return a->src < b->src;
+  return a->eid < b->eid;
+}
+typedef struct {
+  pthread_mutex_t mu;
+  fev* a;
+  uint32_t n, cap;
+} fqueue;
+static int fqueue_push(fqueue* q, fev e) { /* min-heap (BinaryHeap<Reverse<Event>>) */
+  if (q->n == q->cap) {
+    const uint32_t nc = q->cap ? 2 * q->cap : 8;
+    fev* na = (fev*)realloc(q->a, (size_t)nc * sizeof(fev));
+    if (!na) return -1;
+    q->a = na;
+    q->cap = nc;
+  }
+  uint32_t i = q->n++;
+  while (i) {
+    const uint32_t p = (i - 1) / 2;
+    if (!fev_lt(&e, &q->a[p])) break;
+    q->a[i] = q->a[p];
+    i = p;
+  }
+  q->a[i] = e;
+  return 0;
+}
+static fev fqueue_pop(fqueue* q) {
+  const fev top = q->a[0], last = q->a[--q->n];
+  uint32_t i = 0;
+  for (;;) {
+    uint32_t c = 2 * i + 1;
+    if (c >= q->n) break;
+    if (c + 1 < q->n && fev_lt(&q->a[c + 1], &q->a[c])) c++;
+    if (!fev_lt(&q->a[c], &last)) break;
+    q->a[i] = q->a[c];
+    i = c;
+  }
+  if (q->n) q->a[i] = last;
+  return top;
+}
+
+typedef struct {
+  /* inputs */
+  uint64_t round_end, sim_end, bootstrap_end;
+  const uint32_t *src_host, *dst_ip, *payload_len;
+  const uint64_t* send_time;
+  const uint32_t* host_ip;
+  uint32_t n_hosts;
+  const uint32_t* host_first; /* per host: first packet (n_hosts + 1) */
+  uint64_t *rng, *event_ctr;
+  /* the reference's structures */
+  fmap dns, ipa, paths, queues_idx, counters;
+  pthread_rwlock_t counters_lock;
+  fqueue* queues;
+  /* outputs */
+  uint8_t* status;
+  uint64_t *deliver_time, *event_id;
+  uint32_t T;
+  uint64_t mind[64], minl[64];
+  int64_t delivered[64];
+  int err;
+} fdjob;
+typedef struct {
+  fdjob* J;
+  uint32_t t;
+} fdarg;
+
+static void* fdworker(void* p) {
+  fdarg* A = (fdarg*)p;
+  fdjob* J = A->J;
+  uint64_t mind = UINT64_MAX, minl = UINT64_MAX;
+  int64_t nd = 0;
+  for (uint32_t h = A->t; h < J->n_hosts; h += J->T) /* round-robin hosts */
+    for (uint32_t i = J->host_first[h]; i < J->host_first[h + 1]; i++) {
+      const uint64_t now = J->send_time[i];
+      J->deliver_time[i] = 0;
+      J->event_id[i] = UINT64_MAX;
+      if (now >= J->sim_end) {
+        J->status[i] = SGO_ST_SIM_END_F;
+        continue;
+      }
+      const uint32_t src_ip = J->host_ip[h], dst_ip = J->dst_ip[i];
+      const fslot* dh = fmap_get(&J->dns, dst_ip); /* resolve_ip_to_host_id */
+      if (!dh) {
+        J->status[i] = SGO_ST_NO_DST_F;
+        continue;
+      }
+      const uint32_t d = (uint32_t)dh->val.lat;
+      /* reliability(): two get_node + path */
+      uint64_t sn = fmap_get(&J->ipa, src_ip)->val.lat, dn = fmap_get(&J->ipa, dst_ip)->val.lat;
+      const fslot* pp = fmap_get(&J->paths, (dn << 32) | sn);
+      const double reliability = (double)(1.0f - pp->val.loss);
+      const double chance = sgo_xoshiro_next_f64(&J->rng[4 * (size_t)h]);
+      if (!(now < J->bootstrap_end) && chance >= reliability && J->payload_len[i] > 0) {
+        J->status[i] = SGO_ST_DROP_LOSS_F;
+        continue;
+      }
+      /* latency(): two get_node + path, again */
+      sn = fmap_get(&J->ipa, src_ip)->val.lat;
+      dn = fmap_get(&J->ipa, dst_ip)->val.lat;
+      const uint64_t delay = fmap_get(&J->paths, (dn << 32) | sn)->val.lat;
+      if (delay < minl) minl = delay;
+      /* increment_packet_count(): two get_node + the global write lock */
+      sn = fmap_get(&J->ipa, src_ip)->val.lat;
+      dn = fmap_get(&J->ipa, dst_ip)->val.lat;
+      pthread_rwlock_wrlock(&J->counters_lock);
+      int fresh;
+      fslot* c = fmap_entry(&J->counters, (dn << 32) | sn, &fresh);
+      if (!c) J->err = 1;
+      else c->val.lat = fresh ? 1 : (c->val.lat == UINT64_MAX ? UINT64_MAX : c->val.lat + 1);
+      pthread_rwlock_unlock(&J->counters_lock);
+      uint64_t tt = now + delay;
+      if (tt < now || tt == UINT64_MAX) {
+        J->err = 2;
+        tt = UINT64_MAX - 1;
+      }
+      if (tt < J->round_end) tt = J->round_end;
+      if (tt < mind) mind = tt;
+      J->status[i] = SGO_ST_DELIVERED_F;
+      J->deliver_time[i] = tt;
+      const uint64_t eid = J->event_ctr[h]++;
+      J->event_id[i] = eid;
+      /* push_packet_to_host(): queue lookup, its mutex, the heap push */
+      fqueue* q = &J->queues[fmap_get(&J->queues_idx, d)->val.lat];
+      pthread_mutex_lock(&q->mu);
+      if (fqueue_push(q, (fev){tt, eid, h, i})) J->err = 1;
+      pthread_mutex_unlock(&q->mu);
+      nd++;
+    }
+  J->mind[A->t] = mind;
+  J->minl[A->t] = minl;
+  J->delivered[A->t] = nd;
+  return NULL;
+}
+
+/*
+ * One round over packets grouped by source host.  host_node[h] = the routing
+ * node (table row and column) of host h; the table is n_nodes x n_nodes.
+ * t_setup / t_round: seconds spent building the maps and in the round.  Returns
+ * the delivered count, -1 on bad input or allocation failure, -2 on arrival-time
+ * overflow.
+ */
+int64_t sgo_deliver_faithful(uint64_t round_end, uint64_t sim_end, uint64_t bootstrap_end, uint32_t n_pkts,
+                             const uint32_t* src_host, const uint32_t* dst_ip, const uint32_t* payload_len,
+                             const uint64_t* send_time, uint32_t n_hosts, const uint32_t* host_ip,
+                             const uint32_t* host_node, uint32_t n_nodes, const uint64_t* tab_lat,
+                             const float* tab_loss, uint64_t* rng, uint64_t* event_ctr, uint8_t* status,
+                             uint64_t* deliver_time, uint64_t* event_id, uint32_t* dst_order, uint32_t* dst_offsets,
+                             uint64_t* min_deliver, uint64_t* min_lat, int threads, double* t_setup,
+                             double* t_round) {
+  fdjob* J = (fdjob*)calloc(1, sizeof(fdjob));
+  if (!J) return -1;
+  const double t0 = now_s();
+  J->T = threads < 1 ? 1 : (threads > 64 ? 64 : (uint32_t)threads);
+  J->round_end = round_end;
+  J->sim_end = sim_end;
+  J->bootstrap_end = bootstrap_end;
+  J->src_host = src_host;
+  J->dst_ip = dst_ip;
+  J->payload_len = payload_len;
+  J->send_time = send_time;
+  J->host_ip = host_ip;
+  J->n_hosts = n_hosts;
+  J->rng = rng;
+  J->event_ctr = event_ctr;
+  J->status = status;
+  J->deliver_time = deliver_time;
+  J->event_id = event_id;
+  int64_t rc = 0;
+  uint32_t* first = (uint32_t*)calloc((size_t)n_hosts + 1, 4);
+  J->queues = (fqueue*)calloc(n_hosts ? n_hosts : 1, sizeof(fqueue));
+  if (!first || !J->queues) rc = -1;
+  for (uint32_t i = 0; !rc && i < n_pkts; i++) {
+    if (src_host[i] >= n_hosts || (i && src_host[i] < src_host[i - 1])) rc = -1;
+    else first[src_host[i] + 1]++;
+  }
+  for (uint32_t h = 0; !rc && h < n_hosts; h++) {
+    first[h + 1] += first[h];
+    if (host_node[h] >= n_nodes) rc = -1;
+  }
+  J->host_first = first;
+  /* Dns and IpAssignment: one entry per host */
+  if (!rc && (fmap_init(&J->dns, n_hosts, 4) || fmap_init(&J->ipa, n_hosts, 4) ||
+              fmap_init(&J->queues_idx, n_hosts, 4) || fmap_init(&J->counters, 1024, 8)))
+    rc = -1;
+  for (uint32_t h = 0; !rc && h < n_hosts; h++) {
+    int fresh;
+    fslot* s = fmap_entry(&J->dns, host_ip[h], &fresh);
+    if (!s || !fresh) {
+      rc = -1;
+      break;
+    }
+    s->val.lat = h;
+    s = fmap_entry(&J->ipa, host_ip[h], &fresh);
+    s->val.lat = host_node[h];
+    s = fmap_entry(&J->queues_idx, h, &fresh);
+    s->val.lat = h;
+    pthread_mutex_init(&J->queues[h].mu, NULL);
+  }
+  /* RoutingInfo paths: every node pair */
+  if (!rc && fmap_init(&J->paths, (size_t)n_nodes * n_nodes, 8)) rc = -1;
+  for (uint32_t a = 0; !rc && a < n_nodes; a++)
+    for (uint32_t b = 0; b < n_nodes; b++) {
+      int fresh;
+      fslot* s = fmap_entry(&J->paths, ((uint64_t)b << 32) | a, &fresh);
+      if (!s) {
+        rc = -1;
+        break;
+      }
+      s->val = (fpp){tab_lat[(size_t)a * n_nodes + b], tab_loss[(size_t)a * n_nodes + b]};
+    }
+  pthread_rwlock_init(&J->counters_lock, NULL);
+  const double t1 = now_s();
+  double t2 = t1;
+  if (!rc) {
+    pthread_t th[64];
+    fdarg args[64];
+    for (uint32_t t = 0; t < J->T; t++) {
+      args[t] = (fdarg){J, t};
+      if (pthread_create(&th[t], NULL, fdworker, &args[t])) {
+        fdworker(&args[t]);
+        th[t] = 0;
+      }
+    }
+    for (uint32_t t = 0; t < J->T; t++)
+      if (th[t]) pthread_join(th[t], NULL);
+    t2 = now_s();
+    if (J->err) rc = J->err == 2 ? -2 : -1;
+  }
+  if (!rc) { /* the destinations' queues, popped in order (untimed) */
+    int64_t nd = 0;
+    uint64_t md = UINT64_MAX, ml = UINT64_MAX;
+    for (uint32_t t = 0; t < J->T; t++) {
+      nd += J->delivered[t];
+      if (J->mind[t] < md) md = J->mind[t];
+      if (J->minl[t] < ml) ml = J->minl[t];
+    }
+    uint32_t k = 0;
+    for (uint32_t h = 0; h < n_hosts; h++) {
+      dst_offsets[h] = k;
+      while (J->queues[h].n) dst_order[k++] = fqueue_pop(&J->queues[h]).pkt;
+    }
+    dst_offsets[n_hosts] = k;
+    *min_deliver = md;
+    *min_lat = ml;
+    rc = nd;
+  }
+  if (t_setup) *t_setup = t1 - t0;
+  if (t_round) *t_round = t2 - t1;
+  for (uint32_t h = 0; J->queues && h < n_hosts; h++) {
+    free(J->queues[h].a);
+    pthread_mutex_destroy(&J->queues[h].mu);
+  }
+  free(J->queues);
+  if (J->dns.ctrl) fmap_free(&J->dns);
+  if (J->ipa.ctrl) fmap_free(&J->ipa);
+  if (J->queues_idx.ctrl) fmap_free(&J->queues_idx);
+  if (J->counters.ctrl) fmap_free(&J->counters);
+  if (J->paths.ctrl) fmap_free(&J->paths);
+  pthread_rwlock_destroy(&J->counters_lock);
+  free(first);
+  free(J);
   return rc;
 }

@@ -304,3 +304,36 @@ def test_faithful_routing_build_matches_dense(oracle, directed):
     assert rc2 == 0 and all(t >= 0 for t in ph)
     assert np.array_equal(flat, lat[:150])
     assert np.array_equal(floss.view(np.uint32), loss[:150].view(np.uint32))
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_faithful_delivery_round_matches_dense(oracle, threads):
+    """The reference-cost delivery baseline (sg_faithful.c sgo_deliver_faithful: SipHash
+    Dns / IpAssignment / RoutingInfo maps, the locked packet counter, a mutex'd binary
+    heap per destination, hosts round-robin over threads) delivers the same round as
+    the dense restatement: statuses, times, event ids, queue order, minima, streams."""
+    n_nodes = 60
+    g = synth.ring_chords_graph(n_nodes, 5.0, seed=7)
+    rc, lat, loss, _ = oracle.shortest_paths(n_nodes, g["src"], g["dst"], g["lat"], g["loss"], False,
+                                             np.arange(n_nodes, dtype=np.uint32), threads=4)
+    assert rc == 0
+    loss = loss.copy()
+    loss[::4, ::3] = np.float32(0.3)
+    hosts = synth.make_hosts(2500, n_nodes, general_seed=3, exact_seeds=False)
+    t0 = 946684800 * 10**9
+    pk = synth.make_packets(40000, hosts, t0, t0 + 10**6, seed=threads, p_unknown_dst=0.02)
+    sim_end = t0 + 10**6 - 5000  # a few packets past the end
+    outs = []
+    for fn in (oracle.deliver_round, oracle.deliver_faithful):
+        r = np.stack([oracle.xoshiro_seed(int(s)) for s in hosts["seed"]]).astype(np.uint64)
+        c = np.zeros(len(hosts["seed"]), np.uint64)
+        o = fn(t0 + 10**6, sim_end, t0 + 200_000, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
+               hosts["ip"], hosts["route"], lat, loss, r, c, threads=threads)
+        outs.append((o, r, c))
+    (a, ra, ca), (b, rb, cb) = outs
+    for k in ("status", "deliver_time", "event_id", "dst_order", "dst_offsets"):
+        assert np.array_equal(a[k], b[k]), k
+    assert (a["delivered"], a["min_deliver"], a["min_lat"]) == (b["delivered"], b["min_deliver"], b["min_lat"])
+    assert np.array_equal(ra, rb) and np.array_equal(ca, cb)
+    assert b["setup_s"] > 0 and b["round_s"] > 0
+    assert (a["status"] == 3).any() and (a["status"] == 2).any() and (a["status"] == 1).any()
