@@ -170,6 +170,7 @@ struct sg_net {
   uint32_t* self_edge = nullptr;
   // host copy of the out-arc heads and latencies (for sssp plans), and the plans
   std::vector<uint32_t> h_out_off, h_out_head, h_out_lat;
+  std::vector<uint8_t> h_out_zero_loss;  // arc loss == 0 exactly (bits(1f32 - loss) == 1.0f)
   std::deque<std::unique_ptr<sg_sssp_plan>> plans;
   ~sg_net() {
     void* ps[] = {e_src, e_dst, e_lat, e_loss, in_off, in_src, in_dst, in_lat, in_lat32, in_om, in_rec, out_off,
@@ -271,9 +272,13 @@ struct TimedLaunch {
 // listed there (absolute, within [row_begin, row_end)).  ub_row / ub_w (per
 // workgroup, SSSP_KB_MAX each, optional): rows of out-neighbours s' already in
 // the table (~0u: none) and the arc latencies s -> s'; the search starts every
-// key at min over them of (w + D[s'][v]) + 1 instead of infinity.  The bound
-// rows must be final before the launch (an earlier launch on the stream).
-constexpr int SSSP_KB_MAX = 4;  // bound rows per bounded search (sg_sssp.hip SSSP_KB)
+// key at min over them of (w + D[s'][v]) + 1 instead of infinity.  A bound row
+// whose ub_row entry carries SSSP_UB_EXACT (a zero-loss arc s -> s', every node a
+// used node) also seeds exact keys (w + D[s'][v].lat, D[s'][v].loss); see
+// sg_sssp.hip "Exact seeds".  The bound rows must be final before the launch
+// (an earlier launch on the stream).
+constexpr int SSSP_KB_MAX = 8;
+constexpr uint32_t SSSP_UB_EXACT = 0x80000000u;  // bound rows per bounded search (sg_sssp.hip SSSP_KB)
 bool sssp_lds_fits(uint32_t n_nodes);
 void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_arc, uint32_t n, uint32_t n_arcs,
                      const uint32_t* d_used, uint32_t n_used, uint32_t row_begin, uint32_t row_end,

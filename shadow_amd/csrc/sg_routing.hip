@@ -16,7 +16,9 @@
 // Two kernels compute the same fixed point:
 //  * sg_sssp.hip k_sssp_lds (graphs up to ~10.9k nodes, the default there): one
 //    workgroup per source, the source's whole distance row in LDS, an
-//    asynchronous delta-stepping work queue; about 1.05x Dijkstra's relaxations.
+//    asynchronous work queue, rows bounded (and partly seeded exactly) by
+//    neighbour rows finished in earlier phases; about 1.1-1.6x Dijkstra's
+//    relaxations at C3.
 //  * k_relax_w2 below (larger graphs): batched-source pull relaxation.  A wave
 //    owns a few destination nodes of one 64-source batch; lane = source.  The
 //    batch's distance slab is laid out [node][64 sources], so each in-arc
@@ -1162,9 +1164,11 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 // rows the next phase reads.  Cached per (used list, range, settings).
 static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h_used, uint32_t n_used,
                                      uint32_t row_begin, uint32_t row_end) {
-  const int n_phase = std::max(2, std::min(6, env_int("SG_SSSP_PHASES", 3)));
-  const int kb = std::max(1, std::min(SSSP_KB_MAX, env_int("SG_SSSP_BOUNDS", 1)));
-  const int mode = n_phase * 16 + kb;
+  const int n_phase = std::max(2, std::min(6, env_int("SG_SSSP_PHASES", 4)));
+  const int kb = std::max(1, std::min(SSSP_KB_MAX, env_int("SG_SSSP_BOUNDS", 2)));
+  // exact seeds need a column for every node (see sg_sssp.hip "Exact seeds")
+  const bool exact = env_int("SG_SSSP_EXACT", 1) != 0 && n_used == net->n_nodes;
+  const int mode = (n_phase * 16 + kb) * 2 + exact;
   for (auto& p : net->plans)
     if (p->mode == mode && p->row_begin == row_begin && p->row_end == row_end && p->used.size() == n_used &&
         std::equal(p->used.begin(), p->used.end(), h_used))
@@ -1177,13 +1181,16 @@ static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h
     if (net->n_arcs) copy_to_host(ctx, arc.data(), net->out_arc, arc.size() * 4);
     net->h_out_head.resize(net->n_arcs);
     net->h_out_lat.resize(net->n_arcs);
+    net->h_out_zero_loss.resize(net->n_arcs);
     for (size_t a = 0; a < net->n_arcs; a++) {
       net->h_out_head[a] = arc[3 * a];
       net->h_out_lat[a] = arc[3 * a + 1];
+      net->h_out_zero_loss[a] = arc[3 * a + 2] == 0x3F800000u;  // 1f32 - loss == 1.0
     }
   }
   const uint32_t* off = net->h_out_off.data();
   const uint32_t *head = net->h_out_head.data(), *lat = net->h_out_lat.data();
+  const uint8_t* zl = net->h_out_zero_loss.data();
   const uint32_t rows = row_end - row_begin;
   std::vector<uint32_t> rel(n, ~0u);  // node -> its row in range, relative
   for (uint32_t r = 0; r < rows; r++) rel[h_used[row_begin + r]] = r;
@@ -1244,7 +1251,13 @@ static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h
   p->row_begin = row_begin;
   p->row_end = row_end;
   std::vector<uint32_t> all;
-  std::vector<std::pair<uint32_t, uint32_t>> cand;  // (arc latency, row)
+  // (arc latency, row | SSSP_UB_EXACT unless the arc is zero-loss): zero-loss
+  // arcs (exact seeds) rank first, then by latency
+  std::vector<std::pair<uint32_t, uint32_t>> cand;
+  auto rank = [](const std::pair<uint32_t, uint32_t>& a, const std::pair<uint32_t, uint32_t>& b) {
+    const uint32_t fa = a.second & SSSP_UB_EXACT, fb = b.second & SSSP_UB_EXACT;
+    return fa != fb ? fa < fb : a < b;
+  };
   for (int ph = 0; ph < n_phase; ph++) {
     std::vector<uint32_t> list, ubr, ubw;
     for (uint32_t r = 0; r < rows; r++) {
@@ -1255,15 +1268,16 @@ static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h
       cand.clear();
       for (uint32_t a = off[s]; a < off[s + 1]; a++) {
         const uint32_t q = rel[head[a]];
-        if (q != ~0u && phase[q] < ph) cand.push_back({lat[a], row_begin + q});
+        if (q != ~0u && phase[q] < ph) cand.push_back({lat[a], (row_begin + q) | (exact && zl[a] ? 0u : SSSP_UB_EXACT)});
       }
-      std::sort(cand.begin(), cand.end());
+      std::sort(cand.begin(), cand.end(), rank);
       int k = 0;
-      for (size_t c = 0; c < cand.size() && k < kb; c++) {  // distinct rows (parallel arcs: the lowest)
+      for (size_t c = 0; c < cand.size() && k < kb; c++) {  // distinct rows (parallel arcs: the first ranked)
+        const uint32_t row_c = cand[c].second & ~SSSP_UB_EXACT;
         bool dup = false;
-        for (int i = 0; i < k; i++) dup |= ubr[ubr.size() - k + i] == cand[c].second;
+        for (int i = 0; i < k; i++) dup |= (ubr[ubr.size() - k + i] & ~SSSP_UB_EXACT) == row_c;
         if (dup) continue;
-        ubr.push_back(cand[c].second);
+        ubr.push_back(cand[c].second ^ SSSP_UB_EXACT);  // sorted with the flag inverted: exact first
         ubw.push_back(cand[c].first);
         k++;
       }
@@ -1332,8 +1346,13 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
     std::vector<unsigned long long> h((size_t)n_diag * 8);
     copy_to_host(ctx, h.data(), diag, h.size() * 8);
     double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t r = 0; r < n_diag; r++)
+    double setup = 0;
+    for (uint32_t r = 0; r < n_diag; r++) {
       for (int k = 0; k < 8; k++) a[k] += (double)h[(size_t)r * 8 + k];
+      setup += (double)(h[(size_t)r * 8 + 3] >> 24);
+      a[3] -= (double)(h[(size_t)r * 8 + 3] >> 24 << 24);
+    }
+    fprintf(stderr, "[sssp] mean setup (init + bound rows) %.0f cyc of the search\n", setup / n_diag);
     fprintf(stderr, "[sssp] per-wave cycles summed over a row's 16 waves: claim+wait %.0f, pop %.0f, steps %.0f "
             "(per pop: %.0f, %.0f)\n", a[5] / n_diag, a[6] / n_diag, a[7] / n_diag, a[6] / std::max(1.0, a[2]),
             a[7] / std::max(1.0, a[2]));

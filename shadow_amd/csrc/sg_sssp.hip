@@ -66,6 +66,21 @@
 // with per-row flags (searches reading rows other workgroups had just published)
 // was tried: with an L2 write-back before each flag it matched bit for bit and
 // saved 3 %, without it the table came out wrong, so it was dropped.
+//
+// Exact seeds.  When the arc s -> s' has zero loss (bits(1f32 - loss) == 1.0f),
+// the left fold from s over s -> s' followed by any path P from s' gives exactly
+// P's fold from s' (fold(0, 1.0) = 0, then the same sequence of f32 ops), so
+// (w(s, s') + D[s'][v].lat, D[s'][v].loss) is the exact key of a real path.
+// Such keys start CLEAN (never queued).  Still exact: every key is a real path's
+// value (>= the optimum), and along an optimal path s = v0, .., vk every vi ends
+// at its optimum by induction -- either v(i-1) was popped holding its optimum and
+// relaxed vi, or v(i-1) held its optimum from the start, i.e. an exact seed via
+// some s'; then vi's seed via the same s' is at most w + (D[s'][v(i-1)] (+)
+// w(v(i-1), vi)) = opt(vi), so vi also starts at its optimum.  The induction needs
+// a seed for every node, so the plan sets SSSP_UB_EXACT only when every node is a
+// used node, and a bound row flagged for the wide kernel seeds bounds only.  A
+// node reached optimally through an exactly seeded neighbour row is never
+// popped: its subtree drops out of the search.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -79,10 +94,11 @@ constexpr int SSSP_THREADS = 1024;  // the largest workgroup (SG_SSSP_THREADS se
 constexpr int SSSP_WAVES = SSSP_THREADS / 64;
 constexpr int SSSP_K = 4;            // expansion path: chunks of 64 arc slots a wave handles at once
 constexpr int SSSP_KB = SSSP_KB_MAX;  // bound rows per bounded search (sg_routing.hip sssp_plan)
-// static LDS of k_sssp_lds: ctl[8] + red[SSSP_WAVES] (u32), hb (u64), own[SSSP_WAVES][64 * SSSP_K] (u8)
-constexpr size_t SSSP_STATIC_LDS = 4 * (8 + SSSP_WAVES) + 16 + SSSP_WAVES * 64 * SSSP_K;
+// static LDS of k_sssp_lds: ctl[8] + red[SSSP_WAVES] (u32), hb (u64), own[SSSP_WAVES][64 * SSSP_K] (u8),
+// sink[64] (u64)
+constexpr size_t SSSP_STATIC_LDS = 4 * (8 + SSSP_WAVES) + 16 + SSSP_WAVES * 64 * SSSP_K + 512;
 // lane path: arcs a lane has in flight (template LA: 8 or 16, SG_SSSP_LANE_ARCS);
-// used up to out-degree lane_deg_max (SG_SSSP_LANE_DEG, default 32)
+// used up to out-degree lane_deg_max (SG_SSSP_LANE_DEG, default 16)
 
 constexpr size_t LDS_PER_CU = 160 * 1024;
 
@@ -189,6 +205,7 @@ __global__ void __launch_bounds__(NT)
   __shared__ unsigned long long hb;
   __shared__ uint8_t own[NW][64 * SSSP_K];
   __shared__ uint32_t red[NW];
+  __shared__ unsigned long long sink[64];  // per-lane no-op target of offer_all
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // COUNT diagnostics of the first 4096 rows: cycle stamps, pops, bucket advances, relaxations
@@ -198,38 +215,99 @@ __global__ void __launch_bounds__(NT)
   unsigned long long cyc_claim = 0, cyc_pop = 0, cyc_steps = 0;  // per wave, COUNT diagnostics
   const uint32_t row = blk_rows ? blk_rows[blockIdx.x] : row_begin + blockIdx.x;
   const uint32_t src = used[row];
+  // Setup.  Every global read below is a buffer load whose out-of-range lanes
+  // read 0 without a branch, issued in groups so that a thread has a group's
+  // loads in flight at once (one round trip per group, not per element).
+  constexpr uint32_t OOB = 0x80000000u;
   for (uint32_t v = tid; v < n; v += NT) key[v] = FKEY_INF;
-  for (uint32_t v = tid; v <= n; v += NT) off[v] = out_off[v];
   for (uint32_t i = tid; i < cap; i += NT) ring[i] = RING_EMPTY;
   for (int i = tid; i < NW * 64 * SSSP_K; i += NT) (&own[0][0])[i] = 0;
   if (tid < 8) ctl[tid] = 0;
   if (tid == 0) hb = 0;
+  {  // out_off staged in LDS (n + 1 entries)
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)out_off, 0, (int)((n + 1) * 4u),
+                                                                        0x00020000);
+    constexpr int G = 8;
+    for (uint32_t v0 = tid; v0 <= n; v0 += G * NT) {
+      uint32_t t[G];
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        const uint32_t v = v0 + g * NT;
+        t[g] = __builtin_amdgcn_raw_buffer_load_b32(ro, v <= n ? v * 4u : OOB, 0, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < G; g++)
+        if (v0 + g * NT <= n) off[v0 + g * NT] = t[g];
+    }
+  }
   __syncthreads();
   if (ub_row) {  // Bounds: keys start just above the shortest of up to SSSP_KB known paths (clean)
-    const uint64_t* srow[SSSP_KB];
-    uint64_t w[SSSP_KB];
+    // the listed bound rows, compacted (uniform): latency row, loss row (exact seeds only), own column, arc latency
+    uint32_t brow[SSSP_KB], bw[SSSP_KB];
+    bool bex[SSSP_KB];
     int nb = 0;
 #pragma unroll
     for (int k = 0; k < SSSP_KB; k++) {
-      const uint32_t sr = ub_row[(size_t)blockIdx.x * SSSP_KB + k];
-      w[k] = ub_w[(size_t)blockIdx.x * SSSP_KB + k];
-      srow[k] = sr != ~0u ? out_lat + (size_t)(sr - out_row0) * n_used : nullptr;
-      nb += sr != ~0u;
+      const uint32_t e = ub_row[(size_t)blockIdx.x * SSSP_KB + k];
+      if (e == ~0u) continue;
+      const uint32_t sr = e & ~SSSP_UB_EXACT;
+      brow[nb] = sr;
+      bw[nb] = ub_w[(size_t)blockIdx.x * SSSP_KB + k];
+      // a row flagged for the wide kernel (saturated or given up) may not hold
+      // its optimum everywhere: bounds only
+      bex[nb] = (e & SSSP_UB_EXACT) && !sat_row[sr - row_begin];
+      nb++;
     }
     if (nb) {
-      for (uint32_t j = tid; j < n_used; j += NT) {
-        uint64_t m = ~0ull;
+      const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc((void*)used, 0, (int)(n_used * 4u),
+                                                                          0x00020000);
+      constexpr int G = 4;
+      for (uint32_t j0 = tid; j0 < n_used; j0 += G * NT) {
+        uint32_t vv[G];
+        uint64_t m[G], ex[G];
 #pragma unroll
-        for (int k = 0; k < SSSP_KB; k++) {
-          if (!srow[k]) continue;
-          const uint64_t ub = srow[k][j] + w[k];  // w < 2^32: a wrap means >= 2^64
-          if (ub >= w[k]) m = min(m, ub);
+        for (int g = 0; g < G; g++) {
+          const uint32_t j = j0 + g * NT;
+          vv[g] = __builtin_amdgcn_raw_buffer_load_b32(ru, j < n_used ? j * 4u : OOB, 0, 0);
+          m[g] = ex[g] = ~0ull;
         }
-        if (m + 1 < LAT32_SAT) key[used[j]] = ((m + 1) << 32) | ((uint64_t)0x3F800000u << 1);
+        for (int k = 0; k < nb; k++) {
+          const size_t rb = (size_t)(brow[k] - out_row0) * n_used;
+          const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)(out_lat + rb), 0,
+                                                                              (int)(n_used * 8u), 0x00020000);
+          const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc((void*)(out_loss + rb), 0,
+                                                                              (int)(bex[k] ? n_used * 4u : 0u),
+                                                                              0x00020000);
+          uint64_t l[G];
+          uint32_t f[G];
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            const uint32_t j = j0 + g * NT;
+            const auto x = __builtin_amdgcn_raw_buffer_load_b64(rl, j < n_used ? j * 8u : OOB, 0, 0);
+            l[g] = ((uint64_t)x[1] << 32) | x[0];
+            f[g] = __builtin_amdgcn_raw_buffer_load_b32(rf, j < n_used ? j * 4u : OOB, 0, 0);
+          }
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            const uint32_t j = j0 + g * NT;
+            const uint64_t ub = l[g] + bw[k];  // bw < 2^32: a wrap means >= 2^64
+            if (j >= n_used || ub < bw[k]) continue;
+            m[g] = min(m[g], ub);
+            if (bex[k] && ub < LAT32_SAT && j != brow[k])  // exact: the path s -> s' then D[s'][v]
+              ex[g] = min(ex[g], (ub << 32) | ((uint64_t)f[g] << 1));
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+          uint64_t kv = m[g] + 1 < LAT32_SAT ? ((m[g] + 1) << 32) | ((uint64_t)0x3F800000u << 1) : FKEY_INF;
+          kv = min(kv, ex[g]);
+          if (j0 + g * NT < n_used && kv != FKEY_INF) key[vv[g]] = kv;
+        }
       }
     }
     __syncthreads();
   }
+  const unsigned long long c_setup = dg ? clock64() : 0;
   if (tid == 0) {
     key[src] = 1ull;  // PathProperties::default(), dirty and queued
     ring[0] = (uint16_t)src;
@@ -251,12 +329,26 @@ __global__ void __launch_bounds__(NT)
   uint32_t spins = 0;
   constexpr uint32_t SPIN_MAX = 1u << 22;
   auto ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-  // relax one candidate into key[v]; true when v became dirty below split (to be queued)
-  auto offer = [&](bool valid, uint32_t v, uint64_t cand) -> bool {
-    if (!valid || fkey_lat(cand) == LAT32_SAT) return false;  // saturated keys are never propagated
-    const uint64_t old = __hip_atomic_fetch_min(&key[v], (unsigned long long)cand, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-    return (old >> 1) > (cand >> 1) && !(old & 1ull) && fkey_lat(cand) < split;
+  // relax NK candidates into key[v[c]]; app[c]: v[c] became dirty below split (to
+  // be queued).  Branch-free, so the NK LDS atomics issue back to back and share
+  // one wait: a lane with no candidate (or a saturated one, never propagated)
+  // offers ~0 to its own sink word, a no-op.  (With one branch per candidate the
+  // compiler waited for each atomic's return before issuing the next.)
+  auto offer_all = [&](auto nk, const bool* valid, const uint32_t* v, const uint64_t* cand, bool* app) {
+    constexpr int NK = decltype(nk)::value;
+    uint64_t cd[NK], old[NK];
+#pragma unroll
+    for (int c = 0; c < NK; c++) {
+      const bool ok = valid[c] && fkey_lat(cand[c]) != LAT32_SAT;
+      cd[c] = ok ? cand[c] : ~0ull;
+      old[c] = __hip_atomic_fetch_min(ok ? &key[v[c]] : &sink[lane], (unsigned long long)cd[c], __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // keep the scheduler from pulling a use of old[] between the atomics
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < NK; c++)
+      app[c] = (old[c] >> 1) > (cd[c] >> 1) && !(old[c] & 1ull) && fkey_lat(cd[c]) < split;
   };
   __syncthreads();
 
@@ -366,8 +458,10 @@ __global__ void __launch_bounds__(NT)
           lat[c] = r[1];
           om[c] = r[2];
         }
+        uint64_t cand[LA];
 #pragma unroll
-        for (int c = 0; c < LA; c++) app[c] = offer(valid[c], v[c], frelax(ku, lat[c], __uint_as_float(om[c])));
+        for (int c = 0; c < LA; c++) cand[c] = frelax(ku, lat[c], __uint_as_float(om[c]));
+        offer_all(std::integral_constant<int, LA>(), valid, v, cand, app);
         append_q<LA>(app, v, ring, &ctl[TAIL], slot_of, lane);
       }
     } else {
@@ -403,11 +497,13 @@ __global__ void __launch_bounds__(NT)
           lat[c] = r[1];
           om[c] = r[2];
         }
+        uint64_t cand[SSSP_K];
 #pragma unroll
         for (int c = 0; c < SSSP_K; c++) {
           const uint32_t klo = __shfl((uint32_t)ku, (int)o[c]), khi = __shfl((uint32_t)(ku >> 32), (int)o[c]);
-          app[c] = offer(valid[c], v[c], frelax(((uint64_t)khi << 32) | klo, lat[c], __uint_as_float(om[c])));
+          cand[c] = frelax(((uint64_t)khi << 32) | klo, lat[c], __uint_as_float(om[c]));
         }
+        offer_all(std::integral_constant<int, SSSP_K>(), valid, v, cand, app);
         append_q<SSSP_K>(app, v, ring, &ctl[TAIL], slot_of, lane);
       }
     }
@@ -472,7 +568,7 @@ __global__ void __launch_bounds__(NT)
   if (dg) {
     diag[blockIdx.x * 8 + 0] = c_search - c_start;
     diag[blockIdx.x * 8 + 1] = clock64() - c_search;
-    diag[blockIdx.x * 8 + 3] = n_adv;
+    diag[blockIdx.x * 8 + 3] = n_adv | ((c_setup - c_start) << 24);  // bucket advances | setup cycles
   }
 }
 
@@ -503,7 +599,7 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
   const char* ss = getenv("SG_SSSP_SLEEP");  // idle back-off, units of ~512 cycles
   const uint32_t idle_sleep = ss && *ss ? (uint32_t)std::max(0, atoi(ss)) : 0u;
   const char* ls = getenv("SG_SSSP_LANE_DEG");
-  const uint32_t lane_deg = ls && *ls ? (uint32_t)std::max(0, atoi(ls)) : 32u;
+  const uint32_t lane_deg = ls && *ls ? (uint32_t)std::max(0, atoi(ls)) : 16u;
   const char* la = getenv("SG_SSSP_LANE_ARCS");
   const int la16 = la && atoi(la) == 16;
   auto go = [&](auto kern) {

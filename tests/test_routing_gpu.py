@@ -125,6 +125,32 @@ def test_heavy_loss_ties(oracle, ctx):
     _check(oracle, g, np.arange(400, dtype=np.uint32), ctx)
 
 
+@pytest.mark.parametrize("directed", [False, True])
+@pytest.mark.parametrize("bounds", ["1", "4"])
+def test_exact_seeds_with_ties(oracle, ctx, monkeypatch, directed, bounds):
+    """Bound rows reached over zero-loss arcs seed exact keys (sg_sssp.hip "Exact seeds"): many
+    equal-latency paths, lossy arcs beside zero-loss ones, every node used so the seeds apply."""
+    monkeypatch.setenv("SG_SSSP_BOUNDS", bounds)
+    g = synth.ring_chords_graph(600, 8.0, seed=21, directed=directed)
+    rng = np.random.default_rng(21)
+    g["lat"] = (rng.integers(1, 5, len(g["lat"])) * 1000).astype(np.uint64)
+    loss = rng.uniform(0, 0.3, len(g["lat"])).astype(np.float32)
+    loss[rng.random(len(loss)) < 0.6] = 0
+    g["loss"] = loss
+    _check(oracle, g, np.arange(600, dtype=np.uint32), ctx)
+
+
+def test_exact_seeds_next_to_wide_rows(oracle, ctx, monkeypatch):
+    """Rows past 2^32 ns go to the wide kernel after the phases; a later row bounded by such a row
+    must take bounds only from it (its 32-bit row is not final everywhere)."""
+    monkeypatch.setenv("SG_SSSP_BOUNDS", "4")
+    g = synth.ring_chords_graph(300, 6.0, seed=22, directed=True)
+    far = np.isin(g["src"], np.arange(0, 300, 23))  # every out-arc of 13 nodes is 5 s long
+    g["lat"][far] = np.uint64(5_000_000_000)
+    lat, _ = _check(oracle, g, np.arange(300, dtype=np.uint32), ctx)
+    assert lat.max() >= (1 << 32) and np.median(lat) < (1 << 32)
+
+
 def test_wide_fallback_big_latencies(oracle, ctx):
     """Path latencies beyond 2^32 ns take the u64 kernel; must still be exact."""
     g = synth.ring_chords_graph(150, 4.0, seed=8, lat_lo_us=2_000_000, lat_hi_us=9_000_000)
