@@ -794,8 +794,8 @@ def main():
             t_pcie = timed(D, rnd_pcie, max(3, a.steps // 4), 1)
         ctx.enable_timers(True)
         rnd()
-        kt = {k: ctx.read_timer(k) for k in ("seg_bounds", "walk", "scan", "scatter", "sort_small", "sort_big",
-                                             "pack", "rec_count", "rec_scatter")}
+        kt = {k: ctx.read_timer(k) for k in ("seg_bounds", "walk", "scan", "scatter", "scatter2", "sort_small",
+                                             "sort_big", "pack", "rec_count", "rec_scatter")}
         ctx.enable_timers(False)
         walk_ms, walk_n, walk_bytes = kt["walk"]
         walk_s = walk_ms / 1e3 / max(walk_n, 1)

@@ -196,8 +196,8 @@ int32_t sg_ctx_create(int32_t device, sg_ctx** out) {
     SG_HIP(hipMemset(ctx->round_err, 0, 16));
     SG_HIP(hipHostMalloc(&ctx->round_ret, sizeof(sg_round_ret), hipHostMallocMapped | hipHostMallocCoherent));
     SG_HIP(hipHostMalloc(&ctx->apsp_ret, 16, hipHostMallocMapped | hipHostMallocCoherent));
-    SG_HIP(hipMalloc(&ctx->sb_ctl, 2 * sg::SB_CTL_STRIDE * 4));
-    SG_HIP(hipMemset(ctx->sb_ctl, 0, 2 * sg::SB_CTL_STRIDE * 4));
+    SG_HIP(hipMalloc(&ctx->sb_ctl, 4 * sg::SB_CTL_STRIDE * 4));
+    SG_HIP(hipMemset(ctx->sb_ctl, 0, 4 * sg::SB_CTL_STRIDE * 4));
     int cus = 0;
     SG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     ctx->n_cu = cus;

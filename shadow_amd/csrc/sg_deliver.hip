@@ -220,13 +220,30 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
       sh[q] = a.src[i];
       f[q] = a.payload[i] > 0 ? W_PAYLOAD : 0;
     }
+    // Loads below are branch-free where the map is a dense window (the usual
+    // case; a uniform branch): a lane with nothing to read reads entry 0 and
+    // drops it.  Under per-lane branches the compiler waited for each load
+    // before issuing the next one, so the PPT packets' round trips ran in turn.
+    if (a.map.dense) {
 #pragma unroll
-    for (int q = 0; q < PPT; q++) {
-      if (now[q] < a.bootstrap_end) f[q] |= W_BOOT;
-      const uint2 hr = now[q] < a.sim_end ? a.map.resolve(ip[q]) : make_uint2(NONE, 0);  // worker.rs:332-335, 341
-      d[q] = hr.x;
-      ip[q] = hr.y;  // reuse: the destination's route column
-      r[q] = a.route[min(sh[q], a.H - 1)];  // sh < H in an accepted batch
+      for (int q = 0; q < PPT; q++) {
+        if (now[q] < a.bootstrap_end) f[q] |= W_BOOT;
+        const uint32_t off = ip[q] - a.map.ip_base;
+        const bool ok = now[q] < a.sim_end && off < a.map.dense_span;  // worker.rs:332-335, 341
+        const uint2 v = a.map.dense[ok ? off : 0];
+        d[q] = ok ? v.x : NONE;
+        ip[q] = ok ? v.y : 0;  // reuse: the destination's route column
+        r[q] = a.route[min(sh[q], a.H - 1)];  // sh < H in an accepted batch
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < PPT; q++) {
+        if (now[q] < a.bootstrap_end) f[q] |= W_BOOT;
+        const uint2 hr = now[q] < a.sim_end ? a.map.resolve(ip[q]) : make_uint2(NONE, 0);  // worker.rs:332-335, 341
+        d[q] = hr.x;
+        ip[q] = hr.y;  // reuse: the destination's route column
+        r[q] = a.route[min(sh[q], a.H - 1)];  // sh < H in an accepted batch
+      }
     }
 #pragma unroll
     for (int q = 0; q < PPT; q++) {
@@ -243,16 +260,17 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
       const uint32_t i = c0 + t + q * WALK_THREADS;
       uint64_t lat = 0;  // PACKED: the whole cell
       float loss = 0.0f;
-      if (d[q] != NONE) {
-        const size_t cell = (size_t)(r[q] - a.row_begin) * a.n_cols + ip[q];
+      const bool ok = d[q] != NONE;  // then the table has cells (a destination needs its route column)
+      const size_t cell = ok ? (size_t)(r[q] - a.row_begin) * a.n_cols + ip[q] : 0;
+      if (a.n_cols && a.n_rows) {  // uniform; branch-free gathers (cell 0 for the lanes that drop them)
         if (PACKED) {
           lat = a.tab_key[cell];  // one 8-byte gather
         } else {
           lat = a.tab_lat[cell];
           loss = a.tab_loss[cell];
         }
-        f[q] |= W_DRAW;
       }
+      if (ok) f[q] |= W_DRAW;
       if (i < c1) {
         const uint32_t k = i - c0;
         s_t[k] = now[q];
@@ -594,6 +612,7 @@ constexpr int SBT_THREADS = 512;     // k_sb_sort block
 
 struct PacketEntries {  // single GPU: entries are the round's packets, kk = ki = packet index
   static constexpr bool KK = false;  // the order key is the value itself
+  static constexpr bool COARSE = false;
   const uint32_t* dst;
   const uint64_t* t;
   __device__ __forceinline__ uint32_t slot(uint32_t e) const { return dst[e]; }
@@ -606,6 +625,7 @@ struct PacketEntries {  // single GPU: entries are the round's packets, kk = ki 
 
 struct RecordEntries {  // sharded: entries are received records, slot = the destination's local index
   static constexpr bool KK = true;
+  static constexpr bool COARSE = false;
   const sg_record* rec;
   const uint32_t* local;
   uint32_t H;
@@ -620,6 +640,37 @@ struct RecordEntries {  // sharded: entries are received records, slot = the des
     tt = rec[e].deliver_time_ns;
     kk = rec[e].order_key;
     ki = e;
+  }
+};
+
+// Second level of a two-level scatter: the entries are the coarse level's runs,
+// region `region` per coarse bucket, split into SB_SUB sub-regions whose fill
+// counts are in ctl (k_sb_scatter<.., true> with a coarse SbMap).  Entries past
+// a sub-region's fill are holes (slot NONE).  ctl_next: the other coarse parity,
+// cleared by this level for the next two-level call.
+template <bool KK_>
+struct CoarseEntries {
+  static constexpr bool KK = KK_;
+  static constexpr bool COARSE = true;
+  const uint32_t* rd;
+  const uint64_t* rt;
+  const uint64_t* rk;
+  const uint32_t* ri;
+  const uint32_t* ctl;
+  uint32_t* ctl_next;
+  uint32_t region, subcap, cpb;  // coarse region, its sub-regions, super-buckets per coarse bucket
+  __device__ __forceinline__ uint32_t fill_of(uint32_t e, uint32_t& off, uint32_t& sub) const {
+    const uint32_t c = e / region, r = e - c * region;
+    sub = r / subcap;
+    off = r - sub * subcap;
+    return ctl[sub * SB_MAX + c];
+  }
+  // the kernel stops each tile at its sub-region's fill (fill_of), so every entry asked for is a real one
+  __device__ __forceinline__ uint32_t slot(uint32_t e) const { return rd[e]; }
+  __device__ __forceinline__ void get(uint32_t e, uint64_t& tt, uint64_t& kk, uint32_t& ki) const {
+    tt = rt[e];
+    ki = ri[e];
+    kk = KK ? rk[e] : (uint64_t)ki;
   }
 };
 
@@ -694,6 +745,36 @@ __global__ void __launch_bounds__(SBS_THREADS)
     reduce_stats_block<SBS_THREADS>(stats);
     return;
   }
+  if constexpr (E::COARSE) {
+    for (uint32_t i = blockIdx.x * SBS_THREADS + threadIdx.x; i < SB_CTL_STRIDE; i += gridDim.x * SBS_THREADS)
+      src.ctl_next[i] = 0;
+    if (src.ctl[SB_FLAG]) {  // the coarse level overflowed: so does this one (the host reruns the scan path)
+      if (blockIdx.x == 0 && threadIdx.x == 0) ctl[SB_FLAG] = 1u;
+      return;
+    }
+  }
+  uint32_t e_lim = n;  // second level: the tile's sub-region holds `fill` entries from its start
+  if constexpr (E::COARSE) {
+    uint32_t off, sub;  // a tile lies in one sub-region (subcap is a multiple of SB_TILE): skip an empty one
+    const uint32_t fill = src.fill_of(blockIdx.x * SB_TILE, off, sub);
+    if (off >= fill) return;
+    e_lim = blockIdx.x * SB_TILE + (fill - off);
+  }
+  // Sub-region of the runs this tile claims.  One level: the tile's XCD (tiles
+  // are uniform samples, so each sub-region gets an eighth).  Second level: the
+  // coarse sub-region the tile reads, which holds an eighth of its coarse bucket
+  // (tile indices would not: a coarse sub-region's full tiles and its partial
+  // last tile alternate in parity).
+  uint32_t run_sub = blockIdx.x & (SB_SUB - 1);
+  // Second level: the tile's entries all lie in one coarse bucket, i.e. in its
+  // cpb super-buckets [sb_lo, sb_lo + nsb); local counters cover just those.
+  uint32_t sb_lo = 0, nsb = n_sb;
+  if constexpr (E::COARSE) {
+    uint32_t off;
+    src.fill_of(blockIdx.x * SB_TILE, off, run_sub);
+    sb_lo = blockIdx.x * SB_TILE / src.region * src.cpb;
+    nsb = min(src.cpb, n_sb - sb_lo);
+  }
   constexpr int PER = SB_TILE / SBS_THREADS;
   __shared__ uint32_t lcur[SB_MAX];   // local start, then cursor
   __shared__ uint32_t lbase[SB_MAX];  // global position of the run - local start
@@ -702,38 +783,39 @@ __global__ void __launch_bounds__(SBS_THREADS)
   __shared__ uint32_t si[SB_TILE];
   __shared__ uint64_t sk[E::KK ? SB_TILE : 1];
   __shared__ uint32_t wsum[SBS_THREADS / 64];
-  for (uint32_t i = threadIdx.x; i < n_sb; i += SBS_THREADS) lcur[i] = 0;
+  for (uint32_t i = threadIdx.x; i < nsb; i += SBS_THREADS) lcur[i] = 0;
   __syncthreads();
-  const uint32_t e0 = blockIdx.x * SB_TILE, e1 = min(e0 + SB_TILE, n);
-  // every load of the tile up front (one round trip): slot, time, key, value
+  const uint32_t e0 = blockIdx.x * SB_TILE, e1 = min(min(e0 + SB_TILE, n), e_lim);
+  // every load of the tile up front (one round trip): slot, time, key, value.
+  // Branch-free: a lane past the tile's end reads entry e0 again and drops it
+  // (conditional loads would each be waited for before the next one issues).
   uint32_t d[PER], vi[PER];
   uint64_t vt[PER], vk[PER];
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t e = e0 + threadIdx.x + k * SBS_THREADS;
-    d[k] = NONE;
-    if (e < e1) {
-      d[k] = src.slot(e);
-      src.get(e, vt[k], vk[k], vi[k]);
-    }
+    const uint32_t ee = e < e1 ? e : e0;
+    const uint32_t dd = src.slot(ee);
+    src.get(ee, vt[k], vk[k], vi[k]);
+    d[k] = e < e1 ? dd : NONE;
   }
 #pragma unroll
   for (int k = 0; k < PER; k++)
-    if (d[k] != NONE) atomicAdd(&lcur[sm.of(d[k])], 1u);
+    if (d[k] != NONE) atomicAdd(&lcur[sm.of(d[k]) - sb_lo], 1u);
   __syncthreads();
-  const uint32_t total = block_exclusive_scan<SBS_THREADS, SB_MAX / SBS_THREADS>(lcur, n_sb, wsum);
-  for (uint32_t i = threadIdx.x; i < n_sb; i += SBS_THREADS) {
+  const uint32_t total = block_exclusive_scan<SBS_THREADS, SB_MAX / SBS_THREADS>(lcur, nsb, wsum);
+  for (uint32_t i = threadIdx.x; i < nsb; i += SBS_THREADS) {
     if (REGION) {
       // the run of super-bucket i: local [lcur[i], lcur[i] + c) -> sub-region slot g..g+c.
       // A kept base is i * region + sub * subcap + g - lcur[i] >= 0 (i = 0: lcur[0] = 0;
       // i > 0: lcur[i] <= SB_TILE <= region), never RUN_DROPPED.
-      const uint32_t c = (i + 1 < n_sb ? lcur[i + 1] : total) - lcur[i];
-      const uint32_t sub = blockIdx.x & (SB_SUB - 1), subcap = region / SB_SUB;
+      const uint32_t c = (i + 1 < nsb ? lcur[i + 1] : total) - lcur[i];
+      const uint32_t sub = run_sub, subcap = region / SB_SUB;
       uint32_t base = RUN_DROPPED;
       if (c) {
-        const uint32_t g = atomicAdd(&ctl[sub * SB_MAX + i], c);
+        const uint32_t g = atomicAdd(&ctl[sub * SB_MAX + sb_lo + i], c);
         if (g + c <= subcap)
-          base = i * region + sub * subcap + g - lcur[i];
+          base = (sb_lo + i) * region + sub * subcap + g - lcur[i];
         else
           ctl[SB_FLAG] = 1u;
       }
@@ -746,7 +828,7 @@ __global__ void __launch_bounds__(SBS_THREADS)
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     if (d[k] == NONE) continue;
-    const uint32_t p = atomicAdd(&lcur[sm.of(d[k])], 1u);
+    const uint32_t p = atomicAdd(&lcur[sm.of(d[k]) - sb_lo], 1u);
     sd[p] = d[k];
     st_[p] = vt[k];
     si[p] = vi[k];
@@ -755,7 +837,7 @@ __global__ void __launch_bounds__(SBS_THREADS)
   __syncthreads();
   for (uint32_t p = threadIdx.x; p < total; p += SBS_THREADS) {
     const uint32_t dd = sd[p];
-    const uint32_t lb = lbase[sm.of(dd)];
+    const uint32_t lb = lbase[sm.of(dd) - sb_lo];
     if (REGION && lb == RUN_DROPPED) continue;
     const uint32_t g = lb + p;
     rd[g] = dd;
@@ -807,7 +889,9 @@ __device__ __forceinline__ void slot_bitonic(const uint64_t* Tt, const uint64_t*
 // SMALL_BUCKET go to k_sort_big (copied to the global kt/kk/ki when placed in
 // LDS) or, INBLOCK (LDS only), are bitonic-sorted by this block -- the region
 // path, where a super-bucket always fits LDS and no k_sort_big launch is needed.
-template <bool LDS, bool KK, bool INBLOCK>
+// CK: Tt holds compressed keys ((t - t_min) << 32 | value), unique per entry, so
+// one u64 compare is the (t, kk) order (k_sb_sort_region; single GPU).
+template <bool LDS, bool KK, bool INBLOCK, bool CK = false>
 __device__ __forceinline__ void slot_orders(uint64_t* Tt, uint64_t* Tk, uint32_t* Ti, uint16_t* Ts, uint32_t s0,
                                             uint32_t ns, uint32_t d0, uint32_t nd, const uint32_t* cnt,
                                             uint64_t* __restrict__ kt, uint64_t* __restrict__ kk,
@@ -849,7 +933,32 @@ __device__ __forceinline__ void slot_orders(uint64_t* Tt, uint64_t* Tk, uint32_t
     if (e - b > SMALL) continue;  // sorted below / by k_sort_big
     const uint64_t t = Tt[p], k = KK ? Tk[p] : (uint64_t)Ti[p];
     uint32_t rank = 0;
-    for (uint32_t q = b; q < e; q++) rank += key_less(Tt[q], KK ? Tk[q] : (uint64_t)Ti[q], t, k);
+    // 8 entries per step, their LDS reads issued together (one at a time, the
+    // loop waited out each read's latency: C5's ~100-entry slots spent most of
+    // the sort there)
+    uint32_t q = b;
+    if constexpr (CK) {  // one compare per entry: the rank sort was VALU-bound on the two-word key_less
+      for (; q + 8 <= e; q += 8) {
+        uint64_t tq[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) tq[u] = Tt[q + u];
+#pragma unroll
+        for (int u = 0; u < 8; u++) rank += tq[u] < t;
+      }
+      for (; q < e; q++) rank += Tt[q] < t;
+    } else {
+      for (; q + 8 <= e; q += 8) {
+        uint64_t tq[8], kq[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          tq[u] = Tt[q + u];
+          kq[u] = KK ? Tk[q + u] : (uint64_t)Ti[q + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) rank += key_less(tq[u], kq[u], t, k);
+      }
+      for (; q < e; q++) rank += key_less(Tt[q], KK ? Tk[q] : (uint64_t)Ti[q], t, k);
+    }
     order[s0 + b + rank] = Ti[p];
   }
   if (INBLOCK) {
@@ -943,6 +1052,24 @@ __global__ void __launch_bounds__(SBT_THREADS)
                    slot_spill);
 }
 
+// Output start of every super-bucket of the region path (the exclusive scan of
+// its SB_SUB sub-counts), one block, for many super-buckets; with few, each
+// sort block sums the counts before it itself.
+__global__ void __launch_bounds__(1024) k_sb_prefix(const uint32_t* __restrict__ ctl, uint32_t n_sb,
+                                                    uint32_t* __restrict__ pre) {
+  __shared__ uint32_t a[SB_MAX];
+  __shared__ uint32_t wsum[1024 / 64];
+  for (uint32_t i = threadIdx.x; i < n_sb; i += 1024) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < (int)SB_SUB; k++) t += ctl[k * SB_MAX + i];
+    a[i] = t;
+  }
+  __syncthreads();
+  block_exclusive_scan<1024, SB_MAX / 1024>(a, n_sb, wsum);
+  for (uint32_t i = threadIdx.x; i < n_sb; i += 1024) pre[i] = a[i];
+}
+
 // Region path: super-bucket sb's entries are SB_SUB runs, sub-region k holding
 // [sb * region + k * subcap, + count[k][sb]) (k_sb_scatter<E, true>); its output
 // position is the sum of all counts of the super-buckets before it.  The block
@@ -956,7 +1083,8 @@ __global__ void __launch_bounds__(SBT_THREADS)
                      const uint32_t* __restrict__ ri, uint64_t* __restrict__ kt, uint64_t* __restrict__ kk,
                      uint32_t* __restrict__ ki, uint32_t* __restrict__ offsets, uint32_t* __restrict__ order,
                      uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count,
-                     uint16_t* __restrict__ slot_spill, sg_round_ret* __restrict__ ret) {
+                     uint16_t* __restrict__ slot_spill, sg_round_ret* __restrict__ ret,
+                     const uint32_t* __restrict__ pre) {
   __shared__ uint32_t part[SBT_THREADS / 64];
   for (uint32_t i = blockIdx.x * SBT_THREADS + threadIdx.x; i <= SB_FLAG; i += gridDim.x * SBT_THREADS)
     ctl_next[i] = 0;
@@ -964,15 +1092,19 @@ __global__ void __launch_bounds__(SBT_THREADS)
   if (blockIdx.x == 0 && threadIdx.x == 0) ret->overflow = over;
   if (over) return;  // uniform across the grid
   const uint32_t sb = blockIdx.x, subcap = region / SB_SUB;
-  uint32_t before = 0;
-  for (uint32_t i = threadIdx.x; i < sb; i += SBT_THREADS)  // coalesced per sub-counter array
-#pragma unroll
-    for (int k = 0; k < (int)SB_SUB; k++) before += ctl[k * SB_MAX + i];
-  for (int dd = 32; dd > 0; dd >>= 1) before += __shfl_xor(before, dd, 64);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = before;
-  __syncthreads();
   uint32_t s0 = 0;
-  for (int w = 0; w < SBT_THREADS / 64; w++) s0 += part[w];
+  if (pre) {
+    s0 = pre[sb];
+  } else {
+    uint32_t before = 0;
+    for (uint32_t i = threadIdx.x; i < sb; i += SBT_THREADS)  // coalesced per sub-counter array
+#pragma unroll
+      for (int k = 0; k < (int)SB_SUB; k++) before += ctl[k * SB_MAX + i];
+    for (int dd = 32; dd > 0; dd >>= 1) before += __shfl_xor(before, dd, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = before;
+    __syncthreads();
+    for (int w = 0; w < SBT_THREADS / 64; w++) s0 += part[w];
+  }
   uint32_t sub_end[SB_SUB];  // running totals of the SB_SUB runs (wave-uniform)
   uint32_t ns = 0;
 #pragma unroll
@@ -997,21 +1129,51 @@ __global__ void __launch_bounds__(SBT_THREADS)
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t e = threadIdx.x + k * SBT_THREADS;
-    vd[k] = NONE;
-    if (e < ns) {
-      uint32_t sub = 0, start = 0;  // entry e lies in the first run whose running total exceeds it
+    uint32_t sub = 0, start = 0;  // entry e lies in the first run whose running total exceeds it
 #pragma unroll
-      for (int j = 0; j < (int)SB_SUB - 1; j++)
-        if (e >= sub_end[j]) {
-          sub = j + 1;
-          start = sub_end[j];
-        }
-      const uint32_t x = in0 + sub * subcap + (e - start);
-      vd[k] = rd[x] - d0;
-      vt[k] = rt[x];
-      vi[k] = ri[x];
-      if (KK) vk[k] = rk[x];
+    for (int j = 0; j < (int)SB_SUB - 1; j++)
+      if (e >= sub_end[j]) {
+        sub = j + 1;
+        start = sub_end[j];
+      }
+    // branch-free loads (a lane past the end reads the region's first slot and drops it)
+    const uint32_t x = e < ns ? in0 + sub * subcap + (e - start) : in0;
+    const uint32_t dd = rd[x];
+    vt[k] = rt[x];
+    vi[k] = ri[x];
+    if (KK) vk[k] = rk[x];
+    vd[k] = e < ns ? dd - d0 : NONE;
+  }
+  // Compressed keys (single GPU: the order key is the value, a u32): when the
+  // super-bucket's arrival times span less than 2^32 ns, (t - t_min) << 32 | value
+  // is unique and orders like (t, value), and the rank sort compares one word.
+  bool ck = false;
+  if constexpr (!KK) {
+    __shared__ unsigned long long tlo[SBT_THREADS / 64], thi[SBT_THREADS / 64];
+    uint64_t lo = ~0ull, hi = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++)
+      if (vd[k] != NONE) {
+        lo = min(lo, vt[k]);
+        hi = max(hi, vt[k]);
+      }
+    for (int dd = 32; dd > 0; dd >>= 1) {
+      lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, dd, 64));
+      hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, dd, 64));
     }
+    if ((threadIdx.x & 63) == 0) {
+      tlo[threadIdx.x >> 6] = lo;
+      thi[threadIdx.x >> 6] = hi;
+    }
+    __syncthreads();
+    for (int w = 0; w < SBT_THREADS / 64; w++) {
+      lo = min(lo, (uint64_t)tlo[w]);
+      hi = max(hi, (uint64_t)thi[w]);
+    }
+    ck = ns > 0 && hi - lo < (1ull << 32);
+    if (ck)
+#pragma unroll
+      for (int k = 0; k < PER; k++) vt[k] = ((vt[k] - lo) << 32) | vi[k];
   }
   for (uint32_t j = threadIdx.x; j <= nd; j += SBT_THREADS) cnt[j] = 0;
   __syncthreads();
@@ -1034,7 +1196,10 @@ __global__ void __launch_bounds__(SBT_THREADS)
     si[p] = vi[k];
     ss[p] = (uint16_t)vd[k];
   }
-  slot_orders<true, KK, true>(st, sk, si, ss, s0, ns, d0, nd, cnt, kt, kk, ki, order, big_list, big_count);
+  if (ck)  // uniform per block
+    slot_orders<true, KK, true, true>(st, sk, si, ss, s0, ns, d0, nd, cnt, kt, kk, ki, order, big_list, big_count);
+  else
+    slot_orders<true, KK, true>(st, sk, si, ss, s0, ns, d0, nd, cnt, kt, kk, ki, order, big_list, big_count);
 }
 
 // Bucket sort of n entries into n_slots destination slots (see above).
@@ -1083,16 +1248,55 @@ static bool bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
     uint32_t* ctl = ctx->sb_ctl + (size_t)ctx->sb_parity * SB_CTL_STRIDE;
     uint32_t* ctl_next = ctx->sb_ctl + (size_t)(ctx->sb_parity ^ 1) * SB_CTL_STRIDE;
     ctx->sb_parity ^= 1;
-    {
+    // Two levels when a tile would spread over so many super-buckets that its
+    // runs are a few entries long (C5: 10M entries, 3,847 super-buckets, about
+    // one entry per super-bucket per tile -- every store scattered, one global
+    // atomic per entry).  The first level scatters into at most 256 coarse
+    // buckets of cpb consecutive super-buckets (runs of 16+ entries), the second
+    // level scatters each coarse bucket's tiles into its cpb super-buckets.
+    const char* tl_env = getenv("SG_BUCKET_TWO_LEVEL");  // 0 never, 1 always (tests), else when runs are short
+    const int two_env = tl_env && *tl_env ? atoi(tl_env) : -1;
+    const bool two = two_env == 1 || (two_env != 0 && n_sb > 512);
+    if (two) {
+      const uint32_t cpb = std::max<uint32_t>(2, (n_sb + 255) / 256), n_cb = (n_sb + cpb - 1) / cpb;
+      SbMap cm{((1ull << 40) + (uint64_t)spb64 * cpb - 1) / ((uint64_t)spb64 * cpb), (uint32_t)(spb64 * cpb)};
+      // per (coarse bucket, XCD) sub-region: 1.25x its mean share + 1024, in whole tiles
+      const uint64_t mean = ((uint64_t)n + (uint64_t)n_cb * SB_SUB - 1) / ((uint64_t)n_cb * SB_SUB);
+      const uint64_t subcap = (mean + mean / 4 + 1024 + SB_TILE - 1) / SB_TILE * SB_TILE;
+      const uint64_t creg = subcap * SB_SUB, ctot = creg * n_cb;
+      if (ctot >= (1ull << 31)) throw Error(SG_ERR_INVALID_ARG, "round too large for the bucketing workspace");
+      uint32_t* cctl = ctx->sb_ctl + (size_t)(2 + ctx->sb_parity_c) * SB_CTL_STRIDE;
+      uint32_t* cctl_next = ctx->sb_ctl + (size_t)(2 + (ctx->sb_parity_c ^ 1)) * SB_CTL_STRIDE;
+      ctx->sb_parity_c ^= 1;
+      uint32_t* cd = ctx->d_cd.get<uint32_t>(ctot);
+      uint64_t* ct = ctx->d_ct.get<uint64_t>(ctot);
+      uint64_t* ck = ctx->d_ck.get<uint64_t>(E::KK ? ctot : 1);
+      uint32_t* ci = ctx->d_ci.get<uint32_t>(ctot);
+      {
+        TimedLaunch tl(ctx, "scatter", 32.0 * n);
+        hipLaunchKernelGGL((k_sb_scatter<E, true>), dim3(n_tiles + (stats.blk ? 1 : 0)), dim3(SBS_THREADS), 0, st,
+                           src, n, cm, n_cb, nullptr, cctl, (uint32_t)creg, cd, ct, ck, ci, stats);
+      }
+      CoarseEntries<E::KK> ce{cd, ct, ck, ci, cctl, cctl_next, (uint32_t)creg, (uint32_t)subcap, cpb};
+      {
+        TimedLaunch tl(ctx, "scatter2", 32.0 * n);
+        hipLaunchKernelGGL((k_sb_scatter<CoarseEntries<E::KK>, true>), dim3((uint32_t)(ctot / SB_TILE)),
+                           dim3(SBS_THREADS), 0, st, ce, (uint32_t)ctot, sm, n_sb, nullptr, ctl, reg, rd, rt, rk, ri,
+                           StatsJob{});
+      }
+    } else {
       TimedLaunch tl(ctx, "scatter", 32.0 * n);
       hipLaunchKernelGGL((k_sb_scatter<E, true>), dim3(n_tiles + (stats.blk ? 1 : 0)), dim3(SBS_THREADS), 0, st, src,
                          n, sm, n_sb, nullptr, ctl, reg, rd, rt, rk, ri, stats);
     }
+    // many super-buckets: their output starts from one scan, not a sum per sort block
+    uint32_t* pre = n_sb > 512 ? ctx->d_cur.get<uint32_t>(n_sb) : nullptr;
+    if (pre) hipLaunchKernelGGL(k_sb_prefix, dim3(1), dim3(1024), 0, st, ctl, n_sb, pre);
     {
       TimedLaunch tl(ctx, "sort_small", 24.0 * n + 4.0 * n_slots);
       hipLaunchKernelGGL(k_sb_sort_region<E::KK>, dim3(n_sb), dim3(SBT_THREADS), 0, st, sm, n_slots, n_sb, ctl,
                          ctl_next, reg, rd, rt, rk, ri, kt, kk, ki, offsets, order, big_list, big_count, spill,
-                         ctx->round_ret);
+                         ctx->round_ret, (const uint32_t*)pre);
     }
   } else {
     const size_t nh = (size_t)n_sb * n_tiles;

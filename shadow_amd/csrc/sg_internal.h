@@ -109,10 +109,13 @@ struct sg_ctx {
   // the round's stats and error flags straight from that kernel: no copies.
   uint32_t* round_err = nullptr;
   sg_round_ret* round_ret = nullptr;
-  // Region bucketing counters, two parities of [SB_MAX counts + overflow flag]
-  // (zeroed at creation; each call's sort kernel clears the other parity).
+  // Region bucketing counters, two parities of [SB_SUB x SB_MAX counts + overflow
+  // flag] (zeroed at creation; each call's sort kernel clears the other parity),
+  // then two parities for the coarse level of two-level scatters (cleared by the
+  // second level's kernel).
   uint32_t* sb_ctl = nullptr;
-  uint32_t sb_parity = 0;
+  uint32_t sb_parity = 0, sb_parity_c = 0;
+  sg::DevBuf d_cd, d_ct, d_ck, d_ci;  // coarse-level runs of a two-level scatter
   // APSP: the active-batch count of the next pass, written by k_active_list
   // into pinned host-mapped memory at each pass-chunk end
   uint32_t* apsp_ret = nullptr;

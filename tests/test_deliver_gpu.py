@@ -167,6 +167,29 @@ def test_scan_path_bucketing(oracle, ctx, monkeypatch, hot):
     _assert_same(want, got, ost, gst)
 
 
+@pytest.mark.parametrize("hot", [0.0, 0.0025, 0.1, 0.5])
+def test_two_level_bucketing(oracle, ctx, monkeypatch, hot):
+    """SG_BUCKET_TWO_LEVEL=1 forces the two-level region scatter (coarse buckets,
+    then super-buckets; the default from 512 super-buckets on, e.g. C5).  0.1: the
+    hot slot overfills its coarse sub-region, and the round falls back to the scan
+    path from the second level; 0.5 overfills the coarse level itself.  Consecutive
+    rounds alternate with the one-level scatter, so both
+    counter parities of both levels are reused."""
+    lat, loss, hosts = _world(n_hosts=3000, seed=12)
+    ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    rng, ctr = ht.get_state()
+    tab = _device_table(lat, loss)
+    for k in range(5):
+        monkeypatch.setenv("SG_BUCKET_TWO_LEVEL", "0" if k == 2 else "1")
+        start, end = T0 + k * 10**6, T0 + (k + 1) * 10**6
+        pk = synth.make_packets(150000, hosts, start, end, seed=40 + k, hot_dst=7 if hot else -1, p_hot=hot)
+        want = oracle.deliver_round(end, 2**63, 0, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
+                                    hosts["ip"], hosts["route"], lat, loss, rng, ctr)
+        out = deliver_round(ht, tab, PacketBatch.from_numpy(pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"]),
+                            end, 2**63, 0)
+        _assert_same(want, out.to_numpy(150000), (rng, ctr), ht.get_state())
+
+
 def test_equal_times_order_by_source(oracle, ctx):
     """All packets clamp to round_end: order falls back to (src_host_id, event id)."""
     lat, loss, hosts = _world(n_hosts=500, seed=4, lossy=False)

@@ -104,6 +104,14 @@ def test_sharded_round_matches_single(oracle, ctx, W):
     assert want["delivered"] > 0
 
 
+@pytest.mark.parametrize("p_hot", [0.0, 0.1])
+def test_sharded_two_level_bucketing(oracle, ctx, monkeypatch, p_hot):
+    """The destination phase's two-level scatter on received records (order keys carried)."""
+    monkeypatch.setenv("SG_BUCKET_TWO_LEVEL", "1")
+    want = _run(oracle, ctx, 2, 60000, hot=17 if p_hot else -1, seed=6, p_hot=p_hot)
+    assert want["delivered"] > 0
+
+
 @pytest.mark.parametrize("p_hot", [0.1, 0.01])
 def test_sharded_hot_destination(oracle, ctx, p_hot):
     # 0.1: the hot slot overfills its region (scan-path fallback); 0.01: a big
