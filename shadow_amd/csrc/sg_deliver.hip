@@ -167,8 +167,14 @@ enum : uint8_t { W_SIM_END = 0, W_NO_DST = 1, W_DRAW = 2, W_PAYLOAD = 4, W_BOOT 
 // resident at once); else latency and loss are staged separately (21 B).  The
 // destination stays in the registers of the thread that resolved it: phases 1
 // and 3 map packets to threads identically.
+// (the unpacked two-array variant needs 74 VGPRs and stays at 6 waves per SIMD)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wpass-failed"
 template <bool PACKED>
-__global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
+// At most 64 VGPRs (8 waves per SIMD, 8 blocks per CU): a 100k-host round's
+// 1,563 blocks are then all resident at once.  At 74 VGPRs 6 blocks fit a CU,
+// and the last 27 blocks ran as a second round, doubling the kernel time.
+__global__ void __launch_bounds__(WALK_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) k_walk(WalkArgs a) {
   __shared__ uint64_t s_t[WALK_CHUNK];                  // send time -> arrival time
   __shared__ uint64_t s_l[WALK_CHUNK];                  // path latency (or cell) -> event id
   __shared__ float s_loss[PACKED ? 1 : WALK_CHUNK];     // path packet loss (two-array form)
@@ -355,6 +361,7 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(WalkArgs a) {
     }
   }
 }
+#pragma clang diagnostic pop
 
 // Round statistics: sum / min / min over the walk blocks' partials, written
 // with the source phase's error flags straight into the context's pinned
@@ -593,6 +600,7 @@ static void fail_flags(uint32_t err) {
 constexpr int SB_THREADS = 256;
 constexpr int SB_TILE = 4096;        // entries per hist / scatter block
 constexpr int SB_MAX = 4096;         // super-buckets (LDS histogram bins)
+constexpr uint32_t CB_MAX = 256;     // coarse buckets of a two-level scatter (and super-buckets per coarse bucket)
 static_assert(SB_SUB * SB_MAX + 1 == SB_CTL_STRIDE, "region counters: SB_SUB x SB_MAX counts + the overflow flag");
 constexpr uint32_t SB_FLAG = SB_SUB * SB_MAX;  // overflow flag word
 constexpr int SB_SLOTS_MAX = 1024;   // slots per super-bucket
@@ -736,7 +744,9 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* a, uint32_t n
 // the scan path).
 constexpr int SBS_THREADS = 512;
 constexpr uint32_t RUN_DROPPED = 0xFFFFFFFFu;  // cannot be a valid run base (see below)
-template <class E, bool REGION>
+// NB: the most buckets a call may have (SB_MAX, or CB_MAX for the levels of a
+// two-level scatter, whose smaller LDS arrays let two blocks share a CU).
+template <class E, bool REGION, uint32_t NB = SB_MAX>
 __global__ void __launch_bounds__(SBS_THREADS)
     k_sb_scatter(E src, uint32_t n, SbMap sm, uint32_t n_sb, const uint32_t* __restrict__ tile_off,
                  uint32_t* __restrict__ ctl, uint32_t region, uint32_t* __restrict__ rd, uint64_t* __restrict__ rt,
@@ -776,8 +786,8 @@ __global__ void __launch_bounds__(SBS_THREADS)
     nsb = min(src.cpb, n_sb - sb_lo);
   }
   constexpr int PER = SB_TILE / SBS_THREADS;
-  __shared__ uint32_t lcur[SB_MAX];   // local start, then cursor
-  __shared__ uint32_t lbase[SB_MAX];  // global position of the run - local start
+  __shared__ uint32_t lcur[NB];   // local start, then cursor
+  __shared__ uint32_t lbase[NB];  // global position of the run - local start
   __shared__ uint32_t sd[SB_TILE];
   __shared__ uint64_t st_[SB_TILE];
   __shared__ uint32_t si[SB_TILE];
@@ -803,7 +813,7 @@ __global__ void __launch_bounds__(SBS_THREADS)
   for (int k = 0; k < PER; k++)
     if (d[k] != NONE) atomicAdd(&lcur[sm.of(d[k]) - sb_lo], 1u);
   __syncthreads();
-  const uint32_t total = block_exclusive_scan<SBS_THREADS, SB_MAX / SBS_THREADS>(lcur, nsb, wsum);
+  const uint32_t total = block_exclusive_scan<SBS_THREADS, (NB + SBS_THREADS - 1) / SBS_THREADS>(lcur, nsb, wsum);
   for (uint32_t i = threadIdx.x; i < nsb; i += SBS_THREADS) {
     if (REGION) {
       // the run of super-bucket i: local [lcur[i], lcur[i] + c) -> sub-region slot g..g+c.
@@ -1258,7 +1268,8 @@ static bool bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
     const int two_env = tl_env && *tl_env ? atoi(tl_env) : -1;
     const bool two = two_env == 1 || (two_env != 0 && n_sb > 512);
     if (two) {
-      const uint32_t cpb = std::max<uint32_t>(2, (n_sb + 255) / 256), n_cb = (n_sb + cpb - 1) / cpb;
+      const uint32_t cpb = std::max<uint32_t>(2, (n_sb + CB_MAX - 1) / CB_MAX), n_cb = (n_sb + cpb - 1) / cpb;
+      static_assert(SB_MAX / CB_MAX <= CB_MAX, "a coarse bucket's super-buckets must fit CB_MAX");
       SbMap cm{((1ull << 40) + (uint64_t)spb64 * cpb - 1) / ((uint64_t)spb64 * cpb), (uint32_t)(spb64 * cpb)};
       // per (coarse bucket, XCD) sub-region: 1.25x its mean share + 1024, in whole tiles
       const uint64_t mean = ((uint64_t)n + (uint64_t)n_cb * SB_SUB - 1) / ((uint64_t)n_cb * SB_SUB);
@@ -1274,13 +1285,13 @@ static bool bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
       uint32_t* ci = ctx->d_ci.get<uint32_t>(ctot);
       {
         TimedLaunch tl(ctx, "scatter", 32.0 * n);
-        hipLaunchKernelGGL((k_sb_scatter<E, true>), dim3(n_tiles + (stats.blk ? 1 : 0)), dim3(SBS_THREADS), 0, st,
+        hipLaunchKernelGGL((k_sb_scatter<E, true, CB_MAX>), dim3(n_tiles + (stats.blk ? 1 : 0)), dim3(SBS_THREADS), 0, st,
                            src, n, cm, n_cb, nullptr, cctl, (uint32_t)creg, cd, ct, ck, ci, stats);
       }
       CoarseEntries<E::KK> ce{cd, ct, ck, ci, cctl, cctl_next, (uint32_t)creg, (uint32_t)subcap, cpb};
       {
         TimedLaunch tl(ctx, "scatter2", 32.0 * n);
-        hipLaunchKernelGGL((k_sb_scatter<CoarseEntries<E::KK>, true>), dim3((uint32_t)(ctot / SB_TILE)),
+        hipLaunchKernelGGL((k_sb_scatter<CoarseEntries<E::KK>, true, CB_MAX>), dim3((uint32_t)(ctot / SB_TILE)),
                            dim3(SBS_THREADS), 0, st, ce, (uint32_t)ctot, sm, n_sb, nullptr, ctl, reg, rd, rt, rk, ri,
                            StatsJob{});
       }
@@ -1365,7 +1376,7 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   }
   {
     TimedLaunch tl(ctx, "seg_bounds", 4.0 * P + 4.0 * H);
-    hipLaunchKernelGGL(k_host_off, dim3(grid_for((size_t)P + 1, 256, 16384)), dim3(256), 0, st, pk->src_host, P, H,
+    hipLaunchKernelGGL(k_host_off, dim3(grid_for((size_t)P + 1, 256, 1u << 20)), dim3(256), 0, st, pk->src_host, P, H,
                        w.host_off, ctx->round_err, hs->route, tab->row_begin, tab->n_rows);
   }
   WalkArgs a;
