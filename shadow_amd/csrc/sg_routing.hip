@@ -1167,7 +1167,11 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 // rows the next phase reads.  Cached per (used list, range, settings).
 static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h_used, uint32_t n_used,
                                      uint32_t row_begin, uint32_t row_end) {
-  const int n_phase = std::max(2, std::min(6, env_int("SG_SSSP_PHASES", 4)));
+  // phases by rows per CU (one box, tools/sssp_ab.py --rows, C3 graph): 39 rows per CU
+  // (10k rows) 4 phases; 19.5 (a half) 3 phases, 2.25 against 2.57 ms unbounded;
+  // 9.8 (a quarter) 2 phases, 1.30 against 1.38 ms
+  const uint32_t per_cu = (row_end - row_begin) / std::max(1, ctx->n_cu);
+  const int n_phase = std::max(2, std::min(6, env_int("SG_SSSP_PHASES", per_cu >= 32 ? 4 : per_cu >= 16 ? 3 : 2)));
   const int kb = std::max(1, std::min(SSSP_KB_MAX, env_int("SG_SSSP_BOUNDS", 2)));
   // exact seeds need a column for every node (see sg_sssp.hip "Exact seeds")
   const bool exact = env_int("SG_SSSP_EXACT", 1) != 0 && n_used == net->n_nodes;
@@ -1177,6 +1181,13 @@ static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h
         std::equal(p->used.begin(), p->used.end(), h_used))
       return p.get();
   const uint32_t n = net->n_nodes;
+  const auto plan_t0 = std::chrono::steady_clock::now();  // SG_PLAN_DIAG=1: construction time on stderr
+  const bool pdiag = env_int("SG_PLAN_DIAG", 0) != 0;
+  auto lap = [&](const char* what) {
+    if (pdiag)
+      fprintf(stderr, "[sssp]   plan %s at %.3f ms\n", what,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - plan_t0).count());
+  };
   if (net->h_out_off.empty()) {
     std::vector<uint32_t> arc((size_t)net->n_arcs * 3);
     net->h_out_off.resize((size_t)n + 1);
@@ -1191,6 +1202,7 @@ static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h
       net->h_out_zero_loss[a] = arc[3 * a + 2] == 0x3F800000u;  // 1f32 - loss == 1.0
     }
   }
+  lap("arcs on host");
   const uint32_t* off = net->h_out_off.data();
   const uint32_t *head = net->h_out_head.data(), *lat = net->h_out_lat.data();
   const uint8_t* zl = net->h_out_zero_loss.data();
@@ -1214,6 +1226,7 @@ static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h
         if (rel[head[a]] != ~0u) in_row[cur[rel[head[a]]]++] = r;
     }
   }
+  lap("in-arc lists");
   std::vector<int> phase(rows, -1);
   for (int ph = 0; ph + 1 < n_phase; ph++) {
     // greedy dominating set of the rows still unassigned (lazily re-scored max-heap)
@@ -1224,20 +1237,28 @@ static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h
       for (uint32_t k = in_off[v]; k < in_off[v + 1]; k++) g += live(in_row[k]);
       return g;
     };
-    std::vector<std::pair<uint32_t, uint32_t>> heap;  // (gain, ~row): ties to the lower row
+    // bucket queue by gain (gains only fall, so the top bucket only moves down);
+    // a popped row whose gain fell is re-filed: O(arcs) in all.  A binary heap
+    // took ~2 ms per phase at C3, half of a warm build.
+    std::vector<uint32_t> gn(rows, 0);
+    uint32_t top = 0;
     for (uint32_t r = 0; r < rows; r++)
-      if (phase[r] < 0) heap.push_back({gain(r), ~r});
-    std::make_heap(heap.begin(), heap.end());
+      if (phase[r] < 0) top = std::max(top, gn[r] = gain(r));
+    std::vector<std::vector<uint32_t>> bucket(top + 1);
+    for (uint32_t r = rows; r-- > 0;)  // descending, so each bucket pops its lowest row first
+      if (phase[r] < 0 && gn[r]) bucket[gn[r]].push_back(r);
     std::vector<uint32_t> chosen;
-    while (!heap.empty()) {
-      std::pop_heap(heap.begin(), heap.end());
-      const auto [g, nr] = heap.back();
-      heap.pop_back();
-      const uint32_t v = ~nr, gv = gain(v);
+    for (uint32_t g = top; g > 0;) {
+      if (bucket[g].empty()) {
+        g--;
+        continue;
+      }
+      const uint32_t v = bucket[g].back();
+      bucket[g].pop_back();
+      const uint32_t gv = gain(v);
       if (gv == 0) continue;
       if (gv < g) {
-        heap.push_back({gv, nr});
-        std::push_heap(heap.begin(), heap.end());
+        bucket[gv].push_back(v);
         continue;
       }
       chosen.push_back(v);
@@ -1245,6 +1266,7 @@ static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h
       for (uint32_t k = in_off[v]; k < in_off[v + 1]; k++) covered[in_row[k]] = 1;
     }
     for (uint32_t v : chosen) phase[v] = ph;
+    lap("dominating set");
   }
   for (uint32_t r = 0; r < rows; r++)
     if (phase[r] < 0) phase[r] = n_phase - 1;
@@ -1299,9 +1321,14 @@ static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h
     all.insert(all.end(), ubw.begin(), ubw.end());
     if (P.n) p->phases.push_back(P);
   }
+  lap("bound rows");
   SG_HIP(hipMalloc(&p->d, std::max<size_t>(all.size() * 4, 16)));
+  lap("hipMalloc");
   SG_HIP(hipMemcpyAsync(p->d, all.data(), all.size() * 4, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
+  if (env_int("SG_PLAN_DIAG", 0))
+    fprintf(stderr, "[sssp] plan for %u rows, %zu phases: %.3f ms\n", rows, p->phases.size(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - plan_t0).count());
   net->plans.push_front(std::move(p));
   if (net->plans.size() > 16) net->plans.pop_back();
   return net->plans.front().get();
@@ -1324,11 +1351,12 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   const uint32_t n_diag = std::min<uint32_t>(rows, 4096);
   unsigned long long* diag = diag_on ? ctx->r_misc.get<unsigned long long>((size_t)n_diag * 8) : nullptr;
   if (diag) SG_HIP(hipMemsetAsync(diag, 0, (size_t)n_diag * 64, st));
-  // Two phases (sssp_plan) when the rows fill the CUs many times over: with a
-  // few rows per CU the phase boundary costs more than the bounds save (2,000
-  // nodes: 0.41 against 0.39 ms).  SG_SSSP_SEEDS=0 never, =2 always.
+  // Phases (sssp_plan) from 8 rows per CU: with fewer, the phase boundaries cost
+  // more than the bounds save (tools/sssp_ab.py, C3 graph: 1,250 rows 0.78 against
+  // 0.76 ms unbounded, a 2,000-node build 0.45 against 0.43; 2,500 rows 1.30
+  // against 1.38, a 4,000-node build 0.97 against 1.07).  SG_SSSP_SEEDS=0 never, =2 always.
   const int seeds_env = env_int("SG_SSSP_SEEDS", 1);
-  const bool two_phase = h_used && seeds_env != 0 && (seeds_env == 2 || rows >= 16u * 256u);
+  const bool two_phase = h_used && seeds_env != 0 && (seeds_env == 2 || rows >= 8u * (uint32_t)ctx->n_cu);
   const sg_sssp_plan* plan = two_phase ? sssp_plan(ctx, net, h_used, n_used, row_begin, row_end) : nullptr;
   if (plan && plan->phases.size() > 1) {
     for (size_t ph = 0; ph < plan->phases.size(); ph++) {

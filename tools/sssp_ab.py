@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--nodes", type=int, default=10000)
     ap.add_argument("--degree", type=float, default=8.0)
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--rows", default="", help="r0:r1, a rank's row block (default: every row)")
     ap.add_argument("settings", nargs="+", help="space-free env assignments, comma separated per setting")
     a = ap.parse_args()
     import torch
@@ -29,23 +30,24 @@ def main():
     net = NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
     n = a.nodes
     used = np.arange(n, dtype=np.uint32)
-    lat = torch.empty(n * n, dtype=torch.int64, device="cuda")
-    loss = torch.empty(n * n, dtype=torch.float32, device="cuda")
+    r0, r1 = (int(x) for x in a.rows.split(":")) if a.rows else (0, n)
+    lat = torch.empty((r1 - r0) * n, dtype=torch.int64, device="cuda")
+    loss = torch.empty((r1 - r0) * n, dtype=torch.float32, device="cuda")
     first = None
     for st in a.settings:
         env = dict(kv.split("=", 1) for kv in st.split(",") if kv)
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
+        net.build_rows_device(used, r0, r1, lat.data_ptr(), loss.data_ptr(), True)
         torch.cuda.synchronize()
         ts = []
         for _ in range(a.reps):
             t0 = time.perf_counter()
-            net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
+            net.build_rows_device(used, r0, r1, lat.data_ptr(), loss.data_ptr(), True)
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
         ctx.enable_timers(True)
-        net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
+        net.build_rows_device(used, r0, r1, lat.data_ptr(), loss.data_ptr(), True)
         tm = {k: round(ctx.read_timer(k)[0], 4) for k in ("sssp", "sssp_bounded", "relax", "relax_wide")}
         ctx.enable_timers(False)
         h = (lat.view(torch.int64).sum().item(), loss.view(torch.int32).to(torch.int64).sum().item())
