@@ -217,51 +217,46 @@ __global__ void __launch_bounds__(NT)
   const uint32_t src = used[row];
   // Setup.  Every global read below is a buffer load whose out-of-range lanes
   // read 0 without a branch, issued in groups so that a thread has a group's
-  // loads in flight at once (one round trip per group, not per element).
+  // loads in flight at once (one round trip per group, not per element).  The
+  // out_off loads are issued before the LDS initialisation and land during it.
   constexpr uint32_t OOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)out_off, 0, (int)((n + 1) * 4u),
+                                                                      0x00020000);
+  constexpr int GO = 12;  // out_off entries per thread per group: one group up to 12,287 nodes
+  uint32_t to[GO];
+#pragma unroll
+  for (int g = 0; g < GO; g++) {
+    const uint32_t v = tid + g * NT;
+    to[g] = __builtin_amdgcn_raw_buffer_load_b32(ro, v <= n ? v * 4u : OOB, 0, 0);
+  }
   for (uint32_t v = tid; v < n; v += NT) key[v] = FKEY_INF;
   for (uint32_t i = tid; i < cap; i += NT) ring[i] = RING_EMPTY;
   for (int i = tid; i < NW * 64 * SSSP_K; i += NT) (&own[0][0])[i] = 0;
   if (tid < 8) ctl[tid] = 0;
   if (tid == 0) hb = 0;
-  {  // out_off staged in LDS (n + 1 entries)
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)out_off, 0, (int)((n + 1) * 4u),
-                                                                        0x00020000);
-    constexpr int G = 8;
-    for (uint32_t v0 = tid; v0 <= n; v0 += G * NT) {
-      uint32_t t[G];
 #pragma unroll
-      for (int g = 0; g < G; g++) {
-        const uint32_t v = v0 + g * NT;
-        t[g] = __builtin_amdgcn_raw_buffer_load_b32(ro, v <= n ? v * 4u : OOB, 0, 0);
-      }
+  for (int g = 0; g < GO; g++)
+    if (tid + g * NT <= n) off[tid + g * NT] = to[g];
+  for (uint32_t v0 = tid + GO * NT; v0 <= n; v0 += GO * NT) {  // larger graphs: further groups
 #pragma unroll
-      for (int g = 0; g < G; g++)
-        if (v0 + g * NT <= n) off[v0 + g * NT] = t[g];
+    for (int g = 0; g < GO; g++) {
+      const uint32_t v = v0 + g * NT;
+      to[g] = __builtin_amdgcn_raw_buffer_load_b32(ro, v <= n ? v * 4u : OOB, 0, 0);
     }
+#pragma unroll
+    for (int g = 0; g < GO; g++)
+      if (v0 + g * NT <= n) off[v0 + g * NT] = to[g];
   }
   __syncthreads();
   if (ub_row) {  // Bounds: keys start just above the shortest of up to SSSP_KB known paths (clean)
-    // the listed bound rows, compacted (uniform): latency row, loss row (exact seeds only), own column, arc latency
-    uint32_t brow[SSSP_KB], bw[SSSP_KB];
-    bool bex[SSSP_KB];
+    // the bound rows (uniform; read per group from ub_row, not held in an
+    // array: a dynamically indexed array went to scratch memory)
     int nb = 0;
-#pragma unroll
-    for (int k = 0; k < SSSP_KB; k++) {
-      const uint32_t e = ub_row[(size_t)blockIdx.x * SSSP_KB + k];
-      if (e == ~0u) continue;
-      const uint32_t sr = e & ~SSSP_UB_EXACT;
-      brow[nb] = sr;
-      bw[nb] = ub_w[(size_t)blockIdx.x * SSSP_KB + k];
-      // a row flagged for the wide kernel (saturated or given up) may not hold
-      // its optimum everywhere: bounds only
-      bex[nb] = (e & SSSP_UB_EXACT) && !sat_row[sr - row_begin];
-      nb++;
-    }
+    for (int k = 0; k < SSSP_KB; k++) nb += ub_row[(size_t)blockIdx.x * SSSP_KB + k] != ~0u;
     if (nb) {
       const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc((void*)used, 0, (int)(n_used * 4u),
                                                                           0x00020000);
-      constexpr int G = 4;
+      constexpr int G = 6;  // columns per thread per group
       for (uint32_t j0 = tid; j0 < n_used; j0 += G * NT) {
         uint32_t vv[G];
         uint64_t m[G], ex[G];
@@ -271,31 +266,49 @@ __global__ void __launch_bounds__(NT)
           vv[g] = __builtin_amdgcn_raw_buffer_load_b32(ru, j < n_used ? j * 4u : OOB, 0, 0);
           m[g] = ex[g] = ~0ull;
         }
-        for (int k = 0; k < nb; k++) {
-          const size_t rb = (size_t)(brow[k] - out_row0) * n_used;
-          const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)(out_lat + rb), 0,
-                                                                              (int)(n_used * 8u), 0x00020000);
-          const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc((void*)(out_loss + rb), 0,
-                                                                              (int)(bex[k] ? n_used * 4u : 0u),
-                                                                              0x00020000);
-          uint64_t l[G];
-          uint32_t f[G];
+#pragma unroll 1
+        for (int k = 0; k < SSSP_KB; k += 2) {  // two bound rows' loads in flight together
+          bool on[2], exact[2];
+          uint32_t sr[2], w[2];
+          __amdgpu_buffer_rsrc_t rl[2], rf[2];
 #pragma unroll
-          for (int g = 0; g < G; g++) {
-            const uint32_t j = j0 + g * NT;
-            const auto x = __builtin_amdgcn_raw_buffer_load_b64(rl, j < n_used ? j * 8u : OOB, 0, 0);
-            l[g] = ((uint64_t)x[1] << 32) | x[0];
-            f[g] = __builtin_amdgcn_raw_buffer_load_b32(rf, j < n_used ? j * 4u : OOB, 0, 0);
+          for (int u = 0; u < 2; u++) {
+            const uint32_t e = ub_row[(size_t)blockIdx.x * SSSP_KB + k + u];
+            on[u] = e != ~0u;
+            sr[u] = e & ~SSSP_UB_EXACT;
+            w[u] = ub_w[(size_t)blockIdx.x * SSSP_KB + k + u];
+            // a row flagged for the wide kernel (saturated or given up) may not hold
+            // its optimum everywhere: bounds only
+            exact[u] = on[u] && (e & SSSP_UB_EXACT) && !sat_row[sr[u] - row_begin];
+            const size_t rb = on[u] ? (size_t)(sr[u] - out_row0) * n_used : 0;
+            rl[u] = __builtin_amdgcn_make_buffer_rsrc((void*)(out_lat + rb), 0, (int)(on[u] ? n_used * 8u : 0u),
+                                                      0x00020000);
+            rf[u] = __builtin_amdgcn_make_buffer_rsrc((void*)(out_loss + rb), 0, (int)(exact[u] ? n_used * 4u : 0u),
+                                                      0x00020000);
           }
+          if (!on[0] && !on[1]) continue;
+          uint64_t l[2][G];
+          uint32_t f[2][G];
 #pragma unroll
-          for (int g = 0; g < G; g++) {
-            const uint32_t j = j0 + g * NT;
-            const uint64_t ub = l[g] + bw[k];  // bw < 2^32: a wrap means >= 2^64
-            if (j >= n_used || ub < bw[k]) continue;
-            m[g] = min(m[g], ub);
-            if (bex[k] && ub < LAT32_SAT && j != brow[k])  // exact: the path s -> s' then D[s'][v]
-              ex[g] = min(ex[g], (ub << 32) | ((uint64_t)f[g] << 1));
-          }
+          for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+              const uint32_t j = j0 + g * NT;
+              const auto x = __builtin_amdgcn_raw_buffer_load_b64(rl[u], j < n_used ? j * 8u : OOB, 0, 0);
+              l[u][g] = ((uint64_t)x[1] << 32) | x[0];
+              f[u][g] = __builtin_amdgcn_raw_buffer_load_b32(rf[u], j < n_used ? j * 4u : OOB, 0, 0);
+            }
+#pragma unroll
+          for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+              const uint32_t j = j0 + g * NT;
+              const uint64_t ub = l[u][g] + w[u];  // w < 2^32: a wrap means >= 2^64
+              if (!on[u] || j >= n_used || ub < w[u]) continue;
+              m[g] = min(m[g], ub);
+              if (exact[u] && ub < LAT32_SAT && j != sr[u])  // exact: the path s -> s' then D[s'][v]
+                ex[g] = min(ex[g], (ub << 32) | ((uint64_t)f[u][g] << 1));
+            }
         }
 #pragma unroll
         for (int g = 0; g < G; g++) {
