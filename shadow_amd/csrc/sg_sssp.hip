@@ -190,7 +190,8 @@ __global__ void __launch_bounds__(NT)
                uint32_t* __restrict__ sat_row, uint32_t delta, int vec_out, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ diag, uint32_t claim, uint32_t idle_sleep,
                uint32_t lane_deg_max, const uint32_t* __restrict__ blk_rows,
-               const uint32_t* __restrict__ ub_row, const uint32_t* __restrict__ ub_w) {
+               const uint32_t* __restrict__ ub_row, const uint32_t* __restrict__ ub_w,
+               uint32_t* __restrict__ item_ctr, uint32_t n_items) {
   constexpr int NW = NT / 64;
   extern __shared__ __align__(16) unsigned char smem[];
   const uint32_t cap = sssp_ring_cap(n);
@@ -208,380 +209,391 @@ __global__ void __launch_bounds__(NT)
   __shared__ unsigned long long sink[64];  // per-lane no-op target of offer_all
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // COUNT diagnostics of the first 4096 rows: cycle stamps, pops, bucket advances, relaxations
-  const bool dg = COUNT && diag && blockIdx.x < 4096 && tid == 0;
-  const unsigned long long c_start = dg ? clock64() : 0;
-  uint32_t n_adv = 0, n_pops = 0;
-  unsigned long long cyc_claim = 0, cyc_pop = 0, cyc_steps = 0;  // per wave, COUNT diagnostics
-  const uint32_t row = blk_rows ? blk_rows[blockIdx.x] : row_begin + blockIdx.x;
-  const uint32_t src = used[row];
-  // Setup.  Every global read below is a buffer load whose out-of-range lanes
-  // read 0 without a branch, issued in groups so that a thread has a group's
-  // loads in flight at once (one round trip per group, not per element).  The
-  // out_off loads are issued before the LDS initialisation and land during it.
+  // Every global read of the setup is a buffer load whose out-of-range lanes read
+  // 0 without a branch, issued in groups so that a thread has a group's loads in
+  // flight at once (one round trip per group, not per element).
   constexpr uint32_t OOB = 0x80000000u;
-  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)out_off, 0, (int)((n + 1) * 4u),
-                                                                      0x00020000);
-  constexpr int GO = 12;  // out_off entries per thread per group: one group up to 12,287 nodes
-  uint32_t to[GO];
-#pragma unroll
-  for (int g = 0; g < GO; g++) {
-    const uint32_t v = tid + g * NT;
-    to[g] = __builtin_amdgcn_raw_buffer_load_b32(ro, v <= n ? v * 4u : OOB, 0, 0);
-  }
-  for (uint32_t v = tid; v < n; v += NT) key[v] = FKEY_INF;
-  for (uint32_t i = tid; i < cap; i += NT) ring[i] = RING_EMPTY;
-  for (int i = tid; i < NW * 64 * SSSP_K; i += NT) (&own[0][0])[i] = 0;
-  if (tid < 8) ctl[tid] = 0;
-  if (tid == 0) hb = 0;
-#pragma unroll
-  for (int g = 0; g < GO; g++)
-    if (tid + g * NT <= n) off[tid + g * NT] = to[g];
-  for (uint32_t v0 = tid + GO * NT; v0 <= n; v0 += GO * NT) {  // larger graphs: further groups
-#pragma unroll
-    for (int g = 0; g < GO; g++) {
-      const uint32_t v = v0 + g * NT;
-      to[g] = __builtin_amdgcn_raw_buffer_load_b32(ro, v <= n ? v * 4u : OOB, 0, 0);
-    }
-#pragma unroll
-    for (int g = 0; g < GO; g++)
-      if (v0 + g * NT <= n) off[v0 + g * NT] = to[g];
-  }
-  __syncthreads();
-  if (ub_row) {  // Bounds: keys start just above the shortest of up to SSSP_KB known paths (clean)
-    // the bound rows (uniform; read per group from ub_row, not held in an
-    // array: a dynamically indexed array went to scratch memory)
-    int nb = 0;
-    for (int k = 0; k < SSSP_KB; k++) nb += ub_row[(size_t)blockIdx.x * SSSP_KB + k] != ~0u;
-    if (nb) {
-      const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc((void*)used, 0, (int)(n_used * 4u),
-                                                                          0x00020000);
-      constexpr int G = 6;  // columns per thread per group
-      for (uint32_t j0 = tid; j0 < n_used; j0 += G * NT) {
-        uint32_t vv[G];
-        uint64_t m[G], ex[G];
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-          const uint32_t j = j0 + g * NT;
-          vv[g] = __builtin_amdgcn_raw_buffer_load_b32(ru, j < n_used ? j * 4u : OOB, 0, 0);
-          m[g] = ex[g] = ~0ull;
-        }
-#pragma unroll 1
-        for (int k = 0; k < SSSP_KB; k += 2) {  // two bound rows' loads in flight together
-          bool on[2], exact[2];
-          uint32_t sr[2], w[2];
-          __amdgpu_buffer_rsrc_t rl[2], rf[2];
-#pragma unroll
-          for (int u = 0; u < 2; u++) {
-            const uint32_t e = ub_row[(size_t)blockIdx.x * SSSP_KB + k + u];
-            on[u] = e != ~0u;
-            sr[u] = e & ~SSSP_UB_EXACT;
-            w[u] = ub_w[(size_t)blockIdx.x * SSSP_KB + k + u];
-            // a row flagged for the wide kernel (saturated or given up) may not hold
-            // its optimum everywhere: bounds only
-            exact[u] = on[u] && (e & SSSP_UB_EXACT) && !sat_row[sr[u] - row_begin];
-            const size_t rb = on[u] ? (size_t)(sr[u] - out_row0) * n_used : 0;
-            rl[u] = __builtin_amdgcn_make_buffer_rsrc((void*)(out_lat + rb), 0, (int)(on[u] ? n_used * 8u : 0u),
-                                                      0x00020000);
-            rf[u] = __builtin_amdgcn_make_buffer_rsrc((void*)(out_loss + rb), 0, (int)(exact[u] ? n_used * 4u : 0u),
-                                                      0x00020000);
-          }
-          if (!on[0] && !on[1]) continue;
-          uint64_t l[2][G];
-          uint32_t f[2][G];
-#pragma unroll
-          for (int u = 0; u < 2; u++)
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-              const uint32_t j = j0 + g * NT;
-              const auto x = __builtin_amdgcn_raw_buffer_load_b64(rl[u], j < n_used ? j * 8u : OOB, 0, 0);
-              l[u][g] = ((uint64_t)x[1] << 32) | x[0];
-              f[u][g] = __builtin_amdgcn_raw_buffer_load_b32(rf[u], j < n_used ? j * 4u : OOB, 0, 0);
-            }
-#pragma unroll
-          for (int u = 0; u < 2; u++)
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-              const uint32_t j = j0 + g * NT;
-              const uint64_t ub = l[u][g] + w[u];  // w < 2^32: a wrap means >= 2^64
-              if (!on[u] || j >= n_used || ub < w[u]) continue;
-              m[g] = min(m[g], ub);
-              if (exact[u] && ub < LAT32_SAT && j != sr[u])  // exact: the path s -> s' then D[s'][v]
-                ex[g] = min(ex[g], (ub << 32) | ((uint64_t)f[u][g] << 1));
-            }
-        }
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-          uint64_t kv = m[g] + 1 < LAT32_SAT ? ((m[g] + 1) << 32) | ((uint64_t)0x3F800000u << 1) : FKEY_INF;
-          kv = min(kv, ex[g]);
-          if (j0 + g * NT < n_used && kv != FKEY_INF) key[vv[g]] = kv;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  const unsigned long long c_setup = dg ? clock64() : 0;
-  if (tid == 0) {
-    key[src] = 1ull;  // PathProperties::default(), dirty and queued
-    ring[0] = (uint16_t)src;
-    ctl[TAIL] = 1;
-  }
-  uint32_t split = delta;  // delta >= 1
-  const __amdgpu_buffer_rsrc_t arcs = __builtin_amdgcn_make_buffer_rsrc((void*)out_arc, 0, (int)(n_arcs * 12u),
+  {  // out_off staged in LDS, once per workgroup (a persistent one keeps it for all its rows)
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)out_off, 0, (int)((n + 1) * 4u),
                                                                         0x00020000);
-  uint32_t n_rel = 0;
-  // a bound no correct search reaches (a bucket advance queues at least one
-  // node, and a node is queued at most once per improvement); past it the row
-  // is handed to the wide kernel instead of spinning
-  const uint32_t max_adv = 4u * n + 64u;
-  bool gave_up = false;
-  uint8_t* ow = own[wv];
-  // spin budget per wave (sleeps of ~128 cycles): a safety valve against a
-  // queue bug, never reached by a correct search; past it the wave leaves and
-  // the row goes to the wide kernel
-  uint32_t spins = 0;
-  constexpr uint32_t SPIN_MAX = 1u << 22;
-  auto ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-  // relax NK candidates into key[v[c]]; app[c]: v[c] became dirty below split (to
-  // be queued).  Branch-free, so the NK LDS atomics issue back to back and share
-  // one wait: a lane with no candidate (or a saturated one, never propagated)
-  // offers ~0 to its own sink word, a no-op.  (With one branch per candidate the
-  // compiler waited for each atomic's return before issuing the next.)
-  auto offer_all = [&](auto nk, const bool* valid, const uint32_t* v, const uint64_t* cand, bool* app) {
-    constexpr int NK = decltype(nk)::value;
-    uint64_t cd[NK], old[NK];
+    constexpr int GO = 12;  // entries per thread per group: one group up to 12,287 nodes
+    for (uint32_t v0 = tid; v0 <= n; v0 += GO * NT) {
+      uint32_t to[GO];
 #pragma unroll
-    for (int c = 0; c < NK; c++) {
-      const bool ok = valid[c] && fkey_lat(cand[c]) != LAT32_SAT;
-      cd[c] = ok ? cand[c] : ~0ull;
-      old[c] = __hip_atomic_fetch_min(ok ? &key[v[c]] : &sink[lane], (unsigned long long)cd[c], __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int g = 0; g < GO; g++) {
+        const uint32_t v = v0 + g * NT;
+        to[g] = __builtin_amdgcn_raw_buffer_load_b32(ro, v <= n ? v * 4u : OOB, 0, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < GO; g++)
+        if (v0 + g * NT <= n) off[v0 + g * NT] = to[g];
     }
-    // keep the scheduler from pulling a use of old[] between the atomics
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int c = 0; c < NK; c++)
-      app[c] = (old[c] >> 1) > (cd[c] >> 1) && !(old[c] & 1ull) && fkey_lat(cd[c]) < split;
-  };
-  __syncthreads();
-
-  for (;;) {
-    // ---- claim up to `claim` queued entries
-    const unsigned long long tc0 = (COUNT && diag) ? clock64() : 0;
-    uint32_t h = 0, k = 0;
-    if (lane == 0) {
-      for (;;) {
-        const unsigned long long w = __hip_atomic_load(&hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t hh = (uint32_t)(w >> 32), t = ld(&ctl[TAIL]);
-        if (t == hh) break;
-        const uint32_t kk = min(claim, t - hh);
-        const unsigned long long nw = ((unsigned long long)(hh + kk) << 32) | ((w & 0xFFFFFFFFull) + 1);
-        if (atomicCAS(&hb, w, nw) == w) {
-          h = hh;
-          k = kk;
-          break;
+  }
+  // Rows: one per workgroup, or (item_ctr set: persistent workgroups, one per
+  // CU) claimed one after another from a counter the host zeroed
+  __shared__ uint32_t s_item;
+  for (uint32_t it = 0;; it++) {
+    uint32_t bi;
+    if (item_ctr) {
+      if (tid == 0) s_item = atomicAdd(item_ctr, 1u);
+      __syncthreads();
+      bi = s_item;
+      __syncthreads();  // every thread has read s_item before thread 0 writes it again
+      if (bi >= n_items) break;
+    } else {
+      if (it) break;
+      bi = blockIdx.x;
+    }
+    // COUNT diagnostics of the first 4096 rows: cycle stamps, pops, bucket advances, relaxations
+    const bool dg = COUNT && diag && bi < 4096 && tid == 0;
+    const unsigned long long c_start = dg ? clock64() : 0;
+    uint32_t n_adv = 0, n_pops = 0;
+    unsigned long long cyc_claim = 0, cyc_pop = 0, cyc_steps = 0;  // per wave, COUNT diagnostics
+    const uint32_t row = blk_rows ? blk_rows[bi] : row_begin + bi;
+    const uint32_t src = used[row];
+    // Setup: the LDS queue and keys (out_off is staged once, before the row loop)
+    for (uint32_t v = tid; v < n; v += NT) key[v] = FKEY_INF;
+    for (uint32_t i = tid; i < cap; i += NT) ring[i] = RING_EMPTY;
+    for (int i = tid; i < NW * 64 * SSSP_K; i += NT) (&own[0][0])[i] = 0;
+    if (tid < 8) ctl[tid] = 0;
+    if (tid == 0) hb = 0;
+    __syncthreads();
+    if (ub_row) {  // Bounds: keys start just above the shortest of up to SSSP_KB known paths (clean)
+      // the bound rows (uniform; read per group from ub_row, not held in an
+      // array: a dynamically indexed array went to scratch memory)
+      int nb = 0;
+      for (int k = 0; k < SSSP_KB; k++) nb += ub_row[(size_t)bi * SSSP_KB + k] != ~0u;
+      if (nb) {
+        const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc((void*)used, 0, (int)(n_used * 4u),
+                                                                            0x00020000);
+        constexpr int G = 6;  // columns per thread per group
+        for (uint32_t j0 = tid; j0 < n_used; j0 += G * NT) {
+          uint32_t vv[G];
+          uint64_t m[G], ex[G];
+  #pragma unroll
+          for (int g = 0; g < G; g++) {
+            const uint32_t j = j0 + g * NT;
+            vv[g] = __builtin_amdgcn_raw_buffer_load_b32(ru, j < n_used ? j * 4u : OOB, 0, 0);
+            m[g] = ex[g] = ~0ull;
+          }
+  #pragma unroll 1
+          for (int k = 0; k < SSSP_KB; k += 2) {  // two bound rows' loads in flight together
+            bool on[2], exact[2];
+            uint32_t sr[2], w[2];
+            __amdgpu_buffer_rsrc_t rl[2], rf[2];
+  #pragma unroll
+            for (int u = 0; u < 2; u++) {
+              const uint32_t e = ub_row[(size_t)bi * SSSP_KB + k + u];
+              on[u] = e != ~0u;
+              sr[u] = e & ~SSSP_UB_EXACT;
+              w[u] = ub_w[(size_t)bi * SSSP_KB + k + u];
+              // a row flagged for the wide kernel (saturated or given up) may not hold
+              // its optimum everywhere: bounds only
+              exact[u] = on[u] && (e & SSSP_UB_EXACT) && !sat_row[sr[u] - row_begin];
+              const size_t rb = on[u] ? (size_t)(sr[u] - out_row0) * n_used : 0;
+              rl[u] = __builtin_amdgcn_make_buffer_rsrc((void*)(out_lat + rb), 0, (int)(on[u] ? n_used * 8u : 0u),
+                                                        0x00020000);
+              rf[u] = __builtin_amdgcn_make_buffer_rsrc((void*)(out_loss + rb), 0, (int)(exact[u] ? n_used * 4u : 0u),
+                                                        0x00020000);
+            }
+            if (!on[0] && !on[1]) continue;
+            uint64_t l[2][G];
+            uint32_t f[2][G];
+  #pragma unroll
+            for (int u = 0; u < 2; u++)
+  #pragma unroll
+              for (int g = 0; g < G; g++) {
+                const uint32_t j = j0 + g * NT;
+                const auto x = __builtin_amdgcn_raw_buffer_load_b64(rl[u], j < n_used ? j * 8u : OOB, 0, 0);
+                l[u][g] = ((uint64_t)x[1] << 32) | x[0];
+                f[u][g] = __builtin_amdgcn_raw_buffer_load_b32(rf[u], j < n_used ? j * 4u : OOB, 0, 0);
+              }
+  #pragma unroll
+            for (int u = 0; u < 2; u++)
+  #pragma unroll
+              for (int g = 0; g < G; g++) {
+                const uint32_t j = j0 + g * NT;
+                const uint64_t ub = l[u][g] + w[u];  // w < 2^32: a wrap means >= 2^64
+                if (!on[u] || j >= n_used || ub < w[u]) continue;
+                m[g] = min(m[g], ub);
+                if (exact[u] && ub < LAT32_SAT && j != sr[u])  // exact: the path s -> s' then D[s'][v]
+                  ex[g] = min(ex[g], (ub << 32) | ((uint64_t)f[u][g] << 1));
+              }
+          }
+  #pragma unroll
+          for (int g = 0; g < G; g++) {
+            uint64_t kv = m[g] + 1 < LAT32_SAT ? ((m[g] + 1) << 32) | ((uint64_t)0x3F800000u << 1) : FKEY_INF;
+            kv = min(kv, ex[g]);
+            if (j0 + g * NT < n_used && kv != FKEY_INF) key[vv[g]] = kv;
+          }
         }
       }
+      __syncthreads();
     }
-    h = __builtin_amdgcn_readfirstlane(h);
-    k = __builtin_amdgcn_readfirstlane(k);
-    if (!k) {
-      uint32_t q = 0;
-      if (lane == 0) {
-        const unsigned long long w = __hip_atomic_load(&hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (head, busy) before tail (see header)
-        q = (w & 0xFFFFFFFFull) == 0 && (uint32_t)(w >> 32) == ld(&ctl[TAIL]);
+    const unsigned long long c_setup = dg ? clock64() : 0;
+    if (tid == 0) {
+      key[src] = 1ull;  // PathProperties::default(), dirty and queued
+      ring[0] = (uint16_t)src;
+      ctl[TAIL] = 1;
+    }
+    uint32_t split = delta;  // delta >= 1
+    const __amdgpu_buffer_rsrc_t arcs = __builtin_amdgcn_make_buffer_rsrc((void*)out_arc, 0, (int)(n_arcs * 12u),
+                                                                          0x00020000);
+    uint32_t n_rel = 0;
+    // a bound no correct search reaches (a bucket advance queues at least one
+    // node, and a node is queued at most once per improvement); past it the row
+    // is handed to the wide kernel instead of spinning
+    const uint32_t max_adv = 4u * n + 64u;
+    bool gave_up = false;
+    uint8_t* ow = own[wv];
+    // spin budget per wave (sleeps of ~128 cycles): a safety valve against a
+    // queue bug, never reached by a correct search; past it the wave leaves and
+    // the row goes to the wide kernel
+    uint32_t spins = 0;
+    constexpr uint32_t SPIN_MAX = 1u << 22;
+    auto ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    // relax NK candidates into key[v[c]]; app[c]: v[c] became dirty below split (to
+    // be queued).  Branch-free, so the NK LDS atomics issue back to back and share
+    // one wait: a lane with no candidate (or a saturated one, never propagated)
+    // offers ~0 to its own sink word, a no-op.  (With one branch per candidate the
+    // compiler waited for each atomic's return before issuing the next.)
+    auto offer_all = [&](auto nk, const bool* valid, const uint32_t* v, const uint64_t* cand, bool* app) {
+      constexpr int NK = decltype(nk)::value;
+      uint64_t cd[NK], old[NK];
+  #pragma unroll
+      for (int c = 0; c < NK; c++) {
+        const bool ok = valid[c] && fkey_lat(cand[c]) != LAT32_SAT;
+        cd[c] = ok ? cand[c] : ~0ull;
+        old[c] = __hip_atomic_fetch_min(ok ? &key[v[c]] : &sink[lane], (unsigned long long)cd[c], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-      if (!__builtin_amdgcn_readfirstlane(q)) {
-        if (++spins > SPIN_MAX) {
+      // keep the scheduler from pulling a use of old[] between the atomics
+      __builtin_amdgcn_sched_barrier(0);
+  #pragma unroll
+      for (int c = 0; c < NK; c++)
+        app[c] = (old[c] >> 1) > (cd[c] >> 1) && !(old[c] & 1ull) && fkey_lat(cd[c]) < split;
+    };
+    __syncthreads();
+
+    for (;;) {
+      // ---- claim up to `claim` queued entries
+      const unsigned long long tc0 = (COUNT && diag) ? clock64() : 0;
+      uint32_t h = 0, k = 0;
+      if (lane == 0) {
+        for (;;) {
+          const unsigned long long w = __hip_atomic_load(&hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const uint32_t hh = (uint32_t)(w >> 32), t = ld(&ctl[TAIL]);
+          if (t == hh) break;
+          const uint32_t kk = min(claim, t - hh);
+          const unsigned long long nw = ((unsigned long long)(hh + kk) << 32) | ((w & 0xFFFFFFFFull) + 1);
+          if (atomicCAS(&hb, w, nw) == w) {
+            h = hh;
+            k = kk;
+            break;
+          }
+        }
+      }
+      h = __builtin_amdgcn_readfirstlane(h);
+      k = __builtin_amdgcn_readfirstlane(k);
+      if (!k) {
+        uint32_t q = 0;
+        if (lane == 0) {
+          const unsigned long long w = __hip_atomic_load(&hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (head, busy) before tail (see header)
+          q = (w & 0xFFFFFFFFull) == 0 && (uint32_t)(w >> 32) == ld(&ctl[TAIL]);
+        }
+        if (!__builtin_amdgcn_readfirstlane(q)) {
+          if (++spins > SPIN_MAX) {
+            gave_up = true;
+            break;
+          }
+          for (uint32_t z = 0; z < idle_sleep; z++) __builtin_amdgcn_s_sleep(8);  // ~512 cycles each
+          __builtin_amdgcn_s_sleep(2);
+          continue;
+        }
+        // ---- quiescent: every wave is here.  Next bucket, or done.
+        __syncthreads();
+        uint32_t m = LAT32_SAT;
+        for (uint32_t v = tid; v < n; v += NT) {
+          const uint64_t kv = key[v];
+          if (kv & 1ull) m = min(m, fkey_lat(kv));
+        }
+        for (int d = 32; d > 0; d >>= 1) m = min(m, (uint32_t)__shfl_xor(m, d));
+        if (lane == 0) red[wv] = m;
+        __syncthreads();
+        m = red[0];
+        for (int w = 1; w < NW; w++) m = min(m, red[w]);
+        if (m == LAT32_SAT) break;  // nothing dirty (saturated keys are never marked dirty)
+        if (++n_adv > max_adv) {
           gave_up = true;
           break;
         }
-        for (uint32_t z = 0; z < idle_sleep; z++) __builtin_amdgcn_s_sleep(8);  // ~512 cycles each
-        __builtin_amdgcn_s_sleep(2);
+        split = m + delta >= m ? min(m + delta, LAT32_SAT) : LAT32_SAT;
+        for (uint32_t v0 = wv * 64; v0 < n; v0 += NT) {  // queue the dirty nodes below split
+          const uint32_t v = v0 + lane;
+          uint64_t kv = v < n ? key[v] : 0ull;
+          const bool q2 = (kv & 1ull) && fkey_lat(kv) < split;
+          append_q<1>(&q2, &v, ring, &ctl[TAIL], slot_of, lane);
+        }
+        __syncthreads();
         continue;
       }
-      // ---- quiescent: every wave is here.  Next bucket, or done.
-      __syncthreads();
-      uint32_t m = LAT32_SAT;
-      for (uint32_t v = tid; v < n; v += NT) {
-        const uint64_t kv = key[v];
-        if (kv & 1ull) m = min(m, fkey_lat(kv));
+      if (COUNT) n_pops++;
+      const unsigned long long tc1 = (COUNT && diag) ? clock64() : 0;
+      // ---- pop the claimed entries (a slot claimed before its writer stored it reads EMPTY)
+      const bool on = lane < (int)k;
+      uint32_t u = 0, a0 = 0, a1 = 0;
+      uint64_t ku = 0;
+      bool stuck = false;
+      if (on) {
+        volatile uint16_t* slot = &ring[slot_of(h + lane)];
+        uint16_t x;
+        uint32_t sp = 0;
+        while ((x = *slot) == RING_EMPTY && ++sp < SPIN_MAX) __builtin_amdgcn_s_sleep(0);
+        stuck = x == RING_EMPTY;
+        *slot = RING_EMPTY;
+        u = stuck ? src : x;
+        a0 = off[u];
+        a1 = off[u + 1];
+        // clear the dirty flag; the returned key is the one to relax with (see header)
+        ku = __hip_atomic_fetch_and(&key[u], ~1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~1ull;
       }
-      for (int d = 32; d > 0; d >>= 1) m = min(m, (uint32_t)__shfl_xor(m, d));
-      if (lane == 0) red[wv] = m;
-      __syncthreads();
-      m = red[0];
-      for (int w = 1; w < NW; w++) m = min(m, red[w]);
-      if (m == LAT32_SAT) break;  // nothing dirty (saturated keys are never marked dirty)
-      if (++n_adv > max_adv) {
+      if (__any(stuck)) {
+        if (lane == 0) atomicSub(&hb, 1ull);
         gave_up = true;
         break;
       }
-      split = m + delta >= m ? min(m + delta, LAT32_SAT) : LAT32_SAT;
-      for (uint32_t v0 = wv * 64; v0 < n; v0 += NT) {  // queue the dirty nodes below split
-        const uint32_t v = v0 + lane;
-        uint64_t kv = v < n ? key[v] : 0ull;
-        const bool q2 = (kv & 1ull) && fkey_lat(kv) < split;
-        append_q<1>(&q2, &v, ring, &ctl[TAIL], slot_of, lane);
+      const uint32_t deg = a1 - a0;
+      const uint32_t dmax = __builtin_amdgcn_readlane(wave_incl_max(deg), 63);
+      const unsigned long long tc2 = (COUNT && diag) ? clock64() : 0;
+      if (dmax <= lane_deg_max) {
+        // ---- lane path: each lane walks its own node's arcs, LANE_ARCS loads in flight
+        if (COUNT) n_rel += __builtin_amdgcn_readlane(wave_incl_sum(deg), 63);
+        for (uint32_t j0 = 0; j0 < dmax; j0 += LA) {
+          uint32_t v[LA], lat[LA], om[LA];
+          bool valid[LA], app[LA];
+  #pragma unroll
+          for (int c = 0; c < LA; c++) {
+            valid[c] = j0 + c < deg;
+            const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid[c] ? (a0 + j0 + c) * 12u : 0x80000000u,
+                                                                0, 0);
+            v[c] = r[0];
+            lat[c] = r[1];
+            om[c] = r[2];
+          }
+          uint64_t cand[LA];
+  #pragma unroll
+          for (int c = 0; c < LA; c++) cand[c] = frelax(ku, lat[c], __uint_as_float(om[c]));
+          offer_all(std::integral_constant<int, LA>(), valid, v, cand, app);
+          append_q<LA>(app, v, ring, &ctl[TAIL], slot_of, lane);
+        }
+      } else {
+        // ---- expansion path (high out-degree): arcs of the 64 entries in consecutive slots
+        const uint32_t incl = wave_incl_sum(deg);
+        const uint32_t base = incl - deg;
+        const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+        if (COUNT) n_rel += T;
+        uint32_t carry = 0;  // 1 + the owner lane of the previous slot
+        for (uint32_t t0 = 0; t0 < T; t0 += 64 * SSSP_K) {
+          // owner lane of each slot: heads scatter 1 + their lane at their first slot, a max-scan fills the rest
+          if (deg && base >= t0 && base - t0 < 64u * SSSP_K) ow[base - t0] = (uint8_t)(lane + 1);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          uint32_t v[SSSP_K], lat[SSSP_K], om[SSSP_K], o[SSSP_K];
+          bool valid[SSSP_K], app[SSSP_K];
+  #pragma unroll
+          for (int c = 0; c < SSSP_K; c++) {
+            const uint32_t hd = ow[c * 64 + lane];
+            ow[c * 64 + lane] = 0;
+            const uint32_t mx = max(wave_incl_max(hd), carry);
+            carry = __builtin_amdgcn_readlane(mx, 63);
+            o[c] = mx - 1;
+          }
+  #pragma unroll
+          for (int c = 0; c < SSSP_K; c++) {
+            const uint32_t sl = t0 + c * 64 + lane;
+            valid[c] = sl < T;
+            const uint32_t a = __shfl(a0, (int)o[c]) + sl - __shfl(base, (int)o[c]);
+            const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid[c] ? a * 12u : 0x80000000u, 0, 0);
+            v[c] = r[0];
+            lat[c] = r[1];
+            om[c] = r[2];
+          }
+          uint64_t cand[SSSP_K];
+  #pragma unroll
+          for (int c = 0; c < SSSP_K; c++) {
+            const uint32_t klo = __shfl((uint32_t)ku, (int)o[c]), khi = __shfl((uint32_t)(ku >> 32), (int)o[c]);
+            cand[c] = frelax(((uint64_t)khi << 32) | klo, lat[c], __uint_as_float(om[c]));
+          }
+          offer_all(std::integral_constant<int, SSSP_K>(), valid, v, cand, app);
+          append_q<SSSP_K>(app, v, ring, &ctl[TAIL], slot_of, lane);
+        }
       }
-      __syncthreads();
-      continue;
-    }
-    if (COUNT) n_pops++;
-    const unsigned long long tc1 = (COUNT && diag) ? clock64() : 0;
-    // ---- pop the claimed entries (a slot claimed before its writer stored it reads EMPTY)
-    const bool on = lane < (int)k;
-    uint32_t u = 0, a0 = 0, a1 = 0;
-    uint64_t ku = 0;
-    bool stuck = false;
-    if (on) {
-      volatile uint16_t* slot = &ring[slot_of(h + lane)];
-      uint16_t x;
-      uint32_t sp = 0;
-      while ((x = *slot) == RING_EMPTY && ++sp < SPIN_MAX) __builtin_amdgcn_s_sleep(0);
-      stuck = x == RING_EMPTY;
-      *slot = RING_EMPTY;
-      u = stuck ? src : x;
-      a0 = off[u];
-      a1 = off[u + 1];
-      // clear the dirty flag; the returned key is the one to relax with (see header)
-      ku = __hip_atomic_fetch_and(&key[u], ~1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~1ull;
-    }
-    if (__any(stuck)) {
+      // release the claim after this wave's appends (LDS keeps a wave's operations in order)
       if (lane == 0) atomicSub(&hb, 1ull);
-      gave_up = true;
-      break;
-    }
-    const uint32_t deg = a1 - a0;
-    const uint32_t dmax = __builtin_amdgcn_readlane(wave_incl_max(deg), 63);
-    const unsigned long long tc2 = (COUNT && diag) ? clock64() : 0;
-    if (dmax <= lane_deg_max) {
-      // ---- lane path: each lane walks its own node's arcs, LANE_ARCS loads in flight
-      if (COUNT) n_rel += __builtin_amdgcn_readlane(wave_incl_sum(deg), 63);
-      for (uint32_t j0 = 0; j0 < dmax; j0 += LA) {
-        uint32_t v[LA], lat[LA], om[LA];
-        bool valid[LA], app[LA];
-#pragma unroll
-        for (int c = 0; c < LA; c++) {
-          valid[c] = j0 + c < deg;
-          const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid[c] ? (a0 + j0 + c) * 12u : 0x80000000u,
-                                                              0, 0);
-          v[c] = r[0];
-          lat[c] = r[1];
-          om[c] = r[2];
-        }
-        uint64_t cand[LA];
-#pragma unroll
-        for (int c = 0; c < LA; c++) cand[c] = frelax(ku, lat[c], __uint_as_float(om[c]));
-        offer_all(std::integral_constant<int, LA>(), valid, v, cand, app);
-        append_q<LA>(app, v, ring, &ctl[TAIL], slot_of, lane);
-      }
-    } else {
-      // ---- expansion path (high out-degree): arcs of the 64 entries in consecutive slots
-      const uint32_t incl = wave_incl_sum(deg);
-      const uint32_t base = incl - deg;
-      const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
-      if (COUNT) n_rel += T;
-      uint32_t carry = 0;  // 1 + the owner lane of the previous slot
-      for (uint32_t t0 = 0; t0 < T; t0 += 64 * SSSP_K) {
-        // owner lane of each slot: heads scatter 1 + their lane at their first slot, a max-scan fills the rest
-        if (deg && base >= t0 && base - t0 < 64u * SSSP_K) ow[base - t0] = (uint8_t)(lane + 1);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint32_t v[SSSP_K], lat[SSSP_K], om[SSSP_K], o[SSSP_K];
-        bool valid[SSSP_K], app[SSSP_K];
-#pragma unroll
-        for (int c = 0; c < SSSP_K; c++) {
-          const uint32_t hd = ow[c * 64 + lane];
-          ow[c * 64 + lane] = 0;
-          const uint32_t mx = max(wave_incl_max(hd), carry);
-          carry = __builtin_amdgcn_readlane(mx, 63);
-          o[c] = mx - 1;
-        }
-#pragma unroll
-        for (int c = 0; c < SSSP_K; c++) {
-          const uint32_t sl = t0 + c * 64 + lane;
-          valid[c] = sl < T;
-          const uint32_t a = __shfl(a0, (int)o[c]) + sl - __shfl(base, (int)o[c]);
-          const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid[c] ? a * 12u : 0x80000000u, 0, 0);
-          v[c] = r[0];
-          lat[c] = r[1];
-          om[c] = r[2];
-        }
-        uint64_t cand[SSSP_K];
-#pragma unroll
-        for (int c = 0; c < SSSP_K; c++) {
-          const uint32_t klo = __shfl((uint32_t)ku, (int)o[c]), khi = __shfl((uint32_t)(ku >> 32), (int)o[c]);
-          cand[c] = frelax(((uint64_t)khi << 32) | klo, lat[c], __uint_as_float(om[c]));
-        }
-        offer_all(std::integral_constant<int, SSSP_K>(), valid, v, cand, app);
-        append_q<SSSP_K>(app, v, ring, &ctl[TAIL], slot_of, lane);
+      if (COUNT && diag) {
+        const unsigned long long tc3 = clock64();
+        cyc_claim += tc1 - tc0;
+        cyc_pop += tc2 - tc1;
+        cyc_steps += tc3 - tc2;
       }
     }
-    // release the claim after this wave's appends (LDS keeps a wave's operations in order)
-    if (lane == 0) atomicSub(&hb, 1ull);
-    if (COUNT && diag) {
-      const unsigned long long tc3 = clock64();
-      cyc_claim += tc1 - tc0;
-      cyc_pop += tc2 - tc1;
-      cyc_steps += tc3 - tc2;
+    if (COUNT && lane == 0 && n_rel) atomicAdd(&work[bi & 63], (unsigned long long)n_rel);
+    if (COUNT && diag && bi < 4096 && lane == 0) {
+      if (n_rel) atomicAdd(&diag[bi * 8 + 4], (unsigned long long)n_rel);
+      if (n_pops) atomicAdd(&diag[bi * 8 + 2], (unsigned long long)n_pops);
+      atomicAdd(&diag[bi * 8 + 5], cyc_claim);
+      atomicAdd(&diag[bi * 8 + 6], cyc_pop);
+      atomicAdd(&diag[bi * 8 + 7], cyc_steps);
     }
-  }
-  if (COUNT && lane == 0 && n_rel) atomicAdd(&work[blockIdx.x & 63], (unsigned long long)n_rel);
-  if (COUNT && diag && blockIdx.x < 4096 && lane == 0) {
-    if (n_rel) atomicAdd(&diag[blockIdx.x * 8 + 4], (unsigned long long)n_rel);
-    if (n_pops) atomicAdd(&diag[blockIdx.x * 8 + 2], (unsigned long long)n_pops);
-    atomicAdd(&diag[blockIdx.x * 8 + 5], cyc_claim);
-    atomicAdd(&diag[blockIdx.x * 8 + 6], cyc_pop);
-    atomicAdd(&diag[blockIdx.x * 8 + 7], cyc_steps);
-  }
-  const unsigned long long c_search = dg ? clock64() : 0;
+    const unsigned long long c_search = dg ? clock64() : 0;
 
-  // ---- write the row: columns in used order, diagonal = the raw self-loop (graph/mod.rs:210-217)
-  const size_t orow = (size_t)(row - out_row0) * n_used;
-  bool sat = gave_up;
-  auto entry = [&](uint32_t j, uint64_t& l, float& f) {
-    if (j == row) {
-      const uint32_t e = self_edge[used[j]];
-      l = e_lat[e];
-      f = e_loss[e];
+    // ---- write the row: columns in used order, diagonal = the raw self-loop (graph/mod.rs:210-217)
+    const size_t orow = (size_t)(row - out_row0) * n_used;
+    bool sat = gave_up;
+    auto entry = [&](uint32_t j, uint64_t& l, float& f) {
+      if (j == row) {
+        const uint32_t e = self_edge[used[j]];
+        l = e_lat[e];
+        f = e_loss[e];
+      } else {
+        const uint64_t kk = key[used[j]];
+        sat |= fkey_lat(kk) == LAT32_SAT;
+        l = fkey_lat(kk);
+        f = __uint_as_float(fkey_loss_bits(kk));
+      }
+    };
+    if (vec_out) {  // n_used % 4 == 0, 16-B aligned rows: 16-B nontemporal stores
+      typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+      typedef float f32x4 __attribute__((ext_vector_type(4)));
+      for (uint32_t j = tid * 4; j < n_used; j += NT * 4) {
+        uint64_t l0, l1, l2, l3;
+        float f0, f1, f2, f3;
+        entry(j, l0, f0);
+        entry(j + 1, l1, f1);
+        entry(j + 2, l2, f2);
+        entry(j + 3, l3, f3);
+        __builtin_nontemporal_store((u64x2){l0, l1}, (u64x2*)&out_lat[orow + j]);
+        __builtin_nontemporal_store((u64x2){l2, l3}, (u64x2*)&out_lat[orow + j + 2]);
+        __builtin_nontemporal_store((f32x4){f0, f1, f2, f3}, (f32x4*)&out_loss[orow + j]);
+      }
     } else {
-      const uint64_t kk = key[used[j]];
-      sat |= fkey_lat(kk) == LAT32_SAT;
-      l = fkey_lat(kk);
-      f = __uint_as_float(fkey_loss_bits(kk));
+      for (uint32_t j = tid; j < n_used; j += NT) {
+        uint64_t l;
+        float f;
+        entry(j, l, f);
+        out_lat[orow + j] = l;
+        out_loss[orow + j] = f;
+      }
     }
-  };
-  if (vec_out) {  // n_used % 4 == 0, 16-B aligned rows: 16-B nontemporal stores
-    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-    typedef float f32x4 __attribute__((ext_vector_type(4)));
-    for (uint32_t j = tid * 4; j < n_used; j += NT * 4) {
-      uint64_t l0, l1, l2, l3;
-      float f0, f1, f2, f3;
-      entry(j, l0, f0);
-      entry(j + 1, l1, f1);
-      entry(j + 2, l2, f2);
-      entry(j + 3, l3, f3);
-      __builtin_nontemporal_store((u64x2){l0, l1}, (u64x2*)&out_lat[orow + j]);
-      __builtin_nontemporal_store((u64x2){l2, l3}, (u64x2*)&out_lat[orow + j + 2]);
-      __builtin_nontemporal_store((f32x4){f0, f1, f2, f3}, (f32x4*)&out_loss[orow + j]);
+    if (__any(sat) && lane == 0) sat_row[row - row_begin] = 1u;
+    if (dg) {
+      diag[bi * 8 + 0] = c_search - c_start;
+      diag[bi * 8 + 1] = clock64() - c_search;
+      diag[bi * 8 + 3] = n_adv | ((c_setup - c_start) << 24);  // bucket advances | setup cycles
     }
-  } else {
-    for (uint32_t j = tid; j < n_used; j += NT) {
-      uint64_t l;
-      float f;
-      entry(j, l, f);
-      out_lat[orow + j] = l;
-      out_loss[orow + j] = f;
-    }
-  }
-  if (__any(sat) && lane == 0) sat_row[row - row_begin] = 1u;
-  if (dg) {
-    diag[blockIdx.x * 8 + 0] = c_search - c_start;
-    diag[blockIdx.x * 8 + 1] = clock64() - c_search;
-    diag[blockIdx.x * 8 + 3] = n_adv | ((c_setup - c_start) << 24);  // bucket advances | setup cycles
+    __syncthreads();  // the next row reuses the LDS
   }
 }
 
@@ -615,12 +627,24 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
   const uint32_t lane_deg = ls && *ls ? (uint32_t)std::max(0, atoi(ls)) : 16u;
   const char* la = getenv("SG_SSSP_LANE_ARCS");
   const int la16 = la && atoi(la) == 16;
+  // One persistent workgroup per CU claims rows from a counter: out_off is
+  // staged once per CU instead of once per row, and no workgroup is launched and
+  // torn down per row.  C3: 3.92 -> 3.54 ms (same box).  SG_SSSP_PERSIST=0: a
+  // workgroup per row.
+  const char* ps = getenv("SG_SSSP_PERSIST");
+  const bool persist = !(ps && ps[0] == '0') && rows > (uint32_t)ctx->n_cu;
+  uint32_t* item_ctr = nullptr;
+  if (persist) {
+    item_ctr = ctx->r_items.get<uint32_t>(1);
+    SG_HIP(hipMemsetAsync(item_ctr, 0, 4, ctx->stream));
+  }
+  const uint32_t grid = persist ? (uint32_t)ctx->n_cu : rows;
   auto go = [&](auto kern) {
     SG_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)(LDS_PER_CU - SSSP_STATIC_LDS)));
-    hipLaunchKernelGGL(kern, dim3(rows), dim3(nt), lds, ctx->stream, out_off, out_arc, n, n_arcs, d_used, n_used,
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, ctx->stream, out_off, out_arc, n, n_arcs, d_used, n_used,
                        row_begin, row_begin, self_edge, e_lat, e_loss, out_lat, out_loss, sat_row, delta, vec, work,
-                       diag, claim, idle_sleep, lane_deg, blk_rows, ub_row, ub_w);
+                       diag, claim, idle_sleep, lane_deg, blk_rows, ub_row, ub_w, item_ctr, rows);
   };
   if (work) {
     if (nt == 512) go(k_sssp_lds<true, 512, 8, 0>);

@@ -140,6 +140,18 @@ def test_exact_seeds_with_ties(oracle, ctx, monkeypatch, directed, bounds):
     _check(oracle, g, np.arange(600, dtype=np.uint32), ctx)
 
 
+@pytest.mark.parametrize("persist", ["0", "1"])
+def test_lds_persistent_and_per_row_workgroups(oracle, ctx, monkeypatch, persist, apsp_kernel):
+    """More rows than CUs: the LDS search's persistent workgroups (the default, rows
+    claimed from a counter) and one workgroup per row (SG_SSSP_PERSIST=0) give the same
+    table; a search that gives up mid-row must not leave queue state to the next row."""
+    if apsp_kernel == "slab":
+        pytest.skip("LDS knob")
+    monkeypatch.setenv("SG_SSSP_PERSIST", persist)
+    g = synth.ring_chords_graph(900, 7.0, seed=31, directed=True)
+    _check(oracle, g, np.arange(900, dtype=np.uint32), ctx)
+
+
 def test_exact_seeds_next_to_wide_rows(oracle, ctx, monkeypatch):
     """Rows past 2^32 ns go to the wide kernel after the phases; a later row bounded by such a row
     must take bounds only from it (its 32-bit row is not final everywhere)."""
