@@ -270,18 +270,18 @@ __global__ void __launch_bounds__(NT)
         for (uint32_t j0 = tid; j0 < n_used; j0 += G * NT) {
           uint32_t vv[G];
           uint64_t m[G], ex[G];
-  #pragma unroll
+#pragma unroll
           for (int g = 0; g < G; g++) {
             const uint32_t j = j0 + g * NT;
             vv[g] = __builtin_amdgcn_raw_buffer_load_b32(ru, j < n_used ? j * 4u : OOB, 0, 0);
             m[g] = ex[g] = ~0ull;
           }
-  #pragma unroll 1
+#pragma unroll 1
           for (int k = 0; k < SSSP_KB; k += 2) {  // two bound rows' loads in flight together
             bool on[2], exact[2];
             uint32_t sr[2], w[2];
             __amdgpu_buffer_rsrc_t rl[2], rf[2];
-  #pragma unroll
+#pragma unroll
             for (int u = 0; u < 2; u++) {
               const uint32_t e = ub_row[(size_t)bi * SSSP_KB + k + u];
               on[u] = e != ~0u;
@@ -299,18 +299,18 @@ __global__ void __launch_bounds__(NT)
             if (!on[0] && !on[1]) continue;
             uint64_t l[2][G];
             uint32_t f[2][G];
-  #pragma unroll
+#pragma unroll
             for (int u = 0; u < 2; u++)
-  #pragma unroll
+#pragma unroll
               for (int g = 0; g < G; g++) {
                 const uint32_t j = j0 + g * NT;
                 const auto x = __builtin_amdgcn_raw_buffer_load_b64(rl[u], j < n_used ? j * 8u : OOB, 0, 0);
                 l[u][g] = ((uint64_t)x[1] << 32) | x[0];
                 f[u][g] = __builtin_amdgcn_raw_buffer_load_b32(rf[u], j < n_used ? j * 4u : OOB, 0, 0);
               }
-  #pragma unroll
+#pragma unroll
             for (int u = 0; u < 2; u++)
-  #pragma unroll
+#pragma unroll
               for (int g = 0; g < G; g++) {
                 const uint32_t j = j0 + g * NT;
                 const uint64_t ub = l[u][g] + w[u];  // w < 2^32: a wrap means >= 2^64
@@ -320,7 +320,7 @@ __global__ void __launch_bounds__(NT)
                   ex[g] = min(ex[g], (ub << 32) | ((uint64_t)f[u][g] << 1));
               }
           }
-  #pragma unroll
+#pragma unroll
           for (int g = 0; g < G; g++) {
             uint64_t kv = m[g] + 1 < LAT32_SAT ? ((m[g] + 1) << 32) | ((uint64_t)0x3F800000u << 1) : FKEY_INF;
             kv = min(kv, ex[g]);
@@ -360,7 +360,7 @@ __global__ void __launch_bounds__(NT)
     auto offer_all = [&](auto nk, const bool* valid, const uint32_t* v, const uint64_t* cand, bool* app) {
       constexpr int NK = decltype(nk)::value;
       uint64_t cd[NK], old[NK];
-  #pragma unroll
+#pragma unroll
       for (int c = 0; c < NK; c++) {
         const bool ok = valid[c] && fkey_lat(cand[c]) != LAT32_SAT;
         cd[c] = ok ? cand[c] : ~0ull;
@@ -369,7 +369,7 @@ __global__ void __launch_bounds__(NT)
       }
       // keep the scheduler from pulling a use of old[] between the atomics
       __builtin_amdgcn_sched_barrier(0);
-  #pragma unroll
+#pragma unroll
       for (int c = 0; c < NK; c++)
         app[c] = (old[c] >> 1) > (cd[c] >> 1) && !(old[c] & 1ull) && fkey_lat(cd[c]) < split;
     };
@@ -472,7 +472,7 @@ __global__ void __launch_bounds__(NT)
         for (uint32_t j0 = 0; j0 < dmax; j0 += LA) {
           uint32_t v[LA], lat[LA], om[LA];
           bool valid[LA], app[LA];
-  #pragma unroll
+#pragma unroll
           for (int c = 0; c < LA; c++) {
             valid[c] = j0 + c < deg;
             const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid[c] ? (a0 + j0 + c) * 12u : 0x80000000u,
@@ -482,7 +482,7 @@ __global__ void __launch_bounds__(NT)
             om[c] = r[2];
           }
           uint64_t cand[LA];
-  #pragma unroll
+#pragma unroll
           for (int c = 0; c < LA; c++) cand[c] = frelax(ku, lat[c], __uint_as_float(om[c]));
           offer_all(std::integral_constant<int, LA>(), valid, v, cand, app);
           append_q<LA>(app, v, ring, &ctl[TAIL], slot_of, lane);
@@ -502,7 +502,7 @@ __global__ void __launch_bounds__(NT)
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           uint32_t v[SSSP_K], lat[SSSP_K], om[SSSP_K], o[SSSP_K];
           bool valid[SSSP_K], app[SSSP_K];
-  #pragma unroll
+#pragma unroll
           for (int c = 0; c < SSSP_K; c++) {
             const uint32_t hd = ow[c * 64 + lane];
             ow[c * 64 + lane] = 0;
@@ -510,7 +510,7 @@ __global__ void __launch_bounds__(NT)
             carry = __builtin_amdgcn_readlane(mx, 63);
             o[c] = mx - 1;
           }
-  #pragma unroll
+#pragma unroll
           for (int c = 0; c < SSSP_K; c++) {
             const uint32_t sl = t0 + c * 64 + lane;
             valid[c] = sl < T;
@@ -521,7 +521,7 @@ __global__ void __launch_bounds__(NT)
             om[c] = r[2];
           }
           uint64_t cand[SSSP_K];
-  #pragma unroll
+#pragma unroll
           for (int c = 0; c < SSSP_K; c++) {
             const uint32_t klo = __shfl((uint32_t)ku, (int)o[c]), khi = __shfl((uint32_t)(ku >> 32), (int)o[c]);
             cand[c] = frelax(((uint64_t)khi << 32) | klo, lat[c], __uint_as_float(om[c]));
