@@ -318,6 +318,25 @@ def test_c3_full_table(c3_oracle, ctx):
     _check_full(g, used, olat, oloss, ctx)
 
 
+def test_c3_row_blocks(c3_oracle, ctx, apsp_kernel):
+    """The row blocks one rank builds in a sharded C3 build (bench.py at N = 2, 4, 8): their
+    own phase plans (3, 2 and no phases by rows per CU, bounds only from rows in the block),
+    every cell against the oracle's rows."""
+    import torch
+
+    if apsp_kernel == "slab":
+        pytest.skip("the slab kernel's row blocks are covered by test_row_shards_concatenate")
+    g, used, olat, oloss = c3_oracle
+    net = _graph(g, ctx)
+    n = len(used)
+    for r0, r1 in ((5000, 10000), (2500, 5000), (8750, 10000)):
+        dl = torch.empty((r1 - r0) * n, dtype=torch.int64, device="cuda")
+        df = torch.empty((r1 - r0) * n, dtype=torch.float32, device="cuda")
+        net.build_rows_device(used, r0, r1, dl.data_ptr(), df.data_ptr(), True)
+        assert np.array_equal(dl.cpu().numpy().view(np.uint64).reshape(r1 - r0, n), olat[r0:r1]), (r0, r1)
+        assert np.array_equal(df.cpu().numpy().view(np.uint32).reshape(r1 - r0, n), oloss[r0:r1].view(np.uint32))
+
+
 def _check_full(g, used, olat, oloss, ctx):
     import torch
 
