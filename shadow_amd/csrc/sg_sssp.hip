@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(NT)
                unsigned long long* __restrict__ diag, uint32_t claim, uint32_t idle_sleep,
                uint32_t lane_deg_max, const uint32_t* __restrict__ blk_rows,
                const uint32_t* __restrict__ ub_row, const uint32_t* __restrict__ ub_w,
-               uint32_t* __restrict__ item_ctr, uint32_t n_items) {
+               uint32_t* __restrict__ item_ctr, uint32_t n_items, uint32_t spin_max) {
   constexpr int NW = NT / 64;
   extern __shared__ __align__(16) unsigned char smem[];
   const uint32_t cap = sssp_ring_cap(n);
@@ -344,13 +344,24 @@ __global__ void __launch_bounds__(NT)
     // node, and a node is queued at most once per improvement); past it the row
     // is handed to the wide kernel instead of spinning
     const uint32_t max_adv = 4u * n + 64u;
-    bool gave_up = false;
     uint8_t* ow = own[wv];
     // spin budget per wave (sleeps of ~128 cycles): a safety valve against a
     // queue bug, never reached by a correct search; past it the wave leaves and
     // the row goes to the wide kernel
     uint32_t spins = 0;
-    constexpr uint32_t SPIN_MAX = 1u << 22;
+    // Giving up (the safety valves below, never reached by a correct search):
+    // the wave flags the row for the wide kernel, sets ctl[ABORT] and leaves the
+    // kernel; every other wave of the workgroup leaves too, at its next claim or
+    // after the quiescence barrier, so no wave waits at a barrier the others
+    // will not reach, and a persistent workgroup takes no further rows (the
+    // other workgroups claim them).
+    constexpr int ABORT = 2;
+    auto give_up = [&]() {
+      if (lane == 0) {
+        ctl[ABORT] = 1u;
+        sat_row[row - row_begin] = 1u;
+      }
+    };
     auto ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
     // relax NK candidates into key[v[c]]; app[c]: v[c] became dirty below split (to
     // be queued).  Branch-free, so the NK LDS atomics issue back to back and share
@@ -395,6 +406,7 @@ __global__ void __launch_bounds__(NT)
       }
       h = __builtin_amdgcn_readfirstlane(h);
       k = __builtin_amdgcn_readfirstlane(k);
+      if (__builtin_amdgcn_readfirstlane(ld(&ctl[ABORT]))) return;  // another wave gave up
       if (!k) {
         uint32_t q = 0;
         if (lane == 0) {
@@ -403,9 +415,9 @@ __global__ void __launch_bounds__(NT)
           q = (w & 0xFFFFFFFFull) == 0 && (uint32_t)(w >> 32) == ld(&ctl[TAIL]);
         }
         if (!__builtin_amdgcn_readfirstlane(q)) {
-          if (++spins > SPIN_MAX) {
-            gave_up = true;
-            break;
+          if (++spins > spin_max) {
+            give_up();
+            return;
           }
           for (uint32_t z = 0; z < idle_sleep; z++) __builtin_amdgcn_s_sleep(8);  // ~512 cycles each
           __builtin_amdgcn_s_sleep(2);
@@ -413,6 +425,7 @@ __global__ void __launch_bounds__(NT)
         }
         // ---- quiescent: every wave is here.  Next bucket, or done.
         __syncthreads();
+        if (ld(&ctl[ABORT])) return;  // a wave gave up before this barrier (uniform: no wave is spinning now)
         uint32_t m = LAT32_SAT;
         for (uint32_t v = tid; v < n; v += NT) {
           const uint64_t kv = key[v];
@@ -424,9 +437,9 @@ __global__ void __launch_bounds__(NT)
         m = red[0];
         for (int w = 1; w < NW; w++) m = min(m, red[w]);
         if (m == LAT32_SAT) break;  // nothing dirty (saturated keys are never marked dirty)
-        if (++n_adv > max_adv) {
-          gave_up = true;
-          break;
+        if (++n_adv > max_adv) {  // every wave is here together
+          give_up();
+          return;
         }
         split = m + delta >= m ? min(m + delta, LAT32_SAT) : LAT32_SAT;
         for (uint32_t v0 = wv * 64; v0 < n; v0 += NT) {  // queue the dirty nodes below split
@@ -449,7 +462,7 @@ __global__ void __launch_bounds__(NT)
         volatile uint16_t* slot = &ring[slot_of(h + lane)];
         uint16_t x;
         uint32_t sp = 0;
-        while ((x = *slot) == RING_EMPTY && ++sp < SPIN_MAX) __builtin_amdgcn_s_sleep(0);
+        while ((x = *slot) == RING_EMPTY && ++sp < spin_max) __builtin_amdgcn_s_sleep(0);
         stuck = x == RING_EMPTY;
         *slot = RING_EMPTY;
         u = stuck ? src : x;
@@ -459,9 +472,8 @@ __global__ void __launch_bounds__(NT)
         ku = __hip_atomic_fetch_and(&key[u], ~1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~1ull;
       }
       if (__any(stuck)) {
-        if (lane == 0) atomicSub(&hb, 1ull);
-        gave_up = true;
-        break;
+        give_up();
+        return;
       }
       const uint32_t deg = a1 - a0;
       const uint32_t dmax = __builtin_amdgcn_readlane(wave_incl_max(deg), 63);
@@ -551,7 +563,7 @@ __global__ void __launch_bounds__(NT)
 
     // ---- write the row: columns in used order, diagonal = the raw self-loop (graph/mod.rs:210-217)
     const size_t orow = (size_t)(row - out_row0) * n_used;
-    bool sat = gave_up;
+    bool sat = false;
     auto entry = [&](uint32_t j, uint64_t& l, float& f) {
       if (j == row) {
         const uint32_t e = self_edge[used[j]];
@@ -633,6 +645,11 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
   // workgroup per row.
   const char* ps = getenv("SG_SSSP_PERSIST");
   const bool persist = !(ps && ps[0] == '0') && rows > (uint32_t)ctx->n_cu;
+  // spin budget per wave (sleeps of ~128 cycles): a safety valve against a queue
+  // bug, never reached by a correct search; SG_SSSP_SPIN_MAX (tests) lowers it so
+  // that searches give up and their rows take the wide kernel
+  const char* sm = getenv("SG_SSSP_SPIN_MAX");
+  const uint32_t spin_max = sm && *sm ? (uint32_t)std::max(1, atoi(sm)) : (1u << 22);
   uint32_t* item_ctr = nullptr;
   if (persist) {
     item_ctr = ctx->r_items.get<uint32_t>(1);
@@ -644,7 +661,7 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
                                (int)(LDS_PER_CU - SSSP_STATIC_LDS)));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, ctx->stream, out_off, out_arc, n, n_arcs, d_used, n_used,
                        row_begin, row_begin, self_edge, e_lat, e_loss, out_lat, out_loss, sat_row, delta, vec, work,
-                       diag, claim, idle_sleep, lane_deg, blk_rows, ub_row, ub_w, item_ctr, rows);
+                       diag, claim, idle_sleep, lane_deg, blk_rows, ub_row, ub_w, item_ctr, rows, spin_max);
   };
   if (work) {
     if (nt == 512) go(k_sssp_lds<true, 512, 8, 0>);

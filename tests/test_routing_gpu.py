@@ -21,8 +21,8 @@ def apsp_kernel(request, monkeypatch):
     """Every routing test runs on both shortest-path kernels: the per-source
     LDS-resident search (sg_sssp.hip, the default up to ~10.9k nodes) and the
     batched-source slab relaxation (k_relax_w2, larger graphs).  lds_bounded
-    forces the LDS search's two phases (seed rows, then rows whose keys start
-    at a seed neighbour's bounds), which the default uses from 4,096 rows on."""
+    forces the LDS search's phases (seed rows, then rows whose keys start at a
+    seed neighbour's bounds), which the default uses from 8 rows per CU on."""
     monkeypatch.setenv("SG_APSP_LDS", "0" if request.param == "slab" else "1")
     monkeypatch.setenv("SG_SSSP_SEEDS", "2" if request.param == "lds_bounded" else "1")
     return "lds" if request.param.startswith("lds") else request.param
@@ -144,12 +144,27 @@ def test_exact_seeds_with_ties(oracle, ctx, monkeypatch, directed, bounds):
 def test_lds_persistent_and_per_row_workgroups(oracle, ctx, monkeypatch, persist, apsp_kernel):
     """More rows than CUs: the LDS search's persistent workgroups (the default, rows
     claimed from a counter) and one workgroup per row (SG_SSSP_PERSIST=0) give the same
-    table; a search that gives up mid-row must not leave queue state to the next row."""
+    table."""
     if apsp_kernel == "slab":
         pytest.skip("LDS knob")
     monkeypatch.setenv("SG_SSSP_PERSIST", persist)
     g = synth.ring_chords_graph(900, 7.0, seed=31, directed=True)
     _check(oracle, g, np.arange(900, dtype=np.uint32), ctx)
+
+
+@pytest.mark.parametrize("persist", ["0", "1"])
+@pytest.mark.parametrize("spin", ["1", "40"])
+def test_lds_give_up_takes_wide_kernel(oracle, ctx, monkeypatch, persist, spin, apsp_kernel):
+    """The LDS search's safety valve: with a spin budget of 1 or 40 idle polls (SG_SSSP_SPIN_MAX),
+    searches give up; the whole workgroup then leaves the kernel, the row is flagged, and the wide
+    kernel redoes it.  The table must still be exact, and a persistent workgroup that gave up must
+    not leave state behind for the rows other workgroups go on to claim."""
+    if apsp_kernel == "slab":
+        pytest.skip("LDS knob")
+    monkeypatch.setenv("SG_SSSP_PERSIST", persist)
+    monkeypatch.setenv("SG_SSSP_SPIN_MAX", spin)
+    g = synth.ring_chords_graph(700, 6.0, seed=33)
+    _check(oracle, g, np.arange(700, dtype=np.uint32), ctx)
 
 
 def test_exact_seeds_next_to_wide_rows(oracle, ctx, monkeypatch):
