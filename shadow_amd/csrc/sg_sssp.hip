@@ -426,6 +426,9 @@ __global__ void __launch_bounds__(NT)
         // ---- quiescent: every wave is here.  Next bucket, or done.
         __syncthreads();
         if (ld(&ctl[ABORT])) return;  // a wave gave up before this barrier (uniform: no wave is spinning now)
+        // one bucket (split = LAT32_SAT, the default): every node that became dirty was
+        // queued, so a quiescent queue means nothing is dirty -- no key scan needed
+        if (split >= LAT32_SAT) break;
         uint32_t m = LAT32_SAT;
         for (uint32_t v = tid; v < n; v += NT) {
           const uint64_t kv = key[v];
