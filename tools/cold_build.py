@@ -1,5 +1,10 @@
-import os, sys, time
-sys.path.insert(0, "/root/repo")
+"""First (cold) and later routing builds of the C3 graph on fresh NetworkGraphs: the cold build
+also builds the phase plan (SG_PLAN_DIAG=1 prints its steps).  python tools/cold_build.py"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from shadow_amd import Context, NetworkGraph, synth
 ctx = Context(0, stream=torch.cuda.current_stream().cuda_stream)
