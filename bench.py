@@ -85,6 +85,9 @@ def parse_args():
     p.add_argument("--no-codel", action="store_true", help="skip the router CoDel leg")
     p.add_argument("--no-gml", action="store_true", help="skip the GML ingest leg")
     p.add_argument("--no-c2", action="store_true", help="skip the C2 (1,200-node complete graph) leg")
+    p.add_argument("--no-compare", action="store_true",
+                   help="skip the comparison builds (slab kernel, one-launch unbounded search): for rocprof "
+                        "runs whose k_sssp_lds average must be the default plan's alone")
     p.add_argument("--no-pack", action="store_true",
                    help="deliver from the two-array table (no packed path-key copy)")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
@@ -622,7 +625,7 @@ def main():
     # the batched-source slab kernel on the same rows, for comparison (the default above 10.9k nodes)
     t_slab = None
     t_unbounded = None
-    if lds:
+    if lds and not a.no_compare:
         os.environ["SG_APSP_LDS"] = "0"
         t_slab = timed(D, build, max(1, a.steps // 2), 1)
         os.environ.pop("SG_APSP_LDS")
