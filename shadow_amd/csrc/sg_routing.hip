@@ -42,6 +42,7 @@
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -1175,7 +1176,8 @@ static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h
   const int kb = std::max(1, std::min(SSSP_KB_MAX, env_int("SG_SSSP_BOUNDS", 2)));
   // exact seeds need a column for every node (see sg_sssp.hip "Exact seeds")
   const bool exact = env_int("SG_SSSP_EXACT", 1) != 0 && n_used == net->n_nodes;
-  const int mode = (n_phase * 16 + kb) * 2 + exact;
+  const int hops = std::max(1, std::min(env_int("SG_SSSP_HOPS", 3), 4));
+  const int mode = ((n_phase * 16 + kb) * 2 + exact) * 8 + hops;
   for (auto& p : net->plans)
     if (p->mode == mode && p->row_begin == row_begin && p->row_end == row_end && p->used.size() == n_used &&
         std::equal(p->used.begin(), p->used.end(), h_used))
@@ -1276,41 +1278,78 @@ static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h
   p->row_begin = row_begin;
   p->row_end = row_end;
   std::vector<uint32_t> all;
-  // (arc latency, row | SSSP_UB_EXACT unless the arc is zero-loss): zero-loss
-  // arcs (exact seeds) rank first, then by latency
-  std::vector<std::pair<uint32_t, uint32_t>> cand;
-  auto rank = [](const std::pair<uint32_t, uint32_t>& a, const std::pair<uint32_t, uint32_t>& b) {
+  // Candidates are (latency, row | SSSP_UB_EXACT unless exact): exact seeds rank first,
+  // then by latency, then row.  Each row keeps its top kb distinct rows (each row's
+  // best-ranked candidate) by insertion, so no candidate list is built or sorted.
+  using Cand = std::pair<uint32_t, uint32_t>;
+  auto rank = [](const Cand& a, const Cand& b) {
     const uint32_t fa = a.second & SSSP_UB_EXACT, fb = b.second & SSSP_UB_EXACT;
     return fa != fb ? fa < fb : a < b;
   };
-  for (int ph = 0; ph < n_phase; ph++) {
-    std::vector<uint32_t> list, ubr, ubw;
-    for (uint32_t r = 0; r < rows; r++) {
-      if (phase[r] != ph) continue;
-      list.push_back(row_begin + r);
-      if (ph == 0) continue;
-      const uint32_t s = h_used[row_begin + r];
-      cand.clear();
-      for (uint32_t a = off[s]; a < off[s + 1]; a++) {
-        const uint32_t q = rel[head[a]];
-        if (q != ~0u && phase[q] < ph) cand.push_back({lat[a], (row_begin + q) | (exact && zl[a] ? 0u : SSSP_UB_EXACT)});
+  // bound rows of used node s in phase ph -> ubr/ubw[0, SSSP_KB_MAX)
+  auto bound_rows = [&](uint32_t s, int ph, uint32_t* ubr, uint32_t* ubw) {
+    Cand best[SSSP_KB_MAX];
+    int nb = 0;
+    auto offer = [&](uint32_t w, uint32_t rowf) {
+      const Cand c{w, rowf};
+      const uint32_t row_c = rowf & ~SSSP_UB_EXACT;
+      int i = 0;
+      while (i < nb && (best[i].second & ~SSSP_UB_EXACT) != row_c) i++;
+      if (i < nb) {  // this row is held: keep its better candidate
+        if (!rank(c, best[i])) return;
+      } else if (nb < kb) {
+        i = nb++;
+      } else {
+        if (!rank(c, best[nb - 1])) return;
+        i = nb - 1;
       }
-      std::sort(cand.begin(), cand.end(), rank);
-      int k = 0;
-      for (size_t c = 0; c < cand.size() && k < kb; c++) {  // distinct rows (parallel arcs: the first ranked)
-        const uint32_t row_c = cand[c].second & ~SSSP_UB_EXACT;
-        bool dup = false;
-        for (int i = 0; i < k; i++) dup |= (ubr[ubr.size() - k + i] & ~SSSP_UB_EXACT) == row_c;
-        if (dup) continue;
-        ubr.push_back(cand[c].second ^ SSSP_UB_EXACT);  // sorted with the flag inverted: exact first
-        ubw.push_back(cand[c].first);
-        k++;
-      }
-      for (; k < SSSP_KB_MAX; k++) {
-        ubr.push_back(~0u);
-        ubw.push_back(0u);
-      }
+      best[i] = c;
+      for (; i > 0 && rank(best[i], best[i - 1]); i--) std::swap(best[i], best[i - 1]);
+    };
+    for (uint32_t a = off[s]; a < off[s + 1]; a++) {
+      const uint32_t q = rel[head[a]];
+      if (q != ~0u && phase[q] < ph) offer(lat[a], (row_begin + q) | (exact && zl[a] ? 0u : SSSP_UB_EXACT));
     }
+    // a zero-loss path s -> x -> .. -> b of up to `hops` arcs also gives exact seeds from
+    // b's row (the prefix folds to loss 0 either way); a path already slower than the
+    // kb-th exact candidate cannot place (latencies only grow along it)
+    if (exact && hops > 1) {
+      auto walk = [&](auto&& self, uint32_t x, uint64_t w, int left) -> void {
+        for (uint32_t a2 = off[x]; a2 < off[x + 1]; a2++) {
+          if (!zl[a2] || head[a2] == s) continue;
+          const uint64_t w2 = w + lat[a2];
+          if (w2 >= LAT32_SAT) continue;
+          if (nb == kb && !(best[kb - 1].second & SSSP_UB_EXACT) && w2 > best[kb - 1].first) continue;
+          const uint32_t q2 = rel[head[a2]];
+          if (q2 != ~0u && phase[q2] < ph) offer((uint32_t)w2, row_begin + q2);
+          if (left > 1) self(self, head[a2], w2, left - 1);
+        }
+      };
+      for (uint32_t a = off[s]; a < off[s + 1]; a++)
+        if (zl[a] && head[a] != s) walk(walk, head[a], lat[a], hops - 1);
+    }
+    for (int k = 0; k < nb; k++) {
+      ubr[k] = best[k].second ^ SSSP_UB_EXACT;  // ranked with the flag inverted: exact first
+      ubw[k] = best[k].first;
+    }
+  };
+  // rows are independent: a few host threads share each phase's rows
+  const unsigned n_thr = std::max(1u, std::min<unsigned>(8u, std::thread::hardware_concurrency()));
+  for (int ph = 0; ph < n_phase; ph++) {
+    std::vector<uint32_t> list;
+    for (uint32_t r = 0; r < rows; r++)
+      if (phase[r] == ph) list.push_back(row_begin + r);
+    const size_t nl = ph ? list.size() : 0;
+    std::vector<uint32_t> ubr(nl * SSSP_KB_MAX, ~0u), ubw(nl * SSSP_KB_MAX, 0u);
+    auto fill = [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; i++)
+        bound_rows(h_used[list[i]], ph, &ubr[i * SSSP_KB_MAX], &ubw[i * SSSP_KB_MAX]);
+    };
+    const unsigned nt = nl >= 2048 ? n_thr : 1;
+    std::vector<std::thread> thr;
+    for (unsigned t = 1; t < nt; t++) thr.emplace_back(fill, nl * t / nt, nl * (t + 1) / nt);
+    fill(0, nl / nt);
+    for (auto& t : thr) t.join();
     sg_sssp_plan::Phase P;
     P.n = (uint32_t)list.size();
     P.rows = all.size();
