@@ -547,6 +547,14 @@ def main():
         # rows are independent units: each rank keeps its row shard (delivery reads only its own rows)
         net.build_rows_device(used, r0, r1, my_lat.data_ptr(), my_loss.data_ptr(), True)
 
+    def build_fresh():
+        # what a simulation pays for its one table (sim_config.rs:137-141): a new device graph
+        # (sg_net_create: upload, CSC/CSR), the phase plan (on the device) and the search,
+        # then the graph released (sg_net_destroy)
+        fresh = NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
+        fresh.build_rows_device(used, r0, r1, my_lat.data_ptr(), my_loss.data_ptr(), True)
+        fresh.close()
+
     def allgather():
         if D.coll_dev == "cpu":  # gloo rehearsal: host-staged
             for full, mine in ((full_lat, my_lat), (full_loss, my_loss)):
@@ -557,20 +565,23 @@ def main():
         D.dist.all_gather_into_tensor(full_lat, my_lat)
         D.dist.all_gather_into_tensor(full_loss, my_loss)
 
-    # the first build on a fresh graph also builds the cached phase plan (host: dominating sets,
-    # bound rows) -- what a simulation that builds its table once pays; the headline is warm
+    # the first build in the process also pays one-time HIP work (kernel loads, workspace)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    build()
+    build_fresh()
     torch.cuda.synchronize()
     t_cold = time.perf_counter() - t0
-    t_build = timed(D, build, a.steps, a.warmup)
+    # the headline: one-shot builds in a warm process, each on a fresh graph with its own plan
+    t_build = timed(D, build_fresh, a.steps, a.warmup)
+    # beside it: rebuilds on the same device graph (the plan is rebuilt too; nothing is cached)
+    t_warm = timed(D, build, a.steps, a.warmup)
     t_allgather = timed(D, allgather, max(1, a.steps // 2), 1) if D.dist else 0.0
     # instrumented build on the kernel's own stream: HIP-event launch times, then
     # (separately, the counting variant is slower) the relaxations performed
     ctx.enable_timers(True)
     build()
-    timers = {k: ctx.read_timer(k) for k in ("sssp", "sssp_bounded", "relax", "out", "relax_wide")}
+    timers = {k: ctx.read_timer(k) for k in ("sssp", "sssp_bounded", "relax", "out", "relax_wide", "plan_sets",
+                                             "plan_bounds")}
     ctx.enable_timers(True, count_work=True)
     build()
     works = {k: ctx.read_timer(k)[2] for k in ("sssp", "relax")}
@@ -726,6 +737,11 @@ def main():
         "apsp_detail": {"kernel": roofline["kernel"],
                         "slab_kernel_ms": round(t_slab * 1e3, 4) if t_slab else None,
                         "unbounded_one_launch_ms": round(t_unbounded * 1e3, 4) if t_unbounded else None,
+                        "value_is": "one-shot build: sg_net_create + plan + search + sg_net_destroy per step",
+                        "same_graph_rebuild_ms": round(t_warm * 1e3, 4),
+                        "plan_ms": round(timers["plan_sets"][0] + timers["plan_bounds"][0], 4),
+                        "plan_kernels_ms": {"plan_sets": round(timers["plan_sets"][0], 4),
+                                            "plan_bounds": round(timers["plan_bounds"][0], 4)},
                         "cold_build_ms": round(t_cold * 1e3, 4),
                         "out_kernel_ms": round(timers["out"][0], 4),
                         "wide_rows_ms": round(timers["relax_wide"][0], 4),

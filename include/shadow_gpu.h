@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 3
+#define SG_ABI_VERSION 4
 
 typedef enum sg_status {
   SG_OK = 0,
@@ -159,7 +159,7 @@ int32_t sg_routing_min_latency(sg_ctx* ctx, const uint64_t* d_latency_ns, size_t
  * from any number of threads; packet counters are atomic.                    */
 typedef struct sg_routing_info sg_routing_info;
 /* node_ids: the used GML node ids (the table's row / column order).  Allocates
- * the n_used^2 table (pinned when a HIP device is present).  SG_ERR_INVALID_ARG
+ * the n_used^2 table of 8-byte cells (pinned when a HIP device is present).  SG_ERR_INVALID_ARG
  * for a duplicate id. */
 int32_t sg_routing_info_create(uint32_t n_used, const uint32_t* node_ids, sg_routing_info** out);
 void sg_routing_info_destroy(sg_routing_info* ri);
@@ -170,18 +170,28 @@ void sg_routing_info_destroy(sg_routing_info* ri);
  * get_smallest_latency_ns. */
 int32_t sg_routing_info_fill(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32_t flags, sg_routing_info* ri);
 /* Rows [row_begin, row_end) from host arrays (e.g. row shards gathered from
- * other ranks' sg_routing_build). */
+ * other ranks' sg_routing_build).  get_smallest_latency_ns is Some once every row
+ * has been set (by fill or by these calls), over the whole table. */
 int32_t sg_routing_info_set_rows(sg_routing_info* ri, uint32_t row_begin, uint32_t row_end,
                                  const uint64_t* latency_ns, const float* packet_loss);
-/* Zero-copy view: cell (i, j) = path(node_ids[i] -> node_ids[j]). */
+/* Zero-copy view: cell (i, j) = path(node_ids[i] -> node_ids[j]) packed as
+ * (latency_ns << 32) | bits(packet_loss), 8 bytes, while the latency is below
+ * SG_CELL_WIDE; a cell whose upper half is SG_CELL_WIDE holds its loss bits only,
+ * and its u64 latency is one of the n_wide entries that sg_routing_info_rows and
+ * the lookups below resolve (paths of 4.29 s or more are rare: the whole table
+ * moves and lives at 8 bytes per cell instead of 12). */
+#define SG_CELL_WIDE 0xFFFFFFFFu
 typedef struct sg_routing_view {
   uint32_t n;
   const uint32_t* node_ids;
-  const uint64_t* latency_ns;
-  const float* packet_loss;
+  const uint64_t* cells;
+  uint64_t n_wide;
   uint32_t pinned;
 } sg_routing_view;
 int32_t sg_routing_info_view(const sg_routing_info* ri, sg_routing_view* out);
+/* Rows [row_begin, row_end) decoded into caller arrays (latency u64, loss f32, row-major). */
+int32_t sg_routing_info_rows(const sg_routing_info* ri, uint32_t row_begin, uint32_t row_end, uint64_t* latency_ns,
+                             float* packet_loss);
 /* Row of a GML node id (SG_ERR_INVALID_ARG if absent). */
 int32_t sg_routing_info_index(const sg_routing_info* ri, uint32_t node_id, uint32_t* row);
 /* RoutingInfo::path(start, end) (graph/mod.rs:448-450): 1 = Some (outputs

@@ -14,7 +14,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "shadow_gpu.h")
 
 # sg_status (include/shadow_gpu.h)
 SG_OK = 0
-SG_ABI_VERSION = 3  # include/shadow_gpu.h
+SG_ABI_VERSION = 4  # include/shadow_gpu.h
 SG_ERR_NO_EDGE = 1
 SG_ERR_MULTI_EDGE = 2
 SG_ERR_UNREACHABLE = 3
@@ -44,7 +44,7 @@ EXPORTED = [
     "sg_inbound_run", "sg_inbound_get_state", "sg_hosts_event_ctr", "sg_outbound_create", "sg_outbound_destroy",
     "sg_outbound_ring_cap", "sg_outbound_run", "sg_outbound_get_state",
     "sg_routing_info_create", "sg_routing_info_destroy", "sg_routing_info_fill", "sg_routing_info_set_rows",
-    "sg_routing_info_view", "sg_routing_info_index", "sg_routing_info_path", "sg_routing_info_smallest_latency",
+    "sg_routing_info_view", "sg_routing_info_rows", "sg_routing_info_index", "sg_routing_info_path", "sg_routing_info_smallest_latency",
     "sg_routing_info_increment_packet_count", "sg_routing_info_packet_count", "sg_routing_info_set_addresses",
     "sg_worker_get_latency", "sg_worker_get_reliability", "sg_worker_is_routable",
 ]
@@ -110,7 +110,7 @@ class sg_outbound_queue_state(C.Structure):
 
 
 class sg_routing_view(C.Structure):
-    _fields_ = [("n", C.c_uint32), ("node_ids", C.c_void_p), ("latency_ns", C.c_void_p), ("packet_loss", C.c_void_p),
+    _fields_ = [("n", C.c_uint32), ("node_ids", C.c_void_p), ("cells", C.c_void_p), ("n_wide", C.c_uint64),
                 ("pinned", C.c_uint32)]
 
 
@@ -185,6 +185,7 @@ def load(path: str | None = None):
         "sg_routing_info_fill": (i32, [vp, vp, vp, u32, vp]),
         "sg_routing_info_set_rows": (i32, [vp, u32, u32, vp, vp]),
         "sg_routing_info_view": (i32, [vp, C.POINTER(sg_routing_view)]),
+        "sg_routing_info_rows": (i32, [vp, u32, u32, vp, vp]),
         "sg_routing_info_index": (i32, [vp, u32, C.POINTER(C.c_uint32)]),
         "sg_routing_info_path": (i32, [vp, u32, u32, u64p, C.POINTER(C.c_float)]),
         "sg_routing_info_smallest_latency": (i32, [vp, u64p]),
@@ -230,9 +231,10 @@ def load(path: str | None = None):
         f.restype = res
         f.argtypes = args
     v = L.sg_abi_version()
-    # an older library given via SHADOW_GPU_LIB (A/B tools) is accepted: v1's
-    # sg_table lacks path_key, which such callers leave NULL
-    if v != SG_ABI_VERSION and not (path != LIB_PATH and v == 1):
+    # an older library given via SHADOW_GPU_LIB (A/B tools) is accepted for the calls
+    # it shares: v1's sg_table lacks path_key, which such callers leave NULL; v3's
+    # routing view held two arrays (the A/B tools build tables, they do not view them)
+    if v != SG_ABI_VERSION and not (path != LIB_PATH and 1 <= v < SG_ABI_VERSION):
         raise ShadowGpuUnavailable(f"ABI version mismatch: library {v}, bindings {SG_ABI_VERSION}")
     _lib = L
     return L

@@ -92,14 +92,14 @@ struct sg_ctx {
   uint32_t err_row = 0, err_col = 0;
   // routing workspace
   sg::DevBuf r_dist, r_dist2, r_flags, r_used, r_err, r_pair_cnt, r_pair_edge, r_map, r_out_lat,
-      r_out_loss, r_misc, r_dirty, r_work, r_items;
+      r_out_loss, r_misc, r_dirty, r_work, r_items, r_plan;
   // delivery workspace
   sg::DevBuf d_seg, d_dst, d_cnt, d_cur, d_keys, d_vals, d_keys2, d_vals2, d_keys3, d_keys4, d_misc,
       d_scan, d_lists, d_lists2, d_ctr0, d_blk, d_spill;
   sg::DevBuf m_scratch;
   // sg_routing_info_fill: double-buffered device row blocks, copied to the host
   // on copy_stream while the next block computes
-  sg::DevBuf r_stage_lat[2], r_stage_loss[2];
+  sg::DevBuf r_stage_lat[2], r_stage_loss[2], r_stage_pack[2];
   hipStream_t copy_stream = nullptr;
   bool in_fill = false;  // inside sg_routing_info_fill (selects the row-block kernel symbols)
   hipEvent_t stage_done[2] = {nullptr, nullptr}, stage_copied[2] = {nullptr, nullptr};
@@ -124,25 +124,6 @@ struct sg_ctx {
   bool count_work = false;  // SG_TIMERS_COUNT_WORK
   std::deque<std::pair<std::string, sg::KernelTimer>> timers;  // deque: stable addresses
   std::vector<hipEvent_t> event_pool;
-};
-
-// A phased plan for the LDS search over rows [row_begin, row_end) of a used
-// list (sg_routing.hip sssp_plan): phase 0 rows from infinity, then rows bounded
-// by out-neighbours finished in earlier phases.  Device arrays per phase: [rows]
-// [SSSP_KB_MAX bound rows per row][their arc latencies].
-struct sg_sssp_plan {
-  std::vector<uint32_t> used;
-  int mode = 0;  // the settings it was built for (phases, bounds per row)
-  uint32_t row_begin = 0, row_end = 0;
-  struct Phase {
-    uint32_t n = 0;                       // rows in the phase
-    size_t rows = 0, ub_row = 0, ub_w = 0;  // offsets into d (u32): row list, bound rows, bound latencies
-  };
-  std::vector<Phase> phases;
-  uint32_t* d = nullptr;
-  ~sg_sssp_plan() {
-    if (d) (void)hipFree(d);
-  }
 };
 
 // Device-resident network graph (sg_routing.hip builds it).
@@ -171,15 +152,9 @@ struct sg_net {
   // self-loops
   uint32_t* self_cnt = nullptr;
   uint32_t* self_edge = nullptr;
-  // host copy of the out-arc heads and latencies (for sssp plans), and the plans
-  std::vector<uint32_t> h_out_off, h_out_head, h_out_lat;
-  std::vector<uint8_t> h_out_zero_loss;  // arc loss == 0 exactly (bits(1f32 - loss) == 1.0f)
-  std::deque<std::unique_ptr<sg_sssp_plan>> plans;
+  void* mem = nullptr;  // one device allocation holding every array above
   ~sg_net() {
-    void* ps[] = {e_src, e_dst, e_lat, e_loss, in_off, in_src, in_dst, in_lat, in_lat32, in_om, in_rec, out_off,
-                  out_arc, self_cnt, self_edge};
-    for (void* p : ps)
-      if (p) (void)hipFree(p);
+    if (mem) (void)hipFree(mem);
   }
 };
 
@@ -187,9 +162,18 @@ struct sg_net {
 struct sg_routing_info {
   uint32_t n = 0;
   std::vector<uint32_t> node_ids;
-  uint64_t* lat = nullptr;  // n x n, pinned when a device was present at creation
-  float* loss = nullptr;
+  // n x n cells (latency << 32) | bits(loss), pinned when a device was present at
+  // creation; a cell whose latency half is SG_CELL_WIDE has its u64 latency in
+  // `wide` (sorted by cell index)
+  uint64_t* cell = nullptr;
   bool pinned = false;
+  struct Wide {
+    uint64_t cell;
+    uint64_t lat;
+  };
+  std::vector<Wide> wide;
+  std::vector<uint8_t> row_set;  // rows written (set_rows); all set -> filled
+  uint32_t rows_set = 0;
   bool filled = false;
   uint64_t min_lat = UINT64_MAX;
   // GML id -> row: dense window [id_base, id_base + id_span) or sorted (id, row) pairs
@@ -288,6 +272,23 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
                      const uint32_t* self_edge, const uint64_t* e_lat, const float* e_loss, uint64_t* out_lat,
                      float* out_loss, uint32_t* sat_row, uint32_t delta, unsigned long long* work,
                      unsigned long long* diag, const uint32_t* blk_rows = nullptr, uint32_t n_blk = 0,
-                     const uint32_t* ub_row = nullptr, const uint32_t* ub_w = nullptr);
+                     const uint32_t* ub_row = nullptr, const uint32_t* ub_w = nullptr,
+                     const uint32_t* plan_ctl = nullptr, int plan_ph = 0, uint32_t* plan_ctr = nullptr);
+
+// The LDS search's phase plan, built on the device (sg_plan.hip) on the context
+// stream: phase p's rows are list[ctl[2p] .. + ctl[2p + 1]) (absolute row indices),
+// their SSSP_KB_MAX bound rows and latencies at the same list positions of ub_row /
+// ub_w; ctr[2p .. 2p + 2) are the phase launch's claim counters (zeroed).
+struct SsspDevPlan {
+  int n_phase = 0;
+  uint32_t* list = nullptr;
+  uint32_t* ub_row = nullptr;
+  uint32_t* ub_w = nullptr;
+  uint32_t* ctl = nullptr;
+  uint32_t* ctr = nullptr;
+};
+constexpr int SSSP_PHASES_MAX = 6;
+SsspDevPlan sssp_device_plan(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin,
+                             uint32_t row_end, int n_phase, int kb, bool exact, int hops);
 
 }  // namespace sg

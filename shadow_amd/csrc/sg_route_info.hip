@@ -8,10 +8,13 @@
 // two per sent packet (WorkerShared::latency / reliability, worker.rs:517-531)
 // plus the legacy C TCP's worker_getLatency (worker.rs:651-661, tcp.c:448).
 //
-// Here the table is one row-major (latency u64, loss f32) array pair in pinned
-// host memory (the D2H target of sg_routing_info_fill, sg_routing.hip), keyed by
-// a GML-id -> row map and an address -> row map (IpAssignment::get_node,
-// graph/mod.rs:397-399), so a lookup is two array reads and no hashing.
+// Here the table is one row-major array of 8-byte cells (latency u32 << 32 |
+// bits(loss)) in pinned host memory (the D2H target of sg_routing_info_fill,
+// sg_routing.hip), keyed by a GML-id -> row map and an address -> row map
+// (IpAssignment::get_node, graph/mod.rs:397-399), so a lookup is two array reads
+// and no hashing.  A path of 2^32 - 1 ns (4.29 s) or more keeps its u64 latency
+// in a sorted side table (its cell says SG_CELL_WIDE); the reference's u64
+// latency is kept exactly either way.
 // Lookups are read-only; packet counters are atomic (the reference takes a
 // global RwLock write per packet, graph/mod.rs:453-460).
 #include <algorithm>
@@ -22,11 +25,9 @@
 
 sg_routing_info::~sg_routing_info() {
   if (pinned) {
-    if (lat) (void)hipHostFree(lat);
-    if (loss) (void)hipHostFree(loss);
+    if (cell) (void)hipHostFree(cell);
   } else {
-    free(lat);
-    free(loss);
+    free(cell);
   }
   free(counters.load());
 }
@@ -88,6 +89,23 @@ static inline uint32_t row_of_ip_be(const sg_routing_info* ri, uint32_t ip_be) {
   return map_get(__builtin_bswap32(ip_be), ri->ip_base, ri->ip_span, ri->ip_dense, ri->ip_sorted);
 }
 
+// cell c -> (latency, loss)
+static inline void cell_get(const sg_routing_info* ri, size_t c, uint64_t* lat, float* loss) {
+  const uint64_t x = ri->cell[c];
+  if (loss) {
+    const uint32_t b = (uint32_t)x;
+    memcpy(loss, &b, 4);
+  }
+  if (!lat) return;
+  if ((x >> 32) != SG_CELL_WIDE) {
+    *lat = x >> 32;
+    return;
+  }
+  auto it = std::lower_bound(ri->wide.begin(), ri->wide.end(), (uint64_t)c,
+                             [](const sg_routing_info::Wide& w, uint64_t k) { return w.cell < k; });
+  *lat = it != ri->wide.end() && it->cell == c ? it->lat : UINT64_MAX;
+}
+
 static void* host_alloc(size_t bytes, bool& pinned) {
   // pinned (the DMA target of sg_routing_info_fill) when a HIP device is present
   int count = 0;
@@ -121,18 +139,8 @@ int32_t sg_routing_info_create(uint32_t n_used, const uint32_t* node_ids, sg_rou
     sg::build_map(node_ids, rows.data(), n_used, ri->id_base, ri->id_span, ri->id_dense, ri->id_sorted,
                   "node id");
     const size_t cells = (size_t)n_used * n_used;
-    bool p1 = false, p2 = false;
-    ri->lat = (uint64_t*)sg::host_alloc(cells * 8, p1);
-    ri->loss = (float*)sg::host_alloc(cells * 4, p2);
-    ri->pinned = p1 && p2;
-    if (p1 != p2) {  // keep one allocator per object
-      ri->pinned = false;
-      if (p1) (void)hipHostFree(ri->lat);
-      if (p2) (void)hipHostFree(ri->loss);
-      ri->lat = (uint64_t*)aligned_alloc(64, (std::max<size_t>(cells * 8, 16) + 63) & ~(size_t)63);
-      ri->loss = (float*)aligned_alloc(64, (std::max<size_t>(cells * 4, 16) + 63) & ~(size_t)63);
-      if (!ri->lat || !ri->loss) throw std::bad_alloc();
-    }
+    ri->cell = (uint64_t*)sg::host_alloc(cells * 8, ri->pinned);
+    ri->row_set.assign(n_used, 0);
   } catch (const sg::Error& e) {
     delete ri;
     return e.code;
@@ -150,13 +158,42 @@ int32_t sg_routing_info_set_rows(sg_routing_info* ri, uint32_t row_begin, uint32
                                  const uint64_t* latency_ns, const float* packet_loss) {
   if (!ri || row_begin > row_end || row_end > ri->n) return SG_ERR_INVALID_ARG;
   if (row_end > row_begin && (!latency_ns || !packet_loss)) return SG_ERR_INVALID_ARG;
-  const size_t off = (size_t)row_begin * ri->n, cells = (size_t)(row_end - row_begin) * ri->n;
-  memcpy(ri->lat + off, latency_ns, cells * 8);
-  memcpy(ri->loss + off, packet_loss, cells * 4);
-  uint64_t m = ri->min_lat;
-  for (size_t i = 0; i < cells; i++) m = std::min(m, latency_ns[i]);
-  ri->min_lat = m;
-  ri->filled = true;
+  try {
+    const size_t off = (size_t)row_begin * ri->n, cells = (size_t)(row_end - row_begin) * ri->n;
+    // rows written again drop their old wide entries
+    auto lo = std::lower_bound(ri->wide.begin(), ri->wide.end(), (uint64_t)off,
+                               [](const sg_routing_info::Wide& w, uint64_t k) { return w.cell < k; });
+    auto hi = std::lower_bound(lo, ri->wide.end(), (uint64_t)(off + cells),
+                               [](const sg_routing_info::Wide& w, uint64_t k) { return w.cell < k; });
+    std::vector<sg_routing_info::Wide> add;
+    for (size_t i = 0; i < cells; i++) {
+      uint32_t b;
+      memcpy(&b, &packet_loss[i], 4);
+      const uint64_t l = latency_ns[i];
+      const uint32_t hi32 = l < SG_CELL_WIDE ? (uint32_t)l : SG_CELL_WIDE;
+      ri->cell[off + i] = ((uint64_t)hi32 << 32) | b;
+      if (hi32 == SG_CELL_WIDE) add.push_back({off + i, l});
+    }
+    const size_t at = lo - ri->wide.begin();
+    ri->wide.erase(lo, hi);
+    ri->wide.insert(ri->wide.begin() + at, add.begin(), add.end());
+    for (uint32_t r = row_begin; r < row_end; r++) ri->rows_set += !ri->row_set[r]++ ? 1u : 0u;
+    // get_smallest_latency_ns (graph/mod.rs:478-480) is over every entry: once the whole
+    // table is present, recompute it over the whole table (rows may have been rewritten)
+    if (ri->rows_set == ri->n) {
+      uint64_t m = UINT64_MAX;
+      const size_t all = (size_t)ri->n * ri->n;
+      for (size_t i = 0; i < all; i++) m = std::min(m, ri->cell[i] >> 32);
+      if (m == SG_CELL_WIDE) {  // every cell is wide: the smallest u64 latency of the side table
+        m = UINT64_MAX;
+        for (auto& w : ri->wide) m = std::min(m, w.lat);
+      }
+      ri->min_lat = m;
+      ri->filled = true;
+    }
+  } catch (...) {
+    return SG_ERR_OOM;
+  }
   return SG_OK;
 }
 
@@ -164,9 +201,26 @@ int32_t sg_routing_info_view(const sg_routing_info* ri, sg_routing_view* out) {
   if (!ri || !out) return SG_ERR_INVALID_ARG;
   out->n = ri->n;
   out->node_ids = ri->node_ids.data();
-  out->latency_ns = ri->lat;
-  out->packet_loss = ri->loss;
+  out->cells = ri->cell;
+  out->n_wide = ri->wide.size();
   out->pinned = ri->pinned ? 1 : 0;
+  return SG_OK;
+}
+
+int32_t sg_routing_info_rows(const sg_routing_info* ri, uint32_t row_begin, uint32_t row_end, uint64_t* latency_ns,
+                             float* packet_loss) {
+  if (!ri || row_begin > row_end || row_end > ri->n) return SG_ERR_INVALID_ARG;
+  if (row_end > row_begin && (!latency_ns || !packet_loss)) return SG_ERR_INVALID_ARG;
+  const size_t off = (size_t)row_begin * ri->n, cells = (size_t)(row_end - row_begin) * ri->n;
+  for (size_t i = 0; i < cells; i++) {
+    const uint64_t x = ri->cell[off + i];
+    latency_ns[i] = x >> 32;
+    const uint32_t b = (uint32_t)x;
+    memcpy(&packet_loss[i], &b, 4);
+  }
+  auto it = std::lower_bound(ri->wide.begin(), ri->wide.end(), (uint64_t)off,
+                             [](const sg_routing_info::Wide& w, uint64_t k) { return w.cell < k; });
+  for (; it != ri->wide.end() && it->cell < off + cells; ++it) latency_ns[it->cell - off] = it->lat;
   return SG_OK;
 }
 
@@ -183,9 +237,7 @@ int32_t sg_routing_info_path(const sg_routing_info* ri, uint32_t start, uint32_t
   if (!ri) return 0;
   const uint32_t i = sg::row_of(ri, start), j = sg::row_of(ri, end);
   if (i == ~0u || j == ~0u) return 0;  // None
-  const size_t c = (size_t)i * ri->n + j;
-  if (latency_ns) *latency_ns = ri->lat[c];
-  if (packet_loss) *packet_loss = ri->loss[c];
+  sg::cell_get(ri, (size_t)i * ri->n + j, latency_ns, packet_loss);
   return 1;
 }
 
@@ -248,7 +300,7 @@ int32_t sg_worker_get_latency(const sg_routing_info* ri, uint32_t src_be, uint32
   if (!ri || !latency_ns) return SG_ERR_INVALID_ARG;
   const uint32_t i = sg::row_of_ip_be(ri, src_be), j = sg::row_of_ip_be(ri, dst_be);
   if (i >= ri->n || j >= ri->n) return SG_ERR_INVALID_ARG;  // None (worker_getLatency unwraps: a panic)
-  *latency_ns = ri->lat[(size_t)i * ri->n + j];
+  sg::cell_get(ri, (size_t)i * ri->n + j, latency_ns, nullptr);
   return SG_OK;
 }
 
@@ -256,7 +308,9 @@ int32_t sg_worker_get_reliability(const sg_routing_info* ri, uint32_t src_be, ui
   if (!ri || !reliability) return SG_ERR_INVALID_ARG;
   const uint32_t i = sg::row_of_ip_be(ri, src_be), j = sg::row_of_ip_be(ri, dst_be);
   if (i >= ri->n || j >= ri->n) return SG_ERR_INVALID_ARG;
-  *reliability = 1.0f - ri->loss[(size_t)i * ri->n + j];  // one f32 subtraction (worker.rs:530)
+  float loss;
+  sg::cell_get(ri, (size_t)i * ri->n + j, nullptr, &loss);
+  *reliability = 1.0f - loss;  // one f32 subtraction (worker.rs:530)
   return SG_OK;
 }
 

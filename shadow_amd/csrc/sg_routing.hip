@@ -823,6 +823,60 @@ __global__ void __launch_bounds__(256) k_min_final(const unsigned long long* __r
   if (threadIdx.x == 0) *out = min(min(wm[0], wm[1]), min(wm[2], wm[3]));
 }
 
+// sg_routing_info_fill: a block of (latency u64, loss f32) cells -> the host
+// RoutingInfo's 8-byte cells (latency u32 << 32 | bits(loss); SG_CELL_WIDE in the
+// latency half when the path takes 2^32 - 1 ns or more), the block's smallest
+// latency (ctl[0], atomicMin) and its count of wide cells (ctl[1]).
+__global__ void __launch_bounds__(256) k_pack_cells(const uint64_t* __restrict__ lat, const float* __restrict__ loss,
+                                                    size_t cells, uint64_t* __restrict__ out,
+                                                    unsigned long long* __restrict__ ctl) {
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  unsigned long long m = ~0ull;
+  uint32_t nw = 0;
+  auto pack = [&](uint64_t l, float f) -> uint64_t {
+    m = min(m, (unsigned long long)l);
+    const uint32_t hi = l < SG_CELL_WIDE ? (uint32_t)l : SG_CELL_WIDE;
+    nw += hi == SG_CELL_WIDE;
+    return ((uint64_t)hi << 32) | __float_as_uint(f);
+  };
+  const size_t pairs = cells / 2, stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < pairs; i += stride) {
+    const u64x2 l = __builtin_nontemporal_load((const u64x2*)lat + i);
+    const f32x2 f = __builtin_nontemporal_load((const f32x2*)loss + i);
+    __builtin_nontemporal_store((u64x2){pack(l.x, f.x), pack(l.y, f.y)}, (u64x2*)out + i);
+  }
+  if ((cells & 1) && blockIdx.x == 0 && threadIdx.x == 0) out[cells - 1] = pack(lat[cells - 1], loss[cells - 1]);
+  for (int d = 32; d > 0; d >>= 1) {
+    m = min(m, (unsigned long long)__shfl_xor(m, d, 64));
+    nw += __shfl_xor(nw, d, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (m != ~0ull) atomicMin(&ctl[0], m);
+    if (nw) atomicAdd(&ctl[1], (unsigned long long)nw);
+  }
+}
+
+// the wide cells of a block: (cell index + off, u64 latency) pairs, in any order
+__global__ void k_wide_list(const uint64_t* __restrict__ lat, size_t cells, uint64_t off,
+                            unsigned long long* __restrict__ ctr, uint64_t* __restrict__ list) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells; i += stride)
+    if (lat[i] >= SG_CELL_WIDE) {
+      const unsigned long long k = atomicAdd(ctr, 1ull);
+      list[2 * k] = off + i;
+      list[2 * k + 1] = lat[i];
+    }
+}
+
+// Diagnostics only (SG_PLAN_WARM): keep every CU busy for `iters` dependent
+// VALU steps, to tell clock ramp-up from kernel cost in A/B runs.
+__global__ void k_busy(uint32_t iters, float* __restrict__ sink) {
+  float x = threadIdx.x * 1e-3f;
+  for (uint32_t i = 0; i < iters; i++) x = x * 0.999f + 1e-4f;
+  if (x == 12345.0f) sink[0] = x;
+}
+
 // ---------------------------------------------------------------------------
 // Host orchestration
 // ---------------------------------------------------------------------------
@@ -843,10 +897,15 @@ static T* dmalloc(size_t count) {
   return static_cast<T*>(p);
 }
 
+// A fresh network per simulation (the reference builds its graph once and computes
+// the table once, sim_config.rs:76-79, :137-141): one device allocation for every
+// array, the arc count from the host edge list (no device round trip), and no
+// stream synchronisation -- the build that follows orders after these launches.
 static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   const uint32_t n = g->n_nodes, m = g->n_edges;
   if (m && (!g->edge_src || !g->edge_dst || !g->edge_latency_ns || !g->edge_packet_loss))
     throw Error(SG_ERR_INVALID_ARG, "null edge array");
+  uint64_t n_self = 0;
   for (uint32_t e = 0; e < m; e++) {
     if (g->edge_src[e] >= n || g->edge_dst[e] >= n)
       throw Error(SG_ERR_INVALID_ARG, "edge " + std::to_string(e) + " endpoint out of range");
@@ -855,66 +914,80 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
       throw Error(SG_ERR_INVALID_ARG, "Edge 'packet_loss' is not in the range [0,1]");
     if (g->edge_latency_ns[e] == 0)  // graph/mod.rs:105-107
       throw Error(SG_ERR_INVALID_ARG, "Edge 'latency' must not be 0");
+    n_self += g->edge_src[e] == g->edge_dst[e];
   }
+  // arcs without self-loops, both directions when undirected (petgraph semantics, graph/mod.rs:137-152)
+  const uint64_t arcs = ((uint64_t)m - n_self) * (g->directed ? 1u : 2u);
+  if (arcs >= (1ull << 32)) throw Error(SG_ERR_INVALID_ARG, "too many arcs");
+  const uint32_t n_arcs = (uint32_t)arcs;
   net->ctx = ctx;
   net->n_nodes = n;
   net->n_edges = m;
+  net->n_arcs = n_arcs;
   net->directed = g->directed != 0;
   if (g->node_gml_id) net->gml_id.assign(g->node_gml_id, g->node_gml_id + n);
   hipStream_t st = ctx->stream;
-  net->e_src = dmalloc<uint32_t>(m);
-  net->e_dst = dmalloc<uint32_t>(m);
-  net->e_lat = dmalloc<uint64_t>(m);
-  net->e_loss = dmalloc<float>(m);
-  net->in_off = dmalloc<uint32_t>((size_t)n + 1);
-  net->self_cnt = dmalloc<uint32_t>(n);
-  net->self_edge = dmalloc<uint32_t>(n);
+  // one allocation, 256-B aligned sub-arrays
+  size_t total = 0;
+  auto carve = [&](size_t bytes) {
+    const size_t o = total;
+    total += (std::max<size_t>(bytes, 16) + 255) / 256 * 256;
+    return o;
+  };
+  const size_t o_esrc = carve(m * 4ull), o_edst = carve(m * 4ull), o_elat = carve(m * 8ull),
+               o_eloss = carve(m * 4ull), o_inoff = carve(((size_t)n + 1) * 4), o_scnt = carve((size_t)n * 4),
+               o_sedge = carve((size_t)n * 4), o_insrc = carve(n_arcs * 4ull), o_indst = carve(n_arcs * 4ull),
+               o_inlat = carve(n_arcs * 8ull), o_inlat32 = carve(n_arcs * 4ull), o_inom = carve(n_arcs * 4ull),
+               o_inrec = carve(n_arcs * 16ull), o_outoff = carve(((size_t)n + 1) * 4),
+               o_outarc = carve(n_arcs * 12ull);
+  SG_HIP(hipMalloc(&net->mem, total));
+  char* base = (char*)net->mem;
+  net->e_src = (uint32_t*)(base + o_esrc);
+  net->e_dst = (uint32_t*)(base + o_edst);
+  net->e_lat = (uint64_t*)(base + o_elat);
+  net->e_loss = (float*)(base + o_eloss);
+  net->in_off = (uint32_t*)(base + o_inoff);
+  net->self_cnt = (uint32_t*)(base + o_scnt);
+  net->self_edge = (uint32_t*)(base + o_sedge);
+  net->in_src = (uint32_t*)(base + o_insrc);
+  net->in_dst = (uint32_t*)(base + o_indst);
+  net->in_lat = (uint64_t*)(base + o_inlat);
+  net->in_lat32 = (uint32_t*)(base + o_inlat32);
+  net->in_om = (float*)(base + o_inom);
+  net->in_rec = (uint4*)(base + o_inrec);
+  net->out_off = (uint32_t*)(base + o_outoff);
+  net->out_arc = (uint32_t*)(base + o_outarc);
   if (m) {
     SG_HIP(hipMemcpyAsync(net->e_src, g->edge_src, m * 4ull, hipMemcpyHostToDevice, st));
     SG_HIP(hipMemcpyAsync(net->e_dst, g->edge_dst, m * 4ull, hipMemcpyHostToDevice, st));
     SG_HIP(hipMemcpyAsync(net->e_lat, g->edge_latency_ns, m * 8ull, hipMemcpyHostToDevice, st));
     SG_HIP(hipMemcpyAsync(net->e_loss, g->edge_packet_loss, m * 4ull, hipMemcpyHostToDevice, st));
   }
-  uint32_t* indeg = ctx->r_misc.get<uint32_t>((size_t)n + 1);
-  SG_HIP(hipMemsetAsync(indeg, 0, ((size_t)n + 1) * 4, st));
-  SG_HIP(hipMemsetAsync(net->self_cnt, 0, (size_t)n * 4, st));
-  SG_HIP(hipMemsetAsync(net->self_edge, 0, (size_t)n * 4, st));
+  uint32_t* indeg = ctx->r_misc.get<uint32_t>(2 * ((size_t)n + 1));
+  uint32_t* outdeg = indeg + n + 1;
+  SG_HIP(hipMemsetAsync(indeg, 0, 2 * ((size_t)n + 1) * 4, st));
+  SG_HIP(hipMemsetAsync(net->self_cnt, 0, (size_t)n * 4, st));  // (self_edge is read only where the count is 1)
   if (m) {
     hipLaunchKernelGGL(k_count_arcs, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src,
                        net->e_dst, m, (int)net->directed, indeg, net->self_cnt, net->self_edge);
+    hipLaunchKernelGGL(k_count_out, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst, m,
+                       (int)net->directed, outdeg);
     SG_CHECK_LAUNCH();
   }
   exclusive_scan_u32(ctx, indeg, net->in_off, n);
-  uint32_t n_arcs = 0;
-  copy_to_host(ctx, &n_arcs, net->in_off + n, 4);
-  net->n_arcs = n_arcs;
-  net->in_src = dmalloc<uint32_t>(n_arcs);
-  net->in_dst = dmalloc<uint32_t>(n_arcs);
-  net->in_lat = dmalloc<uint64_t>(n_arcs);
-  net->in_lat32 = dmalloc<uint32_t>(n_arcs);
-  net->in_om = dmalloc<float>(n_arcs);
-  net->in_rec = dmalloc<uint4>(n_arcs);
-  net->out_off = dmalloc<uint32_t>((size_t)n + 1);
-  net->out_arc = dmalloc<uint32_t>((size_t)n_arcs * 3);
+  exclusive_scan_u32(ctx, outdeg, net->out_off, n);
   if (n_arcs) {
-    uint32_t* cursor = ctx->r_map.get<uint32_t>((size_t)n + 1);
+    uint32_t* cursor = ctx->r_map.get<uint32_t>(2 * ((size_t)n + 1));
+    uint32_t* ocursor = cursor + n + 1;
     SG_HIP(hipMemcpyAsync(cursor, net->in_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
+    SG_HIP(hipMemcpyAsync(ocursor, net->out_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(k_scatter_arcs, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src,
                        net->e_dst, net->e_lat, net->e_loss, m, (int)net->directed, cursor,
                        net->in_src, net->in_dst, net->in_lat, net->in_lat32, net->in_om, net->in_rec);
-    SG_CHECK_LAUNCH();
-    SG_HIP(hipMemsetAsync(indeg, 0, ((size_t)n + 1) * 4, st));
-    hipLaunchKernelGGL(k_count_out, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst, m,
-                       (int)net->directed, indeg);
-    exclusive_scan_u32(ctx, indeg, net->out_off, n);
-    SG_HIP(hipMemcpyAsync(cursor, net->out_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(k_scatter_out, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst,
-                       net->e_lat, net->e_loss, m, (int)net->directed, cursor, net->out_arc);
+                       net->e_lat, net->e_loss, m, (int)net->directed, ocursor, net->out_arc);
     SG_CHECK_LAUNCH();
-  } else {
-    SG_HIP(hipMemsetAsync(net->out_off, 0, ((size_t)n + 1) * 4, st));
   }
-  SG_HIP(hipStreamSynchronize(st));
 }
 
 static void check_self_loops(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
@@ -1155,226 +1228,12 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 // 5.6 ms at 100 ms buckets and 6.2 ms at 50 ms), for 2.5x Dijkstra's
 // relaxations against 1.06x at 50 ms -- the search is bound by its critical
 // path, not by its relaxation count.
-// Phases and bounds for the LDS search (sg_sssp.hip "Bounds").  For an arc
-// s -> s' and any node v, w(s, s') + D[s'][v] is the latency of a real path, so
-// it bounds D[s][v] from above; a search whose keys start just above those
-// bounds rejects every slower candidate at its first atomic min (no queueing, no
-// pop) and reaches the same fixed point.  Phase 0 is a greedy dominating set of
-// the rows (row u is covered by a chosen v when u == v or u has an arc to v) and
-// runs from infinity; each later phase but the last is a dominating set of the
-// rows left; the last phase takes the rest.  A row of phase p >= 1 is bounded by
-// its SSSP_KB_MAX lowest-latency out-neighbours in phases < p (phase 0 dominates,
-// so it has one).  Each phase is one launch: a kernel boundary publishes the
-// rows the next phase reads.  Cached per (used list, range, settings).
-static const sg_sssp_plan* sssp_plan(sg_ctx* ctx, sg_net* net, const uint32_t* h_used, uint32_t n_used,
-                                     uint32_t row_begin, uint32_t row_end) {
-  // phases by rows per CU (one box, tools/sssp_ab.py --rows, C3 graph): 39 rows per CU
-  // (10k rows) 4 phases; 19.5 (a half) 3 phases, 2.25 against 2.57 ms unbounded;
-  // 9.8 (a quarter) 2 phases, 1.30 against 1.38 ms
-  const uint32_t per_cu = (row_end - row_begin) / std::max(1, ctx->n_cu);
-  const int n_phase = std::max(2, std::min(6, env_int("SG_SSSP_PHASES", per_cu >= 32 ? 4 : per_cu >= 16 ? 3 : 2)));
-  const int kb = std::max(1, std::min(SSSP_KB_MAX, env_int("SG_SSSP_BOUNDS", 2)));
-  // exact seeds need a column for every node (see sg_sssp.hip "Exact seeds")
-  const bool exact = env_int("SG_SSSP_EXACT", 1) != 0 && n_used == net->n_nodes;
-  const int hops = std::max(1, std::min(env_int("SG_SSSP_HOPS", 3), 4));
-  const int mode = ((n_phase * 16 + kb) * 2 + exact) * 8 + hops;
-  for (auto& p : net->plans)
-    if (p->mode == mode && p->row_begin == row_begin && p->row_end == row_end && p->used.size() == n_used &&
-        std::equal(p->used.begin(), p->used.end(), h_used))
-      return p.get();
-  const uint32_t n = net->n_nodes;
-  const auto plan_t0 = std::chrono::steady_clock::now();  // SG_PLAN_DIAG=1: construction time on stderr
-  const bool pdiag = env_int("SG_PLAN_DIAG", 0) != 0;
-  auto lap = [&](const char* what) {
-    if (pdiag)
-      fprintf(stderr, "[sssp]   plan %s at %.3f ms\n", what,
-              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - plan_t0).count());
-  };
-  if (net->h_out_off.empty()) {
-    std::vector<uint32_t> arc((size_t)net->n_arcs * 3);
-    net->h_out_off.resize((size_t)n + 1);
-    copy_to_host(ctx, net->h_out_off.data(), net->out_off, ((size_t)n + 1) * 4);
-    if (net->n_arcs) copy_to_host(ctx, arc.data(), net->out_arc, arc.size() * 4);
-    net->h_out_head.resize(net->n_arcs);
-    net->h_out_lat.resize(net->n_arcs);
-    net->h_out_zero_loss.resize(net->n_arcs);
-    for (size_t a = 0; a < net->n_arcs; a++) {
-      net->h_out_head[a] = arc[3 * a];
-      net->h_out_lat[a] = arc[3 * a + 1];
-      net->h_out_zero_loss[a] = arc[3 * a + 2] == 0x3F800000u;  // 1f32 - loss == 1.0
-    }
-  }
-  lap("arcs on host");
-  const uint32_t* off = net->h_out_off.data();
-  const uint32_t *head = net->h_out_head.data(), *lat = net->h_out_lat.data();
-  const uint8_t* zl = net->h_out_zero_loss.data();
-  const uint32_t rows = row_end - row_begin;
-  std::vector<uint32_t> rel(n, ~0u);  // node -> its row in range, relative
-  for (uint32_t r = 0; r < rows; r++) rel[h_used[row_begin + r]] = r;
-  // in-arcs among the rows: in_row[in_off[v] ..] = the rows u with an arc u -> v
-  std::vector<uint32_t> in_off(rows + 1, 0), in_row;
-  for (uint32_t r = 0; r < rows; r++) {
-    const uint32_t s = h_used[row_begin + r];
-    for (uint32_t a = off[s]; a < off[s + 1]; a++)
-      if (rel[head[a]] != ~0u) in_off[rel[head[a]] + 1]++;
-  }
-  for (uint32_t r = 0; r < rows; r++) in_off[r + 1] += in_off[r];
-  in_row.resize(in_off[rows]);
-  {
-    std::vector<uint32_t> cur(in_off.begin(), in_off.end() - 1);
-    for (uint32_t r = 0; r < rows; r++) {
-      const uint32_t s = h_used[row_begin + r];
-      for (uint32_t a = off[s]; a < off[s + 1]; a++)
-        if (rel[head[a]] != ~0u) in_row[cur[rel[head[a]]]++] = r;
-    }
-  }
-  lap("in-arc lists");
-  std::vector<int> phase(rows, -1);
-  for (int ph = 0; ph + 1 < n_phase; ph++) {
-    // greedy dominating set of the rows still unassigned (lazily re-scored max-heap)
-    std::vector<uint8_t> covered(rows, 0);
-    auto live = [&](uint32_t u) { return phase[u] < 0 && !covered[u]; };
-    auto gain = [&](uint32_t v) {
-      uint32_t g = live(v);
-      for (uint32_t k = in_off[v]; k < in_off[v + 1]; k++) g += live(in_row[k]);
-      return g;
-    };
-    // bucket queue by gain (gains only fall, so the top bucket only moves down);
-    // a popped row whose gain fell is re-filed: O(arcs) in all.  A binary heap
-    // took ~2 ms per phase at C3, half of a warm build.
-    std::vector<uint32_t> gn(rows, 0);
-    uint32_t top = 0;
-    for (uint32_t r = 0; r < rows; r++)
-      if (phase[r] < 0) top = std::max(top, gn[r] = gain(r));
-    std::vector<std::vector<uint32_t>> bucket(top + 1);
-    for (uint32_t r = rows; r-- > 0;)  // descending, so each bucket pops its lowest row first
-      if (phase[r] < 0 && gn[r]) bucket[gn[r]].push_back(r);
-    std::vector<uint32_t> chosen;
-    for (uint32_t g = top; g > 0;) {
-      if (bucket[g].empty()) {
-        g--;
-        continue;
-      }
-      const uint32_t v = bucket[g].back();
-      bucket[g].pop_back();
-      const uint32_t gv = gain(v);
-      if (gv == 0) continue;
-      if (gv < g) {
-        bucket[gv].push_back(v);
-        continue;
-      }
-      chosen.push_back(v);
-      covered[v] = 1;
-      for (uint32_t k = in_off[v]; k < in_off[v + 1]; k++) covered[in_row[k]] = 1;
-    }
-    for (uint32_t v : chosen) phase[v] = ph;
-    lap("dominating set");
-  }
-  for (uint32_t r = 0; r < rows; r++)
-    if (phase[r] < 0) phase[r] = n_phase - 1;
-  auto p = std::make_unique<sg_sssp_plan>();
-  p->used.assign(h_used, h_used + n_used);
-  p->mode = mode;
-  p->row_begin = row_begin;
-  p->row_end = row_end;
-  std::vector<uint32_t> all;
-  // Candidates are (latency, row | SSSP_UB_EXACT unless exact): exact seeds rank first,
-  // then by latency, then row.  Each row keeps its top kb distinct rows (each row's
-  // best-ranked candidate) by insertion, so no candidate list is built or sorted.
-  using Cand = std::pair<uint32_t, uint32_t>;
-  auto rank = [](const Cand& a, const Cand& b) {
-    const uint32_t fa = a.second & SSSP_UB_EXACT, fb = b.second & SSSP_UB_EXACT;
-    return fa != fb ? fa < fb : a < b;
-  };
-  // bound rows of used node s in phase ph -> ubr/ubw[0, SSSP_KB_MAX)
-  auto bound_rows = [&](uint32_t s, int ph, uint32_t* ubr, uint32_t* ubw) {
-    Cand best[SSSP_KB_MAX];
-    int nb = 0;
-    auto offer = [&](uint32_t w, uint32_t rowf) {
-      const Cand c{w, rowf};
-      const uint32_t row_c = rowf & ~SSSP_UB_EXACT;
-      int i = 0;
-      while (i < nb && (best[i].second & ~SSSP_UB_EXACT) != row_c) i++;
-      if (i < nb) {  // this row is held: keep its better candidate
-        if (!rank(c, best[i])) return;
-      } else if (nb < kb) {
-        i = nb++;
-      } else {
-        if (!rank(c, best[nb - 1])) return;
-        i = nb - 1;
-      }
-      best[i] = c;
-      for (; i > 0 && rank(best[i], best[i - 1]); i--) std::swap(best[i], best[i - 1]);
-    };
-    for (uint32_t a = off[s]; a < off[s + 1]; a++) {
-      const uint32_t q = rel[head[a]];
-      if (q != ~0u && phase[q] < ph) offer(lat[a], (row_begin + q) | (exact && zl[a] ? 0u : SSSP_UB_EXACT));
-    }
-    // a zero-loss path s -> x -> .. -> b of up to `hops` arcs also gives exact seeds from
-    // b's row (the prefix folds to loss 0 either way); a path already slower than the
-    // kb-th exact candidate cannot place (latencies only grow along it)
-    if (exact && hops > 1) {
-      auto walk = [&](auto&& self, uint32_t x, uint64_t w, int left) -> void {
-        for (uint32_t a2 = off[x]; a2 < off[x + 1]; a2++) {
-          if (!zl[a2] || head[a2] == s) continue;
-          const uint64_t w2 = w + lat[a2];
-          if (w2 >= LAT32_SAT) continue;
-          if (nb == kb && !(best[kb - 1].second & SSSP_UB_EXACT) && w2 > best[kb - 1].first) continue;
-          const uint32_t q2 = rel[head[a2]];
-          if (q2 != ~0u && phase[q2] < ph) offer((uint32_t)w2, row_begin + q2);
-          if (left > 1) self(self, head[a2], w2, left - 1);
-        }
-      };
-      for (uint32_t a = off[s]; a < off[s + 1]; a++)
-        if (zl[a] && head[a] != s) walk(walk, head[a], lat[a], hops - 1);
-    }
-    for (int k = 0; k < nb; k++) {
-      ubr[k] = best[k].second ^ SSSP_UB_EXACT;  // ranked with the flag inverted: exact first
-      ubw[k] = best[k].first;
-    }
-  };
-  // rows are independent: a few host threads share each phase's rows
-  const unsigned n_thr = std::max(1u, std::min<unsigned>(8u, std::thread::hardware_concurrency()));
-  for (int ph = 0; ph < n_phase; ph++) {
-    std::vector<uint32_t> list;
-    for (uint32_t r = 0; r < rows; r++)
-      if (phase[r] == ph) list.push_back(row_begin + r);
-    const size_t nl = ph ? list.size() : 0;
-    std::vector<uint32_t> ubr(nl * SSSP_KB_MAX, ~0u), ubw(nl * SSSP_KB_MAX, 0u);
-    auto fill = [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; i++)
-        bound_rows(h_used[list[i]], ph, &ubr[i * SSSP_KB_MAX], &ubw[i * SSSP_KB_MAX]);
-    };
-    const unsigned nt = nl >= 2048 ? n_thr : 1;
-    std::vector<std::thread> thr;
-    for (unsigned t = 1; t < nt; t++) thr.emplace_back(fill, nl * t / nt, nl * (t + 1) / nt);
-    fill(0, nl / nt);
-    for (auto& t : thr) t.join();
-    sg_sssp_plan::Phase P;
-    P.n = (uint32_t)list.size();
-    P.rows = all.size();
-    all.insert(all.end(), list.begin(), list.end());
-    P.ub_row = all.size();
-    all.insert(all.end(), ubr.begin(), ubr.end());
-    P.ub_w = all.size();
-    all.insert(all.end(), ubw.begin(), ubw.end());
-    if (P.n) p->phases.push_back(P);
-  }
-  lap("bound rows");
-  SG_HIP(hipMalloc(&p->d, std::max<size_t>(all.size() * 4, 16)));
-  lap("hipMalloc");
-  SG_HIP(hipMemcpyAsync(p->d, all.data(), all.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
-  if (env_int("SG_PLAN_DIAG", 0))
-    fprintf(stderr, "[sssp] plan for %u rows, %zu phases: %.3f ms\n", rows, p->phases.size(),
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - plan_t0).count());
-  net->plans.push_front(std::move(p));
-  if (net->plans.size() > 16) net->plans.pop_back();
-  return net->plans.front().get();
-}
-
-static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, const uint32_t* h_used,
-                               uint32_t n_used, uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
+// Phases and bounds for the LDS search (sg_sssp.hip "Bounds", sg_plan.hip): phase
+// 0 runs from infinity, a row of phase p >= 1 starts from bounds (and exact seeds)
+// taken from neighbour rows of earlier phases; each phase is one launch, so a
+// kernel boundary publishes the rows the next phase reads.  The plan is built on
+// the device for every build (sg_plan.hip), so a one-shot build pays it.
+static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
                                float* out_loss) {
   hipStream_t st = ctx->stream;
   const uint32_t rows = row_end - row_begin;
@@ -1390,22 +1249,33 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   const uint32_t n_diag = std::min<uint32_t>(rows, 4096);
   unsigned long long* diag = diag_on ? ctx->r_misc.get<unsigned long long>((size_t)n_diag * 8) : nullptr;
   if (diag) SG_HIP(hipMemsetAsync(diag, 0, (size_t)n_diag * 64, st));
-  // Phases (sssp_plan) from 8 rows per CU: with fewer, the phase boundaries cost
+  // Phases (sg_plan.hip) from 8 rows per CU: with fewer, the phase boundaries cost
   // more than the bounds save (tools/sssp_ab.py, C3 graph: 1,250 rows 0.78 against
   // 0.76 ms unbounded, a 2,000-node build 0.45 against 0.43; 2,500 rows 1.30
   // against 1.38, a 4,000-node build 0.97 against 1.07).  SG_SSSP_SEEDS=0 never, =2 always.
   const int seeds_env = env_int("SG_SSSP_SEEDS", 1);
-  const bool two_phase = h_used && seeds_env != 0 && (seeds_env == 2 || rows >= 8u * (uint32_t)ctx->n_cu);
-  const sg_sssp_plan* plan = two_phase ? sssp_plan(ctx, net, h_used, n_used, row_begin, row_end) : nullptr;
-  if (plan && plan->phases.size() > 1) {
-    for (size_t ph = 0; ph < plan->phases.size(); ph++) {
-      const auto& P = plan->phases[ph];
+  const bool phased = seeds_env != 0 && (seeds_env == 2 || rows >= 8u * (uint32_t)ctx->n_cu);
+  if (phased) {
+    // phases by rows per CU (one box, tools/sssp_ab.py --rows, C3 graph): 39 rows per CU
+    // (10k rows) 4 phases; 19.5 (a half) 3 phases, 2.25 against 2.57 ms unbounded;
+    // 9.8 (a quarter) 2 phases, 1.30 against 1.38 ms
+    const uint32_t per_cu = rows / std::max(1, ctx->n_cu);
+    const int n_phase = std::max(2, std::min(SSSP_PHASES_MAX,
+                                             env_int("SG_SSSP_PHASES", per_cu >= 32 ? 4 : per_cu >= 16 ? 3 : 2)));
+    const int kb = std::max(1, std::min(SSSP_KB_MAX, env_int("SG_SSSP_BOUNDS", 2)));
+    // exact seeds need a column for every node (see sg_sssp.hip "Exact seeds")
+    const bool exact = env_int("SG_SSSP_EXACT", 1) != 0 && n_used == net->n_nodes;
+    const int hops = std::max(1, std::min(env_int("SG_SSSP_HOPS", 3), 3));
+    const SsspDevPlan plan = sssp_device_plan(ctx, net, d_used, n_used, row_begin, row_end, n_phase, kb, exact, hops);
+    if (const int warm = env_int("SG_PLAN_WARM", 0))
+      hipLaunchKernelGGL(k_busy, dim3(4 * ctx->n_cu), dim3(256), 0, ctx->stream, (uint32_t)warm, (float*)nullptr);
+    for (int ph = 0; ph < plan.n_phase; ph++) {
       const bool bounded = ph > 0;
       TimedLaunch tl(ctx, bounded ? "sssp_bounded" : "sssp", 0.0);
       launch_sssp_lds(ctx, net->out_off, net->out_arc, net->n_nodes, net->n_arcs, d_used, n_used, row_begin,
                       row_end, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work,
-                      ph + 1 == plan->phases.size() ? diag : nullptr, plan->d + P.rows, P.n,
-                      bounded ? plan->d + P.ub_row : nullptr, bounded ? plan->d + P.ub_w : nullptr);
+                      ph + 1 == plan.n_phase ? diag : nullptr, plan.list, rows, bounded ? plan.ub_row : nullptr,
+                      bounded ? plan.ub_w : nullptr, plan.ctl, ph, plan.ctr + 2 * ph);
     }
   } else {
     TimedLaunch tl(ctx, "sssp", 0.0);
@@ -1455,7 +1325,7 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, con
   const bool sparse = net->n_nodes && net->n_arcs <= 64ull * net->n_nodes;
   if (env_int("SG_APSP_LDS", 1) != 0 && sparse && sssp_lds_fits(net->n_nodes) &&
       (uint64_t)net->n_arcs * 12 < (1ull << 31)) {
-    shortest_paths_lds(ctx, net, d_used, h_used, n_used, row_begin, row_end, out_lat, out_loss);
+    shortest_paths_lds(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss);
     return;
   }
   const bool front = env_int("SG_APSP_FRONTIER", 1) != 0;
@@ -1619,8 +1489,9 @@ int32_t sg_routing_build(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32
 }
 
 // The whole table into a host RoutingInfo (sg_route_info.hip): row blocks are
-// built into one of two device staging buffers and copied to the object's
-// pinned host arrays on a second stream while the next block builds.
+// built into one of two device staging buffers, packed into 8-byte cells and
+// copied to the object's pinned host array on a second stream while the next
+// block builds.  The copy (8 bytes per cell over PCIe) is what binds.
 int32_t sg_routing_info_fill(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32_t flags, sg_routing_info* ri) {
   return sg::guarded(ctx, [&] {
     using namespace sg;
@@ -1637,15 +1508,14 @@ int32_t sg_routing_info_fill(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, ui
     }
     ri->filled = false;
     ri->min_lat = UINT64_MAX;
+    ri->wide.clear();
+    std::fill(ri->row_set.begin(), ri->row_set.end(), 0);
+    ri->rows_set = 0;
     if (n_used == 0) {
       ri->filled = true;
       return;
     }
     hipStream_t st = ctx->stream;
-    uint32_t* d_used = ctx->r_used.get<uint32_t>(n_used);
-    SG_HIP(hipMemcpyAsync(d_used, nodes, (size_t)n_used * 4, hipMemcpyHostToDevice, st));
-    const bool shortest = flags & SG_ROUTE_SHORTEST_PATH;
-    if (shortest) check_self_loops(ctx, net, d_used, n_used, nodes);
     if (!ctx->copy_stream) {
       SG_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
       for (int b = 0; b < 2; b++) {
@@ -1653,51 +1523,76 @@ int32_t sg_routing_info_fill(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, ui
         SG_HIP(hipEventCreateWithFlags(&ctx->stage_copied[b], hipEventDisableTiming));
       }
     }
+    // an earlier fill that failed may have left copies in flight into its staging buffers
+    SG_HIP(hipStreamSynchronize(ctx->copy_stream));
+    uint32_t* d_used = ctx->r_used.get<uint32_t>(n_used);
+    SG_HIP(hipMemcpyAsync(d_used, nodes, (size_t)n_used * 4, hipMemcpyHostToDevice, st));
+    const bool shortest = flags & SG_ROUTE_SHORTEST_PATH;
+    if (shortest) check_self_loops(ctx, net, d_used, n_used, nodes);
     // blocks of about 1/8 of the table (at least 64 rows, whole 64-row batches)
     uint32_t rows = (uint32_t)std::max(64, env_int("SG_RI_BLOCK_ROWS", (int)((n_used + 7) / 8)));
     rows = std::min(n_used, (rows + 63) / 64 * 64);
     uint64_t* slat[2];
     float* sloss[2];
+    uint64_t* spack[2];
     for (int b = 0; b < 2; b++) {
       slat[b] = ctx->r_stage_lat[b].get<uint64_t>((size_t)rows * n_used);
       sloss[b] = ctx->r_stage_loss[b].get<float>((size_t)rows * n_used);
+      spack[b] = ctx->r_stage_pack[b].get<uint64_t>((size_t)rows * n_used);
     }
-    const unsigned nbm = grid_for((size_t)rows * n_used, 256, 2048);
+    const unsigned nbp = grid_for((size_t)rows * n_used / 2, 256, 4096);
     uint64_t m = UINT64_MAX;
     int k = 0;
-    for (uint32_t r0 = 0; r0 < n_used; r0 += rows, k++) {
-      const uint32_t r1 = std::min(n_used, r0 + rows), b = k & 1;
-      if (k >= 2) SG_HIP(hipStreamWaitEvent(st, ctx->stage_copied[b], 0));  // block k - 2 left this buffer
-      ctx->in_fill = true;
-      try {
-        if (shortest)
-          shortest_paths(ctx, net, d_used, nodes, n_used, r0, r1, slat[b], sloss[b]);
-        else
-          direct_paths(ctx, net, d_used, nodes, n_used, r0, r1, slat[b], sloss[b]);
-      } catch (...) {
+    try {
+      for (uint32_t r0 = 0; r0 < n_used; r0 += rows, k++) {
+        const uint32_t r1 = std::min(n_used, r0 + rows), b = k & 1;
+        ctx->in_fill = true;
+        try {
+          if (shortest)
+            shortest_paths(ctx, net, d_used, nodes, n_used, r0, r1, slat[b], sloss[b]);
+          else
+            direct_paths(ctx, net, d_used, nodes, n_used, r0, r1, slat[b], sloss[b]);
+        } catch (...) {
+          ctx->in_fill = false;
+          throw;
+        }
         ctx->in_fill = false;
-        throw;
+        const size_t cells = (size_t)(r1 - r0) * n_used;
+        // (workspace fetched after the build, which may grow these buffers)
+        unsigned long long* ctl = ctx->r_err.get<unsigned long long>(4);
+        SG_HIP(hipMemsetAsync(ctl, 0xff, 8, st));
+        SG_HIP(hipMemsetAsync(ctl + 1, 0, 8, st));
+        if (k >= 2) SG_HIP(hipStreamWaitEvent(st, ctx->stage_copied[b], 0));  // block k - 2 left spack[b]
+        hipLaunchKernelGGL(k_pack_cells, dim3(nbp), dim3(256), 0, st, slat[b], sloss[b], cells, spack[b], ctl);
+        SG_CHECK_LAUNCH();
+        SG_HIP(hipEventRecord(ctx->stage_done[b], st));
+        SG_HIP(hipStreamWaitEvent(ctx->copy_stream, ctx->stage_done[b], 0));
+        SG_HIP(hipMemcpyAsync(ri->cell + (size_t)r0 * n_used, spack[b], cells * 8, hipMemcpyDeviceToHost,
+                              ctx->copy_stream));
+        SG_HIP(hipEventRecord(ctx->stage_copied[b], ctx->copy_stream));
+        unsigned long long h[2] = {0, 0};
+        copy_to_host(ctx, h, ctl, 16);  // (the next block's build starts after this sync; the copy runs on)
+        m = std::min<uint64_t>(m, h[0]);
+        if (h[1]) {  // paths of 4.29 s or more: their u64 latencies to the side table
+          uint64_t* list = ctx->r_misc.get<uint64_t>(2 * h[1]);
+          SG_HIP(hipMemsetAsync(ctl + 1, 0, 8, st));
+          hipLaunchKernelGGL(k_wide_list, dim3(grid_for(cells, 256, 4096)), dim3(256), 0, st, slat[b], cells,
+                             (uint64_t)r0 * n_used, ctl + 1, list);
+          SG_CHECK_LAUNCH();
+          std::vector<uint64_t> hl(2 * h[1]);
+          copy_to_host(ctx, hl.data(), list, hl.size() * 8);
+          for (size_t i = 0; i < h[1]; i++) ri->wide.push_back({hl[2 * i], hl[2 * i + 1]});
+        }
       }
-      ctx->in_fill = false;
-      const size_t cells = (size_t)(r1 - r0) * n_used;
-      // (workspace fetched after the build, which may grow these buffers)
-      unsigned long long* dmin = ctx->r_err.get<unsigned long long>(4);
-      unsigned long long* part = ctx->r_misc.get<unsigned long long>(nbm);
-      hipLaunchKernelGGL(k_min_u64, dim3(nbm), dim3(256), 0, st, slat[b], cells, part);
-      hipLaunchKernelGGL(k_min_final, dim3(1), dim3(256), 0, st, part, nbm, dmin);
-      SG_CHECK_LAUNCH();
-      SG_HIP(hipEventRecord(ctx->stage_done[b], st));
-      SG_HIP(hipStreamWaitEvent(ctx->copy_stream, ctx->stage_done[b], 0));
-      SG_HIP(hipMemcpyAsync(ri->lat + (size_t)r0 * n_used, slat[b], cells * 8, hipMemcpyDeviceToHost,
-                            ctx->copy_stream));
-      SG_HIP(hipMemcpyAsync(ri->loss + (size_t)r0 * n_used, sloss[b], cells * 4, hipMemcpyDeviceToHost,
-                            ctx->copy_stream));
-      SG_HIP(hipEventRecord(ctx->stage_copied[b], ctx->copy_stream));
-      unsigned long long h = 0;
-      copy_to_host(ctx, &h, dmin, 8);  // (the next block's build starts after this sync; the copy runs on)
-      m = std::min<uint64_t>(m, h);
+    } catch (...) {
+      (void)hipStreamSynchronize(ctx->copy_stream);  // no copy may still run into the object
+      throw;
     }
     SG_HIP(hipStreamSynchronize(ctx->copy_stream));
+    std::sort(ri->wide.begin(), ri->wide.end(),
+              [](const sg_routing_info::Wide& x, const sg_routing_info::Wide& y) { return x.cell < y.cell; });
+    std::fill(ri->row_set.begin(), ri->row_set.end(), 1);
+    ri->rows_set = n_used;
     ri->min_lat = m;
     ri->filled = true;
   });

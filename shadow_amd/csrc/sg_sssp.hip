@@ -95,8 +95,8 @@ constexpr int SSSP_WAVES = SSSP_THREADS / 64;
 constexpr int SSSP_K = 4;            // expansion path: chunks of 64 arc slots a wave handles at once
 constexpr int SSSP_KB = SSSP_KB_MAX;  // bound rows per bounded search (sg_routing.hip sssp_plan)
 // static LDS of k_sssp_lds: ctl[8] + red[SSSP_WAVES] (u32), hb (u64), own[SSSP_WAVES][64 * SSSP_K] (u8),
-// sink[64] (u64)
-constexpr size_t SSSP_STATIC_LDS = 4 * (8 + SSSP_WAVES) + 16 + SSSP_WAVES * 64 * SSSP_K + 512;
+// sink[64] (u64), s_ub[SSSP_KB][3] + s_nub (u32)
+constexpr size_t SSSP_STATIC_LDS = 4 * (8 + SSSP_WAVES) + 16 + SSSP_WAVES * 64 * SSSP_K + 512 + 4 * (3 * SSSP_KB + 1) + 16;
 // lane path: arcs a lane has in flight (template LA: 8 or 16, SG_SSSP_LANE_ARCS);
 // used up to out-degree lane_deg_max (SG_SSSP_LANE_DEG, default 16)
 
@@ -110,27 +110,6 @@ __device__ __forceinline__ uint64_t frelax(uint64_t ku, uint32_t edge_lat, float
   const uint32_t lat = __builtin_elementwise_add_sat(fkey_lat(ku), edge_lat);
   const float loss = fold_loss(__uint_as_float(fkey_loss_bits(ku)), edge_om);
   return ((uint64_t)lat << 32) | ((uint64_t)__float_as_uint(loss) << 1) | 1ull;
-}
-
-// Inclusive scans across a wave64 with DPP (row shifts, then the row broadcasts
-// of lanes 15 and 31): sum and max of u32.
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));
-  return v;
 }
 
 // Queue capacity: n + 1024 rounded up to 64.  At most n nodes are queued (one
@@ -191,8 +170,18 @@ __global__ void __launch_bounds__(NT)
                unsigned long long* __restrict__ diag, uint32_t claim, uint32_t idle_sleep,
                uint32_t lane_deg_max, const uint32_t* __restrict__ blk_rows,
                const uint32_t* __restrict__ ub_row, const uint32_t* __restrict__ ub_w,
-               uint32_t* __restrict__ item_ctr, uint32_t n_items, uint32_t spin_max) {
+               uint32_t* __restrict__ item_ctr, uint32_t n_items, uint32_t spin_max,
+               const uint32_t* __restrict__ plan_ctl, int plan_ph) {
   constexpr int NW = NT / 64;
+  if (plan_ctl) {  // a device-built plan (sg_plan.hip): this phase's rows and bound rows, its row count
+    const uint32_t base = plan_ctl[2 * plan_ph];
+    n_items = plan_ctl[2 * plan_ph + 1];
+    blk_rows += base;
+    if (ub_row) {
+      ub_row += (size_t)base * SSSP_KB;
+      ub_w += (size_t)base * SSSP_KB;
+    }
+  }
   extern __shared__ __align__(16) unsigned char smem[];
   const uint32_t cap = sssp_ring_cap(n);
   const RingMod slot_of{cap, (uint32_t)(0x100000000ull / cap)};
@@ -207,6 +196,8 @@ __global__ void __launch_bounds__(NT)
   __shared__ uint8_t own[NW][64 * SSSP_K];
   __shared__ uint32_t red[NW];
   __shared__ unsigned long long sink[64];  // per-lane no-op target of offer_all
+  __shared__ uint32_t s_ub[SSSP_KB][3];     // the row's usable bound rows: row, latency, exact
+  __shared__ uint32_t s_nub;
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // Every global read of the setup is a buffer load whose out-of-range lanes read
@@ -243,6 +234,7 @@ __global__ void __launch_bounds__(NT)
     } else {
       if (it) break;
       bi = blockIdx.x;
+      if (bi >= n_items) break;
     }
     // COUNT diagnostics of the first 4096 rows: cycle stamps, pops, bucket advances, relaxations
     const bool dg = COUNT && diag && bi < 4096 && tid == 0;
@@ -257,12 +249,27 @@ __global__ void __launch_bounds__(NT)
     for (int i = tid; i < NW * 64 * SSSP_K; i += NT) (&own[0][0])[i] = 0;
     if (tid < 8) ctl[tid] = 0;
     if (tid == 0) hb = 0;
+    if (ub_row && tid < 64) {
+      // wave 0 lists the row's usable bound rows in LDS while the others initialise: a
+      // row whose search gave up (sat_row 2) was never written, so it gives no bounds; a
+      // saturated one (1) holds real paths but not its optimum everywhere: bounds only
+      const uint32_t e = tid < SSSP_KB ? ub_row[(size_t)bi * SSSP_KB + tid] : ~0u;
+      const uint32_t w = tid < SSSP_KB ? ub_w[(size_t)bi * SSSP_KB + tid] : 0u;
+      const uint32_t srow = e & ~SSSP_UB_EXACT;
+      const uint32_t sf = e != ~0u ? sat_row[srow - row_begin] : 2u;
+      const bool on = sf != 2u;
+      const uint64_t mk = __ballot(on);
+      if (on) {
+        const int at = __popcll(mk & ((1ull << tid) - 1));
+        s_ub[at][0] = srow;
+        s_ub[at][1] = w;
+        s_ub[at][2] = (e & SSSP_UB_EXACT) && sf == 0u;
+      }
+      if (tid == 0) s_nub = (uint32_t)__popcll(mk);
+    }
     __syncthreads();
     if (ub_row) {  // Bounds: keys start just above the shortest of up to SSSP_KB known paths (clean)
-      // the bound rows (uniform; read per group from ub_row, not held in an
-      // array: a dynamically indexed array went to scratch memory)
-      int nb = 0;
-      for (int k = 0; k < SSSP_KB; k++) nb += ub_row[(size_t)bi * SSSP_KB + k] != ~0u;
+      const int nb = (int)s_nub;
       if (nb) {
         const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc((void*)used, 0, (int)(n_used * 4u),
                                                                             0x00020000);
@@ -277,26 +284,22 @@ __global__ void __launch_bounds__(NT)
             m[g] = ex[g] = ~0ull;
           }
 #pragma unroll 1
-          for (int k = 0; k < SSSP_KB; k += 2) {  // two bound rows' loads in flight together
+          for (int k = 0; k < nb; k += 2) {  // two bound rows' loads in flight together
             bool on[2], exact[2];
             uint32_t sr[2], w[2];
             __amdgpu_buffer_rsrc_t rl[2], rf[2];
 #pragma unroll
             for (int u = 0; u < 2; u++) {
-              const uint32_t e = ub_row[(size_t)bi * SSSP_KB + k + u];
-              on[u] = e != ~0u;
-              sr[u] = e & ~SSSP_UB_EXACT;
-              w[u] = ub_w[(size_t)bi * SSSP_KB + k + u];
-              // a row flagged for the wide kernel (saturated or given up) may not hold
-              // its optimum everywhere: bounds only
-              exact[u] = on[u] && (e & SSSP_UB_EXACT) && !sat_row[sr[u] - row_begin];
+              on[u] = k + u < nb;
+              sr[u] = on[u] ? s_ub[k + u][0] : 0u;
+              w[u] = on[u] ? s_ub[k + u][1] : 0u;
+              exact[u] = on[u] && s_ub[k + u][2];
               const size_t rb = on[u] ? (size_t)(sr[u] - out_row0) * n_used : 0;
               rl[u] = __builtin_amdgcn_make_buffer_rsrc((void*)(out_lat + rb), 0, (int)(on[u] ? n_used * 8u : 0u),
                                                         0x00020000);
               rf[u] = __builtin_amdgcn_make_buffer_rsrc((void*)(out_loss + rb), 0, (int)(exact[u] ? n_used * 4u : 0u),
                                                         0x00020000);
             }
-            if (!on[0] && !on[1]) continue;
             uint64_t l[2][G];
             uint32_t f[2][G];
 #pragma unroll
@@ -322,7 +325,7 @@ __global__ void __launch_bounds__(NT)
           }
 #pragma unroll
           for (int g = 0; g < G; g++) {
-            uint64_t kv = m[g] + 1 < LAT32_SAT ? ((m[g] + 1) << 32) | ((uint64_t)0x3F800000u << 1) : FKEY_INF;
+            uint64_t kv = m[g] < LAT32_SAT - 1 ? ((m[g] + 1) << 32) | ((uint64_t)0x3F800000u << 1) : FKEY_INF;
             kv = min(kv, ex[g]);
             if (j0 + g * NT < n_used && kv != FKEY_INF) key[vv[g]] = kv;
           }
@@ -359,7 +362,7 @@ __global__ void __launch_bounds__(NT)
     auto give_up = [&]() {
       if (lane == 0) {
         ctl[ABORT] = 1u;
-        sat_row[row - row_begin] = 1u;
+        sat_row[row - row_begin] = 2u;  // never written: the wide kernel redoes it, and no search bounds by it
       }
     };
     auto ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
@@ -406,7 +409,7 @@ __global__ void __launch_bounds__(NT)
       }
       h = __builtin_amdgcn_readfirstlane(h);
       k = __builtin_amdgcn_readfirstlane(k);
-      if (__builtin_amdgcn_readfirstlane(ld(&ctl[ABORT]))) return;  // another wave gave up
+      if (__builtin_amdgcn_readfirstlane(ld(&ctl[ABORT]))) goto wave_exit;  // another wave gave up
       if (!k) {
         uint32_t q = 0;
         if (lane == 0) {
@@ -417,7 +420,7 @@ __global__ void __launch_bounds__(NT)
         if (!__builtin_amdgcn_readfirstlane(q)) {
           if (++spins > spin_max) {
             give_up();
-            return;
+            goto wave_exit;
           }
           for (uint32_t z = 0; z < idle_sleep; z++) __builtin_amdgcn_s_sleep(8);  // ~512 cycles each
           __builtin_amdgcn_s_sleep(2);
@@ -425,7 +428,7 @@ __global__ void __launch_bounds__(NT)
         }
         // ---- quiescent: every wave is here.  Next bucket, or done.
         __syncthreads();
-        if (ld(&ctl[ABORT])) return;  // a wave gave up before this barrier (uniform: no wave is spinning now)
+        if (ld(&ctl[ABORT])) goto wave_exit;  // a wave gave up before this barrier (uniform: no wave is spinning now)
         // one bucket (split = LAT32_SAT, the default): every node that became dirty was
         // queued, so a quiescent queue means nothing is dirty -- no key scan needed
         if (split >= LAT32_SAT) break;
@@ -442,7 +445,7 @@ __global__ void __launch_bounds__(NT)
         if (m == LAT32_SAT) break;  // nothing dirty (saturated keys are never marked dirty)
         if (++n_adv > max_adv) {  // every wave is here together
           give_up();
-          return;
+          goto wave_exit;
         }
         split = m + delta >= m ? min(m + delta, LAT32_SAT) : LAT32_SAT;
         for (uint32_t v0 = wv * 64; v0 < n; v0 += NT) {  // queue the dirty nodes below split
@@ -476,7 +479,7 @@ __global__ void __launch_bounds__(NT)
       }
       if (__any(stuck)) {
         give_up();
-        return;
+        goto wave_exit;
       }
       const uint32_t deg = a1 - a0;
       const uint32_t dmax = __builtin_amdgcn_readlane(wave_incl_max(deg), 63);
@@ -610,6 +613,18 @@ __global__ void __launch_bounds__(NT)
     }
     __syncthreads();  // the next row reuses the LDS
   }
+wave_exit:
+  // Persistent workgroups: the last wave to leave flags the rows no workgroup
+  // claimed (every workgroup that would have claimed them gave up and left) for
+  // the wide kernel, so no row is left unwritten and unflagged.
+  if (item_ctr && lane == 0) {
+    __threadfence();
+    if (atomicAdd(&item_ctr[1], 1u) == gridDim.x * NW - 1) {
+      const uint32_t c = __hip_atomic_load(&item_ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t i = min(c, n_items); i < n_items; i++)
+        sat_row[(blk_rows ? blk_rows[i] : row_begin + i) - row_begin] = 2u;
+    }
+  }
 }
 
 bool sssp_lds_fits(uint32_t n) {
@@ -624,7 +639,7 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
                      const uint32_t* self_edge, const uint64_t* e_lat, const float* e_loss, uint64_t* out_lat,
                      float* out_loss, uint32_t* sat_row, uint32_t delta, unsigned long long* work,
                      unsigned long long* diag, const uint32_t* blk_rows, uint32_t n_blk, const uint32_t* ub_row,
-                     const uint32_t* ub_w) {
+                     const uint32_t* ub_w, const uint32_t* plan_ctl, int plan_ph, uint32_t* plan_ctr) {
   const size_t lds = sssp_lds_bytes(n);
   if (!sssp_lds_fits(n)) throw Error(SG_ERR_INVALID_ARG, "graph too large for the LDS-resident search");
   if ((uint64_t)n_arcs * 12 >= (1ull << 31)) throw Error(SG_ERR_INVALID_ARG, "too many arcs for 32-bit offsets");
@@ -632,6 +647,7 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
   const char* cs = getenv("SG_SSSP_CLAIM");
   const uint32_t claim = (uint32_t)std::min(64, std::max(1, cs && *cs ? atoi(cs) : 64));
   const int vec = n_used % 4 == 0 && ((uintptr_t)out_lat & 15) == 0 && ((uintptr_t)out_loss & 15) == 0;
+  // with a device plan (plan_ctl), n_blk bounds the phase's row count, which only the device knows
   const uint32_t rows = blk_rows ? n_blk : row_end - row_begin;
   if (!rows) return;
   const char* ts = getenv("SG_SSSP_THREADS");
@@ -647,16 +663,19 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
   // torn down per row.  C3: 3.92 -> 3.54 ms (same box).  SG_SSSP_PERSIST=0: a
   // workgroup per row.
   const char* ps = getenv("SG_SSSP_PERSIST");
-  const bool persist = !(ps && ps[0] == '0') && rows > (uint32_t)ctx->n_cu;
+  const bool persist = !(ps && ps[0] == '0') && (rows > (uint32_t)ctx->n_cu || plan_ctl);
   // spin budget per wave (sleeps of ~128 cycles): a safety valve against a queue
   // bug, never reached by a correct search; SG_SSSP_SPIN_MAX (tests) lowers it so
   // that searches give up and their rows take the wide kernel
   const char* sm = getenv("SG_SSSP_SPIN_MAX");
   const uint32_t spin_max = sm && *sm ? (uint32_t)std::max(1, atoi(sm)) : (1u << 22);
+  // [claims, waves done] (sg_sssp.hip wave_exit); a device plan's counters are zeroed by the plan kernel
   uint32_t* item_ctr = nullptr;
-  if (persist) {
-    item_ctr = ctx->r_items.get<uint32_t>(1);
-    SG_HIP(hipMemsetAsync(item_ctr, 0, 4, ctx->stream));
+  if (persist && plan_ctr) {
+    item_ctr = plan_ctr;
+  } else if (persist) {
+    item_ctr = ctx->r_items.get<uint32_t>(2);
+    SG_HIP(hipMemsetAsync(item_ctr, 0, 8, ctx->stream));
   }
   const uint32_t grid = persist ? (uint32_t)ctx->n_cu : rows;
   auto go = [&](auto kern) {
@@ -664,7 +683,8 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
                                (int)(LDS_PER_CU - SSSP_STATIC_LDS)));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, ctx->stream, out_off, out_arc, n, n_arcs, d_used, n_used,
                        row_begin, row_begin, self_edge, e_lat, e_loss, out_lat, out_loss, sat_row, delta, vec, work,
-                       diag, claim, idle_sleep, lane_deg, blk_rows, ub_row, ub_w, item_ctr, rows, spin_max);
+                       diag, claim, idle_sleep, lane_deg, blk_rows, ub_row, ub_w, item_ctr, rows, spin_max, plan_ctl,
+                       plan_ph);
   };
   if (work) {
     if (nt == 512) go(k_sssp_lds<true, 512, 8, 0>);

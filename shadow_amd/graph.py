@@ -183,8 +183,7 @@ class NetworkGraph:
         self.edge_packet_loss = np.ascontiguousarray(edge_packet_loss, dtype=np.float32)
         ids = np.arange(self.n_nodes, dtype=np.uint32) if node_ids is None else node_ids
         self.node_ids = np.ascontiguousarray(ids, dtype=np.uint32)
-        # graph/mod.rs:155-162: a later duplicate id wins
-        self._id_to_index = {int(i): k for k, i in enumerate(self.node_ids)}
+        self._id_to_index = None  # built on first lookup
         self._net = None
 
     @property
@@ -218,11 +217,15 @@ class NetworkGraph:
         check(self.ctx.handle, L.sg_net_create(self.ctx.handle, C.byref(g), C.byref(h)))
         self._net = h
 
+    def close(self) -> None:
+        """Release the device graph (sg_net_destroy) now rather than at garbage collection."""
+        if self._net:
+            load().sg_net_destroy(self._net)
+            self._net = None
+
     def __del__(self):
         try:
-            if self._net:
-                load().sg_net_destroy(self._net)
-                self._net = None
+            self.close()
         except Exception:
             pass
 
@@ -271,6 +274,8 @@ class NetworkGraph:
         return cls.parse(raw, ctx=ctx, threads=threads)
 
     def node_id_to_index(self, node_id: int) -> Optional[int]:
+        if self._id_to_index is None:  # graph/mod.rs:155-162: a later duplicate id wins
+            self._id_to_index = {int(i): k for k, i in enumerate(self.node_ids)}
         return self._id_to_index.get(int(node_id))
 
     def node_index_to_id(self, index: int) -> Optional[int]:
@@ -319,9 +324,9 @@ class NetworkGraph:
 # ---------------------------------------------------------------------------
 class RoutingInfo:
     """RoutingInfo<u32>: path(start, end), get_smallest_latency_ns and the packet
-    counters, over a dense (latency u64, loss f32) table in pinned host memory.
-    `latency_ns` / `packet_loss` are zero-copy [n x n] views (row = source, in
-    `node_ids` order), valid while this object lives.  With addresses attached
+    counters, over a dense table of 8-byte (latency, loss) cells in pinned host
+    memory (row = source, in `node_ids` order).  `latency_ns` / `packet_loss` /
+    `rows()` decode copies; `cells` is the zero-copy packed view.  With addresses attached
     (set_addresses) it also answers WorkerShared::latency / reliability /
     is_routable (worker.rs:517-555)."""
 
@@ -366,21 +371,38 @@ class RoutingInfo:
         load().sg_routing_info_view(self.handle, C.byref(v))
         return v
 
+    def rows(self, row_begin: int = 0, row_end: Optional[int] = None):
+        """Rows [row_begin, row_end) decoded from the 8-byte cells (sg_routing_info_rows): a
+        (latency u64, loss f32) pair of new arrays."""
+        row_end = self.n if row_end is None else int(row_end)
+        k = max(0, row_end - int(row_begin))
+        lat = np.empty((k, self.n), np.uint64)
+        loss = np.empty((k, self.n), np.float32)
+        rc = load().sg_routing_info_rows(self.handle, int(row_begin), row_end, lat.ctypes.data, loss.ctypes.data)
+        if rc != _capi.SG_OK:
+            raise ShadowGpuError(rc, "sg_routing_info_rows: bad row range")
+        return lat, loss
+
     @property
     def latency_ns(self) -> np.ndarray:
-        v = self._view()
-        if not self.n:
-            return np.zeros((0, 0), np.uint64)
-        buf = (C.c_uint64 * (self.n * self.n)).from_address(v.latency_ns)
-        return np.frombuffer(buf, dtype=np.uint64).reshape(self.n, self.n)
+        """[n x n] latencies (a copy, decoded from the cells)."""
+        return self.rows()[0]
 
     @property
     def packet_loss(self) -> np.ndarray:
+        """[n x n] losses (a copy)."""
+        return self.rows()[1]
+
+    @property
+    def cells(self) -> np.ndarray:
+        """Zero-copy [n x n] view of the packed cells (latency << 32 | bits(loss); SG_CELL_WIDE in the
+        upper half for paths of 2^32 - 1 ns or more).  The array keeps this object alive."""
         v = self._view()
         if not self.n:
-            return np.zeros((0, 0), np.float32)
-        buf = (C.c_float * (self.n * self.n)).from_address(v.packet_loss)
-        return np.frombuffer(buf, dtype=np.float32).reshape(self.n, self.n)
+            return np.zeros((0, 0), np.uint64)
+        buf = (C.c_uint64 * (self.n * self.n)).from_address(v.cells)
+        buf._owner = self  # the frombuffer base chain keeps the table alive
+        return np.frombuffer(buf, dtype=np.uint64).reshape(self.n, self.n)
 
     @property
     def pinned(self) -> bool:

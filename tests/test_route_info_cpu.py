@@ -92,3 +92,41 @@ def test_sparse_addresses():
     for k in range(20):
         for m in range(20):
             assert ri.latency(int(ips[k]), int(ips[m])) == int(lat[nodes[k], nodes[m]])
+
+
+def test_wide_latencies_keep_u64():
+    """Paths of 2^32 - 1 ns (4.29 s) or more: the cell says SG_CELL_WIDE and the u64 latency
+    lives in the side table; every lookup and the decoded rows give it back exactly."""
+    lat, loss = _table(12)
+    lat = lat.copy()
+    lat[2, 5] = (1 << 40) + 3
+    lat[7, 7] = (1 << 32) - 1  # exactly the sentinel value: also kept wide
+    lat[11, 0] = (1 << 63) + 17
+    ri = RoutingInfo(range(12), lat, loss)
+    assert np.array_equal(ri.latency_ns, lat) and np.array_equal(ri.packet_loss.view(np.uint32), loss.view(np.uint32))
+    assert ri.path(2, 5).latency_ns == (1 << 40) + 3 and ri.path(7, 7).latency_ns == (1 << 32) - 1
+    assert ri.cells[2, 5] >> np.uint64(32) == np.uint64(0xFFFFFFFF)
+    lr, _ = ri.rows(7, 12)
+    assert np.array_equal(lr, lat[7:12])
+    ips = [ipv for ipv in range(0x0B000001, 0x0B000001 + 12)]
+    ri.set_addresses(ips, list(range(12)))
+    assert ri.latency(ips[11], ips[0]) == (1 << 63) + 17
+    # rewriting a row drops its old wide entries
+    lat2 = lat.copy()
+    lat2[2, 5] = 77
+    ri.set_rows(2, lat2[2:3], loss[2:3])
+    assert ri.path(2, 5).latency_ns == 77 and ri.path(11, 0).latency_ns == (1 << 63) + 17
+
+
+def test_smallest_latency_needs_every_row():
+    """get_smallest_latency_ns is over the whole table (graph/mod.rs:478-480): None until every
+    row is set, and recomputed when rows are rewritten with larger values."""
+    lat, loss = _table(8)
+    ri = RoutingInfo(range(8))
+    ri.set_rows(0, lat[:4], loss[:4])
+    assert ri.get_smallest_latency_ns() is None
+    ri.set_rows(4, lat[4:], loss[4:])
+    assert ri.get_smallest_latency_ns() == int(lat.min())
+    big = np.full_like(lat, 10**12)
+    ri.set_rows(0, big, loss)
+    assert ri.get_smallest_latency_ns() == 10**12

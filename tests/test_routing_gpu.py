@@ -32,8 +32,12 @@ def _graph(g, ctx):
     return NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
 
 
-def _check(oracle, g, used, ctx, shortest=True, rows=None):
+def _check(oracle, g, used, ctx, shortest=True, rows=None, poison=False):
+    """poison: build into device buffers pre-filled with zeros (latency 0, loss 0), so a row
+    that is never written, or a bound taken from one, cannot pass by holding an earlier table."""
     net = _graph(g, ctx)
+    if rows is None and poison:
+        rows = (0, len(used))
     if rows is None:
         t = net.compute_shortest_paths(used) if shortest else net.get_direct_paths(used)
         lat, loss = t.latency_ns, t.packet_loss
@@ -42,8 +46,8 @@ def _check(oracle, g, used, ctx, shortest=True, rows=None):
 
         r0, r1 = rows
         nu = len(used)
-        dl = torch.empty((r1 - r0) * nu, dtype=torch.int64, device="cuda")
-        df = torch.empty((r1 - r0) * nu, dtype=torch.float32, device="cuda")
+        dl = torch.zeros((r1 - r0) * nu, dtype=torch.int64, device="cuda")
+        df = torch.zeros((r1 - r0) * nu, dtype=torch.float32, device="cuda")
         net.build_rows_device(used, r0, r1, dl.data_ptr(), df.data_ptr(), shortest)
         lat = dl.cpu().numpy().view(np.uint64).reshape(r1 - r0, nu)
         loss = df.cpu().numpy().reshape(r1 - r0, nu)
@@ -158,13 +162,16 @@ def test_lds_give_up_takes_wide_kernel(oracle, ctx, monkeypatch, persist, spin, 
     """The LDS search's safety valve: with a spin budget of 1 or 40 idle polls (SG_SSSP_SPIN_MAX),
     searches give up; the whole workgroup then leaves the kernel, the row is flagged, and the wide
     kernel redoes it.  The table must still be exact, and a persistent workgroup that gave up must
-    not leave state behind for the rows other workgroups go on to claim."""
+    not leave state behind for the rows other workgroups go on to claim.  When every persistent
+    workgroup has given up, the rows none claimed are flagged too (sg_sssp.hip wave_exit); with
+    phases (lds_bounded) a later row takes no bounds from a row that gave up (it was never
+    written).  The output buffer starts poisoned with zeros, so neither can pass by accident."""
     if apsp_kernel == "slab":
         pytest.skip("LDS knob")
     monkeypatch.setenv("SG_SSSP_PERSIST", persist)
     monkeypatch.setenv("SG_SSSP_SPIN_MAX", spin)
     g = synth.ring_chords_graph(700, 6.0, seed=33)
-    _check(oracle, g, np.arange(700, dtype=np.uint32), ctx)
+    _check(oracle, g, np.arange(700, dtype=np.uint32), ctx, poison=True)
 
 
 def test_exact_seeds_next_to_wide_rows(oracle, ctx, monkeypatch):

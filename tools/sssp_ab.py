@@ -48,7 +48,7 @@ def main():
             ts.append((time.perf_counter() - t0) * 1e3)
         ctx.enable_timers(True)
         net.build_rows_device(used, r0, r1, lat.data_ptr(), loss.data_ptr(), True)
-        tm = {k: round(ctx.read_timer(k)[0], 4) for k in ("sssp", "sssp_bounded", "relax", "relax_wide")}
+        tm = {k: round(ctx.read_timer(k)[0], 4) for k in ("sssp", "sssp_bounded", "relax", "relax_wide", "plan_sets", "plan_bounds")}
         ctx.enable_timers(False)
         h = (lat.view(torch.int64).sum().item(), loss.view(torch.int32).to(torch.int64).sum().item())
         if first is None:
