@@ -929,9 +929,11 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   hipStream_t st = ctx->stream;
   // one allocation, 256-B aligned sub-arrays
   size_t total = 0;
+  // (SG_NET_ALIGN, A/B diagnostics: sub-array alignment in bytes)
+  const size_t align = (size_t)std::max(256, env_int("SG_NET_ALIGN", 256));
   auto carve = [&](size_t bytes) {
     const size_t o = total;
-    total += (std::max<size_t>(bytes, 16) + 255) / 256 * 256;
+    total += (std::max<size_t>(bytes, 16) + align - 1) / align * align;
     return o;
   };
   const size_t o_esrc = carve(m * 4ull), o_edst = carve(m * 4ull), o_elat = carve(m * 8ull),
@@ -1261,7 +1263,7 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
     // 9.8 (a quarter) 2 phases, 1.30 against 1.38 ms
     const uint32_t per_cu = rows / std::max(1, ctx->n_cu);
     const int n_phase = std::max(2, std::min(SSSP_PHASES_MAX,
-                                             env_int("SG_SSSP_PHASES", per_cu >= 32 ? 4 : per_cu >= 16 ? 3 : 2)));
+                                             env_int("SG_SSSP_PHASES", per_cu >= 16 ? 3 : 2)));
     const int kb = std::max(1, std::min(SSSP_KB_MAX, env_int("SG_SSSP_BOUNDS", 2)));
     // exact seeds need a column for every node (see sg_sssp.hip "Exact seeds")
     const bool exact = env_int("SG_SSSP_EXACT", 1) != 0 && n_used == net->n_nodes;
@@ -1269,9 +1271,24 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
     const SsspDevPlan plan = sssp_device_plan(ctx, net, d_used, n_used, row_begin, row_end, n_phase, kb, exact, hops);
     if (const int warm = env_int("SG_PLAN_WARM", 0))
       hipLaunchKernelGGL(k_busy, dim3(4 * ctx->n_cu), dim3(256), 0, ctx->stream, (uint32_t)warm, (float*)nullptr);
+    // SG_PLAN_SYNC=1 (A/B diagnostics): read the phase sizes to the host and launch with host-known counts
+    std::vector<uint32_t> hctl;
+    if (env_int("SG_PLAN_SYNC", 0)) {
+      hctl.resize(2 * SSSP_PHASES_MAX);
+      copy_to_host(ctx, hctl.data(), plan.ctl, hctl.size() * 4);
+    }
     for (int ph = 0; ph < plan.n_phase; ph++) {
       const bool bounded = ph > 0;
       TimedLaunch tl(ctx, bounded ? "sssp_bounded" : "sssp", 0.0);
+      if (!hctl.empty()) {
+        const uint32_t b0 = hctl[2 * ph], cnt = hctl[2 * ph + 1];
+        launch_sssp_lds(ctx, net->out_off, net->out_arc, net->n_nodes, net->n_arcs, d_used, n_used, row_begin,
+                        row_end, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work,
+                        ph + 1 == plan.n_phase ? diag : nullptr, plan.list + b0, cnt,
+                        bounded ? plan.ub_row + (size_t)b0 * SSSP_KB_MAX : nullptr,
+                        bounded ? plan.ub_w + (size_t)b0 * SSSP_KB_MAX : nullptr);
+        continue;
+      }
       launch_sssp_lds(ctx, net->out_off, net->out_arc, net->n_nodes, net->n_arcs, d_used, n_used, row_begin,
                       row_end, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work,
                       ph + 1 == plan.n_phase ? diag : nullptr, plan.list, rows, bounded ? plan.ub_row : nullptr,

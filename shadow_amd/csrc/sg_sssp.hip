@@ -361,8 +361,18 @@ __global__ void __launch_bounds__(NT)
     constexpr int ABORT = 2;
     auto give_up = [&]() {
       if (lane == 0) {
-        ctl[ABORT] = 1u;
         sat_row[row - row_begin] = 2u;  // never written: the wide kernel redoes it, and no search bounds by it
+        // the workgroup's first wave to give up counts it out; when every persistent
+        // workgroup has given up (none left to claim the rest), the last one flags the
+        // rows none claimed.  (A workgroup that ends normally has seen every row claimed.)
+        if (atomicExch(&ctl[ABORT], 1u) == 0u && item_ctr) {
+          __threadfence();
+          if (atomicAdd(&item_ctr[1], 1u) == gridDim.x - 1) {
+            const uint32_t c = __hip_atomic_load(&item_ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (uint32_t i = min(c, n_items); i < n_items; i++)
+              sat_row[(blk_rows ? blk_rows[i] : row_begin + i) - row_begin] = 2u;
+          }
+        }
       }
     };
     auto ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
@@ -613,18 +623,9 @@ __global__ void __launch_bounds__(NT)
     }
     __syncthreads();  // the next row reuses the LDS
   }
-wave_exit:
-  // Persistent workgroups: the last wave to leave flags the rows no workgroup
-  // claimed (every workgroup that would have claimed them gave up and left) for
-  // the wide kernel, so no row is left unwritten and unflagged.
-  if (item_ctr && lane == 0) {
-    __threadfence();
-    if (atomicAdd(&item_ctr[1], 1u) == gridDim.x * NW - 1) {
-      const uint32_t c = __hip_atomic_load(&item_ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (uint32_t i = min(c, n_items); i < n_items; i++)
-        sat_row[(blk_rows ? blk_rows[i] : row_begin + i) - row_begin] = 2u;
-    }
-  }
+wave_exit:;
+  // (An earlier version counted every wave out with one device atomic at exit: 4,096
+  // atomics on one word at the end of each launch cost ~0.1 ms.)
 }
 
 bool sssp_lds_fits(uint32_t n) {
