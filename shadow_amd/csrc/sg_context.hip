@@ -230,6 +230,12 @@ void sg_ctx_destroy(sg_ctx* ctx) {
     if (ctx->stage_copied[b]) (void)hipEventDestroy(ctx->stage_copied[b]);
   }
   if (ctx->apsp_ret) (void)hipHostFree(ctx->apsp_ret);
+  for (auto& b : ctx->net_pool) {
+    (void)hipEventDestroy(b.freed);
+    (void)hipFree(b.p);
+  }
+  if (ctx->stage_used) (void)hipEventDestroy(ctx->stage_used);
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }

@@ -119,6 +119,21 @@ struct sg_ctx {
   // APSP: the active-batch count of the next pass, written by k_active_list
   // into pinned host-mapped memory at each pass-chunk end
   uint32_t* apsp_ret = nullptr;
+  // sg_net device blocks released by sg_net_destroy, reused by the next sg_net_create
+  // (a simulation that builds one graph and one table pays no hipMalloc / hipFree,
+  // whose implicit device synchronisation cost ~0.2 ms each); `freed` orders the
+  // reuse after the last work queued on the released block
+  struct NetBlock {
+    void* p;
+    size_t bytes;
+    hipEvent_t freed;
+  };
+  std::vector<NetBlock> net_pool;
+  // pinned staging of a new graph's edge arrays (one H2D copy); `stage_used` marks
+  // when the last copy out of it completed
+  void* h_stage = nullptr;
+  size_t h_stage_bytes = 0;
+  hipEvent_t stage_used = nullptr;
   // kernel timers (off unless sg_ctx_enable_timers)
   bool timing = false;
   bool count_work = false;  // SG_TIMERS_COUNT_WORK
@@ -152,9 +167,10 @@ struct sg_net {
   // self-loops
   uint32_t* self_cnt = nullptr;
   uint32_t* self_edge = nullptr;
-  void* mem = nullptr;  // one device allocation holding every array above
+  void* mem = nullptr;  // one device block holding every array above (from the context's pool)
+  size_t mem_bytes = 0;
   ~sg_net() {
-    if (mem) (void)hipFree(mem);
+    if (mem) (void)hipFree(mem);  // (sg_net_destroy hands it back to the pool instead)
   }
 };
 

@@ -942,7 +942,24 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
                o_inlat = carve(n_arcs * 8ull), o_inlat32 = carve(n_arcs * 4ull), o_inom = carve(n_arcs * 4ull),
                o_inrec = carve(n_arcs * 16ull), o_outoff = carve(((size_t)n + 1) * 4),
                o_outarc = carve(n_arcs * 12ull);
-  SG_HIP(hipMalloc(&net->mem, total));
+  {  // a released block of the right size from the context's pool, else a new one
+    size_t best = ~(size_t)0;
+    for (size_t i = 0; i < ctx->net_pool.size(); i++) {
+      const size_t b = ctx->net_pool[i].bytes;
+      if (b >= total && b <= 2 * total + (1u << 20) && (best == ~(size_t)0 || b < ctx->net_pool[best].bytes)) best = i;
+    }
+    if (best != ~(size_t)0) {
+      auto blk = ctx->net_pool[best];
+      ctx->net_pool.erase(ctx->net_pool.begin() + best);
+      SG_HIP(hipStreamWaitEvent(ctx->stream, blk.freed, 0));
+      (void)hipEventDestroy(blk.freed);
+      net->mem = blk.p;
+      net->mem_bytes = blk.bytes;
+    } else {
+      SG_HIP(hipMalloc(&net->mem, total));
+      net->mem_bytes = total;
+    }
+  }
   char* base = (char*)net->mem;
   net->e_src = (uint32_t*)(base + o_esrc);
   net->e_dst = (uint32_t*)(base + o_edst);
@@ -959,11 +976,25 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   net->in_rec = (uint4*)(base + o_inrec);
   net->out_off = (uint32_t*)(base + o_outoff);
   net->out_arc = (uint32_t*)(base + o_outarc);
-  if (m) {
-    SG_HIP(hipMemcpyAsync(net->e_src, g->edge_src, m * 4ull, hipMemcpyHostToDevice, st));
-    SG_HIP(hipMemcpyAsync(net->e_dst, g->edge_dst, m * 4ull, hipMemcpyHostToDevice, st));
-    SG_HIP(hipMemcpyAsync(net->e_lat, g->edge_latency_ns, m * 8ull, hipMemcpyHostToDevice, st));
-    SG_HIP(hipMemcpyAsync(net->e_loss, g->edge_packet_loss, m * 4ull, hipMemcpyHostToDevice, st));
+  if (m) {  // the edge arrays through the context's pinned staging, one copy (they are adjacent)
+    const size_t eb = o_inoff;  // bytes up to the first derived array
+    if (ctx->h_stage_bytes < eb) {
+      if (ctx->stage_used) SG_HIP(hipEventSynchronize(ctx->stage_used));
+      if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+      ctx->h_stage = nullptr;
+      ctx->h_stage_bytes = 0;
+      SG_HIP(hipHostMalloc(&ctx->h_stage, eb, hipHostMallocDefault));
+      ctx->h_stage_bytes = eb;
+    }
+    if (!ctx->stage_used) SG_HIP(hipEventCreateWithFlags(&ctx->stage_used, hipEventDisableTiming));
+    SG_HIP(hipEventSynchronize(ctx->stage_used));  // the previous copy out of the staging is done
+    char* h = (char*)ctx->h_stage;
+    memcpy(h + o_esrc, g->edge_src, m * 4ull);
+    memcpy(h + o_edst, g->edge_dst, m * 4ull);
+    memcpy(h + o_elat, g->edge_latency_ns, m * 8ull);
+    memcpy(h + o_eloss, g->edge_packet_loss, m * 4ull);
+    SG_HIP(hipMemcpyAsync(base, h, eb, hipMemcpyHostToDevice, st));
+    SG_HIP(hipEventRecord(ctx->stage_used, st));
   }
   uint32_t* indeg = ctx->r_misc.get<uint32_t>(2 * ((size_t)n + 1));
   uint32_t* outdeg = indeg + n + 1;
@@ -1459,7 +1490,25 @@ int32_t sg_net_create(sg_ctx* ctx, const sg_graph* g, sg_net** out) {
 
 void sg_net_destroy(sg_net* net) {
   if (!net) return;
-  if (net->ctx) (void)hipSetDevice(net->ctx->device);
+  sg_ctx* ctx = net->ctx;
+  if (ctx) {
+    (void)hipSetDevice(ctx->device);
+    hipEvent_t ev = nullptr;
+    if (net->mem && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess &&
+        hipEventRecord(ev, ctx->stream) == hipSuccess) {
+      ctx->net_pool.push_back({net->mem, net->mem_bytes, ev});
+      net->mem = nullptr;
+      while (ctx->net_pool.size() > 4) {  // keep a few blocks; release the oldest
+        auto& old = ctx->net_pool.front();
+        (void)hipEventSynchronize(old.freed);
+        (void)hipEventDestroy(old.freed);
+        (void)hipFree(old.p);
+        ctx->net_pool.erase(ctx->net_pool.begin());
+      }
+    } else if (ev) {
+      (void)hipEventDestroy(ev);
+    }
+  }
   delete net;
 }
 
