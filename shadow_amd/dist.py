@@ -38,8 +38,44 @@ def row_range(n_used: int, world: int, rank: int):
     return min(rank * per, n_used), min((rank + 1) * per, n_used), per
 
 
+def balanced_node_order(host_node: Sequence[int], n_nodes: int, world: int, host_weight=None):
+    """Row order of the used nodes that balances delivery across `world` rank blocks.
+
+    A host is owned by the rank holding its node's routing row, so with the identity
+    order a skewed host map (many hosts on a few nodes, as on a Tor-like graph) puts
+    most senders on one rank.  Here nodes are dealt to ranks largest weight first
+    (weight = the summed host_weight of their hosts, 1 per host by default), each
+    to the lightest rank that still has room for a full row block, and then ordered
+    by rank: every rank still builds an equal block of rows, now with an even share
+    of the senders.  A single node heavier than a rank's share cannot be split (its
+    hosts share one routing row) and bounds the balance.
+
+    Returns (order, route): order[i] = node index of table row i (the `used` list to
+    build with), route[h] = table row of host h's node."""
+    host_node = np.asarray(host_node, dtype=np.int64)
+    w = np.bincount(host_node, weights=None if host_weight is None else np.asarray(host_weight, np.float64),
+                    minlength=n_nodes).astype(np.float64)
+    per = (n_nodes + world - 1) // max(world, 1)
+    cap = [min(per, max(0, n_nodes - r * per)) for r in range(world)]
+    load = np.zeros(world)
+    fill = np.zeros(world, np.int64)
+    rank_of = np.empty(n_nodes, np.int64)
+    for v in np.argsort(-w, kind="stable"):  # heaviest first, ties by node index
+        open_ = np.nonzero(fill < cap)[0]
+        r = open_[np.argmin(load[open_])]
+        rank_of[v] = r
+        load[r] += w[v]
+        fill[r] += 1
+    order = np.argsort(rank_of, kind="stable").astype(np.uint32)
+    pos = np.empty(n_nodes, np.uint32)
+    pos[order] = np.arange(n_nodes, dtype=np.uint32)
+    return order, pos[host_node]
+
+
 class HostPartition:
-    """owner[h] = rank holding host h's routing row; local[h] = slot on its owner."""
+    """owner[h] = rank holding host h's routing row; local[h] = slot on its owner.
+    Rows are split in equal blocks (row_range); balanced_node_order chooses a row
+    order whose blocks carry even shares of the hosts."""
 
     def __init__(self, host_route: Sequence[int], n_used: int, world: int):
         route = np.asarray(host_route, dtype=np.int64)

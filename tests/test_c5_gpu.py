@@ -1,0 +1,87 @@
+"""C5 at full size: the 50k-node ring + chords graph, every node
+used, its whole 2.5·10^9-cell routing table built on one GPU, and a 10M-packet
+round over 100k hosts delivered from that table.
+
+* The table is compared with the oracle's Dijkstra (graph/mod.rs:183-228) on one
+  64-row batch out of every 16, across every batch group of the build.
+* The round is compared with the oracle's send_packet restatement
+  (worker.rs:322-397, event.rs:84-155) on every output: status, arrival time,
+  event id, per-destination order and offsets, the round minima, and every host's
+  RNG stream and event counter.  Gather indices run past 2^31 cells here.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from shadow_amd import NetworkGraph, synth
+from shadow_amd.worker import DeviceTable, HostTable, PacketBatch, deliver_round
+
+pytestmark = pytest.mark.gpu
+N = 50_000
+T0 = 946684800 * 10**9  # EmulatedTime SIMULATION_START
+THREADS = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope="module")
+def c5(ctx):
+    import torch
+
+    g = synth.ring_chords_graph(N, 8.0, seed=1)
+    net = NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
+    used = np.arange(N, dtype=np.uint32)
+    lat = torch.empty(N * N, dtype=torch.int64, device="cuda")
+    loss = torch.empty(N * N, dtype=torch.float32, device="cuda")
+    net.build_rows_device(used, 0, N, lat.data_ptr(), loss.data_ptr(), True)
+    torch.cuda.synchronize()
+    yield g, used, lat, loss
+    del lat, loss
+    torch.cuda.empty_cache()
+
+
+def test_c5_table_every_16th_batch(c5, oracle):
+    """One 64-row batch out of every 16 of the whole 50k-row table (49 batches, rows from
+    every batch group of the slab build), every cell bit-exact."""
+    g, used, lat, loss = c5
+    batches = range(0, (N + 63) // 64, 16)
+    assert len(batches) == 49
+    for b in batches:
+        r0, r1 = 64 * b, min(N, 64 * b + 64)
+        rc, olat, oloss, _ = oracle.shortest_paths(g["n"], g["src"], g["dst"], g["lat"], g["loss"], False, used,
+                                                   rows=(r0, r1), threads=THREADS)
+        assert rc == 0
+        glat = lat[r0 * N:r1 * N].cpu().numpy().view(np.uint64).reshape(r1 - r0, N)
+        gloss = loss[r0 * N:r1 * N].cpu().numpy().view(np.uint32).reshape(r1 - r0, N)
+        assert np.array_equal(glat, olat), f"latency mismatch in rows [{r0}, {r1})"
+        assert np.array_equal(gloss, oloss.view(np.uint32)), f"loss mismatch in rows [{r0}, {r1})"
+
+
+@pytest.mark.parametrize("packed", [True, False])
+def test_c5_round_on_full_table(c5, oracle, ctx, packed):
+    """10M packets from 100k hosts (node h mod 50k) delivered from the full 50k table,
+    in both table forms (packed 8-byte path keys and the two arrays)."""
+    g, used, lat, loss = c5
+    hosts = synth.make_hosts(100_000, N, general_seed=1, exact_seeds=True)
+    start, end = T0 + 10**9, T0 + 10**9 + 10**6
+    pk = synth.make_packets(10_000_000, hosts, start, end, seed=5, p_unknown_dst=0.001)
+    table = DeviceTable(lat, loss, N)
+    if packed:
+        assert table.pack(ctx)
+    ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    rng, ctr = ht.get_state()
+    out = deliver_round(ht, table, PacketBatch.from_numpy(pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"]),
+                        end, 2**63, 0, ctx=ctx)
+    got = out.to_numpy(len(pk["src"]))
+    grng, gctr = ht.get_state()
+    del out, table
+    lat_h = lat.cpu().numpy().view(np.uint64).reshape(N, N)
+    loss_h = loss.cpu().numpy().reshape(N, N)
+    want = oracle.deliver_round(end, 2**63, 0, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
+                                hosts["ip"], hosts["route"], lat_h, loss_h, rng, ctr, threads=THREADS)
+    del lat_h, loss_h
+    assert want["delivered"] > 9_000_000
+    for k in ("status", "deliver_time", "event_id", "dst_offsets", "dst_order"):
+        assert np.array_equal(got[k], want[k]), k
+    assert got["delivered"] == want["delivered"]
+    assert got["min_deliver"] == want["min_deliver"] and got["min_lat"] == want["min_lat"]
+    assert np.array_equal(grng, rng) and np.array_equal(gctr, ctr)

@@ -16,7 +16,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from shadow_amd import synth
-from shadow_amd.dist import HostPartition, RECORD_DTYPE, ShardedDelivery, SourceResult, row_range
+from shadow_amd.dist import HostPartition, RECORD_DTYPE, ShardedDelivery, SourceResult, balanced_node_order, row_range
 
 T0 = 946684800 * 10**9
 NONE = 0xFFFFFFFF
@@ -30,15 +30,23 @@ def _free_port():
     return p
 
 
-def _world(O):
-    g = synth.ring_chords_graph(60, 6.0, seed=2)
-    rc, lat, loss, _ = O.shortest_paths(60, g["src"], g["dst"], g["lat"], g["loss"], False, np.arange(60), threads=2)
+def _world(O, skew=False, world=2):
+    """skew: 200 nodes, 90 % of the hosts on 1 % of them (nodes 0 and 1, one routing-row
+    block under the identity order), rows in balanced_node_order's order."""
+    n = 200 if skew else 60
+    g = synth.ring_chords_graph(n, 6.0, seed=2)
+    hosts = synth.make_hosts(400, n, general_seed=4)
+    used = np.arange(n, dtype=np.uint32)
+    if skew:
+        node = np.where(np.arange(400) % 10 < 9, np.arange(400) % 2, 2 + np.arange(400) % (n - 2)).astype(np.uint32)
+        used, hosts["route"] = balanced_node_order(node, n, world)
+        hosts["node"] = node
+    rc, lat, loss, _ = O.shortest_paths(n, g["src"], g["dst"], g["lat"], g["loss"], False, used, threads=2)
     assert rc == 0
     loss = loss.copy()
     loss[::2, 1::2] = np.float32(0.35)
-    hosts = synth.make_hosts(400, 60, general_seed=4)
     pk = synth.make_packets(12000, hosts, T0, T0 + 10**6, seed=8, p_unknown_dst=0.02)
-    return g, lat, loss, hosts, pk
+    return g, lat, loss, hosts, pk, used
 
 
 class _Tables:
@@ -83,17 +91,17 @@ def _cpu_bucket(part, rank):
     return fn
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, skew=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from oracle import oracle as O
 
-        g, lat, loss, hosts, pk = _world(O)
+        g, lat, loss, hosts, pk, used = _world(O, skew, world)
         nu = lat.shape[0]
         # --- routing rows: each rank its block, all-gathered ---
         r0, r1, per = row_range(nu, world, rank)
-        rc, mine, _, _ = O.shortest_paths(60, g["src"], g["dst"], g["lat"], g["loss"], False, np.arange(60),
+        rc, mine, _, _ = O.shortest_paths(g["n"], g["src"], g["dst"], g["lat"], g["loss"], False, used,
                                           rows=(r0, r1))
         block = np.zeros((per, nu), np.uint64)
         block[: r1 - r0] = mine
@@ -124,12 +132,15 @@ def _worker(rank, world, port, q):
         q.put((rank, "error", traceback.format_exc(), None, None, None))
 
 
-def test_two_rank_gloo_exchange_matches_single_round(oracle):
+@pytest.mark.parametrize("skew", [False, True])
+def test_two_rank_gloo_exchange_matches_single_round(oracle, skew):
+    """The sharded round equals one oracle round.  skew: 90 % of the hosts on 1 % of the
+    nodes; with balanced_node_order's rows each rank sends within 1.5x of the other."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, skew)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=240) for _ in range(world)]
@@ -137,7 +148,13 @@ def test_two_rank_gloo_exchange_matches_single_round(oracle):
         p.join(timeout=60)
     for o in out:
         assert o[1] != "error", o[2]
-    g, lat, loss, hosts, pk = _world(oracle)
+    g, lat, loss, hosts, pk, used = _world(oracle, skew, world)
+    if skew:
+        sent = [len(o[4]) for o in out]
+        assert max(sent) <= 1.5 * min(sent), sent
+        # the identity row order would put both hot nodes, and ~94 % of the senders, on rank 0
+        ident = HostPartition(hosts["node"], g["n"], world)
+        assert (ident.owner[pk["src"]] == 0).mean() > 0.9
     rng = np.stack([oracle.xoshiro_seed(int(s)) for s in hosts["seed"]]).astype(np.uint64)
     ctr = np.zeros(hosts["n"], np.uint64)
     want = oracle.deliver_round(T0 + 10**6, 2**63, 0, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
