@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 4
+#define SG_ABI_VERSION 5
 
 typedef enum sg_status {
   SG_OK = 0,
@@ -111,6 +111,14 @@ int32_t sg_gml_parse(const char* text, size_t len, sg_gml** out, char* err, size
  * (load_network_graph feeds it, graph/mod.rs:498-513). */
 int32_t sg_gml_parse_threads(const char* text, size_t len, uint32_t threads, sg_gml** out, char* err,
                              size_t err_len);
+/* load_network_graph + NetworkGraph::parse (graph/mod.rs:483-513): read the GML
+ * file at `path` ("~/" expanded, tilde_expansion), xz-decompress it when
+ * compression = 1 (read_xz, :484-496: the system liblzma.so.5, opened at run
+ * time), check it is UTF-8 (String::from_utf8 / read_to_string), and parse it
+ * on `threads` threads as sg_gml_parse_threads.  compression 0 = plain text.
+ * Read, decompression and UTF-8 failures are SG_ERR_PARSE with a message. */
+int32_t sg_gml_load(const char* path, uint32_t compression, uint32_t threads, sg_gml** out, char* err,
+                    size_t err_len);
 /* Borrow the parsed edge list (valid until sg_gml_destroy). */
 int32_t sg_gml_graph(const sg_gml* g, sg_graph* out);
 /* NetworkGraph::node_id_to_index (graph/mod.rs:126-128); SG_ERR_INVALID_ARG if absent. */
@@ -233,6 +241,11 @@ int32_t sg_hosts_create(sg_ctx* ctx, uint32_t n_hosts, const uint32_t* host_ipv4
  * (Host::event_id_counter) out of / into the device (host memory). */
 int32_t sg_hosts_get_state(sg_hosts* hosts, uint64_t* rng_state, uint64_t* event_ctr);
 int32_t sg_hosts_set_state(sg_hosts* hosts, const uint64_t* rng_state, const uint64_t* event_ctr);
+/* Advance hosts' device RNG streams by steps[i] next_u64 steps each (host
+ * arrays, n entries, host_ids[i] < n_hosts; a host may repeat): the steps other
+ * consumers took (see sg_packets.rng_skip) that no later packet has carried to
+ * the device yet -- e.g. before sg_hosts_get_state for a checkpoint. */
+int32_t sg_hosts_skip(sg_hosts* hosts, uint32_t n, const uint32_t* host_ids, const uint64_t* steps);
 void sg_hosts_destroy(sg_hosts* hosts);
 
 /* Routing-table shard resident on the device (rows [row_begin, row_begin+n_rows)).
@@ -267,13 +280,28 @@ typedef struct sg_round {
 } sg_round;
 
 /* One round's sent packets, device SoA, grouped by ascending source host and
- * in each host's send order (the order Worker::send_packet saw them). */
+ * in each host's send order (the order Worker::send_packet saw them).
+ *
+ * rng_skip (optional, NULL = none): the host's Xoshiro stream is shared with
+ * other consumers on the CPU -- Host::random_mut() (host.rs:645-647) is also
+ * drawn by getrandom (syscall/handler/random.rs:40), socket port choices
+ * (socket.rs:179-858), host_rngDouble / host_rngNextNBytes (host.rs:1288-1300)
+ * and the auxv random bytes (managed_thread.rs:248).  rng_skip[i] = the number
+ * of next_u64 steps those consumers took on packet i's source host since the
+ * previous packet of that host handed to the device (in this batch or an
+ * earlier one).  The device advances the host's stream by that many steps
+ * before packet i (whatever its status), so every packet draws at exactly the
+ * stream position Worker::send_packet (worker.rs:360) drew from.  The CPU keeps
+ * its own copy of the stream in step by taking one step per packet that draws
+ * (now < sim_end and the destination resolves, worker.rs:332-360): no state
+ * crosses the bus per round. */
 typedef struct sg_packets {
   uint32_t n_packets;
   const uint32_t* src_host;     /* HostId of the sending host */
   const uint32_t* dst_ipv4;     /* destination address (host byte order) */
   const uint32_t* payload_len;  /* PacketRc::payload_len (packet.rs:394-396) */
   const uint64_t* send_time_ns; /* Worker::current_time() at the send */
+  const uint32_t* rng_skip;     /* device, n_packets, or NULL (see above) */
 } sg_packets;
 
 enum {

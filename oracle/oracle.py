@@ -80,7 +80,7 @@ def lib():
         L.sgo_deliver_faithful.restype = C.c_int64
         L.sgo_deliver_round.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u32p, u32p, u32p, u64p,
                                         C.c_uint32, u32p, u32p, C.c_uint32, u64p, f32p, u64p, u64p, u8p, u64p,
-                                        u64p, u32p, u32p, u64p, u64p]
+                                        u64p, u32p, u32p, u64p, u64p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -192,10 +192,12 @@ def smallest_latency(lat: np.ndarray) -> int:
 
 
 def deliver_round(round_end, sim_end, bootstrap_end, src_host, dst_ip, payload_len, send_time,
-                  host_ip, host_row, tab_lat, tab_loss, rng, event_ctr, threads: int = 1):
+                  host_ip, host_row, tab_lat, tab_loss, rng, event_ctr, threads: int = 1, rng_skip=None):
     """Worker::send_packet over a round's batch (worker.rs:322-397) + event order (event.rs:84-155).
 
-    rng (H x 4 u64) and event_ctr (H u64) are updated in place.
+    rng (H x 4 u64) and event_ctr (H u64) are updated in place.  rng_skip (per
+    packet, optional): steps the source host's other RNG consumers take before the
+    packet (sg_oracle.c sgo_deliver_round; runs single-threaded).
     Returns dict(status, deliver_time, event_id, dst_order, dst_offsets, min_deliver, min_lat, delivered).
     """
     src_host, dst_ip = _arr(src_host, np.uint32), _arr(dst_ip, np.uint32)
@@ -211,6 +213,10 @@ def deliver_round(round_end, sim_end, bootstrap_end, src_host, dst_ip, payload_l
     order = np.zeros(max(n, 1), np.uint32)
     offs = np.zeros(H + 1, np.uint32)
     mind, minl = C.c_uint64(), C.c_uint64()
+    skip = None if rng_skip is None else _arr(rng_skip, np.uint32)
+    if skip is not None:
+        assert len(skip) == n
+        threads = 1
     if threads > 1:  # the multi-threaded restatement (same results; packets grouped by source host)
         v = lambda a: a.ctypes.data_as(C.c_void_p)
         nd = lib().sgo_deliver_round_mt(round_end, sim_end, bootstrap_end, n, v(src_host), v(dst_ip), v(payload_len),
@@ -229,7 +235,7 @@ def deliver_round(round_end, sim_end, bootstrap_end, src_host, dst_ip, payload_l
                                  _p(tab_lat, C.c_uint64), _p(tab_loss, C.c_float), _p(rng, C.c_uint64),
                                  _p(event_ctr, C.c_uint64), _p(status, C.c_uint8), _p(deliver, C.c_uint64),
                                  _p(eid, C.c_uint64), _p(order, C.c_uint32), _p(offs, C.c_uint32),
-                                 C.byref(mind), C.byref(minl))
+                                 C.byref(mind), C.byref(minl), None if skip is None else skip.ctypes.data)
     if nd == -2:
         raise OverflowError("send time + latency overflows EmulatedTime (emulated_time.rs:121-126 panics)")
     if nd < 0:

@@ -547,6 +547,12 @@ static int cmp_ord(const void* a, const void* b) {
  * Returns the number of delivered packets, -1 on a bad argument, or -2 when a
  * delivered packet's send time + latency overflows EmulatedTime (the reference
  * panics).
+ * rng_skip (NULL = none): before packet i, its source host's stream takes
+ * rng_skip[i] steps for the host's other consumers of Host::random_mut()
+ * (host.rs:645-647: getrandom, syscall/handler/random.rs:40; socket port
+ * choices, socket.rs:179-858; host_rngDouble / host_rngNextNBytes,
+ * host.rs:1288-1300), whatever the packet's status -- the interleaving of those
+ * draws with send_packet's own (worker.rs:360) in the host's event order.
  */
 int64_t sgo_deliver_round(uint64_t round_end, uint64_t sim_end, uint64_t bootstrap_end,
                           uint32_t n_pkts, const uint32_t* src_host, const uint32_t* dst_ip,
@@ -555,7 +561,7 @@ int64_t sgo_deliver_round(uint64_t round_end, uint64_t sim_end, uint64_t bootstr
                           const uint64_t* tab_lat, const float* tab_loss, uint64_t* rng,
                           uint64_t* event_ctr, uint8_t* status, uint64_t* deliver_time,
                           uint64_t* event_id, uint32_t* dst_order, uint32_t* dst_offsets,
-                          uint64_t* min_deliver, uint64_t* min_lat) {
+                          uint64_t* min_deliver, uint64_t* min_lat, const uint32_t* rng_skip) {
   ip_host* map = (ip_host*)malloc(((size_t)n_hosts + 1) * sizeof(ip_host));
   uint32_t* dst_host = (uint32_t*)malloc(((size_t)n_pkts + 1) * sizeof(uint32_t));
   if (!map || !dst_host) return -1;
@@ -574,6 +580,8 @@ int64_t sgo_deliver_round(uint64_t round_end, uint64_t sim_end, uint64_t bootstr
     deliver_time[i] = 0;
     event_id[i] = UINT64_MAX;
     dst_host[i] = UINT32_MAX;
+    if (rng_skip)
+      for (uint32_t z = rng_skip[i]; z; z--) (void)sgo_xoshiro_next_u64(&rng[4 * (size_t)s]);
     if (now >= sim_end) {
       status[i] = SGO_ST_SIM_END;
       continue;

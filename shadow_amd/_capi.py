@@ -14,7 +14,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "shadow_gpu.h")
 
 # sg_status (include/shadow_gpu.h)
 SG_OK = 0
-SG_ABI_VERSION = 4  # include/shadow_gpu.h
+SG_ABI_VERSION = 5  # include/shadow_gpu.h
 SG_ERR_NO_EDGE = 1
 SG_ERR_MULTI_EDGE = 2
 SG_ERR_UNREACHABLE = 3
@@ -35,9 +35,9 @@ SG_PKT_DELIVERED, SG_PKT_DROP_LOSS, SG_PKT_DROP_NO_DST, SG_PKT_SIM_END = range(4
 EXPORTED = [
     "sg_abi_version", "sg_ctx_create", "sg_ctx_destroy", "sg_ctx_set_stream", "sg_ctx_stream",
     "sg_ctx_synchronize", "sg_ctx_last_error", "sg_ctx_last_error_pair", "sg_ctx_enable_timers",
-    "sg_ctx_read_timer", "sg_gml_parse", "sg_gml_parse_threads", "sg_gml_graph",
+    "sg_ctx_read_timer", "sg_gml_parse", "sg_gml_parse_threads", "sg_gml_load", "sg_gml_graph",
     "sg_gml_node_index", "sg_gml_destroy", "sg_net_create", "sg_net_destroy", "sg_routing_build",
-    "sg_routing_min_latency", "sg_hosts_create", "sg_hosts_get_state", "sg_hosts_set_state",
+    "sg_routing_min_latency", "sg_hosts_create", "sg_hosts_get_state", "sg_hosts_set_state", "sg_hosts_skip",
     "sg_hosts_destroy", "sg_deliver_round", "sg_deliver_source", "sg_deliver_bucket",
     "sg_table_pack", "sg_codel_create", "sg_codel_destroy", "sg_codel_run", "sg_codel_ring_cap",
     "sg_codel_get_state", "sg_codel_set_state", "sg_inbound_create", "sg_inbound_destroy", "sg_inbound_ring_cap",
@@ -120,7 +120,7 @@ class sg_round(C.Structure):
 
 class sg_packets(C.Structure):
     _fields_ = [("n_packets", C.c_uint32), ("src_host", C.c_void_p), ("dst_ipv4", C.c_void_p),
-                ("payload_len", C.c_void_p), ("send_time_ns", C.c_void_p)]
+                ("payload_len", C.c_void_p), ("send_time_ns", C.c_void_p), ("rng_skip", C.c_void_p)]
 
 
 class sg_deliveries(C.Structure):
@@ -173,6 +173,7 @@ def load(path: str | None = None):
         "sg_ctx_read_timer": (i32, [vp, C.c_char_p, C.POINTER(C.c_double), u64p, C.POINTER(C.c_double)]),
         "sg_gml_parse": (i32, [C.c_char_p, C.c_size_t, C.POINTER(vp), C.c_char_p, C.c_size_t]),
         "sg_gml_parse_threads": (i32, [C.c_char_p, C.c_size_t, u32, C.POINTER(vp), C.c_char_p, C.c_size_t]),
+        "sg_gml_load": (i32, [C.c_char_p, u32, u32, C.POINTER(vp), C.c_char_p, C.c_size_t]),
         "sg_gml_graph": (i32, [vp, C.POINTER(sg_graph)]),
         "sg_gml_node_index": (i32, [vp, u32, u32p]),
         "sg_gml_destroy": (None, [vp]),
@@ -198,6 +199,7 @@ def load(path: str | None = None):
         "sg_hosts_create": (i32, [vp, u32, vp, vp, vp, C.POINTER(vp)]),
         "sg_hosts_get_state": (i32, [vp, vp, vp]),
         "sg_hosts_set_state": (i32, [vp, vp, vp]),
+        "sg_hosts_skip": (i32, [vp, u32, vp, vp]),
         "sg_hosts_destroy": (None, [vp]),
         "sg_deliver_round": (i32, [vp, vp, C.POINTER(sg_table), C.POINTER(sg_round), C.POINTER(sg_packets),
                                    C.POINTER(sg_deliveries), C.POINTER(sg_round_stats)]),

@@ -176,6 +176,7 @@ struct WalkArgs {
   const uint32_t* dst_ip;
   const uint32_t* payload;
   const uint64_t* send;
+  const uint32_t* skip;  // sg_packets.rng_skip: other consumers' steps before each packet, or null
   uint32_t P, H;
   const uint32_t* host_off;
   const uint32_t* route;
@@ -217,7 +218,10 @@ enum : uint8_t { W_SIM_END = 0, W_NO_DST = 1, W_DRAW = 2, W_PAYLOAD = 4, W_BOOT 
 // (the unpacked two-array variant needs 74 VGPRs and stays at 6 waves per SIMD)
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Wpass-failed"
-template <bool PACKED>
+// SKIP: packets carry rng_skip (sg_packets), staged in LDS beside the rest (4 B
+// more per packet: 7 blocks per CU instead of 8, still every block of a 100k-host
+// round resident); a batch without it runs the SKIP = false variant unchanged.
+template <bool PACKED, bool SKIP>
 // At most 64 VGPRs (8 waves per SIMD, 8 blocks per CU): a 100k-host round's
 // 1,563 blocks are then all resident at once.  At 74 VGPRs 6 blocks fit a CU,
 // and the last 27 blocks ran as a second round, doubling the kernel time.
@@ -226,6 +230,7 @@ __global__ void __launch_bounds__(WALK_THREADS) __attribute__((amdgpu_waves_per_
   __shared__ uint64_t s_l[WALK_CHUNK];                  // path latency (or cell) -> event id
   __shared__ float s_loss[PACKED ? 1 : WALK_CHUNK];     // path packet loss (two-array form)
   __shared__ uint8_t s_f[WALK_CHUNK];                   // W_* flags -> SG_PKT_* status
+  __shared__ uint32_t s_skip[SKIP ? WALK_CHUNK : 1];    // other consumers' RNG steps before the packet
   const uint32_t h0 = blockIdx.x * WALK_HOSTS;
   const uint32_t t = threadIdx.x;
   if (*a.err & ERR_BATCH) {
@@ -265,9 +270,11 @@ __global__ void __launch_bounds__(WALK_THREADS) __attribute__((amdgpu_waves_per_
     uint64_t now[PPT];
     uint32_t ip[PPT], sh[PPT], d[PPT], r[PPT];
     uint8_t f[PPT];
+    uint32_t sk[PPT];
 #pragma unroll
     for (int q = 0; q < PPT; q++) {
       const uint32_t i = min(c0 + t + q * WALK_THREADS, c1 - 1);
+      sk[q] = SKIP ? a.skip[i] : 0u;
       now[q] = a.send[i];
       ip[q] = a.dst_ip[i];
       sh[q] = a.src[i];
@@ -330,6 +337,7 @@ __global__ void __launch_bounds__(WALK_THREADS) __attribute__((amdgpu_waves_per_
         s_l[k] = lat;
         if (!PACKED) s_loss[k] = loss;
         s_f[k] = f[q];
+        if (SKIP) s_skip[k] = sk[q];
       }
     }
     __syncthreads();
@@ -339,6 +347,8 @@ __global__ void __launch_bounds__(WALK_THREADS) __attribute__((amdgpu_waves_per_
       for (uint32_t i = b; i < e; i++) {
         const uint32_t k = i - c0;
         const uint8_t f = s_f[k];
+        if (SKIP)  // the steps Host::random_mut()'s other consumers took before this send (sg_packets.rng_skip)
+          for (uint32_t z = s_skip[k]; z; z--) (void)x.next_u64();
         uint8_t st;
         uint64_t arr = 0, id = ~0ull;
         if (f & W_DRAW) {
@@ -1435,6 +1445,7 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   a.dst_ip = pk->dst_ipv4;
   a.payload = pk->payload_len;
   a.send = pk->send_time_ns;
+  a.skip = pk->rng_skip;
   a.P = P;
   a.H = H;
   a.host_off = w.host_off;
@@ -1462,10 +1473,14 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
     // per packet: 20 B in, 12 B (8 B packed) path gather, 4 B dst map, 21 B out (status, time, id),
     // 4 B dst scratch; per host: 8 B segment, 4 B route, 32+32 B RNG, 8+8 B event counter
     TimedLaunch tl(ctx, "walk", (tab->path_key ? 57.0 : 61.0) * P + 92.0 * H);
-    if (a.tab_key)
-      hipLaunchKernelGGL(k_walk<true>, dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
+    if (a.tab_key && a.skip)
+      hipLaunchKernelGGL((k_walk<true, true>), dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
+    else if (a.tab_key)
+      hipLaunchKernelGGL((k_walk<true, false>), dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
+    else if (a.skip)
+      hipLaunchKernelGGL((k_walk<false, true>), dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
     else
-      hipLaunchKernelGGL(k_walk<false>, dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
+      hipLaunchKernelGGL((k_walk<false, false>), dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
   }
   const StatsJob sj{a.blk_stats, walk_blocks, ctx->round_err, w.big_count, ctx->round_ret};
   if (fuse_stats)
@@ -1559,6 +1574,20 @@ void launch_group_offsets(sg_ctx* ctx, const uint32_t* key, uint32_t n, uint32_t
   hipLaunchKernelGGL(k_host_off, dim3(grid_for((size_t)n + 1, 256, 16384)), dim3(256), 0, ctx->stream, key, n,
                      n_groups, off, err);
   SG_CHECK_LAUNCH();
+}
+
+// sg_hosts_skip: host ids[i] (unique) advances its stream by steps[i] next_u64 steps.
+__global__ void __launch_bounds__(256) k_hosts_skip(const uint32_t* __restrict__ ids, const uint64_t* __restrict__ steps,
+                                                    uint32_t m, uint32_t H, uint64_t* __restrict__ rng) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= m) return;
+  const size_t h = ids[i];
+  Xoshiro x{rng[h], rng[(size_t)H + h], rng[2 * (size_t)H + h], rng[3 * (size_t)H + h]};
+  for (uint64_t z = steps[i]; z; z--) (void)x.next_u64();
+  rng[h] = x.s0;
+  rng[(size_t)H + h] = x.s1;
+  rng[2 * (size_t)H + h] = x.s2;
+  rng[3 * (size_t)H + h] = x.s3;
 }
 
 // Path-key table: (lat << 32) | bits(loss) per cell, so the walk's path gather
@@ -1694,6 +1723,39 @@ int32_t sg_hosts_set_state(sg_hosts* hs, const uint64_t* rng_state, const uint64
       SG_HIP(hipMemcpyAsync(hs->ctr, event_ctr, n * 8, hipMemcpyHostToDevice, hs->ctx->stream));
       SG_HIP(hipStreamSynchronize(hs->ctx->stream));
     }
+  });
+}
+
+int32_t sg_hosts_skip(sg_hosts* hs, uint32_t n, const uint32_t* host_ids, const uint64_t* steps) {
+  if (!hs || (n && (!host_ids || !steps))) return SG_ERR_INVALID_ARG;
+  return sg::guarded(hs->ctx, [&] {
+    // one entry per host (a host may repeat in the call), then one device thread per host
+    std::vector<std::pair<uint32_t, uint64_t>> hv(n);
+    for (uint32_t i = 0; i < n; i++) {
+      if (host_ids[i] >= hs->n) throw sg::Error(SG_ERR_INVALID_ARG, "sg_hosts_skip: host out of range");
+      hv[i] = {host_ids[i], steps[i]};
+    }
+    std::sort(hv.begin(), hv.end());
+    std::vector<uint32_t> ids;
+    std::vector<uint64_t> tot;
+    for (auto& e : hv) {
+      if (!ids.empty() && ids.back() == e.first) {
+        tot.back() += e.second;
+      } else {
+        ids.push_back(e.first);
+        tot.push_back(e.second);
+      }
+    }
+    if (ids.empty()) return;
+    const uint32_t m = (uint32_t)ids.size();
+    uint32_t* d_ids = hs->ctx->d_lists.get<uint32_t>(m);
+    uint64_t* d_tot = hs->ctx->d_keys.get<uint64_t>(m);
+    hipStream_t st = hs->ctx->stream;
+    SG_HIP(hipMemcpyAsync(d_ids, ids.data(), (size_t)m * 4, hipMemcpyHostToDevice, st));
+    SG_HIP(hipMemcpyAsync(d_tot, tot.data(), (size_t)m * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(sg::k_hosts_skip, dim3(sg::grid_for(m, 256)), dim3(256), 0, st, d_ids, d_tot, m, hs->n, hs->rng);
+    SG_CHECK_LAUNCH();
+    SG_HIP(hipStreamSynchronize(st));
   });
 }
 

@@ -27,7 +27,9 @@
 // lands on a later guess.  The result, including which error is reported
 // first, is the single-threaded parse's.
 #include <algorithm>
+#include <dlfcn.h>
 #include <charconv>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -653,9 +655,158 @@ void parse_into(const char* text, size_t len, unsigned threads, sg_gml* g) {
     if (!m.empty()) throw ParseError{m};
 }
 
+// ---- load_network_graph (graph/mod.rs:483-513): the file, plain or xz ------
+//
+// xz goes through the system liblzma (liblzma.so.5, the library Python's lzma
+// module wraps; lzma_rs::xz_decompress in the reference), opened with dlopen: the
+// image ships the library but not lzma.h, so the few entry points used are
+// declared here from liblzma's public, stable ABI (lzma/base.h, lzma/container.h).
+struct LzmaStream {  // lzma_stream
+  const uint8_t* next_in;
+  size_t avail_in;
+  uint64_t total_in;
+  uint8_t* next_out;
+  size_t avail_out;
+  uint64_t total_out;
+  const void* allocator;
+  void* internal;
+  void* reserved_ptr[4];
+  uint64_t reserved_int[2];
+  size_t reserved_sz[2];
+  int reserved_enum[2];
+};
+struct Lzma {
+  int (*stream_decoder)(LzmaStream*, uint64_t memlimit, uint32_t flags);
+  int (*code)(LzmaStream*, int action);
+  void (*end)(LzmaStream*);
+  bool ok = false;
+  Lzma() {
+    void* h = dlopen("liblzma.so.5", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    stream_decoder = (int (*)(LzmaStream*, uint64_t, uint32_t))dlsym(h, "lzma_stream_decoder");
+    code = (int (*)(LzmaStream*, int))dlsym(h, "lzma_code");
+    end = (void (*)(LzmaStream*))dlsym(h, "lzma_end");
+    ok = stream_decoder && code && end;
+  }
+};
+constexpr int LZMA_OK_ = 0, LZMA_STREAM_END_ = 1, LZMA_FINISH_ = 3;
+
+// read_xz (graph/mod.rs:484-496): one .xz stream, decompressed whole
+static std::string xz_decompress(const std::string& packed, const char* path) {
+  static Lzma lz;
+  if (!lz.ok) throw ParseError{std::string("Failed to decompress file: liblzma.so.5 not available (") + path + ")"};
+  LzmaStream st;
+  memset(&st, 0, sizeof(st));  // LZMA_STREAM_INIT
+  if (lz.stream_decoder(&st, UINT64_MAX, 0) != LZMA_OK_) throw ParseError{"Failed to decompress file: decoder init"};
+  std::string out;
+  out.resize(std::max<size_t>(packed.size() * 4, 1 << 16));
+  st.next_in = (const uint8_t*)packed.data();
+  st.avail_in = packed.size();
+  size_t done = 0;
+  for (;;) {
+    st.next_out = (uint8_t*)&out[done];
+    st.avail_out = out.size() - done;
+    const int rc = lz.code(&st, LZMA_FINISH_);
+    done = out.size() - st.avail_out;
+    if (rc == LZMA_STREAM_END_) break;
+    if (rc != LZMA_OK_) {
+      lz.end(&st);
+      throw ParseError{"Failed to decompress file: liblzma error " + std::to_string(rc)};
+    }
+    if (!st.avail_out) out.resize(out.size() * 2);
+    else if (!st.avail_in) {  // input ended inside the stream
+      lz.end(&st);
+      throw ParseError{"Failed to decompress file: truncated xz stream"};
+    }
+  }
+  lz.end(&st);
+  out.resize(done);
+  return out;
+}
+
+// String::from_utf8 / read_to_string: well-formed UTF-8 (no overlong forms, no
+// surrogates, nothing past U+10FFFF)
+static bool utf8_valid(const std::string& t) {
+  const unsigned char* p = (const unsigned char*)t.data();
+  const size_t n = t.size();
+  size_t i = 0;
+  while (i < n) {
+    while (i + 8 <= n) {  // ASCII fast path, 8 bytes at a time
+      uint64_t w;
+      memcpy(&w, p + i, 8);
+      if (w & 0x8080808080808080ull) break;
+      i += 8;
+    }
+    if (i >= n) break;
+    const unsigned c = p[i];
+    if (c < 0x80) {
+      i++;
+      continue;
+    }
+    int len;
+    unsigned lo = 0x80, hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF) len = 2;
+    else if (c >= 0xE0 && c <= 0xEF) {
+      len = 3;
+      if (c == 0xE0) lo = 0xA0;
+      if (c == 0xED) hi = 0x9F;
+    } else if (c >= 0xF0 && c <= 0xF4) {
+      len = 4;
+      if (c == 0xF0) lo = 0x90;
+      if (c == 0xF4) hi = 0x8F;
+    } else {
+      return false;
+    }
+    if (i + len > n) return false;
+    if (p[i + 1] < lo || p[i + 1] > hi) return false;
+    for (int k = 2; k < len; k++)
+      if ((p[i + k] & 0xC0) != 0x80) return false;
+    i += len;
+  }
+  return true;
+}
+
+static std::string read_file(const char* path) {
+  FILE* f = fopen(path, "rb");
+  if (!f) throw ParseError{std::string("Failed to read file: ") + path};
+  std::string t;
+  char buf[1 << 16];
+  size_t k;
+  while ((k = fread(buf, 1, sizeof buf, f)) > 0) t.append(buf, k);
+  const bool bad = ferror(f);
+  fclose(f);
+  if (bad) throw ParseError{std::string("Failed to read file: ") + path};
+  return t;
+}
+
 }  // namespace
 
 extern "C" {
+
+int32_t sg_gml_load(const char* path, uint32_t compression, uint32_t threads, sg_gml** out, char* err,
+                    size_t err_len) {
+  if (!out || !path || compression > 1) return SG_ERR_INVALID_ARG;
+  *out = nullptr;
+  std::string text;
+  try {
+    std::string p = path;
+    if (p.size() >= 2 && p[0] == '~' && p[1] == '/' && getenv("HOME")) p = getenv("HOME") + p.substr(1);  // tilde_expansion
+    text = read_file(p.c_str());
+    if (compression == 1) text = xz_decompress(text, p.c_str());
+    if (!utf8_valid(text))
+      throw ParseError{compression == 1 ? "invalid utf-8 sequence (String::from_utf8)"
+                                        : "Failed to read file: " + p + ": stream did not contain valid UTF-8"};
+  } catch (const ParseError& e) {
+    if (err && err_len) {
+      strncpy(err, e.msg.c_str(), err_len - 1);
+      err[err_len - 1] = 0;
+    }
+    return SG_ERR_PARSE;
+  } catch (const std::bad_alloc&) {
+    return SG_ERR_OOM;
+  }
+  return sg_gml_parse_threads(text.data(), text.size(), threads, out, err, err_len);
+}
 
 int32_t sg_gml_parse_threads(const char* text, size_t len, uint32_t threads, sg_gml** out, char* err,
                              size_t err_len) {

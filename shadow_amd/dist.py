@@ -145,6 +145,8 @@ def gpu_source_phase(ctx, hosts, table, packets, round_end_ns, sim_end_ns, boots
     p.n_packets = n
     p.src_host, p.dst_ipv4 = packets.src_host.data_ptr(), packets.dst_ipv4.data_ptr()
     p.payload_len, p.send_time_ns = packets.payload_len.data_ptr(), packets.send_time_ns.data_ptr()
+    skip = getattr(packets, "rng_skip", None)
+    p.rng_skip = skip.data_ptr() if skip is not None else None
     r = _capi.sg_round(round_end_ns, sim_end_ns, bootstrap_end_ns)
     st = _capi.sg_round_stats()
     t = table.struct()

@@ -240,6 +240,11 @@ class NetworkGraph:
         rc = L.sg_gml_parse_threads(raw, len(raw), int(threads), C.byref(h), err, len(err))
         if rc != _capi.SG_OK:
             raise ShadowGpuError(rc, err.value.decode(errors="replace") or f"parse status {rc}")
+        return cls._from_handle(h, ctx)
+
+    @classmethod
+    def _from_handle(cls, h, ctx) -> "NetworkGraph":
+        L = load()
         try:
             g = _capi.sg_graph()
             check(None, L.sg_gml_graph(h, C.byref(g)))
@@ -254,24 +259,20 @@ class NetworkGraph:
     @classmethod
     def from_file(cls, path, compression: Optional[str] = None, ctx: Optional[Context] = None,
                   threads: int = 0) -> "NetworkGraph":
-        """load_network_graph + NetworkGraph::parse (graph/mod.rs:483-513): a GML file, plain or
-        xz-compressed (compression="xz", as lzma_rs::xz_decompress; here the system liblzma
-        through Python's lzma module).  The text must be UTF-8 (String::from_utf8)."""
-        import os
-
-        path = os.path.expanduser(str(path))  # tilde_expansion
-        if compression is None:
-            with open(path, "rb") as f:
-                raw = f.read()
-        elif compression == "xz":
-            import lzma
-
-            with lzma.open(path, "rb", format=lzma.FORMAT_XZ) as f:
-                raw = f.read()
-        else:
+        """load_network_graph + NetworkGraph::parse (graph/mod.rs:483-513) in the native
+        library (sg_gml_load): a GML file, plain or xz-compressed (compression="xz", read_xz
+        :484-496; decompressed by the system liblzma), checked to be UTF-8
+        (String::from_utf8), then parsed on `threads` threads."""
+        if compression not in (None, "xz"):
             raise ValueError(f"unknown compression {compression!r} (configuration.rs:985-988: xz)")
-        raw.decode("utf-8")  # Err(FromUtf8Error) in the reference
-        return cls.parse(raw, ctx=ctx, threads=threads)
+        L = load()
+        h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        rc = L.sg_gml_load(str(path).encode(), 1 if compression == "xz" else 0, int(threads), C.byref(h), err,
+                           len(err))
+        if rc != _capi.SG_OK:
+            raise ShadowGpuError(rc, err.value.decode(errors="replace") or f"load status {rc}")
+        return cls._from_handle(h, ctx)
 
     def node_id_to_index(self, node_id: int) -> Optional[int]:
         if self._id_to_index is None:  # graph/mod.rs:155-162: a later duplicate id wins

@@ -87,6 +87,14 @@ class HostTable:
         check(self.ctx.handle, load().sg_hosts_set_state(self.handle, None if r is None else r.ctypes.data,
                                                          None if c is None else c.ctypes.data))
 
+    def skip(self, host_ids, steps) -> None:
+        """Advance hosts' device RNG streams by the steps other consumers took
+        (sg_hosts_skip; see PacketBatch.rng_skip).  A host may repeat."""
+        ids = np.ascontiguousarray(host_ids, dtype=np.uint32)
+        st = np.ascontiguousarray(steps, dtype=np.uint64)
+        assert len(ids) == len(st)
+        check(self.ctx.handle, load().sg_hosts_skip(self.handle, len(ids), ids.ctypes.data, st.ctypes.data))
+
     def __del__(self):
         try:
             if getattr(self, "handle", None):
@@ -143,11 +151,14 @@ class PacketBatch:
     dst_ipv4: "object"     # int32 device tensor (u32 bits)
     payload_len: "object"  # int32 device tensor
     send_time_ns: "object"  # int64 device tensor (u64 bits)
+    # int32 device tensor (u32 bits) or None: RNG steps the source host's other
+    # consumers (syscalls, host.rs:645-647) took since its previous packet (sg_packets.rng_skip)
+    rng_skip: "object" = None
 
     @classmethod
-    def from_numpy(cls, src_host, dst_ipv4, payload_len, send_time_ns, device="cuda"):
+    def from_numpy(cls, src_host, dst_ipv4, payload_len, send_time_ns, device="cuda", rng_skip=None):
         return cls(_dev_u32(src_host, device), _dev_u32(dst_ipv4, device), _dev_u32(payload_len, device),
-                   _dev_u64(send_time_ns, device))
+                   _dev_u64(send_time_ns, device), None if rng_skip is None else _dev_u32(rng_skip, device))
 
     def __len__(self):
         return int(self.src_host.numel())
@@ -158,9 +169,10 @@ class PacketBatch:
             p.n_packets = len(self)
             p.src_host, p.dst_ipv4 = self.src_host.data_ptr(), self.dst_ipv4.data_ptr()
             p.payload_len, p.send_time_ns = self.payload_len.data_ptr(), self.send_time_ns.data_ptr()
+            p.rng_skip = self.rng_skip.data_ptr() if self.rng_skip is not None else None
             return p
 
-        return _cached(self, ("src_host", "dst_ipv4", "payload_len", "send_time_ns"), build)
+        return _cached(self, ("src_host", "dst_ipv4", "payload_len", "send_time_ns", "rng_skip"), build)
 
 
 @dataclass

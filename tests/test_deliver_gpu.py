@@ -215,6 +215,39 @@ def test_consecutive_rounds_keep_streams(oracle, ctx):
         _assert_same(want, out.to_numpy(15000), (rng, ctr), ht.get_state())
 
 
+def test_interleaved_rng_consumers(oracle, ctx):
+    """sg_packets.rng_skip: the source host's other Host::random_mut() consumers
+    (getrandom, port choices, host_rngDouble; host.rs:645-647) took rng_skip[i]
+    steps before packet i.  Three rounds with skips on every kind of packet
+    (delivered, lost, unknown destination, past sim end), then sg_hosts_skip for
+    steps no later packet carried (hosts repeated), against the oracle."""
+    lat, loss, hosts = _world(n_hosts=800, seed=6)
+    ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    rng, ctr = ht.get_state()
+    tab = _device_table(lat, loss)
+    g = np.random.default_rng(17)
+    for k in range(3):
+        start, end = T0 + k * 10**6, T0 + (k + 1) * 10**6
+        pk = synth.make_packets(20000, hosts, start, end, seed=60 + k, p_unknown_dst=0.02)
+        sim_end = end + 10**9 if k < 2 else start + 500_000  # the last round crosses sim end
+        skip = np.where(g.random(20000) < 0.7, 0, g.integers(1, 6, 20000)).astype(np.uint32)
+        skip[::1999] = 300  # a long syscall burst
+        want = oracle.deliver_round(end, sim_end, 0, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
+                                    hosts["ip"], hosts["route"], lat, loss, rng, ctr, rng_skip=skip)
+        out = deliver_round(ht, tab, PacketBatch.from_numpy(pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
+                                                            rng_skip=skip), end, sim_end, 0)
+        _assert_same(want, out.to_numpy(20000), (rng, ctr), ht.get_state())
+        assert (want["status"] == oracle.ST_SIM_END).any() == (k == 2)
+    ids = np.array([3, 5, 3, 799, 0], np.uint32)
+    steps = np.array([2, 1, 4, 10, 1], np.uint64)
+    ht.skip(ids, steps)
+    for h, n in zip(ids, steps):
+        for _ in range(int(n)):
+            oracle.xoshiro_next_u64(rng[h])
+    grng, gctr = ht.get_state()
+    assert np.array_equal(grng, rng) and np.array_equal(gctr, ctr)
+
+
 def test_edge_cases(oracle, ctx):
     lat, loss, hosts = _world(n_hosts=40, seed=6)
     # empty round

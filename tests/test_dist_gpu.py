@@ -27,7 +27,7 @@ def _world(oracle, n_nodes=90, n_hosts=1500, seed=3):
     return lat, loss, hosts
 
 
-def _run(oracle, ctx, W, n_packets, hot=None, seed=1, p_hot=0.1):
+def _run(oracle, ctx, W, n_packets, hot=None, seed=1, p_hot=0.1, skip=False):
     import torch
 
     lat, loss, hosts = _world(oracle, seed=seed)
@@ -36,6 +36,7 @@ def _run(oracle, ctx, W, n_packets, hot=None, seed=1, p_hot=0.1):
     start, end = T0 + 10**9, T0 + 10**9 + 10**6
     pk = synth.make_packets(n_packets, hosts, start, end, seed=seed + 10, p_unknown_dst=0.01,
                             hot_dst=-1 if hot is None else hot, p_hot=0.0 if hot is None else p_hot)
+    rs = np.random.default_rng(seed).integers(0, 4, n_packets).astype(np.uint32) if skip else None
     owner_of_pkt = part.owner[pk["src"]]
     ranks = []
     for r in range(W):
@@ -47,7 +48,8 @@ def _run(oracle, ctx, W, n_packets, hot=None, seed=1, p_hot=0.1):
         table = DeviceTable(dl, df, nu, r0)
         if r % 2:  # odd ranks gather from the packed path-key table (row block offset r0)
             assert table.pack(ctx)
-        batch = PacketBatch.from_numpy(pk["src"][sel], pk["dst_ip"][sel], pk["payload"][sel], pk["send_time"][sel])
+        batch = PacketBatch.from_numpy(pk["src"][sel], pk["dst_ip"][sel], pk["payload"][sel], pk["send_time"][sel],
+                                       rng_skip=None if rs is None else rs[sel])
         ranks.append(dict(sel=sel, ht=ht, table=table, batch=batch))
     # source phases
     sends = []
@@ -73,7 +75,7 @@ def _run(oracle, ctx, W, n_packets, hot=None, seed=1, p_hot=0.1):
     ht0 = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
     rng, ctr = ht0.get_state()
     want = oracle.deliver_round(end, 2**63, start + 200_000, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
-                                hosts["ip"], hosts["route"], lat, loss, rng, ctr)
+                                hosts["ip"], hosts["route"], lat, loss, rng, ctr, rng_skip=rs)
     # per-packet outputs + host streams
     for r, R in enumerate(ranks):
         sel = R["sel"]
@@ -101,6 +103,12 @@ def _run(oracle, ctx, W, n_packets, hot=None, seed=1, p_hot=0.1):
 @pytest.mark.parametrize("W", [1, 2, 3, 8])
 def test_sharded_round_matches_single(oracle, ctx, W):
     want = _run(oracle, ctx, W, 30000)
+    assert want["delivered"] > 0
+
+
+def test_sharded_round_with_rng_skip(oracle, ctx):
+    """Other RNG consumers' steps (sg_packets.rng_skip) on the sharded source phase."""
+    want = _run(oracle, ctx, 3, 30000, skip=True)
     assert want["delivered"] > 0
 
 

@@ -125,5 +125,45 @@ def test_from_file_plain_and_xz(tmp_path):
     b = NetworkGraph.from_file(xz, compression="xz")
     _same(a, b)
     assert np.array_equal(b.edge_dst, g["dst"])
-    with pytest.raises(lzma.LZMAError):
-        NetworkGraph.from_file(plain, compression="xz")  # "Failed to decompress file"
+    with pytest.raises(ShadowGpuError, match="Failed to decompress file"):
+        NetworkGraph.from_file(plain, compression="xz")
+    # a truncated stream, a missing file, invalid UTF-8 (String::from_utf8 / read_to_string)
+    cut = tmp_path / "cut.gml.xz"
+    cut.write_bytes(xz.read_bytes()[:-40])
+    with pytest.raises(ShadowGpuError, match="Failed to decompress file"):
+        NetworkGraph.from_file(cut, compression="xz")
+    with pytest.raises(ShadowGpuError, match="Failed to read file"):
+        NetworkGraph.from_file(tmp_path / "absent.gml")
+    bad = tmp_path / "bad.gml"
+    bad.write_bytes(text.encode().replace(b"graph [", b"graph [ \xc0\xaf", 1))
+    with pytest.raises(ShadowGpuError, match="UTF-8"):
+        NetworkGraph.from_file(bad)
+    badxz = tmp_path / "bad.gml.xz"
+    with lzma.open(badxz, "wb", format=lzma.FORMAT_XZ) as f:
+        f.write(b"graph [ \xed\xa0\x80 ]")  # an encoded surrogate
+    with pytest.raises(ShadowGpuError, match="utf-8"):
+        NetworkGraph.from_file(badxz, compression="xz")
+    # threads: the same graph from the xz file on 1 and 8 threads
+    _same(NetworkGraph.from_file(xz, compression="xz", threads=1), NetworkGraph.from_file(xz, compression="xz",
+                                                                                           threads=8))
+
+
+def test_utf8_check_matches_python(tmp_path):
+    """sg_gml_load's UTF-8 check accepts exactly what a strict decoder accepts."""
+    rng = np.random.default_rng(3)
+    cases = [b"\xf4\x90\x80\x80", b"\xf0\x8f\xbf\xbf", b"\xe0\x9f\xbf", b"\xc1\xbf", b"\xef\xbf\xbf",
+             b"\xf4\x8f\xbf\xbf", b"\xe2\x82", "\u00e9\u4e2d\U0001f600".encode()]
+    cases += [bytes(rng.integers(0x80, 0x100, 3).astype(np.uint8)) for _ in range(200)]
+    for k, c in enumerate(cases):
+        f = tmp_path / f"u{k}.gml"
+        f.write_bytes(b"graph [\n  label \"" + c + b"\"\n  node [\n    id 0\n  ]\n]")
+        try:
+            c.decode("utf-8")
+            ok = True
+        except UnicodeDecodeError:
+            ok = False
+        if ok:
+            NetworkGraph.from_file(f)
+        else:
+            with pytest.raises(ShadowGpuError, match="UTF-8"):
+                NetworkGraph.from_file(f)

@@ -246,6 +246,69 @@ def test_deliver_semantics(oracle):
     assert r["dst_offsets"].tolist() == [0, 0, len(delivered)]
 
 
+def test_deliver_interleaved_rng_consumers(oracle):
+    """Host::random_mut() is one stream shared by send_packet's draw (worker.rs:360)
+    and other consumers (getrandom, random.rs:40; socket port choices; host_rngDouble).
+    A host's event log -- syscall draws interleaved with sends -- replayed step by
+    step must match the round run with per-packet rng_skip counts (sg_packets.rng_skip),
+    whatever each packet's status."""
+    lat, loss, host_ip, host_row = _tiny_world()
+    seeds = [31, 32]
+    # per host: ("sys", steps) = a syscall taking `steps` next_u64 steps; ("send", dst, payload, time)
+    log = {0: [("sys", 3), ("send", 200, 10, 100), ("send", 999, 10, 110), ("sys", 1), ("sys", 2),
+               ("send", 200, 10, 120), ("send", 200, 10, 20_000), ("sys", 4), ("send", 200, 0, 130)],
+           1: [("send", 100, 10, 100), ("sys", 7), ("send", 100, 10, 140), ("send", 200, 10, 150)]}
+    sim_end = 10_000
+    src, dst, pay, t, skip = [], [], [], [], []
+    want_st = []
+    rel = {(0, 1): float(np.float32(1) - np.float32(0.5)), (1, 0): float(np.float32(1) - np.float32(0.5)),
+           (0, 0): 1.0, (1, 1): 1.0}
+    model = {h: oracle.xoshiro_seed(seeds[h]) for h in log}
+    ip_host = {100: 0, 200: 1}
+    for h, events in log.items():
+        pending = 0
+        for ev in events:
+            if ev[0] == "sys":
+                pending += ev[1]
+                for _ in range(ev[1]):
+                    oracle.xoshiro_next_u64(model[h])
+                continue
+            _, d, p, tt = ev
+            src.append(h), dst.append(d), pay.append(p), t.append(tt), skip.append(pending)
+            pending = 0
+            if tt >= sim_end:
+                want_st.append(oracle.ST_SIM_END)
+            elif d not in ip_host:
+                want_st.append(oracle.ST_DROP_NO_DST)
+            else:
+                chance = oracle.xoshiro_next_f64(model[h])
+                drop = chance >= rel[(h, ip_host[d])] and p > 0
+                want_st.append(oracle.ST_DROP_LOSS if drop else oracle.ST_DELIVERED)
+        # trailing syscall draws after the host's last send stay with the CPU (sg_hosts_skip carries them)
+    rng = np.stack([oracle.xoshiro_seed(s_) for s_ in seeds])
+    ctr = np.zeros(2, np.uint64)
+    r = oracle.deliver_round(1000, sim_end, 0, src, dst, pay, t, host_ip, host_row, lat, loss, rng, ctr,
+                             rng_skip=skip)
+    assert r["status"].tolist() == want_st
+    for h in log:
+        tail = 0
+        for ev in reversed(log[h]):
+            if ev[0] != "sys":
+                break
+            tail += ev[1]
+        s_ = rng[h].copy()
+        for _ in range(tail):
+            oracle.xoshiro_next_u64(s_)
+        assert np.array_equal(s_, model[h]), h
+    # no skips = the plain round
+    rng0 = np.stack([oracle.xoshiro_seed(s_) for s_ in seeds])
+    a = oracle.deliver_round(1000, sim_end, 0, src, dst, pay, t, host_ip, host_row, lat, loss, rng0.copy(),
+                             np.zeros(2, np.uint64), rng_skip=[0] * len(src))
+    b = oracle.deliver_round(1000, sim_end, 0, src, dst, pay, t, host_ip, host_row, lat, loss, rng0.copy(),
+                             np.zeros(2, np.uint64))
+    assert np.array_equal(a["status"], b["status"]) and np.array_equal(a["deliver_time"], b["deliver_time"])
+
+
 def test_deliver_bootstrap_and_order(oracle):
     lat, loss, host_ip, host_row = _tiny_world()
     loss[:] = 1.0  # everything would drop ...
