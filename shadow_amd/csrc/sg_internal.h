@@ -91,7 +91,7 @@ struct sg_ctx {
   std::string last_error;
   uint32_t err_row = 0, err_col = 0;
   // routing workspace
-  sg::DevBuf r_dist, r_dist2, r_flags, r_used, r_err, r_pair_cnt, r_pair_edge, r_map, r_out_lat,
+  sg::DevBuf r_dist, r_dist2, r_flags, r_used, r_err, r_self, r_pair_cnt, r_pair_edge, r_map, r_out_lat,
       r_out_loss, r_misc, r_dirty, r_work, r_items, r_plan;
   // delivery workspace
   sg::DevBuf d_seg, d_dst, d_cnt, d_cur, d_keys, d_vals, d_keys2, d_vals2, d_keys3, d_keys4, d_misc,

@@ -60,82 +60,83 @@ constexpr int WORK_SHARDS = 64;  // relaxation counter shards (measurement only)
 // Graph upload: CSC of in-arcs (both directions when undirected, petgraph
 // semantics graph/mod.rs:137-152), self-loop census for get_edge_weight(n, n).
 // ---------------------------------------------------------------------------
-__global__ void k_count_arcs(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                             uint32_t m, int directed, uint32_t* __restrict__ indeg,
-                             uint32_t* __restrict__ self_cnt, uint32_t* __restrict__ self_edge) {
+// One pass over the edges for both arc lists and the self-loop census (a graph
+// upload is part of every one-shot build: three launches instead of six).
+__global__ void k_net_count(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst, uint32_t m,
+                            int directed, uint32_t* __restrict__ indeg, uint32_t* __restrict__ outdeg,
+                            uint32_t* __restrict__ self_cnt, uint32_t* __restrict__ self_edge) {
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < m; e += gridDim.x * blockDim.x) {
-    uint32_t s = src[e], d = dst[e];
+    const uint32_t s = src[e], d = dst[e];
     if (s == d) {
       atomicAdd(&self_cnt[s], 1u);
       self_edge[s] = e;  // meaningful only when the count ends at 1
-    } else {
-      atomicAdd(&indeg[d], 1u);
-      if (!directed) atomicAdd(&indeg[s], 1u);
+      continue;
+    }
+    atomicAdd(&indeg[d], 1u);
+    atomicAdd(&outdeg[s], 1u);
+    if (!directed) {
+      atomicAdd(&indeg[s], 1u);
+      atomicAdd(&outdeg[d], 1u);
     }
   }
 }
 
-__global__ void k_scatter_arcs(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                               const uint64_t* __restrict__ lat, const float* __restrict__ loss,
-                               uint32_t m, int directed, uint32_t* __restrict__ cursor,
-                               uint32_t* __restrict__ in_src, uint32_t* __restrict__ in_dst,
-                               uint64_t* __restrict__ in_lat, uint32_t* __restrict__ in_lat32,
-                               float* __restrict__ in_om, uint4* __restrict__ in_rec) {
+// Exclusive scans of indeg and outdeg (n + 1 entries each, the last one the
+// total) in one workgroup, each result written twice: the offsets and the
+// scatter's cursors.  For graphs up to NET_SCAN_SMALL nodes.
+constexpr uint32_t NET_SCAN_SMALL = 1u << 17;
+__global__ void __launch_bounds__(1024) k_net_scan(const uint32_t* __restrict__ indeg, const uint32_t* __restrict__ outdeg,
+                                                   uint32_t n, uint32_t* __restrict__ in_off, uint32_t* __restrict__ in_cur,
+                                                   uint32_t* __restrict__ out_off, uint32_t* __restrict__ out_cur) {
+  __shared__ uint32_t s_w[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t per = (n + 1 + 1023) / 1024;  // consecutive entries per thread
+  for (int k = 0; k < 2; k++) {
+    const uint32_t* x = k ? outdeg : indeg;
+    uint32_t* o1 = k ? out_off : in_off;
+    uint32_t* o2 = k ? out_cur : in_cur;
+    const uint32_t b = tid * per, e = min(b + per, n + 1);
+    uint32_t sum = 0;
+    for (uint32_t i = b; i < e; i++) sum += i < n ? x[i] : 0u;
+    const uint32_t incl = wave_incl_sum(sum);
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (int w = 0; w < wv; w++) run += s_w[w];
+    for (uint32_t i = b; i < e; i++) {
+      o1[i] = run;
+      o2[i] = run;
+      run += i < n ? x[i] : 0u;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_net_scatter(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                              const uint64_t* __restrict__ lat, const float* __restrict__ loss, uint32_t m,
+                              int directed, uint32_t* __restrict__ cursor, uint32_t* __restrict__ in_src,
+                              uint32_t* __restrict__ in_dst, uint64_t* __restrict__ in_lat,
+                              uint32_t* __restrict__ in_lat32, float* __restrict__ in_om, uint4* __restrict__ in_rec,
+                              uint32_t* __restrict__ ocursor, uint32_t* __restrict__ out_arc) {
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < m; e += gridDim.x * blockDim.x) {
-    uint32_t s = src[e], d = dst[e];
+    const uint32_t s = src[e], d = dst[e];
     if (s == d) continue;  // a self-loop never improves D[s][v] (latency >= 1)
     const float om = __fsub_rn(1.0f, loss[e]);
     const uint64_t l = lat[e];
     const uint32_t l32 = l < LAT32_SAT ? (uint32_t)l : LAT32_SAT;
-    uint32_t p = atomicAdd(&cursor[d], 1u);
-    in_src[p] = s;
-    in_dst[p] = d;
-    in_lat[p] = l;
-    in_lat32[p] = l32;
-    in_om[p] = om;
-    in_rec[p] = make_uint4(s, d, l32, __float_as_uint(om));
-    if (!directed) {
-      uint32_t q = atomicAdd(&cursor[s], 1u);
-      in_src[q] = d;
-      in_dst[q] = s;
-      in_lat[q] = l;
-      in_lat32[q] = l32;
-      in_om[q] = om;
-      in_rec[q] = make_uint4(d, s, l32, __float_as_uint(om));
-    }
-  }
-}
-
-// Out-arc CSR (tail-grouped) for the per-source search: the same arcs as the
-// CSC, both directions when undirected, self-loops dropped.
-__global__ void k_count_out(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst, uint32_t m,
-                            int directed, uint32_t* __restrict__ outdeg) {
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < m; e += gridDim.x * blockDim.x) {
-    const uint32_t s = src[e], d = dst[e];
-    if (s == d) continue;
-    atomicAdd(&outdeg[s], 1u);
-    if (!directed) atomicAdd(&outdeg[d], 1u);
-  }
-}
-
-__global__ void k_scatter_out(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                              const uint64_t* __restrict__ lat, const float* __restrict__ loss, uint32_t m,
-                              int directed, uint32_t* __restrict__ cursor, uint32_t* __restrict__ out_arc) {
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < m; e += gridDim.x * blockDim.x) {
-    const uint32_t s = src[e], d = dst[e];
-    if (s == d) continue;
-    const uint32_t om = __float_as_uint(__fsub_rn(1.0f, loss[e]));
-    const uint64_t l = lat[e];
-    const uint32_t l32 = l < LAT32_SAT ? (uint32_t)l : LAT32_SAT;
-    uint32_t p = atomicAdd(&cursor[s], 1u);
-    out_arc[3 * (size_t)p] = d;
-    out_arc[3 * (size_t)p + 1] = l32;
-    out_arc[3 * (size_t)p + 2] = om;
-    if (!directed) {
-      p = atomicAdd(&cursor[d], 1u);
-      out_arc[3 * (size_t)p] = s;
-      out_arc[3 * (size_t)p + 1] = l32;
-      out_arc[3 * (size_t)p + 2] = om;
+    for (int dir = 0; dir < (directed ? 1 : 2); dir++) {
+      const uint32_t a = dir ? d : s, b = dir ? s : d;  // the arc a -> b
+      const uint32_t p = atomicAdd(&cursor[b], 1u);
+      in_src[p] = a;
+      in_dst[p] = b;
+      in_lat[p] = l;
+      in_lat32[p] = l32;
+      in_om[p] = om;
+      in_rec[p] = make_uint4(a, b, l32, __float_as_uint(om));
+      const uint32_t q = atomicAdd(&ocursor[a], 1u);
+      out_arc[3 * (size_t)q] = b;
+      out_arc[3 * (size_t)q + 1] = l32;
+      out_arc[3 * (size_t)q + 2] = __float_as_uint(om);
     }
   }
 }
@@ -999,37 +1000,50 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   uint32_t* indeg = ctx->r_misc.get<uint32_t>(2 * ((size_t)n + 1));
   uint32_t* outdeg = indeg + n + 1;
   SG_HIP(hipMemsetAsync(indeg, 0, 2 * ((size_t)n + 1) * 4, st));
-  SG_HIP(hipMemsetAsync(net->self_cnt, 0, (size_t)n * 4, st));  // (self_edge is read only where the count is 1)
+  // self_cnt and self_edge (adjacent): self_edge stays 0 where no self-loop sets it, so a
+  // build that reads it before the self-loop check's error is raised stays in bounds
+  SG_HIP(hipMemsetAsync(net->self_cnt, 0, o_insrc - o_scnt, st));
   if (m) {
-    hipLaunchKernelGGL(k_count_arcs, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src,
-                       net->e_dst, m, (int)net->directed, indeg, net->self_cnt, net->self_edge);
-    hipLaunchKernelGGL(k_count_out, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst, m,
-                       (int)net->directed, outdeg);
+    hipLaunchKernelGGL(k_net_count, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst, m,
+                       (int)net->directed, indeg, outdeg, net->self_cnt, net->self_edge);
     SG_CHECK_LAUNCH();
   }
-  exclusive_scan_u32(ctx, indeg, net->in_off, n);
-  exclusive_scan_u32(ctx, outdeg, net->out_off, n);
-  if (n_arcs) {
-    uint32_t* cursor = ctx->r_map.get<uint32_t>(2 * ((size_t)n + 1));
-    uint32_t* ocursor = cursor + n + 1;
+  uint32_t* cursor = ctx->r_map.get<uint32_t>(2 * ((size_t)n + 1));
+  uint32_t* ocursor = cursor + n + 1;
+  if (n < NET_SCAN_SMALL) {
+    hipLaunchKernelGGL(k_net_scan, dim3(1), dim3(1024), 0, st, indeg, outdeg, n, net->in_off, cursor, net->out_off,
+                       ocursor);
+    SG_CHECK_LAUNCH();
+  } else {
+    exclusive_scan_u32(ctx, indeg, net->in_off, n);
+    exclusive_scan_u32(ctx, outdeg, net->out_off, n);
     SG_HIP(hipMemcpyAsync(cursor, net->in_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
     SG_HIP(hipMemcpyAsync(ocursor, net->out_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(k_scatter_arcs, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src,
-                       net->e_dst, net->e_lat, net->e_loss, m, (int)net->directed, cursor,
-                       net->in_src, net->in_dst, net->in_lat, net->in_lat32, net->in_om, net->in_rec);
-    hipLaunchKernelGGL(k_scatter_out, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst,
-                       net->e_lat, net->e_loss, m, (int)net->directed, ocursor, net->out_arc);
+  }
+  if (n_arcs) {
+    hipLaunchKernelGGL(k_net_scatter, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst,
+                       net->e_lat, net->e_loss, m, (int)net->directed, cursor, net->in_src, net->in_dst, net->in_lat,
+                       net->in_lat32, net->in_om, net->in_rec, ocursor, net->out_arc);
     SG_CHECK_LAUNCH();
   }
 }
 
-static void check_self_loops(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
-                             const uint32_t* h_used) {
-  unsigned long long* first = ctx->r_err.get<unsigned long long>(4);
+// The self-loop check of every used node (graph/mod.rs:210-217) runs ahead of the
+// search without a host round trip; its result is read once the build has
+// synchronised (raise_self_loops), and an error found there wins over any the
+// search raised, as in the reference, where the self-loops are checked before the
+// n^2 assertion (:219).  The search reads self_edge only at count 1 (and it is
+// zeroed elsewhere), so it stays in bounds on a graph the check rejects.
+static unsigned long long* launch_self_loops(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used) {
+  unsigned long long* first = ctx->r_self.get<unsigned long long>(4);  // (its own word: the build uses r_err)
   SG_HIP(hipMemsetAsync(first, 0xff, 8, ctx->stream));
   hipLaunchKernelGGL(k_self_check, dim3(grid_for(n_used, 256, 4096)), dim3(256), 0, ctx->stream,
                      d_used, n_used, net->self_cnt, first);
   SG_CHECK_LAUNCH();
+  return first;
+}
+
+static void raise_self_loops(sg_ctx* ctx, sg_net* net, const unsigned long long* first, const uint32_t* h_used) {
   unsigned long long h = 0;
   copy_to_host(ctx, &h, first, 8);
   if (h != ~0ull) {
@@ -1536,15 +1550,24 @@ int32_t sg_routing_build(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32
     const bool shortest = flags & SG_ROUTE_SHORTEST_PATH;
     // The reference checks every used node's self-loop (graph/mod.rs:211-217),
     // whichever rows this call computes.
-    if (shortest) check_self_loops(ctx, net, d_used, n_used, nodes);
-    if (row_end == row_begin) return;
+    const unsigned long long* self_first = shortest ? launch_self_loops(ctx, net, d_used, n_used) : nullptr;
+    if (row_end == row_begin) {
+      if (self_first) raise_self_loops(ctx, net, self_first, nodes);
+      return;
+    }
     const size_t count = (size_t)(row_end - row_begin) * n_used;
     const bool dev_out = flags & SG_ROUTE_OUT_DEVICE;
     uint64_t* o_lat = dev_out ? out_latency_ns : ctx->r_out_lat.get<uint64_t>(count);
     float* o_loss = dev_out ? out_packet_loss : ctx->r_out_loss.get<float>(count);
-    if (shortest)
-      shortest_paths(ctx, net, d_used, nodes, n_used, row_begin, row_end, o_lat, o_loss);
-    else
+    if (shortest) {
+      try {
+        shortest_paths(ctx, net, d_used, nodes, n_used, row_begin, row_end, o_lat, o_loss);
+      } catch (const Error&) {
+        raise_self_loops(ctx, net, self_first, nodes);  // a self-loop error first (graph/mod.rs:210-219)
+        throw;
+      }
+      raise_self_loops(ctx, net, self_first, nodes);
+    } else
       direct_paths(ctx, net, d_used, nodes, n_used, row_begin, row_end, o_lat, o_loss);
     if (!dev_out) {
       SG_HIP(hipMemcpyAsync(out_latency_ns, o_lat, count * 8, hipMemcpyDeviceToHost, st));
@@ -1594,7 +1617,7 @@ int32_t sg_routing_info_fill(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, ui
     uint32_t* d_used = ctx->r_used.get<uint32_t>(n_used);
     SG_HIP(hipMemcpyAsync(d_used, nodes, (size_t)n_used * 4, hipMemcpyHostToDevice, st));
     const bool shortest = flags & SG_ROUTE_SHORTEST_PATH;
-    if (shortest) check_self_loops(ctx, net, d_used, n_used, nodes);
+    if (shortest) raise_self_loops(ctx, net, launch_self_loops(ctx, net, d_used, n_used), nodes);
     // blocks of about 1/8 of the table (at least 64 rows, whole 64-row batches)
     uint32_t rows = (uint32_t)std::max(64, env_int("SG_RI_BLOCK_ROWS", (int)((n_used + 7) / 8)));
     rows = std::min(n_used, (rows + 63) / 64 * 64);
