@@ -367,6 +367,38 @@ int32_t sg_deliver_bucket(sg_ctx* ctx, const sg_record* recv, uint32_t n_records
                           const uint32_t* host_local, uint32_t n_hosts, uint32_t n_local_hosts,
                           uint32_t* dst_order, uint32_t* dst_offsets);
 
+/* ---- sharded delivery with a fixed-split exchange (no host round trip) ----
+ * The same round as sg_deliver_source / sg_deliver_bucket, with every rank's
+ * records for rank r in a block of `cap` slots, so the exchange is one
+ * equal-split all-to-all the host need not size (RCCL over xGMI), and the round
+ * synchronises once, at its end.  `cap` must be the same on every rank (e.g.
+ * derived from the largest pair count of the round before).
+ *   1. sg_deliver_source_padded: the source half; rank r's k-th record goes to
+ *      send_padded[r * cap + k] if k < cap, else to its compact position in
+ *      `send` (n_packets records, as sg_deliver_source's).  xrow (device,
+ *      3 + n_ranks u64) = [delivered, min deliver time, min used latency,
+ *      records for rank 0, 1, ...].  Does not synchronise.
+ *   2. the caller all-gathers xrow into xall (n_ranks x (3 + n_ranks)) and
+ *      all-to-alls send_padded (cap records per rank pair) into recv_padded.
+ *   3. sg_deliver_bucket_padded: buckets the valid records of every block (block
+ *      b holds min(xall[b][3 + rank], cap)); dst_order indexes recv_padded.
+ *      stats = the round's global values; recv_counts[b] = records rank b sent
+ *      this rank; pair_max = the largest count any rank sent any rank.  If
+ *      pair_max > cap, some records did not fit: every rank sees the same xall,
+ *      so all of them then run sg_deliver_pad_to_compact (the complete compact
+ *      `send`), the exact exchange of sg_deliver_source's protocol with the
+ *      counts from xall, and sg_deliver_bucket.                                */
+int32_t sg_deliver_source_padded(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table, const sg_round* round,
+                                 const sg_packets* packets, uint8_t* status, uint64_t* deliver_time_ns,
+                                 uint64_t* event_id, const uint32_t* host_owner, uint32_t n_ranks, uint32_t cap,
+                                 sg_record* send_padded, sg_record* send, uint64_t* xrow);
+int32_t sg_deliver_bucket_padded(sg_ctx* ctx, const sg_record* recv_padded, uint32_t n_ranks, uint32_t cap,
+                                 const uint64_t* xall, uint32_t rank, const uint32_t* host_local, uint32_t n_hosts,
+                                 uint32_t n_local_hosts, uint32_t* dst_order, uint32_t* dst_offsets,
+                                 sg_round_stats* stats, uint32_t* recv_counts, uint32_t* pair_max);
+int32_t sg_deliver_pad_to_compact(sg_ctx* ctx, const sg_record* send_padded, uint32_t n_ranks, uint32_t cap,
+                                  const uint64_t* xrow, sg_record* send);
+
 /* ---- router inbound CoDel queues (one per host) ---------------------------
  * Router::inbound_packets (router/mod.rs:15-58): each host's CoDelQueue
  * (router/codel_queue.rs), RFC 8289 with Shadow's TARGET = 10 ms,

@@ -39,6 +39,7 @@ EXPORTED = [
     "sg_gml_node_index", "sg_gml_destroy", "sg_net_create", "sg_net_destroy", "sg_routing_build",
     "sg_routing_min_latency", "sg_hosts_create", "sg_hosts_get_state", "sg_hosts_set_state", "sg_hosts_skip",
     "sg_hosts_destroy", "sg_deliver_round", "sg_deliver_source", "sg_deliver_bucket",
+    "sg_deliver_source_padded", "sg_deliver_bucket_padded", "sg_deliver_pad_to_compact",
     "sg_table_pack", "sg_codel_create", "sg_codel_destroy", "sg_codel_run", "sg_codel_ring_cap",
     "sg_codel_get_state", "sg_codel_set_state", "sg_inbound_create", "sg_inbound_destroy", "sg_inbound_ring_cap",
     "sg_inbound_run", "sg_inbound_get_state", "sg_hosts_event_ctr", "sg_outbound_create", "sg_outbound_destroy",
@@ -206,6 +207,11 @@ def load(path: str | None = None):
         "sg_deliver_source": (i32, [vp, vp, C.POINTER(sg_table), C.POINTER(sg_round), C.POINTER(sg_packets),
                                     vp, vp, vp, vp, u32, vp, u32p, C.POINTER(sg_round_stats)]),
         "sg_deliver_bucket": (i32, [vp, vp, u32, vp, u32, u32, vp, vp]),
+        "sg_deliver_source_padded": (i32, [vp, vp, C.POINTER(sg_table), C.POINTER(sg_round), C.POINTER(sg_packets),
+                                           vp, vp, vp, vp, u32, u32, vp, vp, vp]),
+        "sg_deliver_bucket_padded": (i32, [vp, vp, u32, u32, vp, u32, vp, u32, u32, vp, vp,
+                                           C.POINTER(sg_round_stats), vp, C.POINTER(C.c_uint32)]),
+        "sg_deliver_pad_to_compact": (i32, [vp, vp, u32, u32, vp, vp]),
         "sg_table_pack": (i32, [vp, C.POINTER(sg_table), vp, u32p]),
         "sg_codel_create": (i32, [vp, u32, u32, C.POINTER(vp)]),
         "sg_codel_destroy": (None, [vp]),

@@ -431,6 +431,7 @@ struct StatsJob {
   uint32_t* err;
   uint32_t* big_count;
   sg_round_ret* ret;
+  unsigned long long* row;  // optional (device): the stats also go to row[0..2] (padded exchange)
 };
 
 template <int NT>
@@ -463,6 +464,11 @@ __device__ __forceinline__ void reduce_stats_block(const StatsJob& j) {
     j.ret->stats[0] = nd;
     j.ret->stats[1] = mind;
     j.ret->stats[2] = minl;
+    if (j.row) {
+      j.row[0] = nd;
+      j.row[1] = mind;
+      j.row[2] = minl;
+    }
     j.ret->err = *j.err;
     *j.err = 0;
     *j.big_count = 0;
@@ -598,20 +604,27 @@ __global__ void __launch_bounds__(PACK_BLOCK)
   for (uint32_t r = threadIdx.x; r < n_ranks; r += PACK_BLOCK) block_counts[r * gridDim.x + blockIdx.x] = cnt[r];
 }
 
+// padded (optional): rank r's k-th record goes to padded[r * cap + k] when k < cap
+// (the fixed-split exchange), and to send[p] (its compact position) otherwise.
 __global__ void __launch_bounds__(PACK_BLOCK)
     k_owner_scatter(const uint32_t* __restrict__ src_host, const uint32_t* __restrict__ dst_host,
                     const uint64_t* __restrict__ deliver, const uint64_t* __restrict__ eid,
                     const uint64_t* __restrict__ ctr_start, uint32_t P, const uint32_t* __restrict__ owner,
-                    uint32_t n_ranks, const uint32_t* __restrict__ block_off, sg_record* __restrict__ send) {
-  __shared__ uint32_t cur[MAX_RANKS];
-  for (uint32_t r = threadIdx.x; r < n_ranks; r += PACK_BLOCK) cur[r] = block_off[r * gridDim.x + blockIdx.x];
+                    uint32_t n_ranks, const uint32_t* __restrict__ block_off, sg_record* __restrict__ send,
+                    sg_record* __restrict__ padded, uint32_t cap) {
+  __shared__ uint32_t cur[MAX_RANKS], start[MAX_RANKS];
+  for (uint32_t r = threadIdx.x; r < n_ranks; r += PACK_BLOCK) {
+    cur[r] = block_off[r * gridDim.x + blockIdx.x];
+    start[r] = block_off[r * gridDim.x];
+  }
   __syncthreads();
   const uint32_t chunk = (P + gridDim.x - 1) / gridDim.x;
   const uint32_t i0 = blockIdx.x * chunk, i1 = min(P, i0 + chunk);
   for (uint32_t i = i0 + threadIdx.x; i < i1; i += PACK_BLOCK) {
     uint32_t d = dst_host[i];
     if (d == NONE) continue;
-    uint32_t p = atomicAdd(&cur[owner[d]], 1u);
+    const uint32_t o = owner[d];
+    const uint32_t p = atomicAdd(&cur[o], 1u);
     uint32_t s = src_host[i];
     sg_record r;
     r.deliver_time_ns = deliver[i];
@@ -619,7 +632,69 @@ __global__ void __launch_bounds__(PACK_BLOCK)
     r.event_id = eid[i];
     r.packet = i;
     r.dst_host = d;
-    send[p] = r;
+    const uint32_t k = p - start[o];
+    if (padded && k < cap)
+      padded[(size_t)o * cap + k] = r;
+    else
+      send[p] = r;
+  }
+}
+
+// xrow[3 + r] = records this rank sends rank r (block_off: exclusive scan of the
+// (rank, block) counts, nb blocks per rank).
+__global__ void k_xrow_counts(const uint32_t* __restrict__ block_off, uint32_t nb, uint32_t n_ranks,
+                              unsigned long long* __restrict__ xrow) {
+  const uint32_t r = threadIdx.x;
+  if (r < n_ranks) xrow[3 + r] = block_off[(size_t)(r + 1) * nb] - block_off[(size_t)r * nb];
+}
+
+// The fixed-split exchange's fallback: every record of `padded` to its compact position.
+__global__ void k_pad_to_compact(const sg_record* __restrict__ padded, uint32_t cap,
+                                 const unsigned long long* __restrict__ xrow, uint32_t n_ranks,
+                                 sg_record* __restrict__ compact) {
+  __shared__ uint32_t start[MAX_RANKS + 1];
+  if (threadIdx.x == 0) {
+    uint32_t a = 0;
+    for (uint32_t r = 0; r < n_ranks; r++) {
+      start[r] = a;
+      a += (uint32_t)xrow[3 + r];
+    }
+  }
+  __syncthreads();
+  const size_t total = (size_t)n_ranks * cap;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t r = (uint32_t)(e / cap), k = (uint32_t)(e - (size_t)r * cap);
+    if (k < min((uint32_t)xrow[3 + r], cap)) compact[start[r] + k] = padded[e];
+  }
+}
+
+// After the bucketing of a padded exchange: the round's global stats (sum, min,
+// min over the gathered rows), this rank's receive counts and the largest pair
+// count, into the mapped return block; the bucketing's error word joins the
+// source phase's flags there.
+__global__ void k_xall_reduce(const unsigned long long* __restrict__ xall, uint32_t n_ranks, uint32_t rank,
+                              uint32_t* __restrict__ err, sg_round_ret* ret) {
+  const uint32_t b = threadIdx.x, w = 3 + n_ranks;
+  const bool on = b < n_ranks;
+  unsigned long long nd = on ? xall[(size_t)b * w] : 0, md = on ? xall[(size_t)b * w + 1] : ~0ull,
+                     ml = on ? xall[(size_t)b * w + 2] : ~0ull, pm = 0;
+  if (on) {
+    for (uint32_t r = 0; r < n_ranks; r++) pm = max(pm, xall[(size_t)b * w + 3 + r]);
+    ret->recv_cnt[b] = (uint32_t)xall[(size_t)b * w + 3 + rank];
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    nd += __shfl_xor(nd, d, 64);
+    md = min(md, (unsigned long long)__shfl_xor(md, d, 64));
+    ml = min(ml, (unsigned long long)__shfl_xor(ml, d, 64));
+    pm = max(pm, (unsigned long long)__shfl_xor(pm, d, 64));
+  }
+  if (b == 0) {
+    ret->stats[0] = nd;
+    ret->stats[1] = md;
+    ret->stats[2] = ml;
+    ret->pair_max = (uint32_t)min(pm, 0xFFFFFFFFull);
+    ret->err |= *err;
+    *err = 0;
   }
 }
 
@@ -696,6 +771,32 @@ struct RecordEntries {  // sharded: entries are received records, slot = the des
   uint32_t H;
   uint32_t* err;
   __device__ __forceinline__ uint32_t slot(uint32_t e) const {
+    const uint32_t d = rec[e].dst_host;
+    const uint32_t s = d < H ? local[d] : NONE;
+    if (s == NONE) atomicOr(err, ERR_NOT_LOCAL);
+    return s;
+  }
+  __device__ __forceinline__ void get(uint32_t e, uint64_t& tt, uint64_t& kk, uint32_t& ki) const {
+    tt = rec[e].deliver_time_ns;
+    kk = rec[e].order_key;
+    ki = e;
+  }
+};
+
+// sharded, fixed-split exchange: block b of `cap` records came from rank b, of which
+// the first min(xall[b][3 + rank], cap) are real; the rest are holes (slot NONE)
+struct PaddedRecordEntries {
+  static constexpr bool KK = true;
+  static constexpr bool COARSE = false;
+  const sg_record* rec;
+  const uint32_t* local;
+  uint32_t H;
+  uint32_t* err;
+  uint32_t cap, w, rank;  // w = 3 + n_ranks (an xall row)
+  const unsigned long long* xall;
+  __device__ __forceinline__ uint32_t slot(uint32_t e) const {
+    const uint32_t b = e / cap, k = e - b * cap;
+    if ((unsigned long long)k >= xall[(size_t)b * w + 3 + rank]) return NONE;
     const uint32_t d = rec[e].dst_host;
     const uint32_t s = d < H ? local[d] : NONE;
     if (s == NONE) atomicOr(err, ERR_NOT_LOCAL);
@@ -1412,7 +1513,7 @@ struct RoundWork {
 // dst_host (NONE unless delivered) and the round stats.
 static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const sg_round* rd,
                               const sg_packets* pk, uint8_t* status, uint64_t* deliver, uint64_t* eid,
-                              bool want_ctr_start, bool fuse_stats = false) {
+                              bool want_ctr_start, bool fuse_stats = false, unsigned long long* stats_row = nullptr) {
   hipStream_t st = ctx->stream;
   const uint32_t P = pk->n_packets, H = hs->n;
   RoundWork w;
@@ -1429,6 +1530,12 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   if (w.ctr_start) SG_HIP(hipMemcpyAsync(w.ctr_start, hs->ctr, (size_t)H * 8, hipMemcpyDeviceToDevice, st));
   if (!P) {
     SG_HIP(hipMemsetAsync(w.big_count, 0, 4, st));
+    if (stats_row) {  // no packets: delivered 0, no minima, no source-phase errors
+      ctx->round_ret->err = 0;  // (mapped; the previous round's writes were synchronised)
+      const unsigned long long none[3] = {0, ~0ull, ~0ull};
+      SG_HIP(hipMemcpyAsync(stats_row, none, sizeof(none), hipMemcpyHostToDevice, st));
+      SG_HIP(hipStreamSynchronize(st));  // (the host array leaves scope; an empty round only)
+    }
     return w;
   }
   {
@@ -1482,7 +1589,7 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
     else
       hipLaunchKernelGGL((k_walk<false, false>), dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
   }
-  const StatsJob sj{a.blk_stats, walk_blocks, ctx->round_err, w.big_count, ctx->round_ret};
+  const StatsJob sj{a.blk_stats, walk_blocks, ctx->round_err, w.big_count, ctx->round_ret, stats_row};
   if (fuse_stats)
     w.stats = sj;
   else
@@ -1540,13 +1647,80 @@ static void deliver_source(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const
   exclusive_scan_u32(ctx, bc, bo, n_ranks * nb);
   if (P) {
     hipLaunchKernelGGL(k_owner_scatter, dim3(nb), dim3(PACK_BLOCK), 0, st, pk->src_host, w.dst_host, deliver, eid,
-                       w.ctr_start, P, owner, n_ranks, bo, send);
+                       w.ctr_start, P, owner, n_ranks, bo, send, (sg_record*)nullptr, 0u);
     SG_CHECK_LAUNCH();
   }
   std::vector<uint32_t> starts((size_t)n_ranks * nb + 1);
   SG_HIP(hipMemcpyAsync(starts.data(), bo, starts.size() * 4, hipMemcpyDeviceToHost, st));
   finish(ctx, w, stats);  // synchronises the stream
   for (uint32_t r = 0; r < n_ranks; r++) send_counts[r] = starts[(size_t)(r + 1) * nb] - starts[(size_t)r * nb];
+}
+
+// The fixed-split exchange's source half: as deliver_source, but nothing is read
+// back -- the records for rank r go to padded[r * cap + k] (k < cap; the rest to
+// their compact positions in `send`), and xrow (device) receives the round's
+// stats and the per-rank counts for the caller's all-gather.
+static void deliver_source_padded(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, const sg_round* rd,
+                                  const sg_packets* pk, uint8_t* status, uint64_t* deliver, uint64_t* eid,
+                                  const uint32_t* owner, uint32_t n_ranks, uint32_t cap, sg_record* padded,
+                                  sg_record* send, unsigned long long* xrow) {
+  hipStream_t st = ctx->stream;
+  const uint32_t P = pk->n_packets;
+  RoundWork w = source_phase(ctx, hs, tab, rd, pk, status, deliver, eid, true, false, xrow);
+  const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(grid_for(P, PACK_BLOCK * 8), 2048));
+  uint32_t* bc = ctx->d_cnt.get<uint32_t>((size_t)n_ranks * nb + 1);
+  uint32_t* bo = ctx->d_scan.get<uint32_t>((size_t)n_ranks * nb + 1);
+  SG_HIP(hipMemsetAsync(bc, 0, ((size_t)n_ranks * nb + 1) * 4, st));
+  if (P) {
+    TimedLaunch tl(ctx, "pack", 4.0 * P + 32.0 * P);
+    hipLaunchKernelGGL(k_owner_count, dim3(nb), dim3(PACK_BLOCK), 0, st, w.dst_host, P, owner, n_ranks, bc);
+  }
+  exclusive_scan_u32(ctx, bc, bo, n_ranks * nb);
+  if (P)
+    hipLaunchKernelGGL(k_owner_scatter, dim3(nb), dim3(PACK_BLOCK), 0, st, pk->src_host, w.dst_host, deliver, eid,
+                       w.ctr_start, P, owner, n_ranks, bo, send, padded, cap);
+  hipLaunchKernelGGL(k_xrow_counts, dim3(1), dim3(MAX_RANKS), 0, st, bo, nb, n_ranks, xrow);
+  SG_CHECK_LAUNCH();
+}
+
+// The destination half of a fixed-split exchange: recv holds n_ranks blocks of
+// cap records (block b from rank b), xall the all-gathered rows.  One
+// synchronisation: then the source phase's and the bucketing's errors, the
+// global stats, this rank's receive counts and the largest pair count are read
+// from the mapped return block.
+static void deliver_bucket_padded(sg_ctx* ctx, const sg_record* recv, uint32_t n_ranks, uint32_t cap,
+                                  const unsigned long long* xall, uint32_t rank, const uint32_t* local, uint32_t H,
+                                  uint32_t n_local, uint32_t* order, uint32_t* offsets, sg_round_stats* stats,
+                                  uint32_t* recv_counts, uint32_t* pair_max) {
+  hipStream_t st = ctx->stream;
+  uint32_t* ws = ctx->d_seg.get<uint32_t>(8);
+  uint32_t* big_count = ws;
+  uint32_t* err = ws + 1;
+  SG_HIP(hipMemsetAsync(ws, 0, 8 * 4, st));
+  const uint64_t n64 = (uint64_t)n_ranks * cap;
+  if (n64 >= (1ull << 31)) throw Error(SG_ERR_INVALID_ARG, "padded exchange too large (n_ranks x cap >= 2^31)");
+  const PaddedRecordEntries E{recv, local, H, err, cap, 3 + n_ranks, rank, xall};
+  const bool region = bucket_sort(ctx, E, (uint32_t)n64, n_local, offsets, order, big_count, true);
+  hipLaunchKernelGGL(k_xall_reduce, dim3(1), dim3(MAX_RANKS), 0, st, xall, n_ranks, rank, err, ctx->round_ret);
+  SG_CHECK_LAUNCH();
+  SG_HIP(hipStreamSynchronize(st));
+  const volatile sg_round_ret* r = ctx->round_ret;
+  fail_flags(r->err);
+  if (region && r->overflow) {  // a hot destination overfilled its region
+    SG_HIP(hipMemsetAsync(ws, 0, 8 * 4, st));
+    bucket_sort(ctx, E, (uint32_t)n64, n_local, offsets, order, big_count, false);
+    uint32_t h_err = 0;
+    copy_to_host(ctx, &h_err, err, 4);
+    fail_flags(h_err);
+  }
+  if (stats) {
+    stats->n_delivered = r->stats[0];
+    stats->min_deliver_time_ns = r->stats[1];
+    stats->min_used_latency_ns = r->stats[2];
+  }
+  if (recv_counts)
+    for (uint32_t b = 0; b < n_ranks; b++) recv_counts[b] = r->recv_cnt[b];
+  if (pair_max) *pair_max = r->pair_max;
 }
 
 static void deliver_bucket(sg_ctx* ctx, const sg_record* recv, uint32_t n, const uint32_t* local, uint32_t H,
@@ -1804,6 +1978,55 @@ int32_t sg_deliver_source(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table, c
       throw Error(SG_ERR_INVALID_ARG, "null packet or output array");
     deliver_source(ctx, hosts, table, round, packets, status, deliver_time_ns, event_id, host_owner, n_ranks, send,
                    send_counts, stats);
+  });
+}
+
+int32_t sg_deliver_source_padded(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table, const sg_round* round,
+                                 const sg_packets* packets, uint8_t* status, uint64_t* deliver_time_ns,
+                                 uint64_t* event_id, const uint32_t* host_owner, uint32_t n_ranks, uint32_t cap,
+                                 sg_record* send_padded, sg_record* send, uint64_t* xrow) {
+  return sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (!hosts || hosts->ctx != ctx || !table || !round || !packets || !host_owner || !send_padded || !xrow)
+      throw Error(SG_ERR_INVALID_ARG, "null argument");
+    if (n_ranks == 0 || n_ranks > MAX_RANKS) throw Error(SG_ERR_INVALID_ARG, "n_ranks must be in [1, 64]");
+    if (cap == 0) throw Error(SG_ERR_INVALID_ARG, "cap must be positive");
+    if (hosts->n && hosts->max_route >= table->n_cols)
+      throw Error(SG_ERR_INVALID_ARG, "a host's routing index is outside the table's columns");
+    if (packets->n_packets &&
+        (!packets->src_host || !packets->dst_ipv4 || !packets->payload_len || !packets->send_time_ns || !status ||
+         !deliver_time_ns || !event_id || !send || (!table->path_key && (!table->latency_ns || !table->packet_loss))))
+      throw Error(SG_ERR_INVALID_ARG, "null packet or output array");
+    deliver_source_padded(ctx, hosts, table, round, packets, status, deliver_time_ns, event_id, host_owner, n_ranks,
+                          cap, send_padded, send, (unsigned long long*)xrow);
+  });
+}
+
+int32_t sg_deliver_bucket_padded(sg_ctx* ctx, const sg_record* recv_padded, uint32_t n_ranks, uint32_t cap,
+                                 const uint64_t* xall, uint32_t rank, const uint32_t* host_local, uint32_t n_hosts,
+                                 uint32_t n_local_hosts, uint32_t* dst_order, uint32_t* dst_offsets,
+                                 sg_round_stats* stats, uint32_t* recv_counts, uint32_t* pair_max) {
+  return sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (!recv_padded || !xall || !host_local || !dst_order || !dst_offsets)
+      throw Error(SG_ERR_INVALID_ARG, "null argument");
+    if (n_ranks == 0 || n_ranks > MAX_RANKS || rank >= n_ranks || cap == 0)
+      throw Error(SG_ERR_INVALID_ARG, "bad n_ranks / rank / cap");
+    deliver_bucket_padded(ctx, recv_padded, n_ranks, cap, (const unsigned long long*)xall, rank, host_local, n_hosts,
+                          n_local_hosts, dst_order, dst_offsets, stats, recv_counts, pair_max);
+  });
+}
+
+int32_t sg_deliver_pad_to_compact(sg_ctx* ctx, const sg_record* send_padded, uint32_t n_ranks, uint32_t cap,
+                                  const uint64_t* xrow, sg_record* send) {
+  return sg::guarded(ctx, [&] {
+    using namespace sg;
+    if (!send_padded || !xrow || !send || n_ranks == 0 || n_ranks > MAX_RANKS || cap == 0)
+      throw Error(SG_ERR_INVALID_ARG, "bad argument");
+    const size_t total = (size_t)n_ranks * cap;
+    hipLaunchKernelGGL(k_pad_to_compact, dim3(grid_for(total, 256, 8192)), dim3(256), 0, ctx->stream, send_padded,
+                       cap, (const unsigned long long*)xrow, n_ranks, send);
+    SG_CHECK_LAUNCH();
   });
 }
 

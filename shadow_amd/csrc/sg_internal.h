@@ -81,6 +81,11 @@ struct sg_round_ret {
   unsigned long long stats[3];  // n_delivered, min deliver time, min used latency
   uint32_t err;
   uint32_t overflow;  // a bucketing region overflowed: the scan path must run
+  // sg_deliver_bucket_padded: this rank's receive count from each rank, and the
+  // largest count any rank sent any rank (over the padded capacity: exchange again)
+  uint32_t recv_cnt[64];
+  uint32_t pair_max;
+  uint32_t pad_;
 };
 
 struct sg_ctx {

@@ -13,6 +13,14 @@ Delivery: hosts are owned by the rank that holds their routing row
   2. all-to-all of the per-rank record counts, then of the records
      (32 B each; torch.distributed "nccl" = RCCL);
   3. destination phase (sg_deliver_bucket): per-destination EventQueue order.
+With `padded=True` (ShardedDelivery) the rounds after the first use a
+fixed-split exchange with no host round trip before the round's end: every
+rank's records for rank r fill a block of `cap` slots (sg_deliver_source_padded),
+one all-gather of each rank's [stats, counts] row and one equal-split
+all-to-all move them, and the bucketing reads the valid records of each block
+(sg_deliver_bucket_padded), which synchronises once.  cap follows the largest
+pair count of the round before (all ranks see the same gathered rows, so they
+agree on it); a round whose counts outgrow it is exchanged again exactly.
 The phases are injectable so the exchange logic is testable on CPU (gloo).
 """
 from __future__ import annotations
@@ -173,9 +181,103 @@ def gpu_bucket_phase(ctx, recv, n_records: int, local_dev, n_hosts: int, n_local
     return order[:n_records], offsets
 
 
+@dataclass
+class SourcePadded:
+    status: object
+    deliver_time_ns: object
+    event_id: object
+    send_padded: object  # int64 device tensor [n_ranks * cap, 4] (sg_record blocks)
+    send: object         # int64 device tensor [n, 4]: records past cap at their compact positions
+    xrow: object         # int64 device tensor [3 + n_ranks]: stats, then the count for each rank
+    cap: int
+
+
+def gpu_source_phase_padded(ctx, hosts, table, packets, round_end_ns, sim_end_ns, bootstrap_end_ns, owner_dev,
+                            n_ranks, cap, ws: Optional[Workspace] = None) -> SourcePadded:
+    import torch
+
+    n = len(packets)
+    dev = packets.src_host.device
+    ws = ws or Workspace()
+    status = ws.get("status", max(n, 1), torch.uint8, dev)
+    deliver = ws.get("deliver", max(n, 1), torch.int64, dev)
+    eid = ws.get("eid", max(n, 1), torch.int64, dev)
+    send = ws.get("send", max(n, 1), torch.int64, dev, cols=4)
+    padded = ws.get("send_padded", n_ranks * cap, torch.int64, dev, cols=4)
+    xrow = ws.get("xrow", 3 + n_ranks, torch.int64, dev)
+    p = _capi.sg_packets()
+    p.n_packets = n
+    p.src_host, p.dst_ipv4 = packets.src_host.data_ptr(), packets.dst_ipv4.data_ptr()
+    p.payload_len, p.send_time_ns = packets.payload_len.data_ptr(), packets.send_time_ns.data_ptr()
+    skip = getattr(packets, "rng_skip", None)
+    p.rng_skip = skip.data_ptr() if skip is not None else None
+    r = _capi.sg_round(round_end_ns, sim_end_ns, bootstrap_end_ns)
+    t = table.struct()
+    check(ctx.handle, load().sg_deliver_source_padded(ctx.handle, hosts.handle, C.byref(t), C.byref(r), C.byref(p),
+                                                      status.data_ptr(), deliver.data_ptr(), eid.data_ptr(),
+                                                      owner_dev.data_ptr(), n_ranks, cap, padded.data_ptr(),
+                                                      send.data_ptr(), xrow.data_ptr()))
+    return SourcePadded(status, deliver, eid, padded, send, xrow, cap)
+
+
+def gpu_bucket_phase_padded(ctx, recv_padded, cap: int, xall, rank: int, local_dev, n_hosts: int, n_local: int,
+                            ws: Optional[Workspace] = None):
+    """Returns (order into recv_padded, offsets, global stats, recv_counts, pair_max)."""
+    import torch
+
+    dev = local_dev.device
+    ws = ws or Workspace()
+    n_ranks = recv_padded.shape[0] // cap
+    order = ws.get("order", max(n_ranks * cap, 1), torch.int32, dev)
+    offsets = ws.get("offsets", n_local + 1, torch.int32, dev)
+    st = _capi.sg_round_stats()
+    rc = (C.c_uint32 * n_ranks)()
+    pm = C.c_uint32()
+    check(ctx.handle, load().sg_deliver_bucket_padded(ctx.handle, recv_padded.data_ptr(), n_ranks, cap, xall.data_ptr(),
+                                                      rank, local_dev.data_ptr(), n_hosts, n_local, order.data_ptr(),
+                                                      offsets.data_ptr(), C.byref(st), rc, C.byref(pm)))
+    counts = list(rc)
+    stats = (st.n_delivered, st.min_deliver_time_ns, st.min_used_latency_ns)
+    return order[:sum(min(c, cap) for c in counts)], offsets, stats, counts, pm.value
+
+
+def gpu_pad_to_compact(ctx, src: SourcePadded, n_ranks: int):
+    check(ctx.handle, load().sg_deliver_pad_to_compact(ctx.handle, src.send_padded.data_ptr(), n_ranks, src.cap,
+                                                       src.xrow.data_ptr(), src.send.data_ptr()))
+    return src.send
+
+
+def next_cap(pair_max: int) -> int:
+    """Block size of the next fixed-split exchange: 1.25x the largest pair count seen,
+    plus slack, in whole 256-record units (every rank computes it from the same
+    gathered rows, so every rank picks the same value)."""
+    return max(256, (int(pair_max) * 5 // 4 + 256 + 255) // 256 * 256)
+
+
 # ---------------------------------------------------------------------------
 # Exchange
 # ---------------------------------------------------------------------------
+def exchange_padded(send_padded, xrow, dist, group=None, ws: Optional[Workspace] = None):
+    """The fixed-split exchange: one all-gather of the [stats, counts] rows and one
+    equal-split all_to_all_single of the record blocks, both enqueued on the stream
+    with no host round trip.  Returns (recv_padded, xall)."""
+    import torch
+
+    world = dist.get_world_size(group) if dist is not None else 1
+    if dist is not None and _host_staged(dist, group, send_padded.device):
+        recv, xall = exchange_padded(send_padded.cpu(), xrow.cpu(), dist, group)
+        return recv.to(send_padded.device), xall.to(send_padded.device)
+    ws = ws or Workspace()
+    dev = send_padded.device
+    xall = ws.get("xall", world * xrow.shape[0], torch.int64, dev)
+    recv = ws.get("recv_padded", send_padded.shape[0], torch.int64, dev, cols=4)
+    if dist is None:
+        xall.copy_(xrow)
+        recv.copy_(send_padded)
+        return recv, xall
+    dist.all_gather_into_tensor(xall, xrow, group=group)
+    dist.all_to_all_single(recv, send_padded, group=group)
+    return recv, xall
 def _host_staged(dist, group, dev) -> bool:
     """gloo moves host tensors only: device tensors go through host copies (the
     multi-rank rehearsal on a box with fewer GPUs than ranks; RCCL needs none)."""
@@ -199,7 +301,7 @@ def all_to_all_records(send, send_counts: List[int], dist, group=None):
 
 
 def exchange_round(send, send_counts: List[int], stats, rank: int, dist, group=None,
-                   ws: Optional[Workspace] = None):
+                   ws: Optional[Workspace] = None, want_pair_max: bool = False):
     """The round's one host round trip: an all-gather of every rank's row
     [delivered, min deliver time, min used latency, counts to each rank] (u64),
     so the round scalars ride with the counts exchange, then the records'
@@ -209,8 +311,8 @@ def exchange_round(send, send_counts: List[int], stats, rank: int, dist, group=N
 
     world = len(send_counts)
     if _host_staged(dist, group, send.device):
-        recv, counts, g = exchange_round(send.cpu(), send_counts, stats, rank, dist, group)
-        return recv.to(send.device), counts, g
+        r = exchange_round(send.cpu(), send_counts, stats, rank, dist, group, want_pair_max=want_pair_max)
+        return (r[0].to(send.device),) + tuple(r[1:])
     dev = send.device
     if ws is None:
         ws = Workspace()
@@ -229,7 +331,10 @@ def exchange_round(send, send_counts: List[int], stats, rank: int, dist, group=N
     allv = out_h.numpy().view(np.uint64).reshape(world, w)
     recv_counts = [int(allv[r, 3 + rank]) for r in range(world)]
     g = (int(allv[:, 0].sum()), int(allv[:, 1].min()), int(allv[:, 2].min()))
-    return _records_all_to_all(send, send_counts, recv_counts, dist, group, ws), recv_counts, g
+    recv = _records_all_to_all(send, send_counts, recv_counts, dist, group, ws)
+    if want_pair_max:
+        return recv, recv_counts, g, int(allv[:, 3:].max()) if world else 0
+    return recv, recv_counts, g
 
 
 def _records_all_to_all(send, send_counts: List[int], recv_counts: List[int], dist, group,
@@ -275,7 +380,9 @@ class ShardedDelivery:
 
     def __init__(self, ctx, hosts, table, partition: HostPartition, rank: int, world: int, dist=None, group=None,
                  source_fn: Optional[Callable] = None, bucket_fn: Optional[Callable] = None,
-                 exchange_fn: Optional[Callable] = None, device="cuda"):
+                 exchange_fn: Optional[Callable] = None, device="cuda", padded: bool = False,
+                 source_padded_fn: Optional[Callable] = None, bucket_padded_fn: Optional[Callable] = None,
+                 pad_to_compact_fn: Optional[Callable] = None):
         self.ctx, self.hosts, self.table, self.part = ctx, hosts, table, partition
         self.rank, self.world, self.dist, self.group = rank, world, dist, group
         import functools
@@ -284,6 +391,13 @@ class ShardedDelivery:
         self.source_fn = source_fn or functools.partial(gpu_source_phase, ws=self.ws)
         self.bucket_fn = bucket_fn or functools.partial(gpu_bucket_phase, ws=self.ws)
         self.exchange_fn = exchange_fn  # None: exchange_round (counts and round scalars in one all-gather)
+        # the fixed-split exchange (rounds after the first: see the module docstring)
+        self.padded = padded
+        self.source_padded_fn = source_padded_fn or functools.partial(gpu_source_phase_padded, ws=self.ws)
+        self.bucket_padded_fn = bucket_padded_fn or functools.partial(gpu_bucket_phase_padded, ws=self.ws)
+        self.pad_to_compact_fn = pad_to_compact_fn or gpu_pad_to_compact
+        self.cap = None          # block size of the next padded round (None: the next round is exact)
+        self.last_mode = None    # "exact", "padded" or "padded+exact" (a padded round that overflowed)
         import torch
 
         self.owner_dev = torch.from_numpy(partition.owner.view(np.int32)).to(device)
@@ -295,17 +409,55 @@ class ShardedDelivery:
 
     def round(self, packets, round_end_ns: int, sim_end_ns: int, bootstrap_end_ns: int = 0):
         """One round.  The returned tensors are views of buffers the next round
-        overwrites (copy what must outlive it)."""
+        overwrites (copy what must outlive it).  In a padded round `recv` holds
+        n_ranks blocks of `cap` records and `order` indexes it."""
+        if self.padded and self.cap is not None:
+            return self._round_padded(packets, round_end_ns, sim_end_ns, bootstrap_end_ns)
+        out = self._round_exact(packets, round_end_ns, sim_end_ns, bootstrap_end_ns)
+        if self.padded:  # the first round sizes the blocks: every rank sees the same counts
+            self.cap = next_cap(self._pair_max)
+        return out
+
+    def _round_padded(self, packets, round_end_ns, sim_end_ns, bootstrap_end_ns):
+        import torch
+
+        cap = self.cap
+        src = self.source_padded_fn(self.ctx, self.hosts, self.table, packets, round_end_ns, sim_end_ns,
+                                    bootstrap_end_ns, self.owner_dev, self.world, cap)
+        recv, xall = exchange_padded(src.send_padded, src.xrow, self.dist, self.group, ws=self.ws)
+        order, offsets, g, recv_counts, pair_max = self.bucket_padded_fn(
+            self.ctx, recv, cap, xall, self.rank, self.local_dev, len(self.part.local), self.part.n_local(self.rank))
+        xa = xall.cpu().numpy().view(np.uint64).reshape(self.world, 3 + self.world)  # (after the round's sync)
+        send_counts = [int(x) for x in xa[self.rank, 3:]]
+        self.last_send_counts = send_counts
+        self.last_stats = (int(g[0]), int(g[1]), int(g[2]))
+        self.cap = next_cap(pair_max)
+        if pair_max > cap:  # some pair outgrew its block: every rank exchanges again, exactly
+            self.last_mode = "padded+exact"
+            send = self.pad_to_compact_fn(self.ctx, src, self.world)
+            recv_counts = [int(xa[b, 3 + self.rank]) for b in range(self.world)]
+            recv = _records_all_to_all(send, send_counts, recv_counts, self.dist, self.group, self.ws)
+            order, offsets = self.bucket_fn(self.ctx, recv, int(sum(recv_counts)), self.local_dev,
+                                            len(self.part.local), self.part.n_local(self.rank))
+        else:
+            self.last_mode = "padded"
+        res = SourceResult(src.status, src.deliver_time_ns, src.event_id, src.send, send_counts, *self.last_stats)
+        self.last = (recv, order, offsets)
+        return res, recv, recv_counts, order, offsets
+
+    def _round_exact(self, packets, round_end_ns, sim_end_ns, bootstrap_end_ns):
+        self.last_mode = "exact"
         src = self.source_fn(self.ctx, self.hosts, self.table, packets, round_end_ns, sim_end_ns, bootstrap_end_ns,
                              self.owner_dev, self.world)
         stats = (int(src.n_delivered), int(src.min_deliver_time_ns), int(src.min_used_latency_ns))
         self.last_send_counts = list(src.send_counts)
         if self.exchange_fn is None:
-            recv, recv_counts, self.last_stats = exchange_round(src.send, src.send_counts, stats, self.rank,
-                                                                self.dist, self.group, ws=self.ws)
+            recv, recv_counts, self.last_stats, self._pair_max = exchange_round(
+                src.send, src.send_counts, stats, self.rank, self.dist, self.group, ws=self.ws, want_pair_max=True)
         else:
             recv, recv_counts = self.exchange_fn(src.send, src.send_counts)
             self.last_stats = gather_round_stats(*stats, self.dist, self.group, self.device)
+            self._pair_max = max(list(src.send_counts) + list(recv_counts) + [0])
         order, offsets = self.bucket_fn(self.ctx, recv, int(sum(recv_counts)), self.local_dev,
                                         len(self.part.local), self.part.n_local(self.rank))
         self.last = (recv, order, offsets)  # this rank's destination buckets of the round

@@ -16,7 +16,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from shadow_amd import synth
-from shadow_amd.dist import HostPartition, RECORD_DTYPE, ShardedDelivery, SourceResult, balanced_node_order, row_range
+from shadow_amd.dist import (HostPartition, RECORD_DTYPE, ShardedDelivery, SourcePadded, SourceResult,
+                             balanced_node_order, row_range)
 
 T0 = 946684800 * 10**9
 NONE = 0xFFFFFFFF
@@ -169,3 +170,141 @@ def test_two_rank_gloo_exchange_matches_single_round(oracle, skew):
             assert got == exp, h
             seen.add(h)
     assert seen == set(range(hosts["n"]))
+
+
+# ---- the fixed-split exchange (ShardedDelivery(padded=True)) over gloo ---------------
+def _cpu_source_padded(O, lat, loss, hosts, state, part):
+    exact = _cpu_source(O, lat, loss, hosts, state, part)
+
+    def fn(ctx, h, table, packets, round_end, sim_end, boot, owner_dev, n_ranks, cap):
+        r = exact(ctx, h, table, packets, round_end, sim_end, boot, owner_dev, n_ranks)
+        recs = r.send.numpy()
+        padded = np.zeros((n_ranks * cap, 4), np.int64)
+        send = np.zeros_like(recs)
+        start = 0
+        for d, c in enumerate(r.send_counts):
+            k = min(c, cap)
+            padded[d * cap:d * cap + k] = recs[start:start + k]
+            send[start + k:start + c] = recs[start + k:start + c]  # past cap: compact positions only
+            start += c
+        xrow = np.array([r.n_delivered, r.min_deliver_time_ns, r.min_used_latency_ns, *r.send_counts],
+                        np.uint64).view(np.int64)
+        return SourcePadded(r.status, r.deliver_time_ns, r.event_id, torch.from_numpy(padded), torch.from_numpy(send),
+                            torch.from_numpy(xrow.copy()), cap)
+    return fn
+
+
+def _cpu_bucket_padded(part, rank):
+    def fn(ctx, recv, cap, xall, rk, local_dev, n_hosts, n_local):
+        world = recv.shape[0] // cap
+        xa = xall.numpy().view(np.uint64).reshape(world, 3 + world)
+        rec = recv.numpy().view(RECORD_DTYPE).ravel()
+        idx = np.concatenate([b * cap + np.arange(min(int(xa[b, 3 + rank]), cap)) for b in range(world)])
+        idx = idx.astype(np.int64)
+        slot = part.local[rec["dst_host"][idx]]
+        assert (part.owner[rec["dst_host"][idx]] == rank).all()
+        o = np.lexsort((rec["order_key"][idx], rec["deliver_time_ns"][idx], slot))
+        offsets = np.zeros(n_local + 1, np.uint32)
+        np.add.at(offsets, slot + 1, 1)
+        stats = (int(xa[:, 0].sum()), int(xa[:, 1].min()), int(xa[:, 2].min()))
+        return (idx[o].astype(np.uint32), np.cumsum(offsets).astype(np.uint32), stats,
+                [int(x) for x in xa[:, 3 + rank]], int(xa[:, 3:].max()))
+    return fn
+
+
+def _cpu_pad_to_compact(ctx, src, n_ranks):
+    xrow = src.xrow.numpy().view(np.uint64)
+    send = src.send.numpy()
+    pad = src.send_padded.numpy()
+    start = 0
+    for d in range(n_ranks):
+        c = int(xrow[3 + d])
+        k = min(c, src.cap)
+        send[start:start + k] = pad[d * src.cap:d * src.cap + k]
+        start += c
+    return src.send
+
+
+def _worker_padded(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from oracle import oracle as O
+
+        g, lat, loss, hosts, _, used = _world(O, False, world)
+        nu = lat.shape[0]
+        part = HostPartition(hosts["route"], nu, world)
+        state = _Tables(O, hosts)
+        sd = ShardedDelivery(None, None, None, part, rank, world, dist=dist, device="cpu", padded=True,
+                             source_fn=_cpu_source(O, lat, loss, hosts, state, part),
+                             bucket_fn=_cpu_bucket(part, rank),
+                             source_padded_fn=_cpu_source_padded(O, lat, loss, hosts, state, part),
+                             bucket_padded_fn=_cpu_bucket_padded(part, rank), pad_to_compact_fn=_cpu_pad_to_compact)
+        results = []
+        for k in range(4):  # exact (sizes the blocks), padded, padded with a hot destination (overflow), padded
+            start = T0 + k * 10**6
+            hot = k == 2
+            pk = synth.make_packets(12000, hosts, start, start + 10**6, seed=20 + k, p_unknown_dst=0.02,
+                                    hot_dst=5 if hot else -1, p_hot=0.6 if hot else 0.0)
+            sel = np.nonzero(part.owner[pk["src"]] == rank)[0]
+            packets = (pk["src"][sel], pk["dst_ip"][sel], pk["payload"][sel], pk["send_time"][sel])
+            src, recv, recv_counts, order, offsets = sd.round(packets, start + 10**6, 2**63, 0)
+            rec = recv.numpy().view(RECORD_DTYPE).ravel()
+            sels = [np.nonzero(part.owner[pk["src"]] == r)[0] for r in range(world)]
+            if sd.last_mode == "padded":  # block b of cap records came from rank b
+                origin = np.arange(len(rec)) // sd_cap_prev
+            else:
+                origin = np.repeat(np.arange(world), recv_counts)
+            glob = {}
+            for s_, hh in enumerate(part.hosts_of[rank]):
+                ks = np.asarray(order[offsets[s_]:offsets[s_ + 1]], np.int64)
+                glob[int(hh)] = [int(sels[origin[k_]][rec["packet"][k_]]) for k_ in ks]
+            results.append((sd.last_mode, glob, np.asarray(src.status).tolist(), sel.tolist(), sd.last_stats))
+            sd_cap_prev = sd.cap  # the block size the next round uses
+        q.put((rank, results))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_two_rank_gloo_padded_exchange_rounds(oracle):
+    """ShardedDelivery(padded=True) over gloo: the first round is exact and sizes the
+    blocks, the next ones use the fixed-split exchange (no host round trip before the
+    round's end); a round whose hot destination overfills a block is exchanged again
+    exactly.  Every round equals one oracle round over all packets."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_padded, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for o in out:
+        assert o[1] != "error", o[2]
+    g, lat, loss, hosts, _, used = _world(oracle, False, world)
+    rng = np.stack([oracle.xoshiro_seed(int(s)) for s in hosts["seed"]]).astype(np.uint64)
+    ctr = np.zeros(hosts["n"], np.uint64)
+    modes = []
+    for k in range(4):
+        start = T0 + k * 10**6
+        hot = k == 2
+        pk = synth.make_packets(12000, hosts, start, start + 10**6, seed=20 + k, p_unknown_dst=0.02,
+                                hot_dst=5 if hot else -1, p_hot=0.6 if hot else 0.0)
+        want = oracle.deliver_round(start + 10**6, 2**63, 0, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
+                                    hosts["ip"], hosts["route"], lat, loss, rng, ctr)
+        seen = set()
+        for rank, results in out:
+            mode, per_dst, status, sel, stats = results[k]
+            modes.append(mode)
+            assert stats == (want["delivered"], want["min_deliver"], want["min_lat"]), (k, mode)
+            assert np.array_equal(np.array(status, np.uint8), want["status"][np.array(sel, np.int64)])
+            for h, got in per_dst.items():
+                assert got == want["dst_order"][want["dst_offsets"][h]:want["dst_offsets"][h + 1]].tolist(), (k, h)
+                seen.add(h)
+        assert seen == set(range(hosts["n"]))
+    assert modes == ["exact"] * 2 + ["padded"] * 2 + ["padded+exact"] * 2 + ["padded"] * 2, modes

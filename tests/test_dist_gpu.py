@@ -126,3 +126,76 @@ def test_sharded_hot_destination(oracle, ctx, p_hot):
     # slot sorted inside the region path's block
     want = _run(oracle, ctx, 4, 120000, hot=17, seed=5, p_hot=p_hot)
     assert np.diff(want["dst_offsets"]).max() > 100
+
+
+@pytest.mark.parametrize("W,cap_scale", [(2, 1.3), (4, 1.3), (3, 0.5)])
+def test_padded_exchange_matches_single(oracle, ctx, W, cap_scale):
+    """sg_deliver_source_padded / sg_deliver_bucket_padded: every rank's records for
+    rank d in a block of `cap` slots, exchanged by concatenating block d of every
+    sender (what the equal-split all-to-all does), bucketed with one sync; the same
+    per-destination order, statuses and global stats as one oracle round.  cap_scale
+    0.5: blocks too small, so pair_max > cap, and the round is exchanged again exactly
+    (sg_deliver_pad_to_compact + sg_deliver_bucket)."""
+    import torch
+
+    from shadow_amd.dist import exchange_padded, gpu_bucket_phase_padded, gpu_pad_to_compact, \
+        gpu_source_phase_padded, _records_all_to_all
+
+    lat, loss, hosts = _world(oracle, seed=7)
+    nu = lat.shape[0]
+    part = HostPartition(hosts["route"], nu, W)
+    start, end = T0 + 10**9, T0 + 10**9 + 10**6
+    n = 40000
+    pk = synth.make_packets(n, hosts, start, end, seed=31, p_unknown_dst=0.01, hot_dst=9, p_hot=0.02)
+    owner_of_pkt = part.owner[pk["src"]]
+    cap = max(256, int(cap_scale * n / W / W))
+    ranks = []
+    for r in range(W):
+        r0, r1, per = row_range(nu, W, r)
+        sel = np.nonzero(owner_of_pkt == r)[0]
+        ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+        dl = torch.from_numpy(np.ascontiguousarray(lat[r0:r1]).view(np.int64).ravel()).cuda()
+        df = torch.from_numpy(np.ascontiguousarray(loss[r0:r1]).ravel()).cuda()
+        table = DeviceTable(dl, df, nu, r0)
+        batch = PacketBatch.from_numpy(pk["src"][sel], pk["dst_ip"][sel], pk["payload"][sel], pk["send_time"][sel])
+        sd = ShardedDelivery(ctx, ht, table, part, r, W)
+        src = gpu_source_phase_padded(ctx, ht, table, batch, end, 2**63, 0, sd.owner_dev, W, cap)
+        ranks.append(dict(sel=sel, sd=sd, src=src, send_padded=src.send_padded.clone(), send=src.send.clone(),
+                          xrow=src.xrow.clone(), status=src.status[:len(sel)].cpu().numpy()))
+    xall = torch.cat([R["xrow"] for R in ranks])
+    xa = xall.cpu().numpy().view(np.uint64).reshape(W, 3 + W)
+    rng0 = np.stack([oracle.xoshiro_seed(int(s)) for s in hosts["seed"]]).astype(np.uint64)
+    want = oracle.deliver_round(end, 2**63, 0, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"],
+                                hosts["ip"], hosts["route"], lat, loss, rng0, np.zeros(hosts["n"], np.uint64))
+    overflow = int(xa[:, 3:].max()) > cap
+    assert overflow == (cap_scale < 1)
+    sels = [R["sel"] for R in ranks]
+    for d, R in enumerate(ranks):
+        assert np.array_equal(R["status"], want["status"][R["sel"]])
+        recv = torch.cat([S["send_padded"][d * cap:(d + 1) * cap] for S in ranks]).contiguous()
+        order, offsets, g, recv_counts, pair_max = gpu_bucket_phase_padded(
+            ctx, recv, cap, xall, d, R["sd"].local_dev, len(part.local), part.n_local(d))
+        assert g == (want["delivered"], want["min_deliver"], want["min_lat"])
+        assert recv_counts == [int(x) for x in xa[:, 3 + d]] and pair_max == int(xa[:, 3:].max())
+        if overflow:  # the fallback: compact records, exact exchange by concatenation, exact bucketing
+            comp = []
+            for S in ranks:
+                S["src"].send_padded, S["src"].send, S["src"].xrow = S["send_padded"], S["send"].clone(), S["xrow"]
+                full = gpu_pad_to_compact(ctx, S["src"], W)
+                sc = [int(x) for x in S["xrow"].cpu().numpy().view(np.uint64)[3:]]
+                off = sum(sc[:d])
+                comp.append(full[off:off + sc[d]].clone())
+            recv = torch.cat(comp).contiguous()
+            order, offsets = R["sd"].bucket_fn(ctx, recv, recv.shape[0], R["sd"].local_dev, len(part.local),
+                                               part.n_local(d))
+            origin = np.repeat(np.arange(W), recv_counts)
+        else:
+            origin = np.arange(W * cap) // cap
+        rec = recv.cpu().numpy().view(RECORD_DTYPE).ravel()
+        offs = offsets.cpu().numpy().view(np.uint32)
+        ordr = order.cpu().numpy().view(np.uint32)
+        for slot, h in enumerate(part.hosts_of[d]):
+            ks = ordr[offs[slot]:offs[slot + 1]].astype(np.int64)
+            got = np.array([sels[origin[k]][rec["packet"][k]] for k in ks], np.int64)
+            exp = want["dst_order"][want["dst_offsets"][h]:want["dst_offsets"][h + 1]]
+            assert np.array_equal(got, exp), (d, h)

@@ -80,6 +80,23 @@ def main():
     g1, g2 = ht_s.get_state(), ht.get_state()
     assert np.array_equal(g1[0], g2[0]) and np.array_equal(g1[1], g2[1])
 
+    # ---- the fixed-split exchange (padded=True): round 1 exact (sizes the blocks), then padded
+    ht_p = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    sdp = ShardedDelivery(ctx, ht_p, table, part, 0, 1, dist=dist, padded=True)
+    ht_r = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    for k in range(3):
+        src_p, recv_p, rc_p, order_p, offs_p = sdp.round(batch, end, 2**63, start + 100_000)
+        ref = deliver_round(ht_r, table, batch, end, 2**63, start + 100_000).to_numpy(P)
+        assert sdp.last_mode == ("exact" if k == 0 else "padded"), sdp.last_mode
+        assert np.array_equal(src_p.status[:P].cpu().numpy(), ref["status"])
+        rec_p = recv_p.cpu().numpy().view(RECORD_DTYPE).ravel()
+        glob_p = rec_p["packet"].astype(np.int64)[order_p.cpu().numpy().view(np.uint32)]
+        assert np.array_equal(glob_p, ref["dst_order"].astype(np.int64)), k
+        assert np.array_equal(offs_p.cpu().numpy().view(np.uint32), ref["dst_offsets"])
+        assert sdp.last_stats == (ref["delivered"], ref["min_deliver"], ref["min_lat"])
+    g1, g2 = ht_p.get_state(), ht_r.get_state()
+    assert np.array_equal(g1[0], g2[0]) and np.array_equal(g1[1], g2[1])
+
     # ---- timings: the whole sharded round, and exchange_round alone (its one host sync)
     reps = 20
     torch.cuda.synchronize()
@@ -99,6 +116,12 @@ def main():
         deliver_round(ht, table, batch, end, 2**63, start + 100_000, out=out)
     torch.cuda.synchronize()
     t_single = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sdp.round(batch, end, 2**63, start + 100_000)
+    torch.cuda.synchronize()
+    t_padded = (time.perf_counter() - t0) / reps
+    assert sdp.last_mode == "padded"
     # the sharded round's phases one at a time (each call returns synchronised)
     from shadow_amd.dist import gpu_bucket_phase, gpu_source_phase
     ph = {"source": 0.0, "exchange": 0.0, "bucket": 0.0}
@@ -118,6 +141,7 @@ def main():
         ph["bucket"] += (t3 - t2) / reps
     print(json.dumps({"ok": True, "backend": dist.get_backend(), "packets": P, "records": int(sum(recv_counts)),
                       "sharded_round_ms": round(t_round * 1e3, 4), "exchange_round_ms": round(t_ex * 1e3, 4),
+                      "sharded_round_padded_ms": round(t_padded * 1e3, 4), "padded_cap": sdp.cap,
                       "single_gpu_round_ms": round(t_single * 1e3, 4),
                       "phases_ms": {k: round(v * 1e3, 4) for k, v in ph.items()}}), flush=True)
     dist.destroy_process_group()
