@@ -88,6 +88,9 @@ def parse_args():
     p.add_argument("--no-compare", action="store_true",
                    help="skip the comparison builds (slab kernel, one-launch unbounded search): for rocprof "
                         "runs whose k_sssp_lds average must be the default plan's alone")
+    p.add_argument("--exact-exchange", action="store_true",
+                   help="N > 1: exchange every round's records with host-sized splits (one host round trip "
+                        "more per round) instead of the fixed-split exchange")
     p.add_argument("--no-pack", action="store_true",
                    help="deliver from the two-array table (no packed path-key copy)")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
@@ -784,7 +787,9 @@ def main():
         src_global = pk["src"]
         out = Deliveries.allocate(a.packets, a.hosts)
         round_end, sim_end = T0 + 10**9 + 10**6, 2**63
-        sharded = ShardedDelivery(ctx, ht, table, part, D.rank, D.world, dist=D.dist) if D.world > 1 else None
+        # padded: after the first (warm-up) round, the fixed-split exchange with one host sync per round
+        sharded = ShardedDelivery(ctx, ht, table, part, D.rank, D.world, dist=D.dist,
+                                  padded=not a.exact_exchange) if D.world > 1 else None
 
         def rnd():
             if sharded:
@@ -795,11 +800,11 @@ def main():
         t_round = timed(D, rnd, a.steps, a.warmup)
         per_rank = None
         if sharded:  # load balance of the host partition: packets sent, records sent / received per rank
-            _, recv_l, _ = sharded.last
-            mine_c = [float(a.packets), float(sum(sharded.last_send_counts)), float(recv_l.shape[0])]
+            mine_c = [float(a.packets), float(sum(sharded.last_send_counts)), float(sum(sharded.last_recv_counts))]
             allc = D.gather(mine_c)
             per_rank = {"packets": [int(x[0]) for x in allc], "records_sent": [int(x[1]) for x in allc],
-                        "records_received": [int(x[2]) for x in allc]}
+                        "records_received": [int(x[2]) for x in allc], "exchange": sharded.last_mode,
+                        "padded_cap": sharded.cap}
         t_pcie = None
         if D.world == 1:
             # the boundary takes device buffers; a caller holding the packet log in host memory

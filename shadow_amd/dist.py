@@ -443,6 +443,7 @@ class ShardedDelivery:
             self.last_mode = "padded"
         res = SourceResult(src.status, src.deliver_time_ns, src.event_id, src.send, send_counts, *self.last_stats)
         self.last = (recv, order, offsets)
+        self.last_recv_counts = list(recv_counts)
         return res, recv, recv_counts, order, offsets
 
     def _round_exact(self, packets, round_end_ns, sim_end_ns, bootstrap_end_ns):
@@ -461,4 +462,5 @@ class ShardedDelivery:
         order, offsets = self.bucket_fn(self.ctx, recv, int(sum(recv_counts)), self.local_dev,
                                         len(self.part.local), self.part.n_local(self.rank))
         self.last = (recv, order, offsets)  # this rank's destination buckets of the round
+        self.last_recv_counts = list(recv_counts)
         return src, recv, recv_counts, order, offsets
