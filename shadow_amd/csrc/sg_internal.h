@@ -307,9 +307,14 @@ struct SsspDevPlan {
   uint32_t* ub_w = nullptr;
   uint32_t* ctl = nullptr;
   uint32_t* ctr = nullptr;
+  bool landmarks = false;  // phase 0 = landmark rows; phase 1's bounds come from them (sssp_landmark_bounds)
+  unsigned rows_grid = 0;  // sssp_landmark_bounds' grid (one thread per row of the block)
 };
 constexpr int SSSP_PHASES_MAX = 6;
 SsspDevPlan sssp_device_plan(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin,
-                             uint32_t row_end, int n_phase, int kb, bool exact, int hops);
+                             uint32_t row_end, int n_phase, int kb, bool exact, int hops, uint32_t n_land);
+// After phase 0 (the landmarks) ran: phase 1's bound rows from the landmark rows' columns.
+void sssp_landmark_bounds(sg_ctx* ctx, const SsspDevPlan& p, uint32_t n_used, uint32_t row_begin,
+                          const uint64_t* out_lat, const uint32_t* sat_row, int kb);
 
 }  // namespace sg

@@ -24,6 +24,17 @@
 //    zero-loss arcs), then by latency, then by row.  The zero-loss paths are
 //    walked level by level, the wave's lanes taking the level's arcs in turn.
 //
+//  * Landmarks (undirected graphs): phase 0's rows run from infinity, about twice
+//    as long as a bounded row.  So phase 0 is split: n_land of its rows, spread
+//    evenly over it, run first (one claim round of the persistent workgroups); the
+//    rest of phase 0 then starts from bounds through the nearest landmarks L,
+//    D[s][v] <= D[s][L] + D[L][v] with D[s][L] = D[L][s].latency -- the reversed
+//    path L -> s has the same latency in an undirected graph (petgraph keeps both
+//    arc directions, graph/mod.rs:137-152).  Latency bounds only, never exact
+//    seeds (the reversed path's loss fold differs).  k_plan_landmarks relabels the
+//    phases; sssp_landmark_bounds (a launch between phases 0 and 1) reads D[L][s]
+//    from the landmark rows just written and keeps each row's kb nearest.
+//
 // The plan changes speed only, never the table: any phase assignment whose bound
 // rows lie in earlier phases reaches the same fixed point (sg_sssp.hip header).
 #include <algorithm>
@@ -81,6 +92,111 @@ __global__ void k_vote_name(const uint32_t* __restrict__ out_off, const uint32_t
     if (c != ~0u && open(c)) best = max(best, score(c));
   }
   jn[0xFFFFFFFFu - (uint32_t)best] = tag;
+}
+
+// Landmarks: n_land rows of phase 0 (jn == 1), evenly spread over its rows in row
+// order, stay in phase 0; every other row assigned a phase moves one phase later.
+template <int NT>
+__global__ void __launch_bounds__(NT) k_plan_landmarks(uint8_t* __restrict__ jn, uint32_t rows, uint32_t n_land) {
+  constexpr int NW = NT / 64;
+  __shared__ uint32_t s_wsum[NW];
+  __shared__ uint32_t s_total;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint32_t cnt = 0;  // phase-0 rows
+  for (uint32_t r = tid; r < rows; r += NT) cnt += jn[r] == 1;
+  for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+  if (lane == 0) s_wsum[wv] = cnt;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < NW; w++) t += s_wsum[w];
+    s_total = t;
+  }
+  __syncthreads();
+  const uint32_t s0 = s_total;
+  uint32_t base = 0;  // phase-0 rows before this pass's chunk
+  for (uint32_t r0 = 0; r0 < rows; r0 += NT) {
+    const uint32_t r = r0 + tid;
+    const uint8_t x = r < rows ? jn[r] : 0;
+    const bool f = x == 1;
+    const uint32_t incl = wave_incl_sum(f ? 1u : 0u);
+    __syncthreads();  // s_wsum reuse
+    if (lane == 63) s_wsum[wv] = incl;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (int w = 0; w < NW; w++) {
+      pre += w < wv ? s_wsum[w] : 0u;
+      tot += s_wsum[w];
+    }
+    if (r < rows && x) {
+      bool land = false;
+      if (f && n_land < s0) {  // index i among phase 0: a landmark where floor(i * n_land / s0) steps
+        const uint64_t i = base + pre + incl - 1;
+        land = i == 0 || (i * n_land) / s0 != ((i - 1) * n_land) / s0;
+      }
+      jn[r] = land ? 1 : (uint8_t)(x + 1);
+    }
+    base += tot;
+  }
+}
+
+// Phase 1's bound rows: for each of its rows s, the kb landmarks L nearest to s
+// by D[L][s] (column s of the landmark rows, just written by phase 0), as
+// latency-only bounds with w = D[L][s].  A landmark row that gave up (sat_row 2)
+// was never written and is skipped.
+constexpr int LB_MAX = 4;
+__global__ void __launch_bounds__(256)
+    k_landmark_bounds(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctl, uint32_t n_used,
+                      uint32_t row_begin, const uint64_t* __restrict__ out_lat, const uint32_t* __restrict__ sat_row,
+                      int kb, uint32_t* __restrict__ ub_row, uint32_t* __restrict__ ub_w) {
+  const uint32_t n_land = ctl[1], base = ctl[2], n1 = ctl[3];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n1) return;
+  const uint32_t srow = list[base + i];
+  uint64_t t[LB_MAX];  // (distance << 32) | landmark position, ascending
+#pragma unroll
+  for (int j = 0; j < LB_MAX; j++) t[j] = ~0ull;
+  for (uint32_t k = 0; k < n_land; k++) {
+    const uint32_t L = list[k];
+    if (sat_row[L - row_begin] == 2u) continue;
+    const uint64_t d = out_lat[(size_t)(L - row_begin) * n_used + srow];
+    if (d >= LAT32_SAT) continue;
+    uint64_t key = (d << 32) | k;
+#pragma unroll
+    for (int j = 0; j < LB_MAX; j++) {
+      const uint64_t lo = min(t[j], key);
+      key = max(t[j], key);
+      t[j] = lo;
+    }
+  }
+  // k_plan_bounds' entries for this row (landmarks it has an arc to, exact seeds
+  // first) stay; the nearest landmarks fill the slots left, up to kb in all
+  uint32_t* orow = ub_row + (size_t)(base + i) * SSSP_KB_MAX;
+  uint32_t* ow = ub_w + (size_t)(base + i) * SSSP_KB_MAX;
+  int have = 0;
+  while (have < kb && orow[have] != ~0u) have++;
+  int j = 0;
+  for (int slot = have; slot < kb; slot++) {
+    while (j < LB_MAX && t[j] != ~0ull) {  // skip a landmark already listed
+      bool dup = false;
+      const uint32_t L = list[(uint32_t)t[j]];
+      for (int q = 0; q < have; q++) dup |= (orow[q] & ~SSSP_UB_EXACT) == L;
+      if (!dup) break;
+      j++;
+    }
+    if (j >= LB_MAX || t[j] == ~0ull) break;
+    orow[slot] = list[(uint32_t)t[j]];
+    ow[slot] = (uint32_t)(t[j] >> 32);
+    j++;
+  }
+}
+
+void sssp_landmark_bounds(sg_ctx* ctx, const SsspDevPlan& p, uint32_t n_used, uint32_t row_begin,
+                          const uint64_t* out_lat, const uint32_t* sat_row, int kb) {
+  // phase 1 holds at most the block's rows: one thread each, those past its count (ctl[3]) exit
+  hipLaunchKernelGGL(k_landmark_bounds, dim3(p.rows_grid), dim3(256), 0, ctx->stream, p.list, p.ctl, n_used, row_begin,
+                     out_lat, sat_row, std::max(1, std::min(LB_MAX, kb)), p.ub_row, p.ub_w);
+  SG_CHECK_LAUNCH();
 }
 
 // Rows still in no phase take the last one; each phase's rows in row order (block
@@ -247,10 +363,10 @@ __global__ void __launch_bounds__(PB_WAVES * 64)
 }
 
 SsspDevPlan sssp_device_plan(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin,
-                             uint32_t row_end, int n_phase, int kb, bool exact, int hops) {
+                             uint32_t row_end, int n_phase, int kb, bool exact, int hops, uint32_t n_land) {
   (void)n_used;
   const uint32_t n = net->n_nodes, rows = row_end - row_begin;
-  n_phase = std::max(2, std::min(SSSP_PHASES_MAX, n_phase));
+  n_phase = std::max(2, std::min(SSSP_PHASES_MAX - (n_land ? 1 : 0), n_phase));
   // one workspace: list, ub_row, ub_w (rows x SSSP_KB_MAX each), ctl, ctr, rel (n), gain (rows),
   // jn and phase (u8 rows each)
   const size_t nl = rows, nb = (size_t)rows * SSSP_KB_MAX;
@@ -283,6 +399,13 @@ SsspDevPlan sssp_device_plan(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
                          rel, jn, gain);
       hipLaunchKernelGGL(k_vote_name, dim3(g), dim3(256), 0, st, net->out_off, net->out_arc, d_used, row_begin, rows,
                          rel, jn, gain, ph);
+    }
+    if (n_land) {  // phase 0 split: its landmark rows first (see the header)
+      hipLaunchKernelGGL(k_plan_landmarks<1024>, dim3(1), dim3(1024), 0, st, jn, rows, n_land);
+      n_phase += 1;
+      p.n_phase = n_phase;
+      p.landmarks = true;
+      p.rows_grid = grid_for(rows, 256);
     }
     hipLaunchKernelGGL(k_plan_lists<1024>, dim3(1), dim3(1024), 0, st, jn, rows, row_begin, n_phase, phase_of, p.list,
                        p.ctl, p.ctr);

@@ -1313,7 +1313,15 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
     // exact seeds need a column for every node (see sg_sssp.hip "Exact seeds")
     const bool exact = env_int("SG_SSSP_EXACT", 1) != 0 && n_used == net->n_nodes;
     const int hops = std::max(1, std::min(env_int("SG_SSSP_HOPS", 3), 3));
-    const SsspDevPlan plan = sssp_device_plan(ctx, net, d_used, n_used, row_begin, row_end, n_phase, kb, exact, hops);
+    // Landmarks (sg_plan.hip header; undirected graphs): SG_SSSP_LANDMARKS rows first, the
+    // rest of phase 0 bounded through them.  Off by default: at C3 (tools/sssp_ab.py, one
+    // box, tables bit-identical) 256 landmarks cut phase 0 from 1.30 to 0.36 ms but the
+    // landmark-bounded rows took 113 us each against 129 unbounded and 66 for rows bounded
+    // by a neighbour: the build took 3.53 ms against 3.43 (128: 3.54, 512: 3.67).
+    const int land_env = env_int("SG_SSSP_LANDMARKS", 0);
+    const uint32_t n_land = net->directed || land_env <= 0 ? 0u : (uint32_t)land_env;
+    const SsspDevPlan plan =
+        sssp_device_plan(ctx, net, d_used, n_used, row_begin, row_end, n_phase, kb, exact, hops, n_land);
     if (const int warm = env_int("SG_PLAN_WARM", 0))
       hipLaunchKernelGGL(k_busy, dim3(4 * ctx->n_cu), dim3(256), 0, ctx->stream, (uint32_t)warm, (float*)nullptr);
     // SG_PLAN_SYNC=1 (A/B diagnostics): read the phase sizes to the host and launch with host-known counts
@@ -1332,12 +1340,14 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
                         ph + 1 == plan.n_phase ? diag : nullptr, plan.list + b0, cnt,
                         bounded ? plan.ub_row + (size_t)b0 * SSSP_KB_MAX : nullptr,
                         bounded ? plan.ub_w + (size_t)b0 * SSSP_KB_MAX : nullptr);
+        if (ph == 0 && plan.landmarks) sssp_landmark_bounds(ctx, plan, n_used, row_begin, out_lat, sat, kb);
         continue;
       }
       launch_sssp_lds(ctx, net->out_off, net->out_arc, net->n_nodes, net->n_arcs, d_used, n_used, row_begin,
                       row_end, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work,
                       ph + 1 == plan.n_phase ? diag : nullptr, plan.list, rows, bounded ? plan.ub_row : nullptr,
                       bounded ? plan.ub_w : nullptr, plan.ctl, ph, plan.ctr + 2 * ph);
+      if (ph == 0 && plan.landmarks) sssp_landmark_bounds(ctx, plan, n_used, row_begin, out_lat, sat, kb);
     }
   } else {
     TimedLaunch tl(ctx, "sssp", 0.0);

@@ -10,12 +10,14 @@ from shadow_amd import NetworkGraph
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["lds", "lds_bounded", "slab"])
+@pytest.fixture(autouse=True, params=["lds", "lds_bounded", "lds_landmarks", "slab"])
 def apsp_kernel(request, monkeypatch):
     """Both shortest-path kernels: the per-source LDS search (also in its forced
-    two-phase form, seed rows then bounded rows) and the slab relaxation."""
+    two-phase form, seed rows then bounded rows, and with the first phase split
+    by 8 landmark rows) and the slab relaxation."""
     monkeypatch.setenv("SG_APSP_LDS", "0" if request.param == "slab" else "1")
-    monkeypatch.setenv("SG_SSSP_SEEDS", "2" if request.param == "lds_bounded" else "1")
+    monkeypatch.setenv("SG_SSSP_SEEDS", "2" if request.param in ("lds_bounded", "lds_landmarks") else "1")
+    monkeypatch.setenv("SG_SSSP_LANDMARKS", "8" if request.param == "lds_landmarks" else "0")
     return "lds" if request.param.startswith("lds") else request.param
 
 
