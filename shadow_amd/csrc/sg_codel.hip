@@ -231,12 +231,10 @@ struct CodelArgs {
 // and the kernels ran in two rounds (SG_LANE_DIAG).
 constexpr int CD_THREADS = 64;
 constexpr int CD_UNROLL = 8;
-// Hosts per block (HOSTS, a template parameter of the lane kernels): 64 (every lane
-// walks) or 32 (lanes 32-63 only stage).  Chunks scale with it, so a 100k-host call's
-// blocks stay resident at once: 64 hosts -- 1,024 staged events (22 KB), 7 blocks per
-// CU; 32 hosts -- 512 events (11 KB), 14 per CU.
-template <int HOSTS> constexpr int cd_chunk() { return HOSTS * 16; }
-template <int HOSTS> constexpr int cd_out_chunk() { return HOSTS * 14; }  // k_outbound: 24 B per send
+constexpr int CD_HOSTS = 64;
+constexpr int CD_CHUNK = 1024;
+constexpr int CD_OUT_CHUNK = 896;  // k_outbound: 24 B per send, 21 KB, 7 blocks per CU
+static_assert(CD_THREADS == CD_HOSTS, "a block is its walkers");
 
 // Chunk [c0, c1) staged by the block: ld(i, u) loads element i into slot u of
 // the lane's registers, st(k, u) stores slot u to LDS index k.  Indices past
@@ -275,9 +273,7 @@ __device__ __forceinline__ void lane_diag_store(unsigned long long* d, uint64_t 
   }
 }
 
-template <int HOSTS>
 __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
-  constexpr int CD_HOSTS = HOSTS, CD_CHUNK = cd_chunk<HOSTS>();
   const uint64_t d_t0 = a.bdiag ? wall_clock64() : 0;
   uint64_t d_walk = 0;
   // staged chunk: 22 KB, so 7 one-wave blocks fit a CU (1792 >= the 1563 blocks of a 100k-host call)
@@ -569,9 +565,7 @@ __device__ void relay_task(Q& q, Relay& r, uint64_t now, uint64_t bootstrap_end,
   }
 }
 
-template <int HOSTS>
 __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
-  constexpr int CD_HOSTS = HOSTS, CD_CHUNK = cd_chunk<HOSTS>();
   const uint64_t d_t0 = ia.q.bdiag ? wall_clock64() : 0;
   uint64_t d_walk = 0;
   const CodelArgs& a = ia.q;
@@ -797,9 +791,7 @@ __device__ void out_task(OutQ& q, Relay& r, uint64_t now, const OutboundArgs& a,
   }
 }
 
-template <int HOSTS>
 __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
-  constexpr int CD_HOSTS = HOSTS, CD_OUT_CHUNK = cd_out_chunk<HOSTS>();
   const uint64_t d_t0 = a.bdiag ? wall_clock64() : 0;
   uint64_t d_walk = 0;
   __shared__ uint64_t s_t[CD_OUT_CHUNK];
@@ -941,7 +933,6 @@ __global__ void __launch_bounds__(1024) k_blk_offsets(const unsigned long long* 
 // 256 slots per step (coalesced within a host's range), skips local packets
 // (a ballot prefix gives each kept record its rank) and writes its slice
 // [boff[b], boff[b] + sent) of the batch with coalesced stores.
-template <int HOSTS>
 __global__ void __launch_bounds__(256) k_out_compact(uint32_t H, const uint32_t* __restrict__ start,
                                                      const uint32_t* __restrict__ head,
                                                      const uint8_t* __restrict__ rflags,
@@ -949,14 +940,13 @@ __global__ void __launch_bounds__(256) k_out_compact(uint32_t H, const uint32_t*
                                                      const uint4* __restrict__ ring, uint32_t cap,
                                                      const uint64_t* __restrict__ fwd_time, uint32_t n_status,
                                                      const uint32_t* __restrict__ boff, sg_outbound_sent out) {
-  constexpr int CD_HOSTS = HOSTS;
   __shared__ uint32_t s_off[CD_HOSTS + 1], s_start[CD_HOSTS], s_ip[CD_HOSTS];
   __shared__ uint32_t wsum[4];
   const uint32_t h0 = blockIdx.x * CD_HOSTS, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   if (t < 64) {  // one wave: per-host slot counts and their exclusive prefix
     const uint32_t h = h0 + t;
     uint32_t len = 0;
-    if (t < CD_HOSTS && h < H) {
+    if (h < H) {
       const uint32_t st = start[h], end = head[h] - ((rflags[h] & R_CACHED) ? 1u : 0u);
       len = end - st;
       s_start[t] = st;
@@ -967,7 +957,7 @@ __global__ void __launch_bounds__(256) k_out_compact(uint32_t H, const uint32_t*
       const uint32_t y = __shfl_up(x, d, 64);
       if (lane >= (uint32_t)d) x += y;
     }
-    if (t < CD_HOSTS) s_off[t + 1] = x;
+    s_off[t + 1] = x;
     if (t == 0) s_off[0] = 0;
   }
   __syncthreads();
@@ -1075,12 +1065,6 @@ struct sg_inbound {
   }
 };
 
-// Hosts per block of the lane kernels: SG_LANE_HOSTS (32 or 64)
-static int lane_hosts() {
-  const char* e = getenv("SG_LANE_HOSTS");
-  return e && atoi(e) == 32 ? 32 : 64;
-}
-
 // SG_LANE_DIAG=1: per-block timing of the lane-per-host kernels on stderr (a
 // diagnostic: a synchronous copy after the launch; never set in a measured run)
 unsigned long long* lane_diag_alloc(uint32_t nb) {
@@ -1140,8 +1124,7 @@ int32_t sg_codel_run(sg_ctx* ctx, sg_codel* q, const sg_codel_events* ev, uint32
     uint32_t* gerr = ws + (size_t)H + 1;
     SG_HIP(hipMemsetAsync(gerr, 0, 4, st));
     launch_group_offsets(ctx, ev->host, E, H, ws, gerr);
-    const int hosts = lane_hosts();
-    const uint32_t nb = std::max<uint32_t>(1, (H + hosts - 1) / hosts);
+    const uint32_t nb = std::max<uint32_t>(1, (H + CD_HOSTS - 1) / CD_HOSTS);
     CodelArgs a{ws, H, E, ev->kind, ev->time_ns, ev->packet, ev->len, q->flags, q->iend, q->dnext, q->cur,
                 q->prev, q->bytes, q->head, q->tail, q->ring, q->cap, pop_result,
                 pkt_status, n_packets, ctx->d_blk.get<unsigned long long>(2 * (size_t)nb)};
@@ -1149,8 +1132,7 @@ int32_t sg_codel_run(sg_ctx* ctx, sg_codel* q, const sg_codel_events* ev, uint32
     {
       // per event: 17 B in, 4 B result, ring slot 16 B written (push) or read (pop), 1 B status
       TimedLaunch tl(ctx, "codel", 38.0 * E + 56.0 * H);
-      if (hosts == 32) hipLaunchKernelGGL(k_codel<32>, dim3(nb), dim3(CD_THREADS), 0, st, a);
-      else hipLaunchKernelGGL(k_codel<64>, dim3(nb), dim3(CD_THREADS), 0, st, a);
+      hipLaunchKernelGGL(k_codel, dim3(nb), dim3(CD_THREADS), 0, st, a);
     }
     lane_diag_report(st, "k_codel", a.bdiag, nb);
     hipLaunchKernelGGL(k_codel_reduce, dim3(1), dim3(1024), 0, st, a.blk, nb, gerr, q->ret);
@@ -1290,8 +1272,7 @@ int32_t sg_inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* a
     } else {
       SG_HIP(hipMemsetAsync(ws, 0, ((size_t)H + 1) * 4, st));  // no arrivals: pending tasks only
     }
-    const int hosts = lane_hosts();
-    const uint32_t nb = (H + hosts - 1) / hosts;
+    const uint32_t nb = (H + CD_HOSTS - 1) / CD_HOSTS;
     InboundArgs a;
     a.q = CodelArgs{ws, H, E, nullptr, arr->time_ns, arr->packet, arr->len, q->flags, q->iend, q->dnext, q->cur,
                     q->prev, q->bytes, q->head, q->tail, q->ring, q->cap, nullptr, pkt_status, n_packets,
@@ -1313,8 +1294,7 @@ int32_t sg_inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* a
       // per arrival: 16 B in, a 16-B ring record written and read, 9 B out; per host: ~160 B of state
       a.q.bdiag = lane_diag_alloc(nb);
       TimedLaunch tl(ctx, "inbound", 57.0 * E + 160.0 * H);
-      if (hosts == 32) hipLaunchKernelGGL(k_inbound<32>, dim3(nb), dim3(CD_THREADS), 0, st, a);
-      else hipLaunchKernelGGL(k_inbound<64>, dim3(nb), dim3(CD_THREADS), 0, st, a);
+      hipLaunchKernelGGL(k_inbound, dim3(nb), dim3(CD_THREADS), 0, st, a);
     }
     lane_diag_report(st, "k_inbound", a.q.bdiag, nb);
     hipLaunchKernelGGL(k_codel_reduce, dim3(1), dim3(1024), 0, st, a.q.blk, nb, gerr, q->ret);
@@ -1392,7 +1372,7 @@ int32_t sg_outbound_create(sg_ctx* ctx, uint32_t n_hosts, const uint32_t* host_i
     SG_HIP(hipMalloc(&ob->head, n * 4));
     SG_HIP(hipMalloc(&ob->tail, n * 4));
     SG_HIP(hipMalloc(&ob->start, n * 4));
-    SG_HIP(hipMalloc(&ob->off, ((n + 31) / 32 + 1) * 4));  // per k_outbound block (32 or 64 hosts each)
+    SG_HIP(hipMalloc(&ob->off, ((n + CD_HOSTS - 1) / CD_HOSTS + 1) * 4));  // per k_outbound block
     SG_HIP(hipMalloc(&ob->ring, n * cap * 16));
     SG_HIP(hipMalloc(&ob->rflags, n));
     SG_HIP(hipMalloc(&ob->task_time, n * 8));
@@ -1460,8 +1440,7 @@ int32_t sg_outbound_run(sg_ctx* ctx, sg_outbound* ob, const sg_outbound_sends* s
     } else {
       SG_HIP(hipMemsetAsync(ws, 0, ((size_t)H + 1) * 4, st));  // no sends: pending tasks only
     }
-    const int hosts = lane_hosts();
-    const uint32_t nb = (H + hosts - 1) / hosts;
+    const uint32_t nb = (H + CD_HOSTS - 1) / CD_HOSTS;
     OutboundArgs a;
     a.host_off = ws;
     a.H = H;
@@ -1495,20 +1474,15 @@ int32_t sg_outbound_run(sg_ctx* ctx, sg_outbound* ob, const sg_outbound_sends* s
       // per send: 24 B in, a 16-B ring record written and read, 9 B out; per host: ~90 B of state
       a.bdiag = lane_diag_alloc(nb);
       TimedLaunch tl(ctx, "outbound", 65.0 * E + 90.0 * H);
-      if (hosts == 32) hipLaunchKernelGGL(k_outbound<32>, dim3(nb), dim3(CD_THREADS), 0, st, a);
-      else hipLaunchKernelGGL(k_outbound<64>, dim3(nb), dim3(CD_THREADS), 0, st, a);
+      hipLaunchKernelGGL(k_outbound, dim3(nb), dim3(CD_THREADS), 0, st, a);
     }
     lane_diag_report(st, "k_outbound", a.bdiag, nb);
     if (sent) {
       hipLaunchKernelGGL(k_blk_offsets, dim3(1), dim3(1024), 0, st, a.blk, nb, ob->off);
       sg_outbound_sent o = *sent;
       TimedLaunch tl(ctx, "out_compact", 0.0);
-      if (hosts == 32)
-        hipLaunchKernelGGL(k_out_compact<32>, dim3(nb), dim3(256), 0, st, H, ob->start, ob->head, ob->rflags,
-                           ob->host_ip, ob->ring, ob->cap, fwd_time, n_packets, ob->off, o);
-      else
-        hipLaunchKernelGGL(k_out_compact<64>, dim3(nb), dim3(256), 0, st, H, ob->start, ob->head, ob->rflags,
-                           ob->host_ip, ob->ring, ob->cap, fwd_time, n_packets, ob->off, o);
+      hipLaunchKernelGGL(k_out_compact, dim3(nb), dim3(256), 0, st, H, ob->start, ob->head, ob->rflags, ob->host_ip,
+                         ob->ring, ob->cap, fwd_time, n_packets, ob->off, o);
     }
     hipLaunchKernelGGL(k_codel_reduce, dim3(1), dim3(1024), 0, st, a.blk, nb, gerr, ob->ret);
     SG_CHECK_LAUNCH();
