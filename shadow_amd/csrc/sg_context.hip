@@ -140,7 +140,12 @@ TimedLaunch::TimedLaunch(sg_ctx* c, const char* name, double work) : ctx(c) {
 void timer_add_work(sg_ctx* ctx, const char* name, double work) {
   if (!ctx->timing) return;
   for (auto& kv : ctx->timers)
-    if (kv.first == name) kv.second.work += work;
+    if (kv.first == name) {
+      kv.second.work += work;
+      return;
+    }
+  ctx->timers.emplace_back(name, KernelTimer());  // a counter with no launches of its own
+  ctx->timers.back().second.work = work;
 }
 
 TimedLaunch::~TimedLaunch() {

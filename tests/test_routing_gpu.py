@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(autouse=True, params=["lds", "lds_bounded", "lds_landmarks", "slab"])
+@pytest.fixture(autouse=True, params=["lds", "lds_bounded", "lds_landmarks", "team", "slab"])
 def apsp_kernel(request, monkeypatch):
     """Every routing test runs on both shortest-path kernels: the per-source
     LDS-resident search (sg_sssp.hip, the default up to ~10.9k nodes) and the
@@ -26,9 +26,11 @@ def apsp_kernel(request, monkeypatch):
     lds_landmarks also splits the first phase: 8 landmark rows first, the rest of
     it bounded through them (undirected graphs; an option, measured slower at C3)."""
     monkeypatch.setenv("SG_APSP_LDS", "0" if request.param == "slab" else "1")
-    monkeypatch.setenv("SG_SSSP_SEEDS", "2" if request.param in ("lds_bounded", "lds_landmarks") else "1")
+    monkeypatch.setenv("SG_SSSP_SEEDS", "2" if request.param in ("lds_bounded", "lds_landmarks", "team") else "1")
     monkeypatch.setenv("SG_SSSP_LANDMARKS", "8" if request.param == "lds_landmarks" else "0")
-    return "lds" if request.param.startswith("lds") else request.param
+    # team: the search of graphs past one CU's LDS (sg_team.hip), forced with 3 members, in phases
+    monkeypatch.setenv("SG_SSSP_TEAM", "3" if request.param == "team" else "0")
+    return "lds" if request.param.startswith("lds") or request.param == "team" else request.param
 
 
 def _graph(g, ctx):
