@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(NT)
                uint32_t lane_deg_max, const uint32_t* __restrict__ blk_rows,
                const uint32_t* __restrict__ ub_row, const uint32_t* __restrict__ ub_w,
                uint32_t* __restrict__ item_ctr, uint32_t n_items, uint32_t spin_max,
-               const uint32_t* __restrict__ plan_ctl, int plan_ph, uint32_t prefilter) {
+               const uint32_t* __restrict__ plan_ctl, int plan_ph) {
   constexpr int NW = NT / 64;
   if (plan_ctl) {  // a device-built plan (sg_plan.hip): this phase's rows and bound rows, its row count
     const uint32_t base = plan_ctl[2 * plan_ph];
@@ -384,18 +384,9 @@ __global__ void __launch_bounds__(NT)
     auto offer_all = [&](auto nk, const bool* valid, const uint32_t* v, const uint64_t* cand, bool* app) {
       constexpr int NK = decltype(nk)::value;
       uint64_t cd[NK], old[NK];
-      // prefilter (SG_SSSP_PREFILTER): a plain read of the target's latency first; a
-      // candidate with a larger latency cannot win the min (keys only decrease), so it
-      // goes to the sink instead of a contended key word
-      uint32_t cur[NK];
-#pragma unroll
-      for (int c = 0; c < NK; c++)
-        cur[c] = prefilter && valid[c] ? __hip_atomic_load((uint32_t*)&key[v[c]] + 1, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_WORKGROUP)
-                                       : LAT32_SAT;
 #pragma unroll
       for (int c = 0; c < NK; c++) {
-        const bool ok = valid[c] && fkey_lat(cand[c]) != LAT32_SAT && fkey_lat(cand[c]) <= cur[c];
+        const bool ok = valid[c] && fkey_lat(cand[c]) != LAT32_SAT;
         cd[c] = ok ? cand[c] : ~0ull;
         old[c] = __hip_atomic_fetch_min(ok ? &key[v[c]] : &sink[lane], (unsigned long long)cd[c], __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -668,8 +659,6 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
   const uint32_t lane_deg = ls && *ls ? (uint32_t)std::max(0, atoi(ls)) : 16u;
   const char* la = getenv("SG_SSSP_LANE_ARCS");
   const int la16 = la && atoi(la) == 16;
-  const char* pfs = getenv("SG_SSSP_PREFILTER");
-  const uint32_t prefilter = pfs && *pfs ? (uint32_t)std::max(0, atoi(pfs)) : 0u;
   // One persistent workgroup per CU claims rows from a counter: out_off is
   // staged once per CU instead of once per row, and no workgroup is launched and
   // torn down per row.  C3: 3.92 -> 3.54 ms (same box).  SG_SSSP_PERSIST=0: a
@@ -696,7 +685,7 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, ctx->stream, out_off, out_arc, n, n_arcs, d_used, n_used,
                        row_begin, row_begin, self_edge, e_lat, e_loss, out_lat, out_loss, sat_row, delta, vec, work,
                        diag, claim, idle_sleep, lane_deg, blk_rows, ub_row, ub_w, item_ctr, rows, spin_max, plan_ctl,
-                       plan_ph, prefilter);
+                       plan_ph);
   };
   if (work) {
     if (nt == 512) go(k_sssp_lds<true, 512, 8, 0>);
