@@ -106,6 +106,21 @@ void exclusive_scan_u32(sg_ctx* ctx, const uint32_t* d_in, uint32_t* d_out, uint
   SG_CHECK_LAUNCH();
 }
 
+char* stage_acquire(sg_ctx* ctx, int slot, size_t bytes) {
+  if (!ctx->stage_used[slot]) SG_HIP(hipEventCreateWithFlags(&ctx->stage_used[slot], hipEventDisableTiming));
+  SG_HIP(hipEventSynchronize(ctx->stage_used[slot]));  // the previous copy out of the slot is done
+  if (ctx->h_stage_bytes[slot] < bytes) {
+    if (ctx->h_stage[slot]) (void)hipHostFree(ctx->h_stage[slot]);
+    ctx->h_stage[slot] = nullptr;
+    ctx->h_stage_bytes[slot] = 0;
+    SG_HIP(hipHostMalloc(&ctx->h_stage[slot], bytes, hipHostMallocDefault));
+    ctx->h_stage_bytes[slot] = bytes;
+  }
+  return (char*)ctx->h_stage[slot];
+}
+
+void stage_release(sg_ctx* ctx, int slot) { SG_HIP(hipEventRecord(ctx->stage_used[slot], ctx->stream)); }
+
 void copy_to_host(sg_ctx* ctx, void* dst, const void* src, size_t bytes) {
   SG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
@@ -200,7 +215,7 @@ int32_t sg_ctx_create(int32_t device, sg_ctx** out) {
     SG_HIP(hipMalloc(&ctx->round_err, 16));
     SG_HIP(hipMemset(ctx->round_err, 0, 16));
     SG_HIP(hipHostMalloc(&ctx->round_ret, sizeof(sg_round_ret), hipHostMallocMapped | hipHostMallocCoherent));
-    SG_HIP(hipHostMalloc(&ctx->apsp_ret, 16, hipHostMallocMapped | hipHostMallocCoherent));
+    SG_HIP(hipHostMalloc(&ctx->apsp_ret, 32, hipHostMallocMapped | hipHostMallocCoherent));
     SG_HIP(hipMalloc(&ctx->sb_ctl, 4 * sg::SB_CTL_STRIDE * 4));
     SG_HIP(hipMemset(ctx->sb_ctl, 0, 4 * sg::SB_CTL_STRIDE * 4));
     int cus = 0;
@@ -239,8 +254,10 @@ void sg_ctx_destroy(sg_ctx* ctx) {
     (void)hipEventDestroy(b.freed);
     (void)hipFree(b.p);
   }
-  if (ctx->stage_used) (void)hipEventDestroy(ctx->stage_used);
-  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  for (int i = 0; i < 2; i++) {
+    if (ctx->stage_used[i]) (void)hipEventDestroy(ctx->stage_used[i]);
+    if (ctx->h_stage[i]) (void)hipHostFree(ctx->h_stage[i]);
+  }
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }

@@ -147,6 +147,13 @@ __global__ void __launch_bounds__(256) k_host_off4(const uint32_t* __restrict__ 
   // the source before i0: lane - 1's last one, or a load at a wave's first lane
   uint32_t before = __shfl_up(v[3], 1, 64);
   if (lane == 0) before = i0 ? src[min(i0 - 1, P - 1)] : 0;
+  // every packet's route row loaded up front (L2 hits, all four in flight): under the
+  // first-packet branch below the compiler waited for each in turn
+  uint32_t rr[4] = {0u, 0u, 0u, 0u};
+  if (route && H) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) rr[q] = route[min(v[q], H - 1)];
+  }
   if (i0 > P) return;
 #pragma unroll
   for (int q = 0; q < 4; q++) {
@@ -164,7 +171,7 @@ __global__ void __launch_bounds__(256) k_host_off4(const uint32_t* __restrict__ 
       continue;
     }
     if (route && i < P && (int64_t)s != prev) {  // first packet of host s
-      const uint32_t r = route[s];
+      const uint32_t r = rr[q];
       if (r < row_begin || r - row_begin >= n_rows) atomicOr(err, ERR_ROUTE_RANGE);
     }
     for (int64_t h = prev + 1; h <= (int64_t)s; h++) host_off[h] = i;

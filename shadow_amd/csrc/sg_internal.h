@@ -122,9 +122,17 @@ struct sg_ctx {
   uint32_t* sb_ctl = nullptr;
   uint32_t sb_parity = 0, sb_parity_c = 0;
   sg::DevBuf d_cd, d_ct, d_ck, d_ci;  // coarse-level runs of a two-level scatter
-  // APSP: the active-batch count of the next pass, written by k_active_list
-  // into pinned host-mapped memory at each pass-chunk end
+  // APSP (pinned host-mapped, 32 B): [0] the slab's active-batch count of the next
+  // pass (k_active_list, each pass-chunk end); [4] the LDS search's flagged rows and
+  // [2..3] the self-loop check's first failure (k_build_finish, the build's end)
   uint32_t* apsp_ret = nullptr;
+  // sg_routing_build's self-loop check (graph/mod.rs:210-217), folded into the LDS
+  // search's final kernel when it runs: the inputs, and the result once read
+  const uint32_t* self_used = nullptr;
+  uint32_t self_n = 0;
+  const uint32_t* self_cnt = nullptr;
+  bool self_done = false;
+  unsigned long long self_first = ~0ull;
   // sg_net device blocks released by sg_net_destroy, reused by the next sg_net_create
   // (a simulation that builds one graph and one table pays no hipMalloc / hipFree,
   // whose implicit device synchronisation cost ~0.2 ms each); `freed` orders the
@@ -137,9 +145,10 @@ struct sg_ctx {
   std::vector<NetBlock> net_pool;
   // pinned staging of a new graph's edge arrays (one H2D copy); `stage_used` marks
   // when the last copy out of it completed
-  void* h_stage = nullptr;
-  size_t h_stage_bytes = 0;
-  hipEvent_t stage_used = nullptr;
+  // (slot 0: edges; slot 1: a build's used-node list)
+  void* h_stage[2] = {nullptr, nullptr};
+  size_t h_stage_bytes[2] = {0, 0};
+  hipEvent_t stage_used[2] = {nullptr, nullptr};
   // kernel timers (off unless sg_ctx_enable_timers)
   bool timing = false;
   bool count_work = false;  // SG_TIMERS_COUNT_WORK
@@ -263,6 +272,12 @@ void launch_group_offsets(sg_ctx* ctx, const uint32_t* key, uint32_t n, uint32_t
 // Read a few scalars back (blocking on the context stream).
 void copy_to_host(sg_ctx* ctx, void* dst, const void* src, size_t bytes);
 
+// Pinned staging for host-to-device copies (a pageable source costs the runtime's own
+// staging and ~20 us): stage_acquire waits until the slot's previous copy has left it
+// and returns it (grown to `bytes`); stage_release after the hipMemcpyAsync out of it.
+char* stage_acquire(sg_ctx* ctx, int slot, size_t bytes);
+void stage_release(sg_ctx* ctx, int slot);
+
 // Add algorithmic work to a timer after the fact (e.g. a device-side count).
 void timer_add_work(sg_ctx* ctx, const char* name, double work);
 
@@ -319,7 +334,8 @@ struct SsspDevPlan {
 };
 constexpr int SSSP_PHASES_MAX = 6;
 SsspDevPlan sssp_device_plan(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin,
-                             uint32_t row_end, int n_phase, int kb, bool exact, int hops, uint32_t n_land);
+                             uint32_t row_end, int n_phase, int kb, bool exact, int hops, uint32_t n_land,
+                             uint32_t* zero_rows = nullptr);
 // After phase 0 (the landmarks) ran: phase 1's bound rows from the landmark rows' columns.
 void sssp_landmark_bounds(sg_ctx* ctx, const SsspDevPlan& p, uint32_t n_used, uint32_t row_begin,
                           const uint64_t* out_lat, const uint32_t* sat_row, int kb);

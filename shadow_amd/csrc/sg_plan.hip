@@ -46,10 +46,15 @@
 
 namespace sg {
 
+// rel[used row] = its relative row; also zeroes jn (and the caller's per-row flags):
+// no fills on the build's path
 __global__ void k_plan_rel(const uint32_t* __restrict__ used, uint32_t row_begin, uint32_t rows,
-                           uint32_t* __restrict__ rel) {
+                           uint32_t* __restrict__ rel, uint8_t* __restrict__ jn, uint32_t* __restrict__ zero_rows) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < rows) rel[used[row_begin + r]] = r;
+  if (r >= rows) return;
+  rel[used[row_begin + r]] = r;
+  jn[r] = 0;
+  if (zero_rows) zero_rows[r] = 0;
 }
 
 // jn[r]: 0 while row r is in no phase, else its phase + 1 (set once).  Gain of an
@@ -199,18 +204,72 @@ void sssp_landmark_bounds(sg_ctx* ctx, const SsspDevPlan& p, uint32_t n_used, ui
   SG_CHECK_LAUNCH();
 }
 
-// Rows still in no phase take the last one; each phase's rows in row order (block
-// scans) and the counts; the phase launches' claim counters zeroed.
+// Rows still in no phase take the last one; each phase's rows in row order and the
+// counts; the phase launches' claim counters zeroed.  Two passes over the rows, no
+// barrier inside either: (1) per (chunk of NT rows, wave, phase) counts by ballot
+// into LDS; one block scan of the counts in (phase, chunk, wave) order; (2) each row
+// at its (phase, chunk, wave) offset plus its rank among the wave's lanes of its
+// phase.  (The earlier form scanned the rows once per phase, two barriers per chunk:
+// 22 us at C3.)  Up to PL_CHUNKS chunks; larger plans take the per-phase form.
+constexpr uint32_t PL_CHUNKS = 64;
 template <int NT>
 __global__ void __launch_bounds__(NT)
     k_plan_lists(const uint8_t* __restrict__ jn, uint32_t rows, uint32_t row_begin, int n_phase,
                  uint8_t* __restrict__ phase_out, uint32_t* __restrict__ list, uint32_t* __restrict__ ctl,
                  uint32_t* __restrict__ ctr) {
   constexpr int NW = NT / 64;
+  __shared__ uint32_t s_cnt[SSSP_PHASES_MAX * PL_CHUNKS * NW];  // (phase, chunk, wave) counts, then offsets
   __shared__ uint32_t s_wsum[NW];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int i = tid; i < 2 * SSSP_PHASES_MAX; i += NT) ctr[i] = 0;
   auto phase_of = [&](uint32_t r) { return jn[r] ? (int)jn[r] - 1 : n_phase - 1; };
+  const uint32_t chunks = (rows + NT - 1) / NT;
+  const uint64_t lt = (1ull << lane) - 1;
+  if (chunks <= PL_CHUNKS) {
+    const uint32_t n_ent = (uint32_t)n_phase * chunks * NW;
+    for (uint32_t c = 0; c < chunks; c++) {
+      const uint32_t r = c * NT + tid;
+      const int ph = r < rows ? phase_of(r) : -1;
+      for (int p = 0; p < n_phase; p++) {
+        const uint64_t m = __ballot(ph == p);
+        if (lane == 0) s_cnt[((uint32_t)p * chunks + c) * NW + wv] = (uint32_t)__popcll(m);
+      }
+      if (r < rows) phase_out[r] = (uint8_t)ph;
+    }
+    __syncthreads();
+    // exclusive scan of the n_ent counts: thread t sums a contiguous range of `per`
+    const uint32_t per = (n_ent + NT - 1) / NT, b = tid * per, e = min(b + per, n_ent);
+    uint32_t sum = 0;
+    for (uint32_t i = b; i < e; i++) sum += s_cnt[i];
+    const uint32_t incl = wave_incl_sum(sum);
+    if (lane == 63) s_wsum[wv] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (int w = 0; w < wv; w++) run += s_wsum[w];
+    for (uint32_t i = b; i < e; i++) {
+      const uint32_t x = s_cnt[i];
+      s_cnt[i] = run;
+      run += x;
+    }
+    __syncthreads();
+    if (tid < n_phase) {
+      const uint32_t start = chunks ? s_cnt[(uint32_t)tid * chunks * NW] : 0u;
+      const uint32_t next = tid + 1 < n_phase ? s_cnt[(uint32_t)(tid + 1) * chunks * NW] : rows;
+      ctl[2 * tid] = start;
+      ctl[2 * tid + 1] = next - start;
+    }
+    for (uint32_t c = 0; c < chunks; c++) {
+      const uint32_t r = c * NT + tid;
+      const int ph = r < rows ? phase_of(r) : -1;
+      uint64_t mine = 0;
+      for (int p = 0; p < n_phase; p++) {
+        const uint64_t m = __ballot(ph == p);
+        if (ph == p) mine = m;
+      }
+      if (r < rows) list[s_cnt[((uint32_t)ph * chunks + c) * NW + wv] + (uint32_t)__popcll(mine & lt)] = row_begin + r;
+    }
+    return;
+  }
   uint32_t base = 0;
   for (int ph = 0; ph < n_phase; ph++) {
     const uint32_t start = base;
@@ -363,7 +422,8 @@ __global__ void __launch_bounds__(PB_WAVES * 64)
 }
 
 SsspDevPlan sssp_device_plan(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin,
-                             uint32_t row_end, int n_phase, int kb, bool exact, int hops, uint32_t n_land) {
+                             uint32_t row_end, int n_phase, int kb, bool exact, int hops, uint32_t n_land,
+                             uint32_t* zero_rows) {
   (void)n_used;
   const uint32_t n = net->n_nodes, rows = row_end - row_begin;
   n_phase = std::max(2, std::min(SSSP_PHASES_MAX - (n_land ? 1 : 0), n_phase));
@@ -387,9 +447,8 @@ SsspDevPlan sssp_device_plan(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
   {
     TimedLaunch tl(ctx, "plan_sets", 0.0);
     SG_HIP(hipMemsetAsync(rel, 0xff, (size_t)n * 4, st));
-    SG_HIP(hipMemsetAsync(jn, 0, rows, st));
     const unsigned g = grid_for(rows, 256);
-    hipLaunchKernelGGL(k_plan_rel, dim3(g), dim3(256), 0, st, d_used, row_begin, rows, rel);
+    hipLaunchKernelGGL(k_plan_rel, dim3(g), dim3(256), 0, st, d_used, row_begin, rows, rel, jn, zero_rows);
     // in-neighbours: the CSC when directed; the out-arcs themselves when undirected
     const uint32_t* in_off = net->directed ? net->in_off : net->out_off;
     const uint32_t* in_idx = net->directed ? net->in_src : net->out_arc;

@@ -83,32 +83,63 @@ __global__ void k_net_count(const uint32_t* __restrict__ src, const uint32_t* __
 
 // Exclusive scans of indeg and outdeg (n + 1 entries each, the last one the
 // total) in one workgroup, each result written twice: the offsets and the
-// scatter's cursors.  For graphs up to NET_SCAN_SMALL nodes.
+// scatter's cursors.  For graphs up to NET_SCAN_SMALL nodes.  Both arrays in one
+// pass over chunks of 8 x 1024 consecutive entries (coalesced loads, 16 in flight
+// per thread); a thread's running offset carries across chunks in a register.
+// (The earlier form gave each thread 10+ strided entries, one array at a time: 22 us at C3.)
 constexpr uint32_t NET_SCAN_SMALL = 1u << 17;
 __global__ void __launch_bounds__(1024) k_net_scan(const uint32_t* __restrict__ indeg, const uint32_t* __restrict__ outdeg,
                                                    uint32_t n, uint32_t* __restrict__ in_off, uint32_t* __restrict__ in_cur,
                                                    uint32_t* __restrict__ out_off, uint32_t* __restrict__ out_cur) {
-  __shared__ uint32_t s_w[16];
+  constexpr int PER = 8;
+  __shared__ uint32_t s_w[2][16];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const uint32_t per = (n + 1 + 1023) / 1024;  // consecutive entries per thread
-  for (int k = 0; k < 2; k++) {
-    const uint32_t* x = k ? outdeg : indeg;
-    uint32_t* o1 = k ? out_off : in_off;
-    uint32_t* o2 = k ? out_cur : in_cur;
-    const uint32_t b = tid * per, e = min(b + per, n + 1);
-    uint32_t sum = 0;
-    for (uint32_t i = b; i < e; i++) sum += i < n ? x[i] : 0u;
-    const uint32_t incl = wave_incl_sum(sum);
-    if (lane == 63) s_w[wv] = incl;
-    __syncthreads();
-    uint32_t run = incl - sum;
-    for (int w = 0; w < wv; w++) run += s_w[w];
-    for (uint32_t i = b; i < e; i++) {
-      o1[i] = run;
-      o2[i] = run;
-      run += i < n ? x[i] : 0u;
+  // branch-free loads (past n: an out-of-range offset reads 0), so all 16 are in flight
+  // at once; with a branch per element the compiler waited for each load in turn
+  const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc((void*)indeg, 0, (int)(n * 4u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)outdeg, 0, (int)(n * 4u), 0x00020000);
+  uint32_t carry_i = 0, carry_o = 0;
+  for (uint32_t base = 0; base <= n; base += PER * 1024) {
+    uint32_t xi[PER], xo[PER];
+    uint32_t si = 0, so = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const uint32_t i = base + (uint32_t)tid * PER + k;
+      xi[k] = __builtin_amdgcn_raw_buffer_load_b32(ri, i < n ? i * 4u : 0x80000000u, 0, 0);
+      xo[k] = __builtin_amdgcn_raw_buffer_load_b32(ro, i < n ? i * 4u : 0x80000000u, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      si += xi[k];
+      so += xo[k];
+    }
+    const uint32_t ii = wave_incl_sum(si), io = wave_incl_sum(so);
+    if (lane == 63) {
+      s_w[0][wv] = ii;
+      s_w[1][wv] = io;
     }
     __syncthreads();
+    uint32_t pi = carry_i + ii - si, po = carry_o + io - so;
+    for (int w = 0; w < 16; w++) {
+      const uint32_t a = s_w[0][w], b = s_w[1][w];
+      pi += w < wv ? a : 0u;
+      po += w < wv ? b : 0u;
+      carry_i += a;
+      carry_o += b;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const uint32_t i = base + (uint32_t)tid * PER + k;
+      if (i <= n) {
+        in_off[i] = pi;
+        in_cur[i] = pi;
+        out_off[i] = po;
+        out_cur[i] = po;
+      }
+      pi += xi[k];
+      po += xo[k];
+    }
+    __syncthreads();  // s_w is rewritten by the next chunk
   }
 }
 
@@ -756,6 +787,64 @@ __global__ void k_self_check(const uint32_t* __restrict__ used, uint32_t n_used,
   }
 }
 
+// The LDS search's last launch of a build: how many rows it flagged for the wide
+// kernel, and (when sg_routing_build asked for it) the self-loop check's first
+// failure as k_self_check encodes it, both into the mapped return block -- the
+// build's end is one synchronisation and no copies.  One workgroup, branch-free loads.
+__global__ void __launch_bounds__(1024) k_build_finish(const uint32_t* __restrict__ sat, uint32_t rows,
+                                                       const uint32_t* __restrict__ used, uint32_t n_used,
+                                                       const uint32_t* __restrict__ self_cnt, uint32_t* __restrict__ ret) {
+  constexpr int G = 8;
+  __shared__ uint32_t s_cnt[16];
+  __shared__ unsigned long long s_min[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  constexpr uint32_t OOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sat, 0, (int)(rows * 4u), 0x00020000);
+  uint32_t cnt = 0;
+  for (uint32_t r0 = tid; r0 < rows; r0 += G * 1024) {
+    uint32_t x[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      const uint32_t r = r0 + g * 1024;
+      x[g] = __builtin_amdgcn_raw_buffer_load_b32(rs, r < rows ? r * 4u : OOB, 0, 0);
+    }
+#pragma unroll
+    for (int g = 0; g < G; g++) cnt += x[g] != 0u;
+  }
+  unsigned long long first = ~0ull;
+  if (self_cnt) {
+    const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc((void*)used, 0, (int)(n_used * 4u), 0x00020000);
+    for (uint32_t j0 = tid; j0 < n_used; j0 += G * 1024) {
+      uint32_t v[G], c[G];
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        const uint32_t j = j0 + g * 1024;
+        v[g] = __builtin_amdgcn_raw_buffer_load_b32(ru, j < n_used ? j * 4u : OOB, 0, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < G; g++) c[g] = j0 + g * 1024 < n_used ? self_cnt[v[g]] : 1u;
+#pragma unroll
+      for (int g = 0; g < G; g++)
+        if (c[g] != 1u) first = min(first, ((unsigned long long)(j0 + g * 1024) << 1) | (c[g] > 1u ? 1ull : 0ull));
+    }
+  }
+  cnt = wave_incl_sum(cnt);
+  for (int d = 32; d > 0; d >>= 1) first = min(first, (unsigned long long)__shfl_xor(first, d));
+  if (lane == 63) s_cnt[wv] = cnt;
+  if (lane == 0) s_min[wv] = first;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t t = 0;
+    unsigned long long m = ~0ull;
+    for (int w = 0; w < 16; w++) {
+      t += s_cnt[w];
+      m = min(m, s_min[w]);
+    }
+    ret[4] = t;
+    ((unsigned long long*)ret)[1] = m;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Direct paths (graph/mod.rs:230-252): per used pair, count the edges that
 // petgraph's edges_connecting would yield.
@@ -906,16 +995,32 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   const uint32_t n = g->n_nodes, m = g->n_edges;
   if (m && (!g->edge_src || !g->edge_dst || !g->edge_latency_ns || !g->edge_packet_loss))
     throw Error(SG_ERR_INVALID_ARG, "null edge array");
+  // validation: branch-free passes over the edge arrays (part of every one-shot build);
+  // the per-edge loop that names the first bad edge runs only when one is bad
   uint64_t n_self = 0;
-  for (uint32_t e = 0; e < m; e++) {
-    if (g->edge_src[e] >= n || g->edge_dst[e] >= n)
-      throw Error(SG_ERR_INVALID_ARG, "edge " + std::to_string(e) + " endpoint out of range");
-    float l = g->edge_packet_loss[e];
-    if (!(l >= 0.0f && l <= 1.0f))  // graph/mod.rs:101-103 (NaN rejected too)
-      throw Error(SG_ERR_INVALID_ARG, "Edge 'packet_loss' is not in the range [0,1]");
-    if (g->edge_latency_ns[e] == 0)  // graph/mod.rs:105-107
-      throw Error(SG_ERR_INVALID_ARG, "Edge 'latency' must not be 0");
-    n_self += g->edge_src[e] == g->edge_dst[e];
+  {
+    const uint32_t* __restrict__ es = g->edge_src;
+    const uint32_t* __restrict__ ed = g->edge_dst;
+    const uint64_t* __restrict__ el = g->edge_latency_ns;
+    const float* __restrict__ ef = g->edge_packet_loss;
+    uint32_t bad = 0, ns = 0;
+    for (uint32_t e = 0; e < m; e++) {
+      const uint32_t a = es[e], b = ed[e];
+      bad |= (uint32_t)(a >= n) | (uint32_t)(b >= n);
+      ns += a == b;
+    }
+    for (uint32_t e = 0; e < m; e++) bad |= (uint32_t)!(ef[e] >= 0.0f) | (uint32_t)!(ef[e] <= 1.0f);
+    for (uint32_t e = 0; e < m; e++) bad |= (uint32_t)(el[e] == 0);
+    n_self = ns;
+    for (uint32_t e = 0; bad && e < m; e++) {
+      if (es[e] >= n || ed[e] >= n)
+        throw Error(SG_ERR_INVALID_ARG, "edge " + std::to_string(e) + " endpoint out of range");
+      const float l = ef[e];
+      if (!(l >= 0.0f && l <= 1.0f))  // graph/mod.rs:101-103 (NaN rejected too)
+        throw Error(SG_ERR_INVALID_ARG, "Edge 'packet_loss' is not in the range [0,1]");
+      if (el[e] == 0)  // graph/mod.rs:105-107
+        throw Error(SG_ERR_INVALID_ARG, "Edge 'latency' must not be 0");
+    }
   }
   // arcs without self-loops, both directions when undirected (petgraph semantics, graph/mod.rs:137-152)
   const uint64_t arcs = ((uint64_t)m - n_self) * (g->directed ? 1u : 2u);
@@ -979,23 +1084,13 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   net->out_arc = (uint32_t*)(base + o_outarc);
   if (m) {  // the edge arrays through the context's pinned staging, one copy (they are adjacent)
     const size_t eb = o_inoff;  // bytes up to the first derived array
-    if (ctx->h_stage_bytes < eb) {
-      if (ctx->stage_used) SG_HIP(hipEventSynchronize(ctx->stage_used));
-      if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
-      ctx->h_stage = nullptr;
-      ctx->h_stage_bytes = 0;
-      SG_HIP(hipHostMalloc(&ctx->h_stage, eb, hipHostMallocDefault));
-      ctx->h_stage_bytes = eb;
-    }
-    if (!ctx->stage_used) SG_HIP(hipEventCreateWithFlags(&ctx->stage_used, hipEventDisableTiming));
-    SG_HIP(hipEventSynchronize(ctx->stage_used));  // the previous copy out of the staging is done
-    char* h = (char*)ctx->h_stage;
+    char* h = stage_acquire(ctx, 0, eb);
     memcpy(h + o_esrc, g->edge_src, m * 4ull);
     memcpy(h + o_edst, g->edge_dst, m * 4ull);
     memcpy(h + o_elat, g->edge_latency_ns, m * 8ull);
     memcpy(h + o_eloss, g->edge_packet_loss, m * 4ull);
     SG_HIP(hipMemcpyAsync(base, h, eb, hipMemcpyHostToDevice, st));
-    SG_HIP(hipEventRecord(ctx->stage_used, st));
+    stage_release(ctx, 0);
   }
   uint32_t* indeg = ctx->r_misc.get<uint32_t>(2 * ((size_t)n + 1));
   uint32_t* outdeg = indeg + n + 1;
@@ -1043,9 +1138,7 @@ static unsigned long long* launch_self_loops(sg_ctx* ctx, sg_net* net, const uin
   return first;
 }
 
-static void raise_self_loops(sg_ctx* ctx, sg_net* net, const unsigned long long* first, const uint32_t* h_used) {
-  unsigned long long h = 0;
-  copy_to_host(ctx, &h, first, 8);
+static void raise_self_value(sg_net* net, unsigned long long h, const uint32_t* h_used) {
   if (h != ~0ull) {
     uint32_t j = (uint32_t)(h >> 1);
     std::string id = node_name(net, h_used[j]);
@@ -1053,6 +1146,24 @@ static void raise_self_loops(sg_ctx* ctx, sg_net* net, const unsigned long long*
       throw Error(SG_ERR_MULTI_EDGE, "More than one edge connecting node " + id + " to " + id, j, j);
     throw Error(SG_ERR_NO_EDGE, "No edge connecting node " + id + " to " + id, j, j);
   }
+}
+
+static void raise_self_loops(sg_ctx* ctx, sg_net* net, const unsigned long long* first, const uint32_t* h_used) {
+  unsigned long long h = 0;
+  copy_to_host(ctx, &h, first, 8);
+  raise_self_value(net, h, h_used);
+}
+
+// sg_routing_build's check: the value the LDS search's final kernel read, else a launch of its own
+static void raise_self_check(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
+                             const uint32_t* h_used) {
+  const bool done = ctx->self_done;
+  const unsigned long long v = ctx->self_first;
+  ctx->self_used = nullptr;
+  ctx->self_cnt = nullptr;
+  ctx->self_done = false;
+  if (done) raise_self_value(net, v, h_used);
+  else raise_self_loops(ctx, net, launch_self_loops(ctx, net, d_used, n_used), h_used);
 }
 
 // Wide recomputation of the listed rows (absolute row indices).
@@ -1284,8 +1395,7 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
                                float* out_loss) {
   hipStream_t st = ctx->stream;
   const uint32_t rows = row_end - row_begin;
-  uint32_t* sat = ctx->r_flags.get<uint32_t>(rows);
-  SG_HIP(hipMemsetAsync(sat, 0, rows * 4ull, st));
+  uint32_t* sat = ctx->r_flags.get<uint32_t>(rows);  // zeroed by the plan's first kernel, else here
   unsigned long long* work = ctx->count_work ? ctx->r_work.get<unsigned long long>(WORK_SHARDS) : nullptr;
   if (work) SG_HIP(hipMemsetAsync(work, 0, WORK_SHARDS * 8, st));
   const char* ds = getenv("SG_APSP_DELTA");
@@ -1302,6 +1412,7 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   // against 1.38, a 4,000-node build 0.97 against 1.07).  SG_SSSP_SEEDS=0 never, =2 always.
   const int seeds_env = env_int("SG_SSSP_SEEDS", 1);
   const bool phased = seeds_env != 0 && (seeds_env == 2 || rows >= 8u * (uint32_t)ctx->n_cu);
+  if (!phased) SG_HIP(hipMemsetAsync(sat, 0, rows * 4ull, st));
   if (phased) {
     // phases by rows per CU (one box, tools/sssp_ab.py --rows, C3 graph): 39 rows per CU
     // (10k rows) 4 phases; 19.5 (a half) 3 phases, 2.25 against 2.57 ms unbounded;
@@ -1321,7 +1432,7 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
     const int land_env = env_int("SG_SSSP_LANDMARKS", 0);
     const uint32_t n_land = net->directed || land_env <= 0 ? 0u : (uint32_t)land_env;
     const SsspDevPlan plan =
-        sssp_device_plan(ctx, net, d_used, n_used, row_begin, row_end, n_phase, kb, exact, hops, n_land);
+        sssp_device_plan(ctx, net, d_used, n_used, row_begin, row_end, n_phase, kb, exact, hops, n_land, sat);
     if (const int warm = env_int("SG_PLAN_WARM", 0))
       hipLaunchKernelGGL(k_busy, dim3(4 * ctx->n_cu), dim3(256), 0, ctx->stream, (uint32_t)warm, (float*)nullptr);
     // SG_PLAN_SYNC=1 (A/B diagnostics): read the phase sizes to the host and launch with host-known counts
@@ -1372,11 +1483,25 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
             "%.0f relaxations (%.2f x arcs)\n", delta, n_diag, a[0] / n_diag, a[1] / n_diag, a[2] / n_diag,
             a[3] / n_diag, a[4] / n_diag, a[4] / n_diag / std::max(1u, net->n_arcs));
   }
-  std::vector<uint32_t> h_sat(rows);
-  copy_to_host(ctx, h_sat.data(), sat, rows * 4ull);
+  // the flagged rows' count and the self-loop check in one kernel, one synchronisation;
+  // the flags themselves are copied only when some row was flagged
+  hipLaunchKernelGGL(k_build_finish, dim3(1), dim3(1024), 0, st, sat, rows, ctx->self_used, ctx->self_n,
+                     ctx->self_cnt, ctx->apsp_ret);
+  SG_CHECK_LAUNCH();
+  SG_HIP(hipStreamSynchronize(st));
+  const volatile uint32_t* ret = ctx->apsp_ret;
+  const uint32_t n_flag = ret[4];
+  if (ctx->self_used) {
+    ctx->self_first = *(const volatile unsigned long long*)(ret + 2);
+    ctx->self_done = true;
+  }
   std::vector<uint32_t> wide_rows;
-  for (uint32_t r = 0; r < rows; r++)
-    if (h_sat[r]) wide_rows.push_back(row_begin + r);
+  if (n_flag) {
+    std::vector<uint32_t> h_sat(rows);
+    copy_to_host(ctx, h_sat.data(), sat, rows * 4ull);
+    for (uint32_t r = 0; r < rows; r++)
+      if (h_sat[r]) wide_rows.push_back(row_begin + r);
+  }
   if (work) {
     unsigned long long w[WORK_SHARDS];
     copy_to_host(ctx, w, work, sizeof(w));
@@ -1612,13 +1737,17 @@ int32_t sg_routing_build(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32
     if (n_used == 0) return;
     hipStream_t st = ctx->stream;
     uint32_t* d_used = ctx->r_used.get<uint32_t>(n_used);
-    SG_HIP(hipMemcpyAsync(d_used, nodes, (size_t)n_used * 4, hipMemcpyHostToDevice, st));
+    {
+      char* hu = stage_acquire(ctx, 1, (size_t)n_used * 4);
+      memcpy(hu, nodes, (size_t)n_used * 4);
+      SG_HIP(hipMemcpyAsync(d_used, hu, (size_t)n_used * 4, hipMemcpyHostToDevice, st));
+      stage_release(ctx, 1);
+    }
     const bool shortest = flags & SG_ROUTE_SHORTEST_PATH;
     // The reference checks every used node's self-loop (graph/mod.rs:211-217),
     // whichever rows this call computes.
-    const unsigned long long* self_first = shortest ? launch_self_loops(ctx, net, d_used, n_used) : nullptr;
     if (row_end == row_begin) {
-      if (self_first) raise_self_loops(ctx, net, self_first, nodes);
+      if (shortest) raise_self_loops(ctx, net, launch_self_loops(ctx, net, d_used, n_used), nodes);
       return;
     }
     const size_t count = (size_t)(row_end - row_begin) * n_used;
@@ -1626,13 +1755,20 @@ int32_t sg_routing_build(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32
     uint64_t* o_lat = dev_out ? out_latency_ns : ctx->r_out_lat.get<uint64_t>(count);
     float* o_loss = dev_out ? out_packet_loss : ctx->r_out_loss.get<float>(count);
     if (shortest) {
+      // the check of every used node's self-loop (graph/mod.rs:210-217) rides on the LDS
+      // search's final kernel (k_build_finish); the other kernels leave it to a launch of its own
+      ctx->self_used = d_used;
+      ctx->self_n = n_used;
+      ctx->self_cnt = net->self_cnt;
+      ctx->self_done = false;
       try {
         shortest_paths(ctx, net, d_used, nodes, n_used, row_begin, row_end, o_lat, o_loss);
       } catch (const Error&) {
-        raise_self_loops(ctx, net, self_first, nodes);  // a self-loop error first (graph/mod.rs:210-219)
+        ctx->self_done = false;  // (the search may have failed before its final kernel)
+        raise_self_check(ctx, net, d_used, n_used, nodes);  // a self-loop error first (graph/mod.rs:210-219)
         throw;
       }
-      raise_self_loops(ctx, net, self_first, nodes);
+      raise_self_check(ctx, net, d_used, n_used, nodes);
     } else
       direct_paths(ctx, net, d_used, nodes, n_used, row_begin, row_end, o_lat, o_loss);
     if (!dev_out) {
@@ -1681,7 +1817,12 @@ int32_t sg_routing_info_fill(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, ui
     // an earlier fill that failed may have left copies in flight into its staging buffers
     SG_HIP(hipStreamSynchronize(ctx->copy_stream));
     uint32_t* d_used = ctx->r_used.get<uint32_t>(n_used);
-    SG_HIP(hipMemcpyAsync(d_used, nodes, (size_t)n_used * 4, hipMemcpyHostToDevice, st));
+    {
+      char* hu = stage_acquire(ctx, 1, (size_t)n_used * 4);
+      memcpy(hu, nodes, (size_t)n_used * 4);
+      SG_HIP(hipMemcpyAsync(d_used, hu, (size_t)n_used * 4, hipMemcpyHostToDevice, st));
+      stage_release(ctx, 1);
+    }
     const bool shortest = flags & SG_ROUTE_SHORTEST_PATH;
     if (shortest) raise_self_loops(ctx, net, launch_self_loops(ctx, net, d_used, n_used), nodes);
     // blocks of about 1/8 of the table (at least 64 rows, whole 64-row batches)
