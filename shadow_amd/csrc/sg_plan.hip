@@ -60,6 +60,15 @@ __global__ void k_plan_rel(const uint32_t* __restrict__ used, uint32_t row_begin
 // jn[r]: 0 while row r is in no phase, else its phase + 1 (set once).  Gain of an
 // unassigned row c for the set of phase ph: the unassigned rows in its closed
 // in-neighbourhood (arcs counted).
+// The vote kernels take a row's arcs eight at a time with branch-free buffer loads
+// (an out-of-range offset reads 0, no traffic): each step is one chain of dependent
+// loads (arc -> rel -> jn / gain) with eight arcs in flight, not eight chains in turn.
+constexpr uint32_t PL_OOB = 0x80000000u;
+constexpr int PL_ARCS = 8;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pl_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7FFFFFFF, 0x00020000);
+}
+
 __global__ void k_vote_gain(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_idx,
                             uint32_t in_stride, const uint32_t* __restrict__ used, uint32_t row_begin, uint32_t rows,
                             const uint32_t* __restrict__ rel, const uint8_t* __restrict__ jn,
@@ -67,10 +76,22 @@ __global__ void k_vote_gain(const uint32_t* __restrict__ in_off, const uint32_t*
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= rows || jn[c]) return;
   const uint32_t v = used[row_begin + c];
+  const __amdgpu_buffer_rsrc_t ri = pl_rsrc(in_idx), rr = pl_rsrc(rel), rj = pl_rsrc(jn);
+  const uint32_t a0 = in_off[v], a1 = in_off[v + 1];
   uint32_t g = 1;
-  for (uint32_t a = in_off[v]; a < in_off[v + 1]; a++) {
-    const uint32_t u = rel[in_idx[(size_t)in_stride * a]];
-    g += u != ~0u && !jn[u];
+  for (uint32_t a = a0; a < a1; a += PL_ARCS) {
+    uint32_t t[PL_ARCS], u[PL_ARCS];
+#pragma unroll
+    for (int k = 0; k < PL_ARCS; k++)
+      t[k] = __builtin_amdgcn_raw_buffer_load_b32(ri, a + k < a1 ? (a + k) * in_stride * 4u : PL_OOB, 0, 0);
+#pragma unroll
+    for (int k = 0; k < PL_ARCS; k++) u[k] = __builtin_amdgcn_raw_buffer_load_b32(rr, a + k < a1 ? t[k] * 4u : PL_OOB, 0, 0);
+#pragma unroll
+    for (int k = 0; k < PL_ARCS; k++) {
+      const bool on = a + k < a1 && u[k] != ~0u;
+      const uint8_t x = __builtin_amdgcn_raw_buffer_load_b8(rj, on ? u[k] : PL_OOB, 0, 0);
+      g += on && !x;
+    }
   }
   gain[c] = g;
 }
@@ -84,17 +105,30 @@ __global__ void k_vote_name(const uint32_t* __restrict__ out_off, const uint32_t
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= rows) return;
   const uint8_t tag = (uint8_t)(ph + 1);
-  auto open = [&](uint32_t c) {
-    const uint8_t x = jn[c];
-    return x == 0 || x == tag;
-  };
-  if (!open(u)) return;  // in an earlier phase (a row named during this launch still names)
-  auto score = [&](uint32_t c) { return ((uint64_t)gain[c] << 32) | (0xFFFFFFFFu - c); };
+  auto open_tag = [&](uint8_t x) { return x == 0 || x == tag; };
+  if (!open_tag(jn[u])) return;  // in an earlier phase (a row named during this launch still names)
+  auto score = [&](uint32_t g, uint32_t c) { return ((uint64_t)g << 32) | (0xFFFFFFFFu - c); };
   const uint32_t v = used[row_begin + u];
-  uint64_t best = score(u);
-  for (uint32_t a = out_off[v]; a < out_off[v + 1]; a++) {
-    const uint32_t c = rel[out_arc[3 * (size_t)a]];
-    if (c != ~0u && open(c)) best = max(best, score(c));
+  uint64_t best = score(gain[u], u);
+  const __amdgpu_buffer_rsrc_t ra = pl_rsrc(out_arc), rr = pl_rsrc(rel), rj = pl_rsrc(jn), rg = pl_rsrc(gain);
+  const uint32_t a0 = out_off[v], a1 = out_off[v + 1];
+  for (uint32_t a = a0; a < a1; a += PL_ARCS) {
+    uint32_t t[PL_ARCS], c[PL_ARCS], g[PL_ARCS];
+    uint8_t x[PL_ARCS];
+#pragma unroll
+    for (int k = 0; k < PL_ARCS; k++)
+      t[k] = __builtin_amdgcn_raw_buffer_load_b32(ra, a + k < a1 ? (a + k) * 12u : PL_OOB, 0, 0);
+#pragma unroll
+    for (int k = 0; k < PL_ARCS; k++) c[k] = __builtin_amdgcn_raw_buffer_load_b32(rr, a + k < a1 ? t[k] * 4u : PL_OOB, 0, 0);
+#pragma unroll
+    for (int k = 0; k < PL_ARCS; k++) {
+      const bool on = a + k < a1 && c[k] != ~0u;
+      x[k] = __builtin_amdgcn_raw_buffer_load_b8(rj, on ? c[k] : PL_OOB, 0, 0);
+      g[k] = __builtin_amdgcn_raw_buffer_load_b32(rg, on ? c[k] * 4u : PL_OOB, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < PL_ARCS; k++)
+      if (a + k < a1 && c[k] != ~0u && open_tag(x[k])) best = max(best, score(g[k], c[k]));
   }
   jn[0xFFFFFFFFu - (uint32_t)best] = tag;
 }
@@ -227,14 +261,32 @@ __global__ void __launch_bounds__(NT)
   const uint64_t lt = (1ull << lane) - 1;
   if (chunks <= PL_CHUNKS) {
     const uint32_t n_ent = (uint32_t)n_phase * chunks * NW;
-    for (uint32_t c = 0; c < chunks; c++) {
+    // the first PL_REG chunks' jn loaded up front (branch-free, all in flight) and kept
+    // in registers for pass 2; the loops over them are unrolled (static register indices)
+    constexpr uint32_t PL_REG = 16;
+    uint8_t jr[PL_REG];
+    const __amdgpu_buffer_rsrc_t rj = __builtin_amdgcn_make_buffer_rsrc((void*)jn, 0, (int)rows, 0x00020000);
+#pragma unroll
+    for (uint32_t c = 0; c < PL_REG; c++) {
       const uint32_t r = c * NT + tid;
-      const int ph = r < rows ? phase_of(r) : -1;
+      jr[c] = __builtin_amdgcn_raw_buffer_load_b8(rj, c < chunks && r < rows ? r : 0x80000000u, 0, 0);
+    }
+    auto count_chunk = [&](uint32_t c, int ph) {
       for (int p = 0; p < n_phase; p++) {
         const uint64_t m = __ballot(ph == p);
         if (lane == 0) s_cnt[((uint32_t)p * chunks + c) * NW + wv] = (uint32_t)__popcll(m);
       }
+      const uint32_t r = c * NT + tid;
       if (r < rows) phase_out[r] = (uint8_t)ph;
+    };
+#pragma unroll
+    for (uint32_t c = 0; c < PL_REG; c++) {
+      const uint32_t r = c * NT + tid;
+      if (c < chunks) count_chunk(c, r < rows ? (jr[c] ? (int)jr[c] - 1 : n_phase - 1) : -1);
+    }
+    for (uint32_t c = PL_REG; c < chunks; c++) {
+      const uint32_t r = c * NT + tid;
+      count_chunk(c, r < rows ? phase_of(r) : -1);
     }
     __syncthreads();
     // exclusive scan of the n_ent counts: thread t sums a contiguous range of `per`
@@ -258,15 +310,23 @@ __global__ void __launch_bounds__(NT)
       ctl[2 * tid] = start;
       ctl[2 * tid + 1] = next - start;
     }
-    for (uint32_t c = 0; c < chunks; c++) {
-      const uint32_t r = c * NT + tid;
-      const int ph = r < rows ? phase_of(r) : -1;
+    auto place_chunk = [&](uint32_t c, int ph) {
       uint64_t mine = 0;
       for (int p = 0; p < n_phase; p++) {
         const uint64_t m = __ballot(ph == p);
         if (ph == p) mine = m;
       }
+      const uint32_t r = c * NT + tid;
       if (r < rows) list[s_cnt[((uint32_t)ph * chunks + c) * NW + wv] + (uint32_t)__popcll(mine & lt)] = row_begin + r;
+    };
+#pragma unroll
+    for (uint32_t c = 0; c < PL_REG; c++) {
+      const uint32_t r = c * NT + tid;
+      if (c < chunks) place_chunk(c, r < rows ? (jr[c] ? (int)jr[c] - 1 : n_phase - 1) : -1);
+    }
+    for (uint32_t c = PL_REG; c < chunks; c++) {
+      const uint32_t r = c * NT + tid;
+      place_chunk(c, r < rows ? phase_of(r) : -1);
     }
     return;
   }

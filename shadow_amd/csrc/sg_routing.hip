@@ -84,15 +84,18 @@ __global__ void k_net_count(const uint32_t* __restrict__ src, const uint32_t* __
 // Exclusive scans of indeg and outdeg (n + 1 entries each, the last one the
 // total) in one workgroup, each result written twice: the offsets and the
 // scatter's cursors.  For graphs up to NET_SCAN_SMALL nodes.  Both arrays in one
-// pass over chunks of 8 x 1024 consecutive entries (coalesced loads, 16 in flight
-// per thread); a thread's running offset carries across chunks in a register.
-// (The earlier form gave each thread 10+ strided entries, one array at a time: 22 us at C3.)
+// pass over chunks of 16 x 1024 consecutive entries (32 branch-free loads in flight
+// per thread); a thread's running offset carries across chunks in a register, and
+// the offsets go out through LDS as coalesced stores.  (The earlier form gave each
+// thread 10+ strided entries, one array at a time: 22 us at C3; with 8 entries per
+// thread and stores straight from registers, 28 us; through LDS, 14.7 us.)
 constexpr uint32_t NET_SCAN_SMALL = 1u << 17;
 __global__ void __launch_bounds__(1024) k_net_scan(const uint32_t* __restrict__ indeg, const uint32_t* __restrict__ outdeg,
                                                    uint32_t n, uint32_t* __restrict__ in_off, uint32_t* __restrict__ in_cur,
                                                    uint32_t* __restrict__ out_off, uint32_t* __restrict__ out_cur) {
-  constexpr int PER = 8;
+  constexpr int PER = 16;  // one chunk up to 16,383 nodes
   __shared__ uint32_t s_w[2][16];
+  __shared__ uint32_t s_x[2][PER * 1024];  // 128 KB
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // branch-free loads (past n: an out-of-range offset reads 0), so all 16 are in flight
   // at once; with a branch per element the compiler waited for each load in turn
@@ -127,19 +130,27 @@ __global__ void __launch_bounds__(1024) k_net_scan(const uint32_t* __restrict__ 
       carry_i += a;
       carry_o += b;
     }
+    // the chunk's offsets through LDS, then stored coalesced (entry base + k * 1024 + tid)
 #pragma unroll
     for (int k = 0; k < PER; k++) {
-      const uint32_t i = base + (uint32_t)tid * PER + k;
-      if (i <= n) {
-        in_off[i] = pi;
-        in_cur[i] = pi;
-        out_off[i] = po;
-        out_cur[i] = po;
-      }
+      s_x[0][tid * PER + k] = pi;
+      s_x[1][tid * PER + k] = po;
       pi += xi[k];
       po += xo[k];
     }
-    __syncthreads();  // s_w is rewritten by the next chunk
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const uint32_t i = base + (uint32_t)k * 1024 + tid;
+      const uint32_t a = s_x[0][k * 1024 + tid], b = s_x[1][k * 1024 + tid];
+      if (i <= n) {
+        in_off[i] = a;
+        in_cur[i] = a;
+        out_off[i] = b;
+        out_cur[i] = b;
+      }
+    }
+    __syncthreads();  // s_w and s_x are rewritten by the next chunk
   }
 }
 
