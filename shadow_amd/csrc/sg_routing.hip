@@ -1006,24 +1006,17 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   const uint32_t n = g->n_nodes, m = g->n_edges;
   if (m && (!g->edge_src || !g->edge_dst || !g->edge_latency_ns || !g->edge_packet_loss))
     throw Error(SG_ERR_INVALID_ARG, "null edge array");
-  // validation: branch-free passes over the edge arrays (part of every one-shot build);
-  // the per-edge loop that names the first bad edge runs only when one is bad
-  uint64_t n_self = 0;
-  {
-    const uint32_t* __restrict__ es = g->edge_src;
-    const uint32_t* __restrict__ ed = g->edge_dst;
-    const uint64_t* __restrict__ el = g->edge_latency_ns;
-    const float* __restrict__ ef = g->edge_packet_loss;
-    uint32_t bad = 0, ns = 0;
+  // Validation, in branch-free passes over the edge arrays (part of every one-shot
+  // build).  The endpoints (and the self-loop count the sizes need) before anything
+  // is allocated; the losses and latencies, which index nothing, after the upload's
+  // launches, while the device runs them.  Either way a bad edge is named by the
+  // per-edge loop, which checks every rule edge by edge (the reference's order).
+  const uint32_t* __restrict__ es = g->edge_src;
+  const uint32_t* __restrict__ ed = g->edge_dst;
+  const uint64_t* __restrict__ el = g->edge_latency_ns;
+  const float* __restrict__ ef = g->edge_packet_loss;
+  auto name_bad_edge = [&]() {
     for (uint32_t e = 0; e < m; e++) {
-      const uint32_t a = es[e], b = ed[e];
-      bad |= (uint32_t)(a >= n) | (uint32_t)(b >= n);
-      ns += a == b;
-    }
-    for (uint32_t e = 0; e < m; e++) bad |= (uint32_t)!(ef[e] >= 0.0f) | (uint32_t)!(ef[e] <= 1.0f);
-    for (uint32_t e = 0; e < m; e++) bad |= (uint32_t)(el[e] == 0);
-    n_self = ns;
-    for (uint32_t e = 0; bad && e < m; e++) {
       if (es[e] >= n || ed[e] >= n)
         throw Error(SG_ERR_INVALID_ARG, "edge " + std::to_string(e) + " endpoint out of range");
       const float l = ef[e];
@@ -1032,6 +1025,17 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
       if (el[e] == 0)  // graph/mod.rs:105-107
         throw Error(SG_ERR_INVALID_ARG, "Edge 'latency' must not be 0");
     }
+  };
+  uint64_t n_self = 0;
+  {
+    uint32_t bad = 0, ns = 0;
+    for (uint32_t e = 0; e < m; e++) {
+      const uint32_t a = es[e], b = ed[e];
+      bad |= (uint32_t)(a >= n) | (uint32_t)(b >= n);
+      ns += a == b;
+    }
+    if (bad) name_bad_edge();
+    n_self = ns;
   }
   // arcs without self-loops, both directions when undirected (petgraph semantics, graph/mod.rs:137-152)
   const uint64_t arcs = ((uint64_t)m - n_self) * (g->directed ? 1u : 2u);
@@ -1131,6 +1135,18 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
                        net->e_lat, net->e_loss, m, (int)net->directed, cursor, net->in_src, net->in_dst, net->in_lat,
                        net->in_lat32, net->in_om, net->in_rec, ocursor, net->out_arc);
     SG_CHECK_LAUNCH();
+  }
+  {  // the losses and latencies, while the device runs the upload
+    uint32_t bad = 0;
+    for (uint32_t e = 0; e < m; e++) bad |= (uint32_t)!(ef[e] >= 0.0f) | (uint32_t)!(ef[e] <= 1.0f);
+    for (uint32_t e = 0; e < m; e++) bad |= (uint32_t)(el[e] == 0);
+    if (bad) {
+      // nothing may still run on the block when the caller deletes the net
+      (void)hipStreamSynchronize(st);
+      (void)hipFree(net->mem);
+      net->mem = nullptr;
+      name_bad_edge();
+    }
   }
 }
 

@@ -6,6 +6,7 @@ and seeded random graphs.  Errors must match the reference's error cases.
 """
 import json
 import os
+import re
 
 import numpy as np
 import pytest
@@ -244,6 +245,32 @@ def test_errors_match_reference(oracle, ctx):
     # unused isolated node is fine
     net = NetworkGraph(3, [0, 1, 0, 2], [0, 1, 1, 2], [5] * 4, [0.0] * 4, False, ctx=ctx)
     assert net.compute_shortest_paths([0, 1])[(0, 1)].latency_ns == 5
+
+
+def test_edge_array_validation(oracle, ctx):
+    """sg_net_create's checks of edge arrays (graph/mod.rs:101-107 restated for the array
+    boundary): the first bad edge in edge order names the error, whichever rule it breaks;
+    the endpoint rule is checked before the upload, loss and latency while it runs."""
+    base = dict(n=4, src=[0, 1, 2, 3, 0, 1], dst=[0, 1, 2, 3, 1, 2], lat=[5] * 6, loss=[0.0] * 6)
+    cases = [
+        (dict(loss=[0.0, 0.0, 1.5, 0.0, 0.0, 0.0], dst=[0, 1, 2, 3, 9, 2]), "range [0,1]"),  # loss at 2 before range at 4
+        (dict(dst=[0, 1, 2, 9, 1, 2], lat=[5, 5, 5, 5, 0, 5]), "endpoint out of range"),
+        (dict(lat=[5, 5, 5, 5, 0, 5]), "must not be 0"),
+        (dict(loss=[0.0, 0.0, 0.0, float("nan"), 0.0, 0.0]), "range [0,1]"),
+        (dict(loss=[0.0, -0.5, 0.0, 0.0, 0.0, 0.0]), "range [0,1]"),
+    ]
+    for over, msg in cases:
+        a = dict(base, **over)
+        with pytest.raises(ShadowGpuError, match=re.escape(msg)):
+            NetworkGraph(a["n"], a["src"], a["dst"], a["lat"], np.array(a["loss"], np.float32), False,
+                         ctx=ctx).compute_shortest_paths([0, 1, 2, 3])
+        # the context stays usable: a valid graph right after a rejected one
+        _check(oracle, {"n": 4, "src": np.array(base["src"], np.uint32), "dst": np.array(base["dst"], np.uint32),
+                        "lat": np.array(base["lat"], np.uint64), "loss": np.array(base["loss"], np.float32),
+                        "directed": False}, np.array([0, 1, 2], np.uint32), ctx)
+    # -0.0 is in [0, 1] (a float compare, as the reference's)
+    g = NetworkGraph(2, [0, 1, 0], [0, 1, 1], [5, 5, 5], np.array([0.0, 0.0, -0.0], np.float32), False, ctx=ctx)
+    assert g.compute_shortest_paths([0, 1])[(0, 1)].latency_ns == 5
 
 
 def test_min_latency_device(ctx):

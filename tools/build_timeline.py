@@ -54,16 +54,23 @@ def main():
     used = np.arange(n, dtype=np.uint32)
     lat = torch.empty(n * n, dtype=torch.int64, device="cuda")
     loss = torch.empty(n * n, dtype=torch.float32, device="cuda")
-    ts = []
+    ts, parts = [], []
     for _ in range(a.reps + 1):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         net = NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
+        t1 = time.perf_counter()
+        net._ensure_net()  # sg_net_create: validation, staging copy, upload launches (returns unsynchronised)
+        t2 = time.perf_counter()
         net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
+        t3 = time.perf_counter()
         net.close()
         torch.cuda.synchronize()
-        ts.append((time.perf_counter() - t0) * 1e3)
+        t4 = time.perf_counter()
+        ts.append((t4 - t0) * 1e3)
+        parts.append([round((b - a_) * 1e6, 1) for a_, b in ((t0, t1), (t1, t2), (t2, t3), (t3, t4))])
     print("one-shot build ms:", [round(t, 3) for t in ts], flush=True)
+    print("host us [NetworkGraph(), sg_net_create, build call, close+sync]:", parts[1:], flush=True)
 
 
 if __name__ == "__main__":
