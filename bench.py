@@ -664,8 +664,9 @@ def main():
         t_e2e = (time.perf_counter() - t0) / reps
         same = bool(np.array_equal(ri.latency_ns[: r1 - r0], my_lat.cpu().numpy().view(np.uint64).reshape(-1, nu)[
                     : r1 - r0]))
-        e2e = {"ms": round(t_e2e * 1e3, 3), "pinned": ri.pinned, "table_bytes": 12 * nu * nu,
-               "d2h_GBs": round(12.0 * nu * nu / t_e2e / 1e9, 1), "same_as_device_table": same,
+        # the host table holds 8-byte cells (latency << 32 | bits(loss); sg_route_info.hip)
+        e2e = {"ms": round(t_e2e * 1e3, 3), "pinned": ri.pinned, "table_bytes": 8 * nu * nu,
+               "d2h_GBs": round(8.0 * nu * nu / t_e2e / 1e9, 1), "same_as_device_table": same,
                "what": "sg_routing_info_fill: kernel + D2H of the whole table into the dense host RoutingInfo"}
         del ri
 
