@@ -595,7 +595,46 @@ __global__ void __launch_bounds__(NT)
     if (vec_out) {  // n_used % 4 == 0, 16-B aligned rows: 16-B nontemporal stores
       typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
       typedef float f32x4 __attribute__((ext_vector_type(4)));
-      for (uint32_t j = tid * 4; j < n_used; j += NT * 4) {
+      // Every global read of the output comes before its first store: the columns'
+      // node ids (16-B loads, OU per thread) and the diagonal's raw self-loop.  (Read
+      // inside the loop, each one waited behind the thread's earlier stores, since the
+      // vector-memory counter covers both.)
+      constexpr int OU = 4;
+      const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc((void*)used, 0, (int)(n_used * 4u),
+                                                                          0x00020000);
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 uv[OU];
+#pragma unroll
+      for (int k = 0; k < OU; k++) {
+        const uint32_t j = (tid + (uint32_t)k * NT) * 4;
+        uv[k] = __builtin_amdgcn_raw_buffer_load_b128(ru, j < n_used ? j * 4u : OOB, 0, 0);
+      }
+      const uint32_t de = self_edge[src];
+      const uint64_t d_lat = e_lat[de];
+      const float d_loss = e_loss[de];
+      auto cell = [&](uint32_t j, uint32_t vj, uint64_t& l, float& f) {
+        const uint64_t kk = key[vj];
+        const bool diag = j == row;
+        sat |= !diag && fkey_lat(kk) == LAT32_SAT;
+        l = diag ? d_lat : (uint64_t)fkey_lat(kk);
+        f = diag ? d_loss : __uint_as_float(fkey_loss_bits(kk));
+      };
+#pragma unroll
+      for (int k = 0; k < OU; k++) {
+        const uint32_t j = (tid + (uint32_t)k * NT) * 4;
+        if (j < n_used) {
+          uint64_t l0, l1, l2, l3;
+          float f0, f1, f2, f3;
+          cell(j, uv[k][0], l0, f0);
+          cell(j + 1, uv[k][1], l1, f1);
+          cell(j + 2, uv[k][2], l2, f2);
+          cell(j + 3, uv[k][3], l3, f3);
+          __builtin_nontemporal_store((u64x2){l0, l1}, (u64x2*)&out_lat[orow + j]);
+          __builtin_nontemporal_store((u64x2){l2, l3}, (u64x2*)&out_lat[orow + j + 2]);
+          __builtin_nontemporal_store((f32x4){f0, f1, f2, f3}, (f32x4*)&out_loss[orow + j]);
+        }
+      }
+      for (uint32_t j = (tid + OU * NT) * 4; j < n_used; j += NT * 4) {  // past OU x NT x 4 columns
         uint64_t l0, l1, l2, l3;
         float f0, f1, f2, f3;
         entry(j, l0, f0);
