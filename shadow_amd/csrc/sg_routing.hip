@@ -1788,6 +1788,14 @@ int32_t sg_routing_build(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32
       ctx->self_n = n_used;
       ctx->self_cnt = net->self_cnt;
       ctx->self_done = false;
+      struct Clear {  // however the build ends, no later kernel reads this net's arrays for the check
+        sg_ctx* c;
+        ~Clear() {
+          c->self_used = nullptr;
+          c->self_cnt = nullptr;
+          c->self_done = false;
+        }
+      } clear{ctx};
       try {
         shortest_paths(ctx, net, d_used, nodes, n_used, row_begin, row_end, o_lat, o_loss);
       } catch (const Error&) {
