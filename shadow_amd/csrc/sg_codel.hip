@@ -381,10 +381,10 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
         if (r + 2 < re) k2 = s_qi[r + 2];
         account(pp - pb);
         const uint32_t res = q.pop(now);
-        if (res != CD_NONE) {
-          if (res < q.n_status) q.status[res] = SG_CODEL_DEQUEUED;
-          else q.err |= E_PKT;
-        }
+        // a dequeued packet's status is written with the chunk's results (3. below): a
+        // global store here made the walk's next vector-memory wait (the ring prefetch,
+        // or a register the compiler shares with it) wait for the store too
+        if (res != CD_NONE && res >= q.n_status) q.err |= E_PKT;
         s_p[k] = res;  // a pop's packet slot is read by no one else
       }
       account(pe - pb);
@@ -401,7 +401,9 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
     __syncthreads();
     for (uint32_t i = c0 + t; i < c1; i += CD_THREADS) {  // 3. coalesced results (CD_NONE for a push)
       const uint32_t k = i - c0;
-      a.pop_result[i] = s_pp[k + 1] != s_pp[k] ? CD_NONE : s_p[k];
+      const uint32_t r = s_pp[k + 1] != s_pp[k] ? CD_NONE : s_p[k];
+      a.pop_result[i] = r;
+      if (r < a.n_status) a.status[r] = SG_CODEL_DEQUEUED;  // (CD_NONE >= n_status)
     }
     __syncthreads();
   }
