@@ -648,7 +648,15 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
         }
         if (now >= ia.window_end) q.err |= E_WINDOW;
         while (due(now)) relay_task(q, r, r.tt, ia.bootstrap_end, ia.sim_end, ctr_inc, ia.fwd_time);
-        q.push(pkt, now, len);  // Router::route_incoming_packet
+        // Router::route_incoming_packet: the arrival is the window's next element (staged
+        // slot k, read from LDS when it reaches the head); the ring receives the window's
+        // still-queued elements at the chunk's end, as in k_codel -- a ring store per
+        // arrival made the walk's next vector-memory wait include it
+        (void)pkt;
+        q.tail++;
+        q.bytes += len;
+        if (q.tail - q.head > q.mask + 1u) q.err |= E_FULL;  // an arrival found the ring full
+        if (!q.hv) q.load_head();
         if (!(r.rf & R_PENDING)) {    // notify_router_has_packets: Idle -> forward_later(ZERO)
           ctr_inc++;
           r.rf |= R_PENDING;
@@ -656,6 +664,14 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
           r.tt = now;
         }
       }
+      // the window's elements still queued live on in the ring
+      const uint32_t w0 = q.head - q.t0 <= q.tail - q.t0 ? q.head - q.t0 : 0;
+      for (uint32_t j = w0; j < q.tail - q.t0; j++) {
+        const uint32_t k = q.wb + j;
+        const uint64_t tk = s_t[k];
+        q.ring[(q.t0 + j) & q.mask] = make_uint4(s_p[k], s_l[k], (uint32_t)tk, (uint32_t)(tk >> 32));
+      }
+      q.win = false;  // the next chunk's staging overwrites the window
       if (a.bdiag) d_walk += clock64() - d_w0;
     }
     __syncthreads();
