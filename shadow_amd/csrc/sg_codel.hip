@@ -874,9 +874,11 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
           q.err |= E_FULL;
           continue;
         }
-        const uint4 rec = s_r[k];
-        q.ring[q.tail & q.mask] = rec;  // NetworkInterface::add_data_source
-        if (q.head == q.tail) q.hr = rec;
+        // NetworkInterface::add_data_source: the record is the window's next element (read
+        // from LDS at the head); the ring receives the window's records at the chunk's end
+        // (k_out_compact gathers the sent ones from there) -- a ring store per send made the
+        // walk's next vector-memory wait include it
+        if (q.head == q.tail) q.hr = s_r[k];
         q.tail++;
         if (!(r.rf & R_PENDING)) {  // Relay::notify: Idle -> forward_later(ZERO)
           ctr_inc++;
@@ -885,6 +887,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
           r.tt = now;
         }
       }
+      for (uint32_t j = 0; j < q.tail - q.t0; j++) q.ring[(q.t0 + j) & q.mask] = s_r[q.wb + j];
       if (a.bdiag) d_walk += clock64() - d_w0;
       q.win = false;  // the next chunk's staging overwrites the window
     }
