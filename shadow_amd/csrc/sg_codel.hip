@@ -984,36 +984,50 @@ __global__ void __launch_bounds__(256) k_out_compact(uint32_t H, const uint32_t*
   __syncthreads();
   const uint32_t S = s_off[CD_HOSTS], mask = cap - 1;
   uint32_t o = boff[blockIdx.x];
-  for (uint32_t j0 = 0; j0 < S; j0 += 256) {
-    const uint32_t j = j0 + t;
-    bool keep = false;
-    uint4 rec = make_uint4(0, 0, 0, 0);
-    uint32_t k = 0;
-    if (j < S) {
-      uint32_t lo = 0, hi = CD_HOSTS;  // the host k with s_off[k] <= j < s_off[k + 1]
+  // CU rounds of 256 records per step: every round's ring and forward-time loads are
+  // issued (branch-free, clamped to a valid record) before the step's first store --
+  // a load after a store waited for the store too
+  constexpr int CU = 4;
+  for (uint32_t j0 = 0; j0 < S; j0 += 256 * CU) {
+    uint4 rec[CU];
+    uint32_t kk[CU];
+    bool keep[CU];
+    uint64_t ft[CU];
+#pragma unroll
+    for (int u = 0; u < CU; u++) {
+      const uint32_t j = j0 + u * 256 + t, jc = min(j, S - 1);
+      uint32_t lo = 0, hi = CD_HOSTS;  // the host k with s_off[k] <= jc < s_off[k + 1]
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (s_off[mid] <= j) lo = mid;
+        if (s_off[mid] <= jc) lo = mid;
         else hi = mid;
       }
-      k = lo;
-      rec = ring[(size_t)(h0 + k) * cap + ((s_start[k] + (j - s_off[k])) & mask)];
-      keep = rec.z != s_ip[k];
+      kk[u] = lo;
+      rec[u] = ring[(size_t)(h0 + lo) * cap + ((s_start[lo] + (jc - s_off[lo])) & mask)];
     }
-    const uint64_t m = __ballot(keep);
-    if (lane == 0) wsum[wv] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t pos = o + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-    for (uint32_t w = 0; w < wv; w++) pos += wsum[w];
-    if (keep && pos < out.cap) {
-      out.src_host[pos] = h0 + k;
-      out.dst_ipv4[pos] = rec.z;
-      out.payload_len[pos] = rec.w;
-      out.send_time_ns[pos] = rec.x < n_status ? fwd_time[rec.x] : 0;
-      out.packet[pos] = rec.x;
+#pragma unroll
+    for (int u = 0; u < CU; u++) {
+      keep[u] = j0 + u * 256 + t < S && rec[u].z != s_ip[kk[u]];
+      ft[u] = n_status ? fwd_time[rec[u].x < n_status ? rec[u].x : 0u] : 0ull;
     }
-    o += wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < CU; u++) {
+      if (j0 + u * 256 >= S) break;
+      const uint64_t m = __ballot(keep[u]);
+      if (lane == 0) wsum[wv] = (uint32_t)__popcll(m);
+      __syncthreads();
+      uint32_t pos = o + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+      for (uint32_t w = 0; w < wv; w++) pos += wsum[w];
+      if (keep[u] && pos < out.cap) {
+        out.src_host[pos] = h0 + kk[u];
+        out.dst_ipv4[pos] = rec[u].z;
+        out.payload_len[pos] = rec[u].w;
+        out.send_time_ns[pos] = rec[u].x < n_status ? ft[u] : 0;
+        out.packet[pos] = rec[u].x;
+      }
+      o += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+      __syncthreads();
+    }
   }
 }
 
