@@ -602,11 +602,15 @@ __global__ void __launch_bounds__(NT)
       constexpr int OU = 4;
       const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc((void*)used, 0, (int)(n_used * 4u),
                                                                           0x00020000);
+      // the column indices are computed here, per row, from an opaque copy of tid: hoisted
+      // out of the row loop, the compiler kept (and spilled) them across the whole search
+      uint32_t tt = (uint32_t)tid;
+      asm volatile("" : "+v"(tt));
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
       u32x4 uv[OU];
 #pragma unroll
       for (int k = 0; k < OU; k++) {
-        const uint32_t j = (tid + (uint32_t)k * NT) * 4;
+        const uint32_t j = (tt + (uint32_t)k * NT) * 4;
         uv[k] = __builtin_amdgcn_raw_buffer_load_b128(ru, j < n_used ? j * 4u : OOB, 0, 0);
       }
       const uint32_t de = self_edge[src];
@@ -621,7 +625,7 @@ __global__ void __launch_bounds__(NT)
       };
 #pragma unroll
       for (int k = 0; k < OU; k++) {
-        const uint32_t j = (tid + (uint32_t)k * NT) * 4;
+        const uint32_t j = (tt + (uint32_t)k * NT) * 4;
         if (j < n_used) {
           uint64_t l0, l1, l2, l3;
           float f0, f1, f2, f3;
@@ -634,7 +638,7 @@ __global__ void __launch_bounds__(NT)
           __builtin_nontemporal_store((f32x4){f0, f1, f2, f3}, (f32x4*)&out_loss[orow + j]);
         }
       }
-      for (uint32_t j = (tid + OU * NT) * 4; j < n_used; j += NT * 4) {  // past OU x NT x 4 columns
+      for (uint32_t j = (tt + OU * NT) * 4; j < n_used; j += NT * 4) {  // past OU x NT x 4 columns
         uint64_t l0, l1, l2, l3;
         float f0, f1, f2, f3;
         entry(j, l0, f0);
