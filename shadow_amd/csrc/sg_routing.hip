@@ -81,6 +81,95 @@ __global__ void k_net_count(const uint32_t* __restrict__ src, const uint32_t* __
   }
 }
 
+// Graphs of up to NET_LDS_NODES nodes (C2: a 1,200-node complete graph, 720k edges)
+// count and place their arcs through per-block LDS counters: the global degree and
+// cursor atomics of k_net_count / k_net_scatter all land on a few thousand words there
+// (C2: 0.63 + 1.39 ms).  A block takes a contiguous run of edges; it adds its per-node
+// counts to the global ones once, and reserves each node's range for its arcs with one
+// returning atomic per node, then places them with LDS cursors.
+constexpr uint32_t NET_LDS_NODES = 4096;
+constexpr uint32_t NET_LDS_BLOCKS = 256;
+__global__ void __launch_bounds__(256) k_net_count_lds(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                                                       uint32_t m, uint32_t n, int directed,
+                                                       uint32_t* __restrict__ indeg, uint32_t* __restrict__ outdeg,
+                                                       uint32_t* __restrict__ self_cnt,
+                                                       uint32_t* __restrict__ self_edge) {
+  __shared__ uint32_t s_in[NET_LDS_NODES], s_out[NET_LDS_NODES];
+  for (uint32_t v = threadIdx.x; v < n; v += 256) s_in[v] = s_out[v] = 0;
+  __syncthreads();
+  const uint32_t per = (m + gridDim.x - 1) / gridDim.x, e0 = blockIdx.x * per, e1 = min(e0 + per, m);
+  for (uint32_t e = e0 + threadIdx.x; e < e1; e += 256) {
+    const uint32_t s = src[e], d = dst[e];
+    if (s == d) {
+      atomicAdd(&self_cnt[s], 1u);
+      self_edge[s] = e;  // meaningful only when the count ends at 1
+      continue;
+    }
+    atomicAdd(&s_in[d], 1u);
+    atomicAdd(&s_out[s], 1u);
+    if (!directed) {
+      atomicAdd(&s_in[s], 1u);
+      atomicAdd(&s_out[d], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t v = threadIdx.x; v < n; v += 256) {
+    if (s_in[v]) atomicAdd(&indeg[v], s_in[v]);
+    if (s_out[v]) atomicAdd(&outdeg[v], s_out[v]);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_net_scatter_lds(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                                                         const uint64_t* __restrict__ lat, const float* __restrict__ loss,
+                                                         uint32_t m, uint32_t n, int directed,
+                                                         uint32_t* __restrict__ cursor, uint32_t* __restrict__ in_src,
+                                                         uint32_t* __restrict__ in_dst, uint64_t* __restrict__ in_lat,
+                                                         uint32_t* __restrict__ in_lat32, float* __restrict__ in_om,
+                                                         uint4* __restrict__ in_rec, uint32_t* __restrict__ ocursor,
+                                                         uint32_t* __restrict__ out_arc) {
+  __shared__ uint32_t s_in[NET_LDS_NODES], s_out[NET_LDS_NODES];  // counts, then the block's cursors
+  for (uint32_t v = threadIdx.x; v < n; v += 256) s_in[v] = s_out[v] = 0;
+  __syncthreads();
+  const uint32_t per = (m + gridDim.x - 1) / gridDim.x, e0 = blockIdx.x * per, e1 = min(e0 + per, m);
+  for (uint32_t e = e0 + threadIdx.x; e < e1; e += 256) {
+    const uint32_t s = src[e], d = dst[e];
+    if (s == d) continue;
+    atomicAdd(&s_in[d], 1u);
+    atomicAdd(&s_out[s], 1u);
+    if (!directed) {
+      atomicAdd(&s_in[s], 1u);
+      atomicAdd(&s_out[d], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t v = threadIdx.x; v < n; v += 256) {  // this block's ranges
+    if (s_in[v]) s_in[v] = atomicAdd(&cursor[v], s_in[v]);
+    if (s_out[v]) s_out[v] = atomicAdd(&ocursor[v], s_out[v]);
+  }
+  __syncthreads();
+  for (uint32_t e = e0 + threadIdx.x; e < e1; e += 256) {
+    const uint32_t s = src[e], d = dst[e];
+    if (s == d) continue;  // a self-loop never improves D[s][v] (latency >= 1)
+    const float om = __fsub_rn(1.0f, loss[e]);
+    const uint64_t l = lat[e];
+    const uint32_t l32 = l < LAT32_SAT ? (uint32_t)l : LAT32_SAT;
+    for (int dir = 0; dir < (directed ? 1 : 2); dir++) {
+      const uint32_t a = dir ? d : s, b = dir ? s : d;  // the arc a -> b
+      const uint32_t p = atomicAdd(&s_in[b], 1u);
+      in_src[p] = a;
+      in_dst[p] = b;
+      in_lat[p] = l;
+      in_lat32[p] = l32;
+      in_om[p] = om;
+      in_rec[p] = make_uint4(a, b, l32, __float_as_uint(om));
+      const uint32_t q = atomicAdd(&s_out[a], 1u);
+      out_arc[3 * (size_t)q] = b;
+      out_arc[3 * (size_t)q + 1] = l32;
+      out_arc[3 * (size_t)q + 2] = __float_as_uint(om);
+    }
+  }
+}
+
 // Exclusive scans of indeg and outdeg (n + 1 entries each, the last one the
 // total) in one workgroup, each result written twice: the offsets and the
 // scatter's cursors.  For graphs up to NET_SCAN_SMALL nodes.  Both arrays in one
@@ -1113,9 +1202,15 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   // self_cnt and self_edge (adjacent): self_edge stays 0 where no self-loop sets it, so a
   // build that reads it before the self-loop check's error is raised stays in bounds
   SG_HIP(hipMemsetAsync(net->self_cnt, 0, o_insrc - o_scnt, st));
+  const bool lds_up = n <= NET_LDS_NODES && env_int("SG_NET_LDS", 1) != 0;  // (SG_NET_LDS=0: A/B)
+  const uint32_t lds_blocks = std::max(1u, std::min(NET_LDS_BLOCKS, (m + 255) / 256));
   if (m) {
-    hipLaunchKernelGGL(k_net_count, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst, m,
-                       (int)net->directed, indeg, outdeg, net->self_cnt, net->self_edge);
+    if (lds_up)
+      hipLaunchKernelGGL(k_net_count_lds, dim3(lds_blocks), dim3(256), 0, st, net->e_src, net->e_dst, m, n,
+                         (int)net->directed, indeg, outdeg, net->self_cnt, net->self_edge);
+    else
+      hipLaunchKernelGGL(k_net_count, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst, m,
+                         (int)net->directed, indeg, outdeg, net->self_cnt, net->self_edge);
     SG_CHECK_LAUNCH();
   }
   uint32_t* cursor = ctx->r_map.get<uint32_t>(2 * ((size_t)n + 1));
@@ -1131,9 +1226,14 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
     SG_HIP(hipMemcpyAsync(ocursor, net->out_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
   }
   if (n_arcs) {
-    hipLaunchKernelGGL(k_net_scatter, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst,
-                       net->e_lat, net->e_loss, m, (int)net->directed, cursor, net->in_src, net->in_dst, net->in_lat,
-                       net->in_lat32, net->in_om, net->in_rec, ocursor, net->out_arc);
+    if (lds_up)
+      hipLaunchKernelGGL(k_net_scatter_lds, dim3(lds_blocks), dim3(256), 0, st, net->e_src, net->e_dst, net->e_lat,
+                         net->e_loss, m, n, (int)net->directed, cursor, net->in_src, net->in_dst, net->in_lat,
+                         net->in_lat32, net->in_om, net->in_rec, ocursor, net->out_arc);
+    else
+      hipLaunchKernelGGL(k_net_scatter, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst,
+                         net->e_lat, net->e_loss, m, (int)net->directed, cursor, net->in_src, net->in_dst, net->in_lat,
+                         net->in_lat32, net->in_om, net->in_rec, ocursor, net->out_arc);
     SG_CHECK_LAUNCH();
   }
   {  // the losses and latencies, while the device runs the upload
