@@ -1202,7 +1202,7 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   // self_cnt and self_edge (adjacent): self_edge stays 0 where no self-loop sets it, so a
   // build that reads it before the self-loop check's error is raised stays in bounds
   SG_HIP(hipMemsetAsync(net->self_cnt, 0, o_insrc - o_scnt, st));
-  const bool lds_up = n <= NET_LDS_NODES && env_int("SG_NET_LDS", 0) != 0;  // (SG_NET_LDS=1: the LDS path)
+  const bool lds_up = n <= NET_LDS_NODES && env_int("SG_NET_LDS", 1) != 0;  // (SG_NET_LDS=0: A/B)
   const uint32_t lds_blocks = std::max(1u, std::min(NET_LDS_BLOCKS, (m + 255) / 256));
   if (m) {
     if (lds_up)
