@@ -920,11 +920,17 @@ __global__ void __launch_bounds__(SBS_THREADS)
     reduce_stats_block<SBS_THREADS>(stats);
     return;
   }
+  // second level: the coarse level's next-parity counters are zeroed on the way out,
+  // after this block's loads and run claims (stores ahead of them made each wait)
+  auto zero_next = [&]() {
+    if constexpr (E::COARSE)
+      for (uint32_t i = blockIdx.x * SBS_THREADS + threadIdx.x; i < SB_CTL_STRIDE; i += gridDim.x * SBS_THREADS)
+        src.ctl_next[i] = 0;
+  };
   if constexpr (E::COARSE) {
-    for (uint32_t i = blockIdx.x * SBS_THREADS + threadIdx.x; i < SB_CTL_STRIDE; i += gridDim.x * SBS_THREADS)
-      src.ctl_next[i] = 0;
     if (src.ctl[SB_FLAG]) {  // the coarse level overflowed: so does this one (the host reruns the scan path)
       if (blockIdx.x == 0 && threadIdx.x == 0) ctl[SB_FLAG] = 1u;
+      zero_next();
       return;
     }
   }
@@ -932,7 +938,10 @@ __global__ void __launch_bounds__(SBS_THREADS)
   if constexpr (E::COARSE) {
     uint32_t off, sub;  // a tile lies in one sub-region (subcap is a multiple of SB_TILE): skip an empty one
     const uint32_t fill = src.fill_of(blockIdx.x * SB_TILE, off, sub);
-    if (off >= fill) return;
+    if (off >= fill) {
+      zero_next();
+      return;
+    }
     e_lim = blockIdx.x * SB_TILE + (fill - off);
   }
   // Sub-region of the runs this tile claims.  One level: the tile's XCD (tiles
@@ -1020,6 +1029,7 @@ __global__ void __launch_bounds__(SBS_THREADS)
     ri[g] = si[p];
     if (E::KK) rk[g] = sk[p];
   }
+  zero_next();
 }
 
 // Placement of a super-bucket's entries by slot, then per-slot order by (t, kk).
@@ -1261,11 +1271,19 @@ __global__ void __launch_bounds__(SBT_THREADS)
                      uint16_t* __restrict__ slot_spill, sg_round_ret* __restrict__ ret,
                      const uint32_t* __restrict__ pre) {
   __shared__ uint32_t part[SBT_THREADS / 64];
-  for (uint32_t i = blockIdx.x * SBT_THREADS + threadIdx.x; i <= SB_FLAG; i += gridDim.x * SBT_THREADS)
-    ctl_next[i] = 0;
   const uint32_t over = ctl[SB_FLAG];
-  if (blockIdx.x == 0 && threadIdx.x == 0) ret->overflow = over;
-  if (over) return;  // uniform across the grid
+  // the next parity's counters zeroed and the overflow flag published after this
+  // kernel's loads: stores ahead of them made every later load wait for the stores too
+  // (the flag goes to mapped host memory)
+  auto epilogue = [&]() {
+    for (uint32_t i = blockIdx.x * SBT_THREADS + threadIdx.x; i <= SB_FLAG; i += gridDim.x * SBT_THREADS)
+      ctl_next[i] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) ret->overflow = over;
+  };
+  if (over) {  // uniform across the grid
+    epilogue();
+    return;
+  }
   const uint32_t sb = blockIdx.x, subcap = region / SB_SUB;
   uint32_t s0 = 0;
   if (pre) {
@@ -1375,6 +1393,7 @@ __global__ void __launch_bounds__(SBT_THREADS)
     slot_orders<true, KK, true, true>(st, sk, si, ss, s0, ns, d0, nd, cnt, kt, kk, ki, order, big_list, big_count);
   else
     slot_orders<true, KK, true>(st, sk, si, ss, s0, ns, d0, nd, cnt, kt, kk, ki, order, big_list, big_count);
+  epilogue();
 }
 
 // Bucket sort of n entries into n_slots destination slots (see above).
