@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 5
+#define SG_ABI_VERSION 6
 
 typedef enum sg_status {
   SG_OK = 0,
@@ -493,6 +493,10 @@ typedef struct sg_inbound_relay_state { /* host arrays, n_hosts each */
   uint64_t* task_time;
   uint32_t *cached_packet, *cached_len;
   uint64_t *tb_capacity, *tb_balance, *tb_increment, *tb_last_refill;
+  /* ABI 6 (may be NULL): the pending forward task's Local event id
+     (Host::get_new_event_id, host.rs:649-653, taken from event_ctr when the
+     task was scheduled) and the time it was scheduled at (its creation). */
+  uint64_t *task_event_id, *task_created_ns;
 } sg_inbound_relay_state;
 int32_t sg_inbound_get_state(sg_inbound* ib, sg_codel_state* queue, sg_inbound_relay_state* relay);
 
@@ -513,9 +517,23 @@ int32_t sg_inbound_get_state(sg_inbound* ib, sg_codel_state* queue, sg_inbound_r
  *
  * A call processes each host's sends (times < window_end, nondecreasing per
  * host) and the relay's forward tasks before window_end; later tasks stay
- * pending.  At equal times a send precedes a forward task (the task that a
- * notify schedules runs after every send of that instant).  Assumes Shadow's
- * CPU-delay model is off (host.rs:758-775; its default).                     */
+ * pending.  Assumes Shadow's CPU-delay model is off (host.rs:758-775; its
+ * default).
+ *
+ * Same-time order.  A send happens while the host runs some event E; the
+ * relay's forward task is a Local event (relay/mod.rs:145-157).  At one
+ * EmulatedTime the host runs Packet events first, then Local events by event
+ * id (event.rs:84-155, :163-183), and ids grow in creation order
+ * (host.rs:649-653).  With sends->event_id given, a task at time t runs before
+ * a send at t iff E is a Local event created after the task:
+ * (event_created_ns, event_id) > (task created, task id), the task's id taken
+ * from event_ctr when it is scheduled.  event_id = UINT64_MAX marks E as a
+ * Packet event (it precedes every Local one).  Creation time decides first
+ * because ids are monotone in creation order, so the comparison is exact
+ * whenever the two were created at different times, whatever numbering the
+ * caller's own ids use within a window; at one creation time it falls back
+ * to the ids.  Without event_id (NULL) every send at t
+ * precedes a task at t (all sends treated as Packet-event sends).          */
 typedef struct sg_outbound sg_outbound;
 /* host_ipv4, bw_up_bits (host, n_hosts): each host's address and bandwidth up
  * (HostInfo, bits/s).  ring_cap bounds, per host and call, the packets queued
@@ -534,6 +552,12 @@ typedef struct sg_outbound_sends { /* device arrays, grouped by ascending host, 
   const uint32_t* len;          /* PacketRc::len() (packet.rs:388-390): the bucket's cost */
   const uint32_t* payload_len;  /* PacketRc::payload_len(): carried into the sent batch */
   const uint32_t* dst_ipv4;
+  /* ABI 6, optional (NULL, or both): the sending event's id and the time it was
+     created (scheduled).  event_id UINT64_MAX: a Packet event.  Sends at one time
+     come in the host's execution order: Packet-event sends first, then by
+     (event_created_ns, event_id).  Requires event_ctr in sg_outbound_run. */
+  const uint64_t* event_id;
+  const uint64_t* event_created_ns;
 } sg_outbound_sends;
 
 enum { SG_OUT_QUEUED = 0, SG_OUT_SENT = 1 /* to the router: Worker::send_packet */,

@@ -65,11 +65,11 @@ def lib():
         L.sgo_codel_run.restype = C.c_int
         L.sgo_token_bucket_remove.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]
         L.sgo_token_bucket_remove.restype = C.c_int
-        L.sgo_inbound_run.argtypes = [C.c_uint32, C.c_uint32] + [C.c_void_p] * 19 + [C.c_uint32] + \
+        L.sgo_inbound_run.argtypes = [C.c_uint32, C.c_uint32] + [C.c_void_p] * 21 + [C.c_uint32] + \
             [C.c_void_p] * 4 + [C.c_uint64] * 3 + [C.c_void_p] * 3 + [C.c_uint32]
         L.sgo_inbound_run.restype = C.c_int
-        L.sgo_outbound_run.argtypes = [C.c_uint32, C.c_uint32] + [C.c_void_p] * 13 + [C.c_uint32] + \
-            [C.c_void_p] * 6 + [C.c_uint64] * 3 + [C.c_void_p] * 3 + [C.c_uint32] + [C.c_void_p] * 5 + \
+        L.sgo_outbound_run.argtypes = [C.c_uint32, C.c_uint32] + [C.c_void_p] * 15 + [C.c_uint32] + \
+            [C.c_void_p] * 8 + [C.c_uint64] * 3 + [C.c_void_p] * 3 + [C.c_uint32] + [C.c_void_p] * 5 + \
             [C.c_uint32, C.c_void_p]
         L.sgo_outbound_run.restype = C.c_int
         L.sgo_deliver_round_mt.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32] + [C.c_void_p] * 4 + [
@@ -343,7 +343,8 @@ def inbound_state(bw_down_bits: np.ndarray, cap: int, t0: int = 946684800 * 10**
     n = len(bw_down_bits)
     st = codel_state(n, cap)
     refill = np.maximum(1, (np.asarray(bw_down_bits, np.uint64) // np.uint64(8)) // np.uint64(1000)).astype(np.uint64)
-    st.update(rflags=np.zeros(n, np.uint8), task_time=np.zeros(n, np.uint64), cached_pkt=np.zeros(n, np.uint32),
+    st.update(rflags=np.zeros(n, np.uint8), task_time=np.zeros(n, np.uint64), task_id=np.zeros(n, np.uint64),
+              task_born=np.zeros(n, np.uint64), cached_pkt=np.zeros(n, np.uint32),
               cached_len=np.zeros(n, np.uint32), tb_cap=refill + np.uint64(CODEL_MTU), tb_bal=refill + np.uint64(CODEL_MTU),
               tb_inc=refill, tb_last=np.full(n, t0, np.uint64))
     return st
@@ -357,7 +358,7 @@ def inbound_run(st: dict, host, time, pkt, length, window_end: int, bootstrap_en
     H = len(st["flags"])
     rc = lib().sgo_inbound_run(H, st["cap"], *[v(st[k]) for k in (
         "flags", "interval_end", "drop_next", "cur", "prev", "bytes", "head", "tail", "ring_pkt", "ring_ts",
-        "ring_len", "rflags", "task_time", "cached_pkt", "cached_len", "tb_cap", "tb_bal", "tb_inc", "tb_last")],
+        "ring_len", "rflags", "task_time", "task_id", "task_born", "cached_pkt", "cached_len", "tb_cap", "tb_bal", "tb_inc", "tb_last")],
         len(host), v(host), v(time), v(pkt), v(length), window_end, bootstrap_end, sim_end, v(event_ctr),
         v(fwd_time), v(pkt_status), len(pkt_status))
     if rc:
@@ -376,14 +377,21 @@ def outbound_state(host_ipv4, bw_up_bits: np.ndarray, cap: int, t0: int = 946684
     return dict(cap=c, host_ip=np.ascontiguousarray(host_ipv4, np.uint32), head=np.zeros(n, np.uint32),
                 tail=np.zeros(n, np.uint32), ring_pkt=np.zeros(n * c, np.uint32), ring_len=np.zeros(n * c, np.uint32),
                 ring_dst=np.zeros(n * c, np.uint32), ring_pay=np.zeros(n * c, np.uint32),
-                rflags=np.zeros(n, np.uint8), task_time=np.zeros(n, np.uint64), tb_cap=refill + np.uint64(CODEL_MTU),
+                rflags=np.zeros(n, np.uint8), task_time=np.zeros(n, np.uint64), task_id=np.zeros(n, np.uint64),
+                task_born=np.zeros(n, np.uint64), tb_cap=refill + np.uint64(CODEL_MTU),
                 tb_bal=refill + np.uint64(CODEL_MTU), tb_inc=refill, tb_last=np.full(n, t0, np.uint64))
 
 
 def outbound_run(st: dict, host, time, pkt, length, payload, dst, window_end: int, bootstrap_end: int,
-                 sim_end: int, event_ctr: np.ndarray, fwd_time: np.ndarray, pkt_status: np.ndarray) -> dict:
-    """One window of sends (sgo_outbound_run).  Returns the packets handed to send_packet, in order."""
+                 sim_end: int, event_ctr: np.ndarray, fwd_time: np.ndarray, pkt_status: np.ndarray,
+                 event_id=None, event_created=None) -> dict:
+    """One window of sends (sgo_outbound_run).  Returns the packets handed to send_packet, in order.
+    event_id / event_created (optional, together): the sending event's id (UINT64_MAX: a Packet
+    event) and creation time, which order a send against a forward task at the same time."""
     host, time = _arr(host, np.uint32), _arr(time, np.uint64)
+    assert (event_id is None) == (event_created is None)
+    eid = None if event_id is None else _arr(event_id, np.uint64)
+    eborn = None if event_created is None else _arr(event_created, np.uint64)
     pkt, length, payload, dst = (_arr(x, np.uint32) for x in (pkt, length, payload, dst))
     v = lambda a: a.ctypes.data_as(C.c_void_p)
     H = len(st["head"])
@@ -393,9 +401,9 @@ def outbound_run(st: dict, host, time, pkt, length, payload, dst, window_end: in
                packet=np.zeros(cap_out, np.uint32))
     n_out = C.c_uint32()
     rc = lib().sgo_outbound_run(H, st["cap"], *[v(st[k]) for k in (
-        "host_ip", "head", "tail", "ring_pkt", "ring_len", "ring_dst", "ring_pay", "rflags", "task_time", "tb_cap",
-        "tb_bal", "tb_inc", "tb_last")], len(host), v(host), v(time), v(pkt), v(length), v(payload), v(dst),
-        window_end, bootstrap_end, sim_end, v(event_ctr), v(fwd_time), v(pkt_status), len(pkt_status),
+        "host_ip", "head", "tail", "ring_pkt", "ring_len", "ring_dst", "ring_pay", "rflags", "task_time", "task_id",
+        "task_born", "tb_cap", "tb_bal", "tb_inc", "tb_last")], len(host), v(host), v(time), v(pkt), v(length),
+        v(payload), v(dst), None if eid is None else v(eid), None if eborn is None else v(eborn), window_end, bootstrap_end, sim_end, v(event_ctr), v(fwd_time), v(pkt_status), len(pkt_status),
         *[v(out[k]) for k in ("src_host", "dst_ipv4", "payload_len", "send_time", "packet")], cap_out, C.byref(n_out))
     if rc:
         raise ValueError(f"sgo_outbound_run: error {rc}")

@@ -873,7 +873,7 @@ static int tb_remove(tb_t* b, uint64_t dec, uint64_t now, uint64_t* wait) {
 int sgo_inbound_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* iend, uint64_t* dnext,
                     uint64_t* cur, uint64_t* prev, uint64_t* bytes, uint32_t* head, uint32_t* tail,
                     uint32_t* ring_pkt, uint64_t* ring_ts, uint32_t* ring_len, uint8_t* rflags, uint64_t* task_time,
-                    uint32_t* cached_pkt, uint32_t* cached_len, uint64_t* tb_cap, uint64_t* tb_bal,
+                    uint64_t* task_id, uint64_t* task_born, uint32_t* cached_pkt, uint32_t* cached_len, uint64_t* tb_cap, uint64_t* tb_bal,
                     uint64_t* tb_inc, uint64_t* tb_last, uint32_t n_arr, const uint32_t* host,
                     const uint64_t* time, const uint32_t* pkt, const uint32_t* len, uint64_t window_end,
                     uint64_t bootstrap_end, uint64_t sim_end, uint64_t* event_ctr, uint64_t* fwd_time,
@@ -886,7 +886,7 @@ int sgo_inbound_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* ie
               pkt_status, n_status, 0};
     tb_t tb = {tb_cap[h], tb_bal[h], tb_inc[h], tb_last[h], TB_INTERVAL};
     uint8_t rf = rflags[h];
-    uint64_t tt = task_time[h];
+    uint64_t tt = task_time[h], tid = task_id[h], tborn = task_born[h];
     uint32_t cp = cached_pkt[h], cl = cached_len[h];
     uint32_t e1 = e;
     while (e1 < n_arr && host[e1] == h) e1++;
@@ -903,8 +903,9 @@ int sgo_inbound_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* ie
         q.rlen[slot] = len[e];
         q.tail++;
         q.bytes += len[e];
-        if (!(rf & RL_PENDING)) { /* notify: Idle -> forward_later(ZERO) */
-          event_ctr[h]++;
+        if (!(rf & RL_PENDING)) { /* notify: Idle -> forward_later(ZERO), a Local event (host.rs:690-697) */
+          tid = event_ctr[h]++;
+          tborn = now;
           rf |= RL_PENDING;
           if (now >= sim_end) rf |= RL_NEVER;
           tt = now;
@@ -932,7 +933,8 @@ int sgo_inbound_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* ie
             rf |= RL_CACHED; /* RelayCached; forward_later(wait) */
             cp = p;
             cl = l;
-            event_ctr[h]++;
+            tid = event_ctr[h]++;
+            tborn = now;
             rf |= RL_PENDING;
             const uint64_t at = now > UINT64_MAX - wait ? UINT64_MAX : now + wait;
             if (at >= sim_end) rf |= RL_NEVER;
@@ -961,6 +963,8 @@ int sgo_inbound_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* ie
     tail[h] = q.tail;
     rflags[h] = rf;
     task_time[h] = tt;
+    task_id[h] = tid;
+    task_born[h] = tborn;
     cached_pkt[h] = cp;
     cached_len[h] = cl;
     tb_bal[h] = tb.bal;
@@ -978,31 +982,40 @@ int sgo_inbound_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* ie
  * FIFO is held as a ring of `cap` slots {packet, len, dst, payload_len}; the
  * packet the relay caches (next_packet) is the slot at head - 1, and a call's
  * pushes may not reach the oldest slot it still needs (the library's bound,
- * -2 here).  Sends at a time precede a forward task at the same time.
+ * -2 here).  Same-time order (event.rs:84-155): a send made by a Packet
+ * event (ev_id UINT64_MAX), or with no keys (ev_id NULL), precedes a forward
+ * task at its time; a send made by a Local event follows a task at its time
+ * iff the task was created first: (task created, task id) < (ev_born, ev_id).
+ * Task ids come from event_ctr (host.rs:649-653), creation times are the
+ * times forward_later ran (relay/mod.rs:145-157, host.rs:690-697).  A
+ * Local send's id moves event_ctr past it (the event exists, so the host's
+ * counter is beyond its id): tasks the send schedules are numbered after it.
  * Sent packets are appended to out_* (send_packet order: hosts ascending).
  * Returns 0, or -2 ring full, -3 packet id >= n_status, -4 not grouped,
  * -5 a send at or after window_end, -6 a host's send times decrease,
  * -7 more than out_cap sent. */
 int sgo_outbound_run(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip, uint32_t* head, uint32_t* tail,
                      uint32_t* ring_pkt, uint32_t* ring_len, uint32_t* ring_dst, uint32_t* ring_pay,
-                     uint8_t* rflags, uint64_t* task_time, uint64_t* tb_cap, uint64_t* tb_bal, uint64_t* tb_inc,
-                     uint64_t* tb_last, uint32_t n_sends, const uint32_t* host, const uint64_t* time,
-                     const uint32_t* pkt, const uint32_t* len, const uint32_t* pay, const uint32_t* dst,
-                     uint64_t window_end, uint64_t bootstrap_end, uint64_t sim_end, uint64_t* event_ctr,
+                     uint8_t* rflags, uint64_t* task_time, uint64_t* task_id, uint64_t* task_born, uint64_t* tb_cap,
+                     uint64_t* tb_bal, uint64_t* tb_inc, uint64_t* tb_last, uint32_t n_sends, const uint32_t* host,
+                     const uint64_t* time, const uint32_t* pkt, const uint32_t* len, const uint32_t* pay,
+                     const uint32_t* dst, const uint64_t* ev_id, const uint64_t* ev_born, uint64_t window_end, uint64_t bootstrap_end, uint64_t sim_end, uint64_t* event_ctr,
                      uint64_t* fwd_time, uint8_t* pkt_status, uint32_t n_status, uint32_t* out_host,
                      uint32_t* out_dst, uint32_t* out_pay, uint64_t* out_time, uint32_t* out_pkt, uint32_t out_cap,
                      uint32_t* n_out) {
   if (!cap) return -1;
+  if ((ev_id == NULL) != (ev_born == NULL)) return -1;
   uint32_t e = 0, no = 0;
   *n_out = 0;
   for (uint32_t h = 0; h < n_hosts; h++) {
     const size_t base = (size_t)h * cap;
     tb_t tb = {tb_cap[h], tb_bal[h], tb_inc[h], tb_last[h], TB_INTERVAL};
     uint8_t rf = rflags[h];
-    uint64_t tt = task_time[h];
+    uint64_t tt = task_time[h], tid = task_id[h], tborn = task_born[h];
     uint32_t hd = head[h], tl = tail[h];
     const uint32_t oldest = hd - ((rf & RL_CACHED) ? 1u : 0u);
     uint32_t e1 = e;
+    const uint32_t e_first = e;
     while (e1 < n_sends && host[e1] == h) e1++;
     uint64_t last = 0;
     for (;;) {
@@ -1010,9 +1023,23 @@ int sgo_outbound_run(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip, ui
       const int has_task = (rf & RL_PENDING) && !(rf & RL_NEVER) && tt < window_end;
       if (has_send && time[e] >= window_end) return -5;
       if (has_send && time[e] < last) return -6;
-      if (has_send && (!has_task || time[e] <= tt)) { /* add_data_source + Relay::notify */
+      if (has_send && ev_id && e > e_first && time[e] == time[e - 1]) { /* execution order within a time */
+        const int pk = ev_id[e] == UINT64_MAX, ppk = ev_id[e - 1] == UINT64_MAX;
+        if ((pk && !ppk) || (!pk && !ppk && (ev_born[e] < ev_born[e - 1] ||
+                                             (ev_born[e] == ev_born[e - 1] && ev_id[e] < ev_id[e - 1]))))
+          return -6;
+      }
+      int send_first = has_send && (!has_task || time[e] < tt);
+      if (has_send && has_task && time[e] == tt) {
+        /* one EmulatedTime: Packet events, then Local events by id = creation order */
+        send_first = !ev_id || ev_id[e] == UINT64_MAX || ev_born[e] < tborn ||
+                     (ev_born[e] == tborn && ev_id[e] < tid);
+      }
+      if (send_first) { /* add_data_source + Relay::notify */
         const uint64_t now = time[e];
         last = now;
+        /* the sending event exists: the counter is past its id (a no-op for ids from this counter) */
+        if (ev_id && ev_id[e] != UINT64_MAX && event_ctr[h] <= ev_id[e]) event_ctr[h] = ev_id[e] + 1;
         if (tl - oldest >= cap) return -2;
         const size_t slot = base + tl % cap;
         ring_pkt[slot] = pkt[e];
@@ -1021,7 +1048,8 @@ int sgo_outbound_run(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip, ui
         ring_pay[slot] = pay[e];
         tl++;
         if (!(rf & RL_PENDING)) { /* Idle -> forward_later(ZERO) */
-          event_ctr[h]++;
+          tid = event_ctr[h]++;
+          tborn = now;
           rf |= RL_PENDING;
           if (now >= sim_end) rf |= RL_NEVER;
           tt = now;
@@ -1045,7 +1073,8 @@ int sgo_outbound_run(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip, ui
           uint64_t wait;
           if (!local && now >= bootstrap_end && !tb_remove(&tb, ring_len[slot], now, &wait)) {
             rf |= RL_CACHED | RL_PENDING; /* RelayCached; forward_later(wait) */
-            event_ctr[h]++;
+            tid = event_ctr[h]++;
+            tborn = now;
             const uint64_t at = now > UINT64_MAX - wait ? UINT64_MAX : now + wait;
             if (at >= sim_end) rf |= RL_NEVER;
             tt = at;
@@ -1073,6 +1102,8 @@ int sgo_outbound_run(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip, ui
     tail[h] = tl;
     rflags[h] = rf;
     task_time[h] = tt;
+    task_id[h] = tid;
+    task_born[h] = tborn;
     tb_bal[h] = tb.bal;
     tb_last[h] = tb.last;
   }

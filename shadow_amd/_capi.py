@@ -14,7 +14,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "shadow_gpu.h")
 
 # sg_status (include/shadow_gpu.h)
 SG_OK = 0
-SG_ABI_VERSION = 5  # include/shadow_gpu.h
+SG_ABI_VERSION = 6  # include/shadow_gpu.h
 SG_ERR_NO_EDGE = 1
 SG_ERR_MULTI_EDGE = 2
 SG_ERR_UNREACHABLE = 3
@@ -93,12 +93,13 @@ class sg_inbound_arrivals(C.Structure):
 
 class sg_inbound_relay_state(C.Structure):
     _fields_ = [(k, C.c_void_p) for k in ("flags", "task_time", "cached_packet", "cached_len", "tb_capacity",
-                                          "tb_balance", "tb_increment", "tb_last_refill")]
+                                          "tb_balance", "tb_increment", "tb_last_refill", "task_event_id",
+                                          "task_created_ns")]
 
 
 class sg_outbound_sends(C.Structure):
     _fields_ = [("n", C.c_uint32)] + [(k, C.c_void_p) for k in ("host", "time_ns", "packet", "len", "payload_len",
-                                                                  "dst_ipv4")]
+                                                                  "dst_ipv4", "event_id", "event_created_ns")]
 
 
 class sg_outbound_sent(C.Structure):
@@ -135,11 +136,24 @@ class sg_round_stats(C.Structure):
 
 
 _lib = None
+_lib_version = None
+
+
+def abi_version() -> int:
+    """The loaded library's ABI version (older ones only via SHADOW_GPU_LIB, for A/B tools)."""
+    load()
+    return _lib_version
+
+
+def require_abi(v: int, what: str) -> None:
+    """Raise if the loaded library predates ABI `v`, which `what` needs (its structs differ)."""
+    if abi_version() < v:
+        raise ShadowGpuUnavailable(f"{what} needs ABI {v}; the loaded library is ABI {_lib_version}")
 
 
 def load(path: str | None = None):
     """Load libshadow_gpu.so; raises ShadowGpuUnavailable (never falls back)."""
-    global _lib
+    global _lib, _lib_version
     if _lib is not None:
         return _lib
     path = path or os.environ.get("SHADOW_GPU_LIB", LIB_PATH)
@@ -239,12 +253,14 @@ def load(path: str | None = None):
         f.restype = res
         f.argtypes = args
     v = L.sg_abi_version()
-    # an older library given via SHADOW_GPU_LIB (A/B tools) is accepted for the calls
-    # it shares: v1's sg_table lacks path_key, which such callers leave NULL; v3's
-    # routing view held two arrays (the A/B tools build tables, they do not view them)
+    # An older library given via SHADOW_GPU_LIB (A/B tools: routing builds only) is
+    # accepted, and its version recorded: the calls whose structs changed since check
+    # it with require_abi (v5: routing view cells, packets' rng_skip; v6: outbound
+    # send keys and relay task ids) instead of misreading memory.
     if v != SG_ABI_VERSION and not (path != LIB_PATH and 1 <= v < SG_ABI_VERSION):
         raise ShadowGpuUnavailable(f"ABI version mismatch: library {v}, bindings {SG_ABI_VERSION}")
     _lib = L
+    _lib_version = int(v)
     return L
 
 

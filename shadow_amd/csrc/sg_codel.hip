@@ -481,6 +481,18 @@ struct Relay {
   uint32_t cp, cl;  // cached packet, its length
   uint64_t cap, bal, inc, last;  // token bucket (token_bucket.rs:6-12)
   uint64_t n_max;                 // u64::MAX / inc (inc != 0): the refill count past which tokens saturate
+  uint64_t ctr0;                  // the host's event counter at the call's start (0 without event_ctr)
+  uint64_t tid, tborn;            // the pending task's event id and creation time (Event::new_local)
+
+  // forward_later: the task is a Local event created at `now` (host.rs:690-697); its id is the
+  // host counter's next value (host.rs:649-653), taken even when it lands past sim_end
+  __device__ void schedule(uint64_t now, uint64_t at, uint64_t sim_end, uint64_t& ctr_inc) {
+    rf |= R_PENDING;
+    tid = ctr0 + ctr_inc++;
+    tborn = now;
+    tt = at;
+    if (at >= sim_end) rf |= R_NEVER;
+  }
 
   // inc is fixed for the call: the one u64 division by it happens here, not on every refill
   __device__ void set_inc(uint64_t v) {
@@ -530,6 +542,7 @@ struct InboundArgs {
   uint64_t window_end, bootstrap_end, sim_end;
   uint64_t* event_ctr;  // per host, or null
   uint64_t* fwd_time;   // per packet
+  uint64_t *task_id, *task_born;  // per host: the pending task's event id and creation time
 };
 
 // The relay's forward task at `now` (run_forward_task -> forward_until_blocked).
@@ -550,12 +563,10 @@ __device__ void relay_task(Q& q, Relay& r, uint64_t now, uint64_t bootstrap_end,
     }
     uint64_t wait;
     if (now >= bootstrap_end && !r.remove(l, now, wait)) {  // Worker::is_bootstrapping: no rate limit
-      r.rf |= R_CACHED | R_PENDING;  // RelayCached; forward_later(wait)
+      r.rf |= R_CACHED;  // RelayCached; forward_later(wait)
       r.cp = p;
       r.cl = l;
-      ctr_inc++;
-      r.tt = now > ~0ull - wait ? ~0ull : now + wait;
-      if (r.tt >= sim_end) r.rf |= R_NEVER;
+      r.schedule(now, now > ~0ull - wait ? ~0ull : now + wait, sim_end, ctr_inc);
       return;
     }
     if (p < q.n_status) {  // RelayForwarded: pushed to the internet interface
@@ -607,6 +618,9 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
     r.bal = ia.tb_bal[h];
     r.set_inc(ia.tb_inc[h]);
     r.last = ia.tb_last[h];
+    r.ctr0 = ia.event_ctr ? ia.event_ctr[h] : 0;
+    r.tid = ia.task_id[h];
+    r.tborn = ia.task_born[h];
   }
   auto due = [&](uint64_t before) {  // a pending task earlier than `before` (Packet events go first)
     return (r.rf & R_PENDING) && !(r.rf & R_NEVER) && r.tt < before;
@@ -657,12 +671,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
         q.bytes += len;
         if (q.tail - q.head > q.mask + 1u) q.err |= E_FULL;  // an arrival found the ring full
         if (!q.hv) q.load_head();
-        if (!(r.rf & R_PENDING)) {    // notify_router_has_packets: Idle -> forward_later(ZERO)
-          ctr_inc++;
-          r.rf |= R_PENDING;
-          if (now >= ia.sim_end) r.rf |= R_NEVER;
-          r.tt = now;
-        }
+        if (!(r.rf & R_PENDING)) r.schedule(now, now, ia.sim_end, ctr_inc);  // notify: Idle -> forward_later(ZERO)
       }
       // the window's elements still queued live on in the ring
       const uint32_t w0 = q.head - q.t0 <= q.tail - q.t0 ? q.head - q.t0 : 0;
@@ -693,6 +702,8 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
     ia.cached_len[h] = r.cl;
     ia.tb_bal[h] = r.bal;
     ia.tb_last[h] = r.last;
+    ia.task_id[h] = r.tid;
+    ia.task_born[h] = r.tborn;
     if (ia.event_ctr && ctr_inc) ia.event_ctr[h] += ctr_inc;
     err = q.err;
     dropped = q.dropped;
@@ -737,6 +748,8 @@ struct OutboundArgs {
   uint8_t* status;
   uint32_t n_status;
   uint32_t* start;  // per host: the first ring slot this call forwarded from
+  const uint64_t *ev_id, *ev_born;  // per send (KEYED): the sending event's id and creation time
+  uint64_t *task_id, *task_born;    // per host: the pending task's event id and creation time
   unsigned long long* blk;
   unsigned long long* bdiag = nullptr;  // as CodelArgs::bdiag
 };
@@ -792,11 +805,9 @@ __device__ void out_task(OutQ& q, Relay& r, uint64_t now, const OutboundArgs& a,
     const bool local = rec.z == q.ip;
     uint64_t wait;
     if (!local && now >= a.bootstrap_end && !r.remove(rec.y, now, wait)) {
-      r.rf |= R_CACHED | R_PENDING;  // RelayCached; forward_later(wait)
+      r.rf |= R_CACHED;  // RelayCached; forward_later(wait)
       q.cr = rec;
-      ctr_inc++;
-      r.tt = now > ~0ull - wait ? ~0ull : now + wait;
-      if (r.tt >= a.sim_end) r.rf |= R_NEVER;
+      r.schedule(now, now > ~0ull - wait ? ~0ull : now + wait, a.sim_end, ctr_inc);
       return;
     }
     if (rec.x < a.n_status) {
@@ -809,11 +820,21 @@ __device__ void out_task(OutQ& q, Relay& r, uint64_t now, const OutboundArgs& a,
   }
 }
 
+// KEYED: the sends carry their event's (creation time, id), and a task due at
+// a send's own time runs first iff it was created before the sending event
+// (Local events run in id = creation order, event.rs:163-183; a Packet event's
+// send, id UINT64_MAX, precedes every Local event, event.rs:103-112).  Without
+// keys every send precedes a task at its time.  A Local send's id also moves
+// the host counter past it, so the tasks it schedules are numbered after it.  The keys cost 16 B of LDS per
+// staged send, so the keyed chunk is smaller (40 B per send, 20 KB).
+template <bool KEYED>
 __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
+  constexpr uint32_t CH = KEYED ? 512 : CD_OUT_CHUNK;
   const uint64_t d_t0 = a.bdiag ? wall_clock64() : 0;
   uint64_t d_walk = 0;
-  __shared__ uint64_t s_t[CD_OUT_CHUNK];
-  __shared__ uint4 s_r[CD_OUT_CHUNK];
+  __shared__ uint64_t s_t[CH];
+  __shared__ uint4 s_r[CH];
+  __shared__ uint64_t s_id[KEYED ? CH : 1], s_born[KEYED ? CH : 1];
   const uint32_t h0 = blockIdx.x * CD_HOSTS, t = threadIdx.x;
   const uint32_t p0 = min(a.host_off[min(h0, a.H)], a.E);
   const uint32_t p1 = max(min(a.host_off[min(h0 + CD_HOSTS, a.H)], a.E), p0);
@@ -822,7 +843,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
   uint32_t hb = 0, he = 0;
   OutQ q{};
   Relay r{};
-  uint64_t ctr_inc = 0, last = 0;
+  uint64_t ctr_inc = 0, last = 0, last_born = 0, last_id = 0;
   if (walker) {
     hb = min(a.host_off[h], a.E);
     he = max(min(a.host_off[h + 1], a.E), hb);
@@ -837,25 +858,41 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
     r.bal = a.tb_bal[h];
     r.set_inc(a.tb_inc[h]);
     r.last = a.tb_last[h];
+    r.ctr0 = a.event_ctr ? a.event_ctr[h] : 0;
+    r.tid = a.task_id[h];
+    r.tborn = a.task_born[h];
     q.oldest = q.head - ((r.rf & R_CACHED) ? 1u : 0u);
     if (r.rf & R_CACHED) q.cr = q.ring[(q.head - 1) & q.mask];
     q.load_head();
   }
   auto due = [&](uint64_t before) { return (r.rf & R_PENDING) && !(r.rf & R_NEVER) && r.tt < before; };
-  for (uint32_t c0 = p0; c0 < p1; c0 += CD_OUT_CHUNK) {
-    const uint32_t c1 = min(c0 + CD_OUT_CHUNK, p1);
+  // a task at the send's own time that runs first: created before the sending Local event
+  auto due_tie = [&](uint64_t now, uint64_t born, uint64_t id) {
+    return KEYED && (r.rf & R_PENDING) && !(r.rf & R_NEVER) && r.tt == now && id != ~0ull &&
+           (r.tborn < born || (r.tborn == born && r.tid < id));
+  };
+  for (uint32_t c0 = p0; c0 < p1; c0 += CH) {
+    const uint32_t c1 = min(c0 + CH, p1);
     {
-      uint64_t rt[CD_UNROLL];
+      uint64_t rt[CD_UNROLL], ri[KEYED ? CD_UNROLL : 1], rb[KEYED ? CD_UNROLL : 1];
       uint4 rr[CD_UNROLL];
       stage_chunk(
           c0, c1,
           [&](uint32_t i, int u) {
             rt[u] = a.time[i];
             rr[u] = make_uint4(a.pkt[i], a.len[i], a.dst[i], a.payload[i]);
+            if constexpr (KEYED) {
+              ri[u] = a.ev_id[i];
+              rb[u] = a.ev_born[i];
+            }
           },
           [&](uint32_t k, int u) {
             s_t[k] = rt[u];
             s_r[k] = rr[u];
+            if constexpr (KEYED) {
+              s_id[k] = ri[u];
+              s_born[k] = rb[u];
+            }
           });
     }
     __syncthreads();
@@ -868,8 +905,25 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
         const uint64_t now = s_t[k];
         if (now >= a.window_end) q.err |= E_WINDOW;
         if (now < last) q.err |= E_ORDER;
+        if constexpr (KEYED) {
+          // execution order within a time: Packet-event sends, then Local ones by (created, id)
+          const uint64_t id = s_id[k], born = s_born[k];
+          if (now == last && i > hb) {
+            const bool pk = id == ~0ull, lpk = last_id == ~0ull;
+            if ((pk && !lpk) || (!pk && !lpk && (born < last_born || (born == last_born && id < last_id))))
+              q.err |= E_ORDER;
+          }
+          last_born = born;
+          last_id = id;
+          while (due(now) || due_tie(now, born, id)) out_task(q, r, r.tt, a, ctr_inc);
+          // the sending event exists, so the host's counter is past its id: a task the send
+          // schedules takes a later id (a Lamport-clock step; a no-op when the caller's ids
+          // come from this counter)
+          if (id != ~0ull && id - r.ctr0 >= ctr_inc && id >= r.ctr0) ctr_inc = id + 1 - r.ctr0;
+        } else {
+          while (due(now)) out_task(q, r, r.tt, a, ctr_inc);
+        }
         last = now;
-        while (due(now)) out_task(q, r, r.tt, a, ctr_inc);
         if (q.tail - q.oldest >= a.cap) {  // the push would overwrite a slot this call still needs
           q.err |= E_FULL;
           continue;
@@ -880,12 +934,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
         // walk's next vector-memory wait include it
         if (q.head == q.tail) q.hr = s_r[k];
         q.tail++;
-        if (!(r.rf & R_PENDING)) {  // Relay::notify: Idle -> forward_later(ZERO)
-          ctr_inc++;
-          r.rf |= R_PENDING;
-          if (now >= a.sim_end) r.rf |= R_NEVER;
-          r.tt = now;
-        }
+        if (!(r.rf & R_PENDING)) r.schedule(now, now, a.sim_end, ctr_inc);  // notify: Idle -> forward_later(ZERO)
       }
       for (uint32_t j = 0; j < q.tail - q.t0; j++) q.ring[(q.t0 + j) & q.mask] = s_r[q.wb + j];
       if (a.bdiag) d_walk += clock64() - d_w0;
@@ -902,6 +951,8 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
     a.task_time[h] = r.tt;
     a.tb_bal[h] = r.bal;
     a.tb_last[h] = r.last;
+    a.task_id[h] = r.tid;
+    a.task_born[h] = r.tborn;
     a.start[h] = q.oldest;
     if (a.event_ctr && ctr_inc) a.event_ctr[h] += ctr_inc;
     err = q.err;
@@ -1090,10 +1141,11 @@ struct sg_inbound {
   sg_codel* q = nullptr;
   uint8_t* rflags = nullptr;
   uint64_t* task_time = nullptr;
+  uint64_t *task_id = nullptr, *task_born = nullptr;
   uint32_t *cached_pkt = nullptr, *cached_len = nullptr;
   uint64_t *tb_cap = nullptr, *tb_bal = nullptr, *tb_inc = nullptr, *tb_last = nullptr;
   ~sg_inbound() {
-    void* ps[] = {rflags, task_time, cached_pkt, cached_len, tb_cap, tb_bal, tb_inc, tb_last};
+    void* ps[] = {rflags, task_time, task_id, task_born, cached_pkt, cached_len, tb_cap, tb_bal, tb_inc, tb_last};
     for (void* p : ps)
       if (p) (void)hipFree(p);
     sg_codel_destroy(q);
@@ -1246,6 +1298,8 @@ int32_t sg_inbound_create(sg_ctx* ctx, uint32_t n_hosts, const uint64_t* bw_down
       const size_t n = std::max<uint32_t>(n_hosts, 1);
       SG_HIP(hipMalloc(&ib->rflags, n));
       SG_HIP(hipMalloc(&ib->task_time, n * 8));
+      SG_HIP(hipMalloc(&ib->task_id, n * 8));
+      SG_HIP(hipMalloc(&ib->task_born, n * 8));
       SG_HIP(hipMalloc(&ib->cached_pkt, n * 4));
       SG_HIP(hipMalloc(&ib->cached_len, n * 4));
       SG_HIP(hipMalloc(&ib->tb_cap, n * 8));
@@ -1261,6 +1315,8 @@ int32_t sg_inbound_create(sg_ctx* ctx, uint32_t n_hosts, const uint64_t* bw_down
       hipStream_t st = ctx->stream;
       SG_HIP(hipMemsetAsync(ib->rflags, 0, n, st));
       SG_HIP(hipMemsetAsync(ib->task_time, 0, n * 8, st));
+      SG_HIP(hipMemsetAsync(ib->task_id, 0, n * 8, st));
+      SG_HIP(hipMemsetAsync(ib->task_born, 0, n * 8, st));
       SG_HIP(hipMemsetAsync(ib->cached_pkt, 0, n * 4, st));
       SG_HIP(hipMemsetAsync(ib->cached_len, 0, n * 4, st));
       SG_HIP(hipMemcpyAsync(ib->tb_cap, cap.data(), n * 8, hipMemcpyHostToDevice, st));
@@ -1314,6 +1370,8 @@ int32_t sg_inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* a
                     ctx->d_blk.get<unsigned long long>(2 * (size_t)nb)};
     a.rflags = ib->rflags;
     a.task_time = ib->task_time;
+    a.task_id = ib->task_id;
+    a.task_born = ib->task_born;
     a.cached_pkt = ib->cached_pkt;
     a.cached_len = ib->cached_len;
     a.tb_cap = ib->tb_cap;
@@ -1360,7 +1418,8 @@ int32_t sg_inbound_get_state(sg_inbound* ib, sg_codel_state* queue, sg_inbound_r
         {o->flags, ib->rflags, n}, {o->task_time, ib->task_time, n * 8}, {o->cached_packet, ib->cached_pkt, n * 4},
         {o->cached_len, ib->cached_len, n * 4}, {o->tb_capacity, ib->tb_cap, n * 8},
         {o->tb_balance, ib->tb_bal, n * 8}, {o->tb_increment, ib->tb_inc, n * 8},
-        {o->tb_last_refill, ib->tb_last, n * 8}};
+        {o->tb_last_refill, ib->tb_last, n * 8}, {o->task_event_id, ib->task_id, n * 8},
+        {o->task_created_ns, ib->task_born, n * 8}};
     for (auto& c : cp)
       if (c.h && c.b) SG_HIP(hipMemcpyAsync(c.h, c.d, c.b, hipMemcpyDeviceToHost, st));
     SG_HIP(hipStreamSynchronize(st));
@@ -1376,9 +1435,11 @@ struct sg_outbound {
   uint4* ring = nullptr;
   uint8_t* rflags = nullptr;
   uint64_t *task_time = nullptr, *tb_cap = nullptr, *tb_bal = nullptr, *tb_inc = nullptr, *tb_last = nullptr;
+  uint64_t *task_id = nullptr, *task_born = nullptr;
   unsigned long long* ret = nullptr;  // pinned host-mapped: [sent, error flags]
   ~sg_outbound() {
-    void* ps[] = {host_ip, head, tail, start, off, ring, rflags, task_time, tb_cap, tb_bal, tb_inc, tb_last};
+    void* ps[] = {host_ip, head, tail, start, off, ring, rflags, task_time, task_id, task_born,
+                  tb_cap, tb_bal, tb_inc, tb_last};
     for (void* p : ps)
       if (p) (void)hipFree(p);
     if (ret) (void)hipHostFree(ret);
@@ -1411,6 +1472,8 @@ int32_t sg_outbound_create(sg_ctx* ctx, uint32_t n_hosts, const uint32_t* host_i
     SG_HIP(hipMalloc(&ob->ring, n * cap * 16));
     SG_HIP(hipMalloc(&ob->rflags, n));
     SG_HIP(hipMalloc(&ob->task_time, n * 8));
+    SG_HIP(hipMalloc(&ob->task_id, n * 8));
+    SG_HIP(hipMalloc(&ob->task_born, n * 8));
     SG_HIP(hipMalloc(&ob->tb_cap, n * 8));
     SG_HIP(hipMalloc(&ob->tb_bal, n * 8));
     SG_HIP(hipMalloc(&ob->tb_inc, n * 8));
@@ -1429,6 +1492,8 @@ int32_t sg_outbound_create(sg_ctx* ctx, uint32_t n_hosts, const uint32_t* host_i
     SG_HIP(hipMemsetAsync(ob->tail, 0, n * 4, st));
     SG_HIP(hipMemsetAsync(ob->rflags, 0, n, st));
     SG_HIP(hipMemsetAsync(ob->task_time, 0, n * 8, st));
+    SG_HIP(hipMemsetAsync(ob->task_id, 0, n * 8, st));
+    SG_HIP(hipMemsetAsync(ob->task_born, 0, n * 8, st));
     SG_HIP(hipMemcpyAsync(ob->tb_cap, tcap.data(), n * 8, hipMemcpyHostToDevice, st));
     SG_HIP(hipMemcpyAsync(ob->tb_bal, tcap.data(), n * 8, hipMemcpyHostToDevice, st));
     SG_HIP(hipMemcpyAsync(ob->tb_inc, inc.data(), n * 8, hipMemcpyHostToDevice, st));
@@ -1462,6 +1527,10 @@ int32_t sg_outbound_run(sg_ctx* ctx, sg_outbound* ob, const sg_outbound_sends* s
     if (E && (!s->host || !s->time_ns || !s->packet || !s->len || !s->payload_len || !s->dst_ipv4))
       throw Error(SG_ERR_INVALID_ARG, "null send array");
     if (n_packets && (!pkt_status || !fwd_time)) throw Error(SG_ERR_INVALID_ARG, "null output array");
+    const bool keyed = s->event_id != nullptr;
+    if (keyed != (s->event_created_ns != nullptr))
+      throw Error(SG_ERR_INVALID_ARG, "event_id and event_created_ns are given together or not at all");
+    if (keyed && !event_ctr) throw Error(SG_ERR_INVALID_ARG, "send event ids need the hosts' event counters");
     if (sent && sent->cap && (!sent->src_host || !sent->dst_ipv4 || !sent->payload_len || !sent->send_time_ns ||
                               !sent->packet))
       throw Error(SG_ERR_INVALID_ARG, "null sent-batch array");
@@ -1492,6 +1561,10 @@ int32_t sg_outbound_run(sg_ctx* ctx, sg_outbound* ob, const sg_outbound_sends* s
     a.cap = ob->cap;
     a.rflags = ob->rflags;
     a.task_time = ob->task_time;
+    a.task_id = ob->task_id;
+    a.task_born = ob->task_born;
+    a.ev_id = s->event_id;
+    a.ev_born = s->event_created_ns;
     a.tb_cap = ob->tb_cap;
     a.tb_bal = ob->tb_bal;
     a.tb_inc = ob->tb_inc;
@@ -1509,7 +1582,10 @@ int32_t sg_outbound_run(sg_ctx* ctx, sg_outbound* ob, const sg_outbound_sends* s
       // per send: 24 B in, a 16-B ring record written and read, 9 B out; per host: ~90 B of state
       a.bdiag = lane_diag_alloc(nb);
       TimedLaunch tl(ctx, "outbound", 65.0 * E + 90.0 * H);
-      hipLaunchKernelGGL(k_outbound, dim3(nb), dim3(CD_THREADS), 0, st, a);
+      if (keyed && E)
+        hipLaunchKernelGGL(k_outbound<true>, dim3(nb), dim3(CD_THREADS), 0, st, a);
+      else
+        hipLaunchKernelGGL(k_outbound<false>, dim3(nb), dim3(CD_THREADS), 0, st, a);
     }
     lane_diag_report(st, "k_outbound", a.bdiag, nb);
     if (sent) {
@@ -1526,7 +1602,9 @@ int32_t sg_outbound_run(sg_ctx* ctx, sg_outbound* ob, const sg_outbound_sends* s
     const uint64_t err = r[1];
     if (err & E_UNSORTED) throw Error(SG_ERR_UNSORTED, "sends must be grouped by ascending host");
     if (err & E_HOST) throw Error(SG_ERR_INVALID_ARG, "send host out of range");
-    if (err & E_ORDER) throw Error(SG_ERR_UNSORTED, "a host's send times must not decrease");
+    if (err & E_ORDER)
+      throw Error(SG_ERR_UNSORTED, "a host's sends must come in execution order (time; Packet events, then "
+                                   "Local ones by creation time and id)");
     if (err & E_FULL) throw Error(SG_ERR_CAPACITY, "an interface queue outgrew its ring (raise ring_cap)");
     if (err & E_PKT) throw Error(SG_ERR_INVALID_ARG, "packet id >= n_packets");
     if (err & E_WINDOW) throw Error(SG_ERR_INVALID_ARG, "a send is at or after window_end");
@@ -1550,7 +1628,8 @@ int32_t sg_outbound_get_state(sg_outbound* ob, sg_outbound_queue_state* o, sg_in
       struct { void* h; const void* d; size_t b; } cp[] = {
           {rl->flags, ob->rflags, n}, {rl->task_time, ob->task_time, n * 8}, {rl->tb_capacity, ob->tb_cap, n * 8},
           {rl->tb_balance, ob->tb_bal, n * 8}, {rl->tb_increment, ob->tb_inc, n * 8},
-          {rl->tb_last_refill, ob->tb_last, n * 8}};
+          {rl->tb_last_refill, ob->tb_last, n * 8}, {rl->task_event_id, ob->task_id, n * 8},
+          {rl->task_created_ns, ob->task_born, n * 8}};
       for (auto& c : cp)
         if (c.h && c.b) SG_HIP(hipMemcpyAsync(c.h, c.d, c.b, hipMemcpyDeviceToHost, st));
     }

@@ -375,6 +375,7 @@ class RoutingInfo:
     def rows(self, row_begin: int = 0, row_end: Optional[int] = None):
         """Rows [row_begin, row_end) decoded from the 8-byte cells (sg_routing_info_rows): a
         (latency u64, loss f32) pair of new arrays."""
+        _capi.require_abi(5, "RoutingInfo.rows")
         row_end = self.n if row_end is None else int(row_end)
         k = max(0, row_end - int(row_begin))
         lat = np.empty((k, self.n), np.uint64)
@@ -398,6 +399,7 @@ class RoutingInfo:
     def cells(self) -> np.ndarray:
         """Zero-copy [n x n] view of the packed cells (latency << 32 | bits(loss); SG_CELL_WIDE in the
         upper half for paths of 2^32 - 1 ns or more).  The array keeps this object alive."""
+        _capi.require_abi(5, "RoutingInfo.cells")
         v = self._view()
         if not self.n:
             return np.zeros((0, 0), np.uint64)

@@ -158,12 +158,13 @@ class InboundPipeline:
                   bytes=np.zeros(n, np.uint64), head=np.zeros(n, np.uint32), tail=np.zeros(n, np.uint32),
                   ring_pkt=np.zeros(n * self.cap, np.uint32), ring_ts=np.zeros(n * self.cap, np.uint64),
                   ring_len=np.zeros(n * self.cap, np.uint32), rflags=np.zeros(n, np.uint8),
-                  task_time=np.zeros(n, np.uint64), cached_pkt=np.zeros(n, np.uint32),
+                  task_time=np.zeros(n, np.uint64), task_id=np.zeros(n, np.uint64), task_born=np.zeros(n, np.uint64),
+                  cached_pkt=np.zeros(n, np.uint32),
                   cached_len=np.zeros(n, np.uint32), tb_cap=np.zeros(n, np.uint64), tb_bal=np.zeros(n, np.uint64),
                   tb_inc=np.zeros(n, np.uint64), tb_last=np.zeros(n, np.uint64))
         v = lambda k: st[k].ctypes.data_as(C.c_void_p)
         rs = _capi.sg_inbound_relay_state(v("rflags"), v("task_time"), v("cached_pkt"), v("cached_len"), v("tb_cap"),
-                                          v("tb_bal"), v("tb_inc"), v("tb_last"))
+                                          v("tb_bal"), v("tb_inc"), v("tb_last"), v("task_id"), v("task_born"))
         check(self.ctx.handle, load().sg_inbound_get_state(self.handle, C.byref(CoDelQueues._struct(st)),
                                                            C.byref(rs)))
         return st
@@ -209,14 +210,23 @@ class OutboundPipeline:
         return self._sent
 
     def run(self, host, time_ns, packet, length, payload_len, dst_ipv4, window_end_ns: int, bootstrap_end_ns: int,
-            sim_end_ns: int, fwd_time, pkt_status, event_ctr_ptr: Optional[int] = None, sent_cap: Optional[int] = None):
+            sim_end_ns: int, fwd_time, pkt_status, event_ctr_ptr: Optional[int] = None, sent_cap: Optional[int] = None,
+            event_id=None, event_created_ns=None):
         """Sends as device tensors (int32 host/packet/length/payload_len/dst_ipv4, int64 time); fwd_time
-        (int64) and pkt_status (uint8) are indexed by packet id.  Returns (PacketBatch of the packets
-        sent, in send_packet order, and their packet ids), views of buffers reused by the next call."""
+        (int64) and pkt_status (uint8) are indexed by packet id.  event_id / event_created_ns (int64
+        device tensors, optional, together; they need event_ctr_ptr): the sending event's id (-1 =
+        UINT64_MAX: a Packet event) and creation time, which order a send against a forward task at
+        the same time (sg_outbound_sends).  Returns (PacketBatch of the packets sent, in send_packet
+        order, and their packet ids), views of buffers reused by the next call."""
         from .worker import PacketBatch
         n = int(host.numel())
+        keyed = event_id is not None
+        if keyed:
+            _capi.require_abi(6, "OutboundPipeline.run with event ids")
         s = _capi.sg_outbound_sends(n, host.data_ptr(), time_ns.data_ptr(), packet.data_ptr(), length.data_ptr(),
-                                    payload_len.data_ptr(), dst_ipv4.data_ptr())
+                                    payload_len.data_ptr(), dst_ipv4.data_ptr(),
+                                    event_id.data_ptr() if keyed else None,
+                                    event_created_ns.data_ptr() if event_created_ns is not None else None)
         cap = int(sent_cap if sent_cap is not None else n + self.n * 4)
         b = self.sent_buffers(max(cap, 1), fwd_time.device)
         o = _capi.sg_outbound_sent(cap, *(b[k].data_ptr() for k in ("src_host", "dst_ipv4", "payload_len",
@@ -237,13 +247,14 @@ class OutboundPipeline:
         st = dict(cap=c, head=np.zeros(n, np.uint32), tail=np.zeros(n, np.uint32),
                   ring_pkt=np.zeros(n * c, np.uint32), ring_len=np.zeros(n * c, np.uint32),
                   ring_pay=np.zeros(n * c, np.uint32), ring_dst=np.zeros(n * c, np.uint32),
-                  rflags=np.zeros(n, np.uint8), task_time=np.zeros(n, np.uint64), tb_cap=np.zeros(n, np.uint64),
+                  rflags=np.zeros(n, np.uint8), task_time=np.zeros(n, np.uint64), task_id=np.zeros(n, np.uint64),
+                  task_born=np.zeros(n, np.uint64), tb_cap=np.zeros(n, np.uint64),
                   tb_bal=np.zeros(n, np.uint64), tb_inc=np.zeros(n, np.uint64), tb_last=np.zeros(n, np.uint64))
         v = lambda k: st[k].ctypes.data_as(C.c_void_p)
         q = _capi.sg_outbound_queue_state(v("head"), v("tail"), v("ring_pkt"), v("ring_len"), v("ring_pay"),
                                           v("ring_dst"))
         rs = _capi.sg_inbound_relay_state(v("rflags"), v("task_time"), None, None, v("tb_cap"), v("tb_bal"),
-                                          v("tb_inc"), v("tb_last"))
+                                          v("tb_inc"), v("tb_last"), v("task_id"), v("task_born"))
         check(self.ctx.handle, load().sg_outbound_get_state(self.handle, C.byref(q), C.byref(rs)))
         return st
 

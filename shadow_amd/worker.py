@@ -169,6 +169,8 @@ class PacketBatch:
             p.n_packets = len(self)
             p.src_host, p.dst_ipv4 = self.src_host.data_ptr(), self.dst_ipv4.data_ptr()
             p.payload_len, p.send_time_ns = self.payload_len.data_ptr(), self.send_time_ns.data_ptr()
+            if self.rng_skip is not None:
+                _capi.require_abi(5, "PacketBatch.rng_skip")
             p.rng_skip = self.rng_skip.data_ptr() if self.rng_skip is not None else None
             return p
 

@@ -27,3 +27,24 @@ def ctx():
 
     shadow_amd.load()
     return shadow_amd.default_context(0)
+
+
+# Shortest-path kernels the routing tests run on.  The defaults: the per-source LDS search
+# (sg_sssp.hip) in its unbounded and forced bounded-phase forms (the build picks phases from
+# 8 rows per CU on, i.e. at C3) and the slab relaxation (dense graphs, graphs past the LDS).
+# The non-default options (landmarks, the team search) run in test_option_kernels, or on the
+# whole matrix with SG_TEST_ALL_KERNELS=1.
+APSP_KERNELS = ["lds", "lds_bounded", "slab"]
+APSP_OPTIONS = ["lds_landmarks", "team"]
+if os.environ.get("SG_TEST_ALL_KERNELS"):
+    APSP_KERNELS = APSP_KERNELS + APSP_OPTIONS
+
+
+def set_apsp_kernel(monkeypatch, name: str) -> str:
+    """Select a routing kernel by environment; returns its family ("lds" or "slab")."""
+    monkeypatch.setenv("SG_APSP_LDS", "0" if name == "slab" else "1")
+    monkeypatch.setenv("SG_SSSP_SEEDS", "2" if name in ("lds_bounded", "lds_landmarks", "team") else "1")
+    monkeypatch.setenv("SG_SSSP_LANDMARKS", "8" if name == "lds_landmarks" else "0")
+    # team: the search of graphs past one CU's LDS (sg_team.hip), forced with 3 members, in phases
+    monkeypatch.setenv("SG_SSSP_TEAM", "3" if name == "team" else "0")
+    return "slab" if name == "slab" else "lds"

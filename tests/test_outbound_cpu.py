@@ -10,12 +10,21 @@ MS = 10**6
 NEVER = 2**63
 
 
-def run(O, st, sends, window_end, boot=0, sim_end=NEVER, n_pk=16):
+PACKET = 2**64 - 1  # sends made by a Packet event (event.rs:103-112)
+
+
+def run(O, st, sends, window_end, boot=0, sim_end=NEVER, n_pk=16, keys=None, ctr0=0):
+    """keys: per send (event created at, event id) of the event that made it, or None."""
     host, t, pkt, ln, pay, dst = (list(x) for x in zip(*sends)) if sends else ([],) * 6
-    ctr = np.zeros(len(st["head"]), np.uint64)
+    ctr = np.full(len(st["head"]), ctr0, np.uint64)
     fwd = np.full(n_pk, np.uint64(2**64 - 1))
     status = np.zeros(n_pk, np.uint8)
-    out = O.outbound_run(st, host, t, pkt, ln, pay, dst, window_end, boot, sim_end, ctr, fwd, status)
+    born = eid = None
+    if keys is not None:
+        born = np.array([k[0] for k in keys], np.uint64)
+        eid = np.array([k[1] for k in keys], np.uint64)
+    out = O.outbound_run(st, host, t, pkt, ln, pay, dst, window_end, boot, sim_end, ctr, fwd, status,
+                         event_id=eid, event_created=born)
     return out, ctr, fwd, status
 
 
@@ -90,3 +99,67 @@ def test_errors(oracle):
     st = oracle.outbound_state([10], [10**9], 2)
     with pytest.raises(ValueError, match="-5"):
         run(oracle, st, [(0, T0 + MS, 0, 100, 60, 11)], T0 + MS)
+
+
+# ---- same-time order of a send and a forward task (event.rs:84-155, relay/mod.rs:145-157) ----
+# 8 Mbit/s: refill 1000 B per ms, capacity 2500.  Send A (T0+1) finds the relay Idle: task X
+# (id 100, created T0+1) runs after the sending event (id 5) and forwards A; B blocks (1000 B
+# left) and is cached; the wake-up W (id 101) is created at T0+1 for T0+1ms.  Send C lands on
+# T0+1ms exactly.  Who runs first at T0+1ms depends on when C's event was created.
+AB = [(0, T0 + 1, 0, 1500, 1472, 11), (0, T0 + 1, 1, 1500, 1472, 11)]
+C_AT_WAKE = (0, T0 + MS, 2, 1500, 1472, 11)
+
+
+@pytest.mark.parametrize("c_key,want_ctr", [
+    ((T0, 6), 103),              # C's event created before W (T0 < T0+1): C joins W's run (X, W, W2)
+    ((PACKET, PACKET), 103),     # a Packet event's send precedes every Local event
+    ((T0 + MS // 2, 7), 104),    # created after W (a timer set at T0+0.5ms): W first (X, W, X2, W2)
+    ((T0 + 1, 50), 103),         # same creation time, smaller id: created before W
+    ((T0 + 1, 150), 153),        # same creation time, larger id: after W; X2 and W2 numbered past 150
+])
+def test_wake_vs_send_at_the_same_time(oracle, c_key, want_ctr):
+    st = oracle.outbound_state([10], [8 * 10**6], 8)
+    keys = [(T0, 5), (T0, 5), c_key]
+    out, ctr, fwd, status = run(oracle, st, AB + [C_AT_WAKE], T0 + 10 * MS, keys=keys, ctr0=100)
+    assert list(out["packet"]) == [0, 1, 2]
+    # B leaves with W at T0+1ms either way; C waits for the next refill either way
+    assert list(out["send_time"] - T0) == [1, MS, 2 * MS]
+    assert ctr[0] == want_ctr and st["task_id"][0] == want_ctr - 1
+    assert st["task_time"][0] == T0 + 2 * MS and st["task_born"][0] == T0 + MS
+
+
+def test_wake_first_counts_one_more_task(oracle):
+    """The two orders differ in the host's event count: the wake-first order empties the
+    queue, so C's notify schedules one more task (host.rs:649-653)."""
+    got = {}
+    for name, ck in (("send_first", (T0, 6)), ("wake_first", (T0 + MS // 2, 7))):
+        st = oracle.outbound_state([10], [8 * 10**6], 8)
+        _, ctr, _, _ = run(oracle, st, AB + [C_AT_WAKE], T0 + 10 * MS, keys=[(T0, 5), (T0, 5), ck], ctr0=100)
+        got[name] = (int(ctr[0]), int(st["task_id"][0]), int(st["task_born"][0]))
+    assert got["send_first"] == (103, 102, T0 + MS)  # W2 created by W at T0+1ms
+    assert got["wake_first"] == (104, 103, T0 + MS)  # W2 created by X2
+
+
+def test_notify_task_vs_later_event_at_the_same_time(oracle):
+    """X (notify at T0+5 by event 5) and a send at T0+5 by an event created at T0+5 after X
+    (id 120 > 100): X runs first and forwards A alone; B's notify finds the relay Idle and
+    schedules X2, numbered after B's event (121).  Without keys B joins X's run."""
+    sends = [(0, T0 + 5, 0, 100, 60, 11), (0, T0 + 5, 1, 100, 60, 11)]
+    st = oracle.outbound_state([10], [10**9], 8)
+    out, ctr, _, _ = run(oracle, st, sends, T0 + MS, keys=[(T0, 5), (T0 + 5, 120)], ctr0=100)
+    assert list(out["send_time"] - T0) == [5, 5] and ctr[0] == 122 and st["task_id"][0] == 121
+    st = oracle.outbound_state([10], [10**9], 8)
+    out, ctr, _, _ = run(oracle, st, sends, T0 + MS, ctr0=100)
+    assert list(out["send_time"] - T0) == [5, 5] and ctr[0] == 101 and st["task_id"][0] == 100
+
+
+def test_keys_must_follow_execution_order(oracle):
+    st = oracle.outbound_state([10], [10**9], 8)
+    sends = [(0, T0 + 5, 0, 100, 60, 11), (0, T0 + 5, 1, 100, 60, 11)]
+    with pytest.raises(ValueError, match="-6"):  # a Packet-event send after a Local one, same time
+        run(oracle, st, sends, T0 + MS, keys=[(T0, 5), (PACKET, PACKET)])
+    st = oracle.outbound_state([10], [10**9], 8)
+    with pytest.raises(ValueError, match="-6"):  # Local events out of id order
+        run(oracle, st, sends, T0 + MS, keys=[(T0, 9), (T0, 5)])
+    st = oracle.outbound_state([10], [10**9], 8)
+    run(oracle, st, sends, T0 + MS, keys=[(PACKET, PACKET), (T0, 5)])  # Packet first: fine

@@ -14,7 +14,7 @@ from shadow_amd.worker import DeviceTable, HostTable, deliver_round
 pytestmark = pytest.mark.gpu
 T0 = 946684800 * 10**9
 MS = 10**6
-RKEYS = ("head", "tail", "rflags", "task_time", "tb_cap", "tb_bal", "tb_inc", "tb_last")
+RKEYS = ("head", "tail", "rflags", "task_time", "task_id", "task_born", "tb_cap", "tb_bal", "tb_inc", "tb_last")
 
 
 def _dev(a, np_dtype, torch_dtype):
@@ -90,6 +90,99 @@ def test_windows_match_oracle(oracle, ctx, bw_mbit, boot_ms):
     assert (st_o == 2).any()
     if bw_mbit == 2:
         assert (st_o == 0).any() and (ost["rflags"] & oracle.RL_PENDING).any() and total < n_pk
+
+
+def _keyed_sends(hosts, n, t0, t1, seed):
+    """Sends of which half land exactly on a refill boundary (T0 + k ms, where a blocked
+    relay's wake-up falls), each made by a random event: a Packet event (id UINT64_MAX) or a
+    Local one created up to 3 ms earlier with a random id.  Per (host, time) the sends are put
+    in execution order: Packet events first, then Local ones by (created, id)."""
+    host, t, ln, pay, dst = _sends(hosts, n, t0, t1, seed)
+    rng = np.random.default_rng(seed + 7)
+    snap = rng.random(n) < 0.5
+    t = np.where(snap, (t - T0) // MS * MS + T0, t).astype(np.uint64)
+    t = np.maximum(t, np.uint64(t0))
+    pk = rng.random(n) < 0.2
+    born = (t - rng.integers(0, 3 * MS, n).astype(np.uint64)).astype(np.uint64)
+    born = np.where(rng.random(n) < 0.3, (born - T0) // MS * MS + T0, born).astype(np.uint64)  # wake births
+    eid = rng.integers(0, 5000, n).astype(np.uint64)
+    born = np.where(pk, np.uint64(0), born)
+    eid = np.where(pk, np.uint64(2**64 - 1), eid)
+    o = np.lexsort((eid, born, ~pk, t, host))  # host, time, Packet first, created, id
+    return host[o], t[o], ln[o], pay[o], dst[o], eid[o], born[o]
+
+
+@pytest.mark.parametrize("bw_mbit", [10, 2])
+def test_same_time_ties_match_oracle(oracle, ctx, bw_mbit):
+    """Wake-ups and sends on the same nanosecond, ordered by the sending event's (created, id)
+    against the task's (relay/mod.rs:145-157, event.rs:84-155): 1500 hosts, 4 windows, keyed
+    sends (k_outbound<true>) bit-exact with the oracle, task ids included.  The keys must
+    matter: the oracle with every Local send created first, and with every one created last,
+    disagrees (the ties went both ways)."""
+    import torch
+
+    H, W, per = 1500, 2 * MS, 30000
+    hosts = synth.make_hosts(H, 64, exact_seeds=False)
+    bw = np.full(H, bw_mbit * 10**6, np.uint64)
+    ob = OutboundPipeline(hosts["ip"], bw, 1024, ctx=ctx)
+    ost = oracle.outbound_state(hosts["ip"], bw, ob.cap)
+    alt = {k: oracle.outbound_state(hosts["ip"], bw, ob.cap) for k in ("early", "late")}
+    n_pk = 4 * per
+    fwd_g = torch.full((n_pk,), -1, dtype=torch.int64, device="cuda")
+    st_g = torch.zeros(n_pk, dtype=torch.uint8, device="cuda")
+    ctr_g = torch.zeros(H, dtype=torch.int64, device="cuda")
+    fwd_o, st_o, ctr_o = np.full(n_pk, np.uint64(2**64 - 1)), np.zeros(n_pk, np.uint8), np.zeros(H, np.uint64)
+    ctr_alt = {k: np.zeros(H, np.uint64) for k in alt}
+    sim_end = T0 + 10**12
+    for w in range(4):
+        t0, t1 = T0 + w * W, T0 + (w + 1) * W
+        host, t, ln, pay, dst, eid, born = _keyed_sends(hosts, per, t0, t1, seed=50 * bw_mbit + w)
+        pkt = np.arange(w * per, (w + 1) * per, dtype=np.uint32)
+        batch, ids = ob.run(_dev(host, np.uint32, np.int32), _dev(t, np.uint64, np.int64),
+                            _dev(pkt, np.uint32, np.int32), _dev(ln, np.uint32, np.int32),
+                            _dev(pay, np.uint32, np.int32), _dev(dst, np.uint32, np.int32), t1, 0, sim_end,
+                            fwd_g, st_g, ctr_g.data_ptr(), event_id=_dev(eid, np.uint64, np.int64),
+                            event_created_ns=_dev(born, np.uint64, np.int64))
+        want = oracle.outbound_run(ost, host, t, pkt, ln, pay, dst, t1, 0, sim_end, ctr_o, fwd_o, st_o,
+                                   event_id=eid, event_created=born)
+        assert np.array_equal(st_g.cpu().numpy(), st_o)
+        m = st_o != 0
+        assert np.array_equal(fwd_g.cpu().numpy().view(np.uint64)[m], fwd_o[m])
+        assert np.array_equal(ctr_g.cpu().numpy().view(np.uint64), ctr_o)
+        assert np.array_equal(ids.cpu().numpy().view(np.uint32), want["packet"])
+        assert np.array_equal(batch.send_time_ns.cpu().numpy().view(np.uint64), want["send_time"])
+        got = ob.get_state()
+        for k in RKEYS:
+            assert np.array_equal(got[k], ost[k]), k
+        _live_same(got, ost)
+        scratch = lambda: (np.zeros(n_pk, np.uint64), np.zeros(n_pk, np.uint8))
+        for k, shift in (("early", -10**12), ("late", 10**12)):  # every Local send created first / last
+            b2 = np.where(eid == np.uint64(2**64 - 1), born, (born.astype(np.int64) + shift).astype(np.uint64))
+            oracle.outbound_run(alt[k], host, t, pkt, ln, pay, dst, t1, 0, sim_end, ctr_alt[k], *scratch(),
+                                event_id=eid, event_created=b2)
+    for k in alt:  # the ties went both ways
+        assert not np.array_equal(ctr_alt[k], ctr_o), k
+
+
+def test_keyed_send_errors(ctx):
+    import torch
+
+    ob = OutboundPipeline(np.array([10], np.uint32), np.array([10**9], np.uint64), 16, ctx=ctx)
+    f = torch.zeros(8, dtype=torch.int64, device="cuda")
+    s = torch.zeros(8, dtype=torch.uint8, device="cuda")
+    ctr = torch.zeros(1, dtype=torch.int64, device="cuda")
+    args = [_dev([0, 0], np.uint32, np.int32), _dev([T0 + 1, T0 + 1], np.uint64, np.int64),
+            _dev([0, 1], np.uint32, np.int32), _dev([100] * 2, np.uint32, np.int32),
+            _dev([60] * 2, np.uint32, np.int32), _dev([11, 11], np.uint32, np.int32)]
+    born = _dev([T0, T0], np.uint64, np.int64)
+    with pytest.raises(ShadowGpuError) as e:  # Local events out of id order at one time
+        ob.run(*args, T0 + MS, 0, T0 + 10**12, f, s, ctr.data_ptr(), event_id=_dev([9, 5], np.uint64, np.int64),
+               event_created_ns=born)
+    assert e.value.code == _capi.SG_ERR_UNSORTED
+    with pytest.raises(ShadowGpuError) as e:  # keys need the hosts' counters
+        ob.run(*args, T0 + MS, 0, T0 + 10**12, f, s, None, event_id=_dev([5, 9], np.uint64, np.int64),
+               event_created_ns=born)
+    assert e.value.code == _capi.SG_ERR_INVALID_ARG
 
 
 def test_sent_batch_feeds_delivery(oracle, ctx):

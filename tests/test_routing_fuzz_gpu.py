@@ -5,22 +5,17 @@ undirected, parallel arcs, used-node subsets.  Bit-exact against the oracle."""
 import numpy as np
 import pytest
 
+from conftest import APSP_KERNELS, set_apsp_kernel
 from shadow_amd import NetworkGraph
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["lds", "lds_bounded", "lds_landmarks", "team", "slab"])
+@pytest.fixture(autouse=True, params=APSP_KERNELS)
 def apsp_kernel(request, monkeypatch):
-    """Both shortest-path kernels: the per-source LDS search (also in its forced
-    two-phase form, seed rows then bounded rows, and with the first phase split
-    by 8 landmark rows) and the slab relaxation."""
-    monkeypatch.setenv("SG_APSP_LDS", "0" if request.param == "slab" else "1")
-    monkeypatch.setenv("SG_SSSP_SEEDS", "2" if request.param in ("lds_bounded", "lds_landmarks", "team") else "1")
-    monkeypatch.setenv("SG_SSSP_LANDMARKS", "8" if request.param == "lds_landmarks" else "0")
-    # team: the search of graphs past one CU's LDS (sg_team.hip), forced with 3 members, in phases
-    monkeypatch.setenv("SG_SSSP_TEAM", "3" if request.param == "team" else "0")
-    return "lds" if request.param.startswith("lds") or request.param == "team" else request.param
+    """The default shortest-path kernels (conftest.APSP_KERNELS): the per-source LDS search,
+    also in its forced bounded-phase form, and the slab relaxation."""
+    return set_apsp_kernel(monkeypatch, request.param)
 
 
 def _random_graph(n, avg_deg, directed, seed):
@@ -60,3 +55,4 @@ def test_random_graph_shapes(oracle, ctx, n, avg_deg, directed, frac, seed):
     assert rc == 0
     assert np.array_equal(t.latency_ns, olat)
     assert np.array_equal(t.packet_loss.view(np.uint32), oloss.view(np.uint32))
+

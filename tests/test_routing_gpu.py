@@ -11,27 +11,21 @@ import re
 import numpy as np
 import pytest
 
+from conftest import APSP_KERNELS, set_apsp_kernel
 from shadow_amd import NetworkGraph, ShadowGpuError, _capi, generate_routing_info, synth
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(autouse=True, params=["lds", "lds_bounded", "lds_landmarks", "team", "slab"])
+@pytest.fixture(autouse=True, params=APSP_KERNELS)
 def apsp_kernel(request, monkeypatch):
-    """Every routing test runs on both shortest-path kernels: the per-source
-    LDS-resident search (sg_sssp.hip, the default up to ~10.9k nodes) and the
-    batched-source slab relaxation (k_relax_w2, larger graphs).  lds_bounded
-    forces the LDS search's phases (seed rows, then rows whose keys start at a
-    seed neighbour's bounds), which the default uses from 8 rows per CU on.
-    lds_landmarks also splits the first phase: 8 landmark rows first, the rest of
-    it bounded through them (undirected graphs; an option, measured slower at C3)."""
-    monkeypatch.setenv("SG_APSP_LDS", "0" if request.param == "slab" else "1")
-    monkeypatch.setenv("SG_SSSP_SEEDS", "2" if request.param in ("lds_bounded", "lds_landmarks", "team") else "1")
-    monkeypatch.setenv("SG_SSSP_LANDMARKS", "8" if request.param == "lds_landmarks" else "0")
-    # team: the search of graphs past one CU's LDS (sg_team.hip), forced with 3 members, in phases
-    monkeypatch.setenv("SG_SSSP_TEAM", "3" if request.param == "team" else "0")
-    return "lds" if request.param.startswith("lds") or request.param == "team" else request.param
+    """Every routing test runs on the default shortest-path kernels (conftest.APSP_KERNELS):
+    the per-source LDS-resident search (sg_sssp.hip, the default up to ~10.9k nodes), also in
+    its forced bounded-phase form (seed rows, then rows whose keys start at a seed neighbour's
+    bounds: the default from 8 rows per CU on), and the batched-source slab relaxation
+    (k_relax_w2, dense and larger graphs)."""
+    return set_apsp_kernel(monkeypatch, request.param)
 
 
 def _graph(g, ctx):
