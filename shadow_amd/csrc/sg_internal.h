@@ -203,7 +203,10 @@ struct sg_routing_info {
     uint64_t lat;
   };
   std::vector<Wide> wide;
-  std::vector<uint8_t> row_set;  // rows written (set_rows); all set -> filled
+  // per row: 0 not written, 1 written with its smallest latency in row_min, 2 written by a
+  // fill (row_min not kept; computed once if set_rows later needs it); all written -> filled
+  std::vector<uint8_t> row_set;
+  std::vector<uint64_t> row_min;
   uint32_t rows_set = 0;
   bool filled = false;
   uint64_t min_lat = UINT64_MAX;

@@ -141,6 +141,7 @@ int32_t sg_routing_info_create(uint32_t n_used, const uint32_t* node_ids, sg_rou
     const size_t cells = (size_t)n_used * n_used;
     ri->cell = (uint64_t*)sg::host_alloc(cells * 8, ri->pinned);
     ri->row_set.assign(n_used, 0);
+    ri->row_min.assign(n_used, UINT64_MAX);
   } catch (const sg::Error& e) {
     delete ri;
     return e.code;
@@ -166,27 +167,46 @@ int32_t sg_routing_info_set_rows(sg_routing_info* ri, uint32_t row_begin, uint32
     auto hi = std::lower_bound(lo, ri->wide.end(), (uint64_t)(off + cells),
                                [](const sg_routing_info::Wide& w, uint64_t k) { return w.cell < k; });
     std::vector<sg_routing_info::Wide> add;
-    for (size_t i = 0; i < cells; i++) {
-      uint32_t b;
-      memcpy(&b, &packet_loss[i], 4);
-      const uint64_t l = latency_ns[i];
-      const uint32_t hi32 = l < SG_CELL_WIDE ? (uint32_t)l : SG_CELL_WIDE;
-      ri->cell[off + i] = ((uint64_t)hi32 << 32) | b;
-      if (hi32 == SG_CELL_WIDE) add.push_back({off + i, l});
+    const uint32_t n = ri->n;
+    for (uint32_t r = row_begin; r < row_end; r++) {
+      uint64_t rm = UINT64_MAX;
+      for (uint32_t c = 0; c < n; c++) {
+        const size_t i = (size_t)(r - row_begin) * n + c;
+        uint32_t b;
+        memcpy(&b, &packet_loss[i], 4);
+        const uint64_t l = latency_ns[i];
+        const uint32_t hi32 = l < SG_CELL_WIDE ? (uint32_t)l : SG_CELL_WIDE;
+        ri->cell[off + i] = ((uint64_t)hi32 << 32) | b;
+        if (hi32 == SG_CELL_WIDE) add.push_back({off + i, l});
+        rm = std::min(rm, l);
+      }
+      ri->rows_set += ri->row_set[r] ? 0u : 1u;
+      ri->row_set[r] = 1;
+      ri->row_min[r] = rm;
     }
     const size_t at = lo - ri->wide.begin();
     ri->wide.erase(lo, hi);
     ri->wide.insert(ri->wide.begin() + at, add.begin(), add.end());
-    for (uint32_t r = row_begin; r < row_end; r++) ri->rows_set += !ri->row_set[r]++ ? 1u : 0u;
     // get_smallest_latency_ns (graph/mod.rs:478-480) is over every entry: once the whole
-    // table is present, recompute it over the whole table (rows may have been rewritten)
-    if (ri->rows_set == ri->n) {
+    // table is present, the smallest of the per-row minima (rows may have been rewritten;
+    // a row a fill wrote gets its minimum once, from its cells and the side table)
+    if (ri->rows_set == n) {
       uint64_t m = UINT64_MAX;
-      const size_t all = (size_t)ri->n * ri->n;
-      for (size_t i = 0; i < all; i++) m = std::min(m, ri->cell[i] >> 32);
-      if (m == SG_CELL_WIDE) {  // every cell is wide: the smallest u64 latency of the side table
-        m = UINT64_MAX;
-        for (auto& w : ri->wide) m = std::min(m, w.lat);
+      for (uint32_t r = 0; r < n; r++) {
+        if (ri->row_set[r] == 2) {
+          const size_t o = (size_t)r * n;
+          uint64_t rm = UINT64_MAX;
+          for (uint32_t c = 0; c < n; c++) rm = std::min(rm, ri->cell[o + c] >> 32);
+          if (rm == SG_CELL_WIDE) {  // every cell of the row is wide: its smallest u64 latency
+            rm = UINT64_MAX;
+            auto w = std::lower_bound(ri->wide.begin(), ri->wide.end(), (uint64_t)o,
+                                      [](const sg_routing_info::Wide& x, uint64_t k) { return x.cell < k; });
+            for (; w != ri->wide.end() && w->cell < o + n; ++w) rm = std::min(rm, w->lat);
+          }
+          ri->row_min[r] = rm;
+          ri->row_set[r] = 1;
+        }
+        m = std::min(m, ri->row_min[r]);
       }
       ri->min_lat = m;
       ri->filled = true;

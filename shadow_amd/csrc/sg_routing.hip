@@ -2022,7 +2022,7 @@ int32_t sg_routing_info_fill(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, ui
     SG_HIP(hipStreamSynchronize(ctx->copy_stream));
     std::sort(ri->wide.begin(), ri->wide.end(),
               [](const sg_routing_info::Wide& x, const sg_routing_info::Wide& y) { return x.cell < y.cell; });
-    std::fill(ri->row_set.begin(), ri->row_set.end(), 1);
+    std::fill(ri->row_set.begin(), ri->row_set.end(), 2);  // written; per-row minima not kept
     ri->rows_set = n_used;
     ri->min_lat = m;
     ri->filled = true;

@@ -134,6 +134,8 @@ class SourceResult:
     n_delivered: int
     min_deliver_time_ns: int
     min_used_latency_ns: int
+    send_padded: object = None  # padded rounds: the [n_ranks * cap, 4] blocks (send is then None
+    #                             unless the round overflowed into an exact exchange)
 
 
 def gpu_source_phase(ctx, hosts, table, packets, round_end_ns, sim_end_ns, bootstrap_end_ns, owner_dev,
@@ -245,6 +247,29 @@ def gpu_pad_to_compact(ctx, src: SourcePadded, n_ranks: int):
     check(ctx.handle, load().sg_deliver_pad_to_compact(ctx.handle, src.send_padded.data_ptr(), n_ranks, src.cap,
                                                        src.xrow.data_ptr(), src.send.data_ptr()))
     return src.send
+
+
+def _stream_wait(waiter: int, producer: int) -> None:
+    """Make stream `waiter` wait for the work enqueued on stream `producer` so far (a HIP
+    event; streams as hipStream_t ints, 0 = the legacy default stream).  A no-op for one
+    stream."""
+    if waiter == producer:
+        return
+    import torch
+
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.ExternalStream(producer))
+    torch.cuda.ExternalStream(waiter).wait_event(ev)
+
+
+def _streams(ctx, tensor):
+    """(the library context's stream, torch's current stream) for device tensors, else None."""
+    if ctx is None or not hasattr(ctx, "stream") or getattr(tensor, "device", None) is None \
+            or tensor.device.type != "cuda":
+        return None
+    import torch
+
+    return int(ctx.stream), int(torch.cuda.current_stream(tensor.device).cuda_stream)
 
 
 def next_cap(pair_max: int) -> int:
@@ -372,6 +397,19 @@ def gather_round_stats(n_delivered: int, min_deliver: int, min_lat: int, dist, g
     return int(allv[:, 0].sum()), int(allv[:, 1].min()), int(allv[:, 2].min())
 
 
+def _global_max(v: int, dist, group=None, device="cuda") -> int:
+    """max over ranks of one non-negative int (an all-gather of one value per rank)."""
+    import torch
+
+    world = dist.get_world_size(group) if dist is not None else 1
+    if dist is None or world == 1:
+        return int(v)
+    dev = "cpu" if _host_staged(dist, group, torch.device(device)) else device
+    out = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(out, torch.tensor([int(v)], dtype=torch.int64, device=dev), group=group)
+    return int(out.max().item())
+
+
 class ShardedDelivery:
     """One rank's side of a sharded delivery round (see module docstring).
 
@@ -424,7 +462,15 @@ class ShardedDelivery:
         cap = self.cap
         src = self.source_padded_fn(self.ctx, self.hosts, self.table, packets, round_end_ns, sim_end_ns,
                                     bootstrap_end_ns, self.owner_dev, self.world, cap)
+        # The source phase only enqueues on the library's stream, and the collectives order
+        # against torch's current stream: join the two both ways around the exchange (nothing
+        # is synchronised until the bucketing's end).
+        streams = _streams(self.ctx, src.send_padded)
+        if streams:
+            _stream_wait(streams[1], streams[0])
         recv, xall = exchange_padded(src.send_padded, src.xrow, self.dist, self.group, ws=self.ws)
+        if streams:
+            _stream_wait(streams[0], streams[1])
         order, offsets, g, recv_counts, pair_max = self.bucket_padded_fn(
             self.ctx, recv, cap, xall, self.rank, self.local_dev, len(self.part.local), self.part.n_local(self.rank))
         xa = xall.cpu().numpy().view(np.uint64).reshape(self.world, 3 + self.world)  # (after the round's sync)
@@ -441,7 +487,11 @@ class ShardedDelivery:
                                             len(self.part.local), self.part.n_local(self.rank))
         else:
             self.last_mode = "padded"
-        res = SourceResult(src.status, src.deliver_time_ns, src.event_id, src.send, send_counts, *self.last_stats)
+        # a padded round's records are the blocks (records past cap also sit in src.send, at
+        # their compact positions; its other slots hold an earlier round's records)
+        res = SourceResult(src.status, src.deliver_time_ns, src.event_id,
+                           src.send if self.last_mode == "padded+exact" else None, send_counts, *self.last_stats,
+                           send_padded=src.send_padded)
         self.last = (recv, order, offsets)
         self.last_recv_counts = list(recv_counts)
         return res, recv, recv_counts, order, offsets
@@ -458,7 +508,9 @@ class ShardedDelivery:
         else:
             recv, recv_counts = self.exchange_fn(src.send, src.send_counts)
             self.last_stats = gather_round_stats(*stats, self.dist, self.group, self.device)
-            self._pair_max = max(list(src.send_counts) + list(recv_counts) + [0])
+            # the block size must agree on every rank: the largest pair count of all ranks
+            self._pair_max = _global_max(max(list(src.send_counts) + list(recv_counts) + [0]), self.dist,
+                                         self.group, self.device)
         order, offsets = self.bucket_fn(self.ctx, recv, int(sum(recv_counts)), self.local_dev,
                                         len(self.part.local), self.part.n_local(self.rank))
         self.last = (recv, order, offsets)  # this rank's destination buckets of the round

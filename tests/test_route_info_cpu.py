@@ -130,3 +130,24 @@ def test_smallest_latency_needs_every_row():
     big = np.full_like(lat, 10**12)
     ri.set_rows(0, big, loss)
     assert ri.get_smallest_latency_ns() == 10**12
+
+
+def test_smallest_latency_after_many_row_rewrites():
+    """A row rewritten hundreds of times (the per-row written flag must not wrap) keeps the
+    whole-table minimum current; each rewrite updates its own row's minimum only."""
+    lat, loss = _table(6)
+    ri = RoutingInfo(range(6), lat, loss)
+    for k in range(300):
+        row = lat[3:4] + np.uint64(k)
+        ri.set_rows(3, row, loss[3:4])
+    want = min(int(np.delete(lat, 3, axis=0).min()), int(lat[3].min()) + 299)
+    assert ri.get_smallest_latency_ns() == want
+    small = np.full_like(lat[1:2], 5)
+    ri.set_rows(1, small, loss[1:2])
+    assert ri.get_smallest_latency_ns() == 5
+    ri.set_rows(1, lat[1:2], loss[1:2])  # back up: the minimum rises again
+    assert ri.get_smallest_latency_ns() == want
+    wide = np.full_like(lat, 1 << 40)  # every cell wide: the u64 minimum from the side table
+    wide[4, 2] = (1 << 40) - 9
+    ri.set_rows(0, wide, loss)
+    assert ri.get_smallest_latency_ns() == (1 << 40) - 9

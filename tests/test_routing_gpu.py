@@ -459,6 +459,12 @@ def test_routing_info_direct_and_errors(oracle, ctx):
     rc, olat, oloss, _ = oracle.direct_paths(g["n"], g["src"], g["dst"], g["lat"], g["loss"], False,
                                              np.arange(90, dtype=np.uint32))
     assert rc == 0 and np.array_equal(ri.latency_ns, olat)
+    assert ri.get_smallest_latency_ns() == int(olat.min())
+    # a row rewritten after the fill: the minimum follows it both ways (per-row minima)
+    ri.set_rows(7, np.full((1, 90), 3, np.uint64), oloss[7:8])
+    assert ri.get_smallest_latency_ns() == 3
+    ri.set_rows(7, olat[7:8], oloss[7:8])
+    assert ri.get_smallest_latency_ns() == int(olat.min())
     keep = ~((g["src"] == 5) & (g["dst"] == 5))  # node 5 loses its self-loop
     g2 = dict(g, src=g["src"][keep], dst=g["dst"][keep], lat=g["lat"][keep], loss=g["loss"][keep])
     with pytest.raises(ShadowGpuError) as e:
