@@ -80,6 +80,9 @@ def parse_args():
     p.add_argument("--cpu-rows", type=int, default=0,
                    help="time the CPU routing baseline on the first K source rows and scale to all rows "
                         "(0 = every row)")
+    p.add_argument("--rank-blocks", default="2,4,8",
+                   help="at one GPU: time every rank's one-shot row-block build of these N-way splits "
+                        "(apsp_detail.rank_block_ms; '' skips)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-delivery", action="store_true")
     p.add_argument("--no-codel", action="store_true", help="skip the router CoDel leg")
@@ -594,6 +597,30 @@ def main():
     # beside it: rebuilds on the same device graph (the plan is rebuilt too; nothing is cached)
     t_warm = timed(D, build, a.steps, a.warmup)
     t_allgather = timed(D, allgather, max(1, a.steps // 2), 1) if D.dist else 0.0
+    # The sharded build rehearsed on this one GPU: every rank's row block of an N-way split,
+    # one-shot (upload, the block's own plan, search, release) as that rank would build it.
+    # max_ms is the N-GPU build time less the all-gather; frac_of_linear = (one-shot / N) / max_ms.
+    rank_blocks = None
+    if D.world == 1 and a.rank_blocks:
+        rank_blocks = {}
+        bl = torch.empty(((nu + 1) // 2) * nu, dtype=torch.int64, device="cuda")
+        bf = torch.empty(((nu + 1) // 2) * nu, dtype=torch.float32, device="cuda")
+        for N in (int(x) for x in a.rank_blocks.split(",") if x):
+            per = (nu + N - 1) // N
+            ts = []
+            for r in range(N):
+                b0, b1 = min(r * per, nu), min((r + 1) * per, nu)
+
+                def one(b0=b0, b1=b1):
+                    fresh = NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
+                    fresh.build_rows_device(used, b0, b1, bl.data_ptr(), bf.data_ptr(), True)
+                    fresh.close()
+                ts.append(timed(D, one, 3, 1))
+            rank_blocks[str(N)] = {"rows_per_rank": per, "max_ms": round(max(ts) * 1e3, 4),
+                                   "per_rank_ms": [round(t * 1e3, 4) for t in ts],
+                                   "linear_ms": round(t_build / N * 1e3, 4),
+                                   "frac_of_linear": round(t_build / N / max(ts), 3)}
+        del bl, bf
     # instrumented build on the kernel's own stream: HIP-event launch times, then
     # (separately, the counting variant is slower) the relaxations performed
     ctx.enable_timers(True)
@@ -765,6 +792,7 @@ def main():
                         "out_kernel_ms": round(timers["out"][0], 4),
                         "wide_rows_ms": round(timers["relax_wide"][0], 4),
                         "allgather_ms": round(t_allgather * 1e3, 4),
+                        "rank_block_ms": rank_blocks,
                         "table_bytes": 12 * nu * nu,
                         "end_to_end": e2e,
                         "cpu_baseline_faithful": cpu_faithful},

@@ -55,7 +55,9 @@ namespace sg {
 
 constexpr uint32_t NONE = ~0u;
 constexpr int SMALL_BUCKET = 32;
-constexpr uint32_t INBLOCK_RANK_MAX = 256;  // region path: rank sort up to this many entries per slot
+constexpr uint32_t INBLOCK_RANK_SMALL = 32;  // region path: rank sort up to this many entries per slot,
+constexpr uint32_t WAVE_SORT_MAX = 256;      // in-wave bitonic sort up to this many, the block's beyond
+// (up to 4 keys per lane: 8 took the region sort to 256 VGPRs, one block per CU)
 constexpr int SORT_BLOCK = 256;
 constexpr int SORT_CHUNK = 2048;  // elements sorted in LDS per chunk
 
@@ -1069,6 +1071,98 @@ __device__ __forceinline__ void slot_bitonic(const uint64_t* Tt, const uint64_t*
   __syncthreads();
 }
 
+// In-wave bitonic sort of one slot's m entries [b, b + m) (m <= 64 R),
+// keys in registers: lane l holds elements l, l + 64, ..., l + 64 (R - 1); the
+// network's exchanges at distance < 64 are lane shuffles, at 64 and above register
+// swaps in the lane.  CK: one compressed u64 key per entry ((t - t_min) << 32 |
+// value, unique), the value is its low word.  Else (t, k) pairs and the value
+// ride along (k = the record's order key, or the value itself).  Pads (~0) sort
+// last: every real key is below ~0 (arrival times stop at EMUTIME_MAX).  No
+// barrier: one wave sorts a slot while the block's other waves sort others, where
+// the rank sort cost m LDS reads per entry (C5: ~100-entry slots, the round's
+// second-largest cost) and the block-wide bitonic a barrier per step.
+template <int R, bool KK, bool CK>
+__device__ __forceinline__ void wave_sort_slot(const uint64_t* Tt, const uint64_t* Tk, const uint32_t* Ti, uint32_t b,
+                                               uint32_t m, uint32_t* __restrict__ out) {
+  constexpr uint32_t M = 64u * R;
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t t[R], k[R];
+  uint32_t v[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const uint32_t i = lane + 64u * r;
+    const bool ok = i < m;
+    const uint32_t p = b + (ok ? i : 0u);  // branch-free reads; pads replace the value
+    const uint64_t tt = Tt[p];
+    const uint32_t vv = Ti[p];
+    t[r] = ok ? tt : ~0ull;
+    v[r] = vv;
+    if constexpr (!CK) {
+      const uint64_t kk = KK ? Tk[p] : (uint64_t)vv;
+      k[r] = ok ? kk : ~0ull;
+    }
+  }
+  auto less = [&](uint64_t ta, uint64_t ka, uint64_t tb, uint64_t kb) {
+    if constexpr (CK) return ta < tb;
+    else return ta < tb || (ta == tb && ka < kb);
+  };
+#pragma unroll
+  for (uint32_t kk2 = 2; kk2 <= M; kk2 <<= 1) {
+#pragma unroll
+    for (uint32_t j = kk2 >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {  // partner in this lane's register r ^ (j / 64)
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const int r2 = r ^ (int)(j >> 6);
+          if (r2 <= r) continue;
+          const bool asc = ((lane + 64u * r) & kk2) == 0;
+          const bool lt21 = less(t[r2], CK ? 0 : k[r2], t[r], CK ? 0 : k[r]);
+          const bool lt12 = less(t[r], CK ? 0 : k[r], t[r2], CK ? 0 : k[r2]);
+          if (asc ? lt21 : lt12) {
+            const uint64_t xt = t[r];
+            t[r] = t[r2];
+            t[r2] = xt;
+            if constexpr (!CK) {
+              const uint64_t xk = k[r];
+              k[r] = k[r2];
+              k[r2] = xk;
+              const uint32_t xv = v[r];
+              v[r] = v[r2];
+              v[r2] = xv;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const uint32_t i = lane + 64u * r;
+          const uint64_t ot = __shfl_xor((unsigned long long)t[r], (int)j, 64);
+          uint64_t ok = 0;
+          uint32_t ov = 0;
+          if constexpr (!CK) {
+            ok = __shfl_xor((unsigned long long)k[r], (int)j, 64);
+            ov = __shfl_xor(v[r], (int)j, 64);
+          }
+          const bool want_min = ((i & j) == 0) == ((i & kk2) == 0);
+          const bool o_lt = less(ot, ok, t[r], CK ? 0 : k[r]);
+          if (want_min == o_lt) {  // take the partner's element (equal keys: pads, identical)
+            t[r] = ot;
+            if constexpr (!CK) {
+              k[r] = ok;
+              v[r] = ov;
+            }
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const uint32_t i = lane + 64u * r;
+    if (i < m) out[i] = CK ? (uint32_t)t[r] : v[r];
+  }
+}
+
 // Per-slot order of a placed super-bucket (slot j = entries [cnt[j], cnt[j+1])
 // of Tt/Tk/Ti, Ts = slot per entry): rank sort of small slots; slots above
 // SMALL_BUCKET go to k_sort_big (copied to the global kt/kk/ki when placed in
@@ -1087,17 +1181,27 @@ __device__ __forceinline__ void slot_orders(uint64_t* Tt, uint64_t* Tk, uint32_t
   // a slot's rank sort runs in parallel with every other slot's, where each
   // bitonic slot takes the whole block through log2(m)^2 / 2 barriers in turn
   // (C5: about 100 entries per destination, 1.9 ms of bitonic slots per round).
-  constexpr uint32_t SMALL = INBLOCK ? INBLOCK_RANK_MAX : SMALL_BUCKET;
-  constexpr uint32_t MAX_BIG = SB_CAP<KK> / (SMALL + 1) + 1;
-  __shared__ uint32_t n_big;
+  // In-block: slots up to INBLOCK_RANK_SMALL entries are rank-sorted, up to
+  // WAVE_SORT_MAX sorted by one wave each in registers, larger ones by the block.
+  constexpr uint32_t SMALL = INBLOCK ? INBLOCK_RANK_SMALL : SMALL_BUCKET;
+  constexpr uint32_t MAX_BIG = SB_CAP<KK> / (WAVE_SORT_MAX + 1) + 1;
+  constexpr uint32_t MAX_WAVE = SB_CAP<KK> / (SMALL + 1) + 1;
+  __shared__ uint32_t n_big, n_wave;
   __shared__ uint16_t bigs[INBLOCK ? MAX_BIG : 1];
-  if (INBLOCK && threadIdx.x == 0) n_big = 0;
+  __shared__ uint16_t wslots[INBLOCK ? MAX_WAVE : 1];
+  if (INBLOCK && threadIdx.x == 0) {
+    n_big = 0;
+    n_wave = 0;
+  }
   __syncthreads();  // placement complete
   for (uint32_t j = threadIdx.x; j < nd; j += SBT_THREADS) {
     const uint32_t b = cnt[j], e = cnt[j + 1];
     if (e - b > SMALL) {
       if (INBLOCK) {
-        bigs[atomicAdd(&n_big, 1u)] = (uint16_t)j;
+        if (e - b > WAVE_SORT_MAX)
+          bigs[atomicAdd(&n_big, 1u)] = (uint16_t)j;
+        else
+          wslots[atomicAdd(&n_wave, 1u)] = (uint16_t)j;
         continue;
       }
       big_list[atomicAdd(big_count, 1u)] = d0 + j;
@@ -1145,6 +1249,19 @@ __device__ __forceinline__ void slot_orders(uint64_t* Tt, uint64_t* Tk, uint32_t
       for (; q < e; q++) rank += key_less(Tt[q], KK ? Tk[q] : (uint64_t)Ti[q], t, k);
     }
     order[s0 + b + rank] = Ti[p];
+  }
+  if constexpr (INBLOCK) {
+    __syncthreads();  // n_wave is final (it was before the rank sort too; this orders the reads)
+    for (uint32_t u = threadIdx.x >> 6; u < n_wave; u += SBT_THREADS / 64) {  // one wave per slot
+      const uint32_t j = wslots[u], b = cnt[j], m = cnt[j + 1] - b;
+      uint32_t* o = order + s0 + b;
+      if (m <= 64)
+        wave_sort_slot<1, KK, CK>(Tt, Tk, Ti, b, m, o);
+      else if (m <= 128)
+        wave_sort_slot<2, KK, CK>(Tt, Tk, Ti, b, m, o);
+      else
+        wave_sort_slot<4, KK, CK>(Tt, Tk, Ti, b, m, o);
+    }
   }
   if (INBLOCK) {
     __syncthreads();  // Ts is free: it becomes the index array

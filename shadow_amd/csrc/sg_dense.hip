@@ -1,0 +1,276 @@
+// sg_dense.hip -- per-source shortest paths on dense graphs (C2: the 1,200-node
+// complete graph of docs/network_graph_overview.md:58-63).
+//
+// Replaces, for graphs of at most DENSE_MAX nodes whose mean out-degree is past
+// the sparse searches' range, the per-source petgraph::algo::dijkstra of
+// NetworkGraph::compute_shortest_paths (graph/mod.rs:190-208).
+//
+// One workgroup per source row, its keys in LDS.  The search settles nodes in
+// rounds (Dijkstra with a width) and relaxes only the arcs that can still matter:
+//
+//  * Settling.  A round takes m = the smallest latency of the unsettled keys and
+//    settles every unsettled v with key(v).lat < m + w_min (w_min = the smallest
+//    arc latency, >= 1 ns by graph/mod.rs:105-107).  Such a key is final: any
+//    other path to v leaves the settled set through an unsettled node x, so its
+//    latency is at least key(x).lat + w_min >= m + w_min > key(v).lat -- larger
+//    in the PathProperties order (latency first, graph/mod.rs:305-313).
+//  * Pruning.  The round also takes T = the largest latency of the unsettled
+//    keys (LAT32_SAT while any is unreached).  Keys only fall during the round, so
+//    a candidate with latency > T improves no unsettled key, and no settled one
+//    (those are below every later candidate).  Each node's out-arcs are sorted by
+//    latency once per build (k_sort_arcs), so a settled row u is relaxed only up
+//    to its first arc with key(u).lat + w > T.  On a complete graph with random
+//    latencies that is a few percent of the row: Dijkstra's n^2 arc reads per
+//    source shrink to the short arcs, which every source shares (they stay in L2).
+//
+// Relaxation is the 64-bit LDS atomic min of sg_sssp.hip on the packed key
+// (latency << 32 | bits(loss)), whose integer order is the PathProperties order;
+// the fold applies the edge on the right (sg_device.h relax32), so the result is
+// the fixed point petgraph's Dijkstra returns (sg_sssp.hip header).  Parallel
+// arcs need no merging: the worse one's candidate loses its atomic min.
+//
+// Keys saturate at LAT32_SAT like every 32-bit kernel: a saturated candidate is
+// never offered, and a row with a saturated (unreachable or >= 4.29 s) key is
+// flagged for the wide kernel (sg_routing.hip run_wide).
+#include <algorithm>
+
+#include "sg_device.h"
+#include "sg_internal.h"
+
+namespace sg {
+
+constexpr int DENSE_THREADS = 1024;
+constexpr int DENSE_WAVES = DENSE_THREADS / 64;
+constexpr uint32_t DENSE_SCAP = 512;    // nodes settled per round at most (the rest wait a round)
+constexpr uint32_t SORT_MAXDEG = 4096;  // out-degree sorted in one block's LDS; larger rows stay unsorted
+constexpr int DENSE_G = 2;              // settled rows a wave relaxes together (their loads in flight)
+
+// Per node u: its out-arcs (out_arc, 3 u32 each: head, latency32, bits(1f32 - loss))
+// sorted by latency into 16-B records {head, latency32, bits(om), 0} at the same
+// offsets; sorted[u] = 1, or 0 for a row past SORT_MAXDEG (copied as is, never cut
+// short).  Also the smallest arc latency (w_min).  One block per node.
+__global__ void __launch_bounds__(256) k_sort_arcs(const uint32_t* __restrict__ out_off,
+                                                   const uint32_t* __restrict__ out_arc, uint32_t n,
+                                                   uint4* __restrict__ sa, uint8_t* __restrict__ sorted,
+                                                   uint32_t* __restrict__ wmin) {
+  __shared__ unsigned long long k[SORT_MAXDEG];
+  __shared__ uint32_t s_lo[4];
+  const uint32_t u = blockIdx.x, t = threadIdx.x;
+  const uint32_t a0 = out_off[u], deg = out_off[u + 1] - a0;
+  uint32_t lo = LAT32_SAT;
+  if (deg > SORT_MAXDEG) {
+    for (uint32_t i = t; i < deg; i += 256) {
+      const uint32_t* r = out_arc + 3 * (size_t)(a0 + i);
+      sa[a0 + i] = make_uint4(r[0], r[1], r[2], 0u);
+      lo = min(lo, r[1]);
+    }
+    if (t == 0) sorted[u] = 0;
+  } else {
+    uint32_t M = 1;
+    while (M < deg) M <<= 1;
+    for (uint32_t i = t; i < M; i += 256) {
+      const uint32_t l = i < deg ? out_arc[3 * (size_t)(a0 + i) + 1] : LAT32_SAT;
+      k[i] = i < deg ? ((unsigned long long)l << 32) | i : ~0ull;
+      lo = min(lo, l);
+    }
+    __syncthreads();
+    for (uint32_t kk = 2; kk <= M; kk <<= 1)
+      for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+        for (uint32_t i = t; i < M; i += 256) {
+          const uint32_t l = i ^ j;
+          if (l > i) {
+            const unsigned long long x = k[i], y = k[l];
+            if ((y < x) == ((i & kk) == 0)) {
+              k[i] = y;
+              k[l] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    for (uint32_t i = t; i < deg; i += 256) {
+      const uint32_t* r = out_arc + 3 * (size_t)(a0 + (uint32_t)(k[i] & 0xFFFFFFFFu));
+      sa[a0 + i] = make_uint4(r[0], r[1], r[2], 0u);
+    }
+    if (t == 0) sorted[u] = 1;
+  }
+  for (int d = 32; d > 0; d >>= 1) lo = min(lo, (uint32_t)__shfl_xor(lo, d, 64));
+  if ((t & 63) == 0) s_lo[t >> 6] = lo;
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t m = min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3]));
+    if (m != LAT32_SAT) atomicMin(wmin, m);
+  }
+}
+
+__global__ void __launch_bounds__(DENSE_THREADS) k_sssp_dense(const uint32_t* __restrict__ out_off,
+                                                              const uint4* __restrict__ sa,
+                                                              const uint8_t* __restrict__ sorted, uint32_t n,
+                                                              uint32_t n_arcs, const uint32_t* __restrict__ wmin_p,
+                                                              const uint32_t* __restrict__ used, uint32_t n_used,
+                                                              uint32_t row_begin, const uint32_t* __restrict__ self_edge,
+                                                              const uint64_t* __restrict__ e_lat,
+                                                              const float* __restrict__ e_loss,
+                                                              uint64_t* __restrict__ out_lat,
+                                                              float* __restrict__ out_loss,
+                                                              uint32_t* __restrict__ sat_row,
+                                                              unsigned long long* __restrict__ work) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  unsigned long long* key = (unsigned long long*)smem;        // [n]
+  uint32_t* settled = (uint32_t*)(key + n);                   // [ceil(n / 32)] bitmap
+  const uint32_t nbw = (n + 31) / 32;
+  uint32_t* s_node = settled + ((nbw + 1) & ~1u);             // [DENSE_SCAP] this round's settled nodes
+  __shared__ uint32_t s_cnt;
+  __shared__ uint32_t red_m[DENSE_WAVES], red_t[DENSE_WAVES];
+  __shared__ uint32_t s_m, s_t;
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t row = row_begin + blockIdx.x;
+  const uint32_t src = used[row];
+  const uint32_t wmin = *wmin_p;  // >= 1 (graph/mod.rs:105-107); LAT32_SAT: no arc at all
+  for (uint32_t v = t; v < n; v += DENSE_THREADS) key[v] = v == src ? 0ull : KEY_INF;  // default() at the source
+  for (uint32_t i = t; i < nbw; i += DENSE_THREADS) settled[i] = 0u;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)sa, 0, (int)0x7FFFFFFF, 0x00020000);
+  unsigned long long n_rel = 0;
+  __syncthreads();
+  for (;;) {
+    // the smallest and largest latency of the unsettled keys
+    uint32_t m = LAT32_SAT, T = 0;
+    for (uint32_t v = t; v < n; v += DENSE_THREADS) {
+      if (settled[v >> 5] >> (v & 31) & 1u) continue;
+      const uint32_t l = key_lat(key[v]);
+      m = min(m, l);
+      T = max(T, l);
+    }
+    for (int d = 32; d > 0; d >>= 1) {
+      m = min(m, (uint32_t)__shfl_xor(m, d, 64));
+      T = max(T, (uint32_t)__shfl_xor(T, d, 64));
+    }
+    if (lane == 0) {
+      red_m[wv] = m;
+      red_t[wv] = T;
+    }
+    __syncthreads();
+    if (t == 0) {
+      uint32_t mm = LAT32_SAT, tt = 0;
+      for (int k = 0; k < DENSE_WAVES; k++) {
+        mm = min(mm, red_m[k]);
+        tt = max(tt, red_t[k]);
+      }
+      s_m = mm;
+      s_t = tt;
+      s_cnt = 0;
+    }
+    __syncthreads();
+    m = s_m;
+    T = s_t;
+    if (m == LAT32_SAT) break;  // every key settled, or saturated (unreachable in 32 bits: the wide kernel)
+    const uint32_t thr = m + wmin >= m ? m + wmin : LAT32_SAT;  // settle key.lat < thr
+    for (uint32_t v0 = wv * 64; v0 < n; v0 += DENSE_THREADS) {
+      const uint32_t v = v0 + lane;
+      const bool s = v < n && !(settled[v >> 5] >> (v & 31) & 1u) && key_lat(key[v]) < thr;
+      const uint64_t bal = __ballot(s);
+      if (!bal) continue;
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&s_cnt, (uint32_t)__popcll(bal));
+      base = __builtin_amdgcn_readfirstlane(base);
+      const uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+      if (s && pos < DENSE_SCAP) {  // past the cap a node waits a round (it stays below the threshold)
+        s_node[pos] = v;
+        atomicOr(&settled[v >> 5], 1u << (v & 31));
+      }
+    }
+    __syncthreads();
+    const uint32_t ns = min(s_cnt, DENSE_SCAP);
+    // Relax: a wave takes DENSE_G settled rows at a time, 64 arcs per row and step, and
+    // stops a row at its first arc past T (rows sorted by latency); keys are final for
+    // the settled rows (their (lat, loss) read once here, unchanged during the round)
+    for (uint32_t s0 = wv * DENSE_G; s0 < ns; s0 += DENSE_WAVES * DENSE_G) {
+      uint32_t a[DENSE_G], e[DENSE_G];
+      uint64_t ku[DENSE_G];
+      bool cut[DENSE_G];
+#pragma unroll
+      for (int g = 0; g < DENSE_G; g++) {
+        const bool ok = s0 + g < ns;
+        const uint32_t u = ok ? s_node[s0 + g] : 0u;
+        a[g] = ok ? out_off[u] : 0u;
+        e[g] = ok ? out_off[u + 1] : 0u;
+        ku[g] = ok ? key[u] : KEY_INF;
+        cut[g] = ok && sorted[u];
+      }
+      // the latency budget of row g's arcs: key(u).lat + w <= T
+      uint32_t budget[DENSE_G];
+#pragma unroll
+      for (int g = 0; g < DENSE_G; g++) budget[g] = T - min(T, key_lat(ku[g]));
+      bool live = true;
+      while (live) {
+        uint4 r[DENSE_G];
+#pragma unroll
+        for (int g = 0; g < DENSE_G; g++) {
+          const uint32_t i = a[g] + lane;
+          const auto x = __builtin_amdgcn_raw_buffer_load_b128(ra, i < e[g] ? i * 16u : 0x80000000u, 0, 0);
+          r[g] = make_uint4(x[0], x[1], x[2], x[3]);
+        }
+        live = false;
+#pragma unroll
+        for (int g = 0; g < DENSE_G; g++) {
+          const uint32_t i = a[g] + lane;
+          const bool in = i < e[g] && (!cut[g] || r[g].y <= budget[g]);
+          const uint64_t cd = relax32(ku[g], r[g].y, __uint_as_float(r[g].z));
+          const bool offer = in && key_lat(cd) != LAT32_SAT && !(settled[r[g].x >> 5] >> (r[g].x & 31) & 1u);
+          if (offer) (void)__hip_atomic_fetch_min(&key[r[g].x], (unsigned long long)cd, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (work) n_rel += __popcll(__ballot(in));
+          // the row goes on while its last lane's arc is in range and within the budget
+          const bool more = __builtin_amdgcn_readlane((int)in, 63) != 0 && a[g] + 64 < e[g];
+          a[g] = more ? a[g] + 64 : e[g];
+          live |= more;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (work && lane == 0 && n_rel) atomicAdd(&work[blockIdx.x & 63], n_rel);
+  // ---- write the row: columns in used order, diagonal = the raw self-loop (graph/mod.rs:210-217)
+  bool sat = false;
+  const size_t orow = (size_t)blockIdx.x * n_used;
+  const uint32_t de = self_edge[src];
+  for (uint32_t jj = t; jj < n_used; jj += DENSE_THREADS) {
+    const uint32_t v = used[jj];
+    const unsigned long long k = key[v];
+    const bool diag = jj == row;
+    sat |= !diag && key_lat(k) == LAT32_SAT;
+    out_lat[orow + jj] = diag ? e_lat[de] : (uint64_t)key_lat(k);
+    out_loss[orow + jj] = diag ? e_loss[de] : __uint_as_float(key_loss_bits(k));
+  }
+  if (__any(sat) && lane == 0) sat_row[blockIdx.x] = 1u;
+}
+
+bool sssp_dense_fits(uint32_t n) { return n > 0 && n <= DENSE_MAX; }
+
+void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin,
+                       uint32_t row_end, uint64_t* out_lat, float* out_loss, uint32_t* sat_row,
+                       unsigned long long* work) {
+  const uint32_t n = net->n_nodes, rows = row_end - row_begin;
+  if (!sssp_dense_fits(n)) throw Error(SG_ERR_INVALID_ARG, "graph too large for the dense search");
+  if ((uint64_t)net->n_arcs * 16 >= (1ull << 31)) throw Error(SG_ERR_INVALID_ARG, "too many arcs for the dense search");
+  hipStream_t st = ctx->stream;
+  // workspace: sorted arcs (16 B each), per-node sorted flag, w_min
+  uint4* sa = ctx->r_dense.get<uint4>((size_t)net->n_arcs + 1 + (n + 15) / 16);
+  uint32_t* wmin = (uint32_t*)(sa + net->n_arcs);
+  uint8_t* sorted = (uint8_t*)(sa + net->n_arcs + 1);
+  {
+    TimedLaunch tl(ctx, "dense_sort", 24.0 * net->n_arcs);
+    SG_HIP(hipMemsetAsync(wmin, 0xFF, 4, st));
+    hipLaunchKernelGGL(k_sort_arcs, dim3(n), dim3(256), 0, st, net->out_off, net->out_arc, n, sa, sorted, wmin);
+  }
+  if (!rows) return;
+  const uint32_t nbw = (n + 31) / 32;
+  const size_t lds = (size_t)n * 8 + (size_t)((nbw + 1) & ~1u) * 4 + DENSE_SCAP * 4;
+  TimedLaunch tl(ctx, "sssp_dense", 0.0);
+  hipLaunchKernelGGL(k_sssp_dense, dim3(rows), dim3(DENSE_THREADS), lds, st, net->out_off, (const uint4*)sa,
+                     (const uint8_t*)sorted, n, net->n_arcs, (const uint32_t*)wmin, d_used, n_used, row_begin,
+                     net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat_row, work);
+  SG_CHECK_LAUNCH();
+}
+
+}  // namespace sg

@@ -98,7 +98,7 @@ struct sg_ctx {
   // routing workspace
   sg::DevBuf r_team_arc, r_team_mid, r_team_pair, r_team_box, r_team_ctl, r_team_used;  // sg_team.hip
   sg::DevBuf r_dist, r_dist2, r_flags, r_used, r_err, r_self, r_pair_cnt, r_pair_edge, r_map, r_out_lat,
-      r_out_loss, r_misc, r_dirty, r_work, r_items, r_plan;
+      r_out_loss, r_misc, r_dirty, r_work, r_items, r_plan, r_dense, r_done;
   // delivery workspace
   sg::DevBuf d_seg, d_dst, d_cnt, d_cur, d_keys, d_vals, d_keys2, d_vals2, d_keys3, d_keys4, d_misc,
       d_scan, d_lists, d_lists2, d_ctr0, d_blk, d_spill;
@@ -304,6 +304,17 @@ struct TimedLaunch {
 // used node) also seeds exact keys (w + D[s'][v].lat, D[s'][v].loss); see
 // sg_sssp.hip "Exact seeds".  The bound rows must be final before the launch
 // (an earlier launch on the stream).
+// Per-source search of dense graphs, settling by rounds and relaxing only the arcs
+// below the round's largest unsettled latency (sg_dense.hip): rows [row_begin,
+// row_end); sat_row (zeroed by the caller) receives 1 for rows needing the wide
+// kernel.  Sorts every node's out-arcs by latency on the stream first.  work
+// (optional, WORK_SHARDS counters): arcs relaxed.
+constexpr uint32_t DENSE_MAX = 4096;
+bool sssp_dense_fits(uint32_t n_nodes);
+void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin,
+                       uint32_t row_end, uint64_t* out_lat, float* out_loss, uint32_t* sat_row,
+                       unsigned long long* work);
+
 constexpr int SSSP_KB_MAX = 8;
 constexpr uint32_t SSSP_UB_EXACT = 0x80000000u;  // bound rows per bounded search (sg_sssp.hip SSSP_KB)
 bool sssp_lds_fits(uint32_t n_nodes);
@@ -319,7 +330,8 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
                      float* out_loss, uint32_t* sat_row, uint32_t delta, unsigned long long* work,
                      unsigned long long* diag, const uint32_t* blk_rows = nullptr, uint32_t n_blk = 0,
                      const uint32_t* ub_row = nullptr, const uint32_t* ub_w = nullptr,
-                     const uint32_t* plan_ctl = nullptr, int plan_ph = 0, uint32_t* plan_ctr = nullptr);
+                     const uint32_t* plan_ctl = nullptr, int plan_ph = 0, uint32_t* plan_ctr = nullptr,
+                     uint32_t* done = nullptr);
 
 // The LDS search's phase plan, built on the device (sg_plan.hip) on the context
 // stream: phase p's rows are list[ctl[2p] .. + ctl[2p + 1]) (absolute row indices),
@@ -338,7 +350,7 @@ struct SsspDevPlan {
 constexpr int SSSP_PHASES_MAX = 6;
 SsspDevPlan sssp_device_plan(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin,
                              uint32_t row_end, int n_phase, int kb, bool exact, int hops, uint32_t n_land,
-                             uint32_t* zero_rows = nullptr);
+                             uint32_t* zero_rows = nullptr, uint32_t* zero_rows2 = nullptr);
 // After phase 0 (the landmarks) ran: phase 1's bound rows from the landmark rows' columns.
 void sssp_landmark_bounds(sg_ctx* ctx, const SsspDevPlan& p, uint32_t n_used, uint32_t row_begin,
                           const uint64_t* out_lat, const uint32_t* sat_row, int kb);

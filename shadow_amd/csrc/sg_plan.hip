@@ -49,12 +49,14 @@ namespace sg {
 // rel[used row] = its relative row; also zeroes jn (and the caller's per-row flags):
 // no fills on the build's path
 __global__ void k_plan_rel(const uint32_t* __restrict__ used, uint32_t row_begin, uint32_t rows,
-                           uint32_t* __restrict__ rel, uint8_t* __restrict__ jn, uint32_t* __restrict__ zero_rows) {
+                           uint32_t* __restrict__ rel, uint8_t* __restrict__ jn, uint32_t* __restrict__ zero_rows,
+                           uint32_t* __restrict__ zero_rows2) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= rows) return;
   rel[used[row_begin + r]] = r;
   jn[r] = 0;
   if (zero_rows) zero_rows[r] = 0;
+  if (zero_rows2) zero_rows2[r] = 0;
 }
 
 // jn[r]: 0 while row r is in no phase, else its phase + 1 (set once).  Gain of an
@@ -483,7 +485,7 @@ __global__ void __launch_bounds__(PB_WAVES * 64)
 
 SsspDevPlan sssp_device_plan(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin,
                              uint32_t row_end, int n_phase, int kb, bool exact, int hops, uint32_t n_land,
-                             uint32_t* zero_rows) {
+                             uint32_t* zero_rows, uint32_t* zero_rows2) {
   (void)n_used;
   const uint32_t n = net->n_nodes, rows = row_end - row_begin;
   n_phase = std::max(2, std::min(SSSP_PHASES_MAX - (n_land ? 1 : 0), n_phase));
@@ -508,7 +510,7 @@ SsspDevPlan sssp_device_plan(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
     TimedLaunch tl(ctx, "plan_sets", 0.0);
     SG_HIP(hipMemsetAsync(rel, 0xff, (size_t)n * 4, st));
     const unsigned g = grid_for(rows, 256);
-    hipLaunchKernelGGL(k_plan_rel, dim3(g), dim3(256), 0, st, d_used, row_begin, rows, rel, jn, zero_rows);
+    hipLaunchKernelGGL(k_plan_rel, dim3(g), dim3(256), 0, st, d_used, row_begin, rows, rel, jn, zero_rows, zero_rows2);
     // in-neighbours: the CSC when directed; the out-arcs themselves when undirected
     const uint32_t* in_off = net->directed ? net->in_off : net->out_off;
     const uint32_t* in_idx = net->directed ? net->in_src : net->out_arc;

@@ -1518,6 +1518,51 @@ static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 // taken from neighbour rows of earlier phases; each phase is one launch, so a
 // kernel boundary publishes the rows the next phase reads.  The plan is built on
 // the device for every build (sg_plan.hip), so a one-shot build pays it.
+// The build's end: the flagged rows' count and the self-loop check in one kernel,
+// one synchronisation; the flags themselves are copied only when some row was
+// flagged.  Returns the rows (absolute) that need the wide kernel.
+static std::vector<uint32_t> finish_rows(sg_ctx* ctx, const uint32_t* sat, uint32_t row_begin, uint32_t rows) {
+  hipStream_t st = ctx->stream;
+  hipLaunchKernelGGL(k_build_finish, dim3(1), dim3(1024), 0, st, sat, rows, ctx->self_used, ctx->self_n,
+                     ctx->self_cnt, ctx->apsp_ret);
+  SG_CHECK_LAUNCH();
+  SG_HIP(hipStreamSynchronize(st));
+  const volatile uint32_t* ret = ctx->apsp_ret;
+  const uint32_t n_flag = ret[4];
+  if (ctx->self_used) {
+    ctx->self_first = *(const volatile unsigned long long*)(ret + 2);
+    ctx->self_done = true;
+  }
+  std::vector<uint32_t> wide_rows;
+  if (n_flag) {
+    std::vector<uint32_t> h_sat(rows);
+    copy_to_host(ctx, h_sat.data(), sat, rows * 4ull);
+    for (uint32_t r = 0; r < rows; r++)
+      if (h_sat[r]) wide_rows.push_back(row_begin + r);
+  }
+  return wide_rows;
+}
+
+// Dense graphs (sg_dense.hip): one register-resident search per row, no plan.
+static void shortest_paths_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
+                                 uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
+  const uint32_t rows = row_end - row_begin;
+  uint32_t* sat = ctx->r_flags.get<uint32_t>(std::max(rows, 1u));
+  SG_HIP(hipMemsetAsync(sat, 0, std::max(rows, 1u) * 4ull, ctx->stream));
+  unsigned long long* work = ctx->count_work ? ctx->r_work.get<unsigned long long>(WORK_SHARDS) : nullptr;
+  if (work) SG_HIP(hipMemsetAsync(work, 0, WORK_SHARDS * 8, ctx->stream));
+  launch_sssp_dense(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss, sat, work);
+  std::vector<uint32_t> wide_rows = finish_rows(ctx, sat, row_begin, rows);
+  if (work) {
+    unsigned long long w[WORK_SHARDS];
+    copy_to_host(ctx, w, work, sizeof(w));
+    double total = 0;
+    for (int k = 0; k < WORK_SHARDS; k++) total += (double)w[k];
+    timer_add_work(ctx, "sssp_dense", total);
+  }
+  if (!wide_rows.empty()) run_wide(ctx, net, d_used, n_used, wide_rows, row_begin, out_lat, out_loss);
+}
+
 static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
                                float* out_loss) {
   hipStream_t st = ctx->stream;
@@ -1538,9 +1583,27 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   // 0.76 ms unbounded, a 2,000-node build 0.45 against 0.43; 2,500 rows 1.30
   // against 1.38, a 4,000-node build 0.97 against 1.07).  SG_SSSP_SEEDS=0 never, =2 always.
   const int seeds_env = env_int("SG_SSSP_SEEDS", 1);
-  const bool phased = seeds_env != 0 && (seeds_env == 2 || rows >= 8u * (uint32_t)ctx->n_cu);
-  if (!phased) SG_HIP(hipMemsetAsync(sat, 0, rows * 4ull, st));
-  if (phased) {
+  // Flagged rows (SG_SSSP_FLAGGED=1; sg_sssp.hip): the plan's rows in ONE launch, in phase
+  // order, each row taking the bound rows already published when it starts -- no phase
+  // boundaries, so the bounds pay even with few rows per CU (a rank's row block)
+  const int flag_env = env_int("SG_SSSP_FLAGGED", 0);
+  const bool flagged = seeds_env != 0 && flag_env == 1;
+  const bool phased = !flagged && seeds_env != 0 && (seeds_env == 2 || rows >= 8u * (uint32_t)ctx->n_cu);
+  if (!phased && !flagged) SG_HIP(hipMemsetAsync(sat, 0, rows * 4ull, st));
+  if (flagged) {
+    const uint32_t per_cu = rows / std::max(1, ctx->n_cu);
+    const int n_phase = std::max(2, std::min(SSSP_PHASES_MAX, env_int("SG_SSSP_PHASES", per_cu >= 16 ? 3 : 2)));
+    const int kb = std::max(1, std::min(SSSP_KB_MAX, env_int("SG_SSSP_BOUNDS", 2)));
+    const bool exact = env_int("SG_SSSP_EXACT", 1) != 0 && n_used == net->n_nodes;
+    const int hops = std::max(1, std::min(env_int("SG_SSSP_HOPS", 3), 3));
+    uint32_t* done = ctx->r_done.get<uint32_t>(std::max(rows, 1u));
+    const SsspDevPlan plan =
+        sssp_device_plan(ctx, net, d_used, n_used, row_begin, row_end, n_phase, kb, exact, hops, 0u, sat, done);
+    TimedLaunch tl(ctx, "sssp", 0.0);
+    launch_sssp_lds(ctx, net->out_off, net->out_arc, net->n_nodes, net->n_arcs, d_used, n_used, row_begin, row_end,
+                    net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work, diag, plan.list, rows,
+                    plan.ub_row, plan.ub_w, nullptr, 0, plan.ctr, done);
+  } else if (phased) {
     // phases by rows per CU (one box, tools/sssp_ab.py --rows, C3 graph): 39 rows per CU
     // (10k rows) 4 phases; 19.5 (a half) 3 phases, 2.25 against 2.57 ms unbounded;
     // 9.8 (a quarter) 2 phases, 1.30 against 1.38 ms
@@ -1610,25 +1673,7 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
             "%.0f relaxations (%.2f x arcs)\n", delta, n_diag, a[0] / n_diag, a[1] / n_diag, a[2] / n_diag,
             a[3] / n_diag, a[4] / n_diag, a[4] / n_diag / std::max(1u, net->n_arcs));
   }
-  // the flagged rows' count and the self-loop check in one kernel, one synchronisation;
-  // the flags themselves are copied only when some row was flagged
-  hipLaunchKernelGGL(k_build_finish, dim3(1), dim3(1024), 0, st, sat, rows, ctx->self_used, ctx->self_n,
-                     ctx->self_cnt, ctx->apsp_ret);
-  SG_CHECK_LAUNCH();
-  SG_HIP(hipStreamSynchronize(st));
-  const volatile uint32_t* ret = ctx->apsp_ret;
-  const uint32_t n_flag = ret[4];
-  if (ctx->self_used) {
-    ctx->self_first = *(const volatile unsigned long long*)(ret + 2);
-    ctx->self_done = true;
-  }
-  std::vector<uint32_t> wide_rows;
-  if (n_flag) {
-    std::vector<uint32_t> h_sat(rows);
-    copy_to_host(ctx, h_sat.data(), sat, rows * 4ull);
-    for (uint32_t r = 0; r < rows; r++)
-      if (h_sat[r]) wide_rows.push_back(row_begin + r);
-  }
+  std::vector<uint32_t> wide_rows = finish_rows(ctx, sat, row_begin, rows);
   if (work) {
     unsigned long long w[WORK_SHARDS];
     copy_to_host(ctx, w, work, sizeof(w));
@@ -1703,6 +1748,13 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, con
   // each arc record among 64 sources (C2, 1,200-node complete graph: 3.6 ms
   // against 6.8-9.2 ms for the LDS search).
   const bool sparse = net->n_nodes && net->n_arcs <= 64ull * net->n_nodes;
+  // Dense graphs up to DENSE_MAX nodes (C2): the register-resident search of sg_dense.hip,
+  // Dijkstra's n^2 relaxations per row (SG_APSP_DENSE=0 or SG_APSP_LDS=0: the slab kernel).
+  if (env_int("SG_APSP_LDS", 1) != 0 && env_int("SG_APSP_DENSE", 1) != 0 && !sparse &&
+      sssp_dense_fits(net->n_nodes)) {
+    shortest_paths_dense(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss);
+    return;
+  }
   if (env_int("SG_APSP_LDS", 1) != 0 && sparse && sssp_lds_fits(net->n_nodes) &&
       (uint64_t)net->n_arcs * 12 < (1ull << 31)) {
     shortest_paths_lds(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss);

@@ -160,7 +160,11 @@ size_t sssp_lds_bytes(uint32_t n) {
 // bits(1f32 - loss)), grouped by tail node (out_off).
 // PART: 0 for a routing build, 1 for sg_routing_info_fill's row blocks (the same
 // code; a separate symbol so per-kernel profiles do not mix whole builds with blocks)
-template <bool COUNT, int NT, int LA, int PART>
+// FLAG: one launch for the whole plan (rows in phase order), bound rows taken
+// only once published -- see "Flagged rows" below; `done` (per row, zeroed by the
+// plan) is 1 for a final row, 2 for a final row with saturated keys (bounds only).
+constexpr int SSSP_SC1 = 16;  // buffer cache-policy bits: sc1 (gfx950), MI355X_MICROARCH.md's hand-off
+template <bool COUNT, int NT, int LA, int PART, bool FLAG = false>
 __global__ void __launch_bounds__(NT)
     k_sssp_lds(const uint32_t* __restrict__ out_off, const uint32_t* __restrict__ out_arc, uint32_t n,
                uint32_t n_arcs, const uint32_t* __restrict__ used, uint32_t n_used, uint32_t row_begin,
@@ -171,8 +175,9 @@ __global__ void __launch_bounds__(NT)
                uint32_t lane_deg_max, const uint32_t* __restrict__ blk_rows,
                const uint32_t* __restrict__ ub_row, const uint32_t* __restrict__ ub_w,
                uint32_t* __restrict__ item_ctr, uint32_t n_items, uint32_t spin_max,
-               const uint32_t* __restrict__ plan_ctl, int plan_ph) {
+               const uint32_t* __restrict__ plan_ctl, int plan_ph, uint32_t* __restrict__ done) {
   constexpr int NW = NT / 64;
+  constexpr int AUX = FLAG ? SSSP_SC1 : 0;  // bound rows and the output: sc1 in the flagged launch
   if (plan_ctl) {  // a device-built plan (sg_plan.hip): this phase's rows and bound rows, its row count
     const uint32_t base = plan_ctl[2 * plan_ph];
     n_items = plan_ctl[2 * plan_ph + 1];
@@ -198,6 +203,8 @@ __global__ void __launch_bounds__(NT)
   __shared__ unsigned long long sink[64];  // per-lane no-op target of offer_all
   __shared__ uint32_t s_ub[SSSP_KB][3];     // the row's usable bound rows: row, latency, exact
   __shared__ uint32_t s_nub;
+  __shared__ uint32_t s_sat;  // FLAG: a wave saw a saturated key in the row's output
+  if (FLAG && threadIdx.x == 0) s_sat = 0u;
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // Every global read of the setup is a buffer load whose out-of-range lanes read
@@ -256,7 +263,15 @@ __global__ void __launch_bounds__(NT)
       const uint32_t e = tid < SSSP_KB ? ub_row[(size_t)bi * SSSP_KB + tid] : ~0u;
       const uint32_t w = tid < SSSP_KB ? ub_w[(size_t)bi * SSSP_KB + tid] : 0u;
       const uint32_t srow = e & ~SSSP_UB_EXACT;
-      const uint32_t sf = e != ~0u ? sat_row[srow - row_begin] : 2u;
+      uint32_t sf;
+      if constexpr (FLAG) {  // one sc1 poll per bound row, no wait: an unpublished row gives no bounds
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)done, 0, 0x7FFFFFFF, 0x00020000);
+        const uint32_t dn = __builtin_amdgcn_raw_buffer_load_b32(rd, e != ~0u ? (srow - row_begin) * 4u : 0x80000000u,
+                                                                 0, SSSP_SC1);
+        sf = dn == 1u ? 0u : dn == 2u ? 1u : 2u;
+      } else {
+        sf = e != ~0u ? sat_row[srow - row_begin] : 2u;
+      }
       const bool on = sf != 2u;
       const uint64_t mk = __ballot(on);
       if (on) {
@@ -307,9 +322,9 @@ __global__ void __launch_bounds__(NT)
 #pragma unroll
               for (int g = 0; g < G; g++) {
                 const uint32_t j = j0 + g * NT;
-                const auto x = __builtin_amdgcn_raw_buffer_load_b64(rl[u], j < n_used ? j * 8u : OOB, 0, 0);
+                const auto x = __builtin_amdgcn_raw_buffer_load_b64(rl[u], j < n_used ? j * 8u : OOB, 0, AUX);
                 l[u][g] = ((uint64_t)x[1] << 32) | x[0];
-                f[u][g] = __builtin_amdgcn_raw_buffer_load_b32(rf[u], j < n_used ? j * 4u : OOB, 0, 0);
+                f[u][g] = __builtin_amdgcn_raw_buffer_load_b32(rf[u], j < n_used ? j * 4u : OOB, 0, AUX);
               }
 #pragma unroll
             for (int u = 0; u < 2; u++)
@@ -580,6 +595,30 @@ __global__ void __launch_bounds__(NT)
     // ---- write the row: columns in used order, diagonal = the raw self-loop (graph/mod.rs:210-217)
     const size_t orow = (size_t)(row - out_row0) * n_used;
     bool sat = false;
+    // the row's output: nontemporal 16-B stores; in the flagged launch sc1 (write-through) stores,
+    // which the later rows' sc1 loads read across XCDs (MI355X_MICROARCH.md hand-off protocol)
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t wl = __builtin_amdgcn_make_buffer_rsrc((void*)(out_lat + orow), 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wf = __builtin_amdgcn_make_buffer_rsrc((void*)(out_loss + orow), 0, 0x7FFFFFFF, 0x00020000);
+    auto st_lat2 = [&](uint32_t j, uint64_t a, uint64_t b) {
+      if constexpr (FLAG) {
+        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128((v4){(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)},
+                                               wl, j * 8u, 0, SSSP_SC1);
+      } else {
+        __builtin_nontemporal_store((u64x2){a, b}, (u64x2*)&out_lat[orow + j]);
+      }
+    };
+    auto st_loss4 = [&](uint32_t j, float a, float b, float c, float d) {
+      if constexpr (FLAG) {
+        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128((v4){__float_as_uint(a), __float_as_uint(b), __float_as_uint(c),
+                                                    __float_as_uint(d)}, wf, j * 4u, 0, SSSP_SC1);
+      } else {
+        __builtin_nontemporal_store((f32x4){a, b, c, d}, (f32x4*)&out_loss[orow + j]);
+      }
+    };
     auto entry = [&](uint32_t j, uint64_t& l, float& f) {
       if (j == row) {
         const uint32_t e = self_edge[used[j]];
@@ -592,9 +631,7 @@ __global__ void __launch_bounds__(NT)
         f = __uint_as_float(fkey_loss_bits(kk));
       }
     };
-    if (vec_out) {  // n_used % 4 == 0, 16-B aligned rows: 16-B nontemporal stores
-      typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-      typedef float f32x4 __attribute__((ext_vector_type(4)));
+    if (vec_out) {  // n_used % 4 == 0, 16-B aligned rows: 16-B stores
       // Every global read of the output comes before its first store: the columns'
       // node ids (16-B loads, OU per thread) and the diagonal's raw self-loop.  (Read
       // inside the loop, each one waited behind the thread's earlier stores, since the
@@ -633,9 +670,9 @@ __global__ void __launch_bounds__(NT)
           cell(j + 1, uv[k][1], l1, f1);
           cell(j + 2, uv[k][2], l2, f2);
           cell(j + 3, uv[k][3], l3, f3);
-          __builtin_nontemporal_store((u64x2){l0, l1}, (u64x2*)&out_lat[orow + j]);
-          __builtin_nontemporal_store((u64x2){l2, l3}, (u64x2*)&out_lat[orow + j + 2]);
-          __builtin_nontemporal_store((f32x4){f0, f1, f2, f3}, (f32x4*)&out_loss[orow + j]);
+          st_lat2(j, l0, l1);
+          st_lat2(j + 2, l2, l3);
+          st_loss4(j, f0, f1, f2, f3);
         }
       }
       for (uint32_t j = (tt + OU * NT) * 4; j < n_used; j += NT * 4) {  // past OU x NT x 4 columns
@@ -645,24 +682,45 @@ __global__ void __launch_bounds__(NT)
         entry(j + 1, l1, f1);
         entry(j + 2, l2, f2);
         entry(j + 3, l3, f3);
-        __builtin_nontemporal_store((u64x2){l0, l1}, (u64x2*)&out_lat[orow + j]);
-        __builtin_nontemporal_store((u64x2){l2, l3}, (u64x2*)&out_lat[orow + j + 2]);
-        __builtin_nontemporal_store((f32x4){f0, f1, f2, f3}, (f32x4*)&out_loss[orow + j]);
+        st_lat2(j, l0, l1);
+        st_lat2(j + 2, l2, l3);
+        st_loss4(j, f0, f1, f2, f3);
       }
     } else {
       for (uint32_t j = tid; j < n_used; j += NT) {
         uint64_t l;
         float f;
         entry(j, l, f);
-        out_lat[orow + j] = l;
-        out_loss[orow + j] = f;
+        if constexpr (FLAG) {
+          __builtin_amdgcn_raw_buffer_store_b64((uint32_t __attribute__((ext_vector_type(2)))){(uint32_t)l,
+                                                                                              (uint32_t)(l >> 32)},
+                                                wl, j * 8u, 0, SSSP_SC1);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(f), wf, j * 4u, 0, SSSP_SC1);
+        } else {
+          out_lat[orow + j] = l;
+          out_loss[orow + j] = f;
+        }
       }
     }
-    if (__any(sat) && lane == 0) sat_row[row - row_begin] = 1u;
+    if (__any(sat) && lane == 0) {
+      sat_row[row - row_begin] = 1u;
+      if (FLAG) s_sat = 1u;
+    }
     if (dg) {
       diag[bi * 8 + 0] = c_search - c_start;
       diag[bi * 8 + 1] = clock64() - c_search;
       diag[bi * 8 + 3] = n_adv | ((c_setup - c_start) << 24);  // bucket advances | setup cycles
+    }
+    if constexpr (FLAG) {
+      // Flagged rows: every wave waits for its sc1 stores, then one lane publishes the row
+      // (sc1 flag store behind the barrier: MI355X_MICROARCH.md hand-off table, first row)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)done, 0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(s_sat ? 2u : 1u, rd, (row - row_begin) * 4u, 0, SSSP_SC1);
+        s_sat = 0u;
+      }
     }
     __syncthreads();  // the next row reuses the LDS
   }
@@ -683,7 +741,8 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
                      const uint32_t* self_edge, const uint64_t* e_lat, const float* e_loss, uint64_t* out_lat,
                      float* out_loss, uint32_t* sat_row, uint32_t delta, unsigned long long* work,
                      unsigned long long* diag, const uint32_t* blk_rows, uint32_t n_blk, const uint32_t* ub_row,
-                     const uint32_t* ub_w, const uint32_t* plan_ctl, int plan_ph, uint32_t* plan_ctr) {
+                     const uint32_t* ub_w, const uint32_t* plan_ctl, int plan_ph, uint32_t* plan_ctr,
+                     uint32_t* done) {
   const size_t lds = sssp_lds_bytes(n);
   if (!sssp_lds_fits(n)) throw Error(SG_ERR_INVALID_ARG, "graph too large for the LDS-resident search");
   if ((uint64_t)n_arcs * 12 >= (1ull << 31)) throw Error(SG_ERR_INVALID_ARG, "too many arcs for 32-bit offsets");
@@ -707,7 +766,7 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
   // torn down per row.  C3: 3.92 -> 3.54 ms (same box).  SG_SSSP_PERSIST=0: a
   // workgroup per row.
   const char* ps = getenv("SG_SSSP_PERSIST");
-  const bool persist = !(ps && ps[0] == '0') && (rows > (uint32_t)ctx->n_cu || plan_ctl);
+  const bool persist = done || (!(ps && ps[0] == '0') && (rows > (uint32_t)ctx->n_cu || plan_ctl));
   // spin budget per wave (sleeps of ~128 cycles): a safety valve against a queue
   // bug, never reached by a correct search; SG_SSSP_SPIN_MAX (tests) lowers it so
   // that searches give up and their rows take the wide kernel
@@ -728,9 +787,13 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, ctx->stream, out_off, out_arc, n, n_arcs, d_used, n_used,
                        row_begin, row_begin, self_edge, e_lat, e_loss, out_lat, out_loss, sat_row, delta, vec, work,
                        diag, claim, idle_sleep, lane_deg, blk_rows, ub_row, ub_w, item_ctr, rows, spin_max, plan_ctl,
-                       plan_ph);
+                       plan_ph, done);
   };
-  if (work) {
+  if (done) {  // the flagged one-launch plan (the default kernel shape only)
+    if (work) go(k_sssp_lds<true, 1024, 8, 0, true>);
+    else if (ctx->in_fill) go(k_sssp_lds<false, 1024, 8, 1, true>);
+    else go(k_sssp_lds<false, 1024, 8, 0, true>);
+  } else if (work) {
     if (nt == 512) go(k_sssp_lds<true, 512, 8, 0>);
     else if (la16) go(k_sssp_lds<true, 1024, 16, 0>);
     else go(k_sssp_lds<true, 1024, 8, 0>);

@@ -31,10 +31,12 @@ def ctx():
 
 # Shortest-path kernels the routing tests run on.  The defaults: the per-source LDS search
 # (sg_sssp.hip) in its unbounded and forced bounded-phase forms (the build picks phases from
-# 8 rows per CU on, i.e. at C3) and the slab relaxation (dense graphs, graphs past the LDS).
+# 8 rows per CU on, i.e. at C3), its flagged one-launch form (bound rows taken once published),
+# and the slab relaxation (graphs past the LDS; SG_APSP_LDS=0 also forces it on dense graphs,
+# which otherwise take the register-resident search of sg_dense.hip).
 # The non-default options (landmarks, the team search) run in test_option_kernels, or on the
 # whole matrix with SG_TEST_ALL_KERNELS=1.
-APSP_KERNELS = ["lds", "lds_bounded", "slab"]
+APSP_KERNELS = ["lds", "lds_bounded", "lds_flagged", "slab"]
 APSP_OPTIONS = ["lds_landmarks", "team"]
 if os.environ.get("SG_TEST_ALL_KERNELS"):
     APSP_KERNELS = APSP_KERNELS + APSP_OPTIONS
@@ -47,4 +49,5 @@ def set_apsp_kernel(monkeypatch, name: str) -> str:
     monkeypatch.setenv("SG_SSSP_LANDMARKS", "8" if name == "lds_landmarks" else "0")
     # team: the search of graphs past one CU's LDS (sg_team.hip), forced with 3 members, in phases
     monkeypatch.setenv("SG_SSSP_TEAM", "3" if name == "team" else "0")
+    monkeypatch.setenv("SG_SSSP_FLAGGED", "1" if name == "lds_flagged" else "0")
     return "slab" if name == "slab" else "lds"

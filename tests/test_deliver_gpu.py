@@ -143,15 +143,18 @@ def test_hot_destination_big_buckets(oracle, ctx):
     _assert_same(want, got, ost, gst)
 
 
-def test_slots_around_inblock_rank_limit(oracle, ctx):
-    """About 256 entries per destination: the region path rank-sorts the slots up
-    to INBLOCK_RANK_MAX (256) and bitonic-sorts the ones above it, in one block."""
+@pytest.mark.parametrize("per_dst", [20, 50, 100, 200, 400, 560])
+def test_slots_around_inblock_sort_limits(oracle, ctx, per_dst):
+    """Entries per destination across the region path's in-block sort classes: rank sort
+    up to 32, one wave's register bitonic sort for 33-64, 65-128 and 129-256 (1, 2 and 4
+    keys per lane), the block's bitonic sort above 256."""
     lat, loss, hosts = _world(n_hosts=3000, seed=9)
     start, end = T0 + 10**9, T0 + 10**9 + 10**6
-    pk = synth.make_packets(800000, hosts, start, end, seed=9)
+    pk = synth.make_packets(per_dst * 3000, hosts, start, end, seed=9 + per_dst)
     want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, end, 2**63, 0)
     sizes = np.diff(want["dst_offsets"])
-    assert (sizes > 256).any() and ((sizes > 32) & (sizes <= 256)).any()
+    lo, hi = sizes.min(), sizes.max()
+    assert lo < per_dst < hi
     _assert_same(want, got, ost, gst)
 
 

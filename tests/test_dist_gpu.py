@@ -112,6 +112,15 @@ def test_sharded_round_with_rng_skip(oracle, ctx):
     assert want["delivered"] > 0
 
 
+@pytest.mark.parametrize("n_packets", [150000, 600000])
+def test_sharded_wave_sorted_slots(oracle, ctx, n_packets):
+    """About 100 and 400 received records per destination: order-keyed slots sorted by
+    one wave each in registers ((time, order key) pairs, 2 keys per lane), and by the block
+    past 256."""
+    want = _run(oracle, ctx, 2, n_packets, seed=8)
+    assert 64 < np.median(np.diff(want["dst_offsets"])) < 512
+
+
 @pytest.mark.parametrize("p_hot", [0.0, 0.1])
 def test_sharded_two_level_bucketing(oracle, ctx, monkeypatch, p_hot):
     """The destination phase's two-level scatter on received records (order keys carried)."""

@@ -470,3 +470,31 @@ def test_routing_info_direct_and_errors(oracle, ctx):
     with pytest.raises(ShadowGpuError) as e:
         generate_routing_info(_graph(g2, ctx), range(90), True)
     assert e.value.code == _capi.SG_ERR_NO_EDGE
+
+
+@pytest.mark.parametrize("case", ["ties", "wide", "parallel_directed", "used_subset", "tiny_wmin"])
+def test_dense_graph_cases(oracle, ctx, case):
+    """Dense graphs (mean out-degree past 64: the register-resident search of sg_dense.hip under
+    the LDS fixtures, the slab under `slab`): equal-latency paths decided by loss, latencies past
+    2^32 ns (wide rows), parallel arcs in a directed graph, a used-node subset with rows and
+    columns in a shuffled order, and 1-ns arcs (one-node rounds)."""
+    rng = np.random.default_rng(sum(map(ord, case)))
+    n = 520
+    if case == "parallel_directed":
+        g = synth.ring_chords_graph(n, 150.0, seed=5, directed=True, parallel=0.2)
+    else:
+        g = synth.ring_chords_graph(n, 180.0, seed=6)
+    if case == "ties":
+        g["lat"] = (rng.integers(1, 4, len(g["lat"])) * 1000).astype(np.uint64)
+        g["loss"] = rng.uniform(0, 0.4, len(g["lat"])).astype(np.float32)
+        g["loss"][rng.random(len(g["loss"])) < 0.1] = np.float32(1.0)
+    if case == "wide":
+        g["lat"] = (rng.integers(1_000_000, 9_000_000, len(g["lat"])) * 1000).astype(np.uint64)
+    if case == "tiny_wmin":
+        g["lat"] = rng.integers(1, 40, len(g["lat"])).astype(np.uint64)
+    used = np.arange(n, dtype=np.uint32)
+    if case == "used_subset":
+        used = rng.permutation(n)[:333].astype(np.uint32)
+    lat, _ = _check(oracle, g, used, ctx)
+    if case == "wide":
+        assert lat.max() >= (1 << 32)
