@@ -270,7 +270,7 @@ def codel_leg(a, D, ctx, torch, buckets, n_packets, pmc):
                    "hosts": H, "events": E, "pushes": nd},
         "roofline": {"kernel": "k_codel", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pm.get("hbm_bytes_per_launch"),
-                     "avg_launch_ms": round(k_s * 1e3, 4)},
+                     "avg_launch_ms": round(k_s * 1e3, 4), "valu_frac_pmc": pm.get("valu_frac")},
         "dropped": n_drop,
     }
     if D.rank == 0 and D.world == 1 and not a.no_cpu:
@@ -348,7 +348,7 @@ def outbound_leg(a, D, ctx, torch, pk, hosts, ht, table, round_end, sharded, pmc
         "roofline": {"kernel": "k_outbound", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                      "traffic": pmc.get("outbound", {}).get("hbm_bytes_per_launch"),
-                     "avg_launch_ms": round(k_s * 1e3, 4)},
+                     "avg_launch_ms": round(k_s * 1e3, 4), "valu_frac_pmc": pmc.get("outbound", {}).get("valu_frac")},
         "compact_ms": round(c_ms / max(c_n, 1), 4),
         "sent": len(batch),
         "fused_round": {"ms": round(t_fused * 1e3, 4), "packets_per_s": round(D.sum(float(n)) / t_fused, 1),
@@ -417,7 +417,8 @@ def inbound_leg(a, D, ctx, torch, buckets, n_packets, pmc, round_end):
                    "bw_down_bits": BW_DOWN_BITS},
         "roofline": {"kernel": "k_inbound", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                     "traffic": pmc.get("inbound", {}).get("hbm_bytes_per_launch"), "avg_launch_ms": round(k_s * 1e3, 4)},
+                     "traffic": pmc.get("inbound", {}).get("hbm_bytes_per_launch"), "avg_launch_ms": round(k_s * 1e3, 4),
+                     "valu_frac_pmc": pmc.get("inbound", {}).get("valu_frac")},
         "forwarded": n_fwd, "dropped": n_drop,
     }
     if D.rank == 0 and D.world == 1 and not a.no_cpu:
@@ -468,7 +469,7 @@ def gml_leg(a, NetworkGraph, synth):
 C2_NODES = 1200  # Tor-style complete graph, use_shortest_path: true
 
 
-def c2_leg(a, ctx, torch, NetworkGraph, synth, with_cpu):
+def c2_leg(a, ctx, torch, NetworkGraph, synth, with_cpu, pmc=None):
     """C2 (BASELINE configs[1]): a 1,200-node complete undirected GML graph (about 720k
     edges), every node used -- GML parse on the host, then the routing-table build on
     one GPU (shortest paths; the direct-path table beside it).  CPU baseline: the oracle's
@@ -512,10 +513,29 @@ def c2_leg(a, ctx, torch, NetworkGraph, synth, with_cpu):
     ctx.enable_timers(True)
     net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
     relax_ms, launches, _ = ctx.read_timer("relax")
+    dense_ms, dense_n, _ = ctx.read_timer("sssp_dense")
+    sort_ms, _, _ = ctx.read_timer("dense_sort")
+    ctx.enable_timers(True, count_work=True)  # (a separate build: the counting adds atomics)
+    net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
+    dense_rel = ctx.read_timer("sssp_dense")[2]
     ctx.enable_timers(False)
+    n_arcs = int(2 * np.count_nonzero(g["src"] != g["dst"]))  # undirected: both directions
+    roofline = None
+    if dense_n:  # k_sssp_dense: a 16-B sorted-arc record read (L2) per arc relaxed
+        k_s = dense_ms / 1e3 / dense_n
+        ach = 16.0 * dense_rel / dense_n / k_s / 1e9
+        pm = (pmc or {}).get("sssp_dense", {})
+        roofline = {"kernel": "k_sssp_dense", "bound": "l2", "achieved": round(ach, 1), "peak": L2_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / L2_PEAK_GBS, 4), "traffic": pm.get("hbm_bytes_per_launch"),
+                    "avg_launch_ms": round(dense_ms / dense_n, 4), "arc_sort_ms": round(sort_ms, 4),
+                    "relaxations_per_launch": dense_rel / dense_n,
+                    "redundancy_vs_dijkstra": round(dense_rel / max(1.0, float(n) * n_arcs), 4),
+                    "valu_frac_pmc": pm.get("valu_frac"),
+                    "what": "relaxations = arcs read below the round's cut; Dijkstra relaxes every arc of "
+                            "every settled node (n x arcs)"}
     leg = {"metric": "APSP routing build (s) @1.2k-node complete graph", "unit": "s", "value": round(t_build, 6),
            "higher_is_better": False, "direct_paths_s": round(t_direct, 6), "gml_parse_s": round(t_parse, 4),
-           "one_shot_s": round(t_one_shot, 6),
+           "one_shot_s": round(t_one_shot, 6), "roofline": roofline,
            "relax_ms": round(relax_ms, 4), "relax_launches": launches,
            "config": {"workload": f"C2: {n}-node complete undirected graph from GML ({len(raw)} bytes), latency "
                                   "U[1,300] ms, self-loops U[1,10] ms, loss 0 w.p. 0.8 else U(0,0.02); every node "
@@ -556,6 +576,15 @@ def main():
     g = synth.ring_chords_graph(a.nodes, a.degree, seed=1)
     net = NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
     used = np.arange(a.nodes, dtype=np.uint32)
+    route_bal = None
+    if D.world > 1:
+        # the table's row order that gives every rank's row block an even share of the
+        # sending hosts (synth.make_hosts puts host h on node h mod nodes): the same equal
+        # row blocks, hosts partitioned by the rank holding their node's row
+        from shadow_amd.dist import balanced_node_order
+
+        order, route_bal = balanced_node_order(np.arange(a.hosts) % a.nodes, a.nodes, D.world)
+        used = np.asarray(order, dtype=np.uint32)
     nu = len(used)
     rows = (nu + D.world - 1) // D.world
     r0, r1 = min(D.rank * rows, nu), min((D.rank + 1) * rows, nu)
@@ -806,13 +835,15 @@ def main():
     if D.rank == 0 and not a.no_gml:
         result["gml_ingest"] = gml_leg(a, NetworkGraph, synth)
     if D.rank == 0 and not a.no_c2:
-        result["c2"] = c2_leg(a, ctx, torch, NetworkGraph, synth, D.world == 1 and not a.no_cpu)
+        result["c2"] = c2_leg(a, ctx, torch, NetworkGraph, synth, D.world == 1 and not a.no_cpu, pmc)
 
     # ---------------- delivery round (C4) ----------------
     if not a.no_delivery:
         from shadow_amd.dist import HostPartition, ShardedDelivery
 
         hosts = synth.make_hosts(a.hosts, a.nodes, general_seed=1, exact_seeds=True)
+        if route_bal is not None:  # host -> its node's row in the balanced order
+            hosts["route"] = np.asarray(route_bal, dtype=np.uint32)
         part = HostPartition(hosts["route"], nu, D.world)
         mine = part.hosts_of[D.rank]
         # weak scaling: each rank sends a.packets from the hosts it owns, to destinations anywhere
@@ -895,7 +926,7 @@ def main():
                        "hosts": a.hosts, "packets_per_rank": a.packets},
             "roofline": {"kernel": "k_walk", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmw.get("hbm_bytes_per_launch"),
-                         "avg_launch_ms": round(walk_s * 1e3, 4)},
+                         "avg_launch_ms": round(walk_s * 1e3, 4), "valu_frac_pmc": pmw.get("valu_frac")},
             "round_hbm_GBs": round(round_bytes / t_round / 1e9, 1),
             "per_rank": per_rank,
             "parallelism": f"hosts{D.world}",

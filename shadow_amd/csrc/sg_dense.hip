@@ -47,19 +47,21 @@ constexpr int DENSE_G = 2;              // settled rows a wave relaxes together 
 
 // Per node u: its out-arcs (out_arc, 3 u32 each: head, latency32, bits(1f32 - loss))
 // sorted by latency into 16-B records {head, latency32, bits(om), 0} at the same
-// offsets; sorted[u] = 1, or 0 for a row past SORT_MAXDEG (copied as is, never cut
-// short).  Also the smallest arc latency (w_min).  One block per node.
-__global__ void __launch_bounds__(256) k_sort_arcs(const uint32_t* __restrict__ out_off,
-                                                   const uint32_t* __restrict__ out_arc, uint32_t n,
-                                                   uint4* __restrict__ sa, uint8_t* __restrict__ sorted,
-                                                   uint32_t* __restrict__ wmin) {
-  __shared__ unsigned long long k[SORT_MAXDEG];
-  __shared__ uint32_t s_lo[4];
+// offsets; sorted[u] = 1, or 0 for a row past `cap` arcs (copied as is, never cut
+// short).  Also the smallest arc latency (w_min).  One block per node; cap = the LDS
+// array (a power of two >= n - 1, at most SORT_MAXDEG: parallel arcs can exceed it).
+constexpr int SORT_THREADS = 1024;
+__global__ void __launch_bounds__(SORT_THREADS) k_sort_arcs(const uint32_t* __restrict__ out_off,
+                                                            const uint32_t* __restrict__ out_arc, uint32_t cap,
+                                                            uint4* __restrict__ sa, uint8_t* __restrict__ sorted,
+                                                            uint32_t* __restrict__ wmin) {
+  extern __shared__ __align__(16) unsigned long long k[];  // [cap]
+  __shared__ uint32_t s_lo[SORT_THREADS / 64];
   const uint32_t u = blockIdx.x, t = threadIdx.x;
   const uint32_t a0 = out_off[u], deg = out_off[u + 1] - a0;
   uint32_t lo = LAT32_SAT;
-  if (deg > SORT_MAXDEG) {
-    for (uint32_t i = t; i < deg; i += 256) {
+  if (deg > cap) {
+    for (uint32_t i = t; i < deg; i += SORT_THREADS) {
       const uint32_t* r = out_arc + 3 * (size_t)(a0 + i);
       sa[a0 + i] = make_uint4(r[0], r[1], r[2], 0u);
       lo = min(lo, r[1]);
@@ -68,7 +70,7 @@ __global__ void __launch_bounds__(256) k_sort_arcs(const uint32_t* __restrict__ 
   } else {
     uint32_t M = 1;
     while (M < deg) M <<= 1;
-    for (uint32_t i = t; i < M; i += 256) {
+    for (uint32_t i = t; i < M; i += SORT_THREADS) {
       const uint32_t l = i < deg ? out_arc[3 * (size_t)(a0 + i) + 1] : LAT32_SAT;
       k[i] = i < deg ? ((unsigned long long)l << 32) | i : ~0ull;
       lo = min(lo, l);
@@ -76,7 +78,7 @@ __global__ void __launch_bounds__(256) k_sort_arcs(const uint32_t* __restrict__ 
     __syncthreads();
     for (uint32_t kk = 2; kk <= M; kk <<= 1)
       for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-        for (uint32_t i = t; i < M; i += 256) {
+        for (uint32_t i = t; i < M; i += SORT_THREADS) {
           const uint32_t l = i ^ j;
           if (l > i) {
             const unsigned long long x = k[i], y = k[l];
@@ -88,7 +90,7 @@ __global__ void __launch_bounds__(256) k_sort_arcs(const uint32_t* __restrict__ 
         }
         __syncthreads();
       }
-    for (uint32_t i = t; i < deg; i += 256) {
+    for (uint32_t i = t; i < deg; i += SORT_THREADS) {
       const uint32_t* r = out_arc + 3 * (size_t)(a0 + (uint32_t)(k[i] & 0xFFFFFFFFu));
       sa[a0 + i] = make_uint4(r[0], r[1], r[2], 0u);
     }
@@ -98,7 +100,8 @@ __global__ void __launch_bounds__(256) k_sort_arcs(const uint32_t* __restrict__ 
   if ((t & 63) == 0) s_lo[t >> 6] = lo;
   __syncthreads();
   if (t == 0) {
-    const uint32_t m = min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3]));
+    uint32_t m = LAT32_SAT;
+    for (int w = 0; w < SORT_THREADS / 64; w++) m = min(m, s_lo[w]);
     if (m != LAT32_SAT) atomicMin(wmin, m);
   }
 }
@@ -261,7 +264,10 @@ void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_
   {
     TimedLaunch tl(ctx, "dense_sort", 24.0 * net->n_arcs);
     SG_HIP(hipMemsetAsync(wmin, 0xFF, 4, st));
-    hipLaunchKernelGGL(k_sort_arcs, dim3(n), dim3(256), 0, st, net->out_off, net->out_arc, n, sa, sorted, wmin);
+    uint32_t cap = 64;
+    while (cap < n - 1 && cap < SORT_MAXDEG) cap <<= 1;
+    hipLaunchKernelGGL(k_sort_arcs, dim3(n), dim3(SORT_THREADS), cap * 8, st, net->out_off, net->out_arc, cap, sa,
+                       sorted, wmin);
   }
   if (!rows) return;
   const uint32_t nbw = (n + 31) / 32;

@@ -96,7 +96,6 @@ struct sg_ctx {
   std::string last_error;
   uint32_t err_row = 0, err_col = 0;
   // routing workspace
-  sg::DevBuf r_team_arc, r_team_mid, r_team_pair, r_team_box, r_team_ctl, r_team_used;  // sg_team.hip
   sg::DevBuf r_dist, r_dist2, r_flags, r_used, r_err, r_self, r_pair_cnt, r_pair_edge, r_map, r_out_lat,
       r_out_loss, r_misc, r_dirty, r_work, r_items, r_plan, r_dense, r_done;
   // delivery workspace
@@ -318,11 +317,6 @@ void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_
 constexpr int SSSP_KB_MAX = 8;
 constexpr uint32_t SSSP_UB_EXACT = 0x80000000u;  // bound rows per bounded search (sg_sssp.hip SSSP_KB)
 bool sssp_lds_fits(uint32_t n_nodes);
-// Per-source search by teams of K workgroups, 1/K of the row's keys in each one's LDS
-// (sg_team.hip), for graphs past the one-CU search.  sssp_team_size: the smallest K
-// that fits, 0 if none.
-bool sssp_team_fits(uint32_t n_nodes, uint32_t K);
-uint32_t sssp_team_size(uint32_t n_nodes);
 
 void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_arc, uint32_t n, uint32_t n_arcs,
                      const uint32_t* d_used, uint32_t n_used, uint32_t row_begin, uint32_t row_end,
@@ -354,11 +348,5 @@ SsspDevPlan sssp_device_plan(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 // After phase 0 (the landmarks) ran: phase 1's bound rows from the landmark rows' columns.
 void sssp_landmark_bounds(sg_ctx* ctx, const SsspDevPlan& p, uint32_t n_used, uint32_t row_begin,
                           const uint64_t* out_lat, const uint32_t* sat_row, int kb);
-// The team search (sg_team.hip): its arc order and outbox capacity once per build,
-// then one launch per phase of a device plan (plan null: rows [row_begin, row_end)).
-uint32_t sssp_team_prepare(sg_ctx* ctx, sg_net* net, uint32_t K);
-void launch_sssp_team(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin,
-                      uint32_t row_end, uint64_t* out_lat, float* out_loss, uint32_t* sat_row, uint32_t K,
-                      uint32_t cap, unsigned long long* work, const SsspDevPlan* plan, int ph);
 
 }  // namespace sg

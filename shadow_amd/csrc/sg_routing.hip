@@ -1684,65 +1684,12 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   if (!wide_rows.empty()) run_wide(ctx, net, d_used, n_used, wide_rows, row_begin, out_lat, out_loss);
 }
 
-// Graphs past one CU's LDS (C5): the team search (sg_team.hip), K workgroups per
-// source row.  Rows flagged 1 (saturated) or 2 (a team gave up) take the wide kernel.
-static void shortest_paths_team(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
-                                uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss, uint32_t K) {
-  hipStream_t st = ctx->stream;
-  const uint32_t rows = row_end - row_begin;
-  uint32_t* sat = ctx->r_flags.get<uint32_t>(rows);
-  SG_HIP(hipMemsetAsync(sat, 0, rows * 4ull, st));
-  unsigned long long* work = ctx->count_work ? ctx->r_work.get<unsigned long long>(WORK_SHARDS) : nullptr;
-  if (work) SG_HIP(hipMemsetAsync(work, 0, WORK_SHARDS * 8, st));
-  const uint32_t cap = sssp_team_prepare(ctx, net, K);
-  // phases and bounds as for the one-CU search (sg_plan.hip), from 8 rows per team
-  const uint32_t n_teams = std::max(1u, (uint32_t)ctx->n_cu / K);
-  const int seeds_env = env_int("SG_SSSP_SEEDS", 1);
-  if (seeds_env != 0 && (seeds_env == 2 || rows >= 8u * n_teams)) {
-    const uint32_t per_team = rows / n_teams;
-    const int n_phase = std::max(2, std::min(SSSP_PHASES_MAX, env_int("SG_SSSP_PHASES", per_team >= 16 ? 3 : 2)));
-    const int kb = std::max(1, std::min(SSSP_KB_MAX, env_int("SG_SSSP_BOUNDS", 2)));
-    const bool exact = env_int("SG_SSSP_EXACT", 1) != 0 && n_used == net->n_nodes;
-    const int hops = std::max(1, std::min(env_int("SG_SSSP_HOPS", 3), 3));
-    const SsspDevPlan plan =
-        sssp_device_plan(ctx, net, d_used, n_used, row_begin, row_end, n_phase, kb, exact, hops, 0u);
-    for (int ph = 0; ph < plan.n_phase; ph++)
-      launch_sssp_team(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss, sat, K, cap, work, &plan, ph);
-  } else {
-    launch_sssp_team(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss, sat, K, cap, work, nullptr, 0);
-  }
-  std::vector<uint32_t> h_sat(rows);
-  copy_to_host(ctx, h_sat.data(), sat, rows * 4ull);
-  std::vector<uint32_t> wide_rows;
-  for (uint32_t r = 0; r < rows; r++)
-    if (h_sat[r]) wide_rows.push_back(row_begin + r);
-  if (work) {
-    unsigned long long w[10];
-    copy_to_host(ctx, w, work, sizeof(w));
-    timer_add_work(ctx, "sssp_team", (double)w[0]);
-    timer_add_work(ctx, "sssp_team_msgs", (double)w[1]);
-    timer_add_work(ctx, "sssp_team_steps", (double)w[2]);
-    // workgroup-milliseconds (100 MHz wall clock) per part of the search
-    static const char* part[7] = {"team_t_claim", "team_t_setup", "team_t_local", "team_t_remote",
-                                  "team_t_exchange", "team_t_apply", "team_t_output"};
-    for (int i = 0; i < 7; i++) timer_add_work(ctx, part[i], (double)w[3 + i] * 1e-5);
-  }
-  if (!wide_rows.empty()) run_wide(ctx, net, d_used, n_used, wide_rows, row_begin, out_lat, out_loss);
-}
-
 static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, const uint32_t* h_used,
                            uint32_t n_used, uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
                            float* out_loss) {
-  // SG_SSSP_TEAM=K (2..8) takes the team search (sg_team.hip) with K members for
-  // sparse graphs of up to K x the LDS search's size.  Not the default: at C5 (50k
-  // nodes) it relaxes 1.5x Dijkstra's arcs against the slab kernel's 10.5x, yet
-  // takes 646 ms against the slab's 249 ms ("Team search").
-  const int team_env = env_int("SG_SSSP_TEAM", 0);
-  if (team_env >= 2 && env_int("SG_APSP_LDS", 1) != 0 && net->n_nodes && net->n_arcs <= 64ull * net->n_nodes &&
-      (uint64_t)net->n_arcs * 12 < (1ull << 31) && sssp_team_fits(net->n_nodes, (uint32_t)team_env)) {
-    shortest_paths_team(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss, (uint32_t)team_env);
-    return;
-  }
+  // (Round 3 also built a team search for graphs past one CU's LDS, K workgroups per
+  // row: 1.5x Dijkstra's relaxations at C5 but 646 ms against the slab's 249 ms, so
+  // it was removed in round 4; DESIGN.md, "Team search".)
   // SG_APSP_LDS=0 forces the batched-source slab kernel.  The LDS search takes
   // sparse graphs (mean out-degree <= 64); on dense ones the slab kernel shares
   // each arc record among 64 sources (C2, 1,200-node complete graph: 3.6 ms

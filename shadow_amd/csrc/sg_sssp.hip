@@ -229,14 +229,16 @@ __global__ void __launch_bounds__(NT)
   }
   // Rows: one per workgroup, or (item_ctr set: persistent workgroups, one per
   // CU) claimed one after another from a counter the host zeroed
+  // The next row is claimed while this one's output is written (its returning
+  // atomic then overlaps the stores instead of starting the next row's setup);
+  // give-ups happen only during a search, never with a claim outstanding.
   __shared__ uint32_t s_item;
+  if (item_ctr && tid == 0) s_item = atomicAdd(item_ctr, 1u);
   for (uint32_t it = 0;; it++) {
     uint32_t bi;
     if (item_ctr) {
-      if (tid == 0) s_item = atomicAdd(item_ctr, 1u);
-      __syncthreads();
+      __syncthreads();  // s_item written (first row: above; later rows: in the previous row's output)
       bi = s_item;
-      __syncthreads();  // every thread has read s_item before thread 0 writes it again
       if (bi >= n_items) break;
     } else {
       if (it) break;
@@ -593,6 +595,8 @@ __global__ void __launch_bounds__(NT)
     const unsigned long long c_search = dg ? clock64() : 0;
 
     // ---- write the row: columns in used order, diagonal = the raw self-loop (graph/mod.rs:210-217)
+    __syncthreads();  // every thread has read s_item (at the row's start) before it is written again
+    if (item_ctr && tid == 0) s_item = atomicAdd(item_ctr, 1u);  // the next row (see the row loop)
     const size_t orow = (size_t)(row - out_row0) * n_used;
     bool sat = false;
     // the row's output: nontemporal 16-B stores; in the flagged launch sc1 (write-through) stores,

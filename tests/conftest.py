@@ -34,10 +34,10 @@ def ctx():
 # 8 rows per CU on, i.e. at C3), its flagged one-launch form (bound rows taken once published),
 # and the slab relaxation (graphs past the LDS; SG_APSP_LDS=0 also forces it on dense graphs,
 # which otherwise take the register-resident search of sg_dense.hip).
-# The non-default options (landmarks, the team search) run in test_option_kernels, or on the
-# whole matrix with SG_TEST_ALL_KERNELS=1.
+# The non-default option (landmarks) runs in test_option_kernels, or on the whole matrix with
+# SG_TEST_ALL_KERNELS=1.
 APSP_KERNELS = ["lds", "lds_bounded", "lds_flagged", "slab"]
-APSP_OPTIONS = ["lds_landmarks", "team"]
+APSP_OPTIONS = ["lds_landmarks"]
 if os.environ.get("SG_TEST_ALL_KERNELS"):
     APSP_KERNELS = APSP_KERNELS + APSP_OPTIONS
 
@@ -45,9 +45,7 @@ if os.environ.get("SG_TEST_ALL_KERNELS"):
 def set_apsp_kernel(monkeypatch, name: str) -> str:
     """Select a routing kernel by environment; returns its family ("lds" or "slab")."""
     monkeypatch.setenv("SG_APSP_LDS", "0" if name == "slab" else "1")
-    monkeypatch.setenv("SG_SSSP_SEEDS", "2" if name in ("lds_bounded", "lds_landmarks", "team") else "1")
+    monkeypatch.setenv("SG_SSSP_SEEDS", "2" if name in ("lds_bounded", "lds_landmarks") else "1")
     monkeypatch.setenv("SG_SSSP_LANDMARKS", "8" if name == "lds_landmarks" else "0")
-    # team: the search of graphs past one CU's LDS (sg_team.hip), forced with 3 members, in phases
-    monkeypatch.setenv("SG_SSSP_TEAM", "3" if name == "team" else "0")
     monkeypatch.setenv("SG_SSSP_FLAGGED", "1" if name == "lds_flagged" else "0")
     return "slab" if name == "slab" else "lds"

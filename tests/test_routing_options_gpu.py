@@ -1,7 +1,6 @@
-"""The non-default shortest-path options, one representative graph shape each (the default
+"""The non-default shortest-path option, one representative graph shape each (the default
 kernels run the whole routing suite, conftest.APSP_KERNELS): landmark rows splitting the
-first phase (SG_SSSP_LANDMARKS) and the multi-CU team search (SG_SSSP_TEAM, sg_team.hip).
-Bit-exact against the oracle."""
+first phase (SG_SSSP_LANDMARKS).  Bit-exact against the oracle."""
 import pytest
 
 from conftest import APSP_OPTIONS, set_apsp_kernel
