@@ -157,3 +157,60 @@ def test_errors(ctx):
     with pytest.raises(ShadowGpuError) as e:
         q.run(CoDelEvents.from_numpy([0, 9], [0, 0], [T0] * 2, [0, 1], [100] * 2), _status(8))
     assert e.value.code == _capi.SG_ERR_INVALID_ARG
+
+
+def test_good_state_mix(oracle, ctx):
+    """Most hosts in CoDel's good state (microsecond gaps), a few with queues that
+    stand past TARGET and enter drop mode, in the same blocks and chunks; four
+    calls, so elements pushed in one call are popped from the ring in the next,
+    and hosts cross chunk boundaries."""
+    rng = np.random.default_rng(23)
+    H, E = 20000, 200000
+    q = CoDelQueues(H, 512, ctx=ctx)
+    os_ = oracle.codel_state(H, q.cap)
+    gstat, ostat = _status(4 * E), np.zeros(4 * E, np.uint8)
+    t0 = T0 + 10**9
+    slow = rng.random(H) < 0.02
+    for c in range(4):
+        host = np.sort(rng.integers(0, H, E)).astype(np.uint32)
+        # a few hosts get long runs (several chunks' worth of events)
+        host[: 3000] = 7
+        host[3000: 5500] = 1000 + c
+        host = np.sort(host)
+        kind = (rng.random(E) < np.where(slow[host], 0.3, 0.5)).astype(np.uint8)
+        t = np.zeros(E, np.uint64)
+        for h in np.unique(host):
+            idx = np.nonzero(host == h)[0]
+            gap = 4 * MS if slow[h] else 2000
+            t[idx] = t0 + np.cumsum(rng.integers(0, gap, len(idx))).astype(np.uint64)
+        pkt = (c * E + np.arange(E)).astype(np.uint32)
+        ln = rng.integers(40, 1500, E).astype(np.uint32)
+        _run_both(oracle, q, os_, gstat, ostat, host, kind, t, pkt, ln)
+        t0 = int(t.max()) + 1
+    _same_state(oracle, q.get_state(), os_)
+    assert (ostat == 2).any() and (ostat == 1).any()
+
+
+def test_bytes_below_ring_contents(oracle, ctx):
+    """A state whose byte count is below what its ring holds (set_state): pops
+    saturate the count at zero (codel_queue.rs pop_front)."""
+    H = 64
+    q = CoDelQueues(H, 16, ctx=ctx)
+    os_ = oracle.codel_state(H, q.cap)
+    gstat, ostat = _status(1000), np.zeros(1000, np.uint8)
+    t0 = T0 + 10**9
+    host = np.repeat(np.arange(H, dtype=np.uint32), 4)
+    kind = np.tile(np.array([0, 0, 0, 0], np.uint8), H)
+    t = (t0 + np.tile(np.arange(4), H) * 1000).astype(np.uint64)
+    pkt = np.arange(4 * H, dtype=np.uint32)
+    ln = np.full(4 * H, 1000, np.uint32)
+    _run_both(oracle, q, os_, gstat, ostat, host, kind, t, pkt, ln)
+    st = q.get_state()
+    st["bytes"][::2] = 1500  # below the 4000 queued
+    q.set_state(st)
+    os_["bytes"][:] = st["bytes"]
+    host = np.repeat(np.arange(H, dtype=np.uint32), 3)
+    kind = np.ones(3 * H, np.uint8)
+    t = (t0 + 10**6 + np.tile(np.arange(3), H) * 1000).astype(np.uint64)
+    _run_both(oracle, q, os_, gstat, ostat, host, kind, t, np.zeros(3 * H, np.uint32), np.zeros(3 * H, np.uint32))
+    _same_state(oracle, q.get_state(), os_)

@@ -70,7 +70,10 @@ def test_windows_match_oracle(oracle, ctx, bw_mbit, boot_ms):
         assert np.array_equal(st_g.cpu().numpy(), st_o)
         assert np.array_equal(fwd_g.cpu().numpy().view(np.uint64)[st_o == 1], fwd_o[st_o == 1])
         assert np.array_equal(ctr_g.cpu().numpy().view(np.uint64), ctr_o)
-        _same(oracle, ib.get_state(), ost)
+        got = ib.get_state()
+        _same(oracle, got, ost)
+        for k in ("task_id", "task_born"):
+            assert np.array_equal(got[k], ost[k]), k
     if bw_mbit == 1:
         assert (st_o == 2).any() and (ost["rflags"] & oracle.RL_PENDING).any()
 
@@ -108,3 +111,80 @@ def test_arrival_after_window_rejected(ctx):
                _dev([0], np.uint32, np.int32), _dev([100], np.uint32, np.int32), T0 + 10 * MS, 0, T0 + 10**12,
                torch.zeros(4, dtype=torch.int64, device="cuda"), torch.zeros(4, dtype=torch.uint8, device="cuda"))
     assert e.value.code == _capi.SG_ERR_INVALID_ARG
+
+
+def _run_windows(oracle, ctx, bw, cap, windows, boot, sim_end=T0 + 10**12):
+    """Consecutive windows (host, t, ln, window_end) on the GPU and the oracle,
+    everything compared after each (statuses, forward times, counters, state, ids)."""
+    import torch
+
+    H = len(bw)
+    ib = InboundPipeline(bw, cap, ctx=ctx)
+    ost = oracle.inbound_state(bw, ib.cap)
+    n_pk = sum(len(w[0]) for w in windows)
+    fwd_g = torch.full((max(n_pk, 1),), -1, dtype=torch.int64, device="cuda")
+    st_g = torch.zeros(max(n_pk, 1), dtype=torch.uint8, device="cuda")
+    ctr_g = torch.zeros(H, dtype=torch.int64, device="cuda")
+    fwd_o = np.full(max(n_pk, 1), np.uint64(2**64 - 1))
+    st_o = np.zeros(max(n_pk, 1), np.uint8)
+    ctr_o = np.zeros(H, np.uint64)
+    p0 = 0
+    for host, t, ln, wend in windows:
+        pkt = np.arange(p0, p0 + len(host), dtype=np.uint32)
+        p0 += len(host)
+        ib.run(_dev(host, np.uint32, np.int32), _dev(t, np.uint64, np.int64), _dev(pkt, np.uint32, np.int32),
+               _dev(ln, np.uint32, np.int32), wend, boot, sim_end, fwd_g, st_g, ctr_g.data_ptr())
+        oracle.inbound_run(ost, host, t, pkt, ln, wend, boot, sim_end, ctr_o, fwd_o, st_o)
+        assert np.array_equal(st_g.cpu().numpy(), st_o)
+        assert np.array_equal(fwd_g.cpu().numpy().view(np.uint64)[st_o == 1], fwd_o[st_o == 1])
+        assert np.array_equal(ctr_g.cpu().numpy().view(np.uint64), ctr_o)
+        got = ib.get_state()
+        _same(oracle, got, ost)
+        for k in ("task_id", "task_born"):
+            assert np.array_equal(got[k], ost[k]), k
+    return st_o, ost
+
+
+def test_groups_chunks_and_slow_relays(oracle, ctx):
+    """Same-time groups of arrivals (a task per group, one id each), long hosts
+    crossing chunk boundaries with same-time runs across them, a bootstrap boundary
+    inside a window, bucket refills across many intervals, and throttled hosts
+    beside unthrottled ones in every block; three windows."""
+    rng = np.random.default_rng(41)
+    H = 3000
+    bw = np.where(rng.random(H) < 0.05, 2 * 10**6, 10**9).astype(np.uint64)  # a few slow relays
+    windows = []
+    for w in range(3):
+        t0, t1 = T0 + w * 20 * MS, T0 + (w + 1) * 20 * MS
+        host = np.sort(rng.integers(0, H, 30000)).astype(np.uint32)
+        # hosts 5, 700 and 1500 get long runs (several chunks), with same-time runs
+        host = np.sort(np.r_[host, np.full(2500, 5), np.full(1800, 700), np.full(3000, 1500)].astype(np.uint32))
+        t = np.zeros(len(host), np.uint64)
+        for h in np.unique(host):
+            idx = np.nonzero(host == h)[0]
+            # integer-us times: same-time groups are common; runs of 40 at host 5, 150 at host 1500
+            tt = np.sort(rng.integers(t0, t1 - 1000, len(idx)) // 1000 * 1000)
+            if h == 5:
+                tt = np.sort(np.repeat(tt[::40], 40)[: len(idx)])
+            if h == 1500:
+                tt = np.sort(np.repeat(tt[::150], 150)[: len(idx)])
+            t[idx] = tt
+        ln = rng.choice(np.array([28, 1476, 600], np.uint32), len(host))
+        windows.append((host, t, ln, t1))
+    st_o, ost = _run_windows(oracle, ctx, bw, 4096, windows, boot=T0 + 30 * MS)
+    assert (st_o == 1).sum() > 0.9 * len(st_o) * 0.5
+    assert (ost["rflags"] & oracle.RL_PENDING).any()  # the slow relays carry tasks over
+
+
+def test_same_time_group_beyond_ring(oracle, ctx):
+    """A same-time group of arrivals larger than the ring: SG_ERR_CAPACITY."""
+    import torch
+
+    ib = InboundPipeline(np.array([10**9, 10**9], np.uint64), 16, ctx=ctx)
+    host = np.r_[np.zeros(5, np.uint32), np.ones(20, np.uint32)]
+    with pytest.raises(ShadowGpuError) as e:
+        ib.run(_dev(host, np.uint32, np.int32), _dev(np.full(25, T0 + MS), np.uint64, np.int64),
+               _dev(np.arange(25), np.uint32, np.int32), _dev(np.full(25, 100), np.uint32, np.int32), T0 + 10 * MS,
+               0, T0 + 10**12, torch.zeros(32, dtype=torch.int64, device="cuda"),
+               torch.zeros(32, dtype=torch.uint8, device="cuda"))
+    assert e.value.code == _capi.SG_ERR_CAPACITY

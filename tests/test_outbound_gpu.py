@@ -240,3 +240,57 @@ def test_sent_capacity_and_order_errors(ctx):
     with pytest.raises(ShadowGpuError) as e:
         ob.run(*args, T0 + MS, 0, T0 + 10**12, f, s)
     assert e.value.code == _capi.SG_ERR_UNSORTED
+
+
+def test_groups_locals_and_long_hosts(oracle, ctx):
+    """Sends on a microsecond grid (same-time groups: one task and id each), local
+    sends between non-local ones (no tokens; the bucket's refill time stays at the
+    last non-local send), hosts with thousands of sends across chunks, a bootstrap
+    boundary inside a window, and a few slow relays that block beside unthrottled
+    ones; three windows."""
+    import torch
+
+    H = 1500
+    hosts = synth.make_hosts(H, 64, exact_seeds=False)
+    rng = np.random.default_rng(77)
+    bw = np.where(rng.random(H) < 0.05, 2 * 10**6, 10**9).astype(np.uint64)
+    ob = OutboundPipeline(hosts["ip"], bw, 8192, ctx=ctx)
+    ost = oracle.outbound_state(hosts["ip"], bw, ob.cap)
+    per = 30000
+    n_pk = 3 * (per + 5000)
+    fwd_g = torch.full((n_pk,), -1, dtype=torch.int64, device="cuda")
+    st_g = torch.zeros(n_pk, dtype=torch.uint8, device="cuda")
+    ctr_g = torch.zeros(H, dtype=torch.int64, device="cuda")
+    fwd_o, st_o, ctr_o = np.full(n_pk, np.uint64(2**64 - 1)), np.zeros(n_pk, np.uint8), np.zeros(H, np.uint64)
+    boot, sim_end = T0 + 25 * MS, T0 + 10**12
+    p0 = 0
+    for w in range(3):
+        t0, t1 = T0 + w * 20 * MS, T0 + (w + 1) * 20 * MS
+        host, t, ln, pay, dst = _sends(hosts, per, t0, t1 - 1000, seed=900 + w, p_local=0.15)
+        # two long hosts (several chunks each), times on a 1-us grid
+        host = np.r_[host, np.full(2000, 3, np.uint32), np.full(3000, 900, np.uint32)].astype(np.uint32)
+        t = np.r_[t, rng.integers(t0, t1 - 1000, 5000).astype(np.uint64)]
+        ln = np.r_[ln, rng.integers(40, 1500, 5000).astype(np.uint32)]
+        pay = np.r_[pay, np.full(5000, 100, np.uint32)]
+        dst = np.r_[dst, np.where(rng.random(5000) < 0.1, hosts["ip"][host[-5000:]], hosts["ip"][(host[-5000:] + 1) % H])]
+        t = (t // 1000 * 1000).astype(np.uint64)
+        o = np.lexsort((t, host))
+        host, t, ln, pay, dst = host[o], t[o], ln[o], pay[o], dst[o].astype(np.uint32)
+        pkt = np.arange(p0, p0 + len(host), dtype=np.uint32)
+        p0 += len(host)
+        batch, ids = ob.run(_dev(host, np.uint32, np.int32), _dev(t, np.uint64, np.int64),
+                            _dev(pkt, np.uint32, np.int32), _dev(ln, np.uint32, np.int32),
+                            _dev(pay, np.uint32, np.int32), _dev(dst, np.uint32, np.int32), t1, boot, sim_end,
+                            fwd_g, st_g, ctr_g.data_ptr())
+        want = oracle.outbound_run(ost, host, t, pkt, ln, pay, dst, t1, boot, sim_end, ctr_o, fwd_o, st_o)
+        assert np.array_equal(st_g.cpu().numpy(), st_o)
+        m = st_o != 0
+        assert np.array_equal(fwd_g.cpu().numpy().view(np.uint64)[m], fwd_o[m])
+        assert np.array_equal(ctr_g.cpu().numpy().view(np.uint64), ctr_o)
+        assert np.array_equal(ids.cpu().numpy().view(np.uint32), want["packet"])
+        assert np.array_equal(batch.send_time_ns.cpu().numpy().view(np.uint64), want["send_time"])
+        got = ob.get_state()
+        for k in RKEYS:
+            assert np.array_equal(got[k], ost[k]), k
+        _live_same(got, ost)
+    assert (st_o == 3).any() or (st_o == 2).any()
