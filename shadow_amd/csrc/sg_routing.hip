@@ -1583,11 +1583,15 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   // 0.76 ms unbounded, a 2,000-node build 0.45 against 0.43; 2,500 rows 1.30
   // against 1.38, a 4,000-node build 0.97 against 1.07).  SG_SSSP_SEEDS=0 never, =2 always.
   const int seeds_env = env_int("SG_SSSP_SEEDS", 1);
-  // Flagged rows (SG_SSSP_FLAGGED=1; sg_sssp.hip): the plan's rows in ONE launch, in phase
-  // order, each row taking the bound rows already published when it starts -- no phase
-  // boundaries, so the bounds pay even with few rows per CU (a rank's row block)
-  const int flag_env = env_int("SG_SSSP_FLAGGED", 0);
-  const bool flagged = seeds_env != 0 && flag_env == 1;
+  // Flagged rows (sg_sssp.hip): the plan's rows in ONE launch, in phase order, each row
+  // taking the bound rows already published when it starts -- no phase boundaries, so the
+  // bounds pay even with few rows per CU.  The default for a row block (a rank's share of a
+  // sharded build, or a RoutingInfo fill block); the whole table keeps the phased launches,
+  // which it builds as fast (one box, tools/sssp_ab.py, C3 graph, tables bit-identical:
+  // 10k rows 3.187 against 3.185 ms; row blocks of 5,000 1.93 against 1.99, 2,500 1.13
+  // against 1.20, 1,250 0.685 against 0.706).  SG_SSSP_FLAGGED=0 / 1 forces it.
+  const int flag_env = env_int("SG_SSSP_FLAGGED", -1);
+  const bool flagged = seeds_env != 0 && (flag_env == 1 || (flag_env < 0 && rows < n_used));
   const bool phased = !flagged && seeds_env != 0 && (seeds_env == 2 || rows >= 8u * (uint32_t)ctx->n_cu);
   if (!phased && !flagged) SG_HIP(hipMemsetAsync(sat, 0, rows * 4ull, st));
   if (flagged) {

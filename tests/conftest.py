@@ -30,8 +30,9 @@ def ctx():
 
 
 # Shortest-path kernels the routing tests run on.  The defaults: the per-source LDS search
-# (sg_sssp.hip) in its unbounded and forced bounded-phase forms (the build picks phases from
-# 8 rows per CU on, i.e. at C3), its flagged one-launch form (bound rows taken once published),
+# (sg_sssp.hip) as the build chooses it (whole tables: phases from 8 rows per CU on, i.e. at C3;
+# row blocks: the flagged one-launch plan), its forced bounded-phase form, its forced flagged
+# one-launch form (bound rows taken once published),
 # and the slab relaxation (graphs past the LDS; SG_APSP_LDS=0 also forces it on dense graphs,
 # which otherwise take the register-resident search of sg_dense.hip).
 # The non-default option (landmarks) runs in test_option_kernels, or on the whole matrix with
@@ -47,5 +48,8 @@ def set_apsp_kernel(monkeypatch, name: str) -> str:
     monkeypatch.setenv("SG_APSP_LDS", "0" if name == "slab" else "1")
     monkeypatch.setenv("SG_SSSP_SEEDS", "2" if name in ("lds_bounded", "lds_landmarks") else "1")
     monkeypatch.setenv("SG_SSSP_LANDMARKS", "8" if name == "lds_landmarks" else "0")
-    monkeypatch.setenv("SG_SSSP_FLAGGED", "1" if name == "lds_flagged" else "0")
+    if name == "lds":  # the default choice (flagged one-launch plan for row blocks, phases for whole tables)
+        monkeypatch.delenv("SG_SSSP_FLAGGED", raising=False)
+    else:
+        monkeypatch.setenv("SG_SSSP_FLAGGED", "1" if name == "lds_flagged" else "0")
     return "slab" if name == "slab" else "lds"

@@ -23,12 +23,15 @@ def _status(n):
 def _same_state(O, got, want):
     for k in KEYS:
         assert np.array_equal(got[k], want[k]), k
+    # live ring slots only: [head, tail) per host
     cap = want["cap"]
-    for h in range(len(want["head"])):  # live ring slots only
-        for c in range(int(want["head"][h]), int(want["tail"][h])):
-            s = h * cap + (c % cap)
-            assert (got["ring_pkt"][s], got["ring_ts"][s], got["ring_len"][s]) == \
-                (want["ring_pkt"][s], want["ring_ts"][s], want["ring_len"][s])
+    lo = want["head"].astype(np.int64)
+    n = want["tail"].astype(np.int64) - lo
+    hh = np.repeat(np.arange(len(n)), n)
+    c = lo[hh] + np.arange(int(n.sum())) - np.repeat(np.cumsum(n) - n, n)
+    i = hh * cap + (c % cap)
+    for k in ("ring_pkt", "ring_ts", "ring_len"):
+        assert np.array_equal(got[k][i], want[k][i]), k
 
 
 def _run_both(O, q, ostate, gstat, ostat, host, kind, t, pkt, ln):
