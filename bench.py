@@ -188,6 +188,7 @@ def load_pmc(path):
 
 
 SERVICE_NS = 12_000  # 1500 B at 1 Gbit/s: the interface's pop spacing in the CoDel leg
+SUB_MS_REPS = 100  # timed repetitions of the sub-millisecond legs (delivery round, CoDel batch) at least
 
 
 def codel_events(offsets, order, deliver_time, length):
@@ -252,7 +253,7 @@ def codel_leg(a, D, ctx, torch, buckets, n_packets, pmc):
     def step():
         q.run(ev, status)
 
-    t = timed(D, step, a.steps, a.warmup)
+    t = timed(D, step, max(a.steps, SUB_MS_REPS), a.warmup)
     q.set_state(state0)
     ctx.enable_timers(True)
     _, n_drop = q.run(ev, status)
@@ -872,7 +873,8 @@ def main():
             else:
                 deliver_round(ht, table, batch, round_end, sim_end, 0, out=out, ctx=ctx)
 
-        t_round = timed(D, rnd, a.steps, a.warmup)
+        # a round is ~0.1 ms: at least 100 of them, so one host-side hiccup moves the mean little
+        t_round = timed(D, rnd, max(a.steps, SUB_MS_REPS), a.warmup)
         per_rank = None
         if sharded:  # load balance of the host partition: packets sent, records sent / received per rank
             mine_c = [float(a.packets), float(sum(sharded.last_send_counts)), float(sum(sharded.last_recv_counts))]

@@ -56,7 +56,7 @@ namespace sg {
 constexpr uint32_t NONE = ~0u;
 constexpr int SMALL_BUCKET = 32;
 constexpr uint32_t INBLOCK_RANK_SMALL = 32;  // region path: rank sort up to this many entries per slot,
-constexpr uint32_t WAVE_SORT_MAX = 256;      // one wave's register rank sort up to this many, the block's beyond
+constexpr uint32_t WAVE_SORT_MAX = 256;      // in-wave bitonic sort up to this many, the block's beyond
 // (up to 4 keys per lane: 8 took the region sort to 256 VGPRs, one block per CU)
 constexpr int SORT_BLOCK = 256;
 constexpr int SORT_CHUNK = 2048;  // elements sorted in LDS per chunk
@@ -1071,47 +1071,96 @@ __device__ __forceinline__ void slot_bitonic(const uint64_t* Tt, const uint64_t*
   __syncthreads();
 }
 
-// One wave ranks one slot's m entries [b, b + m) (m <= 64 R): lane l holds
-// elements l, l + 64, .., l + 64 (R - 1) in registers, and every element q is
-// broadcast to the wave in turn (v_readlane into scalar registers) and compared
-// with the lane's own: rank = #(elements of the slot below it), unique keys, so
-// the ranks are the slot's order.  m independent steps of a few instructions, no
-// LDS traffic and no dependent chain: a register bitonic network (r04c) spent its
-// time in 28 dependent lane shuffles per slot (C5: 10.6 us of a 22 us block).
-// CK: one compressed u64 key per entry ((t - t_min) << 32 | value, unique), the
-// value its low word; else (t, k) pairs, k the record's order key or the value.
+// In-wave bitonic sort of one slot's m entries [b, b + m) (m <= 64 R),
+// keys in registers: lane l holds elements l, l + 64, ..., l + 64 (R - 1); the
+// network's exchanges at distance < 64 are lane shuffles, at 64 and above register
+// swaps in the lane.  CK: one compressed u64 key per entry ((t - t_min) << 32 |
+// value, unique), the value is its low word.  Else (t, k) pairs and the value
+// ride along (k = the record's order key, or the value itself).  Pads (~0) sort
+// last: every real key is below ~0 (arrival times stop at EMUTIME_MAX).  No
+// barrier: one wave sorts a slot while the block's other waves sort others, where
+// the rank sort cost m LDS reads per entry (C5: ~100-entry slots, the round's
+// second-largest cost) and the block-wide bitonic a barrier per step.
 template <int R, bool KK, bool CK>
-__device__ __forceinline__ void wave_rank_slot(const uint64_t* Tt, const uint64_t* Tk, const uint32_t* Ti, uint32_t b,
+__device__ __forceinline__ void wave_sort_slot(const uint64_t* Tt, const uint64_t* Tk, const uint32_t* Ti, uint32_t b,
                                                uint32_t m, uint32_t* __restrict__ out) {
+  constexpr uint32_t M = 64u * R;
   const uint32_t lane = threadIdx.x & 63;
   uint64_t t[R], k[R];
-  uint32_t v[R], rank[R];
+  uint32_t v[R];
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const uint32_t i = lane + 64u * r;
-    const uint32_t p = b + (i < m ? i : 0u);  // branch-free reads
-    t[r] = Tt[p];
-    v[r] = Ti[p];
-    k[r] = CK ? 0ull : KK ? Tk[p] : (uint64_t)v[r];
-    rank[r] = 0;
+    const bool ok = i < m;
+    const uint32_t p = b + (ok ? i : 0u);  // branch-free reads; pads replace the value
+    const uint64_t tt = Tt[p];
+    const uint32_t vv = Ti[p];
+    t[r] = ok ? tt : ~0ull;
+    v[r] = vv;
+    if constexpr (!CK) {
+      const uint64_t kk = KK ? Tk[p] : (uint64_t)vv;
+      k[r] = ok ? kk : ~0ull;
+    }
   }
-  auto bcast = [](uint64_t x, uint32_t l) {
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)l) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)l);
+  auto less = [&](uint64_t ta, uint64_t ka, uint64_t tb, uint64_t kb) {
+    if constexpr (CK) return ta < tb;
+    else return ta < tb || (ta == tb && ka < kb);
   };
 #pragma unroll
-  for (int rq = 0; rq < R; rq++) {
-    const uint32_t qn = m > 64u * rq ? min(m - 64u * rq, 64u) : 0u;  // elements held in register rq
-    for (uint32_t l = 0; l < qn; l++) {
-      const uint64_t yt = bcast(t[rq], l);
-      const uint64_t yk = CK ? 0ull : bcast(k[rq], l);
+  for (uint32_t kk2 = 2; kk2 <= M; kk2 <<= 1) {
 #pragma unroll
-      for (int r = 0; r < R; r++) rank[r] += CK ? (yt < t[r]) : (yt < t[r] || (yt == t[r] && yk < k[r]));
+    for (uint32_t j = kk2 >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {  // partner in this lane's register r ^ (j / 64)
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const int r2 = r ^ (int)(j >> 6);
+          if (r2 <= r) continue;
+          const bool asc = ((lane + 64u * r) & kk2) == 0;
+          const bool lt21 = less(t[r2], CK ? 0 : k[r2], t[r], CK ? 0 : k[r]);
+          const bool lt12 = less(t[r], CK ? 0 : k[r], t[r2], CK ? 0 : k[r2]);
+          if (asc ? lt21 : lt12) {
+            const uint64_t xt = t[r];
+            t[r] = t[r2];
+            t[r2] = xt;
+            if constexpr (!CK) {
+              const uint64_t xk = k[r];
+              k[r] = k[r2];
+              k[r2] = xk;
+              const uint32_t xv = v[r];
+              v[r] = v[r2];
+              v[r2] = xv;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const uint32_t i = lane + 64u * r;
+          const uint64_t ot = __shfl_xor((unsigned long long)t[r], (int)j, 64);
+          uint64_t ok = 0;
+          uint32_t ov = 0;
+          if constexpr (!CK) {
+            ok = __shfl_xor((unsigned long long)k[r], (int)j, 64);
+            ov = __shfl_xor(v[r], (int)j, 64);
+          }
+          const bool want_min = ((i & j) == 0) == ((i & kk2) == 0);
+          const bool o_lt = less(ot, ok, t[r], CK ? 0 : k[r]);
+          if (want_min == o_lt) {  // take the partner's element (equal keys: pads, identical)
+            t[r] = ot;
+            if constexpr (!CK) {
+              k[r] = ok;
+              v[r] = ov;
+            }
+          }
+        }
+      }
     }
   }
 #pragma unroll
-  for (int r = 0; r < R; r++)
-    if (lane + 64u * r < m) out[rank[r]] = CK ? (uint32_t)t[r] : v[r];
+  for (int r = 0; r < R; r++) {
+    const uint32_t i = lane + 64u * r;
+    if (i < m) out[i] = CK ? (uint32_t)t[r] : v[r];
+  }
 }
 
 // Per-slot order of a placed super-bucket (slot j = entries [cnt[j], cnt[j+1])
@@ -1126,20 +1175,14 @@ __device__ __forceinline__ void slot_orders(uint64_t* Tt, uint64_t* Tk, uint32_t
                                             uint32_t ns, uint32_t d0, uint32_t nd, const uint32_t* cnt,
                                             uint64_t* __restrict__ kt, uint64_t* __restrict__ kk,
                                             uint32_t* __restrict__ ki, uint32_t* __restrict__ order,
-                                            uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count,
-                                            unsigned long long* __restrict__ dg = nullptr) {
+                                            uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
   static_assert(LDS || !INBLOCK, "in-block big-slot sort needs the LDS copy");
-  // SG_SORT_DIAG: wall-clock stamps of the phases (thread 0, after a barrier)
-  auto stamp = [&](int k) {
-    if (dg && threadIdx.x == 0) dg[k] = wall_clock64();
-  };
   // In-block (region path), slots up to INBLOCK_RANK_MAX are rank-sorted too:
   // a slot's rank sort runs in parallel with every other slot's, where each
   // bitonic slot takes the whole block through log2(m)^2 / 2 barriers in turn
   // (C5: about 100 entries per destination, 1.9 ms of bitonic slots per round).
-  // In-block: slots up to INBLOCK_RANK_SMALL entries are rank-sorted one thread per
-  // entry, up to WAVE_SORT_MAX ranked by one wave each in registers (wave_rank_slot),
-  // larger ones bitonic-sorted by the block.
+  // In-block: slots up to INBLOCK_RANK_SMALL entries are rank-sorted, up to
+  // WAVE_SORT_MAX sorted by one wave each in registers, larger ones by the block.
   constexpr uint32_t SMALL = INBLOCK ? INBLOCK_RANK_SMALL : SMALL_BUCKET;
   constexpr uint32_t MAX_BIG = SB_CAP<KK> / (WAVE_SORT_MAX + 1) + 1;
   constexpr uint32_t MAX_WAVE = SB_CAP<KK> / (SMALL + 1) + 1;
@@ -1151,7 +1194,6 @@ __device__ __forceinline__ void slot_orders(uint64_t* Tt, uint64_t* Tk, uint32_t
     n_wave = 0;
   }
   __syncthreads();  // placement complete
-  stamp(3);
   for (uint32_t j = threadIdx.x; j < nd; j += SBT_THREADS) {
     const uint32_t b = cnt[j], e = cnt[j + 1];
     if (e - b > SMALL) {
@@ -1210,21 +1252,19 @@ __device__ __forceinline__ void slot_orders(uint64_t* Tt, uint64_t* Tk, uint32_t
   }
   if constexpr (INBLOCK) {
     __syncthreads();  // n_wave is final (it was before the rank sort too; this orders the reads)
-    stamp(4);
     for (uint32_t u = threadIdx.x >> 6; u < n_wave; u += SBT_THREADS / 64) {  // one wave per slot
       const uint32_t j = wslots[u], b = cnt[j], m = cnt[j + 1] - b;
       uint32_t* o = order + s0 + b;
       if (m <= 64)
-        wave_rank_slot<1, KK, CK>(Tt, Tk, Ti, b, m, o);
+        wave_sort_slot<1, KK, CK>(Tt, Tk, Ti, b, m, o);
       else if (m <= 128)
-        wave_rank_slot<2, KK, CK>(Tt, Tk, Ti, b, m, o);
+        wave_sort_slot<2, KK, CK>(Tt, Tk, Ti, b, m, o);
       else
-        wave_rank_slot<4, KK, CK>(Tt, Tk, Ti, b, m, o);
+        wave_sort_slot<4, KK, CK>(Tt, Tk, Ti, b, m, o);
     }
   }
   if (INBLOCK) {
     __syncthreads();  // Ts is free: it becomes the index array
-    stamp(5);
     for (uint32_t u = 0; u < n_big; u++) {
       const uint32_t j = bigs[u], b = cnt[j];
       slot_bitonic<KK>(Tt, Tk, Ti, Ts, b, cnt[j + 1] - b, order + s0 + b);
@@ -1346,10 +1386,8 @@ __global__ void __launch_bounds__(SBT_THREADS)
                      uint32_t* __restrict__ ki, uint32_t* __restrict__ offsets, uint32_t* __restrict__ order,
                      uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count,
                      uint16_t* __restrict__ slot_spill, sg_round_ret* __restrict__ ret,
-                     const uint32_t* __restrict__ pre, unsigned long long* __restrict__ diag) {
+                     const uint32_t* __restrict__ pre) {
   __shared__ uint32_t part[SBT_THREADS / 64];
-  unsigned long long* dg = diag ? diag + 8 * (size_t)blockIdx.x : nullptr;
-  if (dg && threadIdx.x == 0) dg[0] = wall_clock64();
   const uint32_t over = ctl[SB_FLAG];
   // the next parity's counters zeroed and the overflow flag published after this
   // kernel's loads: stores ahead of them made every later load wait for the stores too
@@ -1443,7 +1481,6 @@ __global__ void __launch_bounds__(SBT_THREADS)
       hi = max(hi, (uint64_t)thi[w]);
     }
     ck = ns > 0 && hi - lo < (1ull << 32);
-    if (dg && threadIdx.x == 0) dg[1] = wall_clock64();
     if (ck)
 #pragma unroll
       for (int k = 0; k < PER; k++) vt[k] = ((vt[k] - lo) << 32) | vi[k];
@@ -1460,7 +1497,6 @@ __global__ void __launch_bounds__(SBT_THREADS)
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < nd; j += SBT_THREADS) offsets[d0 + j] = s0 + cnt[j];
   if (d0 + nd == n_slots && threadIdx.x == 0) offsets[n_slots] = s0 + ns;
-  if (dg && threadIdx.x == 0) dg[2] = wall_clock64();
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     if (vd[k] == NONE) continue;
@@ -1471,45 +1507,10 @@ __global__ void __launch_bounds__(SBT_THREADS)
     ss[p] = (uint16_t)vd[k];
   }
   if (ck)  // uniform per block
-    slot_orders<true, KK, true, true>(st, sk, si, ss, s0, ns, d0, nd, cnt, kt, kk, ki, order, big_list, big_count, dg);
+    slot_orders<true, KK, true, true>(st, sk, si, ss, s0, ns, d0, nd, cnt, kt, kk, ki, order, big_list, big_count);
   else
-    slot_orders<true, KK, true>(st, sk, si, ss, s0, ns, d0, nd, cnt, kt, kk, ki, order, big_list, big_count, dg);
-  if (dg) {
-    __syncthreads();
-    if (threadIdx.x == 0) dg[6] = wall_clock64();
-  }
+    slot_orders<true, KK, true>(st, sk, si, ss, s0, ns, d0, nd, cnt, kt, kk, ki, order, big_list, big_count);
   epilogue();
-}
-
-// SG_SORT_DIAG=1: per-block phase stamps of k_sb_sort_region on stderr (a diagnostic:
-// a synchronous copy after the launch; never set in a measured run).  Stamps (100 MHz
-// wall clock): 0 start, 1 loads in, 2 counted and offsets out, 3 placed, 4 rank sort
-// done, 5 wave sorts done, 6 block sorts done.
-static unsigned long long* sort_diag_alloc(uint32_t nb) {
-  const char* e = getenv("SG_SORT_DIAG");
-  if (!e || atoi(e) == 0) return nullptr;
-  unsigned long long* d = nullptr;
-  SG_HIP(hipMalloc(&d, (size_t)nb * 64));
-  SG_HIP(hipMemset(d, 0, (size_t)nb * 64));
-  return d;
-}
-static void sort_diag_report(hipStream_t st, unsigned long long* d, uint32_t nb) {
-  if (!d) return;
-  std::vector<unsigned long long> h((size_t)nb * 8);
-  SG_HIP(hipStreamSynchronize(st));
-  SG_HIP(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
-  (void)hipFree(d);
-  uint64_t t_min = ~0ull, t_max = 0;
-  double ph[6] = {0, 0, 0, 0, 0, 0}, dur = 0;
-  for (uint32_t b = 0; b < nb; b++) {
-    const unsigned long long* x = &h[8 * (size_t)b];
-    t_min = std::min<uint64_t>(t_min, x[0]);
-    t_max = std::max<uint64_t>(t_max, x[6]);
-    for (int k = 0; k < 6; k++) ph[k] += (x[k + 1] > x[k] ? (double)(x[k + 1] - x[k]) : 0.0) * 0.01 / nb;
-    dur += (double)(x[6] - x[0]) * 0.01 / nb;
-  }
-  fprintf(stderr, "[sort] %u blocks, span %.1f us, block mean %.2f us: loads %.2f, count %.2f, place %.2f, rank %.2f, "
-          "wave %.2f, block %.2f\n", nb, (t_max - t_min) * 0.01, dur, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
 }
 
 // Bucket sort of n entries into n_slots destination slots (see above).
@@ -1602,15 +1603,13 @@ static bool bucket_sort(sg_ctx* ctx, E src, uint32_t n, uint32_t n_slots, uint32
     }
     // many super-buckets: their output starts from one scan, not a sum per sort block
     uint32_t* pre = n_sb > 512 ? ctx->d_cur.get<uint32_t>(n_sb) : nullptr;
-    unsigned long long* sort_diag = sort_diag_alloc(n_sb);
     if (pre) hipLaunchKernelGGL(k_sb_prefix, dim3(1), dim3(1024), 0, st, ctl, n_sb, pre);
     {
       TimedLaunch tl(ctx, "sort_small", 24.0 * n + 4.0 * n_slots);
       hipLaunchKernelGGL(k_sb_sort_region<E::KK>, dim3(n_sb), dim3(SBT_THREADS), 0, st, sm, n_slots, n_sb, ctl,
                          ctl_next, reg, rd, rt, rk, ri, kt, kk, ki, offsets, order, big_list, big_count, spill,
-                         ctx->round_ret, (const uint32_t*)pre, sort_diag);
+                         ctx->round_ret, (const uint32_t*)pre);
     }
-    sort_diag_report(st, sort_diag, n_sb);
   } else {
     const size_t nh = (size_t)n_sb * n_tiles;
     uint32_t* hist = ctx->d_cnt.get<uint32_t>(nh + 1);
