@@ -45,13 +45,18 @@ def _run_both(O, q, ostate, gstat, ostat, host, kind, t, pkt, ln):
     return want
 
 
+def _host_times(host, gaps, t0):
+    """Per host (host sorted): t0 + the running sum of its own gaps (a segmented cumsum)."""
+    c = np.cumsum(gaps.astype(np.int64))
+    first = np.r_[True, host[1:] != host[:-1]]
+    base = np.maximum.accumulate(np.where(first, c - gaps, 0))
+    return (t0 + c - base).astype(np.uint64)
+
+
 def _stream(rng, H, E, t0, gap_ms, p_pop, n_pkt0=0):
     host = np.sort(rng.integers(0, H, E)).astype(np.uint32)
     kind = (rng.random(E) < p_pop).astype(np.uint8)
-    t = np.zeros(E, np.uint64)
-    for h in np.unique(host):
-        idx = np.nonzero(host == h)[0]
-        t[idx] = t0 + np.cumsum(rng.integers(0, gap_ms * MS, len(idx))).astype(np.uint64)
+    t = _host_times(host, rng.integers(0, gap_ms * MS, E), t0)
     pkt = (n_pkt0 + np.arange(E)).astype(np.uint32)
     ln = rng.integers(40, 1500, E).astype(np.uint32)
     return host, kind, t, pkt, ln
@@ -181,11 +186,7 @@ def test_good_state_mix(oracle, ctx):
         host[3000: 5500] = 1000 + c
         host = np.sort(host)
         kind = (rng.random(E) < np.where(slow[host], 0.3, 0.5)).astype(np.uint8)
-        t = np.zeros(E, np.uint64)
-        for h in np.unique(host):
-            idx = np.nonzero(host == h)[0]
-            gap = 4 * MS if slow[h] else 2000
-            t[idx] = t0 + np.cumsum(rng.integers(0, gap, len(idx))).astype(np.uint64)
+        t = _host_times(host, rng.integers(0, np.where(slow[host], 4 * MS, 2000)), t0)
         pkt = (c * E + np.arange(E)).astype(np.uint32)
         ln = rng.integers(40, 1500, E).astype(np.uint32)
         _run_both(oracle, q, os_, gstat, ostat, host, kind, t, pkt, ln)
