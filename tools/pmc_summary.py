@@ -21,8 +21,10 @@ import os
 from collections import defaultdict
 
 # first match wins: k_relax_wide before the k_relax<...> template instances
-KERNELS = {"relax_wide": "k_relax_wide", "sssp_fill": "k_sssp_lds<false, 1024, 8, 1>",
-           "sssp_count": "k_sssp_lds<true", "sssp": "k_sssp_lds<false, 1024, 8, 0>", "relax": "k_relax_w2<", "relax1": "k_relax_w<", "out": "k_out_batch", "walk": "k_walk",
+KERNELS = {"relax_wide": "k_relax_wide", "sssp_fill": "k_sssp_lds<false, 1024, 8, 1, false>",
+           "sssp_fill_flagged": "k_sssp_lds<false, 1024, 8, 1, true>",
+           "sssp_count": "k_sssp_lds<true", "sssp": "k_sssp_lds<false, 1024, 8, 0, false>",
+           "sssp_flagged": "k_sssp_lds<false, 1024, 8, 0, true>", "relax": "k_relax_w2<", "relax1": "k_relax_w<", "out": "k_out_batch", "walk": "k_walk",
            "sb_hist": "k_sb_hist", "sb_scatter": "k_sb_scatter", "sb_sort_region": "k_sb_sort_region",
            "sb_sort": "k_sb_sort", "sort_big": "k_sort_big", "host_off": "k_host_off", "reduce_stats": "k_reduce_stats",
            "table_pack": "k_table_pack", "codel_reduce": "k_codel_reduce", "codel": "k_codel",
