@@ -276,13 +276,16 @@ __device__ __forceinline__ void lane_diag_store(unsigned long long* d, uint64_t 
 __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
   const uint64_t d_t0 = a.bdiag ? wall_clock64() : 0;
   uint64_t d_walk = 0;
-  // staged chunk: 22 KB, so 7 one-wave blocks fit a CU (1792 >= the 1563 blocks of a 100k-host call)
+  // Staged chunk, 18 KB (8 one-wave blocks fit a CU): the chunk's pushes in push order
+  // from the front of s_t / s_p / s_l (time, packet, length), its pops in pop order from
+  // the back (time, result, pushes before the pop), so a walk step reads its element and
+  // its next pop's fields directly -- no index list between (r03: an index read, then the
+  // data, at every pop and every push accounted)
   __shared__ uint64_t s_t[CD_CHUNK];
-  __shared__ uint32_t s_p[CD_CHUNK];  // pushed packet; a pop event's slot receives its result
+  __shared__ uint32_t s_p[CD_CHUNK];
   __shared__ uint32_t s_l[CD_CHUNK];
   __shared__ uint16_t s_pp[CD_CHUNK + 1];  // pushes before each staged event (kind k = s_pp[k + 1] - s_pp[k])
-  __shared__ uint16_t s_pi[CD_CHUNK];      // staged index of the chunk's r-th push
-  __shared__ uint16_t s_qi[CD_CHUNK];      // staged index of the chunk's r-th pop
+  auto pop_at = [](uint32_t r) { return (uint32_t)CD_CHUNK - 1u - r; };  // the r-th pop's slot
   const uint32_t h0 = blockIdx.x * CD_HOSTS, t = threadIdx.x;
   const uint32_t p0 = min(a.host_off[min(h0, a.H)], a.E);
   const uint32_t p1 = max(min(a.host_off[min(h0 + CD_HOSTS, a.H)], a.E), p0);
@@ -332,12 +335,11 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
           const uint32_t rank = run + (uint32_t)__popcll(m & lt);
           if (in) {
             const uint32_t k = i - c0;
-            s_t[k] = rt[u];
-            s_p[k] = rp[u];
-            s_l[k] = rl[u];
+            const uint32_t slot = push ? rank : pop_at(k - rank);
+            s_t[slot] = rt[u];
+            s_p[slot] = rp[u];
+            s_l[slot] = push ? rl[u] : rank;
             s_pp[k] = (uint16_t)rank;
-            if (push) s_pi[rank] = (uint16_t)k;
-            else s_qi[k - rank] = (uint16_t)k;
           }
           run += (uint32_t)__popcll(m);
         }
@@ -356,29 +358,25 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
       const uint32_t kb = b < e ? b - c0 : 0, ke = b < e ? e - c0 : 0;
       const uint32_t pb = kb < ke ? s_pp[kb] : 0, pe = kb < ke ? s_pp[ke] : 0;
       const uint32_t rb = kb - pb, re = ke - pe;  // this host's pop ranks [rb, re)
-      lds_u16* wi = (lds_u16*)s_pi + pb;
-      q.begin_window((lds_u32*)s_p, (lds_u32*)s_l, (lds_u64*)s_t, wi, kb);
+      // the window's j-th push is push slot pb + j
+      q.begin_window((lds_u32*)s_p, (lds_u32*)s_l, (lds_u64*)s_t, nullptr, pb);
       uint32_t seen = 0;  // window pushes accounted
       auto account = [&](uint32_t upto) {  // the window's pushes [seen, upto) enter the queue
-        for (; seen < upto; seen++) q.bytes += s_l[wi[seen]];
+        for (; seen < upto; seen++) q.bytes += s_l[pb + seen];
         q.tail = q.t0 + upto;
         if (q.tail - q.head > q.mask + 1u) q.err |= E_FULL;  // a push found the ring full
         if (!q.hv) q.load_head();
       };
-      // the next pop's staged index and fields are read a step ahead, its
-      // successor's index two steps ahead
-      uint32_t k1 = rb < re ? s_qi[rb] : 0, k2 = rb + 1 < re ? s_qi[rb + 1] : 0;
-      uint64_t t1 = rb < re ? s_t[k1] : 0;
-      uint32_t pp1 = rb < re ? s_pp[k1] : 0;
+      // the next pop's fields are read a step ahead
+      uint64_t t1 = rb < re ? s_t[pop_at(rb)] : 0;
+      uint32_t pp1 = rb < re ? s_l[pop_at(rb)] : 0;
       for (uint32_t r = rb; r < re; r++) {
-        const uint32_t k = k1, pp = pp1;
+        const uint32_t k = pop_at(r), pp = pp1;
         const uint64_t now = t1;
-        k1 = k2;
         if (r + 1 < re) {
-          t1 = s_t[k1];
-          pp1 = s_pp[k1];
+          t1 = s_t[pop_at(r + 1)];
+          pp1 = s_l[pop_at(r + 1)];
         }
-        if (r + 2 < re) k2 = s_qi[r + 2];
         account(pp - pb);
         const uint32_t res = q.pop(now);
         // a dequeued packet's status is written with the chunk's results (3. below): a
@@ -391,7 +389,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
       // the window's elements still queued live on in the ring
       const uint32_t w0 = q.head - q.t0 <= q.tail - q.t0 ? q.head - q.t0 : 0;
       for (uint32_t j = w0; j < q.tail - q.t0; j++) {
-        const uint32_t k = wi[j];
+        const uint32_t k = pb + j;
         const uint64_t tk = s_t[k];
         q.ring[(q.t0 + j) & q.mask] = make_uint4(s_p[k], s_l[k], (uint32_t)tk, (uint32_t)(tk >> 32));
       }
@@ -401,7 +399,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
     __syncthreads();
     for (uint32_t i = c0 + t; i < c1; i += CD_THREADS) {  // 3. coalesced results (CD_NONE for a push)
       const uint32_t k = i - c0;
-      const uint32_t r = s_pp[k + 1] != s_pp[k] ? CD_NONE : s_p[k];
+      const uint32_t r = s_pp[k + 1] != s_pp[k] ? CD_NONE : s_p[pop_at(k - s_pp[k])];
       a.pop_result[i] = r;
       if (r < a.n_status) a.status[r] = SG_CODEL_DEQUEUED;  // (CD_NONE >= n_status)
     }
