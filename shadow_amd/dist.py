@@ -46,7 +46,7 @@ def row_range(n_used: int, world: int, rank: int):
     return min(rank * per, n_used), min((rank + 1) * per, n_used), per
 
 
-def balanced_node_order(host_node: Sequence[int], n_nodes: int, world: int, host_weight=None):
+def balanced_node_order(host_node: Sequence[int], n_nodes: int, world: int, host_weight=None, tol=0.05):
     """Row order of the used nodes that balances delivery across `world` rank blocks.
 
     A host is owned by the rank holding its node's routing row, so with the identity
@@ -58,12 +58,24 @@ def balanced_node_order(host_node: Sequence[int], n_nodes: int, world: int, host
     of the senders.  A single node heavier than a rank's share cannot be split (its
     hosts share one routing row) and bounds the balance.
 
+    When the identity order is already balanced (every rank's share within `tol` of
+    the mean) it is kept: a rank's row block is then a run of consecutive node ids,
+    which in a graph numbered with any locality (a ring, a geographic order) holds
+    neighbours of its own rows -- the bound rows a block's search plans from
+    (sg_routing.hip, flagged plan).  Dealt by weight, equal weights go round-robin and
+    a block holds almost no neighbours of its rows, so most of its rows search from
+    infinity (C3 at N = 2: 2.36 against 1.93 ms per block, tools/sssp_ab.py --rows).
+
     Returns (order, route): order[i] = node index of table row i (the `used` list to
     build with), route[h] = table row of host h's node."""
     host_node = np.asarray(host_node, dtype=np.int64)
     w = np.bincount(host_node, weights=None if host_weight is None else np.asarray(host_weight, np.float64),
                     minlength=n_nodes).astype(np.float64)
     per = (n_nodes + world - 1) // max(world, 1)
+    ident = np.array([w[r * per:(r + 1) * per].sum() for r in range(world)])
+    if world <= 1 or ident.max() <= (1.0 + tol) * max(ident.mean(), 1e-300):
+        order = np.arange(n_nodes, dtype=np.uint32)
+        return order, host_node.astype(np.uint32)
     cap = [min(per, max(0, n_nodes - r * per)) for r in range(world)]
     load = np.zeros(world)
     fill = np.zeros(world, np.int64)

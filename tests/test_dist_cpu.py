@@ -308,3 +308,20 @@ def test_two_rank_gloo_padded_exchange_rounds(oracle):
                 seen.add(h)
         assert seen == set(range(hosts["n"]))
     assert modes == ["exact"] * 2 + ["padded"] * 2 + ["padded+exact"] * 2 + ["padded"] * 2, modes
+
+
+def test_balanced_order_keeps_local_blocks():
+    """A host map the identity order already balances keeps it (row blocks stay runs of
+    consecutive nodes, whose neighbours bound the blocks' searches); a skewed one is
+    dealt by weight, each rank within one node's weight of the mean."""
+    order, route = balanced_node_order(np.arange(100_000) % 10_000, 10_000, 8)
+    assert np.array_equal(order, np.arange(10_000)) and np.array_equal(route, np.arange(100_000) % 10_000)
+    node = np.where(np.arange(4000) % 10 < 9, np.arange(4000) % 2, 2 + np.arange(4000) % 198)
+    order, route = balanced_node_order(node, 200, 2)
+    assert not np.array_equal(order, np.arange(200))
+    pos = np.empty(200, np.int64)
+    pos[order] = np.arange(200)
+    load = np.bincount(pos[node] // 100, minlength=2)
+    w = np.bincount(node, minlength=200)
+    assert abs(int(load[0]) - int(load[1])) <= w.max()
+    assert np.array_equal(route, pos[node])
