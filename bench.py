@@ -179,6 +179,17 @@ def _pow2(x):
     return 1 << max(0, int(x) - 1).bit_length()
 
 
+def rocprof_view(pm, bytes_per_launch):
+    """The rocprofv3 kernel-trace average of a kernel (from the PMC summary of the default
+    workload) and the HBM fraction it gives: a HIP-event pair around one launch of a
+    30-50 us kernel also holds the dispatch and completion latency (~10 us)."""
+    ns = pm.get("avg_ns")
+    if not ns or not bytes_per_launch:
+        return None
+    return {"avg_launch_ms": round(ns / 1e6, 4),
+            "frac": round(bytes_per_launch / (ns / 1e9) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def load_pmc(path):
     try:
         with open(path) as f:
@@ -271,7 +282,8 @@ def codel_leg(a, D, ctx, torch, buckets, n_packets, pmc):
                    "hosts": H, "events": E, "pushes": nd},
         "roofline": {"kernel": "k_codel", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pm.get("hbm_bytes_per_launch"),
-                     "avg_launch_ms": round(k_s * 1e3, 4), "valu_frac_pmc": pm.get("valu_frac")},
+                     "avg_launch_ms": round(k_s * 1e3, 4), "valu_frac_pmc": pm.get("valu_frac"),
+                     "rocprof": rocprof_view(pm, k_bytes / max(k_n, 1))},
         "dropped": n_drop,
     }
     if D.rank == 0 and D.world == 1 and not a.no_cpu:
@@ -349,7 +361,8 @@ def outbound_leg(a, D, ctx, torch, pk, hosts, ht, table, round_end, sharded, pmc
         "roofline": {"kernel": "k_outbound", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                      "traffic": pmc.get("outbound", {}).get("hbm_bytes_per_launch"),
-                     "avg_launch_ms": round(k_s * 1e3, 4), "valu_frac_pmc": pmc.get("outbound", {}).get("valu_frac")},
+                     "avg_launch_ms": round(k_s * 1e3, 4), "valu_frac_pmc": pmc.get("outbound", {}).get("valu_frac"),
+                     "rocprof": rocprof_view(pmc.get("outbound", {}), k_bytes / max(k_n, 1))},
         "compact_ms": round(c_ms / max(c_n, 1), 4),
         "sent": len(batch),
         "fused_round": {"ms": round(t_fused * 1e3, 4), "packets_per_s": round(D.sum(float(n)) / t_fused, 1),
@@ -419,7 +432,8 @@ def inbound_leg(a, D, ctx, torch, buckets, n_packets, pmc, round_end):
         "roofline": {"kernel": "k_inbound", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                      "traffic": pmc.get("inbound", {}).get("hbm_bytes_per_launch"), "avg_launch_ms": round(k_s * 1e3, 4),
-                     "valu_frac_pmc": pmc.get("inbound", {}).get("valu_frac")},
+                     "valu_frac_pmc": pmc.get("inbound", {}).get("valu_frac"),
+                     "rocprof": rocprof_view(pmc.get("inbound", {}), k_bytes / max(k_n, 1))},
         "forwarded": n_fwd, "dropped": n_drop,
     }
     if D.rank == 0 and D.world == 1 and not a.no_cpu:
@@ -928,7 +942,8 @@ def main():
                        "hosts": a.hosts, "packets_per_rank": a.packets},
             "roofline": {"kernel": "k_walk", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmw.get("hbm_bytes_per_launch"),
-                         "avg_launch_ms": round(walk_s * 1e3, 4), "valu_frac_pmc": pmw.get("valu_frac")},
+                         "avg_launch_ms": round(walk_s * 1e3, 4), "valu_frac_pmc": pmw.get("valu_frac"),
+                         "rocprof": rocprof_view(pmw, walk_bytes / max(walk_n, 1))},
             "round_hbm_GBs": round(round_bytes / t_round / 1e9, 1),
             "per_rank": per_rank,
             "parallelism": f"hosts{D.world}",
