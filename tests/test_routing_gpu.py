@@ -428,11 +428,11 @@ def test_lds_size_limit(oracle, ctx, n):
 
 
 @pytest.mark.parametrize("block_rows", ["64", "1000", "20000"])
-def test_routing_info_fill_c3(c3_oracle, ctx, monkeypatch, block_rows, apsp_kernel):
+def test_routing_info_fill_c3(c3_oracle, ctx, monkeypatch, block_rows, apsp_kernel, request):
     """sg_routing_info_fill: the whole C3 table straight into the dense host
     RoutingInfo, row blocks copied while the next builds (generate_routing_info,
     sim_config.rs:411-448, in a shuffled used-id order as a HashSet yields them)."""
-    if apsp_kernel != "lds" and block_rows != "1000":
+    if request.node.callspec.params["apsp_kernel"] != "lds" and block_rows != "1000":
         pytest.skip("the block sizes on the default kernel; one run of each other kernel")
     monkeypatch.setenv("SG_RI_BLOCK_ROWS", block_rows)
     g, used, olat, oloss = c3_oracle
