@@ -254,6 +254,100 @@ __device__ __forceinline__ void stage_chunk(uint32_t c0, uint32_t c1, LD&& ld, S
   }
 }
 
+// A block's events in chunks of CH LDS positions.  Contiguous: chunk c is the
+// block's events [p0 + c CH, ...), the hosts in order -- at C4 (~20 events per
+// host) a chunk holds ~50 hosts' events and every lane walks.  With hundreds of
+// events per host (C5: ~200) a contiguous chunk holds ~5 hosts: 5 lanes walk
+// while 59 wait, and the block's time is the sum of its hosts' chains.
+// Lane-major: chunk c holds events [c LK, (c + 1) LK) of every host, host l at
+// positions [l LK, l LK + LK) (holes past a host's last event), so all 64 lanes
+// walk every chunk and the block's time is its busiest host's chain.  A host's
+// events stay contiguous in position order, so k_codel's push / pop ranks by
+// ballot work unchanged (a hole counts as a non-push position: the pop slots
+// stay disjoint from the push slots).
+template <bool LM, uint32_t CH = CD_CHUNK>
+struct ChunkMap {
+  static constexpr uint32_t LK = CH / CD_THREADS;  // lane-major: events per host per chunk
+  uint32_t p0, p1;                       // the block's event range
+  const uint32_t *s_hb, *s_hn;           // lane-major: per host, first event and event count (LDS)
+  // chunk c exists (a loop test, not a chunk count: a count's division was hoisted above the
+  // walkers' state loads, and its wait for p0 / p1 put a round trip in front of them)
+  __device__ bool has(uint32_t c, uint32_t max_n) const { return LM ? c * LK < max_n : p0 + c * CH < p1; }
+  // chunk c's positions [0, len)
+  __device__ uint32_t len(uint32_t c) const { return LM ? CH : min(CH, p1 - p0 - c * CH); }
+  // the event at position k of chunk c (a valid index even when !ok: the loads are unconditional)
+  __device__ uint32_t event(uint32_t c, uint32_t k, bool& ok) const {
+    if (!LM) {
+      const uint32_t i = p0 + c * CH + k;
+      ok = i < p1;
+      return ok ? i : p1 - 1;
+    }
+    const uint32_t l = k / LK, o = c * LK + (k % LK), hn = s_hn[l];
+    ok = o < hn;
+    return ok ? s_hb[l] + o : p0;
+  }
+  // host lane t's positions [kb, ke) in chunk c, given its events [hb, he); ib = the event at kb
+  __device__ void host_range(uint32_t c, uint32_t t, uint32_t hb, uint32_t he, uint32_t& kb, uint32_t& ke,
+                             uint32_t& ib) const {
+    if (LM) {
+      const uint32_t o = c * LK, n = he - hb;
+      kb = t * LK;
+      ke = kb + (n > o ? min(LK, n - o) : 0u);
+      ib = hb + o;
+    } else {
+      const uint32_t c0 = p0 + c * CH, c1 = min(c0 + CH, p1);
+      const uint32_t b = max(hb, c0), e = min(he, c1);
+      kb = b < e ? b - c0 : 0;
+      ke = b < e ? e - c0 : 0;
+      ib = b;
+    }
+  }
+};
+
+// Lane-major when the block has more than two contiguous chunks of events and its
+// busiest host needs at most twice as many lane-major chunks (a block whose events
+// are mostly one host's stays contiguous: its chunks would hold a few events each)
+template <uint32_t CH = CD_CHUNK>
+__device__ __forceinline__ bool lane_major_block(int mode, uint32_t n_ev, uint32_t max_n) {
+  if (mode != 2) return mode == 1;
+  constexpr uint32_t LK = CH / CD_THREADS;
+  return n_ev > 2u * CH && (max_n + LK - 1) / LK <= 2u * ((n_ev + CH - 1) / CH);
+}
+
+// ANY: every lane publishes its host's event range for ChunkMap<true> and the busiest
+// host's event count comes back (a barrier); else nothing (0)
+template <bool ANY>
+__device__ __forceinline__ uint32_t lane_major_setup(uint32_t hb, uint32_t hn, uint32_t* s_hb, uint32_t* s_hn) {
+  if constexpr (!ANY) {
+    return 0;
+  } else {
+    uint32_t max_n = hn;
+    for (int o = 32; o > 0; o >>= 1) max_n = max(max_n, (uint32_t)__shfl_xor(max_n, o, 64));
+    s_hb[threadIdx.x] = hb;
+    s_hn[threadIdx.x] = hn;
+    __syncthreads();
+    return max_n;
+  }
+}
+
+// Runs body(ChunkMap<LM, CH>) with the block's layout as a compile-time choice (the
+// contiguous path keeps its r04 code; a runtime flag cost C4 ~1.5 us per launch)
+// ANY: the kernel was launched with lane-major blocks possible (lane_major_launch).  The
+// kernels launched without it keep the r04 contiguous loop verbatim instead of this one:
+// walking through ChunkMap<false> cost C4 5-7 % more walk time (k_inbound 22.2 -> 23.5 us
+// busiest-lane mean, k_outbound 15.0 -> 16.1, same box, SG_LANE_DIAG)
+template <bool ANY, uint32_t CH = CD_CHUNK, class F>
+__device__ __forceinline__ void with_chunk_map(bool lm, uint32_t p0, uint32_t p1, const uint32_t* s_hb,
+                                               const uint32_t* s_hn, F&& body) {
+  if constexpr (ANY) {
+    if (lm) {
+      body(ChunkMap<true, CH>{p0, p1, s_hb, s_hn});
+      return;
+    }
+  }
+  body(ChunkMap<false, CH>{p0, p1, s_hb, s_hn});
+}
+
 // SG_LANE_DIAG: a block's start and end on the 100 MHz wall clock (comparable
 // across CUs), the cycles its walkers spent walking, and its busiest lane's events
 __device__ __forceinline__ void lane_diag_store(unsigned long long* d, uint64_t t0, uint64_t walk, uint32_t ev) {
@@ -273,7 +367,12 @@ __device__ __forceinline__ void lane_diag_store(unsigned long long* d, uint64_t 
   }
 }
 
+// LM: the chunk layouts this launch may use (lane_major_launch): 0 contiguous only, 1 lane-major
+// only, 2 per block (lane_major_block).  A template parameter, not an argument: a field added to
+// the argument structs changed k_inbound's register allocation and cost C4 ~2 us.
+template <int LM>
 __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
+  constexpr bool ANY = LM != 0;
   const uint64_t d_t0 = a.bdiag ? wall_clock64() : 0;
   uint64_t d_walk = 0;
   // Staged chunk, 18 KB (8 one-wave blocks fit a CU): the chunk's pushes in push order
@@ -311,6 +410,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
     q.load_head();
   }
   const uint64_t lt = (1ull << t) - 1;  // lanes below this one
+  if constexpr (!ANY) {  // contiguous chunks only: the r04 loop as it was (see with_chunk_map)
   for (uint32_t c0 = p0; c0 < p1; c0 += CD_CHUNK) {
     const uint32_t c1 = min(c0 + CD_CHUNK, p1);
     {  // 1. coalesced staging, and the chunk's push and pop lists by ballot (the block is one wave)
@@ -404,6 +504,113 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
       if (r < a.n_status) a.status[r] = SG_CODEL_DEQUEUED;  // (CD_NONE >= n_status)
     }
     __syncthreads();
+  }
+  } else {
+  __shared__ uint32_t s_hb[CD_HOSTS], s_hn[CD_HOSTS];
+  const uint32_t hn = he - hb;
+  const uint32_t max_n = lane_major_setup<ANY>(hb, hn, s_hb, s_hn);
+  with_chunk_map<ANY>(ANY && lane_major_block(LM, p1 - p0, max_n), p0, p1, s_hb, s_hn, [&](auto cm) {
+  for (uint32_t c = 0; cm.has(c, max_n); c++) {
+    const uint32_t clen = cm.len(c);
+    {  // 1. staging (coalesced: the chunk's range, or 16-event runs per host), and the chunk's
+       //    push and pop lists by ballot (the block is one wave)
+      uint32_t run = 0;
+      for (uint32_t base = 0; base < clen; base += CD_THREADS * CD_UNROLL) {
+        uint64_t rt[CD_UNROLL];
+        uint32_t rp[CD_UNROLL], rl[CD_UNROLL];
+        uint8_t rk[CD_UNROLL];
+        bool ok[CD_UNROLL];
+#pragma unroll
+        for (int u = 0; u < CD_UNROLL; u++) {
+          const uint32_t i = cm.event(c, base + u * CD_THREADS + t, ok[u]);
+          rt[u] = a.time[i];
+          rp[u] = a.pkt[i];
+          rl[u] = a.len[i];
+          rk[u] = a.kind[i];
+        }
+#pragma unroll
+        for (int u = 0; u < CD_UNROLL; u++) {
+          const uint32_t k = base + u * CD_THREADS + t;
+          const bool in = k < clen, push = in && ok[u] && rk[u] == SG_CODEL_PUSH;
+          const uint64_t m = __ballot(push);
+          const uint32_t rank = run + (uint32_t)__popcll(m & lt);
+          if (in) {
+            const uint32_t slot = push ? rank : pop_at(k - rank);
+            if (ok[u]) {
+              s_t[slot] = rt[u];
+              s_p[slot] = rp[u];
+              s_l[slot] = push ? rl[u] : rank;
+            }
+            s_pp[k] = (uint16_t)rank;
+          }
+          run += (uint32_t)__popcll(m);
+        }
+      }
+      if (t == 0) s_pp[clen] = (uint16_t)run;
+    }
+    __syncthreads();
+    if (walker) {
+      // 2. each host's pops in order.  A host's pushes between two pops only
+      // append (tail, bytes): they are accounted at the next pop, the elements
+      // read from the staged window, and the ring is written at the chunk's end
+      // for the elements still queued -- the walk's steps are the pops alone.
+      const uint64_t d_w0 = a.bdiag ? clock64() : 0;
+      // this host's staged positions [kb, ke) (empty when none of its events is in the chunk)
+      uint32_t kb, ke, ib;
+      cm.host_range(c, t, hb, he, kb, ke, ib);
+      (void)ib;
+      const uint32_t pb = kb < ke ? s_pp[kb] : 0, pe = kb < ke ? s_pp[ke] : 0;
+      const uint32_t rb = kb - pb, re = ke - pe;  // this host's pop ranks [rb, re)
+      // the window's j-th push is push slot pb + j
+      q.begin_window((lds_u32*)s_p, (lds_u32*)s_l, (lds_u64*)s_t, nullptr, pb);
+      uint32_t seen = 0;  // window pushes accounted
+      auto account = [&](uint32_t upto) {  // the window's pushes [seen, upto) enter the queue
+        for (; seen < upto; seen++) q.bytes += s_l[pb + seen];
+        q.tail = q.t0 + upto;
+        if (q.tail - q.head > q.mask + 1u) q.err |= E_FULL;  // a push found the ring full
+        if (!q.hv) q.load_head();
+      };
+      // the next pop's fields are read a step ahead
+      uint64_t t1 = rb < re ? s_t[pop_at(rb)] : 0;
+      uint32_t pp1 = rb < re ? s_l[pop_at(rb)] : 0;
+      for (uint32_t r = rb; r < re; r++) {
+        const uint32_t k = pop_at(r), pp = pp1;
+        const uint64_t now = t1;
+        if (r + 1 < re) {
+          t1 = s_t[pop_at(r + 1)];
+          pp1 = s_l[pop_at(r + 1)];
+        }
+        account(pp - pb);
+        const uint32_t res = q.pop(now);
+        // a dequeued packet's status is written with the chunk's results (3. below): a
+        // global store here made the walk's next vector-memory wait (the ring prefetch,
+        // or a register the compiler shares with it) wait for the store too
+        if (res != CD_NONE && res >= q.n_status) q.err |= E_PKT;
+        s_p[k] = res;  // a pop's packet slot is read by no one else
+      }
+      account(pe - pb);
+      // the window's elements still queued live on in the ring
+      const uint32_t w0 = q.head - q.t0 <= q.tail - q.t0 ? q.head - q.t0 : 0;
+      for (uint32_t j = w0; j < q.tail - q.t0; j++) {
+        const uint32_t k = pb + j;
+        const uint64_t tk = s_t[k];
+        q.ring[(q.t0 + j) & q.mask] = make_uint4(s_p[k], s_l[k], (uint32_t)tk, (uint32_t)(tk >> 32));
+      }
+      if (a.bdiag) d_walk += clock64() - d_w0;
+      q.win = false;  // the next chunk's staging overwrites the window (the head stays cached)
+    }
+    __syncthreads();
+    for (uint32_t k = t; k < clen; k += CD_THREADS) {  // 3. results (CD_NONE for a push)
+      bool ok;
+      const uint32_t i = cm.event(c, k, ok);
+      if (!ok) continue;
+      const uint32_t r = s_pp[k + 1] != s_pp[k] ? CD_NONE : s_p[pop_at(k - s_pp[k])];
+      a.pop_result[i] = r;
+      if (r < a.n_status) a.status[r] = SG_CODEL_DEQUEUED;  // (CD_NONE >= n_status)
+    }
+    __syncthreads();
+  }
+  });
   }
   unsigned long long dropped = 0, err = 0;
   if (walker) {
@@ -576,7 +783,9 @@ __device__ void relay_task(Q& q, Relay& r, uint64_t now, uint64_t bootstrap_end,
   }
 }
 
+template <int LM>
 __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
+  constexpr bool ANY = LM != 0;
   const uint64_t d_t0 = ia.q.bdiag ? wall_clock64() : 0;
   uint64_t d_walk = 0;
   const CodelArgs& a = ia.q;
@@ -623,6 +832,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
   auto due = [&](uint64_t before) {  // a pending task earlier than `before` (Packet events go first)
     return (r.rf & R_PENDING) && !(r.rf & R_NEVER) && r.tt < before;
   };
+  if constexpr (!ANY) {  // contiguous chunks only: the r04 loop as it was (see with_chunk_map)
   for (uint32_t c0 = p0; c0 < p1; c0 += CD_CHUNK) {
     const uint32_t c1 = min(c0 + CD_CHUNK, p1);
     {
@@ -682,6 +892,78 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
       if (a.bdiag) d_walk += clock64() - d_w0;
     }
     __syncthreads();
+  }
+  } else {
+  __shared__ uint32_t s_hb[CD_HOSTS], s_hn[CD_HOSTS];
+  const uint32_t max_n = lane_major_setup<ANY>(hb, he - hb, s_hb, s_hn);
+  with_chunk_map<ANY>(ANY && lane_major_block(LM, p1 - p0, max_n), p0, p1, s_hb, s_hn, [&](auto cm) {
+  for (uint32_t c = 0; cm.has(c, max_n); c++) {
+    const uint32_t clen = cm.len(c);
+    for (uint32_t base = 0; base < clen; base += CD_THREADS * CD_UNROLL) {  // staging (see ChunkMap)
+      uint64_t rt[CD_UNROLL];
+      uint32_t rp[CD_UNROLL], rl[CD_UNROLL];
+      bool ok[CD_UNROLL];
+#pragma unroll
+      for (int u = 0; u < CD_UNROLL; u++) {
+        const uint32_t i = cm.event(c, base + u * CD_THREADS + t, ok[u]);
+        rt[u] = a.time[i];
+        rp[u] = a.pkt[i];
+        rl[u] = a.len[i];
+      }
+#pragma unroll
+      for (int u = 0; u < CD_UNROLL; u++) {
+        const uint32_t k = base + u * CD_THREADS + t;
+        if (k < clen && ok[u]) {
+          s_t[k] = rt[u];
+          s_p[k] = rp[u];
+          s_l[k] = rl[u];
+        }
+      }
+    }
+    __syncthreads();
+    if (walker) {
+      uint32_t kb, ke, ib;
+      cm.host_range(c, t, hb, he, kb, ke, ib);
+      (void)ib;
+      const uint64_t d_w0 = a.bdiag ? clock64() : 0;
+      q.win = false;  // the tasks first run by this chunk pop the previous chunk's elements from HBM
+      q.begin_window((lds_u32*)s_p, (lds_u32*)s_l, (lds_u64*)s_t, nullptr, kb);
+      uint64_t nt = kb < ke ? s_t[kb] : 0;  // the next arrival's fields, read ahead
+      uint32_t np = kb < ke ? s_p[kb] : 0, nl = kb < ke ? s_l[kb] : 0;
+      for (uint32_t k = kb; k < ke; k++) {
+        const uint64_t now = nt;
+        const uint32_t pkt = np, len = nl;
+        if (k + 1 < ke) {
+          nt = s_t[k + 1];
+          np = s_p[k + 1];
+          nl = s_l[k + 1];
+        }
+        if (now >= ia.window_end) q.err |= E_WINDOW;
+        while (due(now)) relay_task(q, r, r.tt, ia.bootstrap_end, ia.sim_end, ctr_inc, ia.fwd_time);
+        // Router::route_incoming_packet: the arrival is the window's next element (staged
+        // slot k, read from LDS when it reaches the head); the ring receives the window's
+        // still-queued elements at the chunk's end, as in k_codel -- a ring store per
+        // arrival made the walk's next vector-memory wait include it
+        (void)pkt;
+        q.tail++;
+        q.bytes += len;
+        if (q.tail - q.head > q.mask + 1u) q.err |= E_FULL;  // an arrival found the ring full
+        if (!q.hv) q.load_head();
+        if (!(r.rf & R_PENDING)) r.schedule(now, now, ia.sim_end, ctr_inc);  // notify: Idle -> forward_later(ZERO)
+      }
+      // the window's elements still queued live on in the ring
+      const uint32_t w0 = q.head - q.t0 <= q.tail - q.t0 ? q.head - q.t0 : 0;
+      for (uint32_t j = w0; j < q.tail - q.t0; j++) {
+        const uint32_t k = q.wb + j;
+        const uint64_t tk = s_t[k];
+        q.ring[(q.t0 + j) & q.mask] = make_uint4(s_p[k], s_l[k], (uint32_t)tk, (uint32_t)(tk >> 32));
+      }
+      q.win = false;  // the next chunk's staging overwrites the window
+      if (a.bdiag) d_walk += clock64() - d_w0;
+    }
+    __syncthreads();
+  }
+  });
   }
   unsigned long long err = 0, dropped = 0;
   if (walker) {
@@ -825,8 +1107,9 @@ __device__ void out_task(OutQ& q, Relay& r, uint64_t now, const OutboundArgs& a,
 // keys every send precedes a task at its time.  A Local send's id also moves
 // the host counter past it, so the tasks it schedules are numbered after it.  The keys cost 16 B of LDS per
 // staged send, so the keyed chunk is smaller (40 B per send, 20 KB).
-template <bool KEYED>
+template <bool KEYED, int LM>
 __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
+  constexpr bool ANY = LM != 0;
   constexpr uint32_t CH = KEYED ? 512 : CD_OUT_CHUNK;
   const uint64_t d_t0 = a.bdiag ? wall_clock64() : 0;
   uint64_t d_walk = 0;
@@ -834,8 +1117,6 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
   __shared__ uint4 s_r[CH];
   __shared__ uint64_t s_id[KEYED ? CH : 1], s_born[KEYED ? CH : 1];
   const uint32_t h0 = blockIdx.x * CD_HOSTS, t = threadIdx.x;
-  const uint32_t p0 = min(a.host_off[min(h0, a.H)], a.E);
-  const uint32_t p1 = max(min(a.host_off[min(h0 + CD_HOSTS, a.H)], a.E), p0);
   const uint32_t h = h0 + t;
   const bool walker = t < CD_HOSTS && h < a.H;
   uint32_t hb = 0, he = 0;
@@ -863,12 +1144,18 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
     if (r.rf & R_CACHED) q.cr = q.ring[(q.head - 1) & q.mask];
     q.load_head();
   }
+  // the block's events [p0, p1): lane 0's first and the last host's end, read from the
+  // walkers' registers (loads of their own were waited for ahead of the walkers' state
+  // loads once the chunk loop used them as scalars: a round trip per block, C4 +2.4 us)
+  const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)hb, 0);
+  const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)he, (int)min(CD_HOSTS - 1u, a.H - 1u - h0));
   auto due = [&](uint64_t before) { return (r.rf & R_PENDING) && !(r.rf & R_NEVER) && r.tt < before; };
   // a task at the send's own time that runs first: created before the sending Local event
   auto due_tie = [&](uint64_t now, uint64_t born, uint64_t id) {
     return KEYED && (r.rf & R_PENDING) && !(r.rf & R_NEVER) && r.tt == now && id != ~0ull &&
            (r.tborn < born || (r.tborn == born && r.tid < id));
   };
+  if constexpr (!ANY) {  // contiguous chunks only: the r04 loop as it was (see with_chunk_map)
   for (uint32_t c0 = p0; c0 < p1; c0 += CH) {
     const uint32_t c1 = min(c0 + CH, p1);
     {
@@ -939,6 +1226,89 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
       q.win = false;  // the next chunk's staging overwrites the window
     }
     __syncthreads();
+  }
+  } else {
+  __shared__ uint32_t s_hb[CD_HOSTS], s_hn[CD_HOSTS];
+  const uint32_t max_n = lane_major_setup<ANY>(hb, he - hb, s_hb, s_hn);
+  with_chunk_map<ANY, CH>(ANY && lane_major_block<CH>(LM, p1 - p0, max_n), p0, p1, s_hb, s_hn, [&](auto cm) {
+  for (uint32_t c = 0; cm.has(c, max_n); c++) {
+    const uint32_t clen = cm.len(c);
+    for (uint32_t base = 0; base < clen; base += CD_THREADS * CD_UNROLL) {  // staging (see ChunkMap)
+      uint64_t rt[CD_UNROLL], ri[KEYED ? CD_UNROLL : 1], rb[KEYED ? CD_UNROLL : 1];
+      uint4 rr[CD_UNROLL];
+      bool ok[CD_UNROLL];
+#pragma unroll
+      for (int u = 0; u < CD_UNROLL; u++) {
+        const uint32_t i = cm.event(c, base + u * CD_THREADS + t, ok[u]);
+        rt[u] = a.time[i];
+        rr[u] = make_uint4(a.pkt[i], a.len[i], a.dst[i], a.payload[i]);
+        if constexpr (KEYED) {
+          ri[u] = a.ev_id[i];
+          rb[u] = a.ev_born[i];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < CD_UNROLL; u++) {
+        const uint32_t k = base + u * CD_THREADS + t;
+        if (k < clen && ok[u]) {
+          s_t[k] = rt[u];
+          s_r[k] = rr[u];
+          if constexpr (KEYED) {
+            s_id[k] = ri[u];
+            s_born[k] = rb[u];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (walker) {
+      uint32_t kb, ke, ib;
+      cm.host_range(c, t, hb, he, kb, ke, ib);
+      const uint64_t d_w0 = a.bdiag ? clock64() : 0;
+      q.begin_window((const __attribute__((address_space(3))) uint4*)s_r, kb);
+      for (uint32_t k = kb; k < ke; k++) {
+        const uint32_t i = ib + (k - kb);
+        const uint64_t now = s_t[k];
+        if (now >= a.window_end) q.err |= E_WINDOW;
+        if (now < last) q.err |= E_ORDER;
+        if constexpr (KEYED) {
+          // execution order within a time: Packet-event sends, then Local ones by (created, id)
+          const uint64_t id = s_id[k], born = s_born[k];
+          if (now == last && i > hb) {
+            const bool pk = id == ~0ull, lpk = last_id == ~0ull;
+            if ((pk && !lpk) || (!pk && !lpk && (born < last_born || (born == last_born && id < last_id))))
+              q.err |= E_ORDER;
+          }
+          last_born = born;
+          last_id = id;
+          while (due(now) || due_tie(now, born, id)) out_task(q, r, r.tt, a, ctr_inc);
+          // the sending event exists, so the host's counter is past its id: a task the send
+          // schedules takes a later id (a Lamport-clock step; a no-op when the caller's ids
+          // come from this counter)
+          if (id != ~0ull && id - r.ctr0 >= ctr_inc && id >= r.ctr0) ctr_inc = id + 1 - r.ctr0;
+        } else {
+          while (due(now)) out_task(q, r, r.tt, a, ctr_inc);
+        }
+        last = now;
+        if (q.tail - q.oldest >= a.cap) {  // the push would overwrite a slot this call still needs
+          q.err |= E_FULL;
+          continue;
+        }
+        // NetworkInterface::add_data_source: the record is the window's next element (read
+        // from LDS at the head); the ring receives the window's records at the chunk's end
+        // (k_out_compact gathers the sent ones from there) -- a ring store per send made the
+        // walk's next vector-memory wait include it
+        if (q.head == q.tail) q.hr = s_r[k];
+        q.tail++;
+        if (!(r.rf & R_PENDING)) r.schedule(now, now, a.sim_end, ctr_inc);  // notify: Idle -> forward_later(ZERO)
+      }
+      for (uint32_t j = 0; j < q.tail - q.t0; j++) q.ring[(q.t0 + j) & q.mask] = s_r[q.wb + j];
+      if (a.bdiag) d_walk += clock64() - d_w0;
+      q.win = false;  // the next chunk's staging overwrites the window
+    }
+    __syncthreads();
+  }
+  });
   }
   unsigned long long err = 0, sent = 0;
   if (walker) {
@@ -1150,6 +1520,20 @@ struct sg_inbound {
   }
 };
 
+// SG_LANE_MAJOR: the chunk layout of the lane kernels (ChunkMap): 0 contiguous, 1 lane-major,
+// unset / 2 by each block's event count (tests force both on the same events)
+int lane_major_env() {
+  const char* e = getenv("SG_LANE_MAJOR");
+  return e && *e ? std::max(0, std::min(2, atoi(e))) : 2;
+}
+
+// The lane-major layout is compiled into a launch when forced (SG_LANE_MAJOR=1) or when
+// the blocks average more than two contiguous chunks of ch events (C5: ~12.8k codel events
+// per block; C4: ~1.3k, which keeps the contiguous-only kernel)
+int lane_major_launch(int mode, size_t n_events, uint32_t nb, uint32_t ch) {
+  return mode == 1 ? 1 : (mode == 2 && n_events > 2ull * ch * nb) ? 2 : 0;
+}
+
 // SG_LANE_DIAG=1: per-block timing of the lane-per-host kernels on stderr (a
 // diagnostic: a synchronous copy after the launch; never set in a measured run)
 unsigned long long* lane_diag_alloc(uint32_t nb) {
@@ -1217,7 +1601,13 @@ int32_t sg_codel_run(sg_ctx* ctx, sg_codel* q, const sg_codel_events* ev, uint32
     {
       // per event: 17 B in, 4 B result, ring slot 16 B written (push) or read (pop), 1 B status
       TimedLaunch tl(ctx, "codel", 38.0 * E + 56.0 * H);
-      hipLaunchKernelGGL(k_codel, dim3(nb), dim3(CD_THREADS), 0, st, a);
+      const int lm = lane_major_launch(lane_major_env(), E, nb, CD_CHUNK);
+      if (lm == 2)
+        hipLaunchKernelGGL(k_codel<2>, dim3(nb), dim3(CD_THREADS), 0, st, a);
+      else if (lm == 1)
+        hipLaunchKernelGGL(k_codel<1>, dim3(nb), dim3(CD_THREADS), 0, st, a);
+      else
+        hipLaunchKernelGGL(k_codel<0>, dim3(nb), dim3(CD_THREADS), 0, st, a);
     }
     lane_diag_report(st, "k_codel", a.bdiag, nb);
     hipLaunchKernelGGL(k_codel_reduce, dim3(1), dim3(1024), 0, st, a.blk, nb, gerr, q->ret);
@@ -1385,7 +1775,13 @@ int32_t sg_inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* a
       // per arrival: 16 B in, a 16-B ring record written and read, 9 B out; per host: ~160 B of state
       a.q.bdiag = lane_diag_alloc(nb);
       TimedLaunch tl(ctx, "inbound", 57.0 * E + 160.0 * H);
-      hipLaunchKernelGGL(k_inbound, dim3(nb), dim3(CD_THREADS), 0, st, a);
+      const int lm = lane_major_launch(lane_major_env(), E, nb, CD_CHUNK);
+      if (lm == 2)
+        hipLaunchKernelGGL(k_inbound<2>, dim3(nb), dim3(CD_THREADS), 0, st, a);
+      else if (lm == 1)
+        hipLaunchKernelGGL(k_inbound<1>, dim3(nb), dim3(CD_THREADS), 0, st, a);
+      else
+        hipLaunchKernelGGL(k_inbound<0>, dim3(nb), dim3(CD_THREADS), 0, st, a);
     }
     lane_diag_report(st, "k_inbound", a.q.bdiag, nb);
     hipLaunchKernelGGL(k_codel_reduce, dim3(1), dim3(1024), 0, st, a.q.blk, nb, gerr, q->ret);
@@ -1579,11 +1975,13 @@ int32_t sg_outbound_run(sg_ctx* ctx, sg_outbound* ob, const sg_outbound_sends* s
     {
       // per send: 24 B in, a 16-B ring record written and read, 9 B out; per host: ~90 B of state
       a.bdiag = lane_diag_alloc(nb);
-      TimedLaunch tl(ctx, "outbound", 65.0 * E + 90.0 * H);
+        TimedLaunch tl(ctx, "outbound", 65.0 * E + 90.0 * H);
+      const int lm = lane_major_launch(lane_major_env(), E, nb, keyed ? 512u : (uint32_t)CD_OUT_CHUNK);
+      auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(nb), dim3(CD_THREADS), 0, st, a); };
       if (keyed && E)
-        hipLaunchKernelGGL(k_outbound<true>, dim3(nb), dim3(CD_THREADS), 0, st, a);
+        lm == 2 ? go(k_outbound<true, 2>) : lm == 1 ? go(k_outbound<true, 1>) : go(k_outbound<true, 0>);
       else
-        hipLaunchKernelGGL(k_outbound<false>, dim3(nb), dim3(CD_THREADS), 0, st, a);
+        lm == 2 ? go(k_outbound<false, 2>) : lm == 1 ? go(k_outbound<false, 1>) : go(k_outbound<false, 0>);
     }
     lane_diag_report(st, "k_outbound", a.bdiag, nb);
     if (sent) {

@@ -76,9 +76,14 @@ def test_reference_drop_many_sequence(oracle, ctx):
     assert st["tail"][0] - st["head"][0] == 1 and st["cur"][0] == 16 and not st["flags"][0] & 1
 
 
-@pytest.mark.parametrize("gap_ms,p_pop", [(3, 0.45), (1, 0.3), (20, 0.5)])
-def test_random_streams_over_calls(oracle, ctx, gap_ms, p_pop):
-    """500 hosts, three consecutive calls of 60k events: state carries over."""
+@pytest.mark.parametrize("gap_ms,p_pop,layout", [(3, 0.45, ""), (1, 0.3, ""), (20, 0.5, ""), (3, 0.45, "0"),
+                                                  (1, 0.3, "1")])
+def test_random_streams_over_calls(oracle, ctx, monkeypatch, gap_ms, p_pop, layout):
+    """500 hosts, three consecutive calls of 60k events: state carries over.  ~120 events
+    per host: the blocks take lane-major chunks by default (sg_codel.hip ChunkMap); layout
+    forces contiguous ("0") or lane-major ("1") chunks."""
+    if layout:
+        monkeypatch.setenv("SG_LANE_MAJOR", layout)
     rng = np.random.default_rng(gap_ms)
     H, E = 500, 60000
     q = CoDelQueues(H, 4096, ctx=ctx)
@@ -93,11 +98,15 @@ def test_random_streams_over_calls(oracle, ctx, gap_ms, p_pop):
     assert (ostat == 2).any() and (ostat == 1).any()
 
 
-def test_queue_deeper_than_a_chunk(oracle, ctx):
+@pytest.mark.parametrize("layout", ["", "1"])
+def test_queue_deeper_than_a_chunk(oracle, ctx, monkeypatch, layout):
     """One host's queue grows past a staged chunk (1024 events) and drains in later
     chunks: its elements are read back from the ring in HBM, which the kernel
     writes only for what outlives each chunk.  Then push/pop cycles wrap the ring
-    indices several times.  Neighbour hosts have a few events each."""
+    indices several times.  Neighbour hosts have a few events each.  layout "1":
+    lane-major chunks of 16 events per host (the default keeps this block contiguous)."""
+    if layout:
+        monkeypatch.setenv("SG_LANE_MAJOR", layout)
     rng = np.random.default_rng(5)
     cap = 4096
     q = CoDelQueues(3, cap, ctx=ctx)
@@ -130,14 +139,33 @@ def test_queue_deeper_than_a_chunk(oracle, ctx):
     assert (ostat == 2).any() and (ostat == 1).any()
 
 
-def test_large_single_call(oracle, ctx):
-    """100k hosts, 1M events (the bench shape), one call."""
+@pytest.mark.parametrize("layout", ["", "1"])
+def test_large_single_call(oracle, ctx, monkeypatch, layout):
+    """100k hosts, 1M events (the bench shape), one call; layout "1" forces lane-major chunks."""
+    if layout:
+        monkeypatch.setenv("SG_LANE_MAJOR", layout)
     rng = np.random.default_rng(11)
     H, E = 100000, 1000000
     q = CoDelQueues(H, 256, ctx=ctx)
     os_ = oracle.codel_state(H, q.cap)
     gstat, ostat = _status(E), np.zeros(E, np.uint8)
     _run_both(oracle, q, os_, gstat, ostat, *_stream(rng, H, E, T0 + 10**9, 30, 0.4))
+    _same_state(oracle, q.get_state(), os_)
+
+
+def test_many_events_per_host(oracle, ctx):
+    """The C5 shape per block (~200 events per host, 1 ms round): 6,400 hosts, 1.28M events,
+    two calls; the blocks take lane-major chunks."""
+    rng = np.random.default_rng(12)
+    H, E = 6400, 1280000
+    q = CoDelQueues(H, 1024, ctx=ctx)
+    os_ = oracle.codel_state(H, q.cap)
+    gstat, ostat = _status(2 * E), np.zeros(2 * E, np.uint8)
+    t0 = T0 + 10**9
+    for c in range(2):
+        ev = _stream(rng, H, E, t0, 0.01, 0.5, n_pkt0=c * E)
+        _run_both(oracle, q, os_, gstat, ostat, *ev)
+        t0 = int(ev[2].max()) + 1
     _same_state(oracle, q.get_state(), os_)
 
 

@@ -39,11 +39,17 @@ def _same(O, got, want):
     assert np.array_equal(got["cached_len"][m], want["cached_len"][m])
 
 
-@pytest.mark.parametrize("bw_mbit,boot_ms", [(1000, 0), (10, 0), (1, 0), (10, 40)])
-def test_windows_match_oracle(oracle, ctx, bw_mbit, boot_ms):
+@pytest.mark.parametrize("bw_mbit,boot_ms,layout", [(1000, 0, ""), (10, 0, ""), (1, 0, ""), (10, 40, ""),
+                                                   (1, 0, "0"), (10, 40, "0")])
+def test_windows_match_oracle(oracle, ctx, monkeypatch, bw_mbit, boot_ms, layout):
     """300 hosts, 5 windows of 60 ms, 60k arrivals: from unthrottled to heavily
-    throttled (standing queues, CoDel drop mode, tasks pending across windows)."""
+    throttled (standing queues, CoDel drop mode, tasks pending across windows).  ~40
+    arrivals per host: lane-major chunks by default (sg_codel.hip ChunkMap); layout "0"
+    forces contiguous ones."""
     import torch
+
+    if layout:
+        monkeypatch.setenv("SG_LANE_MAJOR", layout)
 
     rng = np.random.default_rng(bw_mbit + boot_ms)
     H, W, per = 300, 60 * MS, 12000

@@ -44,11 +44,16 @@ def _live_same(got, want):
         assert np.array_equal(got[k][i], want[k][i]), k
 
 
-@pytest.mark.parametrize("bw_mbit,boot_ms", [(1000, 0), (10, 0), (2, 0), (10, 3)])
-def test_windows_match_oracle(oracle, ctx, bw_mbit, boot_ms):
+@pytest.mark.parametrize("bw_mbit,boot_ms,layout", [(1000, 0, ""), (10, 0, ""), (2, 0, ""), (10, 3, ""),
+                                                   (2, 0, "1"), (10, 3, "1")])
+def test_windows_match_oracle(oracle, ctx, monkeypatch, bw_mbit, boot_ms, layout):
     """2000 hosts, 5 windows of 2 ms, 40k sends each: unthrottled to heavily throttled
-    (queues and cached packets carried across windows, tasks pending)."""
+    (queues and cached packets carried across windows, tasks pending).  layout "1" forces
+    lane-major chunks (sg_codel.hip ChunkMap; ~20 sends per host take contiguous ones)."""
     import torch
+
+    if layout:
+        monkeypatch.setenv("SG_LANE_MAJOR", layout)
 
     H, W, per = 2000, 2 * MS, 40000
     hosts = synth.make_hosts(H, 64, exact_seeds=False)
@@ -112,8 +117,8 @@ def _keyed_sends(hosts, n, t0, t1, seed):
     return host[o], t[o], ln[o], pay[o], dst[o], eid[o], born[o]
 
 
-@pytest.mark.parametrize("bw_mbit", [10, 2])
-def test_same_time_ties_match_oracle(oracle, ctx, bw_mbit):
+@pytest.mark.parametrize("bw_mbit,layout", [(10, ""), (2, ""), (2, "1")])
+def test_same_time_ties_match_oracle(oracle, ctx, monkeypatch, bw_mbit, layout):
     """Wake-ups and sends on the same nanosecond, ordered by the sending event's (created, id)
     against the task's (relay/mod.rs:145-157, event.rs:84-155): 1500 hosts, 4 windows, keyed
     sends (k_outbound<true>) bit-exact with the oracle, task ids included.  The keys must
@@ -121,6 +126,8 @@ def test_same_time_ties_match_oracle(oracle, ctx, bw_mbit):
     disagrees (the ties went both ways)."""
     import torch
 
+    if layout:
+        monkeypatch.setenv("SG_LANE_MAJOR", layout)
     H, W, per = 1500, 2 * MS, 30000
     hosts = synth.make_hosts(H, 64, exact_seeds=False)
     bw = np.full(H, bw_mbit * 10**6, np.uint64)
