@@ -7,7 +7,7 @@ ROOT=$(cd "$(dirname "$0")/../.." && pwd)
 OBJ=/tmp/sg_ab_$NAME; rm -rf $OBJ; mkdir -p $OBJ
 cd $ROOT/shadow_amd/csrc
 pids=()
-for f in sg_context sg_routing sg_sssp sg_route_info sg_deliver sg_codel; do
+for f in $(ls *.hip | sed 's/\.hip$//'); do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=gfx950 -ffp-contract=off \
     -fno-fast-math -munsafe-fp-atomics $DEFS -c $f.hip -o $OBJ/$f.o &
   pids+=($!)
