@@ -64,6 +64,15 @@ typedef __attribute__((address_space(3))) const uint32_t lds_u32;
 typedef __attribute__((address_space(3))) const uint64_t lds_u64;
 typedef __attribute__((address_space(3))) const uint16_t lds_u16;
 
+// s_waitcnt vmcnt(0) as the immediate of __builtin_amdgcn_s_waitcnt (gfx9: lgkmcnt and expcnt
+// left at their maxima)
+constexpr int VMCNT0 = 0x0F70;
+
+// PF: the kernel keeps the next chunk's loads in flight during the walk (k_codel<LM != 0>); the
+// ring path then waits for its own load where it issues it -- where the ring and window paths
+// join, the compiler otherwise waits for every vector-memory operation in flight (vmcnt(0)), the
+// next chunk's loads included
+template <bool PF = false>
 struct Q {
   uint8_t flags;
   uint64_t iend, dnext, cur, prev, bytes;
@@ -141,6 +150,7 @@ struct Q {
     }
     const uint32_t slot = head & mask;
     const uint4 r = ring[slot];
+    if constexpr (PF) __builtin_amdgcn_s_waitcnt(VMCNT0);
     hp = r.x;
     hl = r.y;
     ht = ((uint64_t)r.w << 32) | r.z;
@@ -391,7 +401,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
   const uint32_t h = h0 + t;
   const bool walker = t < CD_HOSTS && h < a.H;
   uint32_t hb = 0, he = 0;
-  Q q{};
+  Q<LM != 0> q{};
   if (walker) {
     hb = min(a.host_off[h], a.E);
     he = max(min(a.host_off[h + 1], a.E), hb);
@@ -510,44 +520,50 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
   const uint32_t hn = he - hb;
   const uint32_t max_n = lane_major_setup<ANY>(hb, hn, s_hb, s_hn);
   with_chunk_map<ANY>(ANY && lane_major_block(LM, p1 - p0, max_n), p0, p1, s_hb, s_hn, [&](auto cm) {
+  // A chunk's events are loaded into registers a chunk ahead (CD_PF per lane, one round of
+  // loads): the next chunk's loads are in flight during this chunk's walk.  At C5 a block walks
+  // ~19 lane-major chunks, and each chunk's staging round trips sat in front of its walk.
+  constexpr int CD_PF = CD_CHUNK / CD_THREADS;
+  uint64_t rt[CD_PF];
+  uint32_t rp[CD_PF], rl[CD_PF];
+  uint8_t rk[CD_PF];
+  bool ok[CD_PF];
+  auto fetch = [&](uint32_t f) {
+#pragma unroll
+    for (int u = 0; u < CD_PF; u++) {
+      const uint32_t i = cm.event(f, u * CD_THREADS + t, ok[u]);
+      rt[u] = a.time[i];
+      rp[u] = a.pkt[i];
+      rl[u] = a.len[i];
+      rk[u] = a.kind[i];
+    }
+  };
+  if (cm.has(0, max_n)) fetch(0);
   for (uint32_t c = 0; cm.has(c, max_n); c++) {
     const uint32_t clen = cm.len(c);
-    {  // 1. staging (coalesced: the chunk's range, or 16-event runs per host), and the chunk's
-       //    push and pop lists by ballot (the block is one wave)
+    {  // 1. staging from the registers (the chunk's range, or 16-event runs per host), and the
+       //    chunk's push and pop lists by ballot (the block is one wave)
       uint32_t run = 0;
-      for (uint32_t base = 0; base < clen; base += CD_THREADS * CD_UNROLL) {
-        uint64_t rt[CD_UNROLL];
-        uint32_t rp[CD_UNROLL], rl[CD_UNROLL];
-        uint8_t rk[CD_UNROLL];
-        bool ok[CD_UNROLL];
 #pragma unroll
-        for (int u = 0; u < CD_UNROLL; u++) {
-          const uint32_t i = cm.event(c, base + u * CD_THREADS + t, ok[u]);
-          rt[u] = a.time[i];
-          rp[u] = a.pkt[i];
-          rl[u] = a.len[i];
-          rk[u] = a.kind[i];
-        }
-#pragma unroll
-        for (int u = 0; u < CD_UNROLL; u++) {
-          const uint32_t k = base + u * CD_THREADS + t;
-          const bool in = k < clen, push = in && ok[u] && rk[u] == SG_CODEL_PUSH;
-          const uint64_t m = __ballot(push);
-          const uint32_t rank = run + (uint32_t)__popcll(m & lt);
-          if (in) {
-            const uint32_t slot = push ? rank : pop_at(k - rank);
-            if (ok[u]) {
-              s_t[slot] = rt[u];
-              s_p[slot] = rp[u];
-              s_l[slot] = push ? rl[u] : rank;
-            }
-            s_pp[k] = (uint16_t)rank;
+      for (int u = 0; u < CD_PF; u++) {
+        const uint32_t k = u * CD_THREADS + t;
+        const bool in = k < clen, push = in && ok[u] && rk[u] == SG_CODEL_PUSH;
+        const uint64_t m = __ballot(push);
+        const uint32_t rank = run + (uint32_t)__popcll(m & lt);
+        if (in) {
+          const uint32_t slot = push ? rank : pop_at(k - rank);
+          if (ok[u]) {
+            s_t[slot] = rt[u];
+            s_p[slot] = rp[u];
+            s_l[slot] = push ? rl[u] : rank;
           }
-          run += (uint32_t)__popcll(m);
+          s_pp[k] = (uint16_t)rank;
         }
+        run += (uint32_t)__popcll(m);
       }
       if (t == 0) s_pp[clen] = (uint16_t)run;
     }
+    if (cm.has(c + 1, max_n)) fetch(c + 1);  // (uniform) in flight during the walk
     __syncthreads();
     if (walker) {
       // 2. each host's pops in order.  A host's pushes between two pops only
@@ -751,7 +767,7 @@ struct InboundArgs {
 };
 
 // The relay's forward task at `now` (run_forward_task -> forward_until_blocked).
-__device__ void relay_task(Q& q, Relay& r, uint64_t now, uint64_t bootstrap_end, uint64_t sim_end,
+__device__ void relay_task(Q<>& q, Relay& r, uint64_t now, uint64_t bootstrap_end, uint64_t sim_end,
                            uint64_t& ctr_inc, uint64_t* fwd_time) {
   r.rf &= (uint8_t)~R_PENDING;
   for (;;) {
@@ -798,7 +814,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
   const uint32_t h = h0 + t;
   const bool walker = t < CD_HOSTS && h < a.H;
   uint32_t hb = 0, he = 0;
-  Q q{};
+  Q<> q{};
   Relay r{};
   uint64_t ctr_inc = 0;
   if (walker) {
