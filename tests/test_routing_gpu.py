@@ -28,6 +28,13 @@ def apsp_kernel(request, monkeypatch):
     return set_apsp_kernel(monkeypatch, request.param)
 
 
+def _dense_once(request):
+    """Dense graphs take k_sssp_dense under every LDS setting (lds, lds_bounded, lds_flagged):
+    one of them runs it; the slab fixture runs the slab kernel."""
+    if request.node.callspec.params["apsp_kernel"] in ("lds_bounded", "lds_flagged"):
+        pytest.skip("the dense-graph search runs under the lds fixture")
+
+
 def _graph(g, ctx):
     return NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
 
@@ -302,9 +309,10 @@ def test_kernel_variants_bit_exact(oracle, ctx, monkeypatch, env, apsp_kernel):
 
 
 @pytest.mark.parametrize("nseg", ["2", "5"])
-def test_arc_segments_directed_dense(oracle, ctx, monkeypatch, nseg, apsp_kernel):
+def test_arc_segments_directed_dense(oracle, ctx, monkeypatch, nseg, apsp_kernel, request):
     """Arc segments (atomic-min flush) on a directed, nearly complete graph with
     parallel arcs, used-subset rows (the LDS search: a dense directed graph)."""
+    _dense_once(request)
     if apsp_kernel == "lds" and nseg != "2":
         pytest.skip("one LDS run is enough")
     monkeypatch.setenv("SG_APSP_SEG", nseg)
@@ -321,11 +329,12 @@ def test_arc_segments_directed_dense(oracle, ctx, monkeypatch, nseg, apsp_kernel
     _check(oracle, gd, used, ctx)
 
 
-def test_c2_scale_from_gml(oracle, ctx):
+def test_c2_scale_from_gml(oracle, ctx, request):
     """C2: a 1,200-node complete undirected graph (about 720k edges)
     parsed from GML text, every node used.  The full shortest-path table is
     bit-exact against the oracle, and so is the direct-path table
     (use_shortest_path: false)."""
+    _dense_once(request)
     g = synth.complete_graph(1200, seed=2)  # dense: the relaxation splits chunks into ~9 arc segments
     net = NetworkGraph.parse(synth.graph_to_gml(g), ctx=ctx)
     assert net.n_nodes == 1200 and len(net.edge_src) == len(g["src"])
@@ -473,11 +482,12 @@ def test_routing_info_direct_and_errors(oracle, ctx):
 
 
 @pytest.mark.parametrize("case", ["ties", "wide", "parallel_directed", "used_subset", "tiny_wmin"])
-def test_dense_graph_cases(oracle, ctx, case):
+def test_dense_graph_cases(oracle, ctx, case, request):
     """Dense graphs (mean out-degree past 64: the register-resident search of sg_dense.hip under
     the LDS fixtures, the slab under `slab`): equal-latency paths decided by loss, latencies past
     2^32 ns (wide rows), parallel arcs in a directed graph, a used-node subset with rows and
     columns in a shuffled order, and 1-ns arcs (one-node rounds)."""
+    _dense_once(request)
     rng = np.random.default_rng(sum(map(ord, case)))
     n = 520
     if case == "parallel_directed":
