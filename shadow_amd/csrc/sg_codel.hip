@@ -314,25 +314,37 @@ struct ChunkMap {
   }
 };
 
-// Lane-major when the block has more than two contiguous chunks of events and its
-// busiest host needs at most twice as many lane-major chunks (a block whose events
-// are mostly one host's stays contiguous: its chunks would hold a few events each)
+// Lane-major when it walks the block in less estimated time: a chunk costs CHUNK_COST walk
+// steps of staging and barriers, plus its walk -- contiguous, about one host's share of the
+// chunk (the active hosts' mean, capped at CH: its hosts are walked side by side); lane-major,
+// LK steps (every host's next LK events side by side).  C5: 13 contiguous chunks of ~200 steps
+// against 18 lane-major ones of 16; a partial last block (32 hosts) the same.  A block that is
+// mostly one host (5,000 of its 5,006 events) stays contiguous: 313 lane-major chunks.  r05q:
+// the earlier rule (lane-major chunks at most twice the contiguous ones) kept the partial last
+// block of the C5 round contiguous, and it set every lane kernel's time (k_outbound 592 us walk
+// against a 256 us mean).
+constexpr uint32_t CHUNK_COST = 10;
 template <uint32_t CH = CD_CHUNK>
-__device__ __forceinline__ bool lane_major_block(int mode, uint32_t n_ev, uint32_t max_n) {
+__device__ __forceinline__ bool lane_major_block(int mode, uint32_t n_ev, uint32_t max_n, uint32_t h_act) {
   if (mode != 2) return mode == 1;
   constexpr uint32_t LK = CH / CD_THREADS;
-  return n_ev > 2u * CH && (max_n + LK - 1) / LK <= 2u * ((n_ev + CH - 1) / CH);
+  if (n_ev <= 2u * CH) return false;  // C4-like blocks: one or two contiguous chunks
+  const uint32_t mean = n_ev / max(h_act, 1u);
+  const uint64_t c_cost = (uint64_t)((n_ev + CH - 1) / CH) * (CHUNK_COST + min(mean, CH));
+  const uint64_t l_cost = (uint64_t)((max_n + LK - 1) / LK) * (CHUNK_COST + LK);
+  return l_cost < c_cost;
 }
 
-// ANY: every lane publishes its host's event range for ChunkMap<true> and the busiest
-// host's event count comes back (a barrier); else nothing (0)
 template <bool ANY>
-__device__ __forceinline__ uint32_t lane_major_setup(uint32_t hb, uint32_t hn, uint32_t* s_hb, uint32_t* s_hn) {
+__device__ __forceinline__ uint32_t lane_major_setup(uint32_t hb, uint32_t hn, uint32_t* s_hb, uint32_t* s_hn,
+                                                     uint32_t& h_act) {
   if constexpr (!ANY) {
+    h_act = 0;
     return 0;
   } else {
     uint32_t max_n = hn;
     for (int o = 32; o > 0; o >>= 1) max_n = max(max_n, (uint32_t)__shfl_xor(max_n, o, 64));
+    h_act = (uint32_t)__popcll(__ballot(hn > 0));  // hosts with events in this call
     s_hb[threadIdx.x] = hb;
     s_hn[threadIdx.x] = hn;
     __syncthreads();
@@ -518,8 +530,9 @@ __global__ void __launch_bounds__(CD_THREADS) k_codel(CodelArgs a) {
   } else {
   __shared__ uint32_t s_hb[CD_HOSTS], s_hn[CD_HOSTS];
   const uint32_t hn = he - hb;
-  const uint32_t max_n = lane_major_setup<ANY>(hb, hn, s_hb, s_hn);
-  with_chunk_map<ANY>(ANY && lane_major_block(LM, p1 - p0, max_n), p0, p1, s_hb, s_hn, [&](auto cm) {
+  uint32_t h_act;
+  const uint32_t max_n = lane_major_setup<ANY>(hb, hn, s_hb, s_hn, h_act);
+  with_chunk_map<ANY>(ANY && lane_major_block(LM, p1 - p0, max_n, h_act), p0, p1, s_hb, s_hn, [&](auto cm) {
   // A chunk's events are loaded into registers a chunk ahead (CD_PF per lane, one round of
   // loads): the next chunk's loads are in flight during this chunk's walk.  At C5 a block walks
   // ~19 lane-major chunks, and each chunk's staging round trips sat in front of its walk.
@@ -911,8 +924,9 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
   }
   } else {
   __shared__ uint32_t s_hb[CD_HOSTS], s_hn[CD_HOSTS];
-  const uint32_t max_n = lane_major_setup<ANY>(hb, he - hb, s_hb, s_hn);
-  with_chunk_map<ANY>(ANY && lane_major_block(LM, p1 - p0, max_n), p0, p1, s_hb, s_hn, [&](auto cm) {
+  uint32_t h_act;
+  const uint32_t max_n = lane_major_setup<ANY>(hb, he - hb, s_hb, s_hn, h_act);
+  with_chunk_map<ANY>(ANY && lane_major_block(LM, p1 - p0, max_n, h_act), p0, p1, s_hb, s_hn, [&](auto cm) {
   for (uint32_t c = 0; cm.has(c, max_n); c++) {
     const uint32_t clen = cm.len(c);
     for (uint32_t base = 0; base < clen; base += CD_THREADS * CD_UNROLL) {  // staging (see ChunkMap)
@@ -1245,8 +1259,10 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
   }
   } else {
   __shared__ uint32_t s_hb[CD_HOSTS], s_hn[CD_HOSTS];
-  const uint32_t max_n = lane_major_setup<ANY>(hb, he - hb, s_hb, s_hn);
-  with_chunk_map<ANY, CH>(ANY && lane_major_block<CH>(LM, p1 - p0, max_n), p0, p1, s_hb, s_hn, [&](auto cm) {
+  uint32_t h_act;
+  const uint32_t max_n = lane_major_setup<ANY>(hb, he - hb, s_hb, s_hn, h_act);
+  with_chunk_map<ANY, CH>(ANY && lane_major_block<CH>(LM, p1 - p0, max_n, h_act), p0, p1, s_hb, s_hn,
+                          [&](auto cm) {
   for (uint32_t c = 0; cm.has(c, max_n); c++) {
     const uint32_t clen = cm.len(c);
     for (uint32_t base = 0; base < clen; base += CD_THREADS * CD_UNROLL) {  // staging (see ChunkMap)
@@ -1584,11 +1600,15 @@ void lane_diag_report(hipStream_t st, const char* name, unsigned long long* d, u
   };
   double mw = 0, me = 0;
   for (uint32_t b = 0; b < nb; b++) mw += walk[b] / nb, me += ev[b] / nb;
+  uint32_t slow = 0;  // the slowest block (its hosts are [64 slow, 64 slow + 64))
+  for (uint32_t b = 1; b < nb; b++)
+    if (dur[b] > dur[slow]) slow = b;
   fprintf(stderr,
           "[lane] %s: %u blocks, span %.2f us, last start +%.2f us; block us p50 %.2f p90 %.2f max %.2f; "
-          "walk us (busiest lane) mean %.2f max %.2f; busiest-lane events mean %.1f max %.0f\n",
+          "walk us (busiest lane) mean %.2f max %.2f; busiest-lane events mean %.1f max %.0f; slowest block %u "
+          "(walk %.2f us, busiest lane %.0f events)\n",
           name, nb, (t_max - t_min) * 0.01, s_max * 0.01, q(dur, 0.5), q(dur, 0.9), q(dur, 1.0), mw, q(walk, 1.0), me,
-          q(ev, 1.0));
+          q(ev, 1.0), slow, walk[slow], ev[slow]);
 }
 
 extern "C" {
