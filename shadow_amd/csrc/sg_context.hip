@@ -132,8 +132,11 @@ static hipEvent_t pool_event(sg_ctx* ctx) {
     ctx->event_pool.pop_back();
     return e;
   }
+  // timing-only events (read after a stream synchronisation): no system-scope fence at
+  // record, whose L2 writeback and invalidation sat inside every timed pair and left the
+  // timed kernel a cold L2 (the HIP header recommends this flag for timing events)
   hipEvent_t e;
-  SG_HIP(hipEventCreate(&e));
+  SG_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
   return e;
 }
 
