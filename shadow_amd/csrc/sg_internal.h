@@ -97,7 +97,7 @@ struct sg_ctx {
   uint32_t err_row = 0, err_col = 0;
   // routing workspace
   sg::DevBuf r_dist, r_dist2, r_flags, r_used, r_err, r_self, r_pair_cnt, r_pair_edge, r_map, r_out_lat,
-      r_out_loss, r_misc, r_dirty, r_work, r_items, r_plan, r_dense, r_done;
+      r_out_loss, r_misc, r_dirty, r_work, r_items, r_plan, r_dense, r_done, r_bucket;
   // delivery workspace
   sg::DevBuf d_seg, d_dst, d_cnt, d_cur, d_keys, d_vals, d_keys2, d_vals2, d_keys3, d_keys4, d_misc,
       d_scan, d_lists, d_lists2, d_ctr0, d_blk, d_spill;
@@ -160,6 +160,10 @@ struct sg_net {
   sg_ctx* ctx = nullptr;
   uint32_t n_nodes = 0, n_edges = 0, n_arcs = 0;
   bool directed = false;
+  // the arcs' smallest latency and mean latency (each clamped to LAT32_SAT), taken on the host
+  // for graphs the bucketed search takes (sg_bucket.hip sizes its bucket width from them)
+  uint32_t arc_lat_min = 0;
+  double arc_lat_mean = 0.0;
   std::vector<uint32_t> gml_id;
   // GML edge list (device)
   uint32_t* e_src = nullptr;
@@ -313,6 +317,15 @@ bool sssp_dense_fits(uint32_t n_nodes);
 void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin,
                        uint32_t row_end, uint64_t* out_lat, float* out_loss, uint32_t* sat_row,
                        unsigned long long* work);
+
+// Per-source delta-stepping search of sparse graphs past the LDS search (sg_bucket.hip): rows
+// [row_begin, row_end); sat_row (zeroed by the caller) receives 1 for rows needing the wide
+// kernel, 2 for rows whose search gave up.  work / diag optional (relaxations; [buckets,
+// entries, far steps, pops]).
+bool sssp_bucket_fits(uint32_t n_nodes);
+void launch_sssp_bucket(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin,
+                        uint32_t row_end, uint64_t* out_lat, float* out_loss, uint32_t* sat_row,
+                        unsigned long long* work, unsigned long long* diag);
 
 constexpr int SSSP_KB_MAX = 8;
 constexpr uint32_t SSSP_UB_EXACT = 0x80000000u;  // bound rows per bounded search (sg_sssp.hip SSSP_KB)

@@ -1240,6 +1240,22 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
     uint32_t bad = 0;
     for (uint32_t e = 0; e < m; e++) bad |= (uint32_t)!(ef[e] >= 0.0f) | (uint32_t)!(ef[e] <= 1.0f);
     for (uint32_t e = 0; e < m; e++) bad |= (uint32_t)(el[e] == 0);
+    // the arcs' latency statistics the bucketed search sizes its buckets from (graphs past the
+    // LDS search, or SG_APSP_BUCKET=1): smallest and mean arc latency, self-loops excluded
+    if (!bad && (!sssp_lds_fits(n) || env_int("SG_APSP_BUCKET", -1) == 1)) {
+      uint64_t lo = LAT32_SAT;
+      double sum = 0.0;
+      uint64_t cnt = 0;
+      for (uint32_t e = 0; e < m; e++) {
+        if (es[e] == ed[e]) continue;
+        const uint64_t l = std::min<uint64_t>(el[e], LAT32_SAT);
+        lo = std::min(lo, l);
+        sum += (double)l;
+        cnt++;
+      }
+      net->arc_lat_min = (uint32_t)lo;
+      net->arc_lat_mean = cnt ? sum / (double)cnt : 0.0;
+    }
     if (bad) {
       // nothing may still run on the block when the caller deletes the net
       (void)hipStreamSynchronize(st);
@@ -1563,6 +1579,47 @@ static void shortest_paths_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_use
   if (!wide_rows.empty()) run_wide(ctx, net, d_used, n_used, wide_rows, row_begin, out_lat, out_loss);
 }
 
+// Sparse graphs past the LDS search (sg_bucket.hip): one delta-stepping search per row, the
+// band of each bucket in LDS, later buckets in a per-workgroup arena; no plan.
+static void shortest_paths_bucket(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
+                                  uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
+  const uint32_t rows = row_end - row_begin;
+  uint32_t* sat = ctx->r_flags.get<uint32_t>(std::max(rows, 1u));
+  SG_HIP(hipMemsetAsync(sat, 0, std::max(rows, 1u) * 4ull, ctx->stream));
+  unsigned long long* work = ctx->count_work ? ctx->r_work.get<unsigned long long>(WORK_SHARDS + 16) : nullptr;
+  unsigned long long* diag = work ? work + WORK_SHARDS : nullptr;
+  if (work) SG_HIP(hipMemsetAsync(work, 0, (WORK_SHARDS + 16) * 8, ctx->stream));
+  {
+    TimedLaunch tl(ctx, "sssp_bucket", 0.0);
+    launch_sssp_bucket(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss, sat, work, diag);
+  }
+  std::vector<uint32_t> wide_rows = finish_rows(ctx, sat, row_begin, rows);
+  if (work) {
+    unsigned long long w[WORK_SHARDS + 16];
+    copy_to_host(ctx, w, work, sizeof(w));
+    double total = 0;
+    for (int k = 0; k < WORK_SHARDS; k++) total += (double)w[k];
+    timer_add_work(ctx, "sssp_bucket", total);
+    if (env_int("SG_BUCKET_DIAG", 0)) {
+      const unsigned long long* d = w + WORK_SHARDS;
+      const double nb = std::max(1.0, (double)d[0]);
+      fprintf(stderr, "[bucket] %u rows: %.1f buckets, %.0f entries, %.2f far steps, %.0f pops in %.0f claims, "
+              "%.0f relaxations (%.3f x arcs) per row\n", rows, d[0] / (double)rows, d[1] / (double)rows,
+              d[2] / (double)rows, d[3] / (double)rows, d[8] / (double)rows, total / rows,
+              total / rows / std::max(1u, net->n_arcs));
+      fprintf(stderr, "[bucket] cycles per bucket (thread 0): phase 0 %.0f, phase 1 %.0f, phase 2 %.0f; output per row %.0f\n",
+              d[4] / nb, d[5] / nb, d[6] / nb, d[7] / (double)rows);
+      fprintf(stderr, "[bucket] band kernel, wave 0 per bucket: offsets %.0f, arcs %.0f, appends %.0f, store wait %.0f\n",
+              d[9] / nb, d[10] / nb, d[11] / nb, d[12] / nb);
+      const double ncl = std::max(1.0, (double)d[8]);
+      fprintf(stderr, "[bucket] per wave and bucket: load step %.0f cyc, idle %.0f; per claim: to offsets %.0f, to "
+              "arcs %.0f (sum over arc rounds), appends %.0f, claim total %.0f\n", d[9] / nb / 4, d[14] / nb / 4,
+              d[10] / ncl, d[11] / ncl, d[12] / ncl, d[13] / ncl);
+    }
+  }
+  if (!wide_rows.empty()) run_wide(ctx, net, d_used, n_used, wide_rows, row_begin, out_lat, out_loss);
+}
+
 static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin, uint32_t row_end, uint64_t* out_lat,
                                float* out_loss) {
   hipStream_t st = ctx->stream;
@@ -1706,8 +1763,16 @@ static void shortest_paths(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, con
     shortest_paths_dense(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss);
     return;
   }
-  if (env_int("SG_APSP_LDS", 1) != 0 && sparse && sssp_lds_fits(net->n_nodes) &&
-      (uint64_t)net->n_arcs * 12 < (1ull << 31)) {
+  // SG_APSP_BUCKET: 1 forces the bucketed search on any sparse graph (tests), 0 keeps the slab
+  // kernel past the LDS search
+  const int bucket_env = env_int("SG_APSP_BUCKET", -1);
+  const bool arcs_ok = (uint64_t)net->n_arcs * 12 < (1ull << 31);
+  if (env_int("SG_APSP_LDS", 1) != 0 && sparse && arcs_ok && bucket_env != 0 && sssp_bucket_fits(net->n_nodes) &&
+      (bucket_env == 1 || !sssp_lds_fits(net->n_nodes))) {
+    shortest_paths_bucket(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss);
+    return;
+  }
+  if (env_int("SG_APSP_LDS", 1) != 0 && sparse && sssp_lds_fits(net->n_nodes) && arcs_ok) {
     shortest_paths_lds(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss);
     return;
   }

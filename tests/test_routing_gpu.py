@@ -29,9 +29,10 @@ def apsp_kernel(request, monkeypatch):
 
 
 def _dense_once(request):
-    """Dense graphs take k_sssp_dense under every LDS setting (lds, lds_bounded, lds_flagged):
-    one of them runs it; the slab fixture runs the slab kernel."""
-    if request.node.callspec.params["apsp_kernel"] in ("lds_bounded", "lds_flagged"):
+    """Dense graphs take k_sssp_dense under every LDS setting (lds, lds_bounded, lds_flagged, and
+    bucket, which takes sparse graphs only): one of them runs it; the slab fixture runs the slab
+    kernel."""
+    if request.node.callspec.params["apsp_kernel"] in ("lds_bounded", "lds_flagged", "bucket"):
         pytest.skip("the dense-graph search runs under the lds fixture")
 
 
@@ -156,7 +157,7 @@ def test_lds_persistent_and_per_row_workgroups(oracle, ctx, monkeypatch, persist
     """More rows than CUs: the LDS search's persistent workgroups (the default, rows
     claimed from a counter) and one workgroup per row (SG_SSSP_PERSIST=0) give the same
     table."""
-    if apsp_kernel == "slab":
+    if apsp_kernel in ("slab", "bucket"):
         pytest.skip("LDS knob")
     monkeypatch.setenv("SG_SSSP_PERSIST", persist)
     g = synth.ring_chords_graph(900, 7.0, seed=31, directed=True)
@@ -299,7 +300,7 @@ def test_empty_used(ctx):
                                  {"SG_APSP_SEG": "4", "SG_APSP_B": "32"}, {"SG_APSP_SEG": "16", "SG_APSP_PASS_CHUNK": "1"}])
 def test_kernel_variants_bit_exact(oracle, ctx, monkeypatch, env, apsp_kernel):
     """Every A/B variant of the slab relaxation kernel (slab width, frontier, item size) is exact."""
-    if apsp_kernel == "lds":
+    if apsp_kernel in ("lds", "bucket"):
         pytest.skip("slab-kernel knobs")
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -415,7 +416,7 @@ def test_lds_bucket_widths(oracle, ctx, monkeypatch, delta, apsp_kernel):
     """The LDS search's bucket width changes the relaxation order only: from
     1 ns (Dijkstra-like, many buckets) to 4 s (one bucket, chaotic Bellman-Ford),
     on a tie-heavy lossy graph, directed and undirected."""
-    if apsp_kernel == "slab":
+    if apsp_kernel in ("slab", "bucket"):
         pytest.skip("LDS knob")
     monkeypatch.setenv("SG_APSP_DELTA", delta)
     for directed in (False, True):
@@ -429,7 +430,8 @@ def test_lds_bucket_widths(oracle, ctx, monkeypatch, delta, apsp_kernel):
 @pytest.mark.parametrize("n", [10900, 11200])
 def test_lds_size_limit(oracle, ctx, n):
     """Node counts just inside and just past the LDS-resident search's limit (the
-    second runs on the slab kernel): sampled rows exact."""
+    second runs on the bucketed search, or the slab kernel under its fixture): sampled
+    rows exact."""
     g = synth.ring_chords_graph(n, 8.0, seed=7)
     used = np.arange(n, dtype=np.uint32)
     for rows in ((0, 64), (n - 64, n)):
@@ -508,3 +510,34 @@ def test_dense_graph_cases(oracle, ctx, case, request):
     lat, _ = _check(oracle, g, used, ctx)
     if case == "wide":
         assert lat.max() >= (1 << 32)
+
+
+@pytest.mark.parametrize("env", [{"SG_BUCKET_DELTA": "4000000000"}, {"SG_BUCKET_DELTA": "4096"},
+                                 {"SG_BUCKET_DELTA": "4194304"}, {"SG_BUCKET_RING": "2"},
+                                 {"SG_BUCKET_RING": "4", "SG_BUCKET_DELTA": "262144"},
+                                 {"SG_BUCKET_HASH": "6"}, {"SG_BUCKET_CHUNKS": "4"},
+                                 {"SG_BUCKET_CHUNKS": "6", "SG_BUCKET_RING": "2"},
+                                 {"SG_BUCKET_STAGE": "0"}, {"SG_BUCKET_STAGE": "40", "SG_BUCKET_DELTA": "30000000"},
+                                 {"SG_BUCKET_THREADS": "1024"}, {"SG_BUCKET_THREADS": "1024", "SG_BUCKET_DELTA": "30000000"},
+                                 {"SG_BUCKET_MODE": "queue"}, {"SG_BUCKET_MODE": "queue", "SG_BUCKET_RING": "2"},
+                                 {"SG_BUCKET_MODE": "queue", "SG_BUCKET_HASH": "6"}])
+def test_bucket_search_knobs(oracle, ctx, monkeypatch, env, apsp_kernel):
+    """The bucketed search (sg_bucket.hip) under its knobs, on a tie-heavy lossy graph (10-ms arc
+    latencies), directed and undirected, a used subset: exact bands (k_sssp_band: the default
+    10-ms width, 4-us and 4-ms), bands past the smallest arc (k_sssp_bucket: one band for the
+    whole row, chaotic relaxation in the hash; 30-ms bands that relax into themselves through the
+    queue; the queue kernel forced at 10 ms), 1024-thread workgroups, rings of 2 and 4 slots (most candidates go to the far lists and come
+    back by far steps), entries stored straight to the arena (no LDS staging) or overflowing a
+    40-entry staging array, and its safety valves -- a 64-slot hash that fills and arenas of 4 and 6
+    chunks that run out: the row gives up, the workgroup leaves, and the wide kernel redoes the
+    row (the output starts poisoned, so no row passes by holding an earlier table)."""
+    if apsp_kernel != "bucket":
+        pytest.skip("bucketed-search knobs")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for directed in (False, True):
+        g = synth.ring_chords_graph(700, 6.0, seed=41, directed=directed, parallel=0.05)
+        g["lat"] = (g["lat"] // 10**7 + 1) * 10**7  # coarse latencies: many equal-latency paths
+        g["loss"] = np.where(np.arange(len(g["loss"])) % 3 == 0, np.float32(0.05), g["loss"]).astype(np.float32)
+        used = np.random.default_rng(41).permutation(700)[:500].astype(np.uint32)
+        _check(oracle, g, used, ctx, poison=True)
