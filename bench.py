@@ -64,6 +64,10 @@ CPU_THREADS = CPU_INFO["nproc"]
 T0 = 946684800 * 10**9  # EmulatedTime SIMULATION_START
 
 
+PMC_DEFAULT = os.path.join(ROOT, "profiles", "pmc_latest.json")
+PMC_C5 = os.path.join(ROOT, "profiles", "pmc_c5_latest.json")
+
+
 def parse_args():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -96,8 +100,9 @@ def parse_args():
                         "more per round) instead of the fixed-split exchange")
     p.add_argument("--no-pack", action="store_true",
                    help="deliver from the two-array table (no packed path-key copy)")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
-                   help="PMC summary (HBM bytes per launch) written by tools/pmc_summary.py")
+    p.add_argument("--pmc-json", default=PMC_DEFAULT,
+                   help="PMC summary (HBM bytes per launch) written by tools/pmc_summary.py (C5: "
+                        "profiles/pmc_c5_latest.json)")
     a = p.parse_args()
     if a.config == "c5":
         a.nodes, a.hosts, a.packets = 50000, 100000, 10000000
@@ -597,9 +602,20 @@ def main():
     from shadow_amd.worker import DeviceTable, HostTable, PacketBatch, Deliveries, deliver_round
 
     ctx = Context(D.local, stream=torch.cuda.current_stream().cuda_stream)
+    # N > 1: the collectives go through the library (sg_comm_*: RCCL on the context's stream, the
+    # calls INTEGRATION.md's Rust caller makes); SG_BENCH_COMM=torch keeps torch.distributed's
+    comm = None
+    if D.dist and os.environ.get("SG_BENCH_COMM", "sg") != "torch":
+        from shadow_amd.comm import maybe_comm
+
+        comm = maybe_comm(ctx, D.dist)
+    collectives = ("sg_comm (RCCL through the C ABI)" if comm else
+                   f"torch.distributed ({D.backend})" if D.dist else None)
     # the PMC summary was collected on the default workload: its per-launch bytes
     # describe no other configuration
-    pmc = load_pmc(a.pmc_json) if a.config == "c3c4" and a.nodes == 10000 else {}
+    if a.config == "c5" and a.pmc_json == PMC_DEFAULT:
+        a.pmc_json = PMC_C5
+    pmc = load_pmc(a.pmc_json) if (a.config == "c3c4" and a.nodes == 10000) or a.config == "c5" else {}
 
     c5 = a.config == "c5"
     if c5:  # 10M packets per round in total, split over the ranks
@@ -638,6 +654,9 @@ def main():
         fresh.close()
 
     def allgather():
+        if comm:  # in place: each rank's block is its own slice of full_lat / full_loss
+            comm.allgather_rows(full_lat, full_loss, rows, nu)
+            return
         if D.coll_dev == "cpu":  # gloo rehearsal: host-staged
             for full, mine in ((full_lat, my_lat), (full_loss, my_loss)):
                 host = full.cpu()
@@ -688,17 +707,40 @@ def main():
     queue_ahead(ctx, torch)
     build()
     timers = {k: ctx.read_timer(k) for k in ("sssp", "sssp_bounded", "relax", "out", "relax_wide", "plan_sets",
-                                             "plan_bounds")}
+                                             "plan_bounds", "sssp_bucket")}
     ctx.enable_timers(True, count_work=True)
     build()
-    works = {k: ctx.read_timer(k)[2] for k in ("sssp", "relax")}
+    works = {k: ctx.read_timer(k)[2] for k in ("sssp", "relax", "sssp_bucket", "sssp_bucket_entries")}
     ctx.enable_timers(False)
     n_arcs = int(net.edge_src.size * 2 - 2 * np.count_nonzero(net.edge_src == net.edge_dst))
     rows_mine = r1 - r0
     dijkstra_relax = float(rows_mine) * n_arcs  # per-source Dijkstra: every arc of every source once
     lds = timers["sssp"][1] > 0
-    pm = pmc.get("sssp" if lds else "relax", {})
-    if lds:
+    band = timers["sssp_bucket"][1] > 0
+    pm = pmc.get("sssp" if lds else "sssp_band" if band else "relax", {})
+    if band:
+        # k_sssp_band (sg_bucket.hip, graphs past the LDS search): per relaxation a 12-B arc record
+        # (L2 / Infinity Cache); per arena entry 12 B written and 12 B read; per cell the settled key
+        # written to and read from the scratch row (8 + 8 B) and the 12-B table cell written
+        k_ms, k_n, _ = timers["sssp_bucket"]
+        k_s = k_ms / 1e3 / max(k_n, 1)
+        relax_per_launch = works["sssp_bucket"] / max(k_n, 1)
+        entries = works["sssp_bucket_entries"] / max(k_n, 1)
+        cells = float(rows_mine) * nu / max(k_n, 1)
+        alg = ARC_BYTES_PER_RELAX * relax_per_launch + 24.0 * entries + 28.0 * cells
+        achieved = alg / k_s / 1e9 if k_n else 0.0
+        roofline = {"kernel": "k_sssp_band", "bound": "l2", "achieved": round(achieved, 1), "peak": L2_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / L2_PEAK_GBS, 4), "traffic": pm.get("hbm_bytes_per_launch"),
+                    "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(k_s * 1e3, 4),
+                    "launches_per_build": k_n, "relaxations_per_launch": relax_per_launch,
+                    "arena_entries_per_launch": entries,
+                    "redundancy_vs_dijkstra": round(relax_per_launch * max(k_n, 1) / max(dijkstra_relax, 1.0), 3),
+                    "valu_frac_pmc": pm.get("valu_frac"),
+                    "hbm_view": {"achieved": round(alg / k_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(alg / k_s / 1e9 / HBM_PEAK_GBS, 4),
+                                 "what": "the same algorithmic bytes against HBM (arena and table pass HBM; "
+                                         "the arcs sit in L2 / the Infinity Cache)"}}
+    elif lds:
         # k_sssp_lds: a 12-B arc record gathered from L2 per relaxation; its HBM
         # traffic is the 12-B (latency, loss) cell per table entry.  A build is one
         # launch, or three (the bounded phases, timer sssp_bounded): per-launch
@@ -743,14 +785,14 @@ def main():
     # the batched-source slab kernel on the same rows, for comparison (the default above 10.9k nodes)
     t_slab = None
     t_unbounded = None
-    if lds and not a.no_compare:
+    if (lds or band) and not a.no_compare:
         os.environ["SG_APSP_LDS"] = "0"
         t_slab = timed(D, build, max(1, a.steps // 2), 1)
         os.environ.pop("SG_APSP_LDS")
-        # and the LDS search in one launch with every key from infinity (no bound rows)
-        os.environ["SG_SSSP_SEEDS"] = "0"
-        t_unbounded = timed(D, build, max(1, a.steps // 2), 1)
-        os.environ.pop("SG_SSSP_SEEDS")
+        if lds:  # and the LDS search in one launch with every key from infinity (no bound rows)
+            os.environ["SG_SSSP_SEEDS"] = "0"
+            t_unbounded = timed(D, build, max(1, a.steps // 2), 1)
+            os.environ.pop("SG_SSSP_SEEDS")
 
     # end to end: the whole table into the dense host RoutingInfo (sg_routing_info_fill:
     # row blocks built on the GPU, copied into pinned host memory while the next builds)
@@ -896,7 +938,7 @@ def main():
         out = Deliveries.allocate(a.packets, a.hosts)
         round_end, sim_end = T0 + 10**9 + 10**6, 2**63
         # padded: after the first (warm-up) round, the fixed-split exchange with one host sync per round
-        sharded = ShardedDelivery(ctx, ht, table, part, D.rank, D.world, dist=D.dist,
+        sharded = ShardedDelivery(ctx, ht, table, part, D.rank, D.world, dist=comm or D.dist,
                                   padded=not a.exact_exchange) if D.world > 1 else None
 
         def rnd():
@@ -1028,8 +1070,11 @@ def main():
             result["inbound"] = inbound_leg(a, D, ctx, torch, buckets, a.packets, pmc, round_end)
             result["outbound"] = outbound_leg(a, D, ctx, torch, pk, hosts, ht, table, round_end, sharded, pmc)
 
+    result["collectives"] = collectives
     if D.rank == 0:
         print(json.dumps(result), flush=True)
+    if comm:
+        comm.close()
     if D.dist:
         D.dist.destroy_process_group()
 

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 6
+#define SG_ABI_VERSION 7
 
 typedef enum sg_status {
   SG_OK = 0,
@@ -50,6 +50,7 @@ typedef enum sg_status {
   SG_ERR_UNSORTED = 8,      /* sg_deliver_round: packets not grouped by ascending source host */
   SG_ERR_DUPLICATE_IP = 9,  /* two hosts with one address (IpAssignment::assign_ip, graph/mod.rs:383-394) */
   SG_ERR_CAPACITY = 10,     /* a CoDel queue outgrew its ring (sg_codel_create ring_cap) */
+  SG_ERR_UNSUPPORTED = 12,  /* sg_comm_*: RCCL (librccl.so.1) could not be opened (ABI 7) */
   SG_ERR_TIME_OVERFLOW = 11 /* send time + latency past EMUTIME_MAX: EmulatedTime + SimulationTime
                                panics in the reference (emulated_time.rs:121-126, worker.rs:381) */
 } sg_status;
@@ -398,6 +399,39 @@ int32_t sg_deliver_bucket_padded(sg_ctx* ctx, const sg_record* recv_padded, uint
                                  sg_round_stats* stats, uint32_t* recv_counts, uint32_t* pair_max);
 int32_t sg_deliver_pad_to_compact(sg_ctx* ctx, const sg_record* send_padded, uint32_t n_ranks, uint32_t cap,
                                   const uint64_t* xrow, sg_record* send);
+
+/* ---- collectives of the sharded path over RCCL (ABI 7) --------------------
+ * One communicator per rank (one process per GPU), bound to an sg_ctx: every call
+ * is enqueued on the context's stream, after the library's kernels, and returns
+ * without synchronising.  They replace the hand-offs between the reference's
+ * worker threads (Worker::push_packet_to_host, worker.rs:597-607, run from the
+ * manager's round loop, manager.rs:415-501) and the routing table every worker
+ * reads (NetworkGraph::compute_shortest_paths, graph/mod.rs:183-228, computed once,
+ * sim_config.rs:137-141) once rows and hosts are sharded over GPUs.  RCCL is
+ * opened at run time (librccl.so.1); without it these return SG_ERR_UNSUPPORTED
+ * and everything else works.
+ *   sg_comm_unique_id: on one rank; the caller passes the bytes to every rank.
+ *   sg_comm_allgather_rows: in place, rank r's rows [r rows_per_rank, (r + 1)
+ *     rows_per_rank) of the n_used-column table (device lat u64 / loss f32; either
+ *     may be NULL) to every rank.
+ *   sg_comm_exchange_padded: step 2 of the fixed-split round above: xrow (3 +
+ *     n_ranks u64, device) all-gathered into xall, and cap records per rank pair
+ *     from send_padded to recv_padded (n_ranks blocks each).
+ *   sg_comm_alltoallv_records: the exact exchange of sg_deliver_source's records
+ *     (grouped by rank: send_counts[r] for rank r), received rank after rank;
+ *     send_counts / recv_counts are host arrays of n_ranks.
+ *   sg_comm_allgather_u64: n u64 per rank (device) into all (n_ranks x n).   */
+typedef struct sg_comm sg_comm;
+#define SG_COMM_ID_BYTES 128
+int32_t sg_comm_unique_id(uint8_t* id /* SG_COMM_ID_BYTES */);
+int32_t sg_comm_create(sg_ctx* ctx, const uint8_t* id, uint32_t n_ranks, uint32_t rank, sg_comm** out);
+void sg_comm_destroy(sg_comm* comm);
+int32_t sg_comm_allgather_rows(sg_comm* comm, uint64_t* lat, float* loss, uint32_t rows_per_rank, uint32_t n_used);
+int32_t sg_comm_exchange_padded(sg_comm* comm, const sg_record* send_padded, sg_record* recv_padded, uint32_t cap,
+                                const uint64_t* xrow, uint64_t* xall);
+int32_t sg_comm_alltoallv_records(sg_comm* comm, const sg_record* send, const uint32_t* send_counts,
+                                  sg_record* recv, const uint32_t* recv_counts);
+int32_t sg_comm_allgather_u64(sg_comm* comm, const uint64_t* mine, uint64_t* all, uint32_t n);
 
 /* ---- router inbound CoDel queues (one per host) ---------------------------
  * Router::inbound_packets (router/mod.rs:15-58): each host's CoDelQueue

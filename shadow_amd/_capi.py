@@ -14,7 +14,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "shadow_gpu.h")
 
 # sg_status (include/shadow_gpu.h)
 SG_OK = 0
-SG_ABI_VERSION = 6  # include/shadow_gpu.h
+SG_ABI_VERSION = 7  # include/shadow_gpu.h
 SG_ERR_NO_EDGE = 1
 SG_ERR_MULTI_EDGE = 2
 SG_ERR_UNREACHABLE = 3
@@ -26,6 +26,8 @@ SG_ERR_UNSORTED = 8
 SG_ERR_DUPLICATE_IP = 9
 SG_ERR_CAPACITY = 10
 SG_ERR_TIME_OVERFLOW = 11
+SG_ERR_UNSUPPORTED = 12
+SG_COMM_ID_BYTES = 128
 
 SG_ROUTE_SHORTEST_PATH = 0x1
 SG_ROUTE_OUT_DEVICE = 0x2
@@ -48,6 +50,8 @@ EXPORTED = [
     "sg_routing_info_view", "sg_routing_info_rows", "sg_routing_info_index", "sg_routing_info_path", "sg_routing_info_smallest_latency",
     "sg_routing_info_increment_packet_count", "sg_routing_info_packet_count", "sg_routing_info_set_addresses",
     "sg_worker_get_latency", "sg_worker_get_reliability", "sg_worker_is_routable",
+    "sg_comm_unique_id", "sg_comm_create", "sg_comm_destroy", "sg_comm_allgather_rows", "sg_comm_exchange_padded",
+    "sg_comm_alltoallv_records", "sg_comm_allgather_u64",
 ]
 
 
@@ -245,6 +249,13 @@ def load(path: str | None = None):
         "sg_outbound_run": (i32, [vp, vp, C.POINTER(sg_outbound_sends), u64, u64, u64, vp, vp, vp, u32,
                                   C.POINTER(sg_outbound_sent), C.POINTER(C.c_uint32)]),
         "sg_outbound_get_state": (i32, [vp, C.POINTER(sg_outbound_queue_state), C.POINTER(sg_inbound_relay_state)]),
+        "sg_comm_unique_id": (i32, [vp]),
+        "sg_comm_create": (i32, [vp, vp, u32, u32, C.POINTER(vp)]),
+        "sg_comm_destroy": (None, [vp]),
+        "sg_comm_allgather_rows": (i32, [vp, vp, vp, u32, u32]),
+        "sg_comm_exchange_padded": (i32, [vp, vp, vp, u32, vp, vp]),
+        "sg_comm_alltoallv_records": (i32, [vp, vp, u32p, vp, u32p]),
+        "sg_comm_allgather_u64": (i32, [vp, vp, vp, u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)

@@ -1287,7 +1287,11 @@ static void launch_sssp_band(sg_ctx* ctx, sg_net* net, BkArgs a, uint32_t n_used
   const uint32_t n = net->n_nodes;
   a.hs_log2 = (uint32_t)std::max(6, std::min(14, bk_env("SG_BUCKET_HASH", 11)));
   a.nch = (uint32_t)std::max(4, std::min(65534, bk_env("SG_BUCKET_CHUNKS", 384)));
-  a.stg_cap = (uint32_t)std::max(0, std::min((int)BD_E_MAX, bk_env("SG_BUCKET_STAGE", 8)));
+  // per-slot staging of the band's appends: off by default -- it coalesces the entry stores but
+  // measured slower at C5 (8,192 rows: 47.5 ms with 8 entries per slot, 64.2 ms with 16 (three
+  // rows per CU), 45.8 ms without; profiles/r05/ab_band_stage.txt): the kernel is bound by the
+  // texture-address unit's lane accesses, not by write requests
+  a.stg_cap = (uint32_t)std::max(0, std::min((int)BD_E_MAX, bk_env("SG_BUCKET_STAGE", 0)));
   const size_t lds = BdLds(n, 1u << a.hs_log2, a.nch, 4, a.stg_cap).bytes;
   if (lds + 256 > 160 * 1024) throw Error(SG_ERR_INVALID_ARG, "graph too large for the banded search");
   const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>((size_t)bk_env("SG_BUCKET_PER_CU", 8),

@@ -1600,6 +1600,7 @@ static void shortest_paths_bucket(sg_ctx* ctx, sg_net* net, const uint32_t* d_us
     double total = 0;
     for (int k = 0; k < WORK_SHARDS; k++) total += (double)w[k];
     timer_add_work(ctx, "sssp_bucket", total);
+    timer_add_work(ctx, "sssp_bucket_entries", (double)w[WORK_SHARDS + 1]);  // entries through the arena
     if (env_int("SG_BUCKET_DIAG", 0)) {
       const unsigned long long* d = w + WORK_SHARDS;
       const double nb = std::max(1.0, (double)d[0]);

@@ -11,7 +11,10 @@ Delivery: hosts are owned by the rank that holds their routing row
   1. source phase on every rank (sg_deliver_source): the send_packet half for
      the packets its hosts sent, records packed by destination owner;
   2. all-to-all of the per-rank record counts, then of the records
-     (32 B each; torch.distributed "nccl" = RCCL);
+     (32 B each).  With a comm.Comm in place of `dist` (the default on RCCL
+     process groups) every exchange is a call into the library (sg_comm_*,
+     RCCL on the context's stream), the same calls the Rust caller makes
+     (INTEGRATION.md); torch.distributed remains for gloo rehearsals;
   3. destination phase (sg_deliver_bucket): per-destination EventQueue order.
 With `padded=True` (ShardedDelivery) the rounds after the first use a
 fixed-split exchange with no host round trip before the round's end: every
@@ -33,6 +36,7 @@ import numpy as np
 
 from . import _capi
 from ._capi import check, load
+from .comm import is_comm
 
 NONE = 0xFFFFFFFF
 RECORD_DTYPE = np.dtype([("deliver_time_ns", "<u8"), ("order_key", "<u8"), ("event_id", "<u8"),
@@ -294,13 +298,35 @@ def next_cap(pair_max: int) -> int:
 # ---------------------------------------------------------------------------
 # Exchange
 # ---------------------------------------------------------------------------
+def _comm_in(comm, t) -> None:
+    """The library's stream waits for torch's current stream (which wrote `t`)."""
+    st = _streams(comm.ctx, t)
+    if st:
+        _stream_wait(st[0], st[1])
+
+
+def _comm_out(comm, t) -> None:
+    """torch's current stream waits for the library's stream (which wrote `t`)."""
+    st = _streams(comm.ctx, t)
+    if st:
+        _stream_wait(st[1], st[0])
+
+
 def exchange_padded(send_padded, xrow, dist, group=None, ws: Optional[Workspace] = None):
     """The fixed-split exchange: one all-gather of the [stats, counts] rows and one
-    equal-split all_to_all_single of the record blocks, both enqueued on the stream
-    with no host round trip.  Returns (recv_padded, xall)."""
+    equal-split all-to-all of the record blocks, both enqueued on the stream with no
+    host round trip.  `dist` is a comm.Comm (sg_comm_exchange_padded in the library,
+    RCCL on the context's stream) or torch.distributed (gloo rehearsals: host-staged).
+    Returns (recv_padded, xall)."""
     import torch
 
     world = dist.get_world_size(group) if dist is not None else 1
+    if is_comm(dist):
+        ws = ws or Workspace()
+        xall = ws.get("xall", world * xrow.shape[0], torch.int64, send_padded.device)
+        recv = ws.get("recv_padded", send_padded.shape[0], torch.int64, send_padded.device, cols=4)
+        dist.exchange_padded(send_padded, recv, send_padded.shape[0] // max(world, 1), xrow, xall)
+        return recv, xall
     if dist is not None and _host_staged(dist, group, send_padded.device):
         recv, xall = exchange_padded(send_padded.cpu(), xrow.cpu(), dist, group)
         return recv.to(send_padded.device), xall.to(send_padded.device)
@@ -318,7 +344,7 @@ def exchange_padded(send_padded, xrow, dist, group=None, ws: Optional[Workspace]
 def _host_staged(dist, group, dev) -> bool:
     """gloo moves host tensors only: device tensors go through host copies (the
     multi-rank rehearsal on a box with fewer GPUs than ranks; RCCL needs none)."""
-    return dev.type != "cpu" and dist.get_backend(group) == "gloo"
+    return not is_comm(dist) and dev.type != "cpu" and dist.get_backend(group) == "gloo"
 
 
 def all_to_all_records(send, send_counts: List[int], dist, group=None):
@@ -360,7 +386,12 @@ def exchange_round(send, send_counts: List[int], stats, rank: int, dist, group=N
     mine_d = ws.get("x_mine_d", w, torch.int64, dev)
     mine_d.copy_(mine_h, non_blocking=True)
     out = ws.get("x_out_d", world * w, torch.int64, dev)
-    dist.all_gather_into_tensor(out, mine_d, group=group)
+    if is_comm(dist):
+        _comm_in(dist, mine_d)
+        dist.allgather_u64(mine_d, out)
+        _comm_out(dist, out)
+    else:
+        dist.all_gather_into_tensor(out, mine_d, group=group)
     out_h = ws.get("x_out_h", world * w, torch.int64, "cpu", pinned=pinned)
     out_h.copy_(out, non_blocking=True)
     if pinned:
@@ -382,6 +413,11 @@ def _records_all_to_all(send, send_counts: List[int], recv_counts: List[int], di
     n_recv = sum(recv_counts)
     recv = (ws or Workspace()).get("x_recv", max(n_recv, 1), torch.int64, dev, cols=4)
     n_send = sum(send_counts)
+    if is_comm(dist):
+        _comm_in(dist, send)
+        dist.alltoallv_records(send, send_counts, recv, recv_counts)
+        _comm_out(dist, recv)
+        return recv[:n_recv]
     dist.all_to_all_single(recv[:n_recv], send[:n_send], output_split_sizes=recv_counts,
                            input_split_sizes=list(send_counts), group=group)
     return recv[:n_recv]
@@ -397,7 +433,11 @@ def gather_round_stats(n_delivered: int, min_deliver: int, min_lat: int, dist, g
     t = torch.from_numpy(mine.copy()).to(device)
     world = dist.get_world_size(group) if dist is not None else 1
     out = torch.empty(3 * world, dtype=torch.int64, device=device)
-    if dist is None or world == 1:
+    if is_comm(dist):
+        _comm_in(dist, t)
+        dist.allgather_u64(t, out)
+        _comm_out(dist, out)
+    elif dist is None or world == 1:
         out.copy_(t)
     elif _host_staged(dist, group, out.device):
         host = out.cpu()
@@ -416,6 +456,13 @@ def _global_max(v: int, dist, group=None, device="cuda") -> int:
     world = dist.get_world_size(group) if dist is not None else 1
     if dist is None or world == 1:
         return int(v)
+    if is_comm(dist):
+        mine = torch.tensor([int(v)], dtype=torch.int64, device=device)
+        out = torch.empty(world, dtype=torch.int64, device=device)
+        _comm_in(dist, mine)
+        dist.allgather_u64(mine, out)
+        _comm_out(dist, out)
+        return int(out.max().item())
     dev = "cpu" if _host_staged(dist, group, torch.device(device)) else device
     out = torch.empty(world, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(out, torch.tensor([int(v)], dtype=torch.int64, device=dev), group=group)

@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
     assert declared == set(_capi.EXPORTED)
     for name in sorted(declared):
         assert hasattr(L, name), name
-    assert L.sg_abi_version() == _capi.SG_ABI_VERSION == 6
+    assert L.sg_abi_version() == _capi.SG_ABI_VERSION == 7
 
 
 def test_missing_library_fails_loudly(tmp_path, monkeypatch):

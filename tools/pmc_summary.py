@@ -32,6 +32,7 @@ KERNELS = {"relax_wide": "k_relax_wide", "sssp_fill": "k_sssp_lds<false, 1024, 8
            "outbound": "k_outbound",
            "out_compact": "k_out_compact",
            "sssp_dense": "k_sssp_dense", "dense_sort": "k_sort_arcs",
+           "sssp_band": "k_sssp_band<false", "sssp_bucket": "k_sssp_bucket<false",
            "init": "k_init_batch"}
 VALU_PEAK_OPS_PER_NS = 256 * 4 * 32 * 2.4  # 78.6e3 lane-ops per ns (MI355X_MICROARCH.md chip table)
 

@@ -1,16 +1,18 @@
 #!/bin/bash
 # rocprofv3 evidence for profiles/: kernel-trace stats, then separate PMC passes.
-# Usage (on the GPU box): bash tools/profile_round.sh r01
+# Usage (on the GPU box): bash tools/profile_round.sh r01 [c5]
 set -u
 TAG=${1:-r01}
+CFG=${2:-c3c4}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 ARGS="--steps 3 --warmup 1 --no-cpu --no-compare"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 bench.py $ARGS > $OUT/stats.log 2>&1 || { echo "stats pass failed"; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS > $OUT/write.log 2>&1 || { echo "write pass failed"; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv -d $OUT/sq -o run -- python3 bench.py $ARGS > $OUT/sq.log 2>&1 || { echo "sq pass failed"; exit 1; }
+[ "$CFG" = c5 ] && ARGS="--config c5 --steps 1 --warmup 1 --no-cpu --no-compare --no-gml --no-c2 --rank-blocks 8"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 bench.py $ARGS > $OUT/stats.log 2>&1 || { echo "stats pass failed"; exit 1; }
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS > $OUT/write.log 2>&1 || { echo "write pass failed"; exit 1; }
+timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv -d $OUT/sq -o run -- python3 bench.py $ARGS > $OUT/sq.log 2>&1 || { echo "sq pass failed"; exit 1; }
 python3 tools/pmc_summary.py --stats $OUT/stats --fetch $OUT/fetch --write $OUT/write --sq $OUT/sq -o $OUT/pmc_$TAG.json > /dev/null
 find $OUT -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats_$TAG.csv \;
 echo "profile done"

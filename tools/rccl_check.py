@@ -1,6 +1,11 @@
 #!/usr/bin/env python3
 """The multi-GPU code path over real RCCL on one GPU (world size 1, backend "nccl").
 
+Every check runs twice: with the collectives through the library's C ABI
+(shadow_amd.comm.Comm: sg_comm_allgather_rows, sg_comm_exchange_padded,
+sg_comm_alltoallv_records, sg_comm_allgather_u64 -- RCCL on the context's stream,
+the calls the Rust caller of INTEGRATION.md makes) and through torch.distributed.
+
 Run as a child process by tests/test_rccl_gpu.py (RCCL needs a process of its
 own per rank; two ranks cannot share a device).  It drives, on device tensors:
   * the APSP row-block all-gather (all_gather_into_tensor, as bench.py does),
@@ -27,6 +32,7 @@ def main():
     import torch.distributed as dist
 
     from shadow_amd import Context, NetworkGraph, synth
+    from shadow_amd.comm import Comm
     from shadow_amd.dist import RECORD_DTYPE, HostPartition, ShardedDelivery, exchange_round
     from shadow_amd.worker import DeviceTable, HostTable, PacketBatch, deliver_round
 
@@ -37,6 +43,22 @@ def main():
     dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
     assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
     ctx = Context(0, stream=torch.cuda.current_stream().cuda_stream)
+    comm = Comm.from_torch(ctx, dist)
+    assert comm.n_ranks == 1 and comm.rank == 0
+    res = {}
+    for name, exch in (("sg_comm", comm), ("torch", dist)):
+        res[name] = check(ctx, exch, dist, torch)
+    comm.close()
+    print(json.dumps({"ok": True, "backend": dist.get_backend(), **res["sg_comm"],
+                      "torch_collectives": res["torch"]}), flush=True)
+    dist.destroy_process_group()
+
+
+def check(ctx, exch, dist, torch):
+    from shadow_amd import NetworkGraph, synth
+    from shadow_amd.comm import is_comm
+    from shadow_amd.dist import RECORD_DTYPE, HostPartition, ShardedDelivery, exchange_round
+    from shadow_amd.worker import DeviceTable, HostTable, PacketBatch, deliver_round
 
     # ---- APSP rows + the RCCL all-gather of the row blocks
     n = 600
@@ -46,10 +68,14 @@ def main():
     mine_lat = torch.empty(n * n, dtype=torch.int64, device="cuda")
     mine_loss = torch.empty(n * n, dtype=torch.float32, device="cuda")
     net.build_rows_device(used, 0, n, mine_lat.data_ptr(), mine_loss.data_ptr(), True)
-    full_lat = torch.empty_like(mine_lat)
-    full_loss = torch.empty_like(mine_loss)
-    dist.all_gather_into_tensor(full_lat, mine_lat)
-    dist.all_gather_into_tensor(full_loss, mine_loss)
+    if is_comm(exch):  # in place: the rank's block is its slice of the table
+        full_lat, full_loss = mine_lat, mine_loss
+        exch.allgather_rows(full_lat, full_loss, n, n)
+    else:
+        full_lat = torch.empty_like(mine_lat)
+        full_loss = torch.empty_like(mine_loss)
+        dist.all_gather_into_tensor(full_lat, mine_lat)
+        dist.all_gather_into_tensor(full_loss, mine_loss)
     torch.cuda.synchronize()
     ref = net.compute_shortest_paths(used)
     assert np.array_equal(full_lat.cpu().numpy().view(np.uint64).reshape(n, n), ref.latency_ns)
@@ -63,7 +89,7 @@ def main():
     batch = PacketBatch.from_numpy(pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"])
     part = HostPartition(hosts["route"], n, 1)
     ht_s = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
-    sd = ShardedDelivery(ctx, ht_s, table, part, 0, 1, dist=dist)
+    sd = ShardedDelivery(ctx, ht_s, table, part, 0, 1, dist=exch)
     src, recv, recv_counts, order, offsets = sd.round(batch, end, 2**63, start + 100_000)
     ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
     out = deliver_round(ht, table, batch, end, 2**63, start + 100_000)
@@ -82,7 +108,7 @@ def main():
 
     # ---- the fixed-split exchange (padded=True): round 1 exact (sizes the blocks), then padded
     ht_p = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
-    sdp = ShardedDelivery(ctx, ht_p, table, part, 0, 1, dist=dist, padded=True)
+    sdp = ShardedDelivery(ctx, ht_p, table, part, 0, 1, dist=exch, padded=True)
     ht_r = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
     for k in range(3):
         src_p, recv_p, rc_p, order_p, offs_p = sdp.round(batch, end, 2**63, start + 100_000)
@@ -108,7 +134,7 @@ def main():
     stats = (int(src.n_delivered), int(src.min_deliver_time_ns), int(src.min_used_latency_ns))
     t0 = time.perf_counter()
     for _ in range(reps):
-        exchange_round(src.send, src.send_counts, stats, 0, dist)
+        exchange_round(src.send, src.send_counts, stats, 0, exch)
     torch.cuda.synchronize()
     t_ex = (time.perf_counter() - t0) / reps
     t0 = time.perf_counter()
@@ -130,7 +156,7 @@ def main():
         s = gpu_source_phase(ctx, ht_s, table, batch, end, 2**63, start + 100_000, sd.owner_dev, 1)
         t1 = time.perf_counter()
         rv, rc, _ = exchange_round(s.send, s.send_counts, (int(s.n_delivered), int(s.min_deliver_time_ns),
-                                                           int(s.min_used_latency_ns)), 0, dist)
+                                                           int(s.min_used_latency_ns)), 0, exch)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         gpu_bucket_phase(ctx, rv, int(sum(rc)), sd.local_dev, len(part.local), part.n_local(0))
@@ -139,12 +165,11 @@ def main():
         ph["source"] += (t1 - t0) / reps
         ph["exchange"] += (t2 - t1) / reps
         ph["bucket"] += (t3 - t2) / reps
-    print(json.dumps({"ok": True, "backend": dist.get_backend(), "packets": P, "records": int(sum(recv_counts)),
-                      "sharded_round_ms": round(t_round * 1e3, 4), "exchange_round_ms": round(t_ex * 1e3, 4),
-                      "sharded_round_padded_ms": round(t_padded * 1e3, 4), "padded_cap": sdp.cap,
-                      "single_gpu_round_ms": round(t_single * 1e3, 4),
-                      "phases_ms": {k: round(v * 1e3, 4) for k, v in ph.items()}}), flush=True)
-    dist.destroy_process_group()
+    return {"packets": P, "records": int(sum(recv_counts)),
+            "sharded_round_ms": round(t_round * 1e3, 4), "exchange_round_ms": round(t_ex * 1e3, 4),
+            "sharded_round_padded_ms": round(t_padded * 1e3, 4), "padded_cap": sdp.cap,
+            "single_gpu_round_ms": round(t_single * 1e3, 4),
+            "phases_ms": {k: round(v * 1e3, 4) for k, v in ph.items()}}
 
 
 if __name__ == "__main__":
