@@ -166,6 +166,14 @@ class Dist:
         return float(t.item())
 
 
+_T_START = time.perf_counter()
+
+
+def note(msg: str) -> None:
+    """A progress line on stderr (a long run stays visibly alive; stdout keeps the one JSON line)."""
+    print(f"[bench {time.perf_counter() - _T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def timed(D, fn, steps, warmup):
     torch = D.torch
     for _ in range(warmup):
@@ -680,6 +688,7 @@ def main():
     # The sharded build rehearsed on this one GPU: every rank's row block of an N-way split,
     # one-shot (upload, the block's own plan, search, release) as that rank would build it.
     # max_ms is the N-GPU build time less the all-gather; frac_of_linear = (one-shot / N) / max_ms.
+    note(f"routing build timed: {t_build * 1e3:.3f} ms one-shot")
     rank_blocks = None
     if D.world == 1 and a.rank_blocks:
         rank_blocks = {}
@@ -796,6 +805,7 @@ def main():
 
     # end to end: the whole table into the dense host RoutingInfo (sg_routing_info_fill:
     # row blocks built on the GPU, copied into pinned host memory while the next builds)
+    note("instrumented builds and comparisons done")
     e2e = None
     if D.world == 1:
         from shadow_amd import RoutingInfo
@@ -816,6 +826,7 @@ def main():
                "what": "sg_routing_info_fill: kernel + D2H of the whole table into the dense host RoutingInfo"}
         del ri
 
+    note("end-to-end RoutingInfo fill done")
     cpu = None
     parity = None
     cpu_faithful = None
@@ -908,10 +919,13 @@ def main():
         if e2e:
             result["apsp_detail"]["speedup_vs_cpu_faithful_end_to_end"] = round(cpu_faithful["value"] / (e2e["ms"] / 1e3), 1)
     if D.rank == 0 and not a.no_gml:
+        note("GML ingest leg")
         result["gml_ingest"] = gml_leg(a, NetworkGraph, synth)
     if D.rank == 0 and not a.no_c2:
+        note("C2 leg")
         result["c2"] = c2_leg(a, ctx, torch, NetworkGraph, synth, D.world == 1 and not a.no_cpu, pmc)
 
+    note("delivery leg")
     # ---------------- delivery round (C4) ----------------
     if not a.no_delivery:
         from shadow_amd.dist import HostPartition, ShardedDelivery
@@ -949,6 +963,7 @@ def main():
 
         # a round is ~0.1 ms: at least 100 of them, so one host-side hiccup moves the mean little
         t_round = timed(D, rnd, max(a.steps, SUB_MS_REPS), a.warmup)
+        note(f"delivery round timed: {t_round * 1e3:.4f} ms")
         per_rank = None
         if sharded:  # load balance of the host partition: packets sent, records sent / received per rank
             mine_c = [float(a.packets), float(sum(sharded.last_send_counts)), float(sum(sharded.last_recv_counts))]
@@ -1021,6 +1036,7 @@ def main():
             rng0 = np.stack([O.xoshiro_seed(int(s)) for s in hosts["seed"]]).astype(np.uint64)
             ctr0 = np.zeros(a.hosts, np.uint64)
             th = CPU_THREADS  # the box's CPU share (16 logical CPUs per GPU)
+            note("delivery: CPU baseline round")
             orng, octr = rng0.copy(), ctr0.copy()
             t0 = time.perf_counter()
             wr = O.deliver_round(round_end, sim_end, 0, src_global, pk["dst_ip"], pk["payload"], pk["send_time"],
@@ -1048,6 +1064,10 @@ def main():
             # Dns / IpAssignment / RoutingInfo lookups (a map of every node pair), the global
             # RwLock'd packet counter, a mutex'd binary heap per destination queue
             frng, fctr = rng0.copy(), ctr0.copy()
+            note("delivery: faithful CPU baseline round" + (" skipped at C5" if c5 else ""))
+        if D.rank == 0 and D.world == 1 and not a.no_cpu and not c5:
+            # (C5: the reference's node-pair map would hold 2.5e9 entries; the dense port above is
+            # the C5 baseline)
             fr = O.deliver_faithful(round_end, sim_end, 0, src_global, pk["dst_ip"], pk["payload"], pk["send_time"],
                                     hosts["ip"], hosts["route"], lat_h, loss_h, frng, fctr, threads=th)
             fsame = all(np.array_equal(fr[k], wr[k]) for k in ("status", "deliver_time", "event_id", "dst_order",
@@ -1066,8 +1086,11 @@ def main():
         result["delivery"] = delivery
         if not a.no_codel:
             buckets = round_buckets(out, pk["payload"], sharded)
+            note("CoDel leg")
             result["codel"] = codel_leg(a, D, ctx, torch, buckets, a.packets, pmc)
+            note("inbound leg")
             result["inbound"] = inbound_leg(a, D, ctx, torch, buckets, a.packets, pmc, round_end)
+            note("outbound leg")
             result["outbound"] = outbound_leg(a, D, ctx, torch, pk, hosts, ht, table, round_end, sharded, pmc)
 
     result["collectives"] = collectives

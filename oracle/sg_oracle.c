@@ -1032,6 +1032,8 @@ int sgo_outbound_run(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip, ui
       int send_first = has_send && (!has_task || time[e] < tt);
       if (has_send && has_task && time[e] == tt) {
         /* one EmulatedTime: Packet events, then Local events by id = creation order */
+        if (ev_id && ev_id[e] != UINT64_MAX && ev_born[e] == tborn && ev_id[e] == tid)
+          return -6; /* the send's key is the pending task's: two events with one id */
         send_first = !ev_id || ev_id[e] == UINT64_MAX || ev_born[e] < tborn ||
                      (ev_born[e] == tborn && ev_id[e] < tid);
       }
@@ -1057,6 +1059,11 @@ int sgo_outbound_run(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip, ui
         e++;
       } else if (has_task) { /* run_forward_task -> forward_until_blocked */
         const uint64_t now = tt;
+        /* the next send's event exists from its creation on: a task running after that time
+           (it may reschedule itself) finds the host's counter past its id.  At the creation
+           time itself the order of the task and the creating event is not known: no bump */
+        if (has_send && ev_id && ev_id[e] != UINT64_MAX && tt > ev_born[e] && event_ctr[h] <= ev_id[e])
+          event_ctr[h] = ev_id[e] + 1;
         rf &= (uint8_t)~RL_PENDING;
         for (;;) {
           size_t slot;

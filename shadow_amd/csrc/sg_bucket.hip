@@ -912,7 +912,8 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
     for (;;) {  // bands
       if (COUNT) n_bk++;
       // ---- load: bucket b's entries into the hash, the smallest key per node (a settled node's are stale)
-      for (uint32_t q = tid; q < R; q += NT) cst[q] = cnt[q];  // the ring's counts before this band's appends
+      if (E)  // the ring's counts before this band's appends (the staging's arena positions)
+        for (uint32_t q = tid; q < R; q += NT) cst[q] = cnt[q];
       {
         const uint32_t sb = b & rmask, c = cnt[sb];
         for (uint32_t i0 = tid; i0 < c; i0 += NT * BD_G) {
@@ -1017,7 +1018,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
           }
         }
       }
-      __syncthreads();  // every append staged
+      if (E) __syncthreads();  // every append staged
       // the staged runs: slot q's entries cst[q] .. cst[q] + min(its appends, E), consecutive threads on
       // consecutive entries of a slot
       for (uint32_t t = tid; t < R * E; t += NT) {

@@ -1230,10 +1230,18 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
           }
           last_born = born;
           last_id = id;
-          while (due(now) || due_tie(now, born, id)) out_task(q, r, r.tt, a, ctr_inc);
-          // the sending event exists, so the host's counter is past its id: a task the send
-          // schedules takes a later id (a Lamport-clock step; a no-op when the caller's ids
-          // come from this counter)
+          // The sending event exists from its creation on, so the host's counter is past its id
+          // (a Lamport-clock step; a no-op when the caller's ids come from this counter): before
+          // a task that runs after that creation time (it may reschedule itself; at the time itself
+          // the order of the task and the creating event is unknown), and
+          // before the send (a task the send schedules takes a later id)
+          while (due(now) || due_tie(now, born, id)) {
+            if (id != ~0ull && r.tt > born && id - r.ctr0 >= ctr_inc && id >= r.ctr0) ctr_inc = id + 1 - r.ctr0;
+            out_task(q, r, r.tt, a, ctr_inc);
+          }
+          // a send whose key equals the pending task's is no event order (two events, one id)
+          if (id != ~0ull && (r.rf & R_PENDING) && !(r.rf & R_NEVER) && r.tt == now && r.tborn == born && r.tid == id)
+            q.err |= E_ORDER;
           if (id != ~0ull && id - r.ctr0 >= ctr_inc && id >= r.ctr0) ctr_inc = id + 1 - r.ctr0;
         } else {
           while (due(now)) out_task(q, r, r.tt, a, ctr_inc);
@@ -1313,10 +1321,18 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
           }
           last_born = born;
           last_id = id;
-          while (due(now) || due_tie(now, born, id)) out_task(q, r, r.tt, a, ctr_inc);
-          // the sending event exists, so the host's counter is past its id: a task the send
-          // schedules takes a later id (a Lamport-clock step; a no-op when the caller's ids
-          // come from this counter)
+          // The sending event exists from its creation on, so the host's counter is past its id
+          // (a Lamport-clock step; a no-op when the caller's ids come from this counter): before
+          // a task that runs after that creation time (it may reschedule itself; at the time itself
+          // the order of the task and the creating event is unknown), and
+          // before the send (a task the send schedules takes a later id)
+          while (due(now) || due_tie(now, born, id)) {
+            if (id != ~0ull && r.tt > born && id - r.ctr0 >= ctr_inc && id >= r.ctr0) ctr_inc = id + 1 - r.ctr0;
+            out_task(q, r, r.tt, a, ctr_inc);
+          }
+          // a send whose key equals the pending task's is no event order (two events, one id)
+          if (id != ~0ull && (r.rf & R_PENDING) && !(r.rf & R_NEVER) && r.tt == now && r.tborn == born && r.tid == id)
+            q.err |= E_ORDER;
           if (id != ~0ull && id - r.ctr0 >= ctr_inc && id >= r.ctr0) ctr_inc = id + 1 - r.ctr0;
         } else {
           while (due(now)) out_task(q, r, r.tt, a, ctr_inc);

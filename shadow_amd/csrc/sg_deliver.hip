@@ -1178,12 +1178,9 @@ __device__ __forceinline__ void slot_orders(uint64_t* Tt, uint64_t* Tk, uint32_t
                                             uint32_t* __restrict__ ki, uint32_t* __restrict__ order,
                                             uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
   static_assert(LDS || !INBLOCK, "in-block big-slot sort needs the LDS copy");
-  // In-block (region path), slots up to INBLOCK_RANK_MAX are rank-sorted too:
-  // a slot's rank sort runs in parallel with every other slot's, where each
-  // bitonic slot takes the whole block through log2(m)^2 / 2 barriers in turn
-  // (C5: about 100 entries per destination, 1.9 ms of bitonic slots per round).
-  // In-block: slots up to INBLOCK_RANK_SMALL entries are rank-sorted, up to
-  // WAVE_SORT_MAX sorted by one wave each in registers, larger ones by the block.
+  // In-block (region path): slots up to INBLOCK_RANK_SMALL entries are rank-sorted,
+  // up to WAVE_SORT_MAX sorted by one wave each in registers (a bitonic network whose
+  // exchanges below 64 are lane shuffles), larger ones by the whole block.
   constexpr uint32_t SMALL = INBLOCK ? INBLOCK_RANK_SMALL : SMALL_BUCKET;
   constexpr uint32_t MAX_BIG = SB_CAP<KK> / (WAVE_SORT_MAX + 1) + 1;
   constexpr uint32_t MAX_WAVE = SB_CAP<KK> / (SMALL + 1) + 1;

@@ -142,6 +142,12 @@ class Workspace:
 # ---------------------------------------------------------------------------
 @dataclass
 class SourceResult:
+    """A rank's source phase of one round.  In a padded round (ShardedDelivery(padded=True),
+    every round after the first) the records are the blocks `send_padded` ([n_ranks * cap, 4],
+    rank r's block at r * cap, min(count, cap) valid records each) and `send` is None: the compact
+    array is complete only when the round overflowed into an exact exchange (last_mode
+    "padded+exact"), where `send` holds it.  Read records of a padded round from send_padded, or
+    call gpu_pad_to_compact for the compact form."""
     status: object           # uint8 device tensor
     deliver_time_ns: object  # int64 device tensor
     event_id: object         # int64 device tensor
@@ -507,7 +513,8 @@ class ShardedDelivery:
     def round(self, packets, round_end_ns: int, sim_end_ns: int, bootstrap_end_ns: int = 0):
         """One round.  The returned tensors are views of buffers the next round
         overwrites (copy what must outlive it).  In a padded round `recv` holds
-        n_ranks blocks of `cap` records and `order` indexes it."""
+        n_ranks blocks of `cap` records and `order` indexes it, and the returned
+        SourceResult's `send` is None (its records are `send_padded`; see SourceResult)."""
         if self.padded and self.cap is not None:
             return self._round_padded(packets, round_end_ns, sim_end_ns, bootstrap_end_ns)
         out = self._round_exact(packets, round_end_ns, sim_end_ns, bootstrap_end_ns)

@@ -56,36 +56,46 @@ def test_c5_table_every_16th_batch(c5, oracle):
         assert np.array_equal(gloss, oloss.view(np.uint32)), f"loss mismatch in rows [{r0}, {r1})"
 
 
-_ORACLE = {}
+PACKET_SEED = 5
 
 
-@pytest.mark.parametrize("packed", [True, False])
-def test_c5_round_on_full_table(c5, oracle, ctx, packed):
-    """10M packets from 100k hosts (node h mod 50k) delivered from the full 50k table,
-    in both table forms (packed 8-byte path keys and the two arrays)."""
+@pytest.fixture(scope="module")
+def c5_round(c5, oracle, ctx):
+    """The 10M-packet round's inputs and the oracle's result for them (one oracle run for both
+    table forms, freed at module teardown)."""
     g, used, lat, loss = c5
     hosts = synth.make_hosts(100_000, N, general_seed=1, exact_seeds=True)
     start, end = T0 + 10**9, T0 + 10**9 + 10**6
-    pk = synth.make_packets(10_000_000, hosts, start, end, seed=5, p_unknown_dst=0.001)
+    pk = synth.make_packets(10_000_000, hosts, start, end, seed=PACKET_SEED, p_unknown_dst=0.001)
+    ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
+    rng0, ctr0 = ht.get_state()
+    del ht
+    lat_h = lat.cpu().numpy().view(np.uint64).reshape(N, N)
+    loss_h = loss.cpu().numpy().reshape(N, N)
+    orng, octr = rng0.copy(), ctr0.copy()
+    want = oracle.deliver_round(end, 2**63, 0, pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"], hosts["ip"],
+                                hosts["route"], lat_h, loss_h, orng, octr, threads=THREADS)
+    del lat_h, loss_h
+    yield hosts, pk, end, (rng0, ctr0), (want, orng, octr)
+
+
+@pytest.mark.parametrize("packed", [True, False])
+def test_c5_round_on_full_table(c5, c5_round, ctx, packed):
+    """10M packets from 100k hosts (node h mod 50k) delivered from the full 50k table,
+    in both table forms (packed 8-byte path keys and the two arrays)."""
+    g, used, lat, loss = c5
+    hosts, pk, end, (rng0, ctr0), (want, rng, ctr) = c5_round
     table = DeviceTable(lat, loss, N)
     if packed:
         assert table.pack(ctx)
     ht = HostTable(hosts["ip"], hosts["route"], hosts["seed"], ctx=ctx)
-    rng, ctr = ht.get_state()
+    hr, hc = ht.get_state()
+    assert np.array_equal(hr, rng0) and np.array_equal(hc, ctr0)  # the oracle ran from this state
     out = deliver_round(ht, table, PacketBatch.from_numpy(pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"]),
                         end, 2**63, 0, ctx=ctx)
     got = out.to_numpy(len(pk["src"]))
     grng, gctr = ht.get_state()
     del out, table
-    if "round" not in _ORACLE:  # the same round for both table forms: the oracle runs once
-        lat_h = lat.cpu().numpy().view(np.uint64).reshape(N, N)
-        loss_h = loss.cpu().numpy().reshape(N, N)
-        orng, octr = rng.copy(), ctr.copy()
-        _ORACLE["round"] = (oracle.deliver_round(end, 2**63, 0, pk["src"], pk["dst_ip"], pk["payload"],
-                                                 pk["send_time"], hosts["ip"], hosts["route"], lat_h, loss_h,
-                                                 orng, octr, threads=THREADS), orng, octr)
-        del lat_h, loss_h
-    want, rng, ctr = _ORACLE["round"]
     assert want["delivered"] > 9_000_000
     for k in ("status", "deliver_time", "event_id", "dst_offsets", "dst_order"):
         assert np.array_equal(got[k], want[k]), k

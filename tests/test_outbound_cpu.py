@@ -163,3 +163,28 @@ def test_keys_must_follow_execution_order(oracle):
         run(oracle, st, sends, T0 + MS, keys=[(T0, 9), (T0, 5)])
     st = oracle.outbound_state([10], [10**9], 8)
     run(oracle, st, sends, T0 + MS, keys=[(PACKET, PACKET), (T0, 5)])  # Packet first: fine
+
+
+def test_tie_task_runs_after_a_later_numbered_event_exists(oracle):
+    """A, B, B2 at T0+1 (8 Mbit/s): X (100) forwards A, B blocks, wake-up W (101, created
+    T0+1) for T0+1ms.  Send C at T0+1ms by an event created at T0+1 with id 150: W's key
+    (T0+1, 101) is smaller, so W runs first -- after event 150 was created.  W forwards B,
+    B2 blocks and W reschedules itself: the new wake-up is numbered past 150 (151), not 102
+    (the host's counter counts every event created before the task ran, event.rs:84-155)."""
+    st = oracle.outbound_state([10], [8 * 10**6], 8)
+    sends = AB + [(0, T0 + 1, 3, 1500, 1472, 11), C_AT_WAKE]
+    out, ctr, _, status = run(oracle, st, sends, T0 + MS + 1, keys=[(T0, 5)] * 3 + [(T0 + 1, 150)], ctr0=100,
+                              n_pk=4)
+    assert list(out["packet"]) == [0, 1] and list(status) == [1, 1, 0, 0]
+    assert st["task_id"][0] == 151 and st["task_born"][0] == T0 + MS and st["task_time"][0] == T0 + 2 * MS
+    assert ctr[0] == 152  # C's notify finds the relay waiting: no new task
+
+
+def test_send_with_the_pending_tasks_key_is_rejected(oracle):
+    """Two events cannot share (created, id): a send made by the key of the pending wake-up
+    W (T0+1, 101) at W's time has no execution order and is refused (-6)."""
+    st = oracle.outbound_state([10], [8 * 10**6], 8)
+    with pytest.raises(ValueError, match="-6"):
+        run(oracle, st, AB + [C_AT_WAKE], T0 + 10 * MS, keys=[(T0, 5), (T0, 5), (T0 + 1, 101)], ctr0=100)
+    st = oracle.outbound_state([10], [8 * 10**6], 8)  # one id further on: fine
+    run(oracle, st, AB + [C_AT_WAKE], T0 + 10 * MS, keys=[(T0, 5), (T0, 5), (T0 + 1, 102)], ctr0=100)

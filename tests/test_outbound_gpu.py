@@ -301,3 +301,35 @@ def test_groups_locals_and_long_hosts(oracle, ctx):
             assert np.array_equal(got[k], ost[k]), k
         _live_same(got, ost)
     assert (st_o == 3).any() or (st_o == 2).any()
+
+
+
+def test_tie_task_after_later_event_and_equal_key(oracle, ctx):
+    """The hand cases of test_outbound_cpu.py on k_outbound<true>: a wake-up that runs at a
+    tie after a later-numbered sending event was created reschedules itself past that id
+    (the counter steps before the task, not after it); a send carrying the pending wake-up's
+    own key is refused (SG_ERR_UNSORTED), as the oracle refuses it (-6)."""
+    import torch
+
+    def go(sends, keys, window_end):
+        n = len(sends)
+        ob = OutboundPipeline(np.array([10], np.uint32), np.array([8 * 10**6], np.uint64), 8, ctx=ctx)
+        f = torch.full((n,), -1, dtype=torch.int64, device="cuda")
+        s = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        ctr = torch.full((1,), 100, dtype=torch.int64, device="cuda")
+        _, ids = ob.run(_dev([0] * n, np.uint32, np.int32), _dev([x[0] for x in sends], np.uint64, np.int64),
+                        _dev([x[1] for x in sends], np.uint32, np.int32), _dev([1500] * n, np.uint32, np.int32),
+                        _dev([1472] * n, np.uint32, np.int32), _dev([11] * n, np.uint32, np.int32),
+                        window_end, 0, T0 + 10**12, f, s, ctr.data_ptr(),
+                        event_id=_dev([k[1] for k in keys], np.uint64, np.int64),
+                        event_created_ns=_dev([k[0] for k in keys], np.uint64, np.int64))
+        return ob.get_state(), ids.cpu().numpy(), s.cpu().numpy(), int(ctr[0])
+
+    st, ids, s, ctr = go([(T0 + 1, 0), (T0 + 1, 1), (T0 + 1, 3), (T0 + MS, 2)], [(T0, 5)] * 3 + [(T0 + 1, 150)],
+                         T0 + MS + 1)
+    assert list(ids) == [0, 1] and list(s) == [1, 1, 0, 0]
+    assert st["task_id"][0] == 151 and st["task_born"][0] == T0 + MS and ctr == 152
+    with pytest.raises(ShadowGpuError) as e:  # C made by the wake-up's own key (T0+1, 101)
+        go([(T0 + 1, 0), (T0 + 1, 1), (T0 + MS, 2)], [(T0, 5), (T0, 5), (T0 + 1, 101)], T0 + 10 * MS)
+    assert e.value.code == _capi.SG_ERR_UNSORTED
+    go([(T0 + 1, 0), (T0 + 1, 1), (T0 + MS, 2)], [(T0, 5), (T0, 5), (T0 + 1, 102)], T0 + 10 * MS)
