@@ -714,7 +714,7 @@ struct BdLds {
     o_tab = o_set + ((size_t)(n + 31) / 32 * 4 + 7) / 8 * 8;
     o_cnt = o_tab + (size_t)BK_SLOTS * BD_MAXCH * 2;
     o_cst = o_cnt + (size_t)BK_SLOTS * 4;
-    o_fst = o_cst + (size_t)BK_R * 4;
+    o_fst = o_cst + (e ? (size_t)BK_R * 4 : 0);  // (none without staging: 512 B decide 3 or 4 rows per CU at C5)
     o_own = (o_fst + (size_t)nch * 2 + 15) / 16 * 16;
     o_stg = o_own + (size_t)nw * 64 * BD_K;
     bytes = o_stg + (size_t)BK_R * e * 12;
@@ -854,7 +854,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
         give_up();
         continue;
       }
-      const uint32_t k = stage && s[c] < BK_R ? pos[c] - cst[s[c]] : E;
+      const uint32_t k = E && stage && s[c] < BK_R ? pos[c] - cst[s[c]] : E;
       if (k < E) {  // staged at its arena order, stored after the band
         uint32_t* q = stg + (s[c] * E + k) * 3;
         q[0] = v[c];

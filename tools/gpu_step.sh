@@ -1,5 +1,4 @@
 set -u
-O=gpurun_out/r6m; mkdir -p $O
-timeout -k 10 300 python3 -u -m pytest tests/test_outbound_gpu.py -x -q --timeout 120 --timeout-method thread > $O/outbound.log 2>&1 || { tail -30 $O/outbound.log; exit 1; }
-tail -2 $O/outbound.log
-timeout -k 10 600 python3 -u tools/apsp_ab.py --nodes 50000 --variants "SG_APSP_BUCKET=0;SG_APSP_BUCKET=1" --reps 1 --rounds 3 > $O/ab.log 2>&1; rc=$?; grep -E "median|round" $O/ab.log; exit $rc
+O=gpurun_out/r6p; mkdir -p $O
+B="SG_APSP_BUCKET=1"
+timeout -k 10 900 python3 -u tools/apsp_ab.py --nodes 50000 --variants "$B;$B SG_BUCKET_DELTA=500000 SG_BUCKET_HASH=10;$B SG_BUCKET_DELTA=333333 SG_BUCKET_HASH=10;$B SG_BUCKET_DELTA=250000 SG_BUCKET_HASH=9;$B SG_BUCKET_DELTA=500000" --reps 1 --rounds 2 > $O/ab.log 2>&1; rc=$?; grep -E "median|round|identical" $O/ab.log; exit $rc
