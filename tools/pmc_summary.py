@@ -52,9 +52,11 @@ def short(name):
     return None
 
 
-def counter_avgs(d, counter):
+def counter_avgs(d, counter, agg=None):
     """Average per dispatch of the most-dispatched instantiation of each kernel
-    (bench's one work-counting run uses another template instance)."""
+    (bench's one work-counting run uses another template instance); agg=max: its largest
+    dispatch (a kernel launched at several sizes, e.g. k_sssp_band's one-shot build beside
+    the row blocks of bench's rank-block leg)."""
     acc = defaultdict(lambda: defaultdict(list))
     for r in _rows(d, "*counter_collection.csv"):
         if r.get("Counter_Name") != counter:
@@ -66,7 +68,7 @@ def counter_avgs(d, counter):
     out = {}
     for k, by_name in acc.items():
         vals = max(by_name.values(), key=len)
-        out[k] = sum(vals) / len(vals)
+        out[k] = agg(vals) if agg else sum(vals) / len(vals)
     return out
 
 
@@ -76,7 +78,7 @@ def stats(d):
         k = short(r.get("Name", ""))
         if k and (k not in res or int(r["Calls"]) > res[k]["calls"]):
             res[k] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "total_ns": float(r["TotalDurationNs"]),
-                      "pct": float(r.get("Percentage", 0) or 0)}
+                      "max_ns": float(r.get("MaxNs", 0) or 0), "pct": float(r.get("Percentage", 0) or 0)}
     return res
 
 
@@ -93,6 +95,9 @@ def main():
     fe = counter_avgs(a.fetch, "FETCH_SIZE") if a.fetch else {}
     wr = counter_avgs(a.write, "WRITE_SIZE") if a.write else {}
     va = counter_avgs(a.sq, "SQ_INSTS_VALU") if a.sq else {}
+    fe_mx = counter_avgs(a.fetch, "FETCH_SIZE", max) if a.fetch else {}
+    wr_mx = counter_avgs(a.write, "WRITE_SIZE", max) if a.write else {}
+    va_mx = counter_avgs(a.sq, "SQ_INSTS_VALU", max) if a.sq else {}
     for k in sorted(set(st) | set(fe) | set(wr) | set(va)):
         e = {}
         if k in st:
@@ -108,6 +113,12 @@ def main():
             e["valu_insts_per_launch"] = va[k]
             if k in st and st[k]["avg_ns"] > 0:  # wave instructions x 64 lanes / time / peak
                 e["valu_frac"] = va[k] * 64 / st[k]["avg_ns"] / VALU_PEAK_OPS_PER_NS
+        if k in fe_mx and k in wr_mx:  # the largest dispatch (its duration: the kernel's MaxNs)
+            e["largest"] = {"hbm_bytes": (2 * fe_mx[k] + wr_mx[k]) * 1024, "fetch_kb_raw": fe_mx[k],
+                            "write_kb": wr_mx[k]}
+            if k in va_mx and k in st and st[k].get("max_ns"):
+                e["largest"]["valu_frac"] = va_mx[k] * 64 / st[k]["max_ns"] / VALU_PEAK_OPS_PER_NS
+                e["largest"]["ns"] = st[k]["max_ns"]
         out[k] = e
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
