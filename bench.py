@@ -416,7 +416,8 @@ def outbound_leg(a, D, ctx, torch, pk, hosts, ht, table, round_end, sharded, pmc
 def inbound_leg(a, D, ctx, torch, buckets, n_packets, pmc, round_end):
     """The C4 round's buckets through every destination's inbound pipeline: router
     CoDel queue -> relay_inet_in token bucket (1 Gbit/s down), one window that holds
-    every arrival."""
+    every arrival.  Timed through sg_inbound_run_ordered (each arrival's fate at its
+    arrival index, a host's outputs consecutive); the by-packet-id call beside it."""
     from shadow_amd.router import InboundPipeline
 
     offs, order, dtime, lens = buckets
@@ -437,19 +438,32 @@ def inbound_leg(a, D, ctx, torch, buckets, n_packets, pmc, round_end):
     cap = max(256, _pow2(int(np.diff(offs).max(initial=0))))  # the deepest router queue
     pipes = [InboundPipeline(bw, cap, ctx=ctx) for _ in range(a.steps + a.warmup + 1)]  # a fresh state per step
     it = iter(pipes)
+    a_fwd = torch.full((max(nd, 1),), -1, dtype=torch.int64, device="cuda")
+    a_st = torch.zeros(max(nd, 1), dtype=torch.uint8, device="cuda")
 
     def step():
-        next(it).run(*args, window_end, 0, 2**63, fwd, status)
+        next(it).run_ordered(*args, window_end, 0, 2**63, fwd, status, a_fwd, a_st)
 
     t_step = timed(D, step, a.steps, a.warmup)
     ctx.enable_timers(True)
     queue_ahead(ctx, torch)
-    n_drop = next(it).run(*args, window_end, 0, 2**63, fwd, status)
+    a_st.zero_()
+    n_drop = next(it).run_ordered(*args, window_end, 0, 2**63, fwd, status, a_fwd, a_st)
     k_ms, k_n, k_bytes = ctx.read_timer("inbound")
     ctx.enable_timers(False)
     k_s = k_ms / 1e3 / max(k_n, 1)
     ach = k_bytes / max(k_n, 1) / k_s / 1e9 if k_n else 0.0
+    # the fates by packet id (one fresh window: every packet arrived in it)
+    if nd:
+        status[args[2].long()] = a_st[:nd]
     n_fwd = int((status.cpu().numpy() == 1).sum())
+    # the by-packet-id call (sg_inbound_run) on the same window, for comparison
+    pipes_id = [InboundPipeline(bw, cap, ctx=ctx) for _ in range(a.steps + a.warmup)]
+    it_id = iter(pipes_id)
+    fwd_id = torch.full((max(n_packets, 1),), -1, dtype=torch.int64, device="cuda")
+    st_id = torch.zeros(max(n_packets, 1), dtype=torch.uint8, device="cuda")
+    t_id = timed(D, lambda: next(it_id).run(*args, window_end, 0, 2**63, fwd_id, st_id), a.steps, a.warmup)
+    del pipes_id
     leg = {
         "metric": "inbound arrivals/sec (router CoDel queue -> relay token bucket, per host)", "unit": "arrivals/s",
         "value": round(D.sum(float(nd)) / t_step, 1), "higher_is_better": True, "ms_per_window": round(t_step * 1e3, 4),
@@ -464,6 +478,9 @@ def inbound_leg(a, D, ctx, torch, buckets, n_packets, pmc, round_end):
                      "valu_frac_pmc": pmc.get("inbound", {}).get("valu_frac"),
                      "rocprof": rocprof_view(pmc.get("inbound", {}), k_bytes / max(k_n, 1))},
         "forwarded": n_fwd, "dropped": n_drop,
+        "by_packet_id": {"ms_per_window": round(t_id * 1e3, 4),
+                         "same_fates": bool(torch.equal(st_id, status)),
+                         "what": "sg_inbound_run: fates written at the packet id (scattered)"},
     }
     if D.rank == 0 and D.world == 1 and not a.no_cpu:
         from oracle import oracle as O

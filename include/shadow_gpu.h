@@ -521,6 +521,21 @@ int32_t sg_inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* a
                        uint64_t bootstrap_end_ns, uint64_t sim_end_ns, uint64_t* event_ctr, uint64_t* fwd_time,
                        uint8_t* pkt_status, uint32_t n_packets, uint64_t* n_dropped);
 
+/* ABI 7: the same call with each arrival's fate written in arrival order
+ * (RelayForwarded / drop_packet of relay/mod.rs:201-273 and
+ * codel_queue.rs:125-148, at the arrival's index instead of its packet id, so
+ * a host's outputs are consecutive).  arr_status (device, arr->n): set to
+ * SG_CODEL_DEQUEUED / SG_CODEL_DROPPED when arrival i of this call leaves its
+ * queue in this call, untouched while it stays queued (the caller zeroes it:
+ * SG_CODEL_QUEUED); arr_fwd_time (device, arr->n): the forward time of a
+ * DEQUEUED arrival, untouched otherwise.  Packets that arrived in earlier calls
+ * and leave in this one still go to pkt_status / fwd_time by packet id
+ * (n_packets covers every id).  arr->n < 2^31. */
+int32_t sg_inbound_run_ordered(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* arr, uint64_t window_end_ns,
+                               uint64_t bootstrap_end_ns, uint64_t sim_end_ns, uint64_t* event_ctr,
+                               uint64_t* fwd_time, uint8_t* pkt_status, uint32_t n_packets, uint64_t* arr_fwd_time,
+                               uint8_t* arr_status, uint64_t* n_dropped);
+
 typedef struct sg_inbound_relay_state { /* host arrays, n_hosts each */
   uint8_t* flags;          /* bit 0 a forward task is pending, bit 1 it was never queued (>= sim_end),
                               bit 2 a packet is cached (RelayCached) */

@@ -72,7 +72,12 @@ constexpr int VMCNT0 = 0x0F70;
 // ring path then waits for its own load where it issues it -- where the ring and window paths
 // join, the compiler otherwise waits for every vector-memory operation in flight (vmcnt(0)), the
 // next chunk's loads included
-template <bool PF = false>
+// ORD (k_inbound<LM, true>, sg_inbound_run_ordered): an element pushed by this call carries
+// ARR_BIT | its arrival index instead of the caller's packet id, and its fate is written at that
+// index (arrival order: a host's outputs are consecutive) instead of at the packet id
+constexpr uint32_t ARR_BIT = 0x80000000u;
+
+template <bool PF = false, bool ORD = false>
 struct Q {
   uint8_t flags;
   uint64_t iend, dnext, cur, prev, bytes;
@@ -105,8 +110,17 @@ struct Q {
   uint32_t n_status;
   uint64_t dropped;
   uint32_t err;
+  uint8_t* astat;  // ORD: per arrival of this call
+  uint64_t* afwd;
 
   __device__ void drop(uint32_t pkt) {  // drop_packet -> RouterDropped
+    if constexpr (ORD) {
+      if (pkt & ARR_BIT) {
+        astat[pkt & ~ARR_BIT] = SG_CODEL_DROPPED;
+        dropped++;
+        return;
+      }
+    }
     if (pkt < n_status) status[pkt] = SG_CODEL_DROPPED;
     else err |= E_PKT;
     dropped++;
@@ -155,6 +169,7 @@ struct Q {
     hl = r.y;
     ht = ((uint64_t)r.w << 32) | r.z;
   }
+  static constexpr bool ord = ORD;
   __device__ bool should_drop(uint64_t now) const { return (flags & F_DNEXT) && now >= dnext; }
   __device__ bool dropping_recently(uint64_t now) const {
     return (flags & F_DNEXT) && since(now, dnext) < 16 * CD_INTERVAL;
@@ -777,10 +792,13 @@ struct InboundArgs {
   uint64_t* event_ctr;  // per host, or null
   uint64_t* fwd_time;   // per packet
   uint64_t *task_id, *task_born;  // per host: the pending task's event id and creation time
+  uint8_t* arr_status;  // ORD: per arrival
+  uint64_t* arr_fwd;
 };
 
 // The relay's forward task at `now` (run_forward_task -> forward_until_blocked).
-__device__ void relay_task(Q<>& q, Relay& r, uint64_t now, uint64_t bootstrap_end, uint64_t sim_end,
+template <class QT>
+__device__ void relay_task(QT& q, Relay& r, uint64_t now, uint64_t bootstrap_end, uint64_t sim_end,
                            uint64_t& ctr_inc, uint64_t* fwd_time) {
   r.rf &= (uint8_t)~R_PENDING;
   for (;;) {
@@ -803,7 +821,10 @@ __device__ void relay_task(Q<>& q, Relay& r, uint64_t now, uint64_t bootstrap_en
       r.schedule(now, now > ~0ull - wait ? ~0ull : now + wait, sim_end, ctr_inc);
       return;
     }
-    if (p < q.n_status) {  // RelayForwarded: pushed to the internet interface
+    if (QT::ord && (p & ARR_BIT)) {  // RelayForwarded, an arrival of this call: at its index
+      q.astat[p & ~ARR_BIT] = SG_CODEL_DEQUEUED;
+      q.afwd[p & ~ARR_BIT] = now;
+    } else if (p < q.n_status) {  // RelayForwarded: pushed to the internet interface
       q.status[p] = SG_CODEL_DEQUEUED;
       fwd_time[p] = now;
     } else {
@@ -812,7 +833,7 @@ __device__ void relay_task(Q<>& q, Relay& r, uint64_t now, uint64_t bootstrap_en
   }
 }
 
-template <int LM>
+template <int LM, bool ORD = false>
 __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
   constexpr bool ANY = LM != 0;
   const uint64_t d_t0 = ia.q.bdiag ? wall_clock64() : 0;
@@ -827,9 +848,10 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
   const uint32_t h = h0 + t;
   const bool walker = t < CD_HOSTS && h < a.H;
   uint32_t hb = 0, he = 0;
-  Q<> q{};
+  Q<false, ORD> q{};
   Relay r{};
   uint64_t ctr_inc = 0;
+  uint32_t tail0 = 0;  // ORD: the tail at the call's start (later elements carry arrival indices)
   if (walker) {
     hb = min(a.host_off[h], a.E);
     he = max(min(a.host_off[h + 1], a.E), hb);
@@ -845,6 +867,9 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
     q.mask = a.cap - 1;
     q.status = a.status;
     q.n_status = a.n_status;
+    q.astat = ia.arr_status;
+    q.afwd = ia.arr_fwd;
+    tail0 = q.tail;
     q.load_head();
     r.rf = ia.rflags[h];
     r.tt = ia.task_time[h];
@@ -871,7 +896,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
           c0, c1,
           [&](uint32_t i, int u) {
             rt[u] = a.time[i];
-            rp[u] = a.pkt[i];
+            rp[u] = ORD ? (ARR_BIT | i) : a.pkt[i];
             rl[u] = a.len[i];
           },
           [&](uint32_t k, int u) {
@@ -937,7 +962,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
       for (int u = 0; u < CD_UNROLL; u++) {
         const uint32_t i = cm.event(c, base + u * CD_THREADS + t, ok[u]);
         rt[u] = a.time[i];
-        rp[u] = a.pkt[i];
+        rp[u] = ORD ? (ARR_BIT | i) : a.pkt[i];
         rl[u] = a.len[i];
       }
 #pragma unroll
@@ -998,6 +1023,16 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
   unsigned long long err = 0, dropped = 0;
   if (walker) {
     while (due(ia.window_end)) relay_task(q, r, r.tt, ia.bootstrap_end, ia.sim_end, ctr_inc, ia.fwd_time);
+    if constexpr (ORD) {
+      // the elements this call pushed that are still queued (the last min(queued, pushed) of
+      // the ring), and a cached one, go back to the caller's packet ids for the next call
+      const uint32_t pushed = q.tail - tail0, queued = q.tail - q.head;
+      for (uint32_t j = q.tail - min(pushed, queued); j != q.tail; j++) {
+        uint32_t* x = (uint32_t*)&q.ring[j & q.mask];
+        *x = a.pkt[*x & ~ARR_BIT];
+      }
+      if ((r.rf & R_CACHED) && (r.cp & ARR_BIT)) r.cp = a.pkt[r.cp & ~ARR_BIT];
+    }
     a.flags[h] = q.flags;
     a.iend[h] = q.iend;
     a.dnext[h] = q.dnext;
@@ -1781,18 +1816,25 @@ void sg_inbound_destroy(sg_inbound* ib) {
 
 uint32_t sg_inbound_ring_cap(const sg_inbound* ib) { return ib ? ib->q->cap : 0; }
 
-int32_t sg_inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* arr, uint64_t window_end_ns,
-                       uint64_t bootstrap_end_ns, uint64_t sim_end_ns, uint64_t* event_ctr, uint64_t* fwd_time,
-                       uint8_t* pkt_status, uint32_t n_packets, uint64_t* n_dropped) {
+}  // extern "C"
+
+namespace sg {
+// sg_inbound_run / sg_inbound_run_ordered (arr_status set: outputs per arrival of this call)
+static int32_t inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* arr, uint64_t window_end_ns,
+                           uint64_t bootstrap_end_ns, uint64_t sim_end_ns, uint64_t* event_ctr, uint64_t* fwd_time,
+                           uint8_t* pkt_status, uint32_t n_packets, uint8_t* arr_status, uint64_t* arr_fwd,
+                           uint64_t* n_dropped) {
   return sg::guarded(ctx, [&] {
-    using namespace sg;
     if (!ib || !arr || ib->q->ctx != ctx) throw Error(SG_ERR_INVALID_ARG, "null argument");
     sg_codel* q = ib->q;
     const uint32_t E = arr->n, H = q->n;
+    const bool ord = arr_status != nullptr;
     if (n_dropped) *n_dropped = 0;
     if (E && (!arr->host || !arr->time_ns || !arr->packet || !arr->len))
       throw Error(SG_ERR_INVALID_ARG, "null arrival array");
     if (n_packets && (!pkt_status || !fwd_time)) throw Error(SG_ERR_INVALID_ARG, "null output array");
+    if (ord && E && !arr_fwd) throw Error(SG_ERR_INVALID_ARG, "null arrival output array");
+    if (ord && E >= ARR_BIT) throw Error(SG_ERR_INVALID_ARG, "too many arrivals for one ordered call");
     if (!H) return;
     hipStream_t st = ctx->stream;
     uint32_t* ws = ctx->d_seg.get<uint32_t>((size_t)H + 8);
@@ -1823,17 +1865,24 @@ int32_t sg_inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* a
     a.sim_end = sim_end_ns;
     a.event_ctr = event_ctr;
     a.fwd_time = fwd_time;
+    a.arr_status = arr_status;
+    a.arr_fwd = arr_fwd;
     {
-      // per arrival: 16 B in, a 16-B ring record written and read, 9 B out; per host: ~160 B of state
+      // per arrival: 16 B in, a 16-B ring record written and read, 9 B out (ordered: 12 B in, the
+      // packet id read only for an element still queued at the end); per host: ~160 B of state
       a.q.bdiag = lane_diag_alloc(nb);
-      TimedLaunch tl(ctx, "inbound", 57.0 * E + 160.0 * H);
+      TimedLaunch tl(ctx, "inbound", (ord ? 53.0 : 57.0) * E + 160.0 * H);
       const int lm = lane_major_launch(lane_major_env(), E, nb, CD_CHUNK);
-      if (lm == 2)
-        hipLaunchKernelGGL(k_inbound<2>, dim3(nb), dim3(CD_THREADS), 0, st, a);
-      else if (lm == 1)
-        hipLaunchKernelGGL(k_inbound<1>, dim3(nb), dim3(CD_THREADS), 0, st, a);
-      else
-        hipLaunchKernelGGL(k_inbound<0>, dim3(nb), dim3(CD_THREADS), 0, st, a);
+      auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(nb), dim3(CD_THREADS), 0, st, a); };
+      if (ord) {
+        if (lm == 2) go(k_inbound<2, true>);
+        else if (lm == 1) go(k_inbound<1, true>);
+        else go(k_inbound<0, true>);
+      } else {
+        if (lm == 2) go(k_inbound<2>);
+        else if (lm == 1) go(k_inbound<1>);
+        else go(k_inbound<0>);
+      }
     }
     lane_diag_report(st, "k_inbound", a.q.bdiag, nb);
     hipLaunchKernelGGL(k_codel_reduce, dim3(1), dim3(1024), 0, st, a.q.blk, nb, gerr, q->ret);
@@ -1848,6 +1897,26 @@ int32_t sg_inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* a
     if (err & E_WINDOW) throw Error(SG_ERR_INVALID_ARG, "an arrival is at or after window_end");
     if (n_dropped) *n_dropped = r[0];
   });
+}
+}  // namespace sg
+
+extern "C" {
+
+int32_t sg_inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* arr, uint64_t window_end_ns,
+                       uint64_t bootstrap_end_ns, uint64_t sim_end_ns, uint64_t* event_ctr, uint64_t* fwd_time,
+                       uint8_t* pkt_status, uint32_t n_packets, uint64_t* n_dropped) {
+  return sg::inbound_run(ctx, ib, arr, window_end_ns, bootstrap_end_ns, sim_end_ns, event_ctr, fwd_time, pkt_status,
+                         n_packets, nullptr, nullptr, n_dropped);
+}
+
+int32_t sg_inbound_run_ordered(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrivals* arr, uint64_t window_end_ns,
+                               uint64_t bootstrap_end_ns, uint64_t sim_end_ns, uint64_t* event_ctr,
+                               uint64_t* fwd_time, uint8_t* pkt_status, uint32_t n_packets, uint64_t* arr_fwd_time,
+                               uint8_t* arr_status, uint64_t* n_dropped) {
+  if (arr && arr->n && !arr_status) return SG_ERR_INVALID_ARG;
+  // (no arrivals: nothing is written per arrival, and the two kernels agree)
+  return sg::inbound_run(ctx, ib, arr, window_end_ns, bootstrap_end_ns, sim_end_ns, event_ctr, fwd_time, pkt_status,
+                         n_packets, arr && arr->n ? arr_status : nullptr, arr_fwd_time, n_dropped);
 }
 
 int32_t sg_inbound_get_state(sg_inbound* ib, sg_codel_state* queue, sg_inbound_relay_state* o) {

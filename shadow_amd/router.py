@@ -150,6 +150,25 @@ class InboundPipeline:
                                                      pkt_status.data_ptr(), int(pkt_status.numel()), C.byref(nd)))
         return int(nd.value)
 
+    def run_ordered(self, host, time_ns, packet, length, window_end_ns: int, bootstrap_end_ns: int,
+                    sim_end_ns: int, fwd_time, pkt_status, arr_fwd_time, arr_status,
+                    event_ctr_ptr: Optional[int] = None) -> int:
+        """run() with this call's arrivals' fates in arrival order (sg_inbound_run_ordered):
+        arr_status (uint8, zeroed by the caller) and arr_fwd_time (int64), one per arrival;
+        packets from earlier calls that leave now still go to fwd_time / pkt_status by id."""
+        n = int(host.numel())
+        if n and (arr_status.numel() < n or arr_fwd_time.numel() < n):
+            raise ValueError("arrival outputs shorter than the arrivals")
+        a = _capi.sg_inbound_arrivals(n, host.data_ptr(), time_ns.data_ptr(), packet.data_ptr(), length.data_ptr())
+        nd = C.c_uint64()
+        check(self.ctx.handle, load().sg_inbound_run_ordered(
+            self.ctx.handle, self.handle, C.byref(a), int(window_end_ns), int(bootstrap_end_ns), int(sim_end_ns),
+            C.c_void_p(event_ctr_ptr or 0), fwd_time.data_ptr() if fwd_time is not None else None,
+            pkt_status.data_ptr() if pkt_status is not None else None,
+            int(pkt_status.numel()) if pkt_status is not None else 0, arr_fwd_time.data_ptr(), arr_status.data_ptr(),
+            C.byref(nd)))
+        return int(nd.value)
+
     def get_state(self) -> dict:
         """Queue state (CoDelQueues.get_state layout) + relay state (the oracle's inbound_state keys)."""
         n = self.n

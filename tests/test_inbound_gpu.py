@@ -30,6 +30,42 @@ def _arrivals(rng, H, n, t0, t1):
     return host, t, ln
 
 
+def _live_ring_same(got, want):
+    """The queued elements (head .. tail of each host's ring) hold the same packets: an
+    ordered call stores arrival indices while it runs and must leave packet ids behind."""
+    cap = want["cap"]
+    for h in np.nonzero(want["tail"] != want["head"])[0]:
+        pos = (np.arange(int(want["head"][h]), int(want["tail"][h]), dtype=np.uint64) % cap).astype(np.int64) + h * cap
+        for k in ("ring_pkt", "ring_len", "ring_ts"):
+            assert np.array_equal(got[k][pos], want[k][pos]), (k, h)
+
+
+def _run(ib, ordered, host, t, pkt, ln, wend, boot, sim_end, fwd_g, st_g, ctr_ptr=None):
+    """One window through run() or run_ordered(); the ordered call's per-arrival fates are
+    scattered to packet ids here (into fwd_g / st_g), so both compare with the oracle alike."""
+    import torch
+
+    args = (_dev(host, np.uint32, np.int32), _dev(t, np.uint64, np.int64), _dev(pkt, np.uint32, np.int32),
+            _dev(ln, np.uint32, np.int32), wend, boot, sim_end)
+    if not ordered:
+        return ib.run(*args, fwd_g, st_g, ctr_ptr)
+    n = len(host)
+    a_st = torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")
+    a_fwd = torch.full((max(n, 1),), -1, dtype=torch.int64, device="cuda")
+    before = st_g.clone()
+    nd = ib.run_ordered(*args, fwd_g, st_g, a_fwd, a_st, ctr_ptr)
+    if n:
+        # this call's arrivals are never written by packet id
+        p = torch.from_numpy(np.asarray(pkt, np.int64)).cuda()
+        assert torch.equal(st_g[p], before[p])
+        left = a_st[:n] != 0
+        st_g[p[left]] = a_st[:n][left]
+        fw = left & (a_st[:n] == 1)
+        fwd_g[p[fw]] = a_fwd[:n][fw]
+        assert bool((a_fwd[:n][~fw] == -1).all())  # untouched unless forwarded
+    return nd
+
+
 def _same(O, got, want):
     for k in QKEYS + RKEYS:
         assert np.array_equal(got[k], want[k]), k
@@ -39,13 +75,16 @@ def _same(O, got, want):
     assert np.array_equal(got["cached_len"][m], want["cached_len"][m])
 
 
-@pytest.mark.parametrize("bw_mbit,boot_ms,layout", [(1000, 0, ""), (10, 0, ""), (1, 0, ""), (10, 40, ""),
-                                                   (1, 0, "0"), (10, 40, "0")])
-def test_windows_match_oracle(oracle, ctx, monkeypatch, bw_mbit, boot_ms, layout):
+@pytest.mark.parametrize("bw_mbit,boot_ms,layout,ordered", [
+    (1000, 0, "", False), (10, 0, "", False), (1, 0, "", False), (10, 40, "", False), (1, 0, "0", False),
+    (10, 40, "0", False), (1000, 0, "", True), (1, 0, "", True), (10, 40, "", True), (1, 0, "0", True),
+    (10, 40, "0", True)])
+def test_windows_match_oracle(oracle, ctx, monkeypatch, bw_mbit, boot_ms, layout, ordered):
     """300 hosts, 5 windows of 60 ms, 60k arrivals: from unthrottled to heavily
     throttled (standing queues, CoDel drop mode, tasks pending across windows).  ~40
     arrivals per host: lane-major chunks by default (sg_codel.hip ChunkMap); layout "0"
-    forces contiguous ones."""
+    forces contiguous ones.  ordered: sg_inbound_run_ordered (fates in arrival order;
+    packets carried from earlier windows by id), the queued rings checked too."""
     import torch
 
     if layout:
@@ -68,8 +107,7 @@ def test_windows_match_oracle(oracle, ctx, monkeypatch, bw_mbit, boot_ms, layout
         t0, t1 = T0 + w * W, T0 + (w + 1) * W
         host, t, ln = _arrivals(rng, H, per, t0, t1)
         pkt = np.arange(w * per, (w + 1) * per, dtype=np.uint32)
-        nd = ib.run(_dev(host, np.uint32, np.int32), _dev(t, np.uint64, np.int64), _dev(pkt, np.uint32, np.int32),
-                    _dev(ln, np.uint32, np.int32), t1, boot, sim_end, fwd_g, st_g, ctr_g.data_ptr())
+        nd = _run(ib, ordered, host, t, pkt, ln, t1, boot, sim_end, fwd_g, st_g, ctr_g.data_ptr())
         before = int((st_o == 2).sum())
         oracle.inbound_run(ost, host, t, pkt, ln, t1, boot, sim_end, ctr_o, fwd_o, st_o)
         assert nd == int((st_o == 2).sum()) - before
@@ -78,6 +116,8 @@ def test_windows_match_oracle(oracle, ctx, monkeypatch, bw_mbit, boot_ms, layout
         assert np.array_equal(ctr_g.cpu().numpy().view(np.uint64), ctr_o)
         got = ib.get_state()
         _same(oracle, got, ost)
+        if ordered:
+            _live_ring_same(got, ost)
         for k in ("task_id", "task_born"):
             assert np.array_equal(got[k], ost[k]), k
     if bw_mbit == 1:
@@ -119,7 +159,7 @@ def test_arrival_after_window_rejected(ctx):
     assert e.value.code == _capi.SG_ERR_INVALID_ARG
 
 
-def _run_windows(oracle, ctx, bw, cap, windows, boot, sim_end=T0 + 10**12):
+def _run_windows(oracle, ctx, bw, cap, windows, boot, sim_end=T0 + 10**12, ordered=False):
     """Consecutive windows (host, t, ln, window_end) on the GPU and the oracle,
     everything compared after each (statuses, forward times, counters, state, ids)."""
     import torch
@@ -138,20 +178,22 @@ def _run_windows(oracle, ctx, bw, cap, windows, boot, sim_end=T0 + 10**12):
     for host, t, ln, wend in windows:
         pkt = np.arange(p0, p0 + len(host), dtype=np.uint32)
         p0 += len(host)
-        ib.run(_dev(host, np.uint32, np.int32), _dev(t, np.uint64, np.int64), _dev(pkt, np.uint32, np.int32),
-               _dev(ln, np.uint32, np.int32), wend, boot, sim_end, fwd_g, st_g, ctr_g.data_ptr())
+        _run(ib, ordered, host, t, pkt, ln, wend, boot, sim_end, fwd_g, st_g, ctr_g.data_ptr())
         oracle.inbound_run(ost, host, t, pkt, ln, wend, boot, sim_end, ctr_o, fwd_o, st_o)
         assert np.array_equal(st_g.cpu().numpy(), st_o)
         assert np.array_equal(fwd_g.cpu().numpy().view(np.uint64)[st_o == 1], fwd_o[st_o == 1])
         assert np.array_equal(ctr_g.cpu().numpy().view(np.uint64), ctr_o)
         got = ib.get_state()
         _same(oracle, got, ost)
+        if ordered:
+            _live_ring_same(got, ost)
         for k in ("task_id", "task_born"):
             assert np.array_equal(got[k], ost[k]), k
     return st_o, ost
 
 
-def test_groups_chunks_and_slow_relays(oracle, ctx):
+@pytest.mark.parametrize("ordered", [False, True])
+def test_groups_chunks_and_slow_relays(oracle, ctx, ordered):
     """Same-time groups of arrivals (a task per group, one id each), long hosts
     crossing chunk boundaries with same-time runs across them, a bootstrap boundary
     inside a window, bucket refills across many intervals, and throttled hosts
@@ -177,7 +219,7 @@ def test_groups_chunks_and_slow_relays(oracle, ctx):
             t[idx] = tt
         ln = rng.choice(np.array([28, 1476, 600], np.uint32), len(host))
         windows.append((host, t, ln, t1))
-    st_o, ost = _run_windows(oracle, ctx, bw, 4096, windows, boot=T0 + 30 * MS)
+    st_o, ost = _run_windows(oracle, ctx, bw, 4096, windows, boot=T0 + 30 * MS, ordered=ordered)
     assert (st_o == 1).sum() > 0.9 * len(st_o) * 0.5
     assert (ost["rflags"] & oracle.RL_PENDING).any()  # the slow relays carry tasks over
 
