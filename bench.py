@@ -316,13 +316,18 @@ def codel_leg(a, D, ctx, torch, buckets, n_packets, pmc):
     if D.rank == 0 and D.world == 1 and not a.no_cpu:
         from oracle import oracle as O
 
-        st = O.codel_state(H, q.cap)
-        ost = np.zeros(max(n_packets, 1), np.uint8)
-        t0 = time.perf_counter()
-        O.codel_run(st, *evs, ost)
-        tc = time.perf_counter() - t0
-        leg["cpu_baseline"] = {"value": round(E / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port", **CPU_INFO,
-                               "sample": f"the same {E} events through the C restatement of codel_queue.rs, 1 thread"}
+        def run(th):
+            st = O.codel_state(H, q.cap)
+            ost = np.zeros(max(n_packets, 1), np.uint8)
+            t0 = time.perf_counter()
+            O.codel_run(st, *evs, ost, threads=th)
+            return time.perf_counter() - t0
+
+        tc, tc1 = run(CPU_THREADS), run(1)
+        leg["cpu_baseline"] = {"value": round(E / tc, 1), "unit": "ops/s", "cores": CPU_THREADS, "kind": "port",
+                               **CPU_INFO, "single_thread": {"value": round(E / tc1, 1)},
+                               "sample": f"the same {E} events through the C restatement of codel_queue.rs, hosts "
+                                         f"round-robin over {CPU_THREADS} threads (thread_per_core.rs:62-64)"}
     return leg
 
 
@@ -399,17 +404,22 @@ def outbound_leg(a, D, ctx, torch, pk, hosts, ht, table, round_end, sharded, pmc
     if D.rank == 0 and D.world == 1 and not a.no_cpu:
         from oracle import oracle as O
 
-        st = O.outbound_state(hosts["ip"], bw, pipes[0].cap)
-        ctr = np.zeros(H, np.uint64)
-        ofwd = np.full(max(n, 1), np.uint64(2**64 - 1))
-        ost = np.zeros(max(n, 1), np.uint8)
-        t0 = time.perf_counter()
-        O.outbound_run(st, pk["src"], pk["send_time"], pkt, ln, pk["payload"], pk["dst_ip"], round_end, 0, 2**63,
-                       ctr, ofwd, ost)
-        tc = time.perf_counter() - t0
-        leg["cpu_baseline"] = {"value": round(n / tc, 1), "unit": "sends/s", "cores": 1, "kind": "port", **CPU_INFO,
+        def run(th):
+            st = O.outbound_state(hosts["ip"], bw, pipes[0].cap)
+            ctr = np.zeros(H, np.uint64)
+            ofwd = np.full(max(n, 1), np.uint64(2**64 - 1))
+            ost = np.zeros(max(n, 1), np.uint8)
+            t0 = time.perf_counter()
+            O.outbound_run(st, pk["src"], pk["send_time"], pkt, ln, pk["payload"], pk["dst_ip"], round_end, 0, 2**63,
+                           ctr, ofwd, ost, threads=th)
+            return time.perf_counter() - t0
+
+        tc, tc1 = run(CPU_THREADS), run(1)
+        leg["cpu_baseline"] = {"value": round(n / tc, 1), "unit": "sends/s", "cores": CPU_THREADS, "kind": "port",
+                               **CPU_INFO, "single_thread": {"value": round(n / tc1, 1)},
                                "sample": f"the same {n} sends through the C restatement (interface fifo + "
-                                         "relay/mod.rs + token_bucket.rs), 1 thread"}
+                                         f"relay/mod.rs + token_bucket.rs), hosts round-robin over {CPU_THREADS} "
+                                         "threads (thread_per_core.rs:62-64)"}
     return leg
 
 
@@ -485,16 +495,21 @@ def inbound_leg(a, D, ctx, torch, buckets, n_packets, pmc, round_end):
     if D.rank == 0 and D.world == 1 and not a.no_cpu:
         from oracle import oracle as O
 
-        st = O.inbound_state(bw, pipes[0].cap)
-        ctr = np.zeros(H, np.uint64)
-        ofwd = np.full(max(n_packets, 1), np.uint64(2**64 - 1))
-        ost = np.zeros(max(n_packets, 1), np.uint8)
-        t0 = time.perf_counter()
-        O.inbound_run(st, host, t, order, ln, window_end, 0, 2**63, ctr, ofwd, ost)
-        tc = time.perf_counter() - t0
-        leg["cpu_baseline"] = {"value": round(nd / tc, 1), "unit": "arrivals/s", "cores": 1, "kind": "port", **CPU_INFO,
+        def run(th):
+            st = O.inbound_state(bw, cap)
+            ctr = np.zeros(H, np.uint64)
+            ofwd = np.full(max(n_packets, 1), np.uint64(2**64 - 1))
+            ost = np.zeros(max(n_packets, 1), np.uint8)
+            t0 = time.perf_counter()
+            O.inbound_run(st, host, t, order, ln, window_end, 0, 2**63, ctr, ofwd, ost, threads=th)
+            return time.perf_counter() - t0, ost
+
+        (tc, ost), (tc1, _) = run(CPU_THREADS), run(1)
+        leg["cpu_baseline"] = {"value": round(nd / tc, 1), "unit": "arrivals/s", "cores": CPU_THREADS, "kind": "port",
+                               **CPU_INFO, "single_thread": {"value": round(nd / tc1, 1)},
                                "sample": f"the same {nd} arrivals through the C restatement (codel_queue.rs + "
-                                         "relay/mod.rs + token_bucket.rs), 1 thread"}
+                                         f"relay/mod.rs + token_bucket.rs), hosts round-robin over {CPU_THREADS} "
+                                         "threads (thread_per_core.rs:62-64)"}
         leg["parity_vs_cpu"] = bool(np.array_equal(ost, status.cpu().numpy()))
     return leg
 

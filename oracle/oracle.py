@@ -72,6 +72,13 @@ def lib():
             [C.c_void_p] * 8 + [C.c_uint64] * 3 + [C.c_void_p] * 3 + [C.c_uint32] + [C.c_void_p] * 5 + \
             [C.c_uint32, C.c_void_p]
         L.sgo_outbound_run.restype = C.c_int
+        # the multi-threaded baselines: the same arguments and a thread count (outbound: + out_group)
+        L.sgo_codel_run_mt.argtypes = L.sgo_codel_run.argtypes + [C.c_uint32]
+        L.sgo_codel_run_mt.restype = C.c_int
+        L.sgo_inbound_run_mt.argtypes = L.sgo_inbound_run.argtypes + [C.c_uint32]
+        L.sgo_inbound_run_mt.restype = C.c_int
+        L.sgo_outbound_run_mt.argtypes = L.sgo_outbound_run.argtypes + [C.c_void_p, C.c_uint32]
+        L.sgo_outbound_run_mt.restype = C.c_int
         L.sgo_deliver_round_mt.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32] + [C.c_void_p] * 4 + [
             C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32] + [C.c_void_p] * 11 + [C.c_int]
         L.sgo_deliver_round_mt.restype = C.c_int64
@@ -302,20 +309,22 @@ def codel_state(n_hosts: int, cap: int) -> dict:
                 ring_len=np.zeros(n_hosts * cap, np.uint32))
 
 
-def codel_run(state: dict, host, kind, time, pkt, length, pkt_status: np.ndarray) -> np.ndarray:
+def codel_run(state: dict, host, kind, time, pkt, length, pkt_status: np.ndarray, threads: int = 1) -> np.ndarray:
     """Push/pop events (grouped by ascending host, each host's in order) through the
     per-host queues; state and pkt_status (1 dequeued, 2 dropped) updated in place.
-    Returns pop_result (the popped packet, or CD_NONE; CD_NONE for pushes)."""
+    Returns pop_result (the popped packet, or CD_NONE; CD_NONE for pushes).  threads > 1:
+    hosts dealt round-robin over that many threads (sgo_codel_run_mt), the same results."""
     host, kind = _arr(host, np.uint32), _arr(kind, np.uint8)
     time, pkt, length = _arr(time, np.uint64), _arr(pkt, np.uint32), _arr(length, np.uint32)
     n = len(host)
     res = np.zeros(max(n, 1), np.uint32)
     H = len(state["flags"])
     v = lambda a: a.ctypes.data_as(C.c_void_p)
-    rc = lib().sgo_codel_run(H, state["cap"], v(state["flags"]), v(state["interval_end"]), v(state["drop_next"]),
-                             v(state["cur"]), v(state["prev"]), v(state["bytes"]), v(state["head"]),
-                             v(state["tail"]), v(state["ring_pkt"]), v(state["ring_ts"]), v(state["ring_len"]), n,
-                             v(host), v(kind), v(time), v(pkt), v(length), v(res), v(pkt_status), len(pkt_status))
+    args = (H, state["cap"], v(state["flags"]), v(state["interval_end"]), v(state["drop_next"]), v(state["cur"]),
+            v(state["prev"]), v(state["bytes"]), v(state["head"]), v(state["tail"]), v(state["ring_pkt"]),
+            v(state["ring_ts"]), v(state["ring_len"]), n, v(host), v(kind), v(time), v(pkt), v(length), v(res),
+            v(pkt_status), len(pkt_status))
+    rc = lib().sgo_codel_run_mt(*args, int(threads)) if threads > 1 else lib().sgo_codel_run(*args)
     if rc:
         raise ValueError(f"sgo_codel_run: error {rc}")
     return res[:n]
@@ -351,16 +360,17 @@ def inbound_state(bw_down_bits: np.ndarray, cap: int, t0: int = 946684800 * 10**
 
 
 def inbound_run(st: dict, host, time, pkt, length, window_end: int, bootstrap_end: int, sim_end: int,
-                event_ctr: np.ndarray, fwd_time: np.ndarray, pkt_status: np.ndarray) -> None:
+                event_ctr: np.ndarray, fwd_time: np.ndarray, pkt_status: np.ndarray, threads: int = 1) -> None:
     host, time = _arr(host, np.uint32), _arr(time, np.uint64)
     pkt, length = _arr(pkt, np.uint32), _arr(length, np.uint32)
     v = lambda a: a.ctypes.data_as(C.c_void_p)
     H = len(st["flags"])
-    rc = lib().sgo_inbound_run(H, st["cap"], *[v(st[k]) for k in (
+    args = (H, st["cap"], *[v(st[k]) for k in (
         "flags", "interval_end", "drop_next", "cur", "prev", "bytes", "head", "tail", "ring_pkt", "ring_ts",
         "ring_len", "rflags", "task_time", "task_id", "task_born", "cached_pkt", "cached_len", "tb_cap", "tb_bal", "tb_inc", "tb_last")],
         len(host), v(host), v(time), v(pkt), v(length), window_end, bootstrap_end, sim_end, v(event_ctr),
         v(fwd_time), v(pkt_status), len(pkt_status))
+    rc = lib().sgo_inbound_run_mt(*args, int(threads)) if threads > 1 else lib().sgo_inbound_run(*args)
     if rc:
         raise ValueError(f"sgo_inbound_run: error {rc}")
 
@@ -384,10 +394,12 @@ def outbound_state(host_ipv4, bw_up_bits: np.ndarray, cap: int, t0: int = 946684
 
 def outbound_run(st: dict, host, time, pkt, length, payload, dst, window_end: int, bootstrap_end: int,
                  sim_end: int, event_ctr: np.ndarray, fwd_time: np.ndarray, pkt_status: np.ndarray,
-                 event_id=None, event_created=None) -> dict:
+                 event_id=None, event_created=None, threads: int = 1) -> dict:
     """One window of sends (sgo_outbound_run).  Returns the packets handed to send_packet, in order.
     event_id / event_created (optional, together): the sending event's id (UINT64_MAX: a Packet
-    event) and creation time, which order a send against a forward task at the same time."""
+    event) and creation time, which order a send against a forward task at the same time.
+    threads > 1 (sgo_outbound_run_mt): hosts round-robin over the threads; the packets come
+    grouped by thread (hosts ascending within one), a stable sort by src_host restores the order."""
     host, time = _arr(host, np.uint32), _arr(time, np.uint64)
     assert (event_id is None) == (event_created is None)
     eid = None if event_id is None else _arr(event_id, np.uint64)
@@ -400,11 +412,15 @@ def outbound_run(st: dict, host, time, pkt, length, payload, dst, window_end: in
                payload_len=np.zeros(cap_out, np.uint32), send_time=np.zeros(cap_out, np.uint64),
                packet=np.zeros(cap_out, np.uint32))
     n_out = C.c_uint32()
-    rc = lib().sgo_outbound_run(H, st["cap"], *[v(st[k]) for k in (
+    args = (H, st["cap"], *[v(st[k]) for k in (
         "host_ip", "head", "tail", "ring_pkt", "ring_len", "ring_dst", "ring_pay", "rflags", "task_time", "task_id",
         "task_born", "tb_cap", "tb_bal", "tb_inc", "tb_last")], len(host), v(host), v(time), v(pkt), v(length),
         v(payload), v(dst), None if eid is None else v(eid), None if eborn is None else v(eborn), window_end, bootstrap_end, sim_end, v(event_ctr), v(fwd_time), v(pkt_status), len(pkt_status),
         *[v(out[k]) for k in ("src_host", "dst_ipv4", "payload_len", "send_time", "packet")], cap_out, C.byref(n_out))
+    if threads > 1:
+        rc = lib().sgo_outbound_run_mt(*args, None, int(threads))
+    else:
+        rc = lib().sgo_outbound_run(*args)
     if rc:
         raise ValueError(f"sgo_outbound_run: error {rc}")
     return {k: a[:n_out.value] for k, a in out.items()}

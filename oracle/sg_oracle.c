@@ -768,14 +768,19 @@ static uint32_t cd_pop(cd_q* q, uint64_t now) {
   return has ? pkt : UINT32_MAX;
 }
 
-int sgo_codel_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* iend, uint64_t* dnext,
-                  uint64_t* cur, uint64_t* prev, uint64_t* bytes, uint32_t* head, uint32_t* tail,
-                  uint32_t* ring_pkt, uint64_t* ring_ts, uint32_t* ring_len, uint32_t n_events,
-                  const uint32_t* host, const uint8_t* kind, const uint64_t* time, const uint32_t* pkt,
-                  const uint32_t* len, uint32_t* pop_result, uint8_t* pkt_status, uint32_t n_status) {
+/* Hosts h = phase, phase + stride, ...; off (n_hosts + 1, or NULL: one pass over every host in
+ * order) gives each host's first event -- the multi-threaded CPU baselines (sgo_*_run_mt) run one
+ * thread per phase, hosts round-robin over the threads as thread_per_core.rs:62-64 deals them. */
+static int codel_impl(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* iend, uint64_t* dnext,
+                      uint64_t* cur, uint64_t* prev, uint64_t* bytes, uint32_t* head, uint32_t* tail,
+                      uint32_t* ring_pkt, uint64_t* ring_ts, uint32_t* ring_len, uint32_t n_events,
+                      const uint32_t* host, const uint8_t* kind, const uint64_t* time, const uint32_t* pkt,
+                      const uint32_t* len, uint32_t* pop_result, uint8_t* pkt_status, uint32_t n_status,
+                      const uint32_t* off, uint32_t stride, uint32_t phase) {
   if (!cap) return -1;
   uint32_t e = 0;
-  for (uint32_t h = 0; h < n_hosts; h++) {
+  for (uint32_t h = phase; h < n_hosts; h += stride) {
+    if (off) e = off[h];
     cd_q q = {flags[h], iend[h], dnext[h], cur[h], prev[h], bytes[h], head[h], tail[h],
               ring_pkt + (size_t)h * cap, ring_ts + (size_t)h * cap, ring_len + (size_t)h * cap, cap,
               pkt_status, n_status, 0};
@@ -808,7 +813,16 @@ int sgo_codel_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* iend
     head[h] = q.head;
     tail[h] = q.tail;
   }
-  return e == n_events ? 0 : -4;  /* -4: events not grouped by ascending host (or host >= n_hosts) */
+  return off || e == n_events ? 0 : -4;  /* -4: events not grouped by ascending host (or host >= n_hosts) */
+}
+
+int sgo_codel_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* iend, uint64_t* dnext,
+                  uint64_t* cur, uint64_t* prev, uint64_t* bytes, uint32_t* head, uint32_t* tail,
+                  uint32_t* ring_pkt, uint64_t* ring_ts, uint32_t* ring_len, uint32_t n_events,
+                  const uint32_t* host, const uint8_t* kind, const uint64_t* time, const uint32_t* pkt,
+                  const uint32_t* len, uint32_t* pop_result, uint8_t* pkt_status, uint32_t n_status) {
+  return codel_impl(n_hosts, cap, flags, iend, dnext, cur, prev, bytes, head, tail, ring_pkt, ring_ts, ring_len,
+                    n_events, host, kind, time, pkt, len, pop_result, pkt_status, n_status, NULL, 1, 0);
 }
 
 /* ------------------------------------------------------------------------- */
@@ -870,17 +884,19 @@ static int tb_remove(tb_t* b, uint64_t dec, uint64_t now, uint64_t* wait) {
   return 0;
 }
 
-int sgo_inbound_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* iend, uint64_t* dnext,
-                    uint64_t* cur, uint64_t* prev, uint64_t* bytes, uint32_t* head, uint32_t* tail,
-                    uint32_t* ring_pkt, uint64_t* ring_ts, uint32_t* ring_len, uint8_t* rflags, uint64_t* task_time,
-                    uint64_t* task_id, uint64_t* task_born, uint32_t* cached_pkt, uint32_t* cached_len, uint64_t* tb_cap, uint64_t* tb_bal,
-                    uint64_t* tb_inc, uint64_t* tb_last, uint32_t n_arr, const uint32_t* host,
-                    const uint64_t* time, const uint32_t* pkt, const uint32_t* len, uint64_t window_end,
-                    uint64_t bootstrap_end, uint64_t sim_end, uint64_t* event_ctr, uint64_t* fwd_time,
-                    uint8_t* pkt_status, uint32_t n_status) {
+static int inbound_impl(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* iend, uint64_t* dnext,
+                        uint64_t* cur, uint64_t* prev, uint64_t* bytes, uint32_t* head, uint32_t* tail,
+                        uint32_t* ring_pkt, uint64_t* ring_ts, uint32_t* ring_len, uint8_t* rflags,
+                        uint64_t* task_time, uint64_t* task_id, uint64_t* task_born, uint32_t* cached_pkt,
+                        uint32_t* cached_len, uint64_t* tb_cap, uint64_t* tb_bal, uint64_t* tb_inc, uint64_t* tb_last,
+                        uint32_t n_arr, const uint32_t* host, const uint64_t* time, const uint32_t* pkt,
+                        const uint32_t* len, uint64_t window_end, uint64_t bootstrap_end, uint64_t sim_end,
+                        uint64_t* event_ctr, uint64_t* fwd_time, uint8_t* pkt_status, uint32_t n_status,
+                        const uint32_t* off, uint32_t stride, uint32_t phase) {
   if (!cap) return -1;
   uint32_t e = 0;
-  for (uint32_t h = 0; h < n_hosts; h++) {
+  for (uint32_t h = phase; h < n_hosts; h += stride) {
+    if (off) e = off[h];
     cd_q q = {flags[h], iend[h], dnext[h], cur[h], prev[h], bytes[h], head[h], tail[h],
               ring_pkt + (size_t)h * cap, ring_ts + (size_t)h * cap, ring_len + (size_t)h * cap, cap,
               pkt_status, n_status, 0};
@@ -970,7 +986,21 @@ int sgo_inbound_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* ie
     tb_bal[h] = tb.bal;
     tb_last[h] = tb.last;
   }
-  return e == n_arr ? 0 : -4;
+  return off || e == n_arr ? 0 : -4;
+}
+
+int sgo_inbound_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* iend, uint64_t* dnext,
+                    uint64_t* cur, uint64_t* prev, uint64_t* bytes, uint32_t* head, uint32_t* tail,
+                    uint32_t* ring_pkt, uint64_t* ring_ts, uint32_t* ring_len, uint8_t* rflags, uint64_t* task_time,
+                    uint64_t* task_id, uint64_t* task_born, uint32_t* cached_pkt, uint32_t* cached_len, uint64_t* tb_cap, uint64_t* tb_bal,
+                    uint64_t* tb_inc, uint64_t* tb_last, uint32_t n_arr, const uint32_t* host,
+                    const uint64_t* time, const uint32_t* pkt, const uint32_t* len, uint64_t window_end,
+                    uint64_t bootstrap_end, uint64_t sim_end, uint64_t* event_ctr, uint64_t* fwd_time,
+                    uint8_t* pkt_status, uint32_t n_status) {
+  return inbound_impl(n_hosts, cap, flags, iend, dnext, cur, prev, bytes, head, tail, ring_pkt, ring_ts, ring_len,
+                      rflags, task_time, task_id, task_born, cached_pkt, cached_len, tb_cap, tb_bal, tb_inc, tb_last,
+                      n_arr, host, time, pkt, len, window_end, bootstrap_end, sim_end, event_ctr, fwd_time,
+                      pkt_status, n_status, NULL, 1, 0);
 }
 
 /* Outbound pipeline: NetworkInterface (fifo qdisc) -> relay_inet_out -> Router
@@ -994,20 +1024,24 @@ int sgo_inbound_run(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* ie
  * Returns 0, or -2 ring full, -3 packet id >= n_status, -4 not grouped,
  * -5 a send at or after window_end, -6 a host's send times decrease,
  * -7 more than out_cap sent. */
-int sgo_outbound_run(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip, uint32_t* head, uint32_t* tail,
-                     uint32_t* ring_pkt, uint32_t* ring_len, uint32_t* ring_dst, uint32_t* ring_pay,
-                     uint8_t* rflags, uint64_t* task_time, uint64_t* task_id, uint64_t* task_born, uint64_t* tb_cap,
-                     uint64_t* tb_bal, uint64_t* tb_inc, uint64_t* tb_last, uint32_t n_sends, const uint32_t* host,
-                     const uint64_t* time, const uint32_t* pkt, const uint32_t* len, const uint32_t* pay,
-                     const uint32_t* dst, const uint64_t* ev_id, const uint64_t* ev_born, uint64_t window_end, uint64_t bootstrap_end, uint64_t sim_end, uint64_t* event_ctr,
-                     uint64_t* fwd_time, uint8_t* pkt_status, uint32_t n_status, uint32_t* out_host,
-                     uint32_t* out_dst, uint32_t* out_pay, uint64_t* out_time, uint32_t* out_pkt, uint32_t out_cap,
-                     uint32_t* n_out) {
+/* out_* [out_begin, out_end): this pass's output slots; *n_out: the slots it used (from out_begin) */
+static int outbound_impl(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip, uint32_t* head, uint32_t* tail,
+                         uint32_t* ring_pkt, uint32_t* ring_len, uint32_t* ring_dst, uint32_t* ring_pay,
+                         uint8_t* rflags, uint64_t* task_time, uint64_t* task_id, uint64_t* task_born, uint64_t* tb_cap,
+                         uint64_t* tb_bal, uint64_t* tb_inc, uint64_t* tb_last, uint32_t n_sends, const uint32_t* host,
+                         const uint64_t* time, const uint32_t* pkt, const uint32_t* len, const uint32_t* pay,
+                         const uint32_t* dst, const uint64_t* ev_id, const uint64_t* ev_born, uint64_t window_end,
+                         uint64_t bootstrap_end, uint64_t sim_end, uint64_t* event_ctr, uint64_t* fwd_time,
+                         uint8_t* pkt_status, uint32_t n_status, uint32_t* out_host, uint32_t* out_dst,
+                         uint32_t* out_pay, uint64_t* out_time, uint32_t* out_pkt, uint32_t out_begin,
+                         uint32_t out_end, uint32_t* n_out, const uint32_t* off, uint32_t stride, uint32_t phase) {
   if (!cap) return -1;
   if ((ev_id == NULL) != (ev_born == NULL)) return -1;
-  uint32_t e = 0, no = 0;
+  uint32_t e = 0, no = out_begin;
+  const uint32_t out_cap = out_end;
   *n_out = 0;
-  for (uint32_t h = 0; h < n_hosts; h++) {
+  for (uint32_t h = phase; h < n_hosts; h += stride) {
+    if (off) e = off[h];
     const size_t base = (size_t)h * cap;
     tb_t tb = {tb_cap[h], tb_bal[h], tb_inc[h], tb_last[h], TB_INTERVAL};
     uint8_t rf = rflags[h];
@@ -1114,8 +1148,23 @@ int sgo_outbound_run(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip, ui
     tb_bal[h] = tb.bal;
     tb_last[h] = tb.last;
   }
-  *n_out = no;
-  return e == n_sends ? 0 : -4;
+  *n_out = no - out_begin;
+  return off || e == n_sends ? 0 : -4;
+}
+
+int sgo_outbound_run(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip, uint32_t* head, uint32_t* tail,
+                     uint32_t* ring_pkt, uint32_t* ring_len, uint32_t* ring_dst, uint32_t* ring_pay,
+                     uint8_t* rflags, uint64_t* task_time, uint64_t* task_id, uint64_t* task_born, uint64_t* tb_cap,
+                     uint64_t* tb_bal, uint64_t* tb_inc, uint64_t* tb_last, uint32_t n_sends, const uint32_t* host,
+                     const uint64_t* time, const uint32_t* pkt, const uint32_t* len, const uint32_t* pay,
+                     const uint32_t* dst, const uint64_t* ev_id, const uint64_t* ev_born, uint64_t window_end, uint64_t bootstrap_end, uint64_t sim_end, uint64_t* event_ctr,
+                     uint64_t* fwd_time, uint8_t* pkt_status, uint32_t n_status, uint32_t* out_host,
+                     uint32_t* out_dst, uint32_t* out_pay, uint64_t* out_time, uint32_t* out_pkt, uint32_t out_cap,
+                     uint32_t* n_out) {
+  return outbound_impl(n_hosts, cap, host_ip, head, tail, ring_pkt, ring_len, ring_dst, ring_pay, rflags, task_time,
+                       task_id, task_born, tb_cap, tb_bal, tb_inc, tb_last, n_sends, host, time, pkt, len, pay, dst,
+                       ev_id, ev_born, window_end, bootstrap_end, sim_end, event_ctr, fwd_time, pkt_status, n_status,
+                       out_host, out_dst, out_pay, out_time, out_pkt, 0, out_cap, n_out, NULL, 1, 0);
 }
 
 /* Test hook: TokenBucket::conforming_remove_inner on an explicit state
@@ -1328,4 +1377,234 @@ int64_t sgo_deliver_round_mt(uint64_t round_end, uint64_t sim_end, uint64_t boot
   *min_deliver = md;
   *min_lat = ml;
   return delivered;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Multi-threaded lane baselines: the same per-host code, hosts dealt round-  */
+/* robin over n_threads threads (Shadow's worker pool, thread_per_core.rs:62-64) */
+/* ------------------------------------------------------------------------- */
+/* off[h] = first event of host h (n_hosts + 1 entries); -4 if the events are not grouped */
+static int host_offsets(const uint32_t* host, uint32_t n, uint32_t n_hosts, uint32_t* off) {
+  uint32_t h = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (host[i] >= n_hosts || host[i] < (i ? host[i - 1] : 0)) return -4;
+    while (h <= host[i]) off[h++] = i;
+  }
+  while (h <= n_hosts) off[h++] = n;
+  return 0;
+}
+
+typedef struct {
+  int kind; /* 0 codel, 1 inbound, 2 outbound */
+  const void* a; /* the call's argument block */
+  const uint32_t* off;
+  uint32_t stride, phase;
+  uint32_t out_begin, out_end, n_out;
+  int rc;
+} lane_job;
+
+typedef struct {
+  uint32_t n_hosts, cap;
+  uint8_t* flags;
+  uint64_t *iend, *dnext, *cur, *prev, *bytes;
+  uint32_t *head, *tail, *ring_pkt;
+  uint64_t* ring_ts;
+  uint32_t* ring_len;
+  uint32_t n_events;
+  const uint32_t* host;
+  const uint8_t* kind;
+  const uint64_t* time;
+  const uint32_t *pkt, *len;
+  uint32_t* pop_result;
+  uint8_t* pkt_status;
+  uint32_t n_status;
+} codel_call;
+
+typedef struct {
+  uint32_t n_hosts, cap;
+  uint8_t* flags;
+  uint64_t *iend, *dnext, *cur, *prev, *bytes;
+  uint32_t *head, *tail, *ring_pkt;
+  uint64_t* ring_ts;
+  uint32_t* ring_len;
+  uint8_t* rflags;
+  uint64_t *task_time, *task_id, *task_born;
+  uint32_t *cached_pkt, *cached_len;
+  uint64_t *tb_cap, *tb_bal, *tb_inc, *tb_last;
+  uint32_t n_arr;
+  const uint32_t* host;
+  const uint64_t* time;
+  const uint32_t *pkt, *len;
+  uint64_t window_end, bootstrap_end, sim_end;
+  uint64_t *event_ctr, *fwd_time;
+  uint8_t* pkt_status;
+  uint32_t n_status;
+} inbound_call;
+
+static void* lane_worker(void* arg) {
+  lane_job* j = (lane_job*)arg;
+  if (j->kind == 0) {
+    const codel_call* c = (const codel_call*)j->a;
+    j->rc = codel_impl(c->n_hosts, c->cap, c->flags, c->iend, c->dnext, c->cur, c->prev, c->bytes, c->head, c->tail,
+                       c->ring_pkt, c->ring_ts, c->ring_len, c->n_events, c->host, c->kind, c->time, c->pkt, c->len,
+                       c->pop_result, c->pkt_status, c->n_status, j->off, j->stride, j->phase);
+  } else if (j->kind == 1) {
+    const inbound_call* c = (const inbound_call*)j->a;
+    j->rc = inbound_impl(c->n_hosts, c->cap, c->flags, c->iend, c->dnext, c->cur, c->prev, c->bytes, c->head, c->tail,
+                         c->ring_pkt, c->ring_ts, c->ring_len, c->rflags, c->task_time, c->task_id, c->task_born,
+                         c->cached_pkt, c->cached_len, c->tb_cap, c->tb_bal, c->tb_inc, c->tb_last, c->n_arr, c->host,
+                         c->time, c->pkt, c->len, c->window_end, c->bootstrap_end, c->sim_end, c->event_ctr,
+                         c->fwd_time, c->pkt_status, c->n_status, j->off, j->stride, j->phase);
+  }
+  return NULL;
+}
+
+static int run_lane_jobs(lane_job* jobs, uint32_t n_threads) {
+  pthread_t* th = (pthread_t*)malloc((size_t)n_threads * sizeof(pthread_t));
+  if (!th) return -1;
+  for (uint32_t t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, lane_worker, &jobs[t]);
+  for (uint32_t t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  free(th);
+  int rc = 0;
+  for (uint32_t t = 0; t < n_threads && !rc; t++) rc = jobs[t].rc;
+  return rc;
+}
+
+int sgo_codel_run_mt(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* iend, uint64_t* dnext,
+                     uint64_t* cur, uint64_t* prev, uint64_t* bytes, uint32_t* head, uint32_t* tail,
+                     uint32_t* ring_pkt, uint64_t* ring_ts, uint32_t* ring_len, uint32_t n_events,
+                     const uint32_t* host, const uint8_t* kind, const uint64_t* time, const uint32_t* pkt,
+                     const uint32_t* len, uint32_t* pop_result, uint8_t* pkt_status, uint32_t n_status,
+                     uint32_t n_threads) {
+  if (!n_threads) return -1;
+  uint32_t* off = (uint32_t*)malloc(((size_t)n_hosts + 1) * 4);
+  lane_job* jobs = (lane_job*)calloc(n_threads, sizeof(lane_job));
+  if (!off || !jobs) return -1;
+  int rc = host_offsets(host, n_events, n_hosts, off);
+  if (!rc) {
+    codel_call c = {n_hosts, cap, flags, iend, dnext, cur, prev, bytes, head, tail, ring_pkt, ring_ts, ring_len,
+                    n_events, host, kind, time, pkt, len, pop_result, pkt_status, n_status};
+    for (uint32_t t = 0; t < n_threads; t++) jobs[t] = (lane_job){0, &c, off, n_threads, t, 0, 0, 0, 0};
+    rc = run_lane_jobs(jobs, n_threads);
+  }
+  free(off);
+  free(jobs);
+  return rc;
+}
+
+int sgo_inbound_run_mt(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* iend, uint64_t* dnext,
+                       uint64_t* cur, uint64_t* prev, uint64_t* bytes, uint32_t* head, uint32_t* tail,
+                       uint32_t* ring_pkt, uint64_t* ring_ts, uint32_t* ring_len, uint8_t* rflags,
+                       uint64_t* task_time, uint64_t* task_id, uint64_t* task_born, uint32_t* cached_pkt,
+                       uint32_t* cached_len, uint64_t* tb_cap, uint64_t* tb_bal, uint64_t* tb_inc, uint64_t* tb_last,
+                       uint32_t n_arr, const uint32_t* host, const uint64_t* time, const uint32_t* pkt,
+                       const uint32_t* len, uint64_t window_end, uint64_t bootstrap_end, uint64_t sim_end,
+                       uint64_t* event_ctr, uint64_t* fwd_time, uint8_t* pkt_status, uint32_t n_status,
+                       uint32_t n_threads) {
+  if (!n_threads) return -1;
+  uint32_t* off = (uint32_t*)malloc(((size_t)n_hosts + 1) * 4);
+  lane_job* jobs = (lane_job*)calloc(n_threads, sizeof(lane_job));
+  if (!off || !jobs) return -1;
+  int rc = host_offsets(host, n_arr, n_hosts, off);
+  if (!rc) {
+    inbound_call c = {n_hosts, cap, flags, iend, dnext, cur, prev, bytes, head, tail, ring_pkt, ring_ts, ring_len,
+                      rflags, task_time, task_id, task_born, cached_pkt, cached_len, tb_cap, tb_bal, tb_inc, tb_last,
+                      n_arr, host, time, pkt, len, window_end, bootstrap_end, sim_end, event_ctr, fwd_time,
+                      pkt_status, n_status};
+    for (uint32_t t = 0; t < n_threads; t++) jobs[t] = (lane_job){1, &c, off, n_threads, t, 0, 0, 0, 0};
+    rc = run_lane_jobs(jobs, n_threads);
+  }
+  free(off);
+  free(jobs);
+  return rc;
+}
+
+/* Outbound: thread t writes its sent packets to out_* [begin_t, end_t), sized by its hosts'
+ * sends plus their queued packets; *n_out = the total, out_* grouped by thread (hosts ascending
+ * within a thread), each group's first slot in out_group (n_threads + 1, may be NULL). */
+typedef struct {
+  uint32_t n_hosts, cap;
+  const uint32_t* host_ip;
+  uint32_t *head, *tail, *ring_pkt, *ring_len, *ring_dst, *ring_pay;
+  uint8_t* rflags;
+  uint64_t *task_time, *task_id, *task_born, *tb_cap, *tb_bal, *tb_inc, *tb_last;
+  uint32_t n_sends;
+  const uint32_t* host;
+  const uint64_t* time;
+  const uint32_t *pkt, *len, *pay, *dst;
+  const uint64_t *ev_id, *ev_born;
+  uint64_t window_end, bootstrap_end, sim_end;
+  uint64_t *event_ctr, *fwd_time;
+  uint8_t* pkt_status;
+  uint32_t n_status;
+  uint32_t *out_host, *out_dst, *out_pay;
+  uint64_t* out_time;
+  uint32_t* out_pkt;
+} outbound_call;
+
+static void* outbound_worker(void* arg) {
+  lane_job* j = (lane_job*)arg;
+  const outbound_call* c = (const outbound_call*)j->a;
+  j->rc = outbound_impl(c->n_hosts, c->cap, c->host_ip, c->head, c->tail, c->ring_pkt, c->ring_len, c->ring_dst,
+                        c->ring_pay, c->rflags, c->task_time, c->task_id, c->task_born, c->tb_cap, c->tb_bal,
+                        c->tb_inc, c->tb_last, c->n_sends, c->host, c->time, c->pkt, c->len, c->pay, c->dst, c->ev_id,
+                        c->ev_born, c->window_end, c->bootstrap_end, c->sim_end, c->event_ctr, c->fwd_time,
+                        c->pkt_status, c->n_status, c->out_host, c->out_dst, c->out_pay, c->out_time, c->out_pkt,
+                        j->out_begin, j->out_end, &j->n_out, j->off, j->stride, j->phase);
+  return NULL;
+}
+
+int sgo_outbound_run_mt(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip, uint32_t* head, uint32_t* tail,
+                        uint32_t* ring_pkt, uint32_t* ring_len, uint32_t* ring_dst, uint32_t* ring_pay,
+                        uint8_t* rflags, uint64_t* task_time, uint64_t* task_id, uint64_t* task_born, uint64_t* tb_cap,
+                        uint64_t* tb_bal, uint64_t* tb_inc, uint64_t* tb_last, uint32_t n_sends, const uint32_t* host,
+                        const uint64_t* time, const uint32_t* pkt, const uint32_t* len, const uint32_t* pay,
+                        const uint32_t* dst, const uint64_t* ev_id, const uint64_t* ev_born, uint64_t window_end,
+                        uint64_t bootstrap_end, uint64_t sim_end, uint64_t* event_ctr, uint64_t* fwd_time,
+                        uint8_t* pkt_status, uint32_t n_status, uint32_t* out_host, uint32_t* out_dst,
+                        uint32_t* out_pay, uint64_t* out_time, uint32_t* out_pkt, uint32_t out_cap, uint32_t* n_out,
+                        uint32_t* out_group, uint32_t n_threads) {
+  if (!n_threads) return -1;
+  uint32_t* off = (uint32_t*)malloc(((size_t)n_hosts + 1) * 4);
+  lane_job* jobs = (lane_job*)calloc(n_threads, sizeof(lane_job));
+  pthread_t* th = (pthread_t*)malloc((size_t)n_threads * sizeof(pthread_t));
+  if (!off || !jobs || !th) return -1;
+  *n_out = 0;
+  int rc = host_offsets(host, n_sends, n_hosts, off);
+  if (!rc) {
+    outbound_call c = {n_hosts, cap, host_ip, head, tail, ring_pkt, ring_len, ring_dst, ring_pay, rflags, task_time,
+                       task_id, task_born, tb_cap, tb_bal, tb_inc, tb_last, n_sends, host, time, pkt, len, pay, dst,
+                       ev_id, ev_born, window_end, bootstrap_end, sim_end, event_ctr, fwd_time, pkt_status, n_status,
+                       out_host, out_dst, out_pay, out_time, out_pkt};
+    uint64_t at = 0;
+    for (uint32_t t = 0; t < n_threads; t++) {
+      uint64_t need = 0;  /* a host sends at most its queued packets and this call's sends */
+      for (uint32_t h = t; h < n_hosts; h += n_threads) need += (uint64_t)(off[h + 1] - off[h]) + (tail[h] - head[h]) + 1;
+      jobs[t] = (lane_job){2, &c, off, n_threads, t, (uint32_t)at, (uint32_t)(at + need < out_cap ? at + need : out_cap), 0, 0};
+      at += need;
+    }
+    for (uint32_t t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, outbound_worker, &jobs[t]);
+    for (uint32_t t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+    for (uint32_t t = 0; t < n_threads && !rc; t++) rc = jobs[t].rc;
+    /* compact the groups to the front */
+    uint32_t w = 0;
+    for (uint32_t t = 0; t < n_threads; t++) {
+      if (out_group) out_group[t] = w;
+      const uint32_t b = jobs[t].out_begin, k = jobs[t].n_out;
+      if (b != w && k) {
+        memmove(out_host + w, out_host + b, (size_t)k * 4);
+        memmove(out_dst + w, out_dst + b, (size_t)k * 4);
+        memmove(out_pay + w, out_pay + b, (size_t)k * 4);
+        memmove(out_time + w, out_time + b, (size_t)k * 8);
+        memmove(out_pkt + w, out_pkt + b, (size_t)k * 4);
+      }
+      w += k;
+    }
+    if (out_group) out_group[n_threads] = w;
+    *n_out = w;
+  }
+  free(off);
+  free(jobs);
+  free(th);
+  return rc;
 }
