@@ -106,10 +106,12 @@ constexpr uint64_t FKEY_INF = ((uint64_t)LAT32_SAT << 32) | ((uint64_t)0x3F80000
 __device__ __forceinline__ uint32_t fkey_lat(uint64_t k) { return (uint32_t)(k >> 32); }
 __device__ __forceinline__ uint32_t fkey_loss_bits(uint64_t k) { return ((uint32_t)k >> 1) & 0x7FFFFFFFu; }
 // key(u) (+) edge (graph/mod.rs:322-331), flagged dirty
+// (the loss is in [0, 1], never -0.0: its bits are below 2^31, so the low word is one 32-bit
+// shift-or and the high word is the latency itself -- no 64-bit shift, no carry)
 __device__ __forceinline__ uint64_t frelax(uint64_t ku, uint32_t edge_lat, float edge_om) {
   const uint32_t lat = __builtin_elementwise_add_sat(fkey_lat(ku), edge_lat);
   const float loss = fold_loss(__uint_as_float(fkey_loss_bits(ku)), edge_om);
-  return ((uint64_t)lat << 32) | ((uint64_t)__float_as_uint(loss) << 1) | 1ull;
+  return ((uint64_t)lat << 32) | (uint32_t)((__float_as_uint(loss) << 1) | 1u);
 }
 
 // Queue capacity: n + 1024 rounded up to 64.  At most n nodes are queued (one
@@ -127,24 +129,21 @@ struct RingMod {
 constexpr uint16_t RING_EMPTY = 0xFFFF;
 
 // Queue the flagged lanes' nodes (NK candidates per lane): one tail add per call.
+// mq[c]: the wave's ballot of candidate c (wave-uniform masks, no per-lane bool kept)
 template <int NK>
-__device__ __forceinline__ void append_q(const bool* app, const uint32_t* v, uint16_t* ring, uint32_t* tail,
+__device__ __forceinline__ void append_q(const uint64_t* mq, const uint32_t* v, uint16_t* ring, uint32_t* tail,
                                          const RingMod& slot_of, int lane) {
   const uint64_t lt = (1ull << lane) - 1;
-  uint64_t mq[NK];  // (NK <= 16)
   uint32_t tot = 0;
 #pragma unroll
-  for (int c = 0; c < NK; c++) {
-    mq[c] = __ballot(app[c]);
-    tot += (uint32_t)__popcll(mq[c]);
-  }
+  for (int c = 0; c < NK; c++) tot += (uint32_t)__popcll(mq[c]);
   if (!tot) return;
   uint32_t b = 0;
   if (lane == 0) b = atomicAdd(tail, tot);
   b = __builtin_amdgcn_readfirstlane(b);
 #pragma unroll
   for (int c = 0; c < NK; c++) {
-    if (app[c]) ring[slot_of(b + (uint32_t)__popcll(mq[c] & lt))] = (uint16_t)v[c];
+    if ((mq[c] >> lane) & 1ull) ring[slot_of(b + (uint32_t)__popcll(mq[c] & lt))] = (uint16_t)v[c];
     b += (uint32_t)__popcll(mq[c]);
   }
 }
@@ -393,18 +392,22 @@ __global__ void __launch_bounds__(NT)
       }
     };
     auto ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-    // relax NK candidates into key[v[c]]; app[c]: v[c] became dirty below split (to
+    // relax NK candidates into key[v[c]]; app[c]: the ballot of the lanes whose v[c] became dirty below split (to
     // be queued).  Branch-free, so the NK LDS atomics issue back to back and share
     // one wait: a lane with no candidate (or a saturated one, never propagated)
     // offers ~0 to its own sink word, a no-op.  (With one branch per candidate the
     // compiler waited for each atomic's return before issuing the next.)
-    auto offer_all = [&](auto nk, const bool* valid, const uint32_t* v, const uint64_t* cand, bool* app) {
+    auto offer_all = [&](auto nk, const bool* valid, const uint32_t* v, const uint64_t* cand, uint64_t* app) {
       constexpr int NK = decltype(nk)::value;
       uint64_t cd[NK], old[NK];
+      bool okk[NK];
 #pragma unroll
       for (int c = 0; c < NK; c++) {
         const bool ok = valid[c] && fkey_lat(cand[c]) != LAT32_SAT;
-        cd[c] = ok ? cand[c] : ~0ull;
+        okk[c] = ok;
+        // (no select of the offered value: a lane without a candidate offers whatever it holds
+        // to its own sink word, whose value nothing reads)
+        cd[c] = cand[c];
         old[c] = __hip_atomic_fetch_min(ok ? &key[v[c]] : &sink[lane], (unsigned long long)cd[c], __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -412,7 +415,11 @@ __global__ void __launch_bounds__(NT)
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int c = 0; c < NK; c++)
-        app[c] = (old[c] >> 1) > (cd[c] >> 1) && !(old[c] & 1ull) && fkey_lat(cd[c]) < split;
+        // improved and was clean: a clean old key (flag 0) is above the candidate (flag 1) iff its
+        // (latency, loss) is larger -- one 64-bit compare, no shifts
+        // (the i1 ballot: the condition's lane mask as is, not a 0/1 VGPR compared back to a mask)
+        app[c] = __builtin_amdgcn_ballot_w64(okk[c] && !((uint32_t)old[c] & 1u) && old[c] > cd[c] &&
+                                             fkey_lat(cd[c]) < split);
     };
     __syncthreads();
 
@@ -479,7 +486,8 @@ __global__ void __launch_bounds__(NT)
           const uint32_t v = v0 + lane;
           uint64_t kv = v < n ? key[v] : 0ull;
           const bool q2 = (kv & 1ull) && fkey_lat(kv) < split;
-          append_q<1>(&q2, &v, ring, &ctl[TAIL], slot_of, lane);
+          const uint64_t m2 = __ballot(q2);
+          append_q<1>(&m2, &v, ring, &ctl[TAIL], slot_of, lane);
         }
         __syncthreads();
         continue;
@@ -516,7 +524,8 @@ __global__ void __launch_bounds__(NT)
         if (COUNT) n_rel += __builtin_amdgcn_readlane(wave_incl_sum(deg), 63);
         for (uint32_t j0 = 0; j0 < dmax; j0 += LA) {
           uint32_t v[LA], lat[LA], om[LA];
-          bool valid[LA], app[LA];
+          bool valid[LA];
+          uint64_t app[LA];
 #pragma unroll
           for (int c = 0; c < LA; c++) {
             valid[c] = j0 + c < deg;
@@ -546,7 +555,8 @@ __global__ void __launch_bounds__(NT)
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           uint32_t v[SSSP_K], lat[SSSP_K], om[SSSP_K], o[SSSP_K];
-          bool valid[SSSP_K], app[SSSP_K];
+          bool valid[SSSP_K];
+          uint64_t app[SSSP_K];
 #pragma unroll
           for (int c = 0; c < SSSP_K; c++) {
             const uint32_t hd = ow[c * 64 + lane];

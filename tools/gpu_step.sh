@@ -1,8 +1,10 @@
 set -u
-O=gpurun_out/r6r; mkdir -p $O
-timeout -k 10 400 python3 -u -m pytest tests/test_inbound_gpu.py tests/test_codel_gpu.py -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
-tail -2 $O/t.log
-timeout -k 10 600 python3 -u bench.py --no-cpu > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
-python3 -c "
-import json; d=json.load(open('$O/bench.json')); i=d['inbound']; print('inbound', i['ms_per_window'], i['roofline']['avg_launch_ms'], i['by_packet_id'])
-print('delivery', d['delivery']['ms_per_round'] if 'delivery' in d else d.get('ms_per_step'))"
+O=gpurun_out/r6w; mkdir -p $O
+timeout -k 10 500 python3 -u -m pytest tests/test_routing_gpu.py -x -q --timeout 200 --timeout-method thread -k "c3_full_table or random_sparse or row_blocks or persistent or variants" > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
+tail -1 $O/t.log
+for r in 1 2 3; do
+  for L in tools/ab/base_r6.so shadow_amd/libshadow_gpu.so; do
+    SHADOW_GPU_LIB=$PWD/$L timeout -k 10 120 python3 -u tools/apsp_ab.py --nodes 10000 --variants "SG_SSSP_X=0" --reps 7 --rounds 1 > $O/ab_$r.log 2>&1 || { tail $O/ab_$r.log; exit 1; }
+    echo "$L $(grep median $O/ab_$r.log | sed 's/; sssp.*//')"
+  done
+done
