@@ -98,7 +98,7 @@ constexpr int SSSP_KB = SSSP_KB_MAX;  // bound rows per bounded search (sg_routi
 // sink[64] (u64), s_ub[SSSP_KB][3] + s_nub (u32)
 constexpr size_t SSSP_STATIC_LDS = 4 * (8 + SSSP_WAVES) + 16 + SSSP_WAVES * 64 * SSSP_K + 512 + 4 * (3 * SSSP_KB + 1) + 16;
 // lane path: arcs a lane has in flight (template LA: 8 or 16, SG_SSSP_LANE_ARCS);
-// used up to out-degree lane_deg_max (SG_SSSP_LANE_DEG, default 16)
+// used up to out-degree lane_deg_max (SG_SSSP_LANE_DEG, default 64; the arcs past LA arc-parallel)
 
 constexpr size_t LDS_PER_CU = 160 * 1024;
 
@@ -519,10 +519,60 @@ __global__ void __launch_bounds__(NT)
       const uint32_t deg = a1 - a0;
       const uint32_t dmax = __builtin_amdgcn_readlane(wave_incl_max(deg), 63);
       const unsigned long long tc2 = (COUNT && diag) ? clock64() : 0;
+      // arcs [ea0, ea0 + edeg) of each lane's node, arc-parallel: the wave's arcs in consecutive
+      // slots, KX chunks of 64 at once (owner lane by scatter + max-scan)
+      auto expand = [&](auto kx, uint32_t ea0, uint32_t edeg) {
+        constexpr int KX = decltype(kx)::value;
+        const uint32_t incl = wave_incl_sum(edeg);
+        const uint32_t base = incl - edeg;
+        const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+        if (COUNT) n_rel += T;
+        uint32_t carry = 0;  // 1 + the owner lane of the previous slot
+        for (uint32_t t0 = 0; t0 < T; t0 += 64 * KX) {
+          // owner lane of each slot: heads scatter 1 + their lane at their first slot, a max-scan fills the rest
+          if (edeg && base >= t0 && base - t0 < 64u * KX) ow[base - t0] = (uint8_t)(lane + 1);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          uint32_t v[KX], lat[KX], om[KX], o[KX];
+          bool valid[KX];
+          uint64_t app[KX];
+#pragma unroll
+          for (int c = 0; c < KX; c++) {
+            const uint32_t hd = ow[c * 64 + lane];
+            ow[c * 64 + lane] = 0;
+            const uint32_t mx = max(wave_incl_max(hd), carry);
+            carry = __builtin_amdgcn_readlane(mx, 63);
+            o[c] = mx - 1;
+          }
+#pragma unroll
+          for (int c = 0; c < KX; c++) {
+            const uint32_t sl = t0 + c * 64 + lane;
+            valid[c] = sl < T;
+            const uint32_t a = __shfl(ea0, (int)o[c]) + sl - __shfl(base, (int)o[c]);
+            const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid[c] ? a * 12u : 0x80000000u, 0, 0);
+            v[c] = r[0];
+            lat[c] = r[1];
+            om[c] = r[2];
+          }
+          uint64_t cand[KX];
+#pragma unroll
+          for (int c = 0; c < KX; c++) {
+            const uint32_t klo = __shfl((uint32_t)ku, (int)o[c]), khi = __shfl((uint32_t)(ku >> 32), (int)o[c]);
+            cand[c] = frelax(((uint64_t)khi << 32) | klo, lat[c], __uint_as_float(om[c]));
+          }
+          offer_all(std::integral_constant<int, KX>(), valid, v, cand, app);
+          append_q<KX>(app, v, ring, &ctl[TAIL], slot_of, lane);
+        }
+      };
       if (dmax <= lane_deg_max) {
-        // ---- lane path: each lane walks its own node's arcs, LANE_ARCS loads in flight
-        if (COUNT) n_rel += __builtin_amdgcn_readlane(wave_incl_sum(deg), 63);
-        for (uint32_t j0 = 0; j0 < dmax; j0 += LA) {
+        // ---- lane path: each lane walks its node's first LA arcs (LA loads in flight); the arcs
+        // past them (nodes of degree > LA only) go arc-parallel like the expansion path.  At C3
+        // (mean degree 8, a wave's largest ~14) a second round of LA slots per lane was mostly
+        // idle lanes: 3.10 -> 2.83 ms (profiles/r05/ab_sssp_hybrid_r6x.txt)
+        if (COUNT) n_rel += __builtin_amdgcn_readlane(wave_incl_sum(min(deg, (uint32_t)LA)), 63);
+        {
+          constexpr uint32_t j0 = 0;
           uint32_t v[LA], lat[LA], om[LA];
           bool valid[LA];
           uint64_t app[LA];
@@ -541,49 +591,11 @@ __global__ void __launch_bounds__(NT)
           offer_all(std::integral_constant<int, LA>(), valid, v, cand, app);
           append_q<LA>(app, v, ring, &ctl[TAIL], slot_of, lane);
         }
+        if (dmax > (uint32_t)LA)  // the arcs past each node's first LA, arc-parallel
+          expand(std::integral_constant<int, 1>(), a0 + LA, deg > (uint32_t)LA ? deg - LA : 0u);
       } else {
         // ---- expansion path (high out-degree): arcs of the 64 entries in consecutive slots
-        const uint32_t incl = wave_incl_sum(deg);
-        const uint32_t base = incl - deg;
-        const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
-        if (COUNT) n_rel += T;
-        uint32_t carry = 0;  // 1 + the owner lane of the previous slot
-        for (uint32_t t0 = 0; t0 < T; t0 += 64 * SSSP_K) {
-          // owner lane of each slot: heads scatter 1 + their lane at their first slot, a max-scan fills the rest
-          if (deg && base >= t0 && base - t0 < 64u * SSSP_K) ow[base - t0] = (uint8_t)(lane + 1);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          uint32_t v[SSSP_K], lat[SSSP_K], om[SSSP_K], o[SSSP_K];
-          bool valid[SSSP_K];
-          uint64_t app[SSSP_K];
-#pragma unroll
-          for (int c = 0; c < SSSP_K; c++) {
-            const uint32_t hd = ow[c * 64 + lane];
-            ow[c * 64 + lane] = 0;
-            const uint32_t mx = max(wave_incl_max(hd), carry);
-            carry = __builtin_amdgcn_readlane(mx, 63);
-            o[c] = mx - 1;
-          }
-#pragma unroll
-          for (int c = 0; c < SSSP_K; c++) {
-            const uint32_t sl = t0 + c * 64 + lane;
-            valid[c] = sl < T;
-            const uint32_t a = __shfl(a0, (int)o[c]) + sl - __shfl(base, (int)o[c]);
-            const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid[c] ? a * 12u : 0x80000000u, 0, 0);
-            v[c] = r[0];
-            lat[c] = r[1];
-            om[c] = r[2];
-          }
-          uint64_t cand[SSSP_K];
-#pragma unroll
-          for (int c = 0; c < SSSP_K; c++) {
-            const uint32_t klo = __shfl((uint32_t)ku, (int)o[c]), khi = __shfl((uint32_t)(ku >> 32), (int)o[c]);
-            cand[c] = frelax(((uint64_t)khi << 32) | klo, lat[c], __uint_as_float(om[c]));
-          }
-          offer_all(std::integral_constant<int, SSSP_K>(), valid, v, cand, app);
-          append_q<SSSP_K>(app, v, ring, &ctl[TAIL], slot_of, lane);
-        }
+        expand(std::integral_constant<int, SSSP_K>(), a0, deg);
       }
       // release the claim after this wave's appends (LDS keeps a wave's operations in order)
       if (lane == 0) atomicSub(&hb, 1ull);
@@ -772,9 +784,11 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
   const char* ss = getenv("SG_SSSP_SLEEP");  // idle back-off, units of ~512 cycles
   const uint32_t idle_sleep = ss && *ss ? (uint32_t)std::max(0, atoi(ss)) : 0u;
   const char* ls = getenv("SG_SSSP_LANE_DEG");
-  const uint32_t lane_deg = ls && *ls ? (uint32_t)std::max(0, atoi(ls)) : 16u;
+  // (with the remainder arc-parallel, every wave takes the lane path unless SG_SSSP_LANE_DEG
+  // lowers it: C3 2.83 ms at 16, 2.79 at 24 and 64)
+  const uint32_t lane_deg = ls && *ls ? (uint32_t)std::max(0, atoi(ls)) : 64u;
   const char* la = getenv("SG_SSSP_LANE_ARCS");
-  const int la16 = la && atoi(la) == 16;
+  const int la16 = la && atoi(la) == 16, la4 = la && atoi(la) == 4;
   // One persistent workgroup per CU claims rows from a counter: out_off is
   // staged once per CU instead of once per row, and no workgroup is launched and
   // torn down per row.  C3: 3.92 -> 3.54 ms (same box).  SG_SSSP_PERSIST=0: a
@@ -816,6 +830,7 @@ void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_a
   } else {
     if (nt == 512) go(k_sssp_lds<false, 512, 8, 0>);
     else if (la16) go(k_sssp_lds<false, 1024, 16, 0>);
+    else if (la4) go(k_sssp_lds<false, 1024, 4, 0>);
     else go(k_sssp_lds<false, 1024, 8, 0>);
   }
   SG_CHECK_LAUNCH();
