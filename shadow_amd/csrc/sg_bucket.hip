@@ -721,6 +721,25 @@ struct BdLds {
   }
 };
 
+// Cache policies of the band kernel's streams (buffer aux bits: 16 sc1, 2 nt; A/B builds set them).
+// Measured at 12,800 C5 rows (r7b-r7d): entry stores sc1 86.8 ms and nt 147.8 against plain 62.3 --
+// the L2 merges a bucket list's 12-B appends into whole lines, and must keep them; entry loads nt
+// 61.1; scratch stores sc1 63.2.  Without the scratch stores at all (a wrong table) 52.4: the
+// settled keys' 8-B stores spread over a row's whole search leave L2 one partial line each.  A
+// settled list in their place (whole-line appends, the row's cells scattered at its end) took
+// 65.7-70.9 against 56.0-62.3: the end-of-row scatter costs more than it saves.
+#ifndef BD_ST_POL
+#define BD_ST_POL 0  // arena entry stores
+#endif
+#ifndef BD_LD_POL
+#define BD_LD_POL (BK_SC1 | 2)  // arena entry loads: read once
+#endif
+#ifndef BD_SCR_POL
+#define BD_SCR_POL 0  // settled keys to the scratch row
+#endif
+#ifndef BD_ARC_POL
+#define BD_ARC_POL 0  // arc records
+#endif
 template <bool COUNT, int NT>
 __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
   constexpr uint32_t NW = NT / 64;
@@ -865,7 +884,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
       typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
       const uint32_t e = ((uint32_t)id << BD_CH_LOG) | (pos[c] & (BD_CH - 1));
       __builtin_amdgcn_raw_buffer_store_b96((u32x3){v[c], (uint32_t)(key[c] >> 32), (uint32_t)key[c]}, ra, e * 12u, 0,
-                                            0);
+                                            BD_ST_POL);
     }
     if (COUNT) {
 #pragma unroll
@@ -925,7 +944,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
             const bool on = i < c;
             const uint32_t id = on ? tab[sb * BD_MAXCH + (i >> BD_CH_LOG)] : 0u;
             const uint32_t e = (id << BD_CH_LOG) | (i & (BD_CH - 1));
-            const auto r = __builtin_amdgcn_raw_buffer_load_b96(ra, on ? e * 12u : 0x80000000u, 0, BK_SC1);
+            const auto r = __builtin_amdgcn_raw_buffer_load_b96(ra, on ? e * 12u : 0x80000000u, 0, BD_LD_POL);
             v[g] = on ? r[0] : NONE;
             key[g] = ((uint64_t)r[1] << 32) | r[2];
           }
@@ -963,7 +982,8 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
             hid[x] = HID_EMPTY;
             hkey[x] = KINF;
             __builtin_amdgcn_raw_buffer_store_b64(
-                (uint32_t __attribute__((ext_vector_type(2)))){(uint32_t)ku, (uint32_t)(ku >> 32)}, rs, u * 8u, 0, 0);
+                (uint32_t __attribute__((ext_vector_type(2)))){(uint32_t)ku, (uint32_t)(ku >> 32)}, rs, u * 8u, 0,
+                BD_SCR_POL);
           }
           const unsigned long long q0 = wclk();
           const uint32_t deg = a1 - a0;
@@ -997,7 +1017,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
               const uint32_t sl = t0 + c * 64 + lane;
               const bool valid = sl < T;
               const uint32_t ai = __shfl(a0, (int)o[c]) + sl - __shfl(base, (int)o[c]);
-              const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid ? ai * 12u : 0x80000000u, 0, 0);
+              const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid ? ai * 12u : 0x80000000u, 0, BD_ARC_POL);
               const uint32_t klo = __shfl((uint32_t)ku, (int)o[c]), khi = __shfl((uint32_t)(ku >> 32), (int)o[c]);
               v[c] = r[0];
               cd[c] = valid ? relax32(((uint64_t)khi << 32) | klo, r[1], __uint_as_float(r[2])) : KINF;
