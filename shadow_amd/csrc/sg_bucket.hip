@@ -758,7 +758,8 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
   uint32_t* cst = (uint32_t*)(smem + L.o_cst);
   uint32_t* stg = (uint32_t*)(smem + L.o_stg);
   const uint32_t nbw = (n + 31) / 32;
-  constexpr int ABORT = 2, FTOP = 3, FBUMP = 4, FARMIN = 7, UCNT = 10;
+  constexpr int ABORT = 2, FTOP = 3, FBUMP = 4, FARMIN = 7, UCNT = 10, OVF = 11;
+  const uint32_t ulim = HS - HS / 4;  // nodes a (sub-)band may hold: past it the band splits
   __shared__ uint32_t ctl[16];
   __shared__ uint32_t s_item;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -809,16 +810,21 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
       t_mark = t;
     }
   };
-  // node v's hash slot, inserted (and listed) if absent; HS: the table is full
+  // node v's hash slot, inserted (and listed) if absent; HS: the table is full.  Past ulim nodes
+  // the pass is flagged (OVF) and redone over the band's lower half (see the band loop); once it
+  // is flagged nothing more is inserted (HS + 1: skip), so the table never fills
   auto hash_slot = [&](uint32_t v) -> uint32_t {
     uint32_t h = (v * 0x9E3779B1u) >> (32 - a.hs_log2);
     for (uint32_t p = 0; p < HS; p++) {
       const uint32_t id = ld(&hid[h]);
       if (id == v) return h;
       if (id == HID_EMPTY) {
+        if (ld(&ctl[OVF])) return HS + 1;
         const uint32_t o = atomicCAS(&hid[h], HID_EMPTY, v);
         if (o == HID_EMPTY) {
-          ulist[atomicAdd(&ctl[UCNT], 1u)] = (uint16_t)h;
+          const uint32_t k = atomicAdd(&ctl[UCNT], 1u);
+          if (k < ulim) ulist[k] = (uint16_t)h;
+          else ctl[OVF] = 1u;
           return h;
         }
         if (o == v) return h;
@@ -926,6 +932,11 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
       ctl[UCNT] = 1;
     }
     uint32_t b = 0, far = BK_R;
+    // the (sub-)band's latencies [sub_lo, sub_hi): the whole band [b delta, (b + 1) delta), or its
+    // lower part when the band holds more nodes than the hash takes (then the rest follows, from the
+    // same bucket list: a candidate is at least w_min >= delta past its tail, so no relaxation of
+    // the band lands in it)
+    uint64_t sub_lo = 0, sub_hi = a.delta;
     __syncthreads();
     stamp(-1);
     for (;;) {  // bands
@@ -945,7 +956,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
             const uint32_t id = on ? tab[sb * BD_MAXCH + (i >> BD_CH_LOG)] : 0u;
             const uint32_t e = (id << BD_CH_LOG) | (i & (BD_CH - 1));
             const auto r = __builtin_amdgcn_raw_buffer_load_b96(ra, on ? e * 12u : 0x80000000u, 0, BD_LD_POL);
-            v[g] = on ? r[0] : NONE;
+            v[g] = on && (uint64_t)r[1] < sub_hi ? r[0] : NONE;  // (past the sub-band: a later pass)
             key[g] = ((uint64_t)r[1] << 32) | r[2];
           }
           uint32_t x[BD_G];
@@ -964,6 +975,23 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
       __syncthreads();
       stamp(0);
       if (ld(&ctl[ABORT])) goto wave_exit;
+      if (ld(&ctl[OVF])) {  // (uniform) too many nodes: the lower half of the (sub-)band again
+        for (uint32_t i = tid; i < HS; i += NT) {
+          hid[i] = HID_EMPTY;
+          hkey[i] = KINF;
+        }
+        __syncthreads();  // every wave has read OVF
+        if (tid == 0) {
+          ctl[OVF] = 0u;
+          ctl[UCNT] = 0u;
+        }
+        sub_hi = sub_lo + (sub_hi - sub_lo) / 2;
+        if (sub_hi <= sub_lo || E) give_up();  // (a 1-ns band, or staging on: the wide kernel)
+        if (COUNT && a.diag && tid == 0) atomicAdd(&a.diag[15], 1ull);  // band splits
+        __syncthreads();
+        if (ld(&ctl[ABORT])) goto wave_exit;
+        continue;
+      }
       // ---- relax: the band's nodes are final; settle them and relax their arcs arc-parallel
       {
         const uint32_t U = ctl[UCNT];
@@ -1059,6 +1087,13 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
       __syncthreads();
       stamp(1);
       if (ld(&ctl[ABORT])) goto wave_exit;
+      if (sub_hi < (uint64_t)b * a.delta + a.delta) {  // the band's next sub-band, from the same list
+        if (tid == 0) ctl[UCNT] = 0;
+        sub_lo = sub_hi;
+        sub_hi = (uint64_t)b * a.delta + a.delta;
+        __syncthreads();
+        continue;
+      }
       // ---- next band: the first non-empty ring slot after b, or a far step (sg_bucket.hip k_sssp_bucket)
       uint32_t nb, fm;
       {
@@ -1105,6 +1140,8 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
       } else {
         b = nb;
       }
+      sub_lo = (uint64_t)b * a.delta;
+      sub_hi = sub_lo + a.delta;
       stamp(2);
     }
     if (COUNT && lane == 0) {
