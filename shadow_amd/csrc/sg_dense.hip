@@ -44,6 +44,18 @@ constexpr int DENSE_WAVES = DENSE_THREADS / 64;
 constexpr uint32_t DENSE_SCAP = 512;    // nodes settled per round at most (the rest wait a round)
 constexpr uint32_t SORT_MAXDEG = 4096;  // out-degree sorted in one block's LDS; larger rows stay unsorted
 constexpr int DENSE_G = 2;              // settled rows a wave relaxes together (their loads in flight)
+// Sorted-arc records of 12 B (b96 loads; DN_REC16 builds the 16-B records with a pad word of r04).
+// A/B knobs (C2, r7h, `profiles/r05/ab_c2_dense_r7h.txt`): 12-B records 0.461-0.465 ms against
+// 0.469-0.474 for 16 B; DN_NT1 (nt loads in a round whose cut is still open: a row's whole arc
+// list, read once) 0.520; DN_NTOUT (nontemporal table stores) 0.470-0.472.
+#ifndef DN_REC16
+#define DN_REC12
+#endif
+#ifdef DN_REC12
+constexpr uint32_t DN_W = 3;
+#else
+constexpr uint32_t DN_W = 4;
+#endif
 
 // Per node u: its out-arcs (out_arc, 3 u32 each: head, latency32, bits(1f32 - loss))
 // sorted by latency into 16-B records {head, latency32, bits(om), 0} at the same
@@ -53,7 +65,7 @@ constexpr int DENSE_G = 2;              // settled rows a wave relaxes together 
 constexpr int SORT_THREADS = 1024;
 __global__ void __launch_bounds__(SORT_THREADS) k_sort_arcs(const uint32_t* __restrict__ out_off,
                                                             const uint32_t* __restrict__ out_arc, uint32_t cap,
-                                                            uint4* __restrict__ sa, uint8_t* __restrict__ sorted,
+                                                            uint32_t* __restrict__ sa, uint8_t* __restrict__ sorted,
                                                             uint32_t* __restrict__ wmin) {
   extern __shared__ __align__(16) unsigned long long k[];  // [cap]
   __shared__ uint32_t s_lo[SORT_THREADS / 64];
@@ -63,7 +75,11 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_arcs(const uint32_t* __re
   if (deg > cap) {
     for (uint32_t i = t; i < deg; i += SORT_THREADS) {
       const uint32_t* r = out_arc + 3 * (size_t)(a0 + i);
-      sa[a0 + i] = make_uint4(r[0], r[1], r[2], 0u);
+      uint32_t* d = sa + DN_W * (size_t)(a0 + i);
+      d[0] = r[0];
+      d[1] = r[1];
+      d[2] = r[2];
+      if (DN_W == 4) d[3] = 0u;
       lo = min(lo, r[1]);
     }
     if (t == 0) sorted[u] = 0;
@@ -92,7 +108,11 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_arcs(const uint32_t* __re
       }
     for (uint32_t i = t; i < deg; i += SORT_THREADS) {
       const uint32_t* r = out_arc + 3 * (size_t)(a0 + (uint32_t)(k[i] & 0xFFFFFFFFu));
-      sa[a0 + i] = make_uint4(r[0], r[1], r[2], 0u);
+      uint32_t* d = sa + DN_W * (size_t)(a0 + i);
+      d[0] = r[0];
+      d[1] = r[1];
+      d[2] = r[2];
+      if (DN_W == 4) d[3] = 0u;
     }
     if (t == 0) sorted[u] = 1;
   }
@@ -107,7 +127,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_arcs(const uint32_t* __re
 }
 
 __global__ void __launch_bounds__(DENSE_THREADS) k_sssp_dense(const uint32_t* __restrict__ out_off,
-                                                              const uint4* __restrict__ sa,
+                                                              const uint32_t* __restrict__ sa,
                                                               const uint8_t* __restrict__ sorted, uint32_t n,
                                                               uint32_t n_arcs, const uint32_t* __restrict__ wmin_p,
                                                               const uint32_t* __restrict__ used, uint32_t n_used,
@@ -205,13 +225,32 @@ __global__ void __launch_bounds__(DENSE_THREADS) k_sssp_dense(const uint32_t* __
 #pragma unroll
       for (int g = 0; g < DENSE_G; g++) budget[g] = T - min(T, key_lat(ku[g]));
       bool live = true;
+#ifdef DN_NT1
+      const bool open = T == LAT32_SAT;  // (uniform) an open cut: whole rows, read once
+#endif
       while (live) {
         uint4 r[DENSE_G];
 #pragma unroll
         for (int g = 0; g < DENSE_G; g++) {
           const uint32_t i = a[g] + lane;
-          const auto x = __builtin_amdgcn_raw_buffer_load_b128(ra, i < e[g] ? i * 16u : 0x80000000u, 0, 0);
+          const uint32_t off = i < e[g] ? i * (4u * DN_W) : 0x80000000u;
+#ifdef DN_REC12
+#ifdef DN_NT1
+          const auto x = open ? __builtin_amdgcn_raw_buffer_load_b96(ra, off, 0, 2)
+                              : __builtin_amdgcn_raw_buffer_load_b96(ra, off, 0, 0);
+#else
+          const auto x = __builtin_amdgcn_raw_buffer_load_b96(ra, off, 0, 0);
+#endif
+          r[g] = make_uint4(x[0], x[1], x[2], 0u);
+#else
+#ifdef DN_NT1
+          const auto x = open ? __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 2)
+                              : __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
+#else
+          const auto x = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
+#endif
           r[g] = make_uint4(x[0], x[1], x[2], x[3]);
+#endif
         }
         live = false;
 #pragma unroll
@@ -242,8 +281,13 @@ __global__ void __launch_bounds__(DENSE_THREADS) k_sssp_dense(const uint32_t* __
     const unsigned long long k = key[v];
     const bool diag = jj == row;
     sat |= !diag && key_lat(k) == LAT32_SAT;
+#ifdef DN_NTOUT
+    __builtin_nontemporal_store(diag ? e_lat[de] : (uint64_t)key_lat(k), &out_lat[orow + jj]);
+    __builtin_nontemporal_store(diag ? e_loss[de] : __uint_as_float(key_loss_bits(k)), &out_loss[orow + jj]);
+#else
     out_lat[orow + jj] = diag ? e_lat[de] : (uint64_t)key_lat(k);
     out_loss[orow + jj] = diag ? e_loss[de] : __uint_as_float(key_loss_bits(k));
+#endif
   }
   if (__any(sat) && lane == 0) sat_row[blockIdx.x] = 1u;
 }
@@ -255,12 +299,12 @@ void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_
                        unsigned long long* work) {
   const uint32_t n = net->n_nodes, rows = row_end - row_begin;
   if (!sssp_dense_fits(n)) throw Error(SG_ERR_INVALID_ARG, "graph too large for the dense search");
-  if ((uint64_t)net->n_arcs * 16 >= (1ull << 31)) throw Error(SG_ERR_INVALID_ARG, "too many arcs for the dense search");
+  if ((uint64_t)net->n_arcs * 4 * DN_W >= (1ull << 31)) throw Error(SG_ERR_INVALID_ARG, "too many arcs for the dense search");
   hipStream_t st = ctx->stream;
-  // workspace: sorted arcs (16 B each), per-node sorted flag, w_min
-  uint4* sa = ctx->r_dense.get<uint4>((size_t)net->n_arcs + 1 + (n + 15) / 16);
-  uint32_t* wmin = (uint32_t*)(sa + net->n_arcs);
-  uint8_t* sorted = (uint8_t*)(sa + net->n_arcs + 1);
+  // workspace: sorted arcs (4 DN_W B each), w_min, per-node sorted flag
+  uint32_t* sa = ctx->r_dense.get<uint32_t>((size_t)net->n_arcs * DN_W + 4 + (n + 3) / 4);
+  uint32_t* wmin = sa + (size_t)net->n_arcs * DN_W;
+  uint8_t* sorted = (uint8_t*)(wmin + 4);
   {
     TimedLaunch tl(ctx, "dense_sort", 24.0 * net->n_arcs);
     SG_HIP(hipMemsetAsync(wmin, 0xFF, 4, st));
@@ -273,7 +317,7 @@ void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_
   const uint32_t nbw = (n + 31) / 32;
   const size_t lds = (size_t)n * 8 + (size_t)((nbw + 1) & ~1u) * 4 + DENSE_SCAP * 4;
   TimedLaunch tl(ctx, "sssp_dense", 0.0);
-  hipLaunchKernelGGL(k_sssp_dense, dim3(rows), dim3(DENSE_THREADS), lds, st, net->out_off, (const uint4*)sa,
+  hipLaunchKernelGGL(k_sssp_dense, dim3(rows), dim3(DENSE_THREADS), lds, st, net->out_off, (const uint32_t*)sa,
                      (const uint8_t*)sorted, n, net->n_arcs, (const uint32_t*)wmin, d_used, n_used, row_begin,
                      net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat_row, work);
   SG_CHECK_LAUNCH();
