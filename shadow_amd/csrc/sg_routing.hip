@@ -1648,8 +1648,12 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   // which it builds as fast (one box, tools/sssp_ab.py, C3 graph, tables bit-identical:
   // 10k rows 3.187 against 3.185 ms; row blocks of 5,000 1.93 against 1.99, 2,500 1.13
   // against 1.20, 1,250 0.685 against 0.706).  SG_SSSP_FLAGGED=0 / 1 forces it.
+  // Below 6 rows per CU neither pays: the plan and the seeding cost more than the bounds save
+  // (r7i-r7j, C3 graph, the hybrid lane path, tables identical: 640 rows 0.351 ms unbounded against
+  // 0.398 flagged, 1,250 rows 0.558 against 0.581; 2,500 rows 1.044 against 0.948 flagged)
   const int flag_env = env_int("SG_SSSP_FLAGGED", -1);
-  const bool flagged = seeds_env != 0 && (flag_env == 1 || (flag_env < 0 && rows < n_used));
+  const bool few_rows = rows < 6u * (uint32_t)std::max(1, ctx->n_cu);
+  const bool flagged = seeds_env != 0 && (flag_env == 1 || (flag_env < 0 && rows < n_used && !few_rows));
   const bool phased = !flagged && seeds_env != 0 && (seeds_env == 2 || rows >= 8u * (uint32_t)ctx->n_cu);
   if (!phased && !flagged) SG_HIP(hipMemsetAsync(sat, 0, rows * 4ull, st));
   if (flagged) {
