@@ -264,6 +264,17 @@ typedef struct sg_table {
   const uint64_t* path_key;   /* device, n_rows x n_cols, or NULL */
 } sg_table;
 
+/* ABI 7: per-pair packet counters on the device.  RoutingInfo::increment_packet_count
+ * (graph/mod.rs:451-459), which Worker::send_packet calls for every delivered
+ * packet (worker.rs:373): with counters set, every sg_deliver_round /
+ * sg_deliver_source on this context adds one to counts[cell] for each packet it
+ * delivers, cell = the path's cell of the table it was given ((route row -
+ * row_begin) * n_cols + destination column).  counts: device u64, n_cells >=
+ * the table's n_rows * n_cols, zeroed by the caller (the reference's counters
+ * start empty); NULL turns counting off (the default).  The reference
+ * saturates its u64; a u64 count of packets cannot reach it. */
+int32_t sg_ctx_set_packet_counters(sg_ctx* ctx, uint64_t* counts, uint64_t n_cells);
+
 /* Pack a table's (latency_ns, packet_loss) cells into path_key form
  * (out_key: device, n_rows x n_cols u64).  *out_packable (host) = 1 if every
  * latency is below 2^32 ns, else 0 and out_key must not be used (latencies of

@@ -44,7 +44,7 @@ EXPORTED = [
     "sg_deliver_source_padded", "sg_deliver_bucket_padded", "sg_deliver_pad_to_compact",
     "sg_table_pack", "sg_codel_create", "sg_codel_destroy", "sg_codel_run", "sg_codel_ring_cap",
     "sg_codel_get_state", "sg_codel_set_state", "sg_inbound_create", "sg_inbound_destroy", "sg_inbound_ring_cap",
-    "sg_inbound_run", "sg_inbound_run_ordered", "sg_inbound_get_state", "sg_hosts_event_ctr", "sg_outbound_create", "sg_outbound_destroy",
+    "sg_inbound_run", "sg_inbound_run_ordered", "sg_ctx_set_packet_counters", "sg_inbound_get_state", "sg_hosts_event_ctr", "sg_outbound_create", "sg_outbound_destroy",
     "sg_outbound_ring_cap", "sg_outbound_run", "sg_outbound_get_state",
     "sg_routing_info_create", "sg_routing_info_destroy", "sg_routing_info_fill", "sg_routing_info_set_rows",
     "sg_routing_info_view", "sg_routing_info_rows", "sg_routing_info_index", "sg_routing_info_path", "sg_routing_info_smallest_latency",
@@ -243,6 +243,7 @@ def load(path: str | None = None):
         "sg_inbound_run": (i32, [vp, vp, C.POINTER(sg_inbound_arrivals), u64, u64, u64, vp, vp, vp, u32, u64p]),
         "sg_inbound_run_ordered": (i32, [vp, vp, C.POINTER(sg_inbound_arrivals), u64, u64, u64, vp, vp, vp, u32, vp,
                                          vp, u64p]),
+        "sg_ctx_set_packet_counters": (i32, [vp, vp, u64]),
         "sg_inbound_get_state": (i32, [vp, C.POINTER(sg_codel_state), C.POINTER(sg_inbound_relay_state)]),
         "sg_hosts_event_ctr": (vp, [vp]),
         "sg_outbound_create": (i32, [vp, u32, vp, vp, u32, C.POINTER(vp)]),

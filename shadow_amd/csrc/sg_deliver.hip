@@ -204,6 +204,7 @@ struct WalkArgs {
   uint32_t* dst_host;
   unsigned long long* blk_stats;  // per block: [n_delivered, min_deliver, min_lat] (reduced by k_reduce_stats)
   uint32_t* err;
+  unsigned long long* pair_count;  // CNT: per table cell, +1 per delivered packet (sg_ctx_set_packet_counters)
 };
 
 // A block owns WALK_HOSTS consecutive source hosts; their packets are one
@@ -231,7 +232,10 @@ enum : uint8_t { W_SIM_END = 0, W_NO_DST = 1, W_DRAW = 2, W_PAYLOAD = 4, W_BOOT 
 // SKIP: packets carry rng_skip (sg_packets), staged in LDS beside the rest (4 B
 // more per packet: 7 blocks per CU instead of 8, still every block of a 100k-host
 // round resident); a batch without it runs the SKIP = false variant unchanged.
-template <bool PACKED, bool SKIP>
+// CNT: every delivered packet adds one to its path's cell in a.pair_count
+// (RoutingInfo::increment_packet_count, graph/mod.rs:451-459, called from worker.rs:373); a round
+// without counters runs CNT = false unchanged.
+template <bool PACKED, bool SKIP, bool CNT = false>
 // At most 64 VGPRs (8 waves per SIMD, 8 blocks per CU): a 100k-host round's
 // 1,563 blocks are then all resident at once.  At 74 VGPRs 6 blocks fit a CU,
 // and the last 27 blocks ran as a second round, doubling the kernel time.
@@ -281,6 +285,7 @@ __global__ void __launch_bounds__(WALK_THREADS) __attribute__((amdgpu_waves_per_
     uint32_t ip[PPT], sh[PPT], d[PPT], r[PPT];
     uint8_t f[PPT];
     uint32_t sk[PPT];
+    size_t cellq[CNT ? PPT : 1];  // CNT: the path's cell, for the counter
 #pragma unroll
     for (int q = 0; q < PPT; q++) {
       const uint32_t i = min(c0 + t + q * WALK_THREADS, c1 - 1);
@@ -332,6 +337,7 @@ __global__ void __launch_bounds__(WALK_THREADS) __attribute__((amdgpu_waves_per_
       float loss = 0.0f;
       const bool ok = d[q] != NONE;  // then the table has cells (a destination needs its route column)
       const size_t cell = ok ? (size_t)(r[q] - a.row_begin) * a.n_cols + ip[q] : 0;
+      if constexpr (CNT) cellq[q] = cell;
       if (a.n_cols && a.n_rows) {  // uniform; branch-free gathers (cell 0 for the lanes that drop them)
         if (PACKED) {
           lat = a.tab_key[cell];  // one 8-byte gather
@@ -403,6 +409,8 @@ __global__ void __launch_bounds__(WALK_THREADS) __attribute__((amdgpu_waves_per_
         a.deliver[i] = s_t[k];
         a.eid[i] = s_l[k];
         a.dst_host[i] = st == SG_PKT_DELIVERED ? d[q] : NONE;
+        if constexpr (CNT)  // u64: saturation (the reference's saturating_add) is out of reach
+          if (st == SG_PKT_DELIVERED) atomicAdd(&a.pair_count[cellq[q]], 1ull);
       }
     }
     __syncthreads();
@@ -1722,18 +1730,28 @@ static RoundWork source_phase(sg_ctx* ctx, sg_hosts* hs, const sg_table* tab, co
   const uint32_t walk_blocks = (H + WALK_HOSTS - 1) / WALK_HOSTS;
   a.blk_stats = ctx->d_blk.get<unsigned long long>(3 * (size_t)walk_blocks);
   a.err = ctx->round_err;
+  a.pair_count = ctx->pair_count;
+  if (a.pair_count && ctx->pair_count_cells < (uint64_t)tab->n_rows * tab->n_cols)
+    throw Error(SG_ERR_INVALID_ARG, "packet counters smaller than the routing table");
   {
     // per packet: 20 B in, 12 B (8 B packed) path gather, 4 B dst map, 21 B out (status, time, id),
     // 4 B dst scratch; per host: 8 B segment, 4 B route, 32+32 B RNG, 8+8 B event counter
     TimedLaunch tl(ctx, "walk", (tab->path_key ? 57.0 : 61.0) * P + 92.0 * H);
-    if (a.tab_key && a.skip)
-      hipLaunchKernelGGL((k_walk<true, true>), dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
-    else if (a.tab_key)
-      hipLaunchKernelGGL((k_walk<true, false>), dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
-    else if (a.skip)
-      hipLaunchKernelGGL((k_walk<false, true>), dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
-    else
-      hipLaunchKernelGGL((k_walk<false, false>), dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a);
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(walk_blocks), dim3(WALK_THREADS), 0, st, a); };
+    if (a.pair_count) {
+      if (a.tab_key && a.skip) go(k_walk<true, true, true>);
+      else if (a.tab_key) go(k_walk<true, false, true>);
+      else if (a.skip) go(k_walk<false, true, true>);
+      else go(k_walk<false, false, true>);
+    } else if (a.tab_key && a.skip) {
+      go(k_walk<true, true>);
+    } else if (a.tab_key) {
+      go(k_walk<true, false>);
+    } else if (a.skip) {
+      go(k_walk<false, true>);
+    } else {
+      go(k_walk<false, false>);
+    }
   }
   const StatsJob sj{a.blk_stats, walk_blocks, ctx->round_err, w.big_count, ctx->round_ret, stats_row};
   if (fuse_stats)
@@ -2105,6 +2123,13 @@ int32_t sg_deliver_round(sg_ctx* ctx, sg_hosts* hosts, const sg_table* table, co
       throw Error(SG_ERR_INVALID_ARG, "null packet or output array");
     deliver_round(ctx, hosts, table, round, packets, out, stats);
   });
+}
+
+int32_t sg_ctx_set_packet_counters(sg_ctx* ctx, uint64_t* counts, uint64_t n_cells) {
+  if (!ctx || (counts && !n_cells)) return SG_ERR_INVALID_ARG;
+  ctx->pair_count = (unsigned long long*)counts;
+  ctx->pair_count_cells = counts ? n_cells : 0;
+  return SG_OK;
 }
 
 }  // extern "C"

@@ -90,6 +90,8 @@ struct sg_round_ret {
 
 struct sg_ctx {
   int device = 0;
+  unsigned long long* pair_count = nullptr;  // sg_ctx_set_packet_counters: per table cell (device), or null
+  uint64_t pair_count_cells = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   int n_cu = 256;

@@ -54,6 +54,18 @@ class Context:
     def synchronize(self) -> None:
         check(self.handle, load().sg_ctx_synchronize(self.handle))
 
+    def set_packet_counters(self, counts=None) -> None:
+        """RoutingInfo::increment_packet_count on the device (sg_ctx_set_packet_counters): a
+        zeroed int64 device tensor with a cell per routing-table cell; every delivered packet of
+        this context's later rounds adds one at its path's cell.  None turns counting off."""
+        if counts is None:
+            check(self.handle, load().sg_ctx_set_packet_counters(self.handle, None, 0))
+            return
+        if counts.dtype.itemsize != 8 or not counts.is_cuda or not counts.is_contiguous():
+            raise ValueError("packet counters: a contiguous 8-byte device tensor")
+        self._packet_counts = counts  # kept alive while the library holds the pointer
+        check(self.handle, load().sg_ctx_set_packet_counters(self.handle, counts.data_ptr(), counts.numel()))
+
     def enable_timers(self, enable: bool = True, count_work: bool = False) -> None:
         """Per-kernel HIP-event timers on this context's stream (resets them).
 

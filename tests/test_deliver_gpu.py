@@ -439,3 +439,36 @@ def test_c5_packet_count_round(oracle, ctx, table_form):
     want, got, ost, gst, _ = _run_both(oracle, ctx, lat, loss, hosts, pk, end, 2**63, 0)
     assert want["delivered"] > 9_000_000
     _assert_same(want, got, ost, gst)
+
+
+def test_packet_counters(oracle, ctx):
+    """RoutingInfo::increment_packet_count on the device (sg_ctx_set_packet_counters,
+    graph/mod.rs:451-459, worker.rs:373): one count per delivered packet at its path's cell,
+    over two rounds; packets dropped by loss, to unknown addresses or past the end count nothing."""
+    import torch
+
+    lat, loss, hosts = _world(seed=4)
+    n = lat.shape[0]
+    start, end = T0 + 10**9, T0 + 10**9 + 10**6
+    counts = torch.zeros(n * n, dtype=torch.int64, device="cuda")
+    want = np.zeros(n * n, np.uint64)
+    ip_to_host = {int(ip): h for h, ip in enumerate(hosts["ip"])}
+    ctx.set_packet_counters(counts)
+    try:
+        rng0 = ctr0 = None
+        for r in range(2):
+            pk = synth.make_packets(30000, hosts, start, end, seed=40 + r, p_unknown_dst=0.01)
+            pk["send_time"][::501] = end + 5 * 10**8
+            w, got, ost, gst, ht = _run_both(oracle, ctx, lat, loss, hosts, pk, end, end + 5 * 10**8, start,
+                                             rng0, ctr0)
+            _assert_same(w, got, ost, gst)
+            rng0, ctr0 = gst
+            dlv = np.nonzero(w["status"] == oracle.ST_DELIVERED)[0]
+            dh = np.array([ip_to_host[int(x)] for x in pk["dst_ip"][dlv]], np.int64)
+            cell = hosts["route"][pk["src"][dlv]].astype(np.int64) * n + hosts["route"][dh].astype(np.int64)
+            np.add.at(want, cell, np.uint64(1))
+            start, end = end, end + 10**6
+        assert want.sum() > 0
+        assert np.array_equal(counts.cpu().numpy().view(np.uint64), want)
+    finally:
+        ctx.set_packet_counters(None)
