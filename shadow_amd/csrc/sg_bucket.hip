@@ -727,7 +727,9 @@ struct BdLds {
 // 61.1; scratch stores sc1 63.2.  Without the scratch stores at all (a wrong table) 52.4: the
 // settled keys' 8-B stores spread over a row's whole search leave L2 one partial line each.  A
 // settled list in their place (whole-line appends, the row's cells scattered at its end) took
-// 65.7-70.9 against 56.0-62.3: the end-of-row scatter costs more than it saves.
+// 65.7-70.9 against 56.0-62.3: the end-of-row scatter costs more than it saves; the same list
+// put in column order by a counting sort over column blocks and written block by block from LDS
+// (no scattered store at all) 64.1-64.3 against 61.5-61.6: three passes over the list cost more.
 #ifndef BD_ST_POL
 #define BD_ST_POL 0  // arena entry stores
 #endif
