@@ -586,12 +586,16 @@ def c2_leg(a, ctx, torch, NetworkGraph, synth, with_cpu, pmc=None):
         one_shot()
     torch.cuda.synchronize()
     t_one_shot = (time.perf_counter() - t0) / a.steps
+    # the arc sort runs once per graph (a rebuild reuses the sorted arcs): timed on a fresh graph
+    ctx.enable_timers(True)
+    queue_ahead(ctx, torch)
+    one_shot()
+    sort_ms, _, _ = ctx.read_timer("dense_sort")
     ctx.enable_timers(True)
     queue_ahead(ctx, torch)
     net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
     relax_ms, launches, _ = ctx.read_timer("relax")
     dense_ms, dense_n, _ = ctx.read_timer("sssp_dense")
-    sort_ms, _, _ = ctx.read_timer("dense_sort")
     ctx.enable_timers(True, count_work=True)  # (a separate build: the counting adds atomics)
     net.build_rows_device(used, 0, n, lat.data_ptr(), loss.data_ptr(), True)
     dense_rel = ctx.read_timer("sssp_dense")[2]

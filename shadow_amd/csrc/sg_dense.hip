@@ -301,17 +301,24 @@ void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_
   if (!sssp_dense_fits(n)) throw Error(SG_ERR_INVALID_ARG, "graph too large for the dense search");
   if ((uint64_t)net->n_arcs * 4 * DN_W >= (1ull << 31)) throw Error(SG_ERR_INVALID_ARG, "too many arcs for the dense search");
   hipStream_t st = ctx->stream;
-  // workspace: sorted arcs (4 DN_W B each), w_min, per-node sorted flag
-  uint32_t* sa = ctx->r_dense.get<uint32_t>((size_t)net->n_arcs * DN_W + 4 + (n + 3) / 4);
+  // workspace: sorted arcs (4 DN_W B each), w_min, per-node sorted flag.  A graph is immutable,
+  // so its arcs are sorted once: a rebuild on the same sg_net reuses them (the context's workspace
+  // remembers whose arcs it holds; C2 rebuild 0.46 -> ~0.33 ms, the sort ~0.13 ms)
+  const size_t words = (size_t)net->n_arcs * DN_W + 4 + (n + 3) / 4;
+  const bool fresh = ctx->dense_owner != net->serial || ctx->r_dense.cap < words * 4;
+  uint32_t* sa = ctx->r_dense.get<uint32_t>(words);
   uint32_t* wmin = sa + (size_t)net->n_arcs * DN_W;
   uint8_t* sorted = (uint8_t*)(wmin + 4);
-  {
+  if (fresh) {
+    ctx->dense_owner = 0;  // (set again once the sort is queued)
     TimedLaunch tl(ctx, "dense_sort", 24.0 * net->n_arcs);
     SG_HIP(hipMemsetAsync(wmin, 0xFF, 4, st));
     uint32_t cap = 64;
     while (cap < n - 1 && cap < SORT_MAXDEG) cap <<= 1;
     hipLaunchKernelGGL(k_sort_arcs, dim3(n), dim3(SORT_THREADS), cap * 8, st, net->out_off, net->out_arc, cap, sa,
                        sorted, wmin);
+    SG_CHECK_LAUNCH();
+    ctx->dense_owner = net->serial;
   }
   if (!rows) return;
   const uint32_t nbw = (n + 31) / 32;

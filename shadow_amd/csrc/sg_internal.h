@@ -92,6 +92,8 @@ struct sg_ctx {
   int device = 0;
   unsigned long long* pair_count = nullptr;  // sg_ctx_set_packet_counters: per table cell (device), or null
   uint64_t pair_count_cells = 0;
+  uint64_t net_serial = 0;   // the last sg_net serial handed out
+  uint64_t dense_owner = 0;  // the net whose arcs r_dense holds sorted (0: none)
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   int n_cu = 256;
@@ -160,6 +162,7 @@ struct sg_ctx {
 // Device-resident network graph (sg_routing.hip builds it).
 struct sg_net {
   sg_ctx* ctx = nullptr;
+  uint64_t serial = 0;  // unique per context: who owns the context's sorted-arc workspace (sg_dense.hip)
   uint32_t n_nodes = 0, n_edges = 0, n_arcs = 0;
   bool directed = false;
   // the arcs' smallest latency and mean latency (each clamped to LAT32_SAT), taken on the host

@@ -1883,6 +1883,7 @@ int32_t sg_net_create(sg_ctx* ctx, const sg_graph* g, sg_net** out) {
   sg_net* net = nullptr;
   int32_t rc = sg::guarded(ctx, [&] {
     net = new sg_net();
+    net->serial = ++ctx->net_serial;
     sg::build_net(ctx, g, net);
   });
   if (rc != SG_OK) {

@@ -541,3 +541,27 @@ def test_bucket_search_knobs(oracle, ctx, monkeypatch, env, apsp_kernel):
         g["loss"] = np.where(np.arange(len(g["loss"])) % 3 == 0, np.float32(0.05), g["loss"]).astype(np.float32)
         used = np.random.default_rng(41).permutation(700)[:500].astype(np.uint32)
         _check(oracle, g, used, ctx, poison=True)
+
+
+def test_dense_sorted_arcs_per_graph(oracle, ctx):
+    """The dense search sorts a graph's arcs once and reuses them on later builds of the same
+    graph (the context's workspace remembers whose arcs it holds): rebuilds with other row ranges
+    and used sets, interleaved with a second graph on the same context, all bit-exact."""
+    import torch
+
+    ga = synth.complete_graph(300, seed=11)
+    gb = synth.complete_graph(260, seed=12)
+    na, nb = _graph(ga, ctx), _graph(gb, ctx)
+    cases = [(na, ga, np.arange(300, dtype=np.uint32), (0, 300)), (nb, gb, np.arange(260, dtype=np.uint32), (0, 260)),
+             (na, ga, np.arange(299, -1, -1, dtype=np.uint32)[::2].copy(), (10, 150)),
+             (na, ga, np.arange(300, dtype=np.uint32), (200, 300)), (nb, gb, np.arange(260, dtype=np.uint32), (5, 60))]
+    for net, g, used, (r0, r1) in cases:
+        nu = len(used)
+        dl = torch.zeros((r1 - r0) * nu, dtype=torch.int64, device="cuda")
+        df = torch.zeros((r1 - r0) * nu, dtype=torch.float32, device="cuda")
+        net.build_rows_device(used, r0, r1, dl.data_ptr(), df.data_ptr(), True)
+        rc, olat, oloss, _ = oracle.shortest_paths(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"],
+                                                   used, rows=(r0, r1), threads=8)
+        assert rc == 0
+        assert np.array_equal(dl.cpu().numpy().view(np.uint64).reshape(r1 - r0, nu), olat)
+        assert np.array_equal(df.cpu().numpy().reshape(r1 - r0, nu).view(np.uint32), oloss.view(np.uint32))
