@@ -740,7 +740,7 @@ def main():
                     fresh = NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
                     fresh.build_rows_device(used, b0, b1, bl.data_ptr(), bf.data_ptr(), True)
                     fresh.close()
-                ts.append(timed(D, one, 3, 1))
+                ts.append(timed(D, one, 5, 2))
             rank_blocks[str(N)] = {"rows_per_rank": per, "max_ms": round(max(ts) * 1e3, 4),
                                    "per_rank_ms": [round(t * 1e3, 4) for t in ts],
                                    "linear_ms": round(t_build / N * 1e3, 4),
