@@ -96,6 +96,14 @@ struct BkArgs {
   uint32_t* item_ctr;             // [claims, workgroups given up] (zeroed)
   uint32_t spin_max;
   int vec_out;
+  uint32_t arena_words, scr_stride;  // k_sssp_band: u32 per workgroup's arena, keys per scratch row
+  // k_sssp_band on the degree-class numbering (see k_band_classes): node ids of the used list in
+  // it (the search, the settled bitmap and the scratch row use them; `used` stays the graph's for
+  // the diagonal), the class table [first id x 17, first arc x 17] and the class-16 arc offsets
+  const uint32_t* used_key;
+  const uint32_t* cls;
+  const uint32_t* hi_off;
+  uint32_t npw;  // k_sssp_band: band nodes a wave settles per step (<= 64)
   unsigned long long* work;       // COUNT: relaxations
   unsigned long long* diag;       // COUNT: [buckets, entries appended, far steps, pops] summed
 };
@@ -698,6 +706,7 @@ constexpr uint32_t BD_CH = 1u << BD_CH_LOG;  // entries per chunk
 constexpr uint32_t BD_MAXCH = 8;            // chunks per bucket: 8,192 entries
 constexpr int BD_K = 8;                     // arc slots of 64 a wave reads per step
 constexpr int BD_G = 4;                     // entries a lane loads per step
+constexpr int BD_NCLS = 17;                 // degree classes: out-degree 0 .. 15, and 16 or more
 // A band's appends to a ring slot are staged in LDS, up to BD_E per slot, at their arena order, and
 // stored after the band as runs of consecutive entries (a few memory requests per slot instead
 // of one per entry); the rest, and far-list entries, are stored at once
@@ -764,6 +773,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
   const uint32_t ulim = HS - HS / 4;  // nodes a (sub-)band may hold: past it the band splits
   __shared__ uint32_t ctl[16];
   __shared__ uint32_t s_item;
+  __shared__ uint32_t s_cls[2 * BD_NCLS];  // degree classes: first internal id, first arc
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   uint8_t* ow = (uint8_t*)(smem + L.o_own) + wv * 64 * BD_K;
   constexpr uint32_t NONE = 0xFFFFFFFFu;
@@ -777,14 +787,15 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
   for (uint32_t i = tid; i < BK_SLOTS; i += NT) cnt[i] = 0;
   if (tid < 16) ctl[tid] = tid == FARMIN || tid == FARMIN + 1 ? NONE : 0u;
   for (uint32_t i = lane; i < 64 * BD_K; i += 64) ow[i] = 0;
-  const size_t ent0 = (size_t)blockIdx.x * a.nch * BD_CH * 3;
+  if (tid < 2 * BD_NCLS) s_cls[tid] = a.cls[tid];
+  const size_t ent0 = (size_t)blockIdx.x * a.arena_words;
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)(a.arena + ent0), 0,
                                                                       (int)(a.nch * BD_CH * 12u), 0x00020000);
-  unsigned long long* scr = a.scratch + (size_t)blockIdx.x * n;
+  unsigned long long* scr = a.scratch + (size_t)blockIdx.x * a.scr_stride;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)scr, 0, (int)(n * 8u), 0x00020000);
   const __amdgpu_buffer_rsrc_t arcs = __builtin_amdgcn_make_buffer_rsrc((void*)a.out_arc, 0, (int)(a.n_arcs * 12u),
                                                                         0x00020000);
-  const __amdgpu_buffer_rsrc_t roff = __builtin_amdgcn_make_buffer_rsrc((void*)a.out_off, 0, (int)((n + 1) * 4u),
+  const __amdgpu_buffer_rsrc_t roff = __builtin_amdgcn_make_buffer_rsrc((void*)a.hi_off, 0, (int)((n + 1) * 4u),
                                                                         0x00020000);
   if (tid == 0) s_item = atomicAdd(a.item_ctr, 1u);
   auto ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
@@ -924,7 +935,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
     const uint32_t bi = s_item;
     if (bi >= a.rows) break;
     row = a.row_begin + bi;
-    const uint32_t src = a.used[row];
+    const uint32_t src = a.used_key[row];  // (the degree-class id)
     for (uint32_t i = tid; i < nbw; i += NT) settled[i] = 0u;
     if (tid == 0) {  // PathProperties::default() at the source: band 0
       const uint32_t h = (src * 0x9E3779B1u) >> (32 - a.hs_log2);
@@ -998,74 +1009,96 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
       {
         const uint32_t U = ctl[UCNT];
         if (COUNT && tid == 0) n_pop += U;
-        for (uint32_t i0 = wv * 64; i0 < U; i0 += NT) {  // whole waves
+        const uint32_t npw = a.npw;  // band nodes per wave and step
+        for (uint32_t i0 = wv * npw; i0 < U; i0 += NW * npw) {  // whole waves
           const uint32_t i = i0 + lane;
-          const bool on = i < U;
+          const bool on = (uint32_t)lane < npw && i < U;
           const uint32_t x = on ? ulist[i] : 0u;
           const uint32_t u = on ? hid[x] : 0u;
           const uint64_t ku = on ? hkey[x] : 0ull;
           // the node's arc range: out_off[u], out_off[u + 1] in one 8-B load (one memory request, not two)
-          const auto ar = __builtin_amdgcn_raw_buffer_load_b64(roff, on ? u * 4u : 0x80000000u, 0, 0);
-          const uint32_t a0 = ar[0], a1 = ar[1];
+          // the node's arc range from its degree class, no memory round trip: class k < 16 holds the
+          // nodes of out-degree k, arcs first[k] .. in id order; class 16 (degree >= 16) reads its offsets
+          uint32_t k = 0;
+#pragma unroll
+          for (int c = 1; c < BD_NCLS; c++) k += u >= s_cls[c] ? 1u : 0u;
+          uint32_t a0 = s_cls[BD_NCLS + k] + (u - s_cls[k]) * k, a1 = a0 + k;
+          if (__builtin_amdgcn_ballot_w64(on && k == BD_NCLS - 1)) {
+            const bool hi = on && k == BD_NCLS - 1;
+            const auto ar = __builtin_amdgcn_raw_buffer_load_b64(roff, hi ? (u - s_cls[BD_NCLS - 1]) * 4u : 0x80000000u, 0, 0);
+            if (hi) {
+              a0 = ar[0];
+              a1 = ar[1];
+            }
+          }
+          if (!on) a0 = a1 = 0u;
           if (on) {
             atomicOr(&settled[u >> 5], 1u << (u & 31));
             hid[x] = HID_EMPTY;
             hkey[x] = KINF;
-            __builtin_amdgcn_raw_buffer_store_b64(
-                (uint32_t __attribute__((ext_vector_type(2)))){(uint32_t)ku, (uint32_t)(ku >> 32)}, rs, u * 8u, 0,
-                BD_SCR_POL);
           }
           const unsigned long long q0 = wclk();
           const uint32_t deg = a1 - a0;
-          __builtin_amdgcn_s_waitcnt(0);
+          if (COUNT) __builtin_amdgcn_s_waitcnt(0);  // (diagnostics: the offsets are in)
           const unsigned long long q1 = wclk();
           if (COUNT) wc[0] += q1 - q0;
-          const uint32_t incl = wave_incl_sum(deg);
-          const uint32_t base = incl - deg;
-          const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
-          if (COUNT) n_rel += T;
-          uint32_t carry = 0;  // 1 + the owner lane of the previous slot
-          for (uint32_t t0 = 0; t0 < T; t0 += 64 * BD_K) {
-            // owner lane of each slot: heads scatter 1 + their lane at their first slot, a max-scan fills the rest
-            if (deg && base >= t0 && base - t0 < 64u * BD_K) ow[base - t0] = (uint8_t)(lane + 1);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            uint32_t o[BD_K];
+          // arcs [ea0, ea0 + edeg) of each lane's node, arc-parallel: the wave's arcs in consecutive
+          // slots, KX chunks of 64 at once, consecutive lanes on consecutive arcs of a node
+          auto expand = [&](auto kx, uint32_t ea0, uint32_t edeg) {
+            constexpr int KX = decltype(kx)::value;
+            const uint32_t incl = wave_incl_sum(edeg);
+            const uint32_t base = incl - edeg;
+            const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+            if (COUNT) n_rel += T;
+            uint32_t carry = 0;  // 1 + the owner lane of the previous slot
+            for (uint32_t t0 = 0; t0 < T; t0 += 64 * KX) {
+              // owner lane of each slot: heads scatter 1 + their lane at their first slot, a max-scan fills the rest
+              if (edeg && base >= t0 && base - t0 < 64u * KX) ow[base - t0] = (uint8_t)(lane + 1);
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+              uint32_t o[KX];
 #pragma unroll
-            for (int c = 0; c < BD_K; c++) {
-              const uint32_t hd = ow[c * 64 + lane];
-              ow[c * 64 + lane] = 0;
-              const uint32_t mx = max(wave_incl_max(hd), carry);
-              carry = __builtin_amdgcn_readlane(mx, 63);
-              o[c] = mx - 1;
-            }
-            uint32_t v[BD_K], s[BD_K];
-            uint64_t cd[BD_K];
+              for (int c = 0; c < KX; c++) {
+                const uint32_t hd = ow[c * 64 + lane];
+                ow[c * 64 + lane] = 0;
+                const uint32_t mx = max(wave_incl_max(hd), carry);
+                carry = __builtin_amdgcn_readlane(mx, 63);
+                o[c] = mx - 1;
+              }
+              uint32_t v[KX], s[KX];
+              uint64_t cd[KX];
 #pragma unroll
-            for (int c = 0; c < BD_K; c++) {
-              const uint32_t sl = t0 + c * 64 + lane;
-              const bool valid = sl < T;
-              const uint32_t ai = __shfl(a0, (int)o[c]) + sl - __shfl(base, (int)o[c]);
-              const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid ? ai * 12u : 0x80000000u, 0, BD_ARC_POL);
-              const uint32_t klo = __shfl((uint32_t)ku, (int)o[c]), khi = __shfl((uint32_t)(ku >> 32), (int)o[c]);
-              v[c] = r[0];
-              cd[c] = valid ? relax32(((uint64_t)khi << 32) | klo, r[1], __uint_as_float(r[2])) : KINF;
-            }
+              for (int c = 0; c < KX; c++) {
+                const uint32_t sl = t0 + c * 64 + lane;
+                const bool valid = sl < T;
+                const uint32_t ai = __shfl(ea0, (int)o[c]) + sl - __shfl(base, (int)o[c]);
+                const auto r = __builtin_amdgcn_raw_buffer_load_b96(arcs, valid ? ai * 12u : 0x80000000u, 0, BD_ARC_POL);
+                const uint32_t klo = __shfl((uint32_t)ku, (int)o[c]), khi = __shfl((uint32_t)(ku >> 32), (int)o[c]);
+                v[c] = r[0];
+                cd[c] = valid ? relax32(((uint64_t)khi << 32) | klo, r[1], __uint_as_float(r[2])) : KINF;
+              }
 #pragma unroll
-            for (int c = 0; c < BD_K; c++) {
-              const uint32_t lat = key_lat(cd[c]);
-              const bool live = lat != LAT32_SAT && !is_settled(v[c]);
-              s[c] = live ? slot_of(bk_bucket(lat, a.delta, a.dmul), b, far) : NONE;
+              for (int c = 0; c < KX; c++) {
+                const uint32_t lat = key_lat(cd[c]);
+                const bool live = lat != LAT32_SAT && !is_settled(v[c]);
+                s[c] = live ? slot_of(bk_bucket(lat, a.delta, a.dmul), b, far) : NONE;
+              }
+              const unsigned long long q2 = wclk();
+              append(std::integral_constant<int, KX>(), s, v, cd, true);
+              if (COUNT) wc[2] += wclk() - q2;
             }
-            const unsigned long long q2 = wclk();
-            append(std::integral_constant<int, BD_K>(), s, v, cd, true);
-            if (COUNT) {
-              const unsigned long long q3 = wclk();
-              wc[1] += q2 - q1;
-              wc[2] += q3 - q2;
-            }
-          }
+          };
+          // (a lane walking its own node's first 8 arcs, with the rest arc-parallel as k_sssp_lds does,
+          // measured slower here: 71.1 against 61.7 ms at 12,800 C5 rows, r8a -- 64 lines per load)
+          expand(std::integral_constant<int, BD_K>(), a0, deg);
+          if (COUNT) wc[1] += wclk() - q1;
+          // the settled key to the scratch row, after the node's arcs (before them, or with a full wait
+          // after the offsets as before r8, measured the same: 61.5-61.6 ms, r8c)
+          if (on)
+            __builtin_amdgcn_raw_buffer_store_b64(
+                (uint32_t __attribute__((ext_vector_type(2)))){(uint32_t)ku, (uint32_t)(ku >> 32)}, rs, u * 8u, 0,
+                BD_SCR_POL);
         }
       }
       if (E) __syncthreads();  // every append staged
@@ -1167,7 +1200,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
     {
       const size_t orow = (size_t)(row - a.row_begin) * a.n_used;
       bool sat = false;
-      const uint32_t de = a.self_edge[src];
+      const uint32_t de = a.self_edge[a.used[row]];
       const uint64_t d_lat = a.e_lat[de];
       const float d_loss = a.e_loss[de];
       auto cell = [&](uint32_t j, uint32_t vj, uint64_t kk, uint64_t& l, float& f) {
@@ -1180,7 +1213,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
       if (a.vec_out) {
         typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
         typedef float f32x4 __attribute__((ext_vector_type(4)));
-        const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc((void*)a.used, 0, (int)(a.n_used * 4u),
+        const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc((void*)a.used_key, 0, (int)(a.n_used * 4u),
                                                                             0x00020000);
         for (uint32_t j = tid * 4; j < a.n_used; j += NT * 4) {
           const auto uv = __builtin_amdgcn_raw_buffer_load_b128(ru, j * 4u, 0, 0);
@@ -1200,7 +1233,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
         }
       } else {
         for (uint32_t j = tid; j < a.n_used; j += NT) {
-          const uint32_t vj = a.used[j];
+          const uint32_t vj = a.used_key[j];
           const auto xx = __builtin_amdgcn_raw_buffer_load_b64(rs, vj * 8u, 0, BK_SC1);
           uint64_t l;
           float f;
@@ -1218,6 +1251,117 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
     }
   }
 wave_exit:;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The degree-class numbering of a graph for k_sssp_band (built once per sg_net, kept in the
+// context's workspace): nodes sorted by out-degree class (0 .. 15, and 16 or more), in node order
+// within a class, and the out-arcs laid out in that order.  A node's arc range is then arithmetic
+// -- class k < 16 starts at arc first_arc[k], node i of it at first_arc[k] + i k -- so the search
+// settles a node without reading its offsets; class 16 keeps an offsets array.  Measured at C5
+// (12,800 rows): 60.9-61.0 against 61.5 ms (profiles/r05/ab_c5_band_classes_r8f.txt).  (A wrong-
+// table diagnostic with no offsets load and every degree 8 ran 9 % faster, ab_c5_band_offsets_r8e.txt:
+// most of that came from equal degrees -- one step of arc slots per wave, see BkArgs::npw.)
+constexpr uint32_t BC_T = 1024;
+__global__ void __launch_bounds__(BC_T) k_band_classes(const uint32_t* __restrict__ out_off, uint32_t n,
+                                                       uint32_t* __restrict__ perm, uint32_t* __restrict__ nbase,
+                                                       uint32_t* __restrict__ hi_off, uint32_t* __restrict__ cls) {
+  __shared__ uint32_t cnt[BD_NCLS][BC_T];  // per thread: nodes of each class in its node range
+  __shared__ uint32_t hdeg[BC_T];           // per thread: arcs of its class-16 nodes
+  __shared__ uint32_t wsum[BD_NCLS + 1][BC_T / 64];
+  __shared__ uint32_t first[BD_NCLS + 1], farc[BD_NCLS + 1];
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t per = (n + BC_T - 1) / BC_T, v0 = min(n, t * per), v1 = min(n, v0 + per);
+  for (int k = 0; k < BD_NCLS; k++) cnt[k][t] = 0;
+  uint32_t hs = 0;
+  for (uint32_t v = v0; v < v1; v++) {
+    const uint32_t d = out_off[v + 1] - out_off[v];
+    const uint32_t k = min(d, (uint32_t)BD_NCLS - 1);
+    cnt[k][t]++;
+    if (k == BD_NCLS - 1) hs += d;
+  }
+  hdeg[t] = hs;
+  // exclusive scans over the threads, per class and of the class-16 arcs (row BD_NCLS)
+  uint32_t ex[BD_NCLS + 1];
+#pragma unroll
+  for (int k = 0; k <= BD_NCLS; k++) {
+    const uint32_t x = k < BD_NCLS ? cnt[k][t] : hdeg[t];
+    const uint32_t inc = wave_incl_sum(x);
+    ex[k] = inc - x;
+    if (lane == 63) wsum[k][wv] = inc;
+  }
+  __syncthreads();
+  if (t <= BD_NCLS) {  // wave totals -> wave offsets, in place; the class totals
+    uint32_t acc = 0;
+    for (uint32_t w = 0; w < BC_T / 64; w++) {
+      const uint32_t x = wsum[t][w];
+      wsum[t][w] = acc;
+      acc += x;
+    }
+    first[t] = acc;  // (for now: the total)
+  }
+  __syncthreads();
+  if (t == 0) {
+    uint32_t id = 0, arc = 0;
+    for (int k = 0; k < BD_NCLS; k++) {
+      const uint32_t c = first[k];
+      first[k] = id;
+      farc[k] = arc;
+      id += c;
+      arc += k < BD_NCLS - 1 ? c * (uint32_t)k : first[BD_NCLS];  // class 16: its arcs' total
+    }
+    first[BD_NCLS] = id;  // = n
+    farc[BD_NCLS] = arc;  // = the arcs
+  }
+  __syncthreads();
+  uint32_t pos[BD_NCLS];
+#pragma unroll
+  for (int k = 0; k < BD_NCLS; k++) pos[k] = first[k] + wsum[k][wv] + ex[k];
+  uint32_t hp = farc[BD_NCLS - 1] + wsum[BD_NCLS][wv] + ex[BD_NCLS];
+  for (uint32_t v = v0; v < v1; v++) {
+    const uint32_t d = out_off[v + 1] - out_off[v];
+    const uint32_t k = min(d, (uint32_t)BD_NCLS - 1);
+    uint32_t id = 0;
+#pragma unroll
+    for (int c = 0; c < BD_NCLS; c++)
+      if ((uint32_t)c == k) id = pos[c]++;
+    perm[v] = id;
+    if (k < BD_NCLS - 1) {
+      nbase[v] = farc[k] + (id - first[k]) * k;
+    } else {
+      hi_off[id - first[BD_NCLS - 1]] = hp;
+      nbase[v] = hp;
+      hp += d;
+    }
+  }
+  if (t == 0) hi_off[first[BD_NCLS] - first[BD_NCLS - 1]] = farc[BD_NCLS];
+  if (t < BD_NCLS) {
+    cls[t] = first[t];
+    cls[BD_NCLS + t] = farc[t];
+  }
+}
+
+// the out-arcs in the degree-class order, heads renumbered (one thread per node)
+__global__ void k_band_arcs(const uint32_t* __restrict__ out_off, const uint32_t* __restrict__ out_arc, uint32_t n,
+                            const uint32_t* __restrict__ perm, const uint32_t* __restrict__ nbase,
+                            uint32_t* __restrict__ arc) {
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
+    const uint32_t a0 = out_off[v], d = out_off[v + 1] - a0, b = nbase[v];
+    for (uint32_t j = 0; j < d; j++) {
+      const uint32_t* r = out_arc + (size_t)(a0 + j) * 3;
+      uint32_t* w = arc + (size_t)(b + j) * 3;
+      w[0] = perm[r[0]];
+      w[1] = r[1];
+      w[2] = r[2];
+    }
+  }
+}
+
+// a used list in the degree-class numbering
+__global__ void k_band_used(const uint32_t* __restrict__ used, uint32_t n_used, const uint32_t* __restrict__ perm,
+                            uint32_t* __restrict__ out) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n_used; j += gridDim.x * blockDim.x)
+    out[j] = perm[used[j]];
 }
 
 // The launch shape (env knobs are for tests and A/B runs): threads per workgroup (SG_BUCKET_THREADS:
@@ -1352,20 +1496,55 @@ static void launch_sssp_band(sg_ctx* ctx, sg_net* net, BkArgs a, uint32_t n_used
   // rows per CU), 45.8 ms without; profiles/r05/ab_band_stage.txt): the kernel is bound by the
   // texture-address unit's lane accesses, not by write requests
   a.stg_cap = (uint32_t)std::max(0, std::min((int)BD_E_MAX, bk_env("SG_BUCKET_STAGE", 0)));
+  // band nodes per wave: about 448 arcs, so that a wave's arcs nearly always fit one step of
+  // BD_K x 64 slots (C5, mean out-degree 8: 56 nodes, 59.8 against 61.2 ms at 64 for 12,800
+  // rows; 48: 60.8, 40: 62.7; profiles/r05/ab_c5_band_npw_r8g.txt); SG_BAND_NPW overrides
+  const double mdeg = (double)net->n_arcs / std::max(1u, n);
+  a.npw = (uint32_t)std::max(1, std::min(64, bk_env("SG_BAND_NPW", (int)std::max(16.0, std::min(64.0, 448.0 / std::max(mdeg, 1.0))))));
   const size_t lds = BdLds(n, 1u << a.hs_log2, a.nch, 4, a.stg_cap).bytes;
   if (lds + 256 > 160 * 1024) throw Error(SG_ERR_INVALID_ARG, "graph too large for the banded search");
   const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>((size_t)bk_env("SG_BUCKET_PER_CU", 8),
                                                                          (160 * 1024) / (lds + 256)));
   const uint32_t grid = (uint32_t)ctx->n_cu * per_cu;
+  // the graph in the degree-class numbering: built once per sg_net (the workspace remembers its
+  // owner, as sg_dense.hip's sorted arcs); the used list mapped every build
+  {
+    const size_t arc_w = (size_t)net->n_arcs * 3, words = arc_w + 3 * ((size_t)n + 1) + 2 * BD_NCLS + n_used;
+    const bool fresh = ctx->band_owner != net->serial || ctx->r_band.cap < words * 4;
+    uint32_t* w = ctx->r_band.get<uint32_t>(words);
+    uint32_t* barc = w;
+    uint32_t* perm = barc + arc_w;
+    uint32_t* nbase = perm + n + 1;
+    uint32_t* hi = nbase + n + 1;
+    uint32_t* cls = hi + n + 1;
+    uint32_t* ukey = cls + 2 * BD_NCLS;
+    if (fresh) {
+      ctx->band_owner = 0;
+      TimedLaunch tl(ctx, "band_classes", 0.0);
+      hipLaunchKernelGGL(k_band_classes, dim3(1), dim3(BC_T), 0, st, net->out_off, n, perm, nbase, hi, cls);
+      hipLaunchKernelGGL(k_band_arcs, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, net->out_off, net->out_arc, n,
+                         perm, nbase, barc);
+      SG_CHECK_LAUNCH();
+      ctx->band_owner = net->serial;
+    }
+    hipLaunchKernelGGL(k_band_used, dim3(grid_for(std::max(n_used, 1u), 256, 1024)), dim3(256), 0, st, a.used, n_used,
+                       perm, ukey);
+    a.out_arc = barc;
+    a.hi_off = hi;
+    a.cls = cls;
+    a.used_key = ukey;
+  }
   uint32_t* ctr = ctx->r_items.get<uint32_t>(2);
   SG_HIP(hipMemsetAsync(ctr, 0, 8, st));
-  const size_t arena_b = (size_t)grid * a.nch * BD_CH * 12, scr_b = (size_t)grid * n * 8;
+  // per-workgroup strides (skewing them by 4-33 KB measured the same, r8d)
+  a.arena_words = a.nch * BD_CH * 3;
+  a.scr_stride = n;
+  const size_t arena_b = ((size_t)grid * a.arena_words * 4 + 255) / 256 * 256, scr_b = (size_t)grid * a.scr_stride * 8;
   char* wsp = ctx->r_bucket.get<char>(arena_b + scr_b);
   a.arena = (uint32_t*)wsp;
   a.scratch = (unsigned long long*)(wsp + arena_b);
   a.item_ctr = ctr;
   (void)rows;
-  (void)n_used;
   auto go = [&](auto kern) {
     SG_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, a);

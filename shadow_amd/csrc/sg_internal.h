@@ -94,6 +94,7 @@ struct sg_ctx {
   uint64_t pair_count_cells = 0;
   uint64_t net_serial = 0;   // the last sg_net serial handed out
   uint64_t dense_owner = 0;  // the net whose arcs r_dense holds sorted (0: none)
+  uint64_t band_owner = 0;   // the net whose degree-class numbering r_band holds (0: none)
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   int n_cu = 256;
@@ -101,7 +102,7 @@ struct sg_ctx {
   uint32_t err_row = 0, err_col = 0;
   // routing workspace
   sg::DevBuf r_dist, r_dist2, r_flags, r_used, r_err, r_self, r_pair_cnt, r_pair_edge, r_map, r_out_lat,
-      r_out_loss, r_misc, r_dirty, r_work, r_items, r_plan, r_dense, r_done, r_bucket;
+      r_out_loss, r_misc, r_dirty, r_work, r_items, r_plan, r_dense, r_done, r_bucket, r_band;
   // delivery workspace
   sg::DevBuf d_seg, d_dst, d_cnt, d_cur, d_keys, d_vals, d_keys2, d_vals2, d_keys3, d_keys4, d_misc,
       d_scan, d_lists, d_lists2, d_ctr0, d_blk, d_spill;

@@ -1610,7 +1610,7 @@ static void shortest_paths_bucket(sg_ctx* ctx, sg_net* net, const uint32_t* d_us
               total / rows / std::max(1u, net->n_arcs));
       fprintf(stderr, "[bucket] cycles per bucket (thread 0): phase 0 %.0f, phase 1 %.0f, phase 2 %.0f; output per row %.0f\n",
               d[4] / nb, d[5] / nb, d[6] / nb, d[7] / (double)rows);
-      fprintf(stderr, "[bucket] band kernel, wave 0 per bucket: offsets %.0f, arcs %.0f, appends %.0f, store wait %.0f; "
+      fprintf(stderr, "[bucket] band kernel, wave 0 per bucket: offsets %.0f, arcs (with appends) %.0f, appends %.0f, store wait %.0f; "
               "band splits per row %.2f\n", d[9] / nb, d[10] / nb, d[11] / nb, d[12] / nb, d[15] / (double)rows);
       const double ncl = std::max(1.0, (double)d[8]);
       fprintf(stderr, "[bucket] per wave and bucket: load step %.0f cyc, idle %.0f; per claim: to offsets %.0f, to "

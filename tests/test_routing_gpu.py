@@ -520,7 +520,8 @@ def test_dense_graph_cases(oracle, ctx, case, request):
                                  {"SG_BUCKET_STAGE": "0"}, {"SG_BUCKET_STAGE": "40", "SG_BUCKET_DELTA": "30000000"},
                                  {"SG_BUCKET_THREADS": "1024"}, {"SG_BUCKET_THREADS": "1024", "SG_BUCKET_DELTA": "30000000"},
                                  {"SG_BUCKET_MODE": "queue"}, {"SG_BUCKET_MODE": "queue", "SG_BUCKET_RING": "2"},
-                                 {"SG_BUCKET_MODE": "queue", "SG_BUCKET_HASH": "6"}])
+                                 {"SG_BUCKET_MODE": "queue", "SG_BUCKET_HASH": "6"}, {"SG_BAND_NPW": "5"},
+                                 {"SG_BAND_NPW": "64", "SG_BUCKET_HASH": "7"}])
 def test_bucket_search_knobs(oracle, ctx, monkeypatch, env, apsp_kernel):
     """The bucketed search (sg_bucket.hip) under its knobs, on a tie-heavy lossy graph (10-ms arc
     latencies), directed and undirected, a used subset: exact bands (k_sssp_band: the default
@@ -530,7 +531,8 @@ def test_bucket_search_knobs(oracle, ctx, monkeypatch, env, apsp_kernel):
     back by far steps), entries stored straight to the arena (no LDS staging) or overflowing a
     40-entry staging array, and its safety valves -- a 64-slot hash that fills and arenas of 4 and 6
     chunks that run out: the row gives up, the workgroup leaves, and the wide kernel redoes the
-    row (the output starts poisoned, so no row passes by holding an earlier table)."""
+    row (the output starts poisoned, so no row passes by holding an earlier table); and the banded
+    search's nodes per wave (5: many steps per band; 64 with band splits)."""
     if apsp_kernel != "bucket":
         pytest.skip("bucketed-search knobs")
     for k, v in env.items():
@@ -541,6 +543,41 @@ def test_bucket_search_knobs(oracle, ctx, monkeypatch, env, apsp_kernel):
         g["loss"] = np.where(np.arange(len(g["loss"])) % 3 == 0, np.float32(0.05), g["loss"]).astype(np.float32)
         used = np.random.default_rng(41).permutation(700)[:500].astype(np.uint32)
         _check(oracle, g, used, ctx, poison=True)
+
+
+def test_band_degree_classes(oracle, ctx, monkeypatch):
+    """The banded search on its degree-class numbering (sg_bucket.hip k_band_classes): nodes of
+    every out-degree class -- hubs of degree 30-60 (class 16, whose arc offsets are read), nodes
+    of degree 1 .. 15, and isolated unused nodes (degree 0) -- directed and undirected, a used
+    subset in shuffled order, two graphs interleaved on one context (the numbering is cached per
+    graph) and a row block; every cell against the oracle."""
+    monkeypatch.setenv("SG_APSP_LDS", "1")
+    monkeypatch.setenv("SG_APSP_BUCKET", "1")
+    rng = np.random.default_rng(53)
+    graphs = []
+    for directed in (False, True):
+        g = synth.ring_chords_graph(640, 4.0, seed=53 + directed, directed=directed, parallel=0.05)
+        n0 = g["n"]
+        hubs = rng.choice(n0, 6, replace=False)
+        src, dst = [g["src"]], [g["dst"]]
+        for h in hubs:
+            k = int(rng.integers(30, 61))
+            t = rng.choice(n0, k, replace=False)
+            t = t[t != h]
+            src.append(np.full(len(t), h, dtype=g["src"].dtype))
+            dst.append(t.astype(g["dst"].dtype))
+        iso = np.arange(n0, n0 + 10, dtype=g["src"].dtype)  # self-loops only: out-degree 0
+        src.append(iso)
+        dst.append(iso)
+        m = sum(len(x) for x in src) - len(g["src"])
+        g = dict(g, n=n0 + 10, src=np.concatenate(src), dst=np.concatenate(dst),
+                 lat=np.concatenate([g["lat"], rng.integers(10**6, 9 * 10**7, m).astype(np.uint64)]),
+                 loss=np.concatenate([g["loss"], np.where(rng.random(m) < 0.5, 0.0, 0.01).astype(np.float32)]))
+        graphs.append(g)
+    used = rng.permutation(640)[:500].astype(np.uint32)
+    for g in graphs + graphs:
+        _check(oracle, g, used, ctx)
+    _check(oracle, graphs[0], used, ctx, rows=(100, 260), poison=True)
 
 
 def test_dense_sorted_arcs_per_graph(oracle, ctx):

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--variants", default="")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--no-check", action="store_true", help="timing diagnostics: tables may differ")
     a = ap.parse_args()
     import torch
 
@@ -64,7 +65,7 @@ def main():
                 else:
                     same = torch.equal(lat, ref[0]) and torch.equal(loss.view(torch.int32), ref[1].view(torch.int32))
                     print(f"variant {v!r}: table {'identical' if same else 'DIFFERS'}", flush=True)
-                    assert same, v
+                    assert same or a.no_check, v
             print(f"round {r} variant {v!r}: {times[v][-1]:9.3f} ms/build", flush=True)
     for v in variants:
         set_env(v + " SG_BUCKET_DIAG=1")
