@@ -1016,7 +1016,6 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
           const uint32_t x = on ? ulist[i] : 0u;
           const uint32_t u = on ? hid[x] : 0u;
           const uint64_t ku = on ? hkey[x] : 0ull;
-          // the node's arc range: out_off[u], out_off[u + 1] in one 8-B load (one memory request, not two)
           // the node's arc range from its degree class, no memory round trip: class k < 16 holds the
           // nodes of out-degree k, arcs first[k] .. in id order; class 16 (degree >= 16) reads its offsets
           uint32_t k = 0;
@@ -1090,7 +1089,9 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
             }
           };
           // (a lane walking its own node's first 8 arcs, with the rest arc-parallel as k_sssp_lds does,
-          // measured slower here: 71.1 against 61.7 ms at 12,800 C5 rows, r8a -- 64 lines per load)
+          // measured slower here: 71.1 against 61.7 ms at 12,800 C5 rows, r8a -- 64 lines per load.
+          // Reading bucket b + 1's first entries behind the arc loads, for the next load step: 56.2
+          // against 54.5 ms, r8i -- that step is its hash inserts and the barrier, not the loads)
           expand(std::integral_constant<int, BD_K>(), a0, deg);
           if (COUNT) wc[1] += wclk() - q1;
           // the settled key to the scratch row, after the node's arcs (before them, or with a full wait
