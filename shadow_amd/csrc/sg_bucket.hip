@@ -815,6 +815,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
   unsigned long long cyc[4] = {0, 0, 0, 0};  // COUNT, thread 0: cycles in load, relax, next, output
   unsigned long long t_mark = 0;
   unsigned long long wc[4] = {0, 0, 0, 0};  // COUNT, thread 0: relax sub-steps (offsets, arcs, appends, store wait)
+  unsigned long long wl[3] = {0, 0, 0};     // COUNT, thread 0: load sub-steps (entry loads, hash, barrier wait)
   auto wclk = [&]() -> unsigned long long { return COUNT ? clock64() : 0ull; };
   auto stamp = [&](int k) {
     if (COUNT && tid == 0) {
@@ -959,6 +960,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
         for (uint32_t q = tid; q < R; q += NT) cst[q] = cnt[q];
       {
         const uint32_t sb = b & rmask, c = cnt[sb];
+        unsigned long long l0 = wclk();
         for (uint32_t i0 = tid; i0 < c; i0 += NT * BD_G) {
           uint32_t v[BD_G];
           uint64_t key[BD_G];
@@ -972,6 +974,16 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
             v[g] = on && (uint64_t)r[1] < sub_hi ? r[0] : NONE;  // (past the sub-band: a later pass)
             key[g] = ((uint64_t)r[1] << 32) | r[2];
           }
+          if (COUNT) {
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long l1 = wclk();
+            wl[0] += l1 - l0;
+            l0 = l1;
+          }
+          // (the thread's BD_G entries hashed together -- settled filter, first probes, CASes in flight at
+          // once, one UCNT add per wave -- with the appends' chunk-id reads batched the same way measured
+          // slower: 60.7 against 59.6 ms, r8l; the load step's hash time rose 6.2k -> 7.2k cycles: the
+          // LDS pipe, shared by four rows, not the round trips, sets it)
           uint32_t x[BD_G];
 #pragma unroll
           for (int g = 0; g < BD_G; g++) {
@@ -983,9 +995,17 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
             if (x[g] < HS)
               (void)__hip_atomic_fetch_min(&hkey[x[g]], (unsigned long long)key[g], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (COUNT) {
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long l1 = wclk();
+            wl[1] += l1 - l0;
+            l0 = l1;
+          }
         }
+        if (COUNT) l0 = wclk();
+        __syncthreads();
+        if (COUNT) wl[2] += wclk() - l0;
       }
-      __syncthreads();
       stamp(0);
       if (ld(&ctl[ABORT])) goto wave_exit;
       if (ld(&ctl[OVF])) {  // (uniform) too many nodes: the lower half of the (sub-)band again
@@ -1190,11 +1210,15 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
           atomicAdd(&a.diag[3], n_pop);
           for (int k = 0; k < 3; k++) atomicAdd(&a.diag[4 + k], cyc[k]);
           for (int k = 0; k < 4; k++) atomicAdd(&a.diag[9 + k], wc[k]);
+          atomicAdd(&a.diag[8], wl[0]);
+          atomicAdd(&a.diag[13], wl[1]);
+          atomicAdd(&a.diag[14], wl[2]);
         }
       }
     }
     n_rel = n_app = n_bk = n_far = n_pop = 0;
     for (int k = 0; k < 4; k++) cyc[k] = wc[k] = 0;
+    wl[0] = wl[1] = wl[2] = 0;
     stamp(-1);
     // ---- write the row (as k_sssp_bucket)
     if (tid == 0) s_item = atomicAdd(a.item_ctr, 1u);

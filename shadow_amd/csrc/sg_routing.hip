@@ -1612,6 +1612,8 @@ static void shortest_paths_bucket(sg_ctx* ctx, sg_net* net, const uint32_t* d_us
               d[4] / nb, d[5] / nb, d[6] / nb, d[7] / (double)rows);
       fprintf(stderr, "[bucket] band kernel, wave 0 per bucket: offsets %.0f, arcs (with appends) %.0f, appends %.0f, store wait %.0f; "
               "band splits per row %.2f\n", d[9] / nb, d[10] / nb, d[11] / nb, d[12] / nb, d[15] / (double)rows);
+      fprintf(stderr, "[bucket] band kernel, thread 0 per bucket in the load step: entry loads %.0f, hash %.0f, barrier wait %.0f\n",
+              d[8] / nb, d[13] / nb, d[14] / nb);
       const double ncl = std::max(1.0, (double)d[8]);
       fprintf(stderr, "[bucket] per wave and bucket: load step %.0f cyc, idle %.0f; per claim: to offsets %.0f, to "
               "arcs %.0f (sum over arc rounds), appends %.0f, claim total %.0f\n", d[9] / nb / 4, d[14] / nb / 4,

@@ -1,14 +1,14 @@
 set -u
-O=gpurun_out/r8j; mkdir -p $O
-export TMPDIR=/tmp
-for l in base wnt wb0 wb1 wb2 wb16 wb17; do
-  if [ $l = base ]; then L=shadow_amd/libshadow_gpu.so; else L=tools/ab/libshadow_gpu_$l.so; fi
-  [ -f $L ] || { echo missing $L; exit 1; }
-  SHADOW_GPU_LIB=$L timeout -k 10 120 python3 -u tools/round_c4.py > $O/t_$l.log 2>&1 || { tail -5 $O/t_$l.log; exit 1; }
-  SHADOW_GPU_LIB=$L timeout -s KILL 120 rocprofv3 --kernel-include-regex k_walk --pmc FETCH_SIZE --output-format csv -d $O/p_$l -o run -- python3 tools/round_c4.py > $O/p_$l.log 2>&1 || { echo "pmc $l failed"; tail -5 $O/p_$l.log; exit 1; }
-  F=$(python3 -c "
-import csv,glob
-v=[float(r['Counter_Value']) for f in glob.glob('$O/p_$l/**/*counter_collection.csv',recursive=True) for r in csv.DictReader(open(f)) if r['Counter_Name']=='FETCH_SIZE']
-print(round(sum(v)/len(v)), len(v))")
-  echo "$l: $(grep round $O/t_$l.log) fetch_kb $F"
+O=gpurun_out/r8l; mkdir -p $O
+[ -f tools/ab/libshadow_gpu_head.so ] || { echo missing lib; exit 1; }
+timeout -k 10 600 python3 -u -m pytest tests/test_routing_gpu.py tests/test_routing_fuzz_gpu.py -x -q --timeout 300 --timeout-method thread -k "bucket or band_degree" > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
+tail -1 $O/t.log
+for r in 0 1; do
+  for l in head new; do
+    if [ $l = new ]; then L=shadow_amd/libshadow_gpu.so; else L=tools/ab/libshadow_gpu_$l.so; fi
+    SHADOW_GPU_LIB=$L timeout -k 10 300 python3 -u tools/apsp_ab.py --rows 12800 --rounds 2 --variants "SG_APSP_BUCKET=1" > $O/$l$r.log 2>&1 || { tail -30 $O/$l$r.log; exit 1; }
+    echo "$l: $(grep median $O/$l$r.log)"
+  done
 done
+SG_BUCKET_DIAG=1 timeout -k 10 300 python3 -u tools/apsp_ab.py --rows 12800 --rounds 1 --variants "SG_APSP_BUCKET=1" > $O/diag.log 2>&1 || { tail -30 $O/diag.log; exit 1; }
+grep -E "bucket\]" $O/diag.log
