@@ -8,6 +8,8 @@ O=gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread --durations=15 > $O/gpu_tests.log 2>&1
 rc=$?; tail -2 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
 timeout -k 10 600 python3 -u bench.py > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
 tail -c 300 $O/bench.json
 bash tools/profile_round.sh $TAG || exit 1
