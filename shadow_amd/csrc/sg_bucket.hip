@@ -980,6 +980,9 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
             wl[0] += l1 - l0;
             l0 = l1;
           }
+          // (Two buckets per load step -- both lists into the hash, bucket b relaxed with its candidates
+          // for bucket b + 1 inserted, then bucket b + 1 -- measured slower, 74.1 against 59.7 ms, r8q: the
+          // load step's hash time grew 6.1k -> 25.9k cycles for twice the entries.)
           // (the thread's BD_G entries hashed together -- settled filter, first probes, CASes in flight at
           // once, one UCNT add per wave -- with the appends' chunk-id reads batched the same way measured
           // slower: 60.7 against 59.6 ms, r8l; the load step's hash time rose 6.2k -> 7.2k cycles: the
