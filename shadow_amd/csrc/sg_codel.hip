@@ -1423,17 +1423,24 @@ __global__ void __launch_bounds__(CD_THREADS) k_outbound(OutboundArgs a) {
 }
 
 // Exclusive prefix of the k_outbound blocks' sent counts (blk[2b]) -> boff[b]:
-// where each block's slice of the sent batch starts.  One block.
+// where each block's slice of the sent batch starts; and k_codel_reduce's sums
+// (the total sent, the error flags) into the mapped return block, in the same
+// launch.  One block.
 __global__ void __launch_bounds__(1024) k_blk_offsets(const unsigned long long* __restrict__ blk, uint32_t nb,
-                                                      uint32_t* __restrict__ boff) {
+                                                      uint32_t* __restrict__ boff,
+                                                      const uint32_t* __restrict__ group_err,
+                                                      unsigned long long* __restrict__ ret) {
   __shared__ uint32_t wsum[16];
+  __shared__ unsigned long long esum[16];
   __shared__ uint32_t carry;
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   if (t == 0) carry = 0;
   __syncthreads();
+  unsigned long long e = 0;
   for (uint32_t c0 = 0; c0 < nb; c0 += 1024) {
     const uint32_t i = c0 + t;
     const uint32_t v = i < nb ? (uint32_t)blk[2 * i] : 0;
+    if (i < nb) e |= blk[2 * i + 1];
     uint32_t x = v;  // inclusive wave scan
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = __shfl_up(x, d, 64);
@@ -1447,6 +1454,14 @@ __global__ void __launch_bounds__(1024) k_blk_offsets(const unsigned long long* 
     __syncthreads();
     if (t == 1023) carry = before + x;
     __syncthreads();
+  }
+  for (int s = 32; s > 0; s >>= 1) e |= __shfl_xor(e, s, 64);
+  if (lane == 0) esum[wv] = e;
+  __syncthreads();
+  if (t == 0) {
+    for (int w = 1; w < 16; w++) e |= esum[w];
+    ret[0] = carry;  // the sent total (k_codel_reduce's sum)
+    ret[1] = e | *group_err;
   }
 }
 
@@ -2105,14 +2120,15 @@ int32_t sg_outbound_run(sg_ctx* ctx, sg_outbound* ob, const sg_outbound_sends* s
         lm == 2 ? go(k_outbound<false, 2>) : lm == 1 ? go(k_outbound<false, 1>) : go(k_outbound<false, 0>);
     }
     lane_diag_report(st, "k_outbound", a.bdiag, nb);
-    if (sent) {
-      hipLaunchKernelGGL(k_blk_offsets, dim3(1), dim3(1024), 0, st, a.blk, nb, ob->off);
+    if (sent) {  // the blocks' offsets and the sums in one launch, then the compaction
+      hipLaunchKernelGGL(k_blk_offsets, dim3(1), dim3(1024), 0, st, a.blk, nb, ob->off, gerr, ob->ret);
       sg_outbound_sent o = *sent;
       TimedLaunch tl(ctx, "out_compact", 0.0);
       hipLaunchKernelGGL(k_out_compact, dim3(nb), dim3(256), 0, st, H, ob->start, ob->head, ob->rflags, ob->host_ip,
                          ob->ring, ob->cap, fwd_time, n_packets, ob->off, o);
+    } else {
+      hipLaunchKernelGGL(k_codel_reduce, dim3(1), dim3(1024), 0, st, a.blk, nb, gerr, ob->ret);
     }
-    hipLaunchKernelGGL(k_codel_reduce, dim3(1), dim3(1024), 0, st, a.blk, nb, gerr, ob->ret);
     SG_CHECK_LAUNCH();
     SG_HIP(hipStreamSynchronize(st));
     const volatile unsigned long long* r = ob->ret;
