@@ -137,7 +137,8 @@ __global__ void __launch_bounds__(DENSE_THREADS) k_sssp_dense(const uint32_t* __
                                                               uint64_t* __restrict__ out_lat,
                                                               float* __restrict__ out_loss,
                                                               uint32_t* __restrict__ sat_row,
-                                                              unsigned long long* __restrict__ work) {
+                                                              unsigned long long* __restrict__ work,
+                                                              uint32_t split_below) {
   extern __shared__ __align__(16) unsigned char smem[];
   unsigned long long* key = (unsigned long long*)smem;        // [n]
   uint32_t* settled = (uint32_t*)(key + n);                   // [ceil(n / 32)] bitmap
@@ -206,7 +207,38 @@ __global__ void __launch_bounds__(DENSE_THREADS) k_sssp_dense(const uint32_t* __
     const uint32_t ns = min(s_cnt, DENSE_SCAP);
     // Relax: a wave takes DENSE_G settled rows at a time, 64 arcs per row and step, and
     // stops a row at its first arc past T (rows sorted by latency); keys are final for
-    // the settled rows (their (lat, loss) read once here, unchanged during the round)
+    // the settled rows (their (lat, loss) read once here, unchanged during the round).
+    // A round with few settled rows (the first ones, whose cut is still near the longest arc:
+    // whole rows) splits each row over DENSE_WAVES / ns waves, which take its 64-arc chunks in
+    // turn -- the row's loads in flight side by side instead of one chunk after the other.
+    if (ns < split_below) {
+      const uint32_t per = DENSE_WAVES / ns, r = wv % ns, p = wv / ns;
+      if (p < per) {
+        const uint32_t u = s_node[r];
+        const uint32_t e = out_off[u + 1];
+        const uint64_t kuv = key[u];
+        const bool cutr = sorted[u];
+        const uint32_t budget = T - min(T, key_lat(kuv));
+        for (uint32_t c0 = out_off[u] + 64 * p; c0 < e; c0 += 64 * per) {
+          const uint32_t i = c0 + lane;
+          const uint32_t off = i < e ? i * (4u * DN_W) : 0x80000000u;
+#ifdef DN_REC12
+          const auto x = __builtin_amdgcn_raw_buffer_load_b96(ra, off, 0, 0);
+#else
+          const auto x = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
+#endif
+          const bool in = i < e && (!cutr || x[1] <= budget);
+          const uint64_t cd = relax32(kuv, x[1], __uint_as_float(x[2]));
+          const bool offer = in && key_lat(cd) != LAT32_SAT && !(settled[x[0] >> 5] >> (x[0] & 31) & 1u);
+          if (offer) (void)__hip_atomic_fetch_min(&key[x[0]], (unsigned long long)cd, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (work) n_rel += __popcll(__ballot(in));
+          if (!__builtin_amdgcn_readlane((int)in, 63)) break;  // the cut (or the row's end): later chunks are past it
+        }
+      }
+      __syncthreads();
+      continue;
+    }
     for (uint32_t s0 = wv * DENSE_G; s0 < ns; s0 += DENSE_WAVES * DENSE_G) {
       uint32_t a[DENSE_G], e[DENSE_G];
       uint64_t ku[DENSE_G];
@@ -294,6 +326,14 @@ __global__ void __launch_bounds__(DENSE_THREADS) k_sssp_dense(const uint32_t* __
 
 bool sssp_dense_fits(uint32_t n) { return n > 0 && n <= DENSE_MAX; }
 
+// rounds with fewer settled rows than this split each row over several waves (SG_DENSE_SPLIT;
+// C2: 0.363 ms without, 0.320 below 4 rows, 0.305 below 8, 0.299 below 16, r8u)
+static uint32_t dense_split_below() {
+  const char* v = getenv("SG_DENSE_SPLIT");
+  const int x = v && *v ? atoi(v) : DENSE_WAVES;
+  return (uint32_t)std::max(0, std::min(DENSE_WAVES, x));
+}
+
 void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used, uint32_t row_begin,
                        uint32_t row_end, uint64_t* out_lat, float* out_loss, uint32_t* sat_row,
                        unsigned long long* work) {
@@ -326,7 +366,8 @@ void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_
   TimedLaunch tl(ctx, "sssp_dense", 0.0);
   hipLaunchKernelGGL(k_sssp_dense, dim3(rows), dim3(DENSE_THREADS), lds, st, net->out_off, (const uint32_t*)sa,
                      (const uint8_t*)sorted, n, net->n_arcs, (const uint32_t*)wmin, d_used, n_used, row_begin,
-                     net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat_row, work);
+                     net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat_row, work,
+                     dense_split_below());
   SG_CHECK_LAUNCH();
 }
 

@@ -483,6 +483,18 @@ def test_routing_info_direct_and_errors(oracle, ctx):
     assert e.value.code == _capi.SG_ERR_NO_EDGE
 
 
+@pytest.mark.parametrize("split", ["0", "1", "5", "16"])
+def test_dense_row_split(oracle, ctx, monkeypatch, split):
+    """The dense search's rounds with few settled rows split each row's arcs over several waves
+    (sg_dense.hip, SG_DENSE_SPLIT: never, below 1, 5 and 16 rows): a complete graph with coarse
+    latencies (ties decided by loss), all rows and a shuffled used subset, bit-exact."""
+    monkeypatch.setenv("SG_DENSE_SPLIT", split)
+    g = synth.complete_graph(300, seed=21)
+    g["lat"] = (g["lat"] // 10**7 + 1) * 10**7
+    _check(oracle, g, np.arange(300, dtype=np.uint32), ctx)
+    _check(oracle, g, np.random.default_rng(21).permutation(300)[:200].astype(np.uint32), ctx)
+
+
 @pytest.mark.parametrize("case", ["ties", "wide", "parallel_directed", "used_subset", "tiny_wmin"])
 def test_dense_graph_cases(oracle, ctx, case, request):
     """Dense graphs (mean out-degree past 64: the register-resident search of sg_dense.hip under
