@@ -39,7 +39,10 @@
 
 namespace sg {
 
-constexpr int DENSE_THREADS = 1024;
+#ifndef DN_THREADS  // (A/B builds: 512 and 256 threads per row measured 0.317-0.321 and 0.312-0.316 ms
+#define DN_THREADS 1024  // against 0.301-0.303 at C2 with the row split, r8x)
+#endif
+constexpr int DENSE_THREADS = DN_THREADS;
 constexpr int DENSE_WAVES = DENSE_THREADS / 64;
 constexpr uint32_t DENSE_SCAP = 512;    // nodes settled per round at most (the rest wait a round)
 constexpr uint32_t SORT_MAXDEG = 4096;  // out-degree sorted in one block's LDS; larger rows stay unsorted
