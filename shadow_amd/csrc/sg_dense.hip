@@ -46,7 +46,10 @@ constexpr int DENSE_THREADS = DN_THREADS;
 constexpr int DENSE_WAVES = DENSE_THREADS / 64;
 constexpr uint32_t DENSE_SCAP = 512;    // nodes settled per round at most (the rest wait a round)
 constexpr uint32_t SORT_MAXDEG = 4096;  // out-degree sorted in one block's LDS; larger rows stay unsorted
-constexpr int DENSE_G = 2;              // settled rows a wave relaxes together (their loads in flight)
+#ifndef DN_G  // (A/B builds at C2, r8y: 1 row 0.320-0.323 ms, 3 rows 0.304-0.305, 4 rows 0.454-0.455, 2 rows 0.304-0.306)
+#define DN_G 2
+#endif
+constexpr int DENSE_G = DN_G;           // settled rows a wave relaxes together (their loads in flight)
 // Sorted-arc records of 12 B (b96 loads; DN_REC16 builds the 16-B records with a pad word of r04).
 // A/B knobs (C2, r7h, `profiles/r05/ab_c2_dense_r7h.txt`): 12-B records 0.461-0.465 ms against
 // 0.469-0.474 for 16 B; DN_NT1 (nt loads in a round whose cut is still open: a row's whole arc
