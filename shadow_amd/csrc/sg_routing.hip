@@ -1104,6 +1104,13 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   const uint32_t* __restrict__ ed = g->edge_dst;
   const uint64_t* __restrict__ el = g->edge_latency_ns;
   const float* __restrict__ ef = g->edge_packet_loss;
+  const bool trace = env_int("SG_NET_TRACE", 0) != 0;  // (diagnostics: host phases on stderr)
+  auto now_us = []() {
+    return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count() / 1e3;
+  };
+  const double tr0 = trace ? now_us() : 0.0;
+  double tr[6] = {0, 0, 0, 0, 0, 0};
   auto name_bad_edge = [&]() {
     for (uint32_t e = 0; e < m; e++) {
       if (es[e] >= n || ed[e] >= n)
@@ -1126,6 +1133,7 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
     if (bad) name_bad_edge();
     n_self = ns;
   }
+  if (trace) tr[0] = now_us();
   // arcs without self-loops, both directions when undirected (petgraph semantics, graph/mod.rs:137-152)
   const uint64_t arcs = ((uint64_t)m - n_self) * (g->directed ? 1u : 2u);
   if (arcs >= (1ull << 32)) throw Error(SG_ERR_INVALID_ARG, "too many arcs");
@@ -1170,6 +1178,7 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
       net->mem_bytes = total;
     }
   }
+  if (trace) tr[1] = now_us();
   char* base = (char*)net->mem;
   net->e_src = (uint32_t*)(base + o_esrc);
   net->e_dst = (uint32_t*)(base + o_edst);
@@ -1193,9 +1202,11 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
     memcpy(h + o_edst, g->edge_dst, m * 4ull);
     memcpy(h + o_elat, g->edge_latency_ns, m * 8ull);
     memcpy(h + o_eloss, g->edge_packet_loss, m * 4ull);
+    if (trace) tr[2] = now_us();
     SG_HIP(hipMemcpyAsync(base, h, eb, hipMemcpyHostToDevice, st));
     stage_release(ctx, 0);
   }
+  if (trace) tr[3] = now_us();
   uint32_t* indeg = ctx->r_misc.get<uint32_t>(2 * ((size_t)n + 1));
   uint32_t* outdeg = indeg + n + 1;
   SG_HIP(hipMemsetAsync(indeg, 0, 2 * ((size_t)n + 1) * 4, st));
@@ -1255,6 +1266,12 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
       }
       net->arc_lat_min = (uint32_t)lo;
       net->arc_lat_mean = cnt ? sum / (double)cnt : 0.0;
+    }
+    if (trace) {
+      tr[4] = now_us();
+      fprintf(stderr, "[net] m=%u: endpoint check %.1f us, allocation %.1f, staging copy %.1f, H2D enqueue %.1f, "
+              "kernels enqueue + loss/latency check %.1f\n", m, tr[0] - tr0, tr[1] - tr[0], tr[2] - tr[1],
+              tr[3] - tr[2], tr[4] - tr[3]);
     }
     if (bad) {
       // nothing may still run on the block when the caller deletes the net
