@@ -1,4 +1,6 @@
 set -u
-O=gpurun_out/r8z; mkdir -p $O
-SG_NET_TRACE=1 timeout -k 10 200 python3 -u tools/oneshot_parts.py 1250 > $O/p.log 2>&1 || { tail -20 $O/p.log; exit 1; }
-grep -v amdgpu $O/p.log | tail -6
+O=gpurun_out/r9a; mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
+tail -1 $O/t.log
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
