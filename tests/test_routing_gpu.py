@@ -487,12 +487,27 @@ def test_routing_info_direct_and_errors(oracle, ctx):
 def test_dense_row_split(oracle, ctx, monkeypatch, split):
     """The dense search's rounds with few settled rows split each row's arcs over several waves
     (sg_dense.hip, SG_DENSE_SPLIT: never, below 1, 5 and 16 rows): a complete graph with coarse
-    latencies (ties decided by loss), all rows and a shuffled used subset, bit-exact."""
+    latencies (ties decided by loss), all rows and a shuffled used subset, and a directed copy with
+    three 700-arc hubs whose rows stay unsorted; bit-exact."""
     monkeypatch.setenv("SG_DENSE_SPLIT", split)
     g = synth.complete_graph(300, seed=21)
     g["lat"] = (g["lat"] // 10**7 + 1) * 10**7
     _check(oracle, g, np.arange(300, dtype=np.uint32), ctx)
     _check(oracle, g, np.random.default_rng(21).permutation(300)[:200].astype(np.uint32), ctx)
+    # three nodes with 700 parallel out-arcs each (past the sort's 512-arc LDS array at 300 nodes):
+    # their rows stay unsorted and are never cut, split or not
+    rng = np.random.default_rng(22)
+    hub = np.repeat(np.array([3, 150, 299], dtype=g["src"].dtype), 700)
+    tail = rng.integers(0, 300, len(hub)).astype(g["dst"].dtype)
+    keep = hub != tail
+    hub, tail = hub[keep], tail[keep]
+    rv = g["src"] != g["dst"]  # the reverse arcs (self-loops once)
+    g2 = dict(g, directed=True, src=np.concatenate([g["src"], g["dst"][rv], hub]),
+              dst=np.concatenate([g["dst"], g["src"][rv], tail]),
+              lat=np.concatenate([g["lat"], g["lat"][rv], rng.integers(10**6, 4 * 10**8, len(hub)).astype(np.uint64)]),
+              loss=np.concatenate([g["loss"], g["loss"][rv],
+                                   np.where(rng.random(len(hub)) < 0.5, 0.0, 0.01).astype(np.float32)]))
+    _check(oracle, g2, np.arange(300, dtype=np.uint32), ctx)
 
 
 @pytest.mark.parametrize("case", ["ties", "wide", "parallel_directed", "used_subset", "tiny_wmin"])
