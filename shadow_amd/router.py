@@ -230,13 +230,14 @@ class OutboundPipeline:
 
     def run(self, host, time_ns, packet, length, payload_len, dst_ipv4, window_end_ns: int, bootstrap_end_ns: int,
             sim_end_ns: int, fwd_time, pkt_status, event_ctr_ptr: Optional[int] = None, sent_cap: Optional[int] = None,
-            event_id=None, event_created_ns=None):
+            event_id=None, event_created_ns=None, collect: bool = True):
         """Sends as device tensors (int32 host/packet/length/payload_len/dst_ipv4, int64 time); fwd_time
         (int64) and pkt_status (uint8) are indexed by packet id.  event_id / event_created_ns (int64
         device tensors, optional, together; they need event_ctr_ptr): the sending event's id (-1 =
         UINT64_MAX: a Packet event) and creation time, which order a send against a forward task at
         the same time (sg_outbound_sends).  Returns (PacketBatch of the packets sent, in send_packet
-        order, and their packet ids), views of buffers reused by the next call."""
+        order, and their packet ids), views of buffers reused by the next call; with collect=False no
+        sent batch is written (sent = NULL) and it returns (None, the number of packets sent)."""
         from .worker import PacketBatch
         n = int(host.numel())
         keyed = event_id is not None
@@ -246,11 +247,18 @@ class OutboundPipeline:
                                     payload_len.data_ptr(), dst_ipv4.data_ptr(),
                                     event_id.data_ptr() if keyed else None,
                                     event_created_ns.data_ptr() if event_created_ns is not None else None)
+        ns = C.c_uint32()
+        if not collect:
+            check(self.ctx.handle, load().sg_outbound_run(self.ctx.handle, self.handle, C.byref(s),
+                                                          int(window_end_ns), int(bootstrap_end_ns), int(sim_end_ns),
+                                                          C.c_void_p(event_ctr_ptr or 0), fwd_time.data_ptr(),
+                                                          pkt_status.data_ptr(), int(pkt_status.numel()), None,
+                                                          C.byref(ns)))
+            return None, ns.value
         cap = int(sent_cap if sent_cap is not None else n + self.n * 4)
         b = self.sent_buffers(max(cap, 1), fwd_time.device)
         o = _capi.sg_outbound_sent(cap, *(b[k].data_ptr() for k in ("src_host", "dst_ipv4", "payload_len",
                                                                      "send_time_ns", "packet")))
-        ns = C.c_uint32()
         check(self.ctx.handle, load().sg_outbound_run(self.ctx.handle, self.handle, C.byref(s), int(window_end_ns),
                                                       int(bootstrap_end_ns), int(sim_end_ns),
                                                       C.c_void_p(event_ctr_ptr or 0), fwd_time.data_ptr(),

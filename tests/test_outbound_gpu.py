@@ -333,3 +333,33 @@ def test_tie_task_after_later_event_and_equal_key(oracle, ctx):
         go([(T0 + 1, 0), (T0 + 1, 1), (T0 + MS, 2)], [(T0, 5), (T0, 5), (T0 + 1, 101)], T0 + 10 * MS)
     assert e.value.code == _capi.SG_ERR_UNSORTED
     go([(T0 + 1, 0), (T0 + 1, 1), (T0 + MS, 2)], [(T0, 5), (T0, 5), (T0 + 1, 102)], T0 + 10 * MS)
+
+
+def test_without_sent_batch(ctx):
+    """sg_outbound_run with sent = NULL (no sent batch: the window's sums alone, k_codel_reduce)
+    gives the same statuses, forward times, event counters, queue and relay state and sent count
+    as with one (the offsets and sums in one launch, then the compaction), over three windows."""
+    import torch
+
+    H, W, per = 500, 2 * MS, 8000
+    hosts = synth.make_hosts(H, 64, exact_seeds=False)
+    bw = np.random.default_rng(5).integers(2 * 10**6, 10 * 10**6, H).astype(np.uint64)
+    obs = [OutboundPipeline(hosts["ip"], bw, 512, ctx=ctx) for _ in range(2)]
+    n_pk = 3 * per
+    out = [(torch.full((n_pk,), -1, dtype=torch.int64, device="cuda"), torch.zeros(n_pk, dtype=torch.uint8, device="cuda"),
+            torch.zeros(H, dtype=torch.int64, device="cuda")) for _ in range(2)]
+    for w in range(3):
+        t0, t1 = T0 + w * W, T0 + (w + 1) * W
+        host, t, ln, pay, dst = _sends(hosts, per, t0, t1, seed=900 + w)
+        pkt = np.arange(w * per, (w + 1) * per, dtype=np.uint32)
+        args = (_dev(host, np.uint32, np.int32), _dev(t, np.uint64, np.int64), _dev(pkt, np.uint32, np.int32),
+                _dev(ln, np.uint32, np.int32), _dev(pay, np.uint32, np.int32), _dev(dst, np.uint32, np.int32),
+                t1, T0, T0 + 10**12)
+        batch, _ = obs[0].run(*args, out[0][0], out[0][1], out[0][2].data_ptr())
+        none, n_sent = obs[1].run(*args, out[1][0], out[1][1], out[1][2].data_ptr(), collect=False)
+        assert none is None and n_sent == len(batch)
+        for a, b in zip(out[0], out[1]):
+            assert torch.equal(a, b)
+        sa, sb = obs[0].get_state(), obs[1].get_state()
+        for k in RKEYS:
+            assert np.array_equal(sa[k], sb[k]), k
