@@ -34,6 +34,8 @@
 #include <string.h>
 #include <time.h>
 
+void sgo_run_threads(void* (*fn)(void*), void* args, size_t stride, uint32_t n); /* sg_oracle.c */
+
 typedef struct {
   uint64_t lat;
   float loss;
@@ -341,10 +343,7 @@ int sgo_routing_faithful(uint32_t n, uint32_t m, const uint32_t* esrc, const uin
   pthread_mutex_init(&J.mu, NULL);
   int T = n_threads < 1 ? 1 : n_threads;
   double t0 = now_s();
-  pthread_t* th = (pthread_t*)malloc((size_t)T * sizeof(pthread_t));
-  for (int t = 0; t < T; t++) pthread_create(&th[t], NULL, fworker, &J);
-  for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
-  free(th);
+  sgo_run_threads(fworker, &J, 0, (uint32_t)T);
   double t1 = now_s();
   int rc = J.err ? 1 : 0;
   /* global collect: reserve the total, insert every per-source entry on one thread */
@@ -668,17 +667,9 @@ int64_t sgo_deliver_faithful(uint64_t round_end, uint64_t sim_end, uint64_t boot
   const double t1 = now_s();
   double t2 = t1;
   if (!rc) {
-    pthread_t th[64];
     fdarg args[64];
-    for (uint32_t t = 0; t < J->T; t++) {
-      args[t] = (fdarg){J, t};
-      if (pthread_create(&th[t], NULL, fdworker, &args[t])) {
-        fdworker(&args[t]);
-        th[t] = 0;
-      }
-    }
-    for (uint32_t t = 0; t < J->T; t++)
-      if (th[t]) pthread_join(th[t], NULL);
+    for (uint32_t t = 0; t < J->T; t++) args[t] = (fdarg){J, t};
+    sgo_run_threads(fdworker, args, sizeof(fdarg), J->T);
     t2 = now_s();
     if (J->err) rc = J->err == 2 ? -2 : -1;
   }

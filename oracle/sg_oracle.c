@@ -28,6 +28,23 @@
 #include <string.h>
 #include <pthread.h>
 
+/* Runs fn(args + t * stride) for t in [0, n) on n threads.  A thread that cannot be created runs
+ * its share on the calling thread instead, and only the threads that started are joined (no join
+ * of an uninitialised handle).  Shared by sg_faithful.c. */
+void sgo_run_threads(void* (*fn)(void*), void* args, size_t stride, uint32_t n) {
+  pthread_t* th = (pthread_t*)malloc((size_t)(n ? n : 1) * sizeof(pthread_t));
+  uint8_t* ok = (uint8_t*)calloc(n ? n : 1, 1);
+  for (uint32_t t = 0; t < n; t++) {
+    void* a = (char*)args + (size_t)t * stride;
+    if (th && ok && pthread_create(&th[t], NULL, fn, a) == 0) ok[t] = 1;
+    else fn(a);
+  }
+  for (uint32_t t = 0; t < n; t++)
+    if (ok && ok[t]) pthread_join(th[t], NULL);
+  free(th);
+  free(ok);
+}
+
 #define SGO_OK 0
 #define SGO_ERR_NO_EDGE 1     /* graph/mod.rs:266-268 "No edge connecting node" */
 #define SGO_ERR_MULTI_EDGE 2  /* graph/mod.rs:269-275 "More than one edge connecting" */
@@ -309,10 +326,7 @@ int sgo_shortest_paths(uint32_t n, uint32_t m, const uint32_t* esrc, const uint3
   if (n_threads <= 1) {
     sssp_worker(&J);
   } else {
-    pthread_t* th = (pthread_t*)malloc((size_t)n_threads * sizeof(pthread_t));
-    for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, sssp_worker, &J);
-    for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
-    free(th);
+    sgo_run_threads(sssp_worker, &J, 0, (uint32_t)n_threads);  /* (a shared job: every thread takes rows) */
   }
   pthread_mutex_destroy(&J.mu);
   if (J.err == SGO_ERR_OOM) {
@@ -1291,17 +1305,9 @@ static void* mt_worker(void* p) {
 }
 
 static void mt_run(mt_job* J, int phase) {
-  pthread_t th[64];
   mt_arg args[64];
-  for (uint32_t t = 0; t < J->T; t++) {
-    args[t] = (mt_arg){J, t, phase};
-    if (pthread_create(&th[t], NULL, mt_worker, &args[t])) {
-      mt_worker(&args[t]);
-      th[t] = 0;
-    }
-  }
-  for (uint32_t t = 0; t < J->T; t++)
-    if (th[t]) pthread_join(th[t], NULL);
+  for (uint32_t t = 0; t < J->T; t++) args[t] = (mt_arg){J, t, phase};
+  sgo_run_threads(mt_worker, args, sizeof(mt_arg), J->T);
 }
 
 int64_t sgo_deliver_round_mt(uint64_t round_end, uint64_t sim_end, uint64_t bootstrap_end, uint32_t n_pkts,
@@ -1460,11 +1466,7 @@ static void* lane_worker(void* arg) {
 }
 
 static int run_lane_jobs(lane_job* jobs, uint32_t n_threads) {
-  pthread_t* th = (pthread_t*)malloc((size_t)n_threads * sizeof(pthread_t));
-  if (!th) return -1;
-  for (uint32_t t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, lane_worker, &jobs[t]);
-  for (uint32_t t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
-  free(th);
+  sgo_run_threads(lane_worker, jobs, sizeof(lane_job), n_threads);
   int rc = 0;
   for (uint32_t t = 0; t < n_threads && !rc; t++) rc = jobs[t].rc;
   return rc;
@@ -1479,7 +1481,11 @@ int sgo_codel_run_mt(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t* i
   if (!n_threads) return -1;
   uint32_t* off = (uint32_t*)malloc(((size_t)n_hosts + 1) * 4);
   lane_job* jobs = (lane_job*)calloc(n_threads, sizeof(lane_job));
-  if (!off || !jobs) return -1;
+  if (!off || !jobs) {
+    free(off);
+    free(jobs);
+    return -1;
+  }
   int rc = host_offsets(host, n_events, n_hosts, off);
   if (!rc) {
     codel_call c = {n_hosts, cap, flags, iend, dnext, cur, prev, bytes, head, tail, ring_pkt, ring_ts, ring_len,
@@ -1504,7 +1510,11 @@ int sgo_inbound_run_mt(uint32_t n_hosts, uint32_t cap, uint8_t* flags, uint64_t*
   if (!n_threads) return -1;
   uint32_t* off = (uint32_t*)malloc(((size_t)n_hosts + 1) * 4);
   lane_job* jobs = (lane_job*)calloc(n_threads, sizeof(lane_job));
-  if (!off || !jobs) return -1;
+  if (!off || !jobs) {
+    free(off);
+    free(jobs);
+    return -1;
+  }
   int rc = host_offsets(host, n_arr, n_hosts, off);
   if (!rc) {
     inbound_call c = {n_hosts, cap, flags, iend, dnext, cur, prev, bytes, head, tail, ring_pkt, ring_ts, ring_len,
@@ -1567,8 +1577,11 @@ int sgo_outbound_run_mt(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip,
   if (!n_threads) return -1;
   uint32_t* off = (uint32_t*)malloc(((size_t)n_hosts + 1) * 4);
   lane_job* jobs = (lane_job*)calloc(n_threads, sizeof(lane_job));
-  pthread_t* th = (pthread_t*)malloc((size_t)n_threads * sizeof(pthread_t));
-  if (!off || !jobs || !th) return -1;
+  if (!off || !jobs) {
+    free(off);
+    free(jobs);
+    return -1;
+  }
   *n_out = 0;
   int rc = host_offsets(host, n_sends, n_hosts, off);
   if (!rc) {
@@ -1583,8 +1596,7 @@ int sgo_outbound_run_mt(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip,
       jobs[t] = (lane_job){2, &c, off, n_threads, t, (uint32_t)at, (uint32_t)(at + need < out_cap ? at + need : out_cap), 0, 0};
       at += need;
     }
-    for (uint32_t t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, outbound_worker, &jobs[t]);
-    for (uint32_t t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+    sgo_run_threads(outbound_worker, jobs, sizeof(lane_job), n_threads);
     for (uint32_t t = 0; t < n_threads && !rc; t++) rc = jobs[t].rc;
     /* compact the groups to the front */
     uint32_t w = 0;
@@ -1605,6 +1617,5 @@ int sgo_outbound_run_mt(uint32_t n_hosts, uint32_t cap, const uint32_t* host_ip,
   }
   free(off);
   free(jobs);
-  free(th);
   return rc;
 }

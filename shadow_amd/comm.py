@@ -46,17 +46,39 @@ class Comm:
 
     @classmethod
     def from_torch(cls, ctx, dist, group=None) -> "Comm":
-        """Rank 0 makes the id; torch.distributed broadcasts its bytes to the others."""
+        """Rank 0 makes the id; torch.distributed broadcasts its bytes to the others.  Raises
+        ShadowGpuError on every rank alike when RCCL cannot be set up on some rank (see
+        _agree): no rank is left waiting in a collective the others never enter."""
         import torch
 
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         dev = "cpu" if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
+        # every rank opens RCCL first (sg_comm_unique_id also probes the library), and the
+        # ranks agree on the outcome before any of them enters the communicator's setup
+        uid, code = b"", _capi.SG_OK
+        try:
+            uid = cls.unique_id()
+        except _capi.ShadowGpuError as e:
+            code = e.code
+        code = _agree(code, dist, group, dev)
+        if code != _capi.SG_OK:
+            raise _capi.ShadowGpuError(code, "sg_comm_unique_id failed on some rank")
         t = torch.zeros(_capi.SG_COMM_ID_BYTES, dtype=torch.uint8, device=dev)
         if rank == 0:
-            t.copy_(torch.frombuffer(bytearray(cls.unique_id()), dtype=torch.uint8))
+            t.copy_(torch.frombuffer(bytearray(uid), dtype=torch.uint8))
         if world > 1:
             dist.broadcast(t, 0, group=group)
-        return cls(ctx, bytes(t.cpu().numpy().tobytes()), world, rank)
+        comm, code = None, _capi.SG_OK
+        try:
+            comm = cls(ctx, bytes(t.cpu().numpy().tobytes()), world, rank)
+        except _capi.ShadowGpuError as e:
+            code = e.code
+        code = _agree(code, dist, group, dev)
+        if code != _capi.SG_OK:
+            if comm is not None:
+                comm.close()
+            raise _capi.ShadowGpuError(code, "sg_comm_create failed on some rank")
+        return comm
 
     def get_world_size(self, group=None) -> int:
         return self.n_ranks
@@ -95,12 +117,25 @@ class Comm:
         check(self.ctx.handle, load().sg_comm_alltoallv_records(self.handle, _ptr(send), sc, _ptr(recv), rc))
 
 
+def _agree(code: int, dist, group, dev) -> int:
+    """The largest status over the ranks (status codes are >= 0, SG_OK = 0): one all-reduce, so
+    every rank takes the same branch."""
+    import torch
+
+    if dist.get_world_size(group) <= 1:
+        return int(code)
+    t = torch.tensor([int(code)], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
 def is_comm(d) -> bool:
     return isinstance(d, Comm)
 
 
 def maybe_comm(ctx, dist, group=None) -> Optional[Comm]:
-    """A Comm for an RCCL process group (None for gloo, or when RCCL cannot be opened)."""
+    """A Comm for an RCCL process group (None for gloo, or when RCCL cannot be opened on some
+    rank: then on every rank, so all of them fall back to torch.distributed together)."""
     if dist is None or dist.get_backend(group) == "gloo":
         return None
     try:

@@ -369,6 +369,8 @@ void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_
   if (!rows) return;
   const uint32_t nbw = (n + 31) / 32;
   const size_t lds = (size_t)n * 8 + (size_t)((nbw + 1) & ~1u) * 4 + DENSE_SCAP * 4;
+  // the arc record's size (bytes read per relaxation), for the roofline accounting of bench.py
+  timer_add_work(ctx, "sssp_dense_rec_bytes", 4.0 * DN_W);
   TimedLaunch tl(ctx, "sssp_dense", 0.0);
   hipLaunchKernelGGL(k_sssp_dense, dim3(rows), dim3(DENSE_THREADS), lds, st, net->out_off, (const uint32_t*)sa,
                      (const uint8_t*)sorted, n, net->n_arcs, (const uint32_t*)wmin, d_used, n_used, row_begin,

@@ -325,3 +325,52 @@ def test_balanced_order_keeps_local_blocks():
     w = np.bincount(node, minlength=200)
     assert abs(int(load[0]) - int(load[1])) <= w.max()
     assert np.array_equal(route, pos[node])
+
+
+def _agree_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from shadow_amd import _capi
+        from shadow_amd import comm as CM
+
+        got = [CM._agree(_capi.SG_OK, dist, None, "cpu"),
+               CM._agree(_capi.SG_ERR_UNSUPPORTED if rank == 1 else _capi.SG_OK, dist, None, "cpu")]
+
+        # sg_comm_unique_id failing on rank 1 only: every rank raises the same status, none
+        # enters the broadcast or the communicator's setup alone
+        def uid():
+            if rank == 1:
+                raise _capi.ShadowGpuError(_capi.SG_ERR_UNSUPPORTED, "no RCCL here")
+            return bytes(_capi.SG_COMM_ID_BYTES)
+
+        CM.Comm.unique_id = staticmethod(uid)
+        try:
+            CM.Comm.from_torch(None, dist)
+            got.append(None)
+        except _capi.ShadowGpuError as e:
+            got.append(e.code)
+        dist.destroy_process_group()
+        q.put((rank, got))
+    except Exception:
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+
+
+def test_comm_setup_agrees_across_ranks():
+    """comm.Comm.from_torch / maybe_comm: a failure on one rank is every rank's failure."""
+    from shadow_amd import _capi
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, got in out:
+        assert got == [_capi.SG_OK, _capi.SG_ERR_UNSUPPORTED, _capi.SG_ERR_UNSUPPORTED], (rank, got)

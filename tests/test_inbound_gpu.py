@@ -224,15 +224,94 @@ def test_groups_chunks_and_slow_relays(oracle, ctx, ordered):
     assert (ost["rflags"] & oracle.RL_PENDING).any()  # the slow relays carry tasks over
 
 
-def test_same_time_group_beyond_ring(oracle, ctx):
-    """A same-time group of arrivals larger than the ring: SG_ERR_CAPACITY."""
+@pytest.mark.parametrize("ordered,carried", [(False, False), (True, False), (True, True)])
+def test_same_time_group_beyond_ring(oracle, ctx, ordered, carried):
+    """A same-time group of arrivals larger than the ring: SG_ERR_CAPACITY.  Ordered calls
+    too, with and without elements carried from an earlier call in the ring (the
+    ordered call's end-of-call id translation must not run over the wrapped ring)."""
     import torch
 
-    ib = InboundPipeline(np.array([10**9, 10**9], np.uint64), 16, ctx=ctx)
-    host = np.r_[np.zeros(5, np.uint32), np.ones(20, np.uint32)]
+    bw = np.array([8000 if carried else 10**9, 10**9], np.uint64)  # 1 B/ms: the carried ones stay queued
+    ib = InboundPipeline(bw, 16, ctx=ctx)
+    st = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    fwd = torch.zeros(64, dtype=torch.int64, device="cuda")
+    if carried:  # 6 elements queued on host 0 (ids 40..45), one of them cached by the relay
+        k = 6
+        ib.run(_dev(np.zeros(k), np.uint32, np.int32), _dev(np.full(k, T0), np.uint64, np.int64),
+               _dev(np.arange(40, 40 + k), np.uint32, np.int32), _dev(np.full(k, 1500), np.uint32, np.int32),
+               T0 + MS, 0, T0 + 10**12, fwd, st)
+        assert int(ib.get_state()["tail"][0] - ib.get_state()["head"][0]) >= 4
+    host = np.r_[np.zeros(20, np.uint32), np.ones(5, np.uint32)]
+    args = (_dev(host, np.uint32, np.int32), _dev(np.full(25, T0 + 2 * MS), np.uint64, np.int64),
+            _dev(np.arange(25), np.uint32, np.int32), _dev(np.full(25, 100), np.uint32, np.int32), T0 + 10 * MS,
+            0, T0 + 10**12, fwd, st)
     with pytest.raises(ShadowGpuError) as e:
-        ib.run(_dev(host, np.uint32, np.int32), _dev(np.full(25, T0 + MS), np.uint64, np.int64),
-               _dev(np.arange(25), np.uint32, np.int32), _dev(np.full(25, 100), np.uint32, np.int32), T0 + 10 * MS,
-               0, T0 + 10**12, torch.zeros(32, dtype=torch.int64, device="cuda"),
-               torch.zeros(32, dtype=torch.uint8, device="cuda"))
+        if ordered:
+            ib.run_ordered(*args, torch.zeros(32, dtype=torch.int64, device="cuda"),
+                           torch.zeros(32, dtype=torch.uint8, device="cuda"))
+        else:
+            ib.run(*args)
     assert e.value.code == _capi.SG_ERR_CAPACITY
+    torch.cuda.synchronize()  # the device is still usable: no fault
+
+
+def test_ordered_carried_ids_past_2_31(oracle, ctx):
+    """Packets carried from an earlier call with ids >= 2^31: an ordered call must
+    write their fates by packet id and its own arrivals' by arrival index.  (The r05 kernel told
+    the two apart by bit 31 of the queued value and read such a carried id as an arrival index.)
+    The status and forward-time arrays span 2^31 + 64 ids (2 GB + 16 GB on the device); the oracle
+    runs the same events with the carried ids renumbered 100 + k."""
+    import torch
+
+    BIG, NB = 2**31, 64
+    rng = np.random.default_rng(77)
+    H = 40
+    bw = np.where(np.arange(H) % 2 == 0, 8000 * 200, 10**9).astype(np.uint64)  # 200 B/ms on even hosts
+    ib = InboundPipeline(bw, 64, ctx=ctx)
+    ost = oracle.inbound_state(bw, ib.cap)
+    n_all = BIG + NB
+    st_g = torch.zeros(n_all, dtype=torch.uint8, device="cuda")
+    fwd_g = torch.full((n_all,), -1, dtype=torch.int64, device="cuda")
+    st_o = np.zeros(100 + NB, np.uint8)
+    fwd_o = np.full(100 + NB, np.uint64(2**64 - 1))
+    ctr_g = torch.zeros(H, dtype=torch.int64, device="cuda")
+    ctr_o = np.zeros(H, np.uint64)
+    sim_end = T0 + 10**12
+    # call 1 (by id): NB arrivals with ids 2^31 + k at one instant, so the slow relays queue them
+    h1 = np.sort(rng.integers(0, H, NB)).astype(np.uint32)
+    t1 = np.full(NB, T0 + MS, np.uint64)
+    l1 = np.full(NB, 1500, np.uint32)
+    ib.run(_dev(h1, np.uint32, np.int32), _dev(t1, np.uint64, np.int64),
+           _dev((BIG + np.arange(NB)).astype(np.uint32), np.uint32, np.int32), _dev(l1, np.uint32, np.int32),
+           T0 + 2 * MS, 0, sim_end, fwd_g, st_g, ctr_g.data_ptr())
+    oracle.inbound_run(ost, h1, t1, 100 + np.arange(NB, dtype=np.uint32), l1, T0 + 2 * MS, 0, sim_end, ctr_o,
+                       fwd_o, st_o)
+    got = ib.get_state()
+    q = got["tail"] - got["head"]
+    assert q.sum() > 8  # carried elements
+    assert (got["ring_pkt"][got["ring_pkt"] != 0] >= BIG).any()
+    # call 2 (ordered): 60 arrivals with ids 0..59 over 300 ms; the carried ids leave in it
+    n2 = 60
+    h2 = np.sort(rng.integers(0, H, n2)).astype(np.uint32)
+    t2 = np.sort(rng.integers(T0 + 3 * MS, T0 + 300 * MS, n2)).astype(np.uint64)
+    o = np.lexsort((t2, h2))
+    h2, t2 = h2[o], t2[o]
+    l2 = rng.choice(np.array([28, 1476], np.uint32), n2)
+    p2 = np.arange(n2, dtype=np.uint32)
+    _run(ib, True, h2, t2, p2, l2, T0 + 400 * MS, 0, sim_end, fwd_g, st_g, ctr_g.data_ptr())
+    oracle.inbound_run(ost, h2, t2, p2, l2, T0 + 400 * MS, 0, sim_end, ctr_o, fwd_o, st_o)
+    # the carried ids' fates at 2^31 + k, the arrivals' at their ids; nothing else written
+    gst = np.r_[st_g[:n2].cpu().numpy(), st_g[BIG:BIG + NB].cpu().numpy()]
+    ost_ = np.r_[st_o[:n2], st_o[100:100 + NB]]
+    assert np.array_equal(gst, ost_)
+    assert (ost_[n2:] != 0).sum() > 8  # carried packets left in call 2 (forwarded or dropped)
+    assert int(st_g.count_nonzero()) == int((ost_ != 0).sum())
+    gfw = np.r_[fwd_g[:n2].cpu().numpy(), fwd_g[BIG:BIG + NB].cpu().numpy()].view(np.uint64)
+    ofw = np.r_[fwd_o[:n2], fwd_o[100:100 + NB]]
+    assert np.array_equal(gfw[ost_ == 1], ofw[ost_ == 1])
+    assert np.array_equal(ctr_g.cpu().numpy().view(np.uint64), ctr_o)
+    got = ib.get_state()
+    for k in QKEYS + RKEYS:
+        assert np.array_equal(got[k], ost[k]), k
+    del st_g, fwd_g
+    torch.cuda.empty_cache()
