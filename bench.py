@@ -36,6 +36,8 @@ L2_PEAK_GBS = 34500.0
 ROW_BYTES_PER_RELAX = 8  # slab kernel: one 8-B packed key gathered per lane-relaxation (512-B row per 64 sources)
 ARC_BYTES_PER_RELAX = 12  # LDS search: one 12-B out-arc record (head, latency, 1 - loss) read per relaxation
 FAITHFUL_ROWS = 400  # sources in the reference-faithful CPU sample (~10 s of CPU work at C3 on 16 threads)
+C5_CPU_ROWS = 1024  # C5 dense-port sample (the first rows, scaled by 50k / 1,024)
+C5_FAITHFUL_ROWS = 96  # C5 reference-faithful sample (~5x C3's cost per source)
 
 
 def _cpu_info():
@@ -81,9 +83,9 @@ def parse_args():
                    help="c3c4 (default): the C3 routing build + C4 delivery round (weak scaling, 1M packets per "
                         "rank); c5: SURVEY 8d C5, a 50k-node graph and 10M packets per round in total, split "
                         "over the ranks (strong scaling)")
-    p.add_argument("--cpu-rows", type=int, default=0,
+    p.add_argument("--cpu-rows", type=int, default=None,
                    help="time the CPU routing baseline on the first K source rows and scale to all rows "
-                        "(0 = every row)")
+                        "(0 = every row; default: every row at C3, the first 1,024 at C5)")
     p.add_argument("--rank-blocks", default="2,4,8",
                    help="at one GPU: time every rank's one-shot row-block build of these N-way splits "
                         "(apsp_detail.rank_block_ms; '' skips)")
@@ -106,6 +108,8 @@ def parse_args():
     a = p.parse_args()
     if a.config == "c5":
         a.nodes, a.hosts, a.packets = 50000, 100000, 10000000
+    if a.cpu_rows is None:  # C5: ~25x C3's CPU work per row; a sample of ~20-30 s on the 16-CPU share
+        a.cpu_rows = C5_CPU_ROWS if a.config == "c5" else 0
     return a
 
 
@@ -898,7 +902,7 @@ def main():
                          f"on the same graph, {threads} threads"}
         # the reference's own cost: SipHash score maps, nodes.contains filter, per-source and
         # global HashMaps, self pairs, the id remap (oracle/sg_faithful.c), on a bounded sample
-        kf = min(nu, FAITHFUL_ROWS)
+        kf = min(nu, C5_FAITHFUL_ROWS if c5 else FAITHFUL_ROWS)
         rcf, _, _, ph = O.routing_faithful(g["n"], g["src"], g["dst"], g["lat"], g["loss"], False, used, rows=kf,
                                            threads=threads, read_back=False)
         assert rcf == 0

@@ -38,6 +38,10 @@ def lib():
         L.sgo_shortest_paths.restype = C.c_int
         L.sgo_shortest_paths.argtypes = [C.c_uint32, C.c_uint32, u32p, u32p, u64p, f32p, C.c_int, u32p,
                                          C.c_uint32, C.c_uint32, C.c_uint32, u64p, f32p, C.c_int, u32p, u32p]
+        L.sgo_check_fixed_point.restype = C.c_int64
+        L.sgo_check_fixed_point.argtypes = [C.c_uint32, C.c_uint32, u32p, u32p, u64p, f32p, C.c_int, u32p,
+                                             C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int,
+                                             u32p, u32p]
         L.sgo_direct_paths.restype = C.c_int
         L.sgo_direct_paths.argtypes = [C.c_uint32, C.c_uint32, u32p, u32p, u64p, f32p, C.c_int, u32p,
                                        C.c_uint32, u64p, f32p, u32p, u32p]
@@ -125,6 +129,28 @@ def shortest_paths(n_nodes, src, dst, lat, loss, directed, used, rows=None, thre
                                   _p(used, C.c_uint32), nu, r0, r1, _p(out_lat, C.c_uint64),
                                   _p(out_loss, C.c_float), threads, C.byref(ea), C.byref(eb))
     return rc, out_lat, out_loss, (ea.value, eb.value)
+
+
+def check_fixed_point(n_nodes, src, dst, lat, loss, directed, used, tab_lat, tab_loss, rows=None, threads=1):
+    """Whole-table certificate (sg_oracle.c sgo_check_fixed_point): the number of cells of the
+    given rows [r0, r1) (tab_lat u64 / tab_loss f32, (r1 - r0) x n_used, row-major, any object
+    exposing a C-contiguous buffer) that break compute_shortest_paths' fixed-point equations
+    (graph/mod.rs:183-228), 0 when the rows are the reference's table bit for bit; and the first
+    failing (row, col).  Every node must be used."""
+    src, dst = _arr(src, np.uint32), _arr(dst, np.uint32)
+    lat, loss = _arr(lat, np.uint64), _arr(loss, np.float32)
+    used = _arr(used, np.uint32)
+    nu = len(used)
+    r0, r1 = (0, nu) if rows is None else rows
+    tl, tf = np.asarray(tab_lat), np.asarray(tab_loss)
+    assert tl.dtype.itemsize == 8 and tf.dtype.itemsize == 4 and tl.size == tf.size == (r1 - r0) * nu
+    assert tl.flags.c_contiguous and tf.flags.c_contiguous
+    br, bc = C.c_uint32(0), C.c_uint32(0)
+    bad = lib().sgo_check_fixed_point(n_nodes, len(src), _p(src, C.c_uint32), _p(dst, C.c_uint32),
+                                      _p(lat, C.c_uint64), _p(loss, C.c_float), int(bool(directed)),
+                                      _p(used, C.c_uint32), nu, r0, r1, tl.ctypes.data, tf.ctypes.data, threads,
+                                      C.byref(br), C.byref(bc))
+    return int(bad), (br.value, bc.value)
 
 
 def routing_faithful(n_nodes, src, dst, lat, loss, directed, used, rows=None, node_ids=None, threads=1,

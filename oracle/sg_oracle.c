@@ -359,6 +359,242 @@ int sgo_shortest_paths(uint32_t n, uint32_t m, const uint32_t* esrc, const uint3
   return SGO_OK;
 }
 
+/* ------------------------------------------------------------------------- */
+/* A whole-table certificate: is a given table compute_shortest_paths' result? */
+/* ------------------------------------------------------------------------- */
+/* Every edge latency is >= 1 ns (graph/mod.rs:105-107) and the loss fold of
+ * graph/mod.rs:322-331 is monotone in the (latency, loss) order of :305-313, so
+ * petgraph's Dijkstra (the restatement above) ends with, for every node v != s,
+ *     D[s][v] = min over the arcs u -> v of D[s][u] (+) w(u, v),
+ * the minimum taken in that order and attained (an arc from a node settled later
+ * cannot win: its candidate is later than v's key), with D[s][s] = default().  The
+ * solution of these equations is unique: of two solutions, take the node with the
+ * smallest value where they differ; its value in one of them comes through a
+ * predecessor of strictly smaller latency, where both agree, so the other one
+ * reaches it too -- a contradiction.  So a table that satisfies them in every cell
+ * (and carries the single self-loop on its diagonal, :210-217) IS the reference's
+ * table, bit for bit, with no Dijkstra run: one pass over every in-arc per row,
+ * i.e. rows x arcs candidate folds instead of a heap per row.
+ * Needs every node used (a path may cross any node: the equations need its value).
+ * Returns the number of cells that fail (0: the table is the reference's), the first
+ * failing (row, column) in row-major order in bad_row / bad_col, or -SGO_ERR_ARG /
+ * -SGO_ERR_OOM.  Rows [row_begin, row_end) of the used order; tab_* hold those rows. */
+typedef struct {
+  uint32_t n, n_used, row_begin, row_end;
+  const uint32_t *in_off, *in_src, *in_edge, *used, *col;
+  const uint32_t* in_rec; /* per in-arc {tail, latency (< 2^32), bits(loss)} when every edge latency fits 32 bits */
+  const uint64_t* elat;
+  const float* eloss;
+  const uint64_t* tab_lat;
+  const float* tab_loss;
+  const uint32_t* self_cnt;  /* self-loops per node */
+  const uint32_t* self_edge; /* the first one */
+  int64_t next_row;
+  int64_t bad;
+  uint32_t bad_row, bad_col;
+  int err;
+  pthread_mutex_t mu;
+} fp_job;
+
+static inline uint32_t f32_bits(float f) {
+  uint32_t b;
+  memcpy(&b, &f, 4);
+  return b;
+}
+
+static void* fp_worker(void* arg) {
+  fp_job* J = (fp_job*)arg;
+  const uint32_t n = J->n;
+  sgo_pp* D = (sgo_pp*)malloc(((size_t)n + 1) * sizeof(sgo_pp));
+  uint64_t* K = (uint64_t*)malloc(((size_t)n + 1) * 8); /* the row as packed keys (the fast path) */
+  if (!D || !K) {
+    free(D);
+    free(K);
+    pthread_mutex_lock(&J->mu);
+    J->err = SGO_ERR_OOM;
+    pthread_mutex_unlock(&J->mu);
+    return NULL;
+  }
+  for (;;) {
+    const int64_t row = __atomic_fetch_add(&J->next_row, 1, __ATOMIC_RELAXED);
+    if (row >= (int64_t)J->row_end) break;
+    const size_t base = (size_t)(row - J->row_begin) * J->n_used;
+    const uint32_t s = J->used[row];
+    int narrow = J->in_rec != NULL; /* every latency of the row below 2^32: packed keys */
+    const uint64_t* tl = J->tab_lat + base;
+    const float* tf = J->tab_loss + base;
+    uint64_t wide = 0;
+    for (uint32_t v = 0; v < n; v++) {
+      const uint32_t c = J->col[v];
+      wide |= tl[c];
+      K[v] = (tl[c] << 32) | f32_bits(tf[c]);
+    }
+    narrow &= (wide >> 32) == 0;
+    if (!narrow)
+      for (uint32_t v = 0; v < n; v++) {
+        D[v].lat = tl[J->col[v]];
+        D[v].loss = tf[J->col[v]];
+      }
+    const sgo_pp diag = {tl[J->col[s]], tf[J->col[s]]};
+    D[s].lat = 0; /* PathProperties::default() at the source */
+    D[s].loss = 0.0f;
+    K[s] = 0;
+    int64_t bad = 0;
+    uint32_t first = UINT32_MAX;
+    for (uint32_t v = 0; v < n; v++) {
+      int ok;
+      if (v == s) { /* the diagonal: the single self-loop (graph/mod.rs:210-217) */
+        ok = J->self_cnt[v] == 1 && diag.lat == J->elat[J->self_edge[v]] &&
+             f32_bits(diag.loss) == f32_bits(J->eloss[J->self_edge[v]]);
+      } else if (narrow) {
+        /* the same minimum on packed keys: (latency << 32) | bits(loss) orders as (latency, loss)
+         * (loss >= 0); a candidate of 2^32 ns or more is later than every key of the row */
+        uint64_t best = UINT64_MAX;
+        for (uint32_t k = J->in_off[v]; k < J->in_off[v + 1]; k++) {
+          const uint32_t* r = J->in_rec + 3 * (size_t)k;
+          const uint64_t ku = K[r[0]];
+          const uint64_t lat = (ku >> 32) + r[1];
+          sgo_pp a = {0, 0.0f};
+          float el;
+          const uint32_t lb = (uint32_t)ku, eb = r[2];
+          memcpy(&a.loss, &lb, 4);
+          memcpy(&el, &eb, 4);
+          const sgo_pp c = pp_add(a, 0, el);
+          const uint64_t kc = lat >> 32 ? UINT64_MAX : (lat << 32) | f32_bits(c.loss);
+          best = kc < best ? kc : best;
+        }
+        ok = best == K[v];
+      } else {
+        sgo_pp best = {UINT64_MAX, 1.0f};
+        int any = 0;
+        for (uint32_t k = J->in_off[v]; k < J->in_off[v + 1]; k++) {
+          const uint32_t u = J->in_src[k], e = J->in_edge[k];
+          if (D[u].lat == UINT64_MAX) continue; /* (a table cell that claims unreachable) */
+          const sgo_pp c = pp_add(D[u], J->elat[e], J->eloss[e]);
+          if (!any || pp_lt(c, best)) best = c;
+          any = 1;
+        }
+        ok = any && best.lat == D[v].lat && f32_bits(best.loss) == f32_bits(D[v].loss);
+      }
+      if (!ok) {
+        bad++;
+        if (J->col[v] < first) first = J->col[v];
+      }
+    }
+    if (bad) {
+      pthread_mutex_lock(&J->mu);
+      J->bad += bad;
+      if ((uint32_t)row < J->bad_row || ((uint32_t)row == J->bad_row && first < J->bad_col)) {
+        J->bad_row = (uint32_t)row;
+        J->bad_col = first;
+      }
+      pthread_mutex_unlock(&J->mu);
+    }
+  }
+  free(D);
+  free(K);
+  return NULL;
+}
+
+int64_t sgo_check_fixed_point(uint32_t n, uint32_t m, const uint32_t* esrc, const uint32_t* edst,
+                              const uint64_t* elat, const float* eloss, int directed, const uint32_t* used,
+                              uint32_t n_used, uint32_t row_begin, uint32_t row_end, const uint64_t* tab_lat,
+                              const float* tab_loss, int n_threads, uint32_t* bad_row, uint32_t* bad_col) {
+  if (n_used != n || row_begin > row_end || row_end > n_used) return -SGO_ERR_ARG;
+  uint32_t* col = (uint32_t*)malloc(((size_t)n + 1) * 4);
+  uint32_t* in_off = (uint32_t*)calloc((size_t)n + 1, 4);
+  uint32_t* self_cnt = (uint32_t*)calloc((size_t)n + 1, 4);
+  uint32_t* self_edge = (uint32_t*)calloc((size_t)n + 1, 4);
+  const size_t cap = (directed ? (size_t)m : 2 * (size_t)m) + 1;
+  uint32_t* in_src = (uint32_t*)malloc(cap * 4);
+  uint32_t* in_edge = (uint32_t*)malloc(cap * 4);
+  uint32_t* cur = (uint32_t*)malloc(((size_t)n + 1) * 4);
+  int64_t rc = 0;
+  if (!col || !in_off || !self_cnt || !self_edge || !in_src || !in_edge || !cur) rc = -SGO_ERR_OOM;
+  if (!rc) { /* used must be a permutation of the nodes */
+    for (uint32_t v = 0; v < n; v++) col[v] = UINT32_MAX;
+    for (uint32_t j = 0; j < n_used && !rc; j++) {
+      if (used[j] >= n || col[used[j]] != UINT32_MAX) rc = -SGO_ERR_ARG;
+      else col[used[j]] = j;
+    }
+  }
+  if (!rc) { /* in-arcs (self-loops apart: they never win), both directions when undirected */
+    for (uint32_t i = 0; i < m; i++) {
+      const uint32_t a = esrc[i], b = edst[i];
+      if (a >= n || b >= n) {
+        rc = -SGO_ERR_ARG;
+        break;
+      }
+      if (a == b) {
+        if (self_cnt[a]++ == 0) self_edge[a] = i;
+        continue;
+      }
+      in_off[b + 1]++;
+      if (!directed) in_off[a + 1]++;
+    }
+  }
+  if (!rc) {
+    for (uint32_t v = 0; v < n; v++) in_off[v + 1] += in_off[v];
+    memcpy(cur, in_off, ((size_t)n + 1) * 4);
+    for (uint32_t i = 0; i < m; i++) {
+      const uint32_t a = esrc[i], b = edst[i];
+      if (a == b) continue;
+      in_src[cur[b]] = a;
+      in_edge[cur[b]++] = i;
+      if (!directed) {
+        in_src[cur[a]] = b;
+        in_edge[cur[a]++] = i;
+      }
+    }
+    /* in-arc records for the packed-key path: tail, latency, loss bits, in CSC order */
+    int narrow = 1;
+    for (uint32_t i = 0; i < m; i++) narrow &= elat[i] < ((uint64_t)1 << 32);
+    uint32_t* rec = narrow ? (uint32_t*)malloc(((size_t)in_off[n] + 1) * 12) : NULL;
+    if (rec)
+      for (uint32_t k = 0; k < in_off[n]; k++) {
+        rec[3 * (size_t)k] = in_src[k];
+        rec[3 * (size_t)k + 1] = (uint32_t)elat[in_edge[k]];
+        rec[3 * (size_t)k + 2] = f32_bits(eloss[in_edge[k]]);
+      }
+    fp_job J;
+    memset(&J, 0, sizeof(J));
+    J.in_rec = rec;
+    J.n = n;
+    J.n_used = n_used;
+    J.row_begin = row_begin;
+    J.row_end = row_end;
+    J.in_off = in_off;
+    J.in_src = in_src;
+    J.in_edge = in_edge;
+    J.used = used;
+    J.col = col;
+    J.elat = elat;
+    J.eloss = eloss;
+    J.tab_lat = tab_lat;
+    J.tab_loss = tab_loss;
+    J.self_cnt = self_cnt;
+    J.self_edge = self_edge;
+    J.next_row = row_begin;
+    J.bad_row = UINT32_MAX;
+    J.bad_col = UINT32_MAX;
+    pthread_mutex_init(&J.mu, NULL);
+    sgo_run_threads(fp_worker, &J, 0, n_threads < 1 ? 1u : (uint32_t)n_threads);
+    pthread_mutex_destroy(&J.mu);
+    rc = J.err ? -(int64_t)J.err : J.bad;
+    free(rec);
+    if (bad_row) *bad_row = J.bad_row;
+    if (bad_col) *bad_col = J.bad_col;
+  }
+  free(col);
+  free(in_off);
+  free(self_cnt);
+  free(self_edge);
+  free(in_src);
+  free(in_edge);
+  free(cur);
+  return rc;
+}
+
 /*
  * NetworkGraph::get_direct_paths (graph/mod.rs:230-252): the raw edge for every
  * used pair; exactly one edge required; first failing pair in row-major order.

@@ -400,3 +400,41 @@ def test_faithful_delivery_round_matches_dense(oracle, threads):
     assert np.array_equal(ra, rb) and np.array_equal(ca, cb)
     assert b["setup_s"] > 0 and b["round_s"] > 0
     assert (a["status"] == 3).any() and (a["status"] == 2).any() and (a["status"] == 1).any()
+
+
+@pytest.mark.parametrize("directed,parallel,wide", [(False, 0.0, False), (True, 0.0, False), (False, 0.2, False),
+                                                   (True, 0.3, False), (False, 0.0, True), (True, 0.1, True)])
+def test_fixed_point_certificate(oracle, directed, parallel, wide):
+    """sgo_check_fixed_point accepts exactly the Dijkstra table: 0 failing cells on the
+    restatement's own table (ties, parallel edges, zero-loss runs), and the first failing
+    cell of a table changed in one latency, one loss bit, one diagonal, or two rows swapped."""
+    g = synth.ring_chords_graph(700, 6.0, seed=11 + int(directed), directed=directed, parallel=parallel,
+                                lat_lo_us=1, lat_hi_us=4)  # tiny latency range: many equal-latency paths
+    if wide:  # some edges and paths of 2^32 ns and more: the checker's u64 path instead of packed keys
+        g["lat"] = g["lat"] * np.where(np.random.default_rng(5).random(len(g["lat"])) < 0.3, 2**31, 1).astype(np.uint64)
+    n = g["n"]
+    used = np.random.default_rng(3).permutation(n).astype(np.uint32)  # any order of all nodes
+    rc, lat, loss, _ = oracle.shortest_paths(n, g["src"], g["dst"], g["lat"], g["loss"], directed, used, threads=4)
+    assert rc == 0
+    args = (n, g["src"], g["dst"], g["lat"], g["loss"], directed, used)
+    assert oracle.check_fixed_point(*args, lat, loss, threads=4) == (0, (2**32 - 1, 2**32 - 1))
+    # a row block
+    assert oracle.check_fixed_point(*args, lat[100:300].copy(), loss[100:300].copy(), rows=(100, 300))[0] == 0
+    cases = []
+    l2 = lat.copy(); l2[37, 400] += 1; cases.append((l2, loss, (37, None)))  # (neighbours fail too)
+    f2 = loss.copy(); off = 401 if f2[37, 401] > 0 else 402
+    f2.view(np.uint32)[37, off] ^= 1; cases.append((lat, f2, (37, None)))
+    l3 = lat.copy(); l3[5, 5] += 7; cases.append((l3, loss, (5, 5)))  # the diagonal alone
+    l4, f4 = lat.copy(), loss.copy(); l4[[8, 9]] = l4[[9, 8]]; f4[[8, 9]] = f4[[9, 8]]
+    cases.append((l4, f4, (8, None)))
+    for tl, tf, (r, c) in cases:
+        bad, (br, bc) = oracle.check_fixed_point(*args, tl, tf, threads=3)
+        assert bad > 0 and br == r and (c is None or bc == c), (bad, br, bc, r, c)
+
+
+def test_fixed_point_certificate_needs_every_node(oracle):
+    g = synth.ring_chords_graph(50, 4.0, seed=2)
+    used = np.arange(40, dtype=np.uint32)
+    z = np.zeros((40, 40), np.uint64)
+    assert oracle.check_fixed_point(50, g["src"], g["dst"], g["lat"], g["loss"], False, used, z,
+                                    z.astype(np.float32))[0] == -oracle.ERR_ARG

@@ -14,7 +14,13 @@ own per rank; two ranks cannot share a device).  It drives, on device tensors:
     sg_deliver_bucket,
 and checks them against the single-GPU path (sg_routing_build, deliver_round).
 Prints one JSON line: ok, and the exchange's timings.
+
+Sizes: the defaults are a 600-node graph, 4,000 hosts and 200k packets (the -m gpu test);
+--c5 runs BASELINE configs[4]'s sizes through the same calls: the 50k-node table (2.5·10^9
+cells, compared on the device with a second build instead of a host copy), 100k hosts and
+10M packets.
 """
+import argparse
 import json
 import os
 import sys
@@ -28,6 +34,12 @@ T0 = 946684800 * 10**9
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--c5", action="store_true", help="configs[4] sizes: 50k nodes, 100k hosts, 10M packets")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    size = dict(nodes=50_000, degree=8.0, hosts=100_000, packets=10_000_000) if a.c5 else \
+        dict(nodes=600, degree=6.0, hosts=4000, packets=200_000)
     import torch
     import torch.distributed as dist
 
@@ -47,22 +59,22 @@ def main():
     assert comm.n_ranks == 1 and comm.rank == 0
     res = {}
     for name, exch in (("sg_comm", comm), ("torch", dist)):
-        res[name] = check(ctx, exch, dist, torch)
+        res[name] = check(ctx, exch, dist, torch, size, a.reps)
     comm.close()
-    print(json.dumps({"ok": True, "backend": dist.get_backend(), **res["sg_comm"],
+    print(json.dumps({"ok": True, "backend": dist.get_backend(), "size": size, **res["sg_comm"],
                       "torch_collectives": res["torch"]}), flush=True)
     dist.destroy_process_group()
 
 
-def check(ctx, exch, dist, torch):
+def check(ctx, exch, dist, torch, size, reps):
     from shadow_amd import NetworkGraph, synth
     from shadow_amd.comm import is_comm
     from shadow_amd.dist import RECORD_DTYPE, HostPartition, ShardedDelivery, exchange_round
     from shadow_amd.worker import DeviceTable, HostTable, PacketBatch, deliver_round
 
     # ---- APSP rows + the RCCL all-gather of the row blocks
-    n = 600
-    g = synth.ring_chords_graph(n, 6.0, seed=9)
+    n = size["nodes"]
+    g = synth.ring_chords_graph(n, size["degree"], seed=9)
     net = NetworkGraph(g["n"], g["src"], g["dst"], g["lat"], g["loss"], g["directed"], ctx=ctx)
     used = np.arange(n, dtype=np.uint32)
     mine_lat = torch.empty(n * n, dtype=torch.int64, device="cuda")
@@ -77,14 +89,23 @@ def check(ctx, exch, dist, torch):
         dist.all_gather_into_tensor(full_lat, mine_lat)
         dist.all_gather_into_tensor(full_loss, mine_loss)
     torch.cuda.synchronize()
-    ref = net.compute_shortest_paths(used)
-    assert np.array_equal(full_lat.cpu().numpy().view(np.uint64).reshape(n, n), ref.latency_ns)
-    assert np.array_equal(full_loss.cpu().numpy().view(np.uint32).reshape(n, n), ref.packet_loss.view(np.uint32))
+    if n <= 4096:
+        ref = net.compute_shortest_paths(used)
+        assert np.array_equal(full_lat.cpu().numpy().view(np.uint64).reshape(n, n), ref.latency_ns)
+        assert np.array_equal(full_loss.cpu().numpy().view(np.uint32).reshape(n, n), ref.packet_loss.view(np.uint32))
+    else:  # (configs[4]: a second build, compared on the device; its parity: tests/test_c5_gpu.py)
+        ref_lat, ref_loss = torch.empty_like(mine_lat), torch.empty_like(mine_loss)
+        net.build_rows_device(used, 0, n, ref_lat.data_ptr(), ref_loss.data_ptr(), True)
+        torch.cuda.synchronize()
+        assert torch.equal(full_lat, ref_lat) and torch.equal(full_loss.view(torch.int32), ref_loss.view(torch.int32))
+        del ref_lat, ref_loss
+        if full_lat is not mine_lat:
+            del mine_lat, mine_loss
 
     # ---- a sharded delivery round through RCCL vs the single-GPU round
-    hosts = synth.make_hosts(4000, n, general_seed=9)
+    hosts = synth.make_hosts(size["hosts"], n, general_seed=9, exact_seeds=size["hosts"] <= 10_000)
     start, end = T0 + 10**9, T0 + 10**9 + 10**6
-    pk = synth.make_packets(200000, hosts, start, end, seed=9, p_unknown_dst=0.01)
+    pk = synth.make_packets(size["packets"], hosts, start, end, seed=9, p_unknown_dst=0.01)
     table = DeviceTable(full_lat, full_loss, n, 0)
     batch = PacketBatch.from_numpy(pk["src"], pk["dst_ip"], pk["payload"], pk["send_time"])
     part = HostPartition(hosts["route"], n, 1)
@@ -124,7 +145,6 @@ def check(ctx, exch, dist, torch):
     assert np.array_equal(g1[0], g2[0]) and np.array_equal(g1[1], g2[1])
 
     # ---- timings: the whole sharded round, and exchange_round alone (its one host sync)
-    reps = 20
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
