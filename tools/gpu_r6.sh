@@ -11,7 +11,7 @@ for step in "$@"; do
     smoke) timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }; tail -2 $O/smoke.log ;;
     bench) timeout -k 10 420 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }; tail -c 600 $O/bench.json ;;
     c5bench) timeout -k 10 600 python -u bench.py --config c5 --no-gml --no-c2 --steps 3 --warmup 1 --rank-blocks 8 > $O/bench_c5.json 2> $O/bench_c5.err || { tail -20 $O/bench_c5.err; exit 1; }; tail -c 400 $O/bench_c5.json ;;
-    rccl5) timeout -k 10 300 python -u tools/rccl_check.py --c5 --reps 5 > $O/rccl_c5.json 2> $O/rccl_c5.err || { tail -20 $O/rccl_c5.err; exit 1; }; tail -c 800 $O/rccl_c5.json ;;
+    rccl5) MASTER_PORT=29561 timeout -k 10 300 python -u tools/rccl_check.py --c5 --reps 5 > $O/rccl_c5.json 2> $O/rccl_c5.err || { tail -20 $O/rccl_c5.err; exit 1; }; tail -c 800 $O/rccl_c5.json ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
