@@ -104,6 +104,10 @@ struct BkArgs {
   const uint32_t* cls;
   const uint32_t* hi_off;
   uint32_t npw;  // k_sssp_band: band nodes a wave settles per step (<= 64)
+  // k_sssp_band's per-node append filter (null: off): per workgroup filt_stride bytes, one per node
+  // (degree-class id): 0, or 1 + (the bucket of the best candidate appended for it so far mod 255)
+  uint8_t* filt;
+  uint32_t filt_stride;
   unsigned long long* work;       // COUNT: relaxations
   unsigned long long* diag;       // COUNT: [buckets, entries appended, far steps, pops] summed
 };
@@ -797,6 +801,9 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
                                                                         0x00020000);
   const __amdgpu_buffer_rsrc_t roff = __builtin_amdgcn_make_buffer_rsrc((void*)a.hi_off, 0, (int)((n + 1) * 4u),
                                                                         0x00020000);
+  const bool use_filt = a.filt != nullptr;
+  const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(use_filt ? a.filt + (size_t)blockIdx.x * a.filt_stride : a.filt), 0, (int)a.filt_stride, 0x00020000);
   if (tid == 0) s_item = atomicAdd(a.item_ctr, 1u);
   auto ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
   auto is_settled = [&](uint32_t v) { return (settled[v >> 5] >> (v & 31)) & 1u; };
@@ -938,6 +945,12 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
     row = a.row_begin + bi;
     const uint32_t src = a.used_key[row];  // (the degree-class id)
     for (uint32_t i = tid; i < nbw; i += NT) settled[i] = 0u;
+    if (use_filt) {  // the filter starts empty; in L2 before any read of this row (the barrier below)
+      for (uint32_t i = tid * 16u; i < a.filt_stride; i += NT * 16u)
+        __builtin_amdgcn_raw_buffer_store_b128((uint32_t __attribute__((ext_vector_type(4)))){0u, 0u, 0u, 0u}, rf, i,
+                                               0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if (tid == 0) {  // PathProperties::default() at the source: band 0
       const uint32_t h = (src * 0x9E3779B1u) >> (32 - a.hs_log2);
       hid[h] = src;
@@ -1031,6 +1044,7 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
       // ---- relax: the band's nodes are final; settle them and relax their arcs arc-parallel
       {
         const uint32_t U = ctl[UCNT];
+        const uint32_t bm = b % 255u;  // (the append filter's buckets are kept mod 255)
         if (COUNT && tid == 0) n_pop += U;
         const uint32_t npw = a.npw;  // band nodes per wave and step
         for (uint32_t i0 = wv * npw; i0 < U; i0 += NW * npw) {  // whole waves
@@ -1105,6 +1119,33 @@ __global__ void __launch_bounds__(NT) k_sssp_band(BkArgs a) {
                 const uint32_t lat = key_lat(cd[c]);
                 const bool live = lat != LAT32_SAT && !is_settled(v[c]);
                 s[c] = live ? slot_of(bk_bucket(lat, a.delta, a.dmul), b, far) : NONE;
+              }
+              if (use_filt) {
+                // The append filter: a candidate in a later bucket than one already appended for its
+                // node cannot be that node's key (its latency is larger), so it is dropped.  Each node
+                // keeps 1 + (its best appended bucket mod 255); while a node is unsettled that bucket
+                // is >= b, and it is recorded only within b + 254, so it decodes relative to b.  Reads
+                // are L2-served (sc1) and racy: a stale value is an older, larger bucket of a real
+                // entry, or none, so it only lets more candidates through.  The values of the row
+                // before were cleared before this row's first barrier.
+                uint32_t fv[KX], d[KX];
+#pragma unroll
+                for (int c = 0; c < KX; c++) {
+                  d[c] = s[c] != NONE ? bk_bucket(key_lat(cd[c]), a.delta, a.dmul) - b : 0u;
+                  fv[c] = __builtin_amdgcn_raw_buffer_load_b8(rf, s[c] != NONE ? v[c] : 0x80000000u, 0, BK_SC1);
+                }
+#pragma unroll
+                for (int c = 0; c < KX; c++) {
+                  if (s[c] == NONE) continue;
+                  const uint32_t e = fv[c];
+                  const uint32_t rel = e == 0u ? 0xFFFFFFFFu : (e - 1u >= bm ? e - 1u - bm : e - 1u + 255u - bm);
+                  if (d[c] > rel) {
+                    s[c] = NONE;  // later than an appended candidate of its node
+                  } else if (d[c] < rel && d[c] < 255u) {
+                    const uint32_t t = bm + d[c];
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(1u + (t >= 255u ? t - 255u : t)), rf, v[c], 0, 0);
+                  }
+                }
               }
               const unsigned long long q2 = wclk();
               append(std::integral_constant<int, KX>(), s, v, cd, true);
@@ -1567,10 +1608,21 @@ static void launch_sssp_band(sg_ctx* ctx, sg_net* net, BkArgs a, uint32_t n_used
   // per-workgroup strides (skewing them by 4-33 KB measured the same, r8d)
   a.arena_words = a.nch * BD_CH * 3;
   a.scr_stride = n;
+  // The append filter (SG_BAND_FILTER=1; off by default): n bytes per workgroup, 256-B aligned.
+  // Measured at C5 (r6, tools/apsp_ab.py, tables identical; profiles/r06/ab_c5_band_filter_r6d.txt):
+  // arena entries 3.98 -> 1.80 per cell, but 287 against 226.5 ms per build -- each filter read is
+  // one more dependent L2 / Infinity-Cache round trip on the relaxation's chain (the relax step per
+  // band 20.5k -> 34.1k cycles), while the load step it shortens gained only 1.2k (10.8k -> 9.6k):
+  // the kernel is bound by the requests each CU keeps in flight (TCP_PENDING_STALL_CYCLES ~0.8 of
+  // its cycles, profiles/r05/pmc_band_r06h.txt), and the filter adds a read per live candidate
+  const bool filt = bk_env("SG_BAND_FILTER", 0) != 0;
+  a.filt_stride = filt ? (n + 255u) / 256u * 256u : 0u;
   const size_t arena_b = ((size_t)grid * a.arena_words * 4 + 255) / 256 * 256, scr_b = (size_t)grid * a.scr_stride * 8;
-  char* wsp = ctx->r_bucket.get<char>(arena_b + scr_b);
+  const size_t filt_b = (size_t)grid * a.filt_stride;
+  char* wsp = ctx->r_bucket.get<char>(arena_b + scr_b + filt_b);
   a.arena = (uint32_t*)wsp;
   a.scratch = (unsigned long long*)(wsp + arena_b);
+  a.filt = filt ? (uint8_t*)(wsp + arena_b + scr_b) : nullptr;
   a.item_ctr = ctr;
   (void)rows;
   auto go = [&](auto kern) {

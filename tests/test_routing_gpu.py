@@ -548,7 +548,9 @@ def test_dense_graph_cases(oracle, ctx, case, request):
                                  {"SG_BUCKET_THREADS": "1024"}, {"SG_BUCKET_THREADS": "1024", "SG_BUCKET_DELTA": "30000000"},
                                  {"SG_BUCKET_MODE": "queue"}, {"SG_BUCKET_MODE": "queue", "SG_BUCKET_RING": "2"},
                                  {"SG_BUCKET_MODE": "queue", "SG_BUCKET_HASH": "6"}, {"SG_BAND_NPW": "5"},
-                                 {"SG_BAND_NPW": "64", "SG_BUCKET_HASH": "7"}])
+                                 {"SG_BAND_NPW": "64", "SG_BUCKET_HASH": "7"}, {"SG_BAND_FILTER": "1"},
+                                 {"SG_BAND_FILTER": "1", "SG_BUCKET_DELTA": "4096"},
+                                 {"SG_BAND_FILTER": "1", "SG_BUCKET_RING": "2"}])
 def test_bucket_search_knobs(oracle, ctx, monkeypatch, env, apsp_kernel):
     """The bucketed search (sg_bucket.hip) under its knobs, on a tie-heavy lossy graph (10-ms arc
     latencies), directed and undirected, a used subset: exact bands (k_sssp_band: the default
@@ -559,7 +561,10 @@ def test_bucket_search_knobs(oracle, ctx, monkeypatch, env, apsp_kernel):
     40-entry staging array, and its safety valves -- a 64-slot hash that fills and arenas of 4 and 6
     chunks that run out: the row gives up, the workgroup leaves, and the wide kernel redoes the
     row (the output starts poisoned, so no row passes by holding an earlier table); and the banded
-    search's nodes per wave (5: many steps per band; 64 with band splits)."""
+    search's nodes per wave (5: many steps per band; 64 with band splits); and the banded search's
+    append filter (SG_BAND_FILTER, off by default: a candidate later than its node's best appended
+    bucket is dropped), with 10-ms and 4-us bands (buckets past the filter's 255-bucket window) and
+    a 2-slot ring (far lists)."""
     if apsp_kernel != "bucket":
         pytest.skip("bucketed-search knobs")
     for k, v in env.items():

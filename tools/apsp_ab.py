@@ -78,6 +78,9 @@ def main():
             if launches:
                 parts.append(f"{k} {ms:.3f} ms / {launches} launches, {work / 1e9:.3f} G relaxations "
                              f"({work / (rows * max(1, n_arcs)):.3f} x rows*arcs)")
+        ent = ctx.read_timer("sssp_bucket_entries")[2]
+        if ent:
+            parts.append(f"{ent / (rows * n):.3f} arena entries per cell")
         ctx.enable_timers(False)
         print(f"variant {v!r}: median {np.median(times[v]):9.3f} ms/build; " + "; ".join(parts), flush=True)
 
