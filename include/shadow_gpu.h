@@ -522,7 +522,10 @@ typedef struct sg_inbound_arrivals { /* device arrays, grouped by ascending host
   const uint32_t* len;     /* PacketRc::len() */
 } sg_inbound_arrivals;
 
-/* event_ctr (device, n_hosts, may be NULL): each host's event-id counter,
+/* Packet ids are below n_packets <= 2^31: SG_ERR_INVALID_ARG otherwise, for an id at or past
+ * n_packets as soon as it enters a queue (sg_inbound_run) or would stay queued past the call
+ * (sg_inbound_run_ordered).
+ * event_ctr (device, n_hosts, may be NULL): each host's event-id counter,
  * advanced by one per forward task the relay schedules (host.rs:649-653) --
  * e.g. sg_hosts_event_ctr(hosts).  fwd_time (device, n_packets): the time the
  * relay pushed the packet to the interface; pkt_status (device, n_packets):

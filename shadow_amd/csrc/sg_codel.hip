@@ -72,12 +72,15 @@ constexpr int VMCNT0 = 0x0F70;
 // ring path then waits for its own load where it issues it -- where the ring and window paths
 // join, the compiler otherwise waits for every vector-memory operation in flight (vmcnt(0)), the
 // next chunk's loads included
-// ORD (k_inbound<LM, true>, sg_inbound_run_ordered): an element pushed by this call carries its
-// arrival index instead of the caller's packet id, and its fate is written at that index (arrival
-// order: a host's outputs are consecutive) instead of at the packet id.  Which elements those are
-// follows from their ring position -- at or past the tail the call started with -- never from the
-// value, so a carried packet id of any value (2^31 and up included) is never read as an index
-constexpr uint32_t ARR_MAX = 0x80000000u;  // arrivals per ordered call (the host checks)
+// ORD (k_inbound<LM, true>, sg_inbound_run_ordered): an element pushed by this call carries
+// ARR_BIT | its arrival index instead of the caller's packet id, and its fate is written at that
+// index (arrival order: a host's outputs are consecutive) instead of at the packet id.  That is
+// unambiguous because no packet id reaches a ring with the bit set: packet ids are below
+// n_packets <= 2^31 (the host checks), an id at or past n_packets is refused when it is pushed
+// (E_PKT) by the by-id call and when it would be left queued by the ordered one, and an index is
+// checked against the call's arrivals before a fate is written at it (after a failed call, e.g.
+// a ring overflow, the queue state is undefined but no write leaves the outputs)
+constexpr uint32_t ARR_BIT = 0x80000000u;
 
 template <bool PF = false, bool ORD = false>
 struct Q {
@@ -114,14 +117,13 @@ struct Q {
   uint32_t err;
   uint8_t* astat;  // ORD: per arrival of this call
   uint64_t* afwd;
-  uint32_t tc0, n_arr;  // ORD: the tail at the call's start; the call's arrivals
-  bool last_arr;        // ORD: the element pop_front returned last was pushed by this call
+  uint32_t n_arr;  // ORD: the call's arrivals (the bound of astat / afwd)
 
   __device__ void drop(uint32_t pkt) {  // drop_packet -> RouterDropped
     if constexpr (ORD) {
-      if (last_arr) {
-        if (pkt < n_arr) astat[pkt] = SG_CODEL_DROPPED;
-        else err |= E_PKT;  // (only after a ring overflow: the call fails with E_FULL)
+      if (pkt & ARR_BIT) {
+        if ((pkt & ~ARR_BIT) < n_arr) astat[pkt & ~ARR_BIT] = SG_CODEL_DROPPED;
+        else err |= E_PKT;
         dropped++;
         return;
       }
@@ -149,7 +151,6 @@ struct Q {
     }
     pkt = hp;
     last_len = hl;
-    if constexpr (ORD) last_arr = head - tc0 < tail - tc0;  // (a carried element's position wraps past it)
     const uint64_t len = hl, ts = ht;
     head++;
     load_head();
@@ -728,9 +729,7 @@ __global__ void __launch_bounds__(1024) k_codel_reduce(const unsigned long long*
 // or the token bucket blocks, then reschedules itself after the conforming
 // duration.  Tasks at or after the window end stay pending for the next call.
 constexpr uint64_t TB_INTERVAL = 1000000ull;  // relay/mod.rs:297: refill every 1 ms
-// R_CARR (k_inbound<.., ORD> only, never in the saved state): the cached element is an arrival of
-// this call (its arrival index, not a packet id)
-enum : uint8_t { R_PENDING = 1, R_NEVER = 2, R_CACHED = 4, R_CARR = 8 };
+enum : uint8_t { R_PENDING = 1, R_NEVER = 2, R_CACHED = 4 };
 
 struct Relay {
   uint8_t rf;
@@ -811,33 +810,30 @@ __device__ void relay_task(QT& q, Relay& r, uint64_t now, uint64_t bootstrap_end
   r.rf &= (uint8_t)~R_PENDING;
   for (;;) {
     uint32_t p, l;
-    bool arr = false;  // QT::ord: p is an arrival index of this call
     if (r.rf & R_CACHED) {
       p = r.cp;
       l = r.cl;
-      arr = QT::ord && (r.rf & R_CARR);
-      r.rf &= (uint8_t)~(R_CACHED | R_CARR);
+      r.rf &= (uint8_t)~R_CACHED;
     } else {
       const uint32_t popped = q.pop(now);
       if (popped == CD_NONE) return;  // empty: Idle
       p = popped;
       l = q.last_len;  // the popped element is the last one pop_front returned
-      if constexpr (QT::ord) arr = q.last_arr;
     }
     uint64_t wait;
     if (now >= bootstrap_end && !r.remove(l, now, wait)) {  // Worker::is_bootstrapping: no rate limit
-      r.rf |= arr ? (uint8_t)(R_CACHED | R_CARR) : (uint8_t)R_CACHED;  // RelayCached; forward_later(wait)
+      r.rf |= R_CACHED;  // RelayCached; forward_later(wait)
       r.cp = p;
       r.cl = l;
       r.schedule(now, now > ~0ull - wait ? ~0ull : now + wait, sim_end, ctr_inc);
       return;
     }
-    if (arr) {  // RelayForwarded, an arrival of this call: at its index
-      if (p < q.n_arr) {
-        q.astat[p] = SG_CODEL_DEQUEUED;
-        q.afwd[p] = now;
+    if (QT::ord && (p & ARR_BIT)) {  // RelayForwarded, an arrival of this call: at its index
+      if ((p & ~ARR_BIT) < q.n_arr) {
+        q.astat[p & ~ARR_BIT] = SG_CODEL_DEQUEUED;
+        q.afwd[p & ~ARR_BIT] = now;
       } else {
-        q.err |= E_PKT;  // (only after a ring overflow)
+        q.err |= E_PKT;
       }
     } else if (p < q.n_status) {  // RelayForwarded: pushed to the internet interface
       q.status[p] = SG_CODEL_DEQUEUED;
@@ -867,6 +863,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
   Relay r{};
   uint64_t ctr_inc = 0;
   uint32_t tail0 = 0;  // ORD: the tail at the call's start (later elements carry arrival indices)
+  bool id_bad = false;  // !ORD: a staged packet id at or past n_packets (refused when it is pushed: E_PKT)
   if (walker) {
     hb = min(a.host_off[h], a.E);
     he = max(min(a.host_off[h + 1], a.E), hb);
@@ -884,12 +881,10 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
     q.n_status = a.n_status;
     q.astat = ia.arr_status;
     q.afwd = ia.arr_fwd;
-    tail0 = q.tail;
-    q.tc0 = q.tail;
     q.n_arr = a.E;
-    q.last_arr = false;
+    tail0 = q.tail;
     q.load_head();
-    r.rf = ia.rflags[h] & (uint8_t)~R_CARR;
+    r.rf = ia.rflags[h];
     r.tt = ia.task_time[h];
     r.cp = ia.cached_pkt[h];
     r.cl = ia.cached_len[h];
@@ -914,7 +909,8 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
           c0, c1,
           [&](uint32_t i, int u) {
             rt[u] = a.time[i];
-            rp[u] = ORD ? i : a.pkt[i];
+            rp[u] = ORD ? (ARR_BIT | i) : a.pkt[i];
+            if (!ORD) id_bad |= rp[u] >= a.n_status;
             rl[u] = a.len[i];
           },
           [&](uint32_t k, int u) {
@@ -980,7 +976,8 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
       for (int u = 0; u < CD_UNROLL; u++) {
         const uint32_t i = cm.event(c, base + u * CD_THREADS + t, ok[u]);
         rt[u] = a.time[i];
-        rp[u] = ORD ? i : a.pkt[i];
+        rp[u] = ORD ? (ARR_BIT | i) : a.pkt[i];
+        if (!ORD) id_bad |= rp[u] >= a.n_status;
         rl[u] = a.len[i];
       }
 #pragma unroll
@@ -1043,22 +1040,24 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
     while (due(ia.window_end)) relay_task(q, r, r.tt, ia.bootstrap_end, ia.sim_end, ctr_inc, ia.fwd_time);
     if constexpr (ORD) {
       // the elements this call pushed that are still queued (the last min(queued, pushed) of
-      // the ring), and a cached one, go back to the caller's packet ids for the next call.  After
-      // a ring overflow (E_FULL: the call fails, SG_ERR_CAPACITY) the ring no longer holds them:
-      // nothing is translated, and no index is read past the arrivals
+      // the ring), and a cached one, go back to the caller's packet ids for the next call; an id
+      // past n_packets would read as an index in a later call, so it fails this one (E_PKT).
+      // After a ring overflow (E_FULL: the call fails with SG_ERR_CAPACITY) the ring no longer
+      // holds those elements, and nothing is translated
+      auto to_id = [&](uint32_t v) -> uint32_t {
+        const uint32_t i = v & ~ARR_BIT;
+        const uint32_t id = i < a.E ? a.pkt[i] : 0xFFFFFFFFu;
+        if (id >= a.n_status) q.err |= E_PKT;
+        return id;
+      };
       if (!(q.err & E_FULL)) {
         const uint32_t pushed = q.tail - tail0, queued = q.tail - q.head;
         for (uint32_t j = q.tail - min(min(pushed, queued), q.mask + 1u); j != q.tail; j++) {
           uint32_t* x = (uint32_t*)&q.ring[j & q.mask];
-          if (*x < a.E) *x = a.pkt[*x];
-          else q.err |= E_PKT;
+          if (*x & ARR_BIT) *x = to_id(*x);
         }
-        if ((r.rf & R_CACHED) && (r.rf & R_CARR)) {
-          if (r.cp < a.E) r.cp = a.pkt[r.cp];
-          else q.err |= E_PKT;
-        }
+        if ((r.rf & R_CACHED) && (r.cp & ARR_BIT)) r.cp = to_id(r.cp);
       }
-      r.rf &= (uint8_t)~R_CARR;
     }
     a.flags[h] = q.flags;
     a.iend[h] = q.iend;
@@ -1080,6 +1079,7 @@ __global__ void __launch_bounds__(CD_THREADS) k_inbound(InboundArgs ia) {
     err = q.err;
     dropped = q.dropped;
   }
+  if (!ORD && id_bad) err |= E_PKT;  // (every lane staged ids)
   lane_diag_store(a.bdiag, d_t0, d_walk, he - hb);
   if (t < 64) {
     for (int d = 32; d > 0; d >>= 1) {
@@ -1876,7 +1876,9 @@ static int32_t inbound_run(sg_ctx* ctx, sg_inbound* ib, const sg_inbound_arrival
       throw Error(SG_ERR_INVALID_ARG, "null arrival array");
     if (n_packets && (!pkt_status || !fwd_time)) throw Error(SG_ERR_INVALID_ARG, "null output array");
     if (ord && E && !arr_fwd) throw Error(SG_ERR_INVALID_ARG, "null arrival output array");
-    if (ord && E > ARR_MAX) throw Error(SG_ERR_INVALID_ARG, "too many arrivals for one ordered call");
+    if (ord && E >= ARR_BIT) throw Error(SG_ERR_INVALID_ARG, "too many arrivals for one ordered call");
+    // packet ids stay below 2^31 (an ordered call tells its arrival indices by bit 31)
+    if (n_packets > ARR_BIT) throw Error(SG_ERR_INVALID_ARG, "n_packets above 2^31");
     if (!H) return;
     hipStream_t st = ctx->stream;
     uint32_t* ws = ctx->d_seg.get<uint32_t>((size_t)H + 8);

@@ -255,21 +255,22 @@ def test_same_time_group_beyond_ring(oracle, ctx, ordered, carried):
     torch.cuda.synchronize()  # the device is still usable: no fault
 
 
-def test_ordered_carried_ids_past_2_31(oracle, ctx):
-    """Packets carried from an earlier call with ids >= 2^31: an ordered call must
-    write their fates by packet id and its own arrivals' by arrival index.  (The r05 kernel told
-    the two apart by bit 31 of the queued value and read such a carried id as an arrival index.)
-    The status and forward-time arrays span 2^31 + 64 ids (2 GB + 16 GB on the device); the oracle
-    runs the same events with the carried ids renumbered 100 + k."""
+def test_ordered_carried_ids_at_the_top(oracle, ctx):
+    """Packets carried from an earlier call with the largest ids allowed (just below 2^31 =
+    n_packets): an ordered call writes their fates by packet id and its own arrivals'
+    by arrival index (it tells them apart by bit 31, which no packet id may set).  The status and
+    forward-time arrays span 2^31 ids (2 GB + 16 GB on the device); the oracle runs the same events
+    with the carried ids renumbered 100 + k."""
     import torch
 
-    BIG, NB = 2**31, 64
+    NB = 64
+    BIG = 2**31 - NB  # carried ids BIG + k, the last NB ids below 2^31
     rng = np.random.default_rng(77)
     H = 16
     bw = np.where(np.arange(H) < 8, 8000 * 30, 10**9).astype(np.uint64)  # 30 B/ms on hosts 0-7
     ib = InboundPipeline(bw, 64, ctx=ctx)
     ost = oracle.inbound_state(bw, ib.cap)
-    n_all = BIG + NB
+    n_all = 2**31
     st_g = torch.zeros(n_all, dtype=torch.uint8, device="cuda")
     fwd_g = torch.full((n_all,), -1, dtype=torch.int64, device="cuda")
     st_o = np.zeros(100 + NB, np.uint8)
@@ -317,3 +318,36 @@ def test_ordered_carried_ids_past_2_31(oracle, ctx):
         assert np.array_equal(got[k], ost[k]), k
     del st_g, fwd_g
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("ordered", [False, True])
+def test_packet_ids_bounded(ctx, ordered):
+    """Packet ids stay below n_packets <= 2^31 (an ordered call marks its arrival indices with
+    bit 31): n_packets above 2^31 is refused before any work, and an id at or past n_packets is
+    refused as soon as it enters a queue (by id) or would be left queued by an ordered call."""
+    import torch
+
+    ib = InboundPipeline(np.array([8000, 10**9], np.uint64), 16, ctx=ctx)  # host 0: 1 B/ms (keeps packets)
+    small = torch.zeros(8, dtype=torch.int64, device="cuda")
+    huge = torch.zeros(2**31 + 1, dtype=torch.uint8, device="cuda")
+    arr = (_dev([0, 0, 0], np.uint32, np.int32), _dev([T0 + MS] * 3, np.uint64, np.int64),
+           _dev([0, 1, 2], np.uint32, np.int32), _dev([1500] * 3, np.uint32, np.int32), T0 + 2 * MS, 0, T0 + 10**12)
+    with pytest.raises(ShadowGpuError) as e:  # n_packets = 2^31 + 1
+        if ordered:
+            ib.run_ordered(*arr, small, huge, small, torch.zeros(8, dtype=torch.uint8, device="cuda"))
+        else:
+            ib.run(*arr, small, huge)
+    assert e.value.code == _capi.SG_ERR_INVALID_ARG
+    del huge
+    torch.cuda.empty_cache()
+    st = torch.zeros(4, dtype=torch.uint8, device="cuda")
+    fwd = torch.zeros(4, dtype=torch.int64, device="cuda")
+    # ids 0, 1 and 7 (>= n_packets = 4): the first is forwarded, the second cached, the third queued
+    bad = (arr[0], arr[1], _dev([0, 1, 7], np.uint32, np.int32), *arr[3:])
+    with pytest.raises(ShadowGpuError) as e:
+        if ordered:
+            ib.run_ordered(*bad, fwd, st, small, torch.zeros(8, dtype=torch.uint8, device="cuda"))
+        else:
+            ib.run(*bad, fwd, st)
+    assert e.value.code == _capi.SG_ERR_INVALID_ARG
+    torch.cuda.synchronize()
