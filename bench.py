@@ -91,6 +91,9 @@ def parse_args():
                         "(apsp_detail.rank_block_ms; '' skips)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-delivery", action="store_true")
+    p.add_argument("--no-e2e", action="store_true",
+                   help="skip the end-to-end RoutingInfo fill (its row-block launches of the search would mix "
+                        "into a profile of the headline's whole-table launches)")
     p.add_argument("--no-codel", action="store_true", help="skip the router CoDel leg")
     p.add_argument("--no-gml", action="store_true", help="skip the GML ingest leg")
     p.add_argument("--no-c2", action="store_true", help="skip the C2 (1,200-node complete graph) leg")
@@ -207,6 +210,16 @@ def queue_ahead(ctx, torch, cycles=2_000_000):
         torch.cuda._sleep(cycles)
 
 
+# The lane kernels' HIP-event pairs: queue_ahead keeps the host ahead of the GPU, and each pair still
+# holds the command processor's gap between the kernel before and the one it brackets (~4-5 us
+# against 30-50 us kernels: r6, tools/inbound_timer_diag.py, profiles/r06/ab_lane_timers_r6.txt);
+# the line's "rocprof" object beside it gives the kernel-trace duration of the same kernel.  (A
+# kernel launched with hipExtLaunchKernelGGL's own events measured the same gap; the kernel's span
+# from its first block's start to its last block's end, by the device wall clock, fell 1-4 us
+# short of rocprof's: neither is used.)
+EVENT_TIMER = "HIP event pair around the launch (holds a ~4-5 us dispatch gap; rocprof beside it)"
+
+
 def rocprof_view(pm, bytes_per_launch):
     """The rocprofv3 kernel-trace average of a kernel (from the PMC summary of the default
     workload) and the HBM fraction it gives, beside the line's own HIP-event figure."""
@@ -313,7 +326,7 @@ def codel_leg(a, D, ctx, torch, buckets, n_packets, pmc):
                    "hosts": H, "events": E, "pushes": nd},
         "roofline": {"kernel": "k_codel", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pm.get("hbm_bytes_per_launch"),
-                     "avg_launch_ms": round(k_s * 1e3, 4), "valu_frac_pmc": pm.get("valu_frac"),
+                     "avg_launch_ms": round(k_s * 1e3, 4), "timer": EVENT_TIMER, "valu_frac_pmc": pm.get("valu_frac"),
                      "rocprof": rocprof_view(pm, k_bytes / max(k_n, 1))},
         "dropped": n_drop,
     }
@@ -398,7 +411,7 @@ def outbound_leg(a, D, ctx, torch, pk, hosts, ht, table, round_end, sharded, pmc
         "roofline": {"kernel": "k_outbound", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                      "traffic": pmc.get("outbound", {}).get("hbm_bytes_per_launch"),
-                     "avg_launch_ms": round(k_s * 1e3, 4), "valu_frac_pmc": pmc.get("outbound", {}).get("valu_frac"),
+                     "avg_launch_ms": round(k_s * 1e3, 4), "timer": EVENT_TIMER, "valu_frac_pmc": pmc.get("outbound", {}).get("valu_frac"),
                      "rocprof": rocprof_view(pmc.get("outbound", {}), k_bytes / max(k_n, 1))},
         "compact_ms": round(c_ms / max(c_n, 1), 4),
         "sent": len(batch),
@@ -459,9 +472,13 @@ def inbound_leg(a, D, ctx, torch, buckets, n_packets, pmc, round_end):
         next(it).run_ordered(*args, window_end, 0, 2**63, fwd, status, a_fwd, a_st)
 
     t_step = timed(D, step, a.steps, a.warmup)
+    # (zeroed before the spin: this process's first fill kernel loads its code object on the host,
+    # ~1 ms, and queued after the spin it left the GPU idle between the ops the timer brackets --
+    # 17-us gaps, the r05 line's 0.0595 ms against 0.0414 ms by rocprof)
+    a_st.zero_()
+    torch.cuda.synchronize()
     ctx.enable_timers(True)
     queue_ahead(ctx, torch)
-    a_st.zero_()
     n_drop = next(it).run_ordered(*args, window_end, 0, 2**63, fwd, status, a_fwd, a_st)
     k_ms, k_n, k_bytes = ctx.read_timer("inbound")
     ctx.enable_timers(False)
@@ -489,6 +506,7 @@ def inbound_leg(a, D, ctx, torch, buckets, n_packets, pmc, round_end):
         "roofline": {"kernel": "k_inbound", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                      "traffic": pmc.get("inbound", {}).get("hbm_bytes_per_launch"), "avg_launch_ms": round(k_s * 1e3, 4),
+                     "timer": EVENT_TIMER,
                      "valu_frac_pmc": pmc.get("inbound", {}).get("valu_frac"),
                      "rocprof": rocprof_view(pmc.get("inbound", {}), k_bytes / max(k_n, 1))},
         "forwarded": n_fwd, "dropped": n_drop,
@@ -858,7 +876,7 @@ def main():
     # row blocks built on the GPU, copied into pinned host memory while the next builds)
     note("instrumented builds and comparisons done")
     e2e = None
-    if D.world == 1:
+    if D.world == 1 and not a.no_e2e:
         from shadow_amd import RoutingInfo
 
         ri = RoutingInfo(np.arange(nu, dtype=np.uint32))
