@@ -94,6 +94,7 @@ struct sg_ctx {
   uint64_t pair_count_cells = 0;
   uint64_t net_serial = 0;   // the last sg_net serial handed out
   uint64_t dense_owner = 0;  // the net whose arcs r_dense holds sorted (0: none)
+  uint32_t dense_gen = 0;    // stamp of the dense search's seed-row marks in r_dense (0: none valid)
   uint64_t band_owner = 0;   // the net whose degree-class numbering r_band holds (0: none)
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;

@@ -510,6 +510,54 @@ def test_dense_row_split(oracle, ctx, monkeypatch, split):
     _check(oracle, g2, np.arange(300, dtype=np.uint32), ctx)
 
 
+@pytest.mark.parametrize("env", [{}, {"SG_DENSE_SPEC": "0"}, {"SG_DENSE_SW": "4", "SG_DENSE_G": "4"},
+                                 {"SG_DENSE_SW": "16", "SG_DENSE_THREADS": "512", "SG_DENSE_SPEC": "0"},
+                                 {"SG_DENSE_LAZY": "0"}, {"SG_DENSE_LAZY": "0", "SG_DENSE_SEED": "0"},
+                                 {"SG_DENSE_LAZY": "0", "SG_DENSE_SEED": "1"}, {"SG_DENSE_LAZY": "0", "SG_DENSE_SEED": "64"},
+                                 {"SG_DENSE_LAZY": "0", "SG_DENSE_SEED": "150", "SG_DENSE_SEED_SW": "64",
+                                  "SG_DENSE_SEED_THREADS": "1024"},
+                                 {"SG_DENSE_LAZY": "0", "SG_DENSE_SEED": "16,48", "SG_DENSE_SEED_SW": "16"},
+                                 {"SG_DENSE_LAZY": "0", "SG_DENSE_SEED": "8,24,100", "SG_DENSE_SEED_SW": "32",
+                                  "SG_DENSE_SW": "8", "SG_DENSE_THREADS": "512"}])
+def test_dense_search_forms(oracle, ctx, monkeypatch, env, request):
+    """The dense search's forms (sg_dense.hip): the lazy search (the default: rows resumed where
+    they stopped, whole chunks or cut at the threshold, 4 to 16 lanes per row, 2 or 4 rows in
+    flight, 256 or 512 threads) and the T-cut search with seed rows (SG_DENSE_LAZY=0,
+    SG_DENSE_SEED: a first launch computes the block's first rows, the second starts every row's
+    keys at bounds from its nearest seed row).
+    A complete graph with coarse latencies (ties decided by loss) on all rows, a shuffled used
+    subset and a row block into a zeroed buffer; the directed copy with unsorted 700-arc hubs
+    (relaxed whole; a seed row is the first marked arc, not the lightest); latencies past 2^32 ns
+    (saturated rows, finished by the wide kernel); the 1,200-node C2 graph; bit-exact every cell.
+    The T-cut search under its defaults (one seed launch of n_cu rows from 2 n_cu rows on: the
+    300-node cases run unseeded), no seeds, 1 to 150 seed rows, two and three levels."""
+    _dense_once(request)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = synth.complete_graph(300, seed=31)
+    g["lat"] = (g["lat"] // 10**7 + 1) * 10**7
+    g["loss"] = np.where(np.arange(len(g["loss"])) % 4 == 0, np.float32(0.03), g["loss"]).astype(np.float32)
+    _check(oracle, g, np.arange(300, dtype=np.uint32), ctx)
+    _check(oracle, g, np.random.default_rng(31).permutation(300)[:290].astype(np.uint32), ctx)
+    _check(oracle, g, np.arange(300, dtype=np.uint32), ctx, rows=(7, 300), poison=True)
+    rng = np.random.default_rng(32)
+    hub = np.repeat(np.array([0, 1, 150, 299], dtype=g["src"].dtype), 700)
+    tail = rng.integers(0, 300, len(hub)).astype(g["dst"].dtype)
+    keep = hub != tail
+    hub, tail = hub[keep], tail[keep]
+    rv = g["src"] != g["dst"]
+    g2 = dict(g, directed=True, src=np.concatenate([g["src"], g["dst"][rv], hub]),
+              dst=np.concatenate([g["dst"], g["src"][rv], tail]),
+              lat=np.concatenate([g["lat"], g["lat"][rv], rng.integers(10**6, 4 * 10**8, len(hub)).astype(np.uint64)]),
+              loss=np.concatenate([g["loss"], g["loss"][rv],
+                                   np.where(rng.random(len(hub)) < 0.5, 0.0, 0.01).astype(np.float32)]))
+    _check(oracle, g2, np.arange(300, dtype=np.uint32), ctx)
+    g3 = dict(g, lat=(rng.integers(1_000_000, 9_000_000, len(g["lat"])) * 1000).astype(np.uint64))
+    lat, _ = _check(oracle, g3, np.arange(300, dtype=np.uint32), ctx)
+    assert lat.max() >= (1 << 32)
+    _check(oracle, synth.complete_graph(1200, seed=2), np.arange(1200, dtype=np.uint32), ctx)
+
+
 @pytest.mark.parametrize("case", ["ties", "wide", "parallel_directed", "used_subset", "tiny_wmin"])
 def test_dense_graph_cases(oracle, ctx, case, request):
     """Dense graphs (mean out-degree past 64: the register-resident search of sg_dense.hip under
