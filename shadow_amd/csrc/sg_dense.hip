@@ -410,6 +410,11 @@ __global__ void __launch_bounds__(TH) k_sssp_dense(const uint32_t* __restrict__ 
 // it.  Each row relaxes only its arcs below the largest final key plus w_min: C2 ~11k arcs per
 // source against ~88k under the T cut (~15k with seed rows), in one launch without seed rows.
 // A row past the sort's `cap` (sorted[u] = 0, nxt = 0: listed at once) is relaxed whole.
+#ifdef DN_PROF
+// diagnostic build only (-DDN_PROF): per-phase wall-clock totals of the lazy search, 10-ns ticks:
+// init, listing, relaxation, settling, write-out, rounds, rows listed, whole row
+__device__ unsigned long long g_dn_prof[8];
+#endif
 template <int TH, uint32_t SW, int G, bool SPEC>
 __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restrict__ out_off,
                                                         const uint32_t* __restrict__ sa,
@@ -440,6 +445,9 @@ __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restri
   const uint32_t src = used[row];
   const uint32_t wmin = *wmin_p;  // >= 1 (graph/mod.rs:105-107); LAT32_SAT: no arc at all
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)sa, 0, (int)0x7FFFFFFF, 0x00020000);
+#ifdef DN_PROF
+  const unsigned long long pt_start = wall_clock64();
+#endif
   for (uint32_t v = t; v < n; v += TH) {
     key[v] = v == src ? 0ull : KEY_INF;  // default() at the source
     const uint32_t a0 = out_off[v], e0 = out_off[v + 1];
@@ -453,6 +461,13 @@ __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restri
   unsigned long long n_rel = 0;
   uint32_t m = 0, me = LAT32_SAT, un = 1;  // the source: the only key, unsettled
   __syncthreads();
+#ifdef DN_PROF
+  unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tq = wall_clock64(), t0q = tq;
+  pt[0] = tq - pt_start;
+#define DN_MARK(k) do { const unsigned long long q_ = wall_clock64(); pt[k] += q_ - tq; tq = q_; } while (0)
+#else
+#define DN_MARK(k) do {} while (0)
+#endif
   for (;;) {
     const uint32_t base = min(m, me);
     // (uniform) every node settled, or nothing left below LAT32_SAT (unreachable or saturated
@@ -480,6 +495,11 @@ __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restri
     }
     __syncthreads();
     const uint32_t nl = s_cnt;
+    DN_MARK(1);
+#ifdef DN_PROF
+    pt[5] += 1;
+    pt[6] += nl;
+#endif
     // 2. relax them up to thr: SW lanes per row, G * NGR rows per wave side by side
     uint32_t mo = LAT32_SAT;
     for (uint32_t s0 = wv * G * NGR; s0 < nl; s0 += TW * G * NGR) {
@@ -529,28 +549,39 @@ __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restri
           }
           const uint64_t bin = __ballot(in);
           if (work) n_rel += __popcll(bin);
+          // where the row stops, written by the lane that holds it (no cross-lane moves: masks only)
           const uint32_t sh = gi * SW;
           bool more;
-          uint32_t p_at, n_at;  // where the row stops and a lower bound of that arc's latency
           if (SPEC) {
-            const uint32_t lat_l = (uint32_t)__shfl((int)r[g].y, (int)(sh + SW - 1), 64);
+            // the next chunk while this one is full and its last arc within budget; stopping, the
+            // last lane records ptr = the chunk's end and nxt = its own latency (a lower bound of
+            // the next arc's)
             const bool full = a[g] + SW < e[g];
-            more = full && lat_l <= budget[g];
-            p_at = full ? a[g] + SW : e[g];
-            n_at = full ? lat_l : LAT32_SAT;
+            const uint64_t inb = __ballot(r[g].y <= budget[g]);
+            more = full && (inb >> (sh + SW - 1) & 1u);
+            if (!more && a[g] < e[g]) {
+              if (full && gl == SW - 1) {
+                ptr[u[g]] = a[g] + SW;
+                nxt[u[g]] = r[g].y;
+              } else if (!full && gl == 0) {
+                ptr[u[g]] = e[g];
+                nxt[u[g]] = LAT32_SAT;
+              }
+            }
           } else {
             // the group's first arc past the budget (its arcs are sorted: the in-lanes are a prefix)
             const uint64_t gmask = (SW == 64 ? ~0ull : ((1ull << SW) - 1ull)) << sh;
             const uint64_t stop = __ballot(i < e[g] && !in) & gmask;
-            const uint32_t fl = stop ? (uint32_t)__builtin_ctzll(stop) : sh;
-            const uint32_t lat_f = (uint32_t)__shfl((int)r[g].y, (int)fl, 64);
             more = !stop && a[g] + SW < e[g];
-            p_at = stop ? a[g] + (fl - sh) : e[g];
-            n_at = stop ? lat_f : LAT32_SAT;
-          }
-          if (!more && a[g] < e[g] && gl == 0) {  // where the row stopped
-            ptr[u[g]] = p_at;
-            nxt[u[g]] = n_at;
+            if (stop) {
+              if (lane == (uint32_t)__builtin_ctzll(stop)) {
+                ptr[u[g]] = i;
+                nxt[u[g]] = r[g].y;
+              }
+            } else if (!more && a[g] < e[g] && gl == 0) {
+              ptr[u[g]] = e[g];
+              nxt[u[g]] = LAT32_SAT;
+            }
           }
           a[g] = more ? a[g] + SW : e[g];
           more_any |= __ballot(more);
@@ -561,6 +592,7 @@ __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restri
     for (int d = 32; d > 0; d >>= 1) mo = min(mo, (uint32_t)__shfl_xor(mo, d, 64));
     if (lane == 0 && mo < LAT32_SAT) atomicMin(&s_mo, mo);
     __syncthreads();
+    DN_MARK(2);
     // 3. settle below min(thr, m2 + w_min); the next m (unsettled keys) and me (settled rows)
     const uint32_t m2 = s_mo;
     const uint32_t thr2 = min(thr, m2 + wmin >= m2 ? m2 + wmin : LAT32_SAT);
@@ -590,10 +622,18 @@ __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restri
     me = s_me;
     un = s_un;
     __syncthreads();  // (s_m / s_me are reset by the next round's listing)
+    DN_MARK(3);
   }
   if (work && lane == 0 && n_rel) atomicAdd(&work[blockIdx.x & 63], n_rel);
   dense_write_row<TH>(key, src, row, used, n_used, self_edge, e_lat, e_loss, out_lat + (size_t)blockIdx.x * n_used,
                       out_loss + (size_t)blockIdx.x * n_used, sat_row + blockIdx.x);
+#ifdef DN_PROF
+  DN_MARK(4);
+  pt[7] = tq - t0q;
+  if (t == 0)
+    for (int k = 0; k < 8; k++) atomicAdd(&g_dn_prof[k], pt[k]);
+#endif
+#undef DN_MARK
 }
 
 bool sssp_dense_fits(uint32_t n) { return n > 0 && n <= DENSE_MAX; }
@@ -690,18 +730,24 @@ void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_
                        work, dense_split_below(th / 64), sd);
     SG_CHECK_LAUNCH();
   };
-  // the lazy search (default; SG_DENSE_LAZY=0: the T-cut search with seed rows).  C2 (r6,
+  // the lazy search (default; SG_DENSE_LAZY=0: the T-cut search with seed rows).  Latency-bound:
+  // 64 rows take 75 us at 256 threads (50 at 512), all 1,200 92 us (106 at 512: past the 32
+  // waves per CU); per row at 1,200 rows, 256 threads (a -DDN_PROF build): init 3.6 us, listing
+  // 11.8, relaxation 61.1, settling 12.8, write-out 5.7 over 8 rounds and ~2,000 listed rows.  A
+  // scheduling barrier that issues both rows' loads before the first use measured 0.127 ms against
+  // 0.124 (not kept).  C2 (r6,
   // `profiles/r06/ab_c2_lazy_r6.txt`): T cut 0.297 ms, with 256 seed rows 0.190; lazy 512 threads x
   // 8 lanes 0.171, 256 x 4 0.151; lazy whole chunks (SG_DENSE_SPEC) 256 x 4 0.130, 256 x 8 0.124,
   // 256 x 16 0.126, 512 x 8 0.136; 4 rows in flight per lane group (SG_DENSE_G=4) 0.132-0.136
   if (dense_env("SG_DENSE_LAZY", 1)) {
-    const int th = dense_env("SG_DENSE_THREADS", 256) == 512 ? 512 : 256;
+    const int th0 = dense_env("SG_DENSE_THREADS", 256), th = th0 == 512 || th0 == 384 ? th0 : 256;
     const int sw = dense_env("SG_DENSE_SW", 8), gg = dense_env("SG_DENSE_G", 2) == 4 ? 4 : 2;
     const bool spec = dense_env("SG_DENSE_SPEC", 1) != 0;
 #define SG_LAZY_K(T_, S_, G_) (spec ? k_sssp_dense_lazy<T_, S_, G_, true> : k_sssp_dense_lazy<T_, S_, G_, false>)
     auto pick = [&](auto k4, auto k8, auto k16) { return sw == 4 ? k4 : sw == 16 ? k16 : k8; };
     auto kern = th == 256 ? (gg == 4 ? pick(SG_LAZY_K(256, 4, 4), SG_LAZY_K(256, 8, 4), SG_LAZY_K(256, 16, 4))
                                      : pick(SG_LAZY_K(256, 4, 2), SG_LAZY_K(256, 8, 2), SG_LAZY_K(256, 16, 2)))
+              : th == 384 ? pick(SG_LAZY_K(384, 4, 2), SG_LAZY_K(384, 8, 2), SG_LAZY_K(384, 16, 2))
                           : (gg == 4 ? pick(SG_LAZY_K(512, 4, 4), SG_LAZY_K(512, 8, 4), SG_LAZY_K(512, 16, 4))
                                      : pick(SG_LAZY_K(512, 4, 2), SG_LAZY_K(512, 8, 2), SG_LAZY_K(512, 16, 2)));
 #undef SG_LAZY_K
@@ -712,6 +758,18 @@ void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_
                        n, (const uint32_t*)wmin, d_used, n_used, row_begin, net->self_edge, net->e_lat, net->e_loss,
                        out_lat, out_loss, sat_row, work);
     SG_CHECK_LAUNCH();
+#ifdef DN_PROF
+    {
+      unsigned long long h[8], z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      SG_HIP(hipStreamSynchronize(st));
+      SG_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dn_prof), sizeof(h)));
+      SG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dn_prof), z, sizeof(z)));
+      const double r = rows ? (double)rows : 1.0;
+      fprintf(stderr, "dense_prof rows %u per row (us): init %.2f list %.2f relax %.2f settle %.2f write %.2f "
+              "whole %.2f rounds %.2f listed %.1f\n", rows, h[0] / r / 100, h[1] / r / 100, h[2] / r / 100,
+              h[3] / r / 100, h[4] / r / 100, h[7] / r / 100 + h[0] / r / 100, h[5] / r, h[6] / r);
+    }
+#endif
     return;
   }
   const std::vector<uint32_t> lv = dense_seed_levels(rows, (uint32_t)std::max(1, ctx->n_cu));
