@@ -415,7 +415,7 @@ __global__ void __launch_bounds__(TH) k_sssp_dense(const uint32_t* __restrict__ 
 // init, listing, relaxation, settling, write-out, rounds, rows listed, whole row
 __device__ unsigned long long g_dn_prof[8];
 #endif
-template <int TH, uint32_t SW, int G, bool SPEC>
+template <int TH, uint32_t SW, int G, bool SPEC, bool RTN = false>
 __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restrict__ out_off,
                                                         const uint32_t* __restrict__ sa,
                                                         const uint8_t* __restrict__ sorted, uint32_t n,
@@ -541,11 +541,22 @@ __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restri
           // that only come early), and the next chunk while this one's last arc is within budget
           const bool in = i < e[g] && (SPEC || r[g].y <= budget[g]);
           const uint64_t cd = relax32(ku[g], r[g].y, __uint_as_float(r[g].z));
-          const bool offer = in && key_lat(cd) != LAT32_SAT && !(settled[r[g].x >> 5] >> (r[g].x & 31) & 1u);
-          if (offer) {
-            (void)__hip_atomic_fetch_min(&key[r[g].x], (unsigned long long)cd, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_WORKGROUP);
-            mo = min(mo, key_lat(cd));
+          if (RTN) {
+            // no settled-bit read ahead of the atomic: a settled node's key is final, so no real
+            // path's candidate lowers it; the returned key tells an improvement (an unsettled
+            // node), which alone may lower m
+            if (in && key_lat(cd) != LAT32_SAT) {
+              const unsigned long long old = __hip_atomic_fetch_min(&key[r[g].x], (unsigned long long)cd,
+                                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              if (cd < old) mo = min(mo, key_lat(cd));
+            }
+          } else {
+            const bool offer = in && key_lat(cd) != LAT32_SAT && !(settled[r[g].x >> 5] >> (r[g].x & 31) & 1u);
+            if (offer) {
+              (void)__hip_atomic_fetch_min(&key[r[g].x], (unsigned long long)cd, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+              mo = min(mo, key_lat(cd));
+            }
           }
           const uint64_t bin = __ballot(in);
           if (work) n_rel += __popcll(bin);
@@ -735,17 +746,22 @@ void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_
   // waves per CU); per row at 1,200 rows, 256 threads (a -DDN_PROF build): init 3.6 us, listing
   // 11.8, relaxation 61.1, settling 12.8, write-out 5.7 over 8 rounds and ~2,000 listed rows.  A
   // scheduling barrier that issues both rows' loads before the first use measured 0.127 ms against
-  // 0.124 (not kept).  C2 (r6,
+  // 0.124 (not kept).  384 threads (6 waves; 1,200 rows still fit 32 waves per CU) 0.121-0.123
+  // against 0.126-0.127 for 256; the atomic's returned key instead of a settled-bit read ahead
+  // of it (SG_DENSE_RTN, default) 0.125 against 0.126 (`profiles/r06/ab_c2_lazy_r6.txt`)  C2 (r6,
   // `profiles/r06/ab_c2_lazy_r6.txt`): T cut 0.297 ms, with 256 seed rows 0.190; lazy 512 threads x
   // 8 lanes 0.171, 256 x 4 0.151; lazy whole chunks (SG_DENSE_SPEC) 256 x 4 0.130, 256 x 8 0.124,
   // 256 x 16 0.126, 512 x 8 0.136; 4 rows in flight per lane group (SG_DENSE_G=4) 0.132-0.136
   if (dense_env("SG_DENSE_LAZY", 1)) {
-    const int th0 = dense_env("SG_DENSE_THREADS", 256), th = th0 == 512 || th0 == 384 ? th0 : 256;
+    const int th0 = dense_env("SG_DENSE_THREADS", 384), th = th0 == 512 || th0 == 256 ? th0 : 384;
     const int sw = dense_env("SG_DENSE_SW", 8), gg = dense_env("SG_DENSE_G", 2) == 4 ? 4 : 2;
     const bool spec = dense_env("SG_DENSE_SPEC", 1) != 0;
 #define SG_LAZY_K(T_, S_, G_) (spec ? k_sssp_dense_lazy<T_, S_, G_, true> : k_sssp_dense_lazy<T_, S_, G_, false>)
     auto pick = [&](auto k4, auto k8, auto k16) { return sw == 4 ? k4 : sw == 16 ? k16 : k8; };
-    auto kern = th == 256 ? (gg == 4 ? pick(SG_LAZY_K(256, 4, 4), SG_LAZY_K(256, 8, 4), SG_LAZY_K(256, 16, 4))
+    const bool rtn = dense_env("SG_DENSE_RTN", 1) != 0 && spec && sw == 8 && gg == 2;
+    auto kern = rtn ? (th == 384 ? k_sssp_dense_lazy<384, 8, 2, true, true> : th == 512 ? k_sssp_dense_lazy<512, 8, 2, true, true>
+                                                                               : k_sssp_dense_lazy<256, 8, 2, true, true>)
+              : th == 256 ? (gg == 4 ? pick(SG_LAZY_K(256, 4, 4), SG_LAZY_K(256, 8, 4), SG_LAZY_K(256, 16, 4))
                                      : pick(SG_LAZY_K(256, 4, 2), SG_LAZY_K(256, 8, 2), SG_LAZY_K(256, 16, 2)))
               : th == 384 ? pick(SG_LAZY_K(384, 4, 2), SG_LAZY_K(384, 8, 2), SG_LAZY_K(384, 16, 2))
                           : (gg == 4 ? pick(SG_LAZY_K(512, 4, 4), SG_LAZY_K(512, 8, 4), SG_LAZY_K(512, 16, 4))

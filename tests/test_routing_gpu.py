@@ -510,7 +510,8 @@ def test_dense_row_split(oracle, ctx, monkeypatch, split):
     _check(oracle, g2, np.arange(300, dtype=np.uint32), ctx)
 
 
-@pytest.mark.parametrize("env", [{}, {"SG_DENSE_SPEC": "0"}, {"SG_DENSE_SW": "4", "SG_DENSE_G": "4"},
+@pytest.mark.parametrize("env", [{}, {"SG_DENSE_RTN": "0"}, {"SG_DENSE_THREADS": "256"},
+                                 {"SG_DENSE_SPEC": "0"}, {"SG_DENSE_SW": "4", "SG_DENSE_G": "4"},
                                  {"SG_DENSE_SW": "16", "SG_DENSE_THREADS": "512", "SG_DENSE_SPEC": "0"},
                                  {"SG_DENSE_LAZY": "0"}, {"SG_DENSE_LAZY": "0", "SG_DENSE_SEED": "0"},
                                  {"SG_DENSE_LAZY": "0", "SG_DENSE_SEED": "1"}, {"SG_DENSE_LAZY": "0", "SG_DENSE_SEED": "64"},
@@ -522,7 +523,7 @@ def test_dense_row_split(oracle, ctx, monkeypatch, split):
 def test_dense_search_forms(oracle, ctx, monkeypatch, env, request):
     """The dense search's forms (sg_dense.hip): the lazy search (the default: rows resumed where
     they stopped, whole chunks or cut at the threshold, 4 to 16 lanes per row, 2 or 4 rows in
-    flight, 256 or 512 threads) and the T-cut search with seed rows (SG_DENSE_LAZY=0,
+    flight, 256, 384 or 512 threads, the atomic's returned key or a settled-bit read) and the T-cut search with seed rows (SG_DENSE_LAZY=0,
     SG_DENSE_SEED: a first launch computes the block's first rows, the second starts every row's
     keys at bounds from its nearest seed row).
     A complete graph with coarse latencies (ties decided by loss) on all rows, a shuffled used
