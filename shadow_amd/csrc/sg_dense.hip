@@ -747,13 +747,16 @@ void launch_sssp_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_
   // 11.8, relaxation 61.1, settling 12.8, write-out 5.7 over 8 rounds and ~2,000 listed rows.  A
   // scheduling barrier that issues both rows' loads before the first use measured 0.127 ms against
   // 0.124 (not kept).  384 threads (6 waves; 1,200 rows still fit 32 waves per CU) 0.121-0.123
-  // against 0.126-0.127 for 256; the atomic's returned key instead of a settled-bit read ahead
-  // of it (SG_DENSE_RTN, default) 0.125 against 0.126 (`profiles/r06/ab_c2_lazy_r6.txt`)  C2 (r6,
+  // against 0.126-0.127 for 256 (rocprof 92 against ~97 us per rebuild launch), but its HIP-event
+  // pair behind bench.py's spin kernel reads 0.118 ms, 26 us over the trace, so the line's
+  // roofline would not match the profile: 256 stays the default.  The atomic's returned key
+  // instead of a settled-bit read ahead of it (SG_DENSE_RTN, default) 0.125 against 0.126
+  // (`profiles/r06/ab_c2_lazy_r6.txt`)  C2 (r6,
   // `profiles/r06/ab_c2_lazy_r6.txt`): T cut 0.297 ms, with 256 seed rows 0.190; lazy 512 threads x
   // 8 lanes 0.171, 256 x 4 0.151; lazy whole chunks (SG_DENSE_SPEC) 256 x 4 0.130, 256 x 8 0.124,
   // 256 x 16 0.126, 512 x 8 0.136; 4 rows in flight per lane group (SG_DENSE_G=4) 0.132-0.136
   if (dense_env("SG_DENSE_LAZY", 1)) {
-    const int th0 = dense_env("SG_DENSE_THREADS", 384), th = th0 == 512 || th0 == 256 ? th0 : 384;
+    const int th0 = dense_env("SG_DENSE_THREADS", 256), th = th0 == 512 || th0 == 384 ? th0 : 256;
     const int sw = dense_env("SG_DENSE_SW", 8), gg = dense_env("SG_DENSE_G", 2) == 4 ? 4 : 2;
     const bool spec = dense_env("SG_DENSE_SPEC", 1) != 0;
 #define SG_LAZY_K(T_, S_, G_) (spec ? k_sssp_dense_lazy<T_, S_, G_, true> : k_sssp_dense_lazy<T_, S_, G_, false>)

@@ -510,7 +510,7 @@ def test_dense_row_split(oracle, ctx, monkeypatch, split):
     _check(oracle, g2, np.arange(300, dtype=np.uint32), ctx)
 
 
-@pytest.mark.parametrize("env", [{}, {"SG_DENSE_RTN": "0"}, {"SG_DENSE_THREADS": "256"},
+@pytest.mark.parametrize("env", [{}, {"SG_DENSE_RTN": "0"}, {"SG_DENSE_THREADS": "384"},
                                  {"SG_DENSE_SPEC": "0"}, {"SG_DENSE_SW": "4", "SG_DENSE_G": "4"},
                                  {"SG_DENSE_SW": "16", "SG_DENSE_THREADS": "512", "SG_DENSE_SPEC": "0"},
                                  {"SG_DENSE_LAZY": "0"}, {"SG_DENSE_LAZY": "0", "SG_DENSE_SEED": "0"},
