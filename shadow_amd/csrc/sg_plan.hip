@@ -508,7 +508,8 @@ SsspDevPlan sssp_device_plan(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
   hipStream_t st = ctx->stream;
   {
     TimedLaunch tl(ctx, "plan_sets", 0.0);
-    SG_HIP(hipMemsetAsync(rel, 0xff, (size_t)n * 4, st));
+    // rel of a node outside the block's rows reads ~0; a block of all n rows writes every entry
+    if (rows != n) SG_HIP(hipMemsetAsync(rel, 0xff, (size_t)n * 4, st));
     const unsigned g = grid_for(rows, 256);
     hipLaunchKernelGGL(k_plan_rel, dim3(g), dim3(256), 0, st, d_used, row_begin, rows, rel, jn, zero_rows, zero_rows2);
     // in-neighbours: the CSC when directed; the out-arcs themselves when undirected
