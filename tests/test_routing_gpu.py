@@ -559,6 +559,19 @@ def test_dense_search_forms(oracle, ctx, monkeypatch, env, request):
     _check(oracle, synth.complete_graph(1200, seed=2), np.arange(1200, dtype=np.uint32), ctx)
 
 
+def test_dense_at_size_limit(oracle, ctx, request):
+    """The dense search at its size limit (DENSE_MAX = 4,096 nodes: 96 KB of LDS per row, one row
+    per CU) on a 140-arcs-per-node graph with coarse latencies (ties by loss): the whole table,
+    and a row block of a shuffled used subset into a zeroed buffer; bit-exact."""
+    _dense_once(request)
+    g = synth.ring_chords_graph(4096, 140.0, seed=77)
+    g["lat"] = (g["lat"] // 10**6 + 1) * 10**6
+    assert len(g["src"]) * 2 > 64 * 4096  # dense: more than 64 arcs per node
+    _check(oracle, g, np.arange(4096, dtype=np.uint32), ctx)
+    used = np.random.default_rng(77).permutation(4096)[:3000].astype(np.uint32)
+    _check(oracle, g, used, ctx, rows=(500, 2600), poison=True)
+
+
 @pytest.mark.parametrize("case", ["ties", "wide", "parallel_directed", "used_subset", "tiny_wmin"])
 def test_dense_graph_cases(oracle, ctx, case, request):
     """Dense graphs (mean out-degree past 64: the register-resident search of sg_dense.hip under
