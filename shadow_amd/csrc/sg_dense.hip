@@ -397,17 +397,19 @@ __global__ void __launch_bounds__(TH) k_sssp_dense(const uint32_t* __restrict__ 
 // threshold only, and resumed in later rounds where it stopped (its arcs are sorted: ptr = the
 // first arc not yet relaxed, nxt = that arc's latency, both in LDS).  A round, from
 // m = the smallest unsettled key and me = the smallest key(u).lat + nxt[u] of the settled rows:
-//   1. thr = min(m, me) + w_min; list the settled rows with key(u).lat + nxt[u] < thr;
+//   1. thr = min(m, me) + w_min (m + w_min after a round that settled nothing; me + a doubling
+//      budget while no key below LAT32_SAT is unsettled); list the settled rows with
+//      key(u).lat + nxt[u] < thr;
 //   2. relax them, SW lanes per row, over their arcs with key(u).lat + w < thr, and record where
 //      each stopped; m2 = min(m, the smallest latency offered to an unsettled node);
 //   3. settle every unsettled v with key(v).lat < min(thr, m2 + w_min); the scan also gives the
 //      next round's m and me.
 // Step 3 is Dijkstra's rule: a path to v other than its key leaves the settled set over an arc
 // not yet relaxed (latency >= thr, every arc below thr having been relaxed) or through an
-// unsettled x != v (latency >= key(x).lat + w_min >= m2 + w_min).  Each round settles the node of
-// key m2 (or advances the row of key(u) + nxt[u] = me), so the search ends; it ends when no key
-// below LAT32_SAT is left unsettled and no settled row has an arc left whose candidate stays below
-// it.  Each row relaxes only its arcs below the largest final key plus w_min: C2 ~11k arcs per
+// unsettled x != v (latency >= key(x).lat + w_min >= m2 + w_min).  Of two rounds in a row with m
+// below LAT32_SAT one settles a node; a round without relaxes rows from me over a doubling
+// budget -- so the search ends, when every node is settled or no key below LAT32_SAT is left unsettled and no
+// settled row has an arc left whose candidate stays below it.  Each row relaxes only its arcs below the largest final key plus w_min: C2 ~11k arcs per
 // source against ~88k under the T cut (~15k with seed rows), in one launch without seed rows.
 // A row past the sort's `cap` (sorted[u] = 0, nxt = 0: listed at once) is relaxed whole.
 #ifdef DN_PROF
@@ -438,7 +440,7 @@ __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restri
   uint32_t* lst = nxt + n;                              // [n] this round's rows to relax
   uint32_t* settled = lst + n;                          // [ceil(n / 32)] bitmap
   const uint32_t nbw = (n + 31) / 32;
-  __shared__ uint32_t s_cnt, s_mo, s_m, s_me, s_un;
+  __shared__ uint32_t s_cnt, s_mo, s_m, s_me, s_un, s_new;
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t gl = lane % SW, gi = lane / SW;
   const uint32_t row = row_begin + blockIdx.x;
@@ -460,6 +462,8 @@ __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restri
   if (t == 0) s_cnt = 0;
   unsigned long long n_rel = 0;
   uint32_t m = 0, me = LAT32_SAT, un = 1;  // the source: the only key, unsettled
+  uint32_t k_far = 0;   // rounds in a row with no unsettled key below LAT32_SAT (see thr below)
+  uint32_t settled_any = 1;  // the last round settled a node
   __syncthreads();
 #ifdef DN_PROF
   unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tq = wall_clock64(), t0q = tq;
@@ -473,7 +477,25 @@ __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restri
     // (uniform) every node settled, or nothing left below LAT32_SAT (unreachable or saturated
     // keys: the wide kernel's)
     if (!un || base == LAT32_SAT) break;
-    const uint32_t thr = base + wmin >= base ? base + wmin : LAT32_SAT;
+    // The relaxation threshold.  Any thr works for exactness (every arc below it is relaxed
+    // before the settling rule uses it); it is chosen for progress.  With an unsettled key m:
+    // thr = min(m, me) + w_min, or m + w_min after a round that settled nothing -- then the node
+    // of key m2 <= m settles, so there are at most 2n such rounds.  With none (m = LAT32_SAT: the
+    // nodes left are unreached so far), the rows' next arcs from me on are relaxed over a budget
+    // that doubles each such round in a row: at most ~32 of them before the whole rest is
+    // relaxed.  (thr = min(m, me) + w_min alone took one round per distinct candidate value on a
+    // graph whose far nodes are reached over long arcs and a 1-ns w_min; m + w_min every round
+    // cost C2 0.130 ms against 0.125.)
+    uint32_t thr;
+    if (m != LAT32_SAT) {
+      const uint32_t b = settled_any ? base : m;
+      thr = b + wmin >= b ? b + wmin : LAT32_SAT;
+      k_far = 0;
+    } else {
+      const uint64_t x = (uint64_t)wmin << min(k_far, 32u);
+      thr = (uint32_t)min((uint64_t)me + x, (uint64_t)LAT32_SAT);
+      k_far++;
+    }
     // 1. the settled rows with an arc below thr
     for (uint32_t v0 = wv * 64; v0 < n; v0 += TH) {
       const uint32_t v = v0 + lane;
@@ -492,6 +514,7 @@ __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restri
       s_m = LAT32_SAT;
       s_me = LAT32_SAT;
       s_un = 0;
+      s_new = 0;
     }
     __syncthreads();
     const uint32_t nl = s_cnt;
@@ -614,6 +637,7 @@ __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restri
       if (!st && l < thr2) {
         atomicOr(&settled[v >> 5], 1u << (v & 31));
         st = true;
+        s_new = 1u;  // (benign race, as s_un)
       }
       if (st) men = min(men, __builtin_elementwise_add_sat(l, nxt[v]));
       else mn = min(mn, l);
@@ -632,6 +656,7 @@ __global__ void __launch_bounds__(TH) k_sssp_dense_lazy(const uint32_t* __restri
     m = s_m;
     me = s_me;
     un = s_un;
+    settled_any = s_new;
     __syncthreads();  // (s_m / s_me are reset by the next round's listing)
     DN_MARK(3);
   }

@@ -572,17 +572,36 @@ def test_dense_at_size_limit(oracle, ctx, request):
     _check(oracle, g, used, ctx, rows=(500, 2600), poison=True)
 
 
-@pytest.mark.parametrize("case", ["ties", "wide", "parallel_directed", "used_subset", "tiny_wmin"])
+@pytest.mark.parametrize("case", ["ties", "wide", "parallel_directed", "used_subset", "tiny_wmin",
+                                  "far_tiny_wmin"])
 def test_dense_graph_cases(oracle, ctx, case, request):
     """Dense graphs (mean out-degree past 64: the register-resident search of sg_dense.hip under
     the LDS fixtures, the slab under `slab`): equal-latency paths decided by loss, latencies past
     2^32 ns (wide rows), parallel arcs in a directed graph, a used-node subset with rows and
-    columns in a shuffled order, and 1-ns arcs (one-node rounds)."""
+    columns in a shuffled order, 1-ns arcs (one-node rounds), and a directed graph with a 1-ns
+    smallest arc and latencies spread to 1 ms whose last 40 nodes are reached over 100-200 ms arcs
+    only: the lazy search's rounds with every reached key settled and the far nodes not yet reached
+    (a relaxation budget that doubles; stepping by w_min took one round per distinct candidate
+    value)."""
     _dense_once(request)
     rng = np.random.default_rng(sum(map(ord, case)))
     n = 520
     if case == "parallel_directed":
         g = synth.ring_chords_graph(n, 150.0, seed=5, directed=True, parallel=0.2)
+    elif case == "far_tiny_wmin":
+        m = 100 * n
+        src, dst = rng.integers(0, n, m), rng.integers(0, n, m)
+        keep = src != dst
+        src, dst = src[keep], dst[keep]
+        lat = rng.integers(1, 10**6, len(src)).astype(np.uint64)
+        lat[0] = 1
+        far = dst >= n - 40  # the last 40 nodes are reached over 100-200 ms arcs only
+        lat[far] = rng.integers(10**8, 2 * 10**8, int(far.sum()))
+        src = np.concatenate([src, np.arange(n)]).astype(np.uint32)  # + one self-loop each
+        dst = np.concatenate([dst, np.arange(n)]).astype(np.uint32)
+        lat = np.concatenate([lat, np.full(n, 10**6, np.uint64)])
+        loss = np.where(rng.random(len(src)) < 0.5, 0.0, 0.01).astype(np.float32)
+        g = dict(n=n, src=src, dst=dst, lat=lat, loss=loss, directed=True)
     else:
         g = synth.ring_chords_graph(n, 180.0, seed=6)
     if case == "ties":
@@ -599,6 +618,8 @@ def test_dense_graph_cases(oracle, ctx, case, request):
     lat, _ = _check(oracle, g, used, ctx)
     if case == "wide":
         assert lat.max() >= (1 << 32)
+    if case == "far_tiny_wmin":
+        assert lat[: n - 40, n - 40:].min() >= 10**8
 
 
 @pytest.mark.parametrize("env", [{"SG_BUCKET_DELTA": "4000000000"}, {"SG_BUCKET_DELTA": "4096"},
