@@ -559,6 +559,51 @@ def test_dense_search_forms(oracle, ctx, monkeypatch, env, request):
     _check(oracle, synth.complete_graph(1200, seed=2), np.arange(1200, dtype=np.uint32), ctx)
 
 
+@pytest.mark.parametrize("env", [{}, {"SG_DENSE_SPEC": "0"}, {"SG_DENSE_SW": "4"}, {"SG_DENSE_SW": "16", "SG_DENSE_THREADS": "512"},
+                                 {"SG_DENSE_RTN": "0", "SG_DENSE_THREADS": "384"}])
+def test_dense_fuzz(oracle, ctx, monkeypatch, env, request):
+    """Random dense graphs through the lazy search's forms: 70-400 nodes, 65-220 arcs per node,
+    directed or not, latencies wide (1 ns - 100 ms), coarse (ties decided by loss) or tiny (1-9 ns),
+    parallel arcs, a few nodes reached over long arcs only, hubs with more arcs than the sort's LDS
+    array (unsorted rows), losses of 0, 1 and in between; every cell bit-exact."""
+    _dense_once(request)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(4242)
+    for case in range(8):
+        n = int(rng.integers(70, 400))
+        deg = float(rng.integers(65, 220))
+        directed = bool(case % 2)
+        m = int(n * deg / (1 if directed else 2))
+        src, dst = rng.integers(0, n, m), rng.integers(0, n, m)
+        if case % 4 == 3:  # hubs past the sort's array: 1.5 n arcs each
+            hub = rng.choice(n, 3, replace=False)
+            src = np.r_[src, np.repeat(hub, int(1.5 * n))]
+            dst = np.r_[dst, rng.integers(0, n, 3 * int(1.5 * n))]
+        keep = src != dst
+        src, dst = src[keep], dst[keep]
+        kind = case % 3
+        if kind == 0:
+            lat = rng.integers(1, 10**8, len(src))
+        elif kind == 1:
+            lat = rng.integers(1, 6, len(src)) * 10**6
+        else:
+            lat = rng.integers(1, 10, len(src))
+        if case in (2, 5):  # the last 5 nodes reached over long arcs only
+            lat = np.where(dst >= n - 5, rng.integers(10**8, 2 * 10**8, len(src)), lat)
+        loss = rng.choice(np.array([0.0, 0.0, 0.01, 0.3, 1.0], np.float32), len(src))
+        src = np.r_[src, np.arange(n)].astype(np.uint32)  # one self-loop per node
+        dst = np.r_[dst, np.arange(n)].astype(np.uint32)
+        lat = np.r_[lat, np.full(n, 1000)].astype(np.uint64)
+        loss = np.r_[loss, np.zeros(n, np.float32)].astype(np.float32)
+        g = dict(n=n, src=src, dst=dst, lat=lat, loss=loss, directed=directed)
+        if not directed:
+            assert 2 * (len(src) - n) > 64 * n
+        else:
+            assert len(src) - n > 64 * n
+        _check(oracle, g, np.arange(n, dtype=np.uint32), ctx)
+
+
 def test_dense_at_size_limit(oracle, ctx, request):
     """The dense search at its size limit (DENSE_MAX = 4,096 nodes: 96 KB of LDS per row, one row
     per CU) on a 140-arcs-per-node graph with coarse latencies (ties by loss): the whole table,
