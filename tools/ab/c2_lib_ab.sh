@@ -7,7 +7,7 @@ for r in $(seq $REPS); do
       --no-e2e --rank-blocks= --steps 20 2>/dev/null | grep metric > /tmp/ab_c2l.json || { echo "run failed: $lib"; exit 1; }
     python3 -c "
 import json,sys; d=json.load(open('/tmp/ab_c2l.json'))['c2']; r=d['roofline'] or {}
-print(f\"{sys.argv[1]:40s} c2 {d['value']*1e3:.4f} ms one_shot {d['one_shot_s']*1e3:.4f} ms launch {r.get('avg_launch_ms')} rel {r.get('relaxations_per_launch')}\")" $lib >> $OUT
+print(f\"{sys.argv[1]:40s} c2 {d['value']*1e3:.4f} ms one_shot {d['one_shot_s']*1e3:.4f} ms sort {r.get('arc_sort_ms')} launch {r.get('avg_launch_ms')} rel {r.get('relaxations_per_launch')}\")" $lib >> $OUT
   done
 done
 cat $OUT
