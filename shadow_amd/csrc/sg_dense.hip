@@ -5,8 +5,11 @@
 // the sparse searches' range, the per-source petgraph::algo::dijkstra of
 // NetworkGraph::compute_shortest_paths (graph/mod.rs:190-208).
 //
-// One workgroup per source row, its keys in LDS.  The search settles nodes in
-// rounds (Dijkstra with a width) and relaxes only the arcs that can still matter:
+// One workgroup per source row, its keys in LDS.  Two searches: the lazy search
+// (k_sssp_dense_lazy, the default since r6; see "Lazy relaxation" below), and the
+// T-cut search described here (k_sssp_dense; SG_DENSE_LAZY=0, with seed rows).  Both
+// settle nodes in rounds (Dijkstra with a width) and relax only the arcs that can
+// still matter:
 //
 //  * Settling.  A round takes m = the smallest latency of the unsettled keys and
 //    settles every unsettled v with key(v).lat < m + w_min (w_min = the smallest
@@ -63,8 +66,8 @@ constexpr uint32_t DN_W = 4;
 #endif
 
 // Per node u: its out-arcs (out_arc, 3 u32 each: head, latency32, bits(1f32 - loss))
-// sorted by latency into 16-B records {head, latency32, bits(om), 0} at the same
-// offsets; sorted[u] = 1, or 0 for a row past `cap` arcs (copied as is, never cut
+// sorted by latency into 12-B records {head, latency32, bits(om)} (16 B with a pad word
+// under DN_REC16) at the same offsets; sorted[u] = 1, or 0 for a row past `cap` arcs (copied as is, never cut
 // short).  Also the smallest arc latency (w_min).  One block per node; cap = the LDS
 // array (a power of two >= n - 1, at most SORT_MAXDEG: parallel arcs can exceed it).
 constexpr int SORT_THREADS = 1024;
