@@ -1131,8 +1131,57 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
         throw Error(SG_ERR_INVALID_ARG, "Edge 'latency' must not be 0");
     }
   };
+  // one allocation, 256-B aligned sub-arrays; the edge arrays first (their offsets depend on m
+  // only, so they can be staged before the self-loop count sizes the rest)
+  size_t total = 0;
+  // (SG_NET_ALIGN, A/B diagnostics: sub-array alignment in bytes)
+  const size_t align = (size_t)std::max(256, env_int("SG_NET_ALIGN", 256));
+  auto carve = [&](size_t bytes) {
+    const size_t o = total;
+    total += (std::max<size_t>(bytes, 16) + align - 1) / align * align;
+    return o;
+  };
+  const size_t o_esrc = carve(m * 4ull), o_edst = carve(m * 4ull), o_elat = carve(m * 8ull),
+               o_eloss = carve(m * 4ull);
+  const size_t eb = total;  // bytes of the edge arrays, up to the first derived array
+  // Large edge lists (C2's 720k edges): the endpoint check, the self-loop count and the copy
+  // into the pinned staging in one pass split over up to 4 host threads (one thread 349 us,
+  // 4 threads 134 us on the MI355X box's host; tools/debug/stage_thread_probe.cpp).  Small
+  // ones in one thread, where the threads' start-up costs more than they save.
+  // (SG_NET_THREADS: A/B diagnostics, 1 = one thread)
+  const uint32_t n_thr = m >= (1u << 18) ? (uint32_t)std::max(1, std::min(4, env_int("SG_NET_THREADS", 4))) : 1u;
+  char* staged = nullptr;
   uint64_t n_self = 0;
-  {
+  if (n_thr > 1) {
+    staged = stage_acquire(ctx, 0, eb);
+    std::vector<uint32_t> bad_t(n_thr, 0u), ns_t(n_thr, 0u);
+    auto part = [&](uint32_t t) {
+      const uint32_t e0 = (uint32_t)((uint64_t)m * t / n_thr), e1 = (uint32_t)((uint64_t)m * (t + 1) / n_thr);
+      uint32_t bad = 0, ns = 0;
+      for (uint32_t e = e0; e < e1; e++) {
+        const uint32_t a = es[e], b = ed[e];
+        bad |= (uint32_t)(a >= n) | (uint32_t)(b >= n);
+        ns += a == b;
+      }
+      bad_t[t] = bad;
+      ns_t[t] = ns;
+      const size_t c = (size_t)(e1 - e0);
+      memcpy(staged + o_esrc + e0 * 4ull, es + e0, c * 4);
+      memcpy(staged + o_edst + e0 * 4ull, ed + e0, c * 4);
+      memcpy(staged + o_elat + e0 * 8ull, el + e0, c * 8);
+      memcpy(staged + o_eloss + e0 * 4ull, ef + e0, c * 4);
+    };
+    std::vector<std::thread> pool;
+    for (uint32_t t = 1; t < n_thr; t++) pool.emplace_back(part, t);
+    part(0);
+    for (auto& th : pool) th.join();
+    uint32_t bad = 0;
+    for (uint32_t t = 0; t < n_thr; t++) {
+      bad |= bad_t[t];
+      n_self += ns_t[t];
+    }
+    if (bad) name_bad_edge();
+  } else {
     uint32_t bad = 0, ns = 0;
     for (uint32_t e = 0; e < m; e++) {
       const uint32_t a = es[e], b = ed[e];
@@ -1154,17 +1203,7 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   net->directed = g->directed != 0;
   if (g->node_gml_id) net->gml_id.assign(g->node_gml_id, g->node_gml_id + n);
   hipStream_t st = ctx->stream;
-  // one allocation, 256-B aligned sub-arrays
-  size_t total = 0;
-  // (SG_NET_ALIGN, A/B diagnostics: sub-array alignment in bytes)
-  const size_t align = (size_t)std::max(256, env_int("SG_NET_ALIGN", 256));
-  auto carve = [&](size_t bytes) {
-    const size_t o = total;
-    total += (std::max<size_t>(bytes, 16) + align - 1) / align * align;
-    return o;
-  };
-  const size_t o_esrc = carve(m * 4ull), o_edst = carve(m * 4ull), o_elat = carve(m * 8ull),
-               o_eloss = carve(m * 4ull), o_inoff = carve(((size_t)n + 1) * 4), o_scnt = carve((size_t)n * 4),
+  const size_t o_inoff = carve(((size_t)n + 1) * 4), o_scnt = carve((size_t)n * 4),
                o_sedge = carve((size_t)n * 4), o_insrc = carve(n_arcs * 4ull), o_indst = carve(n_arcs * 4ull),
                o_inlat = carve(n_arcs * 8ull), o_inlat32 = carve(n_arcs * 4ull), o_inom = carve(n_arcs * 4ull),
                o_inrec = carve(n_arcs * 16ull), o_outoff = carve(((size_t)n + 1) * 4),
@@ -1205,12 +1244,14 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   net->out_off = (uint32_t*)(base + o_outoff);
   net->out_arc = (uint32_t*)(base + o_outarc);
   if (m) {  // the edge arrays through the context's pinned staging, one copy (they are adjacent)
-    const size_t eb = o_inoff;  // bytes up to the first derived array
-    char* h = stage_acquire(ctx, 0, eb);
-    memcpy(h + o_esrc, g->edge_src, m * 4ull);
-    memcpy(h + o_edst, g->edge_dst, m * 4ull);
-    memcpy(h + o_elat, g->edge_latency_ns, m * 8ull);
-    memcpy(h + o_eloss, g->edge_packet_loss, m * 4ull);
+    char* h = staged;
+    if (!h) {
+      h = stage_acquire(ctx, 0, eb);
+      memcpy(h + o_esrc, g->edge_src, m * 4ull);
+      memcpy(h + o_edst, g->edge_dst, m * 4ull);
+      memcpy(h + o_elat, g->edge_latency_ns, m * 8ull);
+      memcpy(h + o_eloss, g->edge_packet_loss, m * 4ull);
+    }
     if (trace) tr[2] = now_us();
     SG_HIP(hipMemcpyAsync(base, h, eb, hipMemcpyHostToDevice, st));
     stage_release(ctx, 0);

@@ -275,6 +275,37 @@ def test_edge_array_validation(oracle, ctx):
     assert g.compute_shortest_paths([0, 1])[(0, 1)].latency_ns == 5
 
 
+@pytest.mark.parametrize("threads", ["1", "4"])
+def test_edge_array_validation_threaded(oracle, ctx, monkeypatch, request, threads):
+    """Edge lists of 2^18 edges and more are checked and staged by up to 4 host threads
+    (sg_routing.hip build_net): the first bad edge in edge order still names the error when
+    bad edges sit in several threads' ranges, and a valid graph builds the oracle's table."""
+    if request.node.callspec.params["apsp_kernel"] != "lds":
+        pytest.skip("host-side upload: runs once, under the lds fixture")
+    monkeypatch.setenv("SG_NET_THREADS", threads)
+    rng = np.random.default_rng(11)
+    n, m = 1500, 300_001
+    src = rng.integers(0, n, m).astype(np.uint32)
+    dst = ((src + 1 + rng.integers(0, n - 1, m)) % n).astype(np.uint32)  # no self-loop ...
+    src[:n], dst[:n] = np.arange(n), np.arange(n)  # ... but one per node
+    lat = rng.integers(1, 300_000_000, m).astype(np.uint64)
+    loss = np.where(rng.random(m) < 0.8, 0.0, rng.random(m) * 0.02).astype(np.float32)
+    g = {"n": n, "src": src, "dst": dst, "lat": lat, "loss": loss, "directed": False}
+    _check(oracle, g, np.arange(0, n, 37, dtype=np.uint32), ctx)
+    cases = [  # (edge, field, value) in edge order; the error of the first one is raised
+        ([(290_000, "dst", n + 5), (80_000, "loss", 2.0), (150_000, "lat", 0)], "range [0,1]"),
+        ([(250_000, "lat", 0), (140_000, "src", n), (299_999, "loss", -1.0)], "endpoint out of range"),
+        ([(299_999, "lat", 0), (220_000, "loss", float("nan"))], "range [0,1]"),
+        ([(300_000, "lat", 0)], "must not be 0"),
+    ]
+    for bad, msg in cases:
+        a = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in g.items()}
+        for e, field, value in bad:
+            a[field][e] = value
+        with pytest.raises(ShadowGpuError, match=re.escape(msg)):
+            _graph(a, ctx).compute_shortest_paths([0, 1])
+
+
 def test_min_latency_device(ctx):
     import torch
 
