@@ -39,9 +39,11 @@
 // aligned dwordx2 halves.  Dense graphs (arc segments) flush with 64-bit
 // atomicMin instead.  The LDS kernel updates keys with 64-bit LDS atomics.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <type_traits>
 #include <vector>
@@ -1144,44 +1146,22 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   const size_t o_esrc = carve(m * 4ull), o_edst = carve(m * 4ull), o_elat = carve(m * 8ull),
                o_eloss = carve(m * 4ull);
   const size_t eb = total;  // bytes of the edge arrays, up to the first derived array
-  // Large edge lists (C2's 720k edges): the endpoint check, the self-loop count and the copy
-  // into the pinned staging in one pass split over up to 4 host threads (one thread 349 us,
-  // 4 threads 134 us on the MI355X box's host; tools/debug/stage_thread_probe.cpp).  Small
-  // ones in one thread, where the threads' start-up costs more than they save.
+  // Large edge lists (C2's 720k edges): validation and the copy into the pinned staging over
+  // up to 4 host threads (one thread 349 us, 4 threads 134 us on the MI355X box's host;
+  // tools/debug/stage_thread_probe.cpp), in two parts, each DMA'd as soon as it is staged:
+  // (A) the endpoints -- checked, self-loops counted -- then (B) the latencies and losses --
+  // checked -- while A's DMA runs.  The block is sized for no self-loops, since it is allocated
+  // before the count is known (the arrays then have a little unused room).  Small lists
+  // (C3's 50k edges: 22 us) take one thread, where the threads' start-up costs more than they
+  // save, and check the losses and latencies after the upload's launches.
   // (SG_NET_THREADS: A/B diagnostics, 1 = one thread)
-  const uint32_t n_thr = m >= (1u << 18) ? (uint32_t)std::max(1, std::min(4, env_int("SG_NET_THREADS", 4))) : 1u;
-  char* staged = nullptr;
+  const uint64_t arcs_cap = (uint64_t)m * (g->directed ? 1u : 2u);
+  const uint32_t n_thr = m >= (1u << 18) && arcs_cap < (1ull << 32)
+                             ? (uint32_t)std::max(1, std::min(4, env_int("SG_NET_THREADS", 4)))
+                             : 1u;
+  const bool threaded = n_thr > 1;
   uint64_t n_self = 0;
-  if (n_thr > 1) {
-    staged = stage_acquire(ctx, 0, eb);
-    std::vector<uint32_t> bad_t(n_thr, 0u), ns_t(n_thr, 0u);
-    auto part = [&](uint32_t t) {
-      const uint32_t e0 = (uint32_t)((uint64_t)m * t / n_thr), e1 = (uint32_t)((uint64_t)m * (t + 1) / n_thr);
-      uint32_t bad = 0, ns = 0;
-      for (uint32_t e = e0; e < e1; e++) {
-        const uint32_t a = es[e], b = ed[e];
-        bad |= (uint32_t)(a >= n) | (uint32_t)(b >= n);
-        ns += a == b;
-      }
-      bad_t[t] = bad;
-      ns_t[t] = ns;
-      const size_t c = (size_t)(e1 - e0);
-      memcpy(staged + o_esrc + e0 * 4ull, es + e0, c * 4);
-      memcpy(staged + o_edst + e0 * 4ull, ed + e0, c * 4);
-      memcpy(staged + o_elat + e0 * 8ull, el + e0, c * 8);
-      memcpy(staged + o_eloss + e0 * 4ull, ef + e0, c * 4);
-    };
-    std::vector<std::thread> pool;
-    for (uint32_t t = 1; t < n_thr; t++) pool.emplace_back(part, t);
-    part(0);
-    for (auto& th : pool) th.join();
-    uint32_t bad = 0;
-    for (uint32_t t = 0; t < n_thr; t++) {
-      bad |= bad_t[t];
-      n_self += ns_t[t];
-    }
-    if (bad) name_bad_edge();
-  } else {
+  if (!threaded) {
     uint32_t bad = 0, ns = 0;
     for (uint32_t e = 0; e < m; e++) {
       const uint32_t a = es[e], b = ed[e];
@@ -1193,21 +1173,20 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   }
   if (trace) tr[0] = now_us();
   // arcs without self-loops, both directions when undirected (petgraph semantics, graph/mod.rs:137-152)
-  const uint64_t arcs = ((uint64_t)m - n_self) * (g->directed ? 1u : 2u);
-  if (arcs >= (1ull << 32)) throw Error(SG_ERR_INVALID_ARG, "too many arcs");
-  const uint32_t n_arcs = (uint32_t)arcs;
+  const uint64_t arcs_sz = threaded ? arcs_cap : ((uint64_t)m - n_self) * (g->directed ? 1u : 2u);
+  if (arcs_sz >= (1ull << 32)) throw Error(SG_ERR_INVALID_ARG, "too many arcs");
+  const uint32_t n_arcs_sz = (uint32_t)arcs_sz;  // the layout's arc count (an upper bound when threaded)
   net->ctx = ctx;
   net->n_nodes = n;
   net->n_edges = m;
-  net->n_arcs = n_arcs;
   net->directed = g->directed != 0;
   if (g->node_gml_id) net->gml_id.assign(g->node_gml_id, g->node_gml_id + n);
   hipStream_t st = ctx->stream;
   const size_t o_inoff = carve(((size_t)n + 1) * 4), o_scnt = carve((size_t)n * 4),
-               o_sedge = carve((size_t)n * 4), o_insrc = carve(n_arcs * 4ull), o_indst = carve(n_arcs * 4ull),
-               o_inlat = carve(n_arcs * 8ull), o_inlat32 = carve(n_arcs * 4ull), o_inom = carve(n_arcs * 4ull),
-               o_inrec = carve(n_arcs * 16ull), o_outoff = carve(((size_t)n + 1) * 4),
-               o_outarc = carve(n_arcs * 12ull);
+               o_sedge = carve((size_t)n * 4), o_insrc = carve(n_arcs_sz * 4ull), o_indst = carve(n_arcs_sz * 4ull),
+               o_inlat = carve(n_arcs_sz * 8ull), o_inlat32 = carve(n_arcs_sz * 4ull), o_inom = carve(n_arcs_sz * 4ull),
+               o_inrec = carve(n_arcs_sz * 16ull), o_outoff = carve(((size_t)n + 1) * 4),
+               o_outarc = carve(n_arcs_sz * 12ull);
   {  // a released block of the right size from the context's pool, else a new one
     size_t best = ~(size_t)0;
     for (size_t i = 0; i < ctx->net_pool.size(); i++) {
@@ -1243,19 +1222,98 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   net->in_rec = (uint4*)(base + o_inrec);
   net->out_off = (uint32_t*)(base + o_outoff);
   net->out_arc = (uint32_t*)(base + o_outarc);
-  if (m) {  // the edge arrays through the context's pinned staging, one copy (they are adjacent)
-    char* h = staged;
-    if (!h) {
-      h = stage_acquire(ctx, 0, eb);
-      memcpy(h + o_esrc, g->edge_src, m * 4ull);
-      memcpy(h + o_edst, g->edge_dst, m * 4ull);
-      memcpy(h + o_elat, g->edge_latency_ns, m * 8ull);
-      memcpy(h + o_eloss, g->edge_packet_loss, m * 4ull);
+  // a bad edge found once the block is allocated: nothing may still run on the block when
+  // the caller deletes the net, then the per-edge loop names it
+  auto reject = [&]() {
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(net->mem);
+    net->mem = nullptr;
+    name_bad_edge();
+  };
+  bool checked = false;  // losses and latencies checked (threaded: in part B)
+  if (threaded) {
+    char* staged = stage_acquire(ctx, 0, eb);
+    std::vector<uint32_t> bad_t(n_thr, 0u), ns_t(n_thr, 0u);
+    std::atomic<uint32_t> done_a{0u}, done_b{0u};
+    auto range = [&](uint32_t t, uint32_t& e0, uint32_t& e1) {
+      e0 = (uint32_t)((uint64_t)m * t / n_thr);
+      e1 = (uint32_t)((uint64_t)m * (t + 1) / n_thr);
+    };
+    auto part_a = [&](uint32_t t) {  // endpoints: checked, self-loops counted, staged
+      uint32_t e0, e1, bad = 0, ns = 0;
+      range(t, e0, e1);
+      for (uint32_t e = e0; e < e1; e++) {
+        const uint32_t a = es[e], b = ed[e];
+        bad |= (uint32_t)(a >= n) | (uint32_t)(b >= n);
+        ns += a == b;
+      }
+      memcpy(staged + o_esrc + e0 * 4ull, es + e0, (e1 - e0) * 4ull);
+      memcpy(staged + o_edst + e0 * 4ull, ed + e0, (e1 - e0) * 4ull);
+      bad_t[t] = bad;
+      ns_t[t] = ns;
+      done_a.fetch_add(1u, std::memory_order_release);
+    };
+    auto part_b = [&](uint32_t t) {  // losses and latencies: checked, staged
+      uint32_t e0, e1, bad = 0;
+      range(t, e0, e1);
+      for (uint32_t e = e0; e < e1; e++) bad |= (uint32_t)!(ef[e] >= 0.0f) | (uint32_t)!(ef[e] <= 1.0f);
+      for (uint32_t e = e0; e < e1; e++) bad |= (uint32_t)(el[e] == 0);
+      memcpy(staged + o_elat + e0 * 8ull, el + e0, (e1 - e0) * 8ull);
+      memcpy(staged + o_eloss + e0 * 4ull, ef + e0, (e1 - e0) * 4ull);
+      bad_t[t] |= bad;
+      done_b.fetch_add(1u, std::memory_order_release);
+    };
+    std::vector<std::thread> pool;
+    struct Joiner {  // every started thread is joined, whatever is thrown below
+      std::vector<std::thread>& p;
+      ~Joiner() {
+        for (auto& th : p)
+          if (th.joinable()) th.join();
+      }
+    } joiner{pool};
+    uint32_t started = 1;  // threads 1 .. started-1 run their parts; this thread runs the others
+    try {
+      for (uint32_t t = 1; t < n_thr; t++, started++)
+        pool.emplace_back([&, t] {
+          part_a(t);
+          part_b(t);
+        });
+    } catch (const std::system_error&) {
     }
+    // each part's DMA once every thread has staged it: A's runs while part B is staged
+    for (uint32_t t = 0; t < n_thr; t++)
+      if (t == 0 || t >= started) part_a(t);
+    while (done_a.load(std::memory_order_acquire) < n_thr) std::this_thread::yield();
+    const hipError_t ea = hipMemcpyAsync(base, staged, o_elat, hipMemcpyHostToDevice, st);
+    for (uint32_t t = 0; t < n_thr; t++)
+      if (t == 0 || t >= started) part_b(t);
+    while (done_b.load(std::memory_order_acquire) < n_thr) std::this_thread::yield();
+    const hipError_t eb2 = ea == hipSuccess ? hipMemcpyAsync(base + o_elat, staged + o_elat, eb - o_elat,
+                                                             hipMemcpyHostToDevice, st)
+                                            : ea;
+    for (auto& th : pool) th.join();
+    SG_HIP(eb2);
+    stage_release(ctx, 0);
+    uint32_t bad = 0;
+    for (uint32_t t = 0; t < n_thr; t++) {
+      bad |= bad_t[t];
+      n_self += ns_t[t];
+    }
+    if (bad) reject();
+    checked = true;
+    if (trace) tr[2] = now_us();
+  } else if (m) {  // the edge arrays through the context's pinned staging, one copy (they are adjacent)
+    char* h = stage_acquire(ctx, 0, eb);
+    memcpy(h + o_esrc, g->edge_src, m * 4ull);
+    memcpy(h + o_edst, g->edge_dst, m * 4ull);
+    memcpy(h + o_elat, g->edge_latency_ns, m * 8ull);
+    memcpy(h + o_eloss, g->edge_packet_loss, m * 4ull);
     if (trace) tr[2] = now_us();
     SG_HIP(hipMemcpyAsync(base, h, eb, hipMemcpyHostToDevice, st));
     stage_release(ctx, 0);
   }
+  const uint32_t n_arcs = (uint32_t)(((uint64_t)m - n_self) * (g->directed ? 1u : 2u));
+  net->n_arcs = n_arcs;
   if (trace) tr[3] = now_us();
   uint32_t* indeg = ctx->r_misc.get<uint32_t>(2 * ((size_t)n + 1));
   uint32_t* outdeg = indeg + n + 1;
@@ -1302,10 +1360,12 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
                          net->in_lat32, net->in_om, net->in_rec, ocursor, net->out_arc);
     SG_CHECK_LAUNCH();
   }
-  {  // the losses and latencies, while the device runs the upload
+  {  // the losses and latencies, while the device runs the upload (threaded: checked already)
     uint32_t bad = 0;
-    for (uint32_t e = 0; e < m; e++) bad |= (uint32_t)!(ef[e] >= 0.0f) | (uint32_t)!(ef[e] <= 1.0f);
-    for (uint32_t e = 0; e < m; e++) bad |= (uint32_t)(el[e] == 0);
+    if (!checked) {
+      for (uint32_t e = 0; e < m; e++) bad |= (uint32_t)!(ef[e] >= 0.0f) | (uint32_t)!(ef[e] <= 1.0f);
+      for (uint32_t e = 0; e < m; e++) bad |= (uint32_t)(el[e] == 0);
+    }
     // the arcs' latency statistics the bucketed search sizes its buckets from (graphs past the
     // LDS search, or SG_APSP_BUCKET=1): smallest and mean arc latency, self-loops excluded
     if (!bad && (!sssp_lds_fits(n) || env_int("SG_APSP_BUCKET", -1) == 1)) {
@@ -1328,13 +1388,7 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
               "kernels enqueue + loss/latency check %.1f\n", m, tr[0] - tr0, tr[1] - tr[0], tr[2] - tr[1],
               tr[3] - tr[2], tr[4] - tr[3]);
     }
-    if (bad) {
-      // nothing may still run on the block when the caller deletes the net
-      (void)hipStreamSynchronize(st);
-      (void)hipFree(net->mem);
-      net->mem = nullptr;
-      name_bad_edge();
-    }
+    if (bad) reject();
   }
 }
 
