@@ -1107,10 +1107,11 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   if (m && (!g->edge_src || !g->edge_dst || !g->edge_latency_ns || !g->edge_packet_loss))
     throw Error(SG_ERR_INVALID_ARG, "null edge array");
   // Validation, in branch-free passes over the edge arrays (part of every one-shot
-  // build).  The endpoints (and the self-loop count the sizes need) before anything
-  // is allocated; the losses and latencies, which index nothing, after the upload's
-  // launches, while the device runs them.  Either way a bad edge is named by the
-  // per-edge loop, which checks every rule edge by edge (the reference's order).
+  // build).  One thread: the endpoints (and the self-loop count the sizes need) before
+  // anything is allocated, the losses and latencies, which index nothing, after the
+  // upload's launches, while the device runs them.  Large lists: every check in the
+  // threaded staging pass below, before any launch.  Either way a bad edge is named by
+  // the per-edge loop, which checks every rule edge by edge (the reference's order).
   const uint32_t* __restrict__ es = g->edge_src;
   const uint32_t* __restrict__ ed = g->edge_dst;
   const uint64_t* __restrict__ el = g->edge_latency_ns;
