@@ -1784,7 +1784,15 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   const bool few_rows = rows < 6u * (uint32_t)std::max(1, ctx->n_cu);
   const bool flagged = seeds_env != 0 && (flag_env == 1 || (flag_env < 0 && rows < n_used && !few_rows));
   const bool phased = !flagged && seeds_env != 0 && (seeds_env == 2 || rows >= 8u * (uint32_t)ctx->n_cu);
-  if (!phased && !flagged) SG_HIP(hipMemsetAsync(sat, 0, rows * 4ull, st));
+  // without a plan: the row flags and the persistent workgroups' claim counters zeroed by one
+  // launch (two fills cost two dispatches and ~10 us of host time in a one-shot block build)
+  uint32_t* claim_ctr = nullptr;
+  if (!phased && !flagged) {
+    claim_ctr = ctx->r_items.get<uint32_t>(2);
+    hipLaunchKernelGGL(k_zero2, dim3(grid_for((size_t)rows + 2, 256, 1024)), dim3(256), 0, st, sat, rows,
+                       claim_ctr, 2u);
+    SG_CHECK_LAUNCH();
+  }
   if (flagged) {
     const uint32_t per_cu = rows / std::max(1, ctx->n_cu);
     const int n_phase = std::max(2, std::min(SSSP_PHASES_MAX, env_int("SG_SSSP_PHASES", per_cu >= 16 ? 3 : 2)));
@@ -1848,7 +1856,8 @@ static void shortest_paths_lds(sg_ctx* ctx, sg_net* net, const uint32_t* d_used,
   } else {
     TimedLaunch tl(ctx, "sssp", 0.0);
     launch_sssp_lds(ctx, net->out_off, net->out_arc, net->n_nodes, net->n_arcs, d_used, n_used, row_begin,
-                    row_end, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work, diag);
+                    row_end, net->self_edge, net->e_lat, net->e_loss, out_lat, out_loss, sat, delta, work, diag,
+                    nullptr, 0, nullptr, nullptr, nullptr, 0, claim_ctr);
   }
   if (diag) {
     std::vector<unsigned long long> h((size_t)n_diag * 8);
@@ -2047,6 +2056,29 @@ void sg_net_destroy(sg_net* net) {
   delete net;
 }
 
+namespace sg {
+// The used-node list: every index in range, none twice.  One branch-free pass; only a bad
+// list is walked again, entry by entry, for the first bad entry's error.
+static void check_node_list(const sg_net* net, const uint32_t* nodes, uint32_t n_used) {
+  const uint32_t n = net->n_nodes;
+  std::vector<uint8_t> seen((size_t)n + 1, 0);  // the spare last byte takes out-of-range ids
+  uint32_t bad = 0;
+  for (uint32_t j = 0; j < n_used; j++) {
+    const uint32_t v = nodes[j];
+    const uint32_t out = v >= n;
+    const uint32_t x = out ? n : v;
+    bad |= out | (uint32_t)seen[x];
+    seen[x] = 1;
+  }
+  if (!bad) return;
+  std::fill(seen.begin(), seen.end(), (uint8_t)0);
+  for (uint32_t j = 0; j < n_used; j++) {
+    if (nodes[j] >= n) throw Error(SG_ERR_INVALID_ARG, "node index out of range");
+    if (seen[nodes[j]]++) throw Error(SG_ERR_INVALID_ARG, "duplicate node in node list");
+  }
+}
+}  // namespace sg
+
 int32_t sg_routing_build(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32_t n_used,
                          uint32_t row_begin, uint32_t row_end, uint32_t flags,
                          uint64_t* out_latency_ns, float* out_packet_loss) {
@@ -2057,13 +2089,7 @@ int32_t sg_routing_build(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, uint32
     if (n_used && !nodes) throw Error(SG_ERR_INVALID_ARG, "null node list");
     if (row_end > row_begin && (!out_latency_ns || !out_packet_loss))
       throw Error(SG_ERR_INVALID_ARG, "null output");
-    {
-      std::vector<uint8_t> seen(net->n_nodes, 0);
-      for (uint32_t j = 0; j < n_used; j++) {
-        if (nodes[j] >= net->n_nodes) throw Error(SG_ERR_INVALID_ARG, "node index out of range");
-        if (seen[nodes[j]]++) throw Error(SG_ERR_INVALID_ARG, "duplicate node in node list");
-      }
-    }
+    check_node_list(net, nodes, n_used);
     if (n_used == 0) return;
     hipStream_t st = ctx->stream;
     uint32_t* d_used = ctx->r_used.get<uint32_t>(n_used);
@@ -2128,13 +2154,7 @@ int32_t sg_routing_info_fill(sg_ctx* ctx, sg_net* net, const uint32_t* nodes, ui
     if (!ri) throw Error(SG_ERR_INVALID_ARG, "null routing info");
     const uint32_t n_used = ri->n;
     if (n_used && !nodes) throw Error(SG_ERR_INVALID_ARG, "null node list");
-    {
-      std::vector<uint8_t> seen(net->n_nodes, 0);
-      for (uint32_t j = 0; j < n_used; j++) {
-        if (nodes[j] >= net->n_nodes) throw Error(SG_ERR_INVALID_ARG, "node index out of range");
-        if (seen[nodes[j]]++) throw Error(SG_ERR_INVALID_ARG, "duplicate node in node list");
-      }
-    }
+    check_node_list(net, nodes, n_used);
     ri->filled = false;
     ri->min_lat = UINT64_MAX;
     ri->wide.clear();

@@ -193,10 +193,18 @@ class NetworkGraph:
         self.edge_dst = np.ascontiguousarray(edge_dst, dtype=np.uint32)
         self.edge_latency_ns = np.ascontiguousarray(edge_latency_ns, dtype=np.uint64)
         self.edge_packet_loss = np.ascontiguousarray(edge_packet_loss, dtype=np.float32)
-        ids = np.arange(self.n_nodes, dtype=np.uint32) if node_ids is None else node_ids
-        self.node_ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        # GML node ids; None: each node's index (built only if asked for, and not passed to
+        # sg_net_create, which then names nodes by index -- a one-shot build skips both)
+        self._node_ids = None if node_ids is None else np.ascontiguousarray(node_ids, dtype=np.uint32)
         self._id_to_index = None  # built on first lookup
         self._net = None
+
+    @property
+    def node_ids(self) -> np.ndarray:
+        """The GML node id of each node index."""
+        if self._node_ids is None:
+            self._node_ids = np.arange(self.n_nodes, dtype=np.uint32)
+        return self._node_ids
 
     @property
     def ctx(self) -> Context:
@@ -208,11 +216,14 @@ class NetworkGraph:
         g = _capi.sg_graph()
         g.n_nodes = self.n_nodes
         g.n_edges = len(self.edge_src)
-        g.edge_src = self.edge_src.ctypes.data_as(C.POINTER(C.c_uint32))
-        g.edge_dst = self.edge_dst.ctypes.data_as(C.POINTER(C.c_uint32))
-        g.edge_latency_ns = self.edge_latency_ns.ctypes.data_as(C.POINTER(C.c_uint64))
-        g.edge_packet_loss = self.edge_packet_loss.ctypes.data_as(C.POINTER(C.c_float))
-        g.node_gml_id = self.node_ids.ctypes.data_as(C.POINTER(C.c_uint32))
+        # (the arrays' addresses straight from the array interface: ndarray.ctypes builds a helper
+        # object per call, and this runs in every one-shot build)
+        ptr = lambda a, t: C.cast(a.__array_interface__["data"][0], C.POINTER(t))
+        g.edge_src = ptr(self.edge_src, C.c_uint32)
+        g.edge_dst = ptr(self.edge_dst, C.c_uint32)
+        g.edge_latency_ns = ptr(self.edge_latency_ns, C.c_uint64)
+        g.edge_packet_loss = ptr(self.edge_packet_loss, C.c_float)
+        g.node_gml_id = None if self._node_ids is None else ptr(self._node_ids, C.c_uint32)
         g.directed = 1 if self.directed else 0
         return g
 

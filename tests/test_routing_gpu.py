@@ -315,6 +315,17 @@ def test_min_latency_device(ctx):
     assert g.min_latency_device(x.data_ptr(), 0) == (1 << 64) - 1
 
 
+def test_bad_node_lists(ctx):
+    """sg_routing_build's node-list check: the first bad entry names the error (an index out
+    of range, or a node listed twice), and the context stays usable."""
+    g = NetworkGraph(4, [0, 1, 2, 3, 0, 1, 2], [0, 1, 2, 3, 1, 2, 3], [5] * 7, [0.0] * 7, False, ctx=ctx)
+    for used, msg in (([0, 9, 0], "node index out of range"), ([0, 1, 0, 9], "duplicate node in node list"),
+                      ([3, 2, 1, 0, 3], "duplicate node in node list"), ([4], "node index out of range")):
+        with pytest.raises(ShadowGpuError, match=re.escape(msg)):
+            g.compute_shortest_paths(np.array(used, np.uint32))
+    assert g.compute_shortest_paths([3, 0])[(3, 0)].latency_ns == 15
+
+
 def test_empty_used(ctx):
     g = NetworkGraph(2, [0, 1], [0, 1], [1, 1], [0.0, 0.0], False, ctx=ctx)
     assert len(g.compute_shortest_paths([])) == 0
