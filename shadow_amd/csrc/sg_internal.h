@@ -180,11 +180,10 @@ struct sg_net {
   // in-arc CSC without self-loops (device)
   uint32_t* in_off = nullptr;  // n_nodes + 1
   uint32_t* in_src = nullptr;
-  uint32_t* in_dst = nullptr;
   uint64_t* in_lat = nullptr;    // exact latency (wide kernel)
-  uint32_t* in_lat32 = nullptr;  // latency clamped to LAT32_SAT (packed-key kernel)
   float* in_om = nullptr;        // 1f32 - loss
   uint4* in_rec = nullptr;       // per in-arc (source, destination, latency32, bits(1f32 - loss))
+  bool csc = false;              // the in-arc arrays above are built (ensure_csc, on first use)
   // out-arc CSR without self-loops (device), for the per-source LDS search
   // (sg_sssp.hip): out_arc = 3 u32 per arc (head node, latency32, bits(1f32 - loss))
   uint32_t* out_off = nullptr;  // n_nodes + 1
@@ -337,6 +336,8 @@ void launch_sssp_bucket(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32
 constexpr int SSSP_KB_MAX = 8;
 constexpr uint32_t SSSP_UB_EXACT = 0x80000000u;  // bound rows per bounded search (sg_sssp.hip SSSP_KB)
 bool sssp_lds_fits(uint32_t n_nodes);
+// build the in-arc CSC of a net on its first use (sg_routing.hip; the upload writes the out-arcs only)
+void ensure_csc(sg_ctx* ctx, sg_net* net);
 
 void launch_sssp_lds(sg_ctx* ctx, const uint32_t* out_off, const uint32_t* out_arc, uint32_t n, uint32_t n_arcs,
                      const uint32_t* d_used, uint32_t n_used, uint32_t row_begin, uint32_t row_end,

@@ -513,6 +513,7 @@ SsspDevPlan sssp_device_plan(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
     const unsigned g = grid_for(rows, 256);
     hipLaunchKernelGGL(k_plan_rel, dim3(g), dim3(256), 0, st, d_used, row_begin, rows, rel, jn, zero_rows, zero_rows2);
     // in-neighbours: the CSC when directed; the out-arcs themselves when undirected
+    if (net->directed) ensure_csc(ctx, net);
     const uint32_t* in_off = net->directed ? net->in_off : net->out_off;
     const uint32_t* in_idx = net->directed ? net->in_src : net->out_arc;
     const uint32_t in_stride = net->directed ? 1u : 3u;

@@ -130,12 +130,15 @@ __global__ void __launch_bounds__(256) k_net_count_lds(const uint32_t* __restric
   }
 }
 
+// OUT: the out-arcs (out_arc, every search's input) -- the upload; CSC: the in-arcs (in_src,
+// in_lat, in_om, in_rec: the slab and wide kernels' and a directed plan's input) -- built on
+// first use (ensure_csc), so an upload writes 12 B per arc instead of 52.
+template <bool OUT, bool CSC>
 __global__ void __launch_bounds__(256) k_net_scatter_lds(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
                                                          const uint64_t* __restrict__ lat, const float* __restrict__ loss,
                                                          uint32_t m, uint32_t n, int directed,
                                                          uint32_t* __restrict__ cursor, uint32_t* __restrict__ in_src,
-                                                         uint32_t* __restrict__ in_dst, uint64_t* __restrict__ in_lat,
-                                                         uint32_t* __restrict__ in_lat32, float* __restrict__ in_om,
+                                                         uint64_t* __restrict__ in_lat, float* __restrict__ in_om,
                                                          uint4* __restrict__ in_rec, uint32_t* __restrict__ ocursor,
                                                          uint32_t* __restrict__ out_arc) {
   __shared__ uint32_t s_in[NET_LDS_NODES], s_out[NET_LDS_NODES];  // counts, then the block's cursors
@@ -145,17 +148,17 @@ __global__ void __launch_bounds__(256) k_net_scatter_lds(const uint32_t* __restr
   for (uint32_t e = e0 + threadIdx.x; e < e1; e += 256) {
     const uint32_t s = src[e], d = dst[e];
     if (s == d) continue;
-    atomicAdd(&s_in[d], 1u);
-    atomicAdd(&s_out[s], 1u);
+    if (CSC) atomicAdd(&s_in[d], 1u);
+    if (OUT) atomicAdd(&s_out[s], 1u);
     if (!directed) {
-      atomicAdd(&s_in[s], 1u);
-      atomicAdd(&s_out[d], 1u);
+      if (CSC) atomicAdd(&s_in[s], 1u);
+      if (OUT) atomicAdd(&s_out[d], 1u);
     }
   }
   __syncthreads();
   for (uint32_t v = threadIdx.x; v < n; v += 256) {  // this block's ranges
-    if (s_in[v]) s_in[v] = atomicAdd(&cursor[v], s_in[v]);
-    if (s_out[v]) s_out[v] = atomicAdd(&ocursor[v], s_out[v]);
+    if (CSC && s_in[v]) s_in[v] = atomicAdd(&cursor[v], s_in[v]);
+    if (OUT && s_out[v]) s_out[v] = atomicAdd(&ocursor[v], s_out[v]);
   }
   __syncthreads();
   for (uint32_t e = e0 + threadIdx.x; e < e1; e += 256) {
@@ -166,17 +169,19 @@ __global__ void __launch_bounds__(256) k_net_scatter_lds(const uint32_t* __restr
     const uint32_t l32 = l < LAT32_SAT ? (uint32_t)l : LAT32_SAT;
     for (int dir = 0; dir < (directed ? 1 : 2); dir++) {
       const uint32_t a = dir ? d : s, b = dir ? s : d;  // the arc a -> b
-      const uint32_t p = atomicAdd(&s_in[b], 1u);
-      in_src[p] = a;
-      in_dst[p] = b;
-      in_lat[p] = l;
-      in_lat32[p] = l32;
-      in_om[p] = om;
-      in_rec[p] = make_uint4(a, b, l32, __float_as_uint(om));
-      const uint32_t q = atomicAdd(&s_out[a], 1u);
-      out_arc[3 * (size_t)q] = b;
-      out_arc[3 * (size_t)q + 1] = l32;
-      out_arc[3 * (size_t)q + 2] = __float_as_uint(om);
+      if (CSC) {
+        const uint32_t p = atomicAdd(&s_in[b], 1u);
+        in_src[p] = a;
+        in_lat[p] = l;
+        in_om[p] = om;
+        in_rec[p] = make_uint4(a, b, l32, __float_as_uint(om));
+      }
+      if (OUT) {
+        const uint32_t q = atomicAdd(&s_out[a], 1u);
+        out_arc[3 * (size_t)q] = b;
+        out_arc[3 * (size_t)q + 1] = l32;
+        out_arc[3 * (size_t)q + 2] = __float_as_uint(om);
+      }
     }
   }
 }
@@ -254,11 +259,11 @@ __global__ void __launch_bounds__(1024) k_net_scan(const uint32_t* __restrict__ 
   }
 }
 
+template <bool OUT, bool CSC>  // (as k_net_scatter_lds)
 __global__ void k_net_scatter(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
                               const uint64_t* __restrict__ lat, const float* __restrict__ loss, uint32_t m,
                               int directed, uint32_t* __restrict__ cursor, uint32_t* __restrict__ in_src,
-                              uint32_t* __restrict__ in_dst, uint64_t* __restrict__ in_lat,
-                              uint32_t* __restrict__ in_lat32, float* __restrict__ in_om, uint4* __restrict__ in_rec,
+                              uint64_t* __restrict__ in_lat, float* __restrict__ in_om, uint4* __restrict__ in_rec,
                               uint32_t* __restrict__ ocursor, uint32_t* __restrict__ out_arc) {
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < m; e += gridDim.x * blockDim.x) {
     const uint32_t s = src[e], d = dst[e];
@@ -268,17 +273,19 @@ __global__ void k_net_scatter(const uint32_t* __restrict__ src, const uint32_t* 
     const uint32_t l32 = l < LAT32_SAT ? (uint32_t)l : LAT32_SAT;
     for (int dir = 0; dir < (directed ? 1 : 2); dir++) {
       const uint32_t a = dir ? d : s, b = dir ? s : d;  // the arc a -> b
-      const uint32_t p = atomicAdd(&cursor[b], 1u);
-      in_src[p] = a;
-      in_dst[p] = b;
-      in_lat[p] = l;
-      in_lat32[p] = l32;
-      in_om[p] = om;
-      in_rec[p] = make_uint4(a, b, l32, __float_as_uint(om));
-      const uint32_t q = atomicAdd(&ocursor[a], 1u);
-      out_arc[3 * (size_t)q] = b;
-      out_arc[3 * (size_t)q + 1] = l32;
-      out_arc[3 * (size_t)q + 2] = __float_as_uint(om);
+      if (CSC) {
+        const uint32_t p = atomicAdd(&cursor[b], 1u);
+        in_src[p] = a;
+        in_lat[p] = l;
+        in_om[p] = om;
+        in_rec[p] = make_uint4(a, b, l32, __float_as_uint(om));
+      }
+      if (OUT) {
+        const uint32_t q = atomicAdd(&ocursor[a], 1u);
+        out_arc[3 * (size_t)q] = b;
+        out_arc[3 * (size_t)q + 1] = l32;
+        out_arc[3 * (size_t)q + 2] = __float_as_uint(om);
+      }
     }
   }
 }
@@ -1184,8 +1191,8 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   if (g->node_gml_id) net->gml_id.assign(g->node_gml_id, g->node_gml_id + n);
   hipStream_t st = ctx->stream;
   const size_t o_inoff = carve(((size_t)n + 1) * 4), o_scnt = carve((size_t)n * 4),
-               o_sedge = carve((size_t)n * 4), o_insrc = carve(n_arcs_sz * 4ull), o_indst = carve(n_arcs_sz * 4ull),
-               o_inlat = carve(n_arcs_sz * 8ull), o_inlat32 = carve(n_arcs_sz * 4ull), o_inom = carve(n_arcs_sz * 4ull),
+               o_sedge = carve((size_t)n * 4), o_insrc = carve(n_arcs_sz * 4ull),
+               o_inlat = carve(n_arcs_sz * 8ull), o_inom = carve(n_arcs_sz * 4ull),
                o_inrec = carve(n_arcs_sz * 16ull), o_outoff = carve(((size_t)n + 1) * 4),
                o_outarc = carve(n_arcs_sz * 12ull);
   {  // a released block of the right size from the context's pool, else a new one
@@ -1216,9 +1223,7 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
   net->self_cnt = (uint32_t*)(base + o_scnt);
   net->self_edge = (uint32_t*)(base + o_sedge);
   net->in_src = (uint32_t*)(base + o_insrc);
-  net->in_dst = (uint32_t*)(base + o_indst);
   net->in_lat = (uint64_t*)(base + o_inlat);
-  net->in_lat32 = (uint32_t*)(base + o_inlat32);
   net->in_om = (float*)(base + o_inom);
   net->in_rec = (uint4*)(base + o_inrec);
   net->out_off = (uint32_t*)(base + o_outoff);
@@ -1351,14 +1356,15 @@ static void build_net(sg_ctx* ctx, const sg_graph* g, sg_net* net) {
     SG_HIP(hipMemcpyAsync(ocursor, net->out_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
   }
   if (n_arcs) {
+    // the out-arcs only; the in-arcs wait for a search that reads them (ensure_csc)
     if (lds_up)
-      hipLaunchKernelGGL(k_net_scatter_lds, dim3(lds_blocks), dim3(256), 0, st, net->e_src, net->e_dst, net->e_lat,
-                         net->e_loss, m, n, (int)net->directed, cursor, net->in_src, net->in_dst, net->in_lat,
-                         net->in_lat32, net->in_om, net->in_rec, ocursor, net->out_arc);
+      hipLaunchKernelGGL((k_net_scatter_lds<true, false>), dim3(lds_blocks), dim3(256), 0, st, net->e_src, net->e_dst,
+                         net->e_lat, net->e_loss, m, n, (int)net->directed, cursor, net->in_src, net->in_lat,
+                         net->in_om, net->in_rec, ocursor, net->out_arc);
     else
-      hipLaunchKernelGGL(k_net_scatter, dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src, net->e_dst,
-                         net->e_lat, net->e_loss, m, (int)net->directed, cursor, net->in_src, net->in_dst, net->in_lat,
-                         net->in_lat32, net->in_om, net->in_rec, ocursor, net->out_arc);
+      hipLaunchKernelGGL((k_net_scatter<true, false>), dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src,
+                         net->e_dst, net->e_lat, net->e_loss, m, (int)net->directed, cursor, net->in_src, net->in_lat,
+                         net->in_om, net->in_rec, ocursor, net->out_arc);
     SG_CHECK_LAUNCH();
   }
   {  // the losses and latencies, while the device runs the upload (threaded: checked already)
@@ -1437,9 +1443,33 @@ static void raise_self_check(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, u
 }
 
 // Wide recomputation of the listed rows (absolute row indices).
+// The in-arc CSC (in_src, in_lat, in_om, in_rec), built on its first use: the scatter again,
+// in-arcs only, from cursors set to in_off (the upload's scan wrote it).
+void ensure_csc(sg_ctx* ctx, sg_net* net) {
+  if (net->csc) return;
+  const uint32_t n = net->n_nodes, m = net->n_edges;
+  if (net->n_arcs) {
+    hipStream_t st = ctx->stream;
+    uint32_t* cursor = ctx->r_map.get<uint32_t>((size_t)n + 1);
+    SG_HIP(hipMemcpyAsync(cursor, net->in_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
+    if (n <= NET_LDS_NODES && env_int("SG_NET_LDS", 1) != 0)
+      hipLaunchKernelGGL((k_net_scatter_lds<false, true>), dim3(std::max(1u, std::min(NET_LDS_BLOCKS, (m + 255) / 256))),
+                         dim3(256), 0, st, net->e_src, net->e_dst, net->e_lat, net->e_loss, m, n, (int)net->directed,
+                         cursor, net->in_src, net->in_lat, net->in_om, net->in_rec, (uint32_t*)nullptr,
+                         (uint32_t*)nullptr);
+    else
+      hipLaunchKernelGGL((k_net_scatter<false, true>), dim3(grid_for(m, 256, 8192)), dim3(256), 0, st, net->e_src,
+                         net->e_dst, net->e_lat, net->e_loss, m, (int)net->directed, cursor, net->in_src,
+                         net->in_lat, net->in_om, net->in_rec, (uint32_t*)nullptr, (uint32_t*)nullptr);
+    SG_CHECK_LAUNCH();
+  }
+  net->csc = true;
+}
+
 static void run_wide(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                      const std::vector<uint32_t>& rows, uint32_t out_row0, uint64_t* out_lat,
                      float* out_loss) {
+  ensure_csc(ctx, net);
   hipStream_t st = ctx->stream;
   const uint32_t n = net->n_nodes;
   const uint32_t nr = (uint32_t)rows.size();
@@ -1490,6 +1520,7 @@ static void run_wide(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t 
 template <int B, int NPW, int STG, int GR, bool FRONT, int SPL = 1>
 static void shortest_paths_t(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                              uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
+  ensure_csc(ctx, net);  // the slab kernel gathers in-arcs
   hipStream_t st = ctx->stream;
   const uint32_t n = net->n_nodes;
   const uint32_t n_rows = row_end - row_begin;
