@@ -158,7 +158,9 @@ __device__ __forceinline__ void dense_write_row(const unsigned long long* key, u
     oloss[jj] = diag ? e_loss[de] : __uint_as_float(key_loss_bits(k));
 #endif
   }
-  if (__any(sat) && (threadIdx.x & 63) == 0) *sat_flag = 1u;
+  // the row's flag written whatever its value (every row is one block's), so no fill precedes a build
+  const int any = __syncthreads_or(sat ? 1 : 0);
+  if (threadIdx.x == 0) *sat_flag = any ? 1u : 0u;
 }
 
 // Seeded rows (SG_DENSE_SEED, launch_sssp_dense): the block's rows run in levels, one launch

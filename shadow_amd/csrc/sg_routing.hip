@@ -1721,8 +1721,8 @@ static std::vector<uint32_t> finish_rows(sg_ctx* ctx, const uint32_t* sat, uint3
 static void shortest_paths_dense(sg_ctx* ctx, sg_net* net, const uint32_t* d_used, uint32_t n_used,
                                  uint32_t row_begin, uint32_t row_end, uint64_t* out_lat, float* out_loss) {
   const uint32_t rows = row_end - row_begin;
+  // (no fill: the dense kernels write every row's flag, sg_dense.hip dense_write_row)
   uint32_t* sat = ctx->r_flags.get<uint32_t>(std::max(rows, 1u));
-  SG_HIP(hipMemsetAsync(sat, 0, std::max(rows, 1u) * 4ull, ctx->stream));
   unsigned long long* work = ctx->count_work ? ctx->r_work.get<unsigned long long>(WORK_SHARDS) : nullptr;
   if (work) SG_HIP(hipMemsetAsync(work, 0, WORK_SHARDS * 8, ctx->stream));
   launch_sssp_dense(ctx, net, d_used, n_used, row_begin, row_end, out_lat, out_loss, sat, work);
